@@ -1,0 +1,245 @@
+#!/usr/bin/env python
+"""Benchmark: binned events/s for a DREAM-scale detector view on MI355X.
+
+Workload (BASELINE.json configs[2], "DREAM cylinder_mantle_z projection with
+noise replicas + TOA binning (non-uniform edges), skewed hot-pixel
+distribution"): 491,520-pixel mantle, 80 x 320 screen, 5 replicas, 100
+geomspace TOA bins, Zipf(1.2) pixel skew + 3 hot TOA bins.  One step = one 1 Hz
+service batch: 14 ev44 pulses of 1e7 events each (1.4e8 events) staged from
+HBM, binned into the current window (accumulate), then finalized (cumulative
++= window, images and totals to the host).  With N > 1 ranks every rank bins
+its own batch (event-batch sharding, weak scaling) and the window histograms
+are summed onto rank 0 with an RCCL reduce over xGMI before rank 0 finalizes.
+
+Prints ONE JSON line on rank 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+BYTES_PER_EVENT = 8  # int32 pixel_id + int32 time_of_flight
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--workload', default='dream', choices=['dream', 'loki'])
+    ap.add_argument('--pulses', type=int, default=14)
+    ap.add_argument('--events-per-pulse', type=int, default=10_000_000)
+    ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition'])
+    ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    return ap.parse_args()
+
+
+def cpu_baseline(inst, view_coords_screen, seconds: float) -> dict:
+    """Time the oracle (NumPy restatement of the scipp pipeline) on host cores."""
+    from esslivedata_amd import synthetic
+    from oracle import scipp_semantics as ora
+
+    n = 2_000_000
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=view_coords_screen,
+        screen_shape=tuple(inst.resolution.values()),
+        toa_edges_ns=inst.edges.edges_ns(),
+    )
+    done = 0
+    batches = 0
+    t_total = 0.0
+    seed = 1
+    while t_total < seconds and batches < 64:
+        if inst.name == 'dream_mantle':
+            pid, toa = synthetic.dream_events(n, inst, seed=seed)
+        else:
+            pid, toa = synthetic.uniform_events(n, 1, 802816, seed=seed)
+        t0 = time.perf_counter()
+        o.accumulate(pid, toa)
+        t_total += time.perf_counter() - t0
+        done += n
+        batches += 1
+        seed += 1
+    t0 = time.perf_counter()
+    o.finalize()
+    t_total += time.perf_counter() - t0
+    return {
+        'value': done / t_total,
+        'unit': 'events/s',
+        'cores': 1,
+        'kind': 'port',
+        'sample': f'{batches} batches x {n} events of the same workload through '
+        f'oracle/scipp_semantics.py (group -> project -> hist -> +=), {t_total:.1f} s',
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.engine import BinningEngine
+
+    inst = synthetic.dream_mantle() if args.workload == 'dream' else synthetic.loki_bank0()
+    view = projection.geometric_lut(
+        inst.detector_number, inst.coords, inst.resolution, flip_x=args.workload == 'loki'
+    )
+    edges = inst.edges.edges_ns()
+    stream = torch.cuda.current_stream(dev)
+    eng = BinningEngine(
+        toa_edges_ns=edges,
+        out_lut=view.lut,
+        pid_offset=view.pid_offset,
+        n_screen=view.n_screen,
+        strategy=args.strategy,
+        device=local,
+        stream=stream.cuda_stream,
+    )
+    n_pulse = args.events_per_pulse
+    n_step = n_pulse * args.pulses
+    seed = 7 + 1000 * rank
+    if args.workload == 'dream':
+        pid, toa = synthetic.torch_dream_events(n_step, inst, seed, dev)
+    else:
+        pid, toa = synthetic.torch_uniform_events(n_step, 1, 802816, seed, dev)
+    torch.cuda.synchronize(dev)
+    nbins = view.n_screen * eng.n_toa_bins
+    merged = torch.zeros(nbins, dtype=torch.int32, device=dev) if world > 1 else None
+
+    def step(i: int):
+        for p in range(args.pulses):
+            eng.stage_tensors(pid[p * n_pulse : (p + 1) * n_pulse], toa[p * n_pulse : (p + 1) * n_pulse])
+        eng.accumulate(i % view.n_replicas)
+        if world > 1:
+            eng.export_window(merged.data_ptr())
+            dist.reduce(merged, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                eng.import_window(merged.data_ptr())
+        if rank == 0 or world == 1:
+            eng.finalize(images=True)
+        else:
+            eng.clear()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    eng.timing_enable(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    stats = {k: eng.kernel_stats(k) for k in ('atomic', 'partition', 'tile_accumulate', 'plan', 'binning', 'finalize')}
+    info = eng.info()
+    total_events = n_step * args.steps * world
+    value = total_events / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # dominant kernel and its roofline (algorithmic bytes per launch / avg duration)
+    dom = max(('atomic', 'partition', 'tile_accumulate'), key=lambda k: stats[k][0])
+    ms, launches = stats[dom]
+    if dom == 'partition':
+        events_per_launch = n_pulse  # one launch per staged pulse segment
+    else:
+        events_per_launch = n_step
+    alg_bytes = BYTES_PER_EVENT * events_per_launch
+    if dom == 'tile_accumulate':
+        alg_bytes += 4 * nbins  # window written once per batch
+    avg_s = (ms / max(launches, 1)) / 1e3
+    achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
+    bin_ms, bin_n = stats['binning']
+    pipeline_gbs = BYTES_PER_EVENT * n_step / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0
+
+    result = {
+        'metric': 'binned events/sec (whole node), DREAM-scale detector view; % HBM roofline',
+        'value': value,
+        'unit': 'events/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': ms_per_step,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'int32',
+        'data': 'synthetic (seeded ev44-shaped streams generated in HBM; no recorded data offline)',
+        'config': {
+            'workload': 'dream_mantle_cylinder_mantle_z' if args.workload == 'dream' else 'loki_bank0_xy_plane',
+            'pixels': int(inst.detector_number.size),
+            'screen': list(view.screen_shape),
+            'replicas': view.n_replicas,
+            'toa_bins': eng.n_toa_bins,
+            'toa_edges': inst.edges.scale,
+            'events_per_step': n_step,
+            'pulses_per_step': args.pulses,
+            'strategy': info['last_strategy'],
+            'tile_bits': info['tile_bits'],
+            'parallelism': f'event-batch sharding x{world} + RCCL reduce' if world > 1 else 'single GPU',
+        },
+        'roofline': {
+            'bound': 'hbm',
+            'kernel': dom,
+            'achieved': achieved,
+            'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s',
+            'frac': achieved / HBM_PEAK_GBS,
+            'traffic': None,
+            'avg_launch_ms': ms / max(launches, 1),
+            'launches': launches,
+            'pipeline_achieved': pipeline_gbs,
+            'pipeline_frac': pipeline_gbs / HBM_PEAK_GBS,
+            'kernel_ms': {k: v[0] / max(v[1], 1) for k, v in stats.items()},
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import scipp_semantics as ora
+
+        edges_s = {d: ora.screen_edges(inst.coords[d] if d != 'x' or args.workload != 'loki' else -inst.coords[d], r) for d, r in inst.resolution.items()}
+        coords = dict(inst.coords)
+        if args.workload == 'loki':
+            coords['x'] = -coords['x']
+        ps = np.stack([ora.geometric_screen_index(coords, edges_s, k) for k in range(view.n_replicas)])
+        result['cpu_baseline'] = cpu_baseline(inst, ps, args.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

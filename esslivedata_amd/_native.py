@@ -1,0 +1,177 @@
+"""ctypes binding of the C ABI in ``include/lde.h``.
+
+The product path has exactly one implementation: the HIP engine in
+``libesslivedata_amd.so``.  If the library is missing or cannot be loaded the
+import of :func:`lib` raises -- there is no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import threading
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / 'libesslivedata_amd.so'
+
+ABI_VERSION = 1
+
+LDE_OK = 0
+LDE_EINVAL = -1
+LDE_ESTATE = -2
+LDE_ENOMEM = -3
+LDE_EHIP = -4
+LDE_ENODATA = -5
+
+LDE_F64 = 0
+LDE_F32 = 1
+
+STRATEGIES = {'auto': 0, 'atomic': 1, 'partition': 2}
+
+LDE_CURRENT = 0
+LDE_CUMULATIVE = 1
+
+KERNELS = {
+    'atomic': 0,
+    'partition': 1,
+    'plan': 2,
+    'tile_accumulate': 3,
+    'monitor': 4,
+    'finalize': 5,
+    'binning': 6,
+}
+
+# every symbol include/lde.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = (
+    'lde_abi_version',
+    'lde_last_error',
+    'lde_create',
+    'lde_destroy',
+    'lde_stage',
+    'lde_stage_device',
+    'lde_accumulate',
+    'lde_finalize',
+    'lde_read_histogram',
+    'lde_clear',
+    'lde_reset_cumulative',
+    'lde_export_window',
+    'lde_import_window',
+    'lde_synchronize',
+    'lde_timing_enable',
+    'lde_kernel_stats',
+    'lde_info',
+)
+
+
+class LdeConfig(ctypes.Structure):
+    _fields_ = [
+        ('abi_version', ctypes.c_int32),
+        ('device_id', ctypes.c_int32),
+        ('stream', ctypes.c_void_p),
+        ('pid_offset', ctypes.c_int32),
+        ('n_replicas', ctypes.c_int32),
+        ('lut_len', ctypes.c_int64),
+        ('out_lut', ctypes.POINTER(ctypes.c_int32)),
+        ('n_screen', ctypes.c_int64),
+        ('n_toa_bins', ctypes.c_int32),
+        ('toa_edges', ctypes.POINTER(ctypes.c_double)),
+        ('out_dtype', ctypes.c_int32),
+        ('strategy', ctypes.c_int32),
+        ('range_lo', ctypes.c_int32),
+        ('range_hi', ctypes.c_int32),
+    ]
+
+
+class LdeOutputs(ctypes.Structure):
+    _fields_ = [
+        ('current_image', ctypes.c_void_p),
+        ('cumulative_image', ctypes.c_void_p),
+        ('current_hist', ctypes.c_void_p),
+        ('cumulative_hist', ctypes.c_void_p),
+        ('totals', ctypes.c_uint64 * 4),
+    ]
+
+
+_lock = threading.Lock()
+_lib: ctypes.CDLL | None = None
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    H = ctypes.c_void_p
+    i32, i64 = ctypes.c_int32, ctypes.c_int64
+    P = ctypes.c_void_p
+    sig = {
+        'lde_abi_version': (ctypes.c_int, []),
+        'lde_last_error': (ctypes.c_char_p, [H]),
+        'lde_create': (ctypes.c_int, [ctypes.POINTER(LdeConfig), ctypes.POINTER(H)]),
+        'lde_destroy': (None, [H]),
+        'lde_stage': (ctypes.c_int, [H, P, P, i64]),
+        'lde_stage_device': (ctypes.c_int, [H, P, P, i64]),
+        'lde_accumulate': (ctypes.c_int, [H, i32]),
+        'lde_finalize': (ctypes.c_int, [H, ctypes.POINTER(LdeOutputs)]),
+        'lde_read_histogram': (ctypes.c_int, [H, i32, P]),
+        'lde_clear': (ctypes.c_int, [H]),
+        'lde_reset_cumulative': (ctypes.c_int, [H]),
+        'lde_export_window': (ctypes.c_int, [H, P]),
+        'lde_import_window': (ctypes.c_int, [H, P]),
+        'lde_synchronize': (ctypes.c_int, [H]),
+        'lde_timing_enable': (ctypes.c_int, [H, i32]),
+        'lde_kernel_stats': (
+            ctypes.c_int,
+            [H, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)],
+        ),
+        'lde_info': (
+            ctypes.c_int,
+            [
+                H,
+                ctypes.POINTER(i64),
+                ctypes.POINTER(i32),
+                ctypes.POINTER(i64),
+                ctypes.POINTER(i32),
+                ctypes.POINTER(i32),
+                ctypes.POINTER(i64),
+                ctypes.POINTER(i32),
+            ],
+        ),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib() -> ctypes.CDLL:
+    """Load the engine library (once).  Raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f'HIP engine library {LIB_PATH} is missing; build it with '
+                '`python -m esslivedata_amd.build` (no CPU fallback exists)'
+            )
+        try:  # share torch's HIP runtime (same SONAME) when torch is present
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is part of the image
+            pass
+        cdll = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        _declare(cdll)
+        if cdll.lde_abi_version() != ABI_VERSION:
+            raise RuntimeError('libesslivedata_amd ABI version mismatch')
+        _lib = cdll
+        return cdll
+
+
+def last_error(handle) -> str:
+    msg = lib().lde_last_error(handle)
+    return msg.decode() if msg else ''
+
+
+def check(rc: int, handle=None) -> None:
+    """Map engine error codes onto the reference's exception conventions."""
+    if rc == LDE_OK:
+        return
+    msg = last_error(handle)
+    if rc in (LDE_EINVAL, LDE_ENODATA):
+        raise ValueError(msg)
+    raise RuntimeError(msg or f'lde error {rc}')

@@ -1,0 +1,921 @@
+// lde_engine.cpp -- host side of the C ABI declared in include/lde.h.
+//
+// Owns the device state of one detector view / monitor job:
+//   LUT  [R][L] int32  screen*T or -1          (setup-time, projectors.py:306-352)
+//   TOA thresholds [T+1] int64 + bucket table  (setup-time, providers.py:205-207)
+//   window u32 [S*T] (+ u64 fold buffer)       (window accumulator, accumulators.py:138-163)
+//   cumulative u64 [S*T]                       (NoCopyAccumulator, accumulators.py:86-135)
+//   f32 window/cumulative for LDE_F32 views    (BIFROST, bifrost/specs.py:295)
+//   staging: pinned host ring -> device event buffers (ToNXevent_data.add, to_nxevent_data.py:140-153)
+//   partition workspace (payload, run starts, plan tables)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/lde.h"
+#include "lde_internal.h"
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct Segment {
+    const int *pid;
+    const int *toa;
+    long long n;
+};
+
+struct TimedLaunch {
+    int kid;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct lde_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int cus = 256;
+
+    int pid_off = 0;
+    int R = 1;
+    long long L = 0;
+    bool monitor = false;
+    long long S = 1;
+    int T = 1;
+    long long nbins = 1;
+    int out_dtype = LDE_F64;
+    int strategy = LDE_STRATEGY_AUTO;
+    int range_lo = 0, range_hi = 1;
+    lde::ToaParams tp{};
+
+    int *d_lut = nullptr;
+    long long *d_thr = nullptr;
+    uint32_t *d_bp = nullptr;
+
+    uint32_t *d_win32 = nullptr;
+    unsigned long long *d_win64 = nullptr;
+    unsigned long long *d_cum = nullptr;
+    float *d_winf = nullptr;
+    float *d_cumf = nullptr;
+
+    // staging
+    int *d_spid = nullptr, *d_stoa = nullptr;
+    long long stage_cap = 0, staged_host = 0;
+    int *h_ppid = nullptr, *h_ptoa = nullptr;
+    long long pin_cap = 0;
+    hipEvent_t pin_done = nullptr;
+    bool pin_pending = false;
+    std::vector<Segment> dev_segments;
+
+    // partition workspace
+    int tile_bits = 13, n_tiles = 0;
+    uint16_t *d_payload = nullptr;
+    uint32_t *d_starts = nullptr;
+    long long chunk_cap = 0;
+    uint32_t *d_part = nullptr;
+    int part_rows = 0;
+    uint32_t *d_ttot = nullptr, *d_tile_items = nullptr, *d_item_count = nullptr;
+    uint2 *d_items = nullptr;
+    long long items_cap = 0;
+    long long item_events_override = 0;
+    long long atomic_threshold = -1;
+
+    // finalize scratch
+    unsigned long long *d_tot4 = nullptr;
+    void *d_img_cur = nullptr, *d_img_cum = nullptr;
+    unsigned long long *d_snap = nullptr;
+
+    // state
+    bool window_has_data = false;
+    bool cum_has_data = false;
+    bool win64_dirty = false;
+    unsigned long long win_events = 0;
+    long long events_binned = 0;
+    int last_strategy = 0;
+
+    // timing
+    bool timing = false;
+    std::vector<TimedLaunch> launches;
+    std::vector<hipEvent_t> event_pool;
+    double kms[LDE_K_COUNT] = {};
+    long long kcount[LDE_K_COUNT] = {};
+
+    std::string err;
+};
+
+namespace {
+
+int fail(lde_handle *h, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (h) h->err = buf;
+    else g_create_error = buf;
+    return code;
+}
+
+#define HIPCALL(h, expr)                                                                  \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail((h), LDE_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));   \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+long long env_ll(const char *name, long long dflt) {
+    const char *v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    return std::atoll(v);
+}
+
+template <typename T>
+int dev_alloc(lde_handle *h, T **p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void **)p, count * sizeof(T));
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return fail(h, LDE_ENOMEM, "hipMalloc(%zu bytes) failed: %s", count * sizeof(T),
+                    hipGetErrorString(e));
+    }
+    return LDE_OK;
+}
+
+template <typename T>
+void dev_free(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+// ---- TOA edge preprocessing (exact f64 -> int thresholds) -----------------
+long long ceil_clamped(double e) {
+    // t (int32) >= e  <=>  t >= ceil(e); clamp into [INT32_MIN, INT32_MAX + 1]
+    const double lo = -2147483648.0, hi = 2147483648.0;
+    if (e <= lo) return (long long)lo;
+    if (e >= hi) return (long long)hi;
+    return (long long)std::ceil(e);
+}
+
+int build_toa_tables(lde_handle *h, const double *edges, int T, std::vector<long long> &thr,
+                     std::vector<uint32_t> &bp, lde::ToaParams &tp) {
+    if (!edges) return fail(h, LDE_EINVAL, "toa_edges is NULL");
+    if (T < 1 || T > 65535) return fail(h, LDE_EINVAL, "n_toa_bins=%d out of range [1, 65535]", T);
+    for (int i = 0; i <= T; ++i) {
+        if (!std::isfinite(edges[i]))
+            return fail(h, LDE_EINVAL, "toa edge %d is not finite", i);
+        if (i > 0 && edges[i] < edges[i - 1])
+            return fail(h, LDE_EINVAL, "toa edges must be sorted (edge %d < edge %d)", i, i - 1);
+    }
+    thr.resize(T + 1);
+    for (int i = 0; i <= T; ++i) thr[i] = ceil_clamped(edges[i]);
+    tp.T = T;
+    tp.lo = thr[0];
+    tp.hi = thr[T];
+    const long long span = tp.hi - tp.lo;  // 0 .. 2^32
+    int shift = 0;
+    while (span > 0 && ((span - 1) >> shift) >= lde::kMaxBuckets) ++shift;
+    tp.shift = shift;
+    tp.G = span > 0 ? (int)(((span - 1) >> shift) + 1) : 1;
+    bp.assign(tp.G, 0u);
+    // bin(x) = largest b in [0, T-1] with thr[b] <= x, for x in [lo, hi)
+    auto bin_of = [&](long long x) {
+        int b = (int)(std::upper_bound(thr.begin(), thr.begin() + T, x) - thr.begin()) - 1;
+        return std::max(0, std::min(b, T - 1));
+    };
+    for (int g = 0; g < tp.G; ++g) {
+        const long long x0 = tp.lo + ((long long)g << shift);
+        long long x1 = tp.lo + (((long long)g + 1) << shift) - 1;
+        if (x1 > tp.hi - 1) x1 = tp.hi - 1;
+        const int b0 = span > 0 ? bin_of(x0) : 0;
+        const int b1 = span > 0 ? bin_of(std::max(x0, x1)) : 0;
+        bp[g] = (uint32_t)b0 | ((uint32_t)b1 << 16);
+    }
+    return LDE_OK;
+}
+
+// ---- timing ----------------------------------------------------------------
+hipEvent_t pool_event(lde_handle *h) {
+    if (!h->event_pool.empty()) {
+        hipEvent_t e = h->event_pool.back();
+        h->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+struct Timed {
+    lde_handle *h;
+    int kid;
+    hipEvent_t a = nullptr;
+    Timed(lde_handle *h_, int kid_) : h(h_), kid(kid_) {
+        if (h->timing) {
+            a = pool_event(h);
+            if (a) (void)hipEventRecord(a, h->stream);
+        }
+    }
+    ~Timed() {
+        if (h->timing && a) {
+            hipEvent_t b = pool_event(h);
+            if (b) {
+                (void)hipEventRecord(b, h->stream);
+                h->launches.push_back({kid, a, b});
+            } else {
+                h->event_pool.push_back(a);
+            }
+        }
+    }
+};
+
+void resolve_timing(lde_handle *h) {
+    for (auto &l : h->launches) {
+        float ms = 0.f;
+        if (hipEventSynchronize(l.b) == hipSuccess && hipEventElapsedTime(&ms, l.a, l.b) == hipSuccess) {
+            h->kms[l.kid] += ms;
+            h->kcount[l.kid] += 1;
+        }
+        h->event_pool.push_back(l.a);
+        h->event_pool.push_back(l.b);
+    }
+    h->launches.clear();
+}
+
+// ---- staging ---------------------------------------------------------------
+int ensure_stage_capacity(lde_handle *h, long long need) {
+    if (need <= h->stage_cap && need <= h->pin_cap) return LDE_OK;
+    long long cap = std::max<long long>(need, std::max<long long>(2 * h->stage_cap, 1 << 20));
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    int *np = nullptr, *nt = nullptr;
+    if (!h->monitor) {
+        if (int rc = dev_alloc(h, &np, cap)) return rc;
+    }
+    if (int rc = dev_alloc(h, &nt, cap)) {
+        dev_free(np);
+        return rc;
+    }
+    if (h->staged_host > 0) {
+        if (!h->monitor)
+            HIPCALL(h, hipMemcpy(np, h->d_spid, h->staged_host * 4, hipMemcpyDeviceToDevice));
+        HIPCALL(h, hipMemcpy(nt, h->d_stoa, h->staged_host * 4, hipMemcpyDeviceToDevice));
+    }
+    dev_free(h->d_spid);
+    dev_free(h->d_stoa);
+    h->d_spid = np;
+    h->d_stoa = nt;
+    h->stage_cap = cap;
+    // pinned host ring (previous content already copied to the device)
+    if (h->h_ppid) (void)hipHostFree(h->h_ppid);
+    if (h->h_ptoa) (void)hipHostFree(h->h_ptoa);
+    h->h_ppid = h->h_ptoa = nullptr;
+    h->pin_cap = 0;
+    if (!h->monitor) HIPCALL(h, hipHostMalloc((void **)&h->h_ppid, cap * 4, hipHostMallocDefault));
+    HIPCALL(h, hipHostMalloc((void **)&h->h_ptoa, cap * 4, hipHostMallocDefault));
+    h->pin_cap = cap;
+    h->pin_pending = false;
+    return LDE_OK;
+}
+
+int ensure_partition_capacity(lde_handle *h, long long chunks, long long max_items) {
+    if (chunks > h->chunk_cap) {
+        long long cap = std::max(chunks, 2 * h->chunk_cap);
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        dev_free(h->d_payload);
+        dev_free(h->d_starts);
+        if (int rc = dev_alloc(h, &h->d_payload, (size_t)cap * lde::kChunk)) return rc;
+        if (int rc = dev_alloc(h, &h->d_starts, (size_t)cap * (h->n_tiles + 1))) return rc;
+        h->chunk_cap = cap;
+    }
+    if (max_items > h->items_cap) {
+        long long cap = std::max(max_items, 2 * h->items_cap);
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        dev_free(h->d_items);
+        if (int rc = dev_alloc(h, &h->d_items, (size_t)cap)) return rc;
+        h->items_cap = cap;
+    }
+    return LDE_OK;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+// ---- binning ---------------------------------------------------------------
+int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long total, int replica) {
+    const int *lut = h->monitor ? nullptr : h->d_lut + (long long)replica * h->L;
+    if (h->monitor) {
+        h->last_strategy = LDE_STRATEGY_AUTO;
+        for (const Segment &s : segs) {
+            if (s.n == 0) continue;
+            const bool vec = aligned16(s.toa);
+            long long g = (s.n / 4 + 255) / 256;
+            g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 4));
+            Timed tm(h, LDE_K_MONITOR);
+            HIPCALL(h, lde::launch_monitor(s.toa, s.n, h->d_thr, h->d_bp, h->tp, h->d_win32, vec,
+                                           (int)g, h->stream));
+        }
+        return LDE_OK;
+    }
+    int strat = h->strategy;
+    if (strat == LDE_STRATEGY_AUTO) {
+        const long long thr = h->atomic_threshold >= 0
+                                  ? h->atomic_threshold
+                                  : std::max<long long>(1 << 20, h->nbins / 2);
+        strat = (h->n_tiles > 0 && total >= thr) ? LDE_STRATEGY_PARTITION : LDE_STRATEGY_ATOMIC;
+    }
+    if (strat == LDE_STRATEGY_PARTITION && h->n_tiles == 0) strat = LDE_STRATEGY_ATOMIC;
+    h->last_strategy = strat;
+    if (strat == LDE_STRATEGY_ATOMIC) {
+        for (const Segment &s : segs) {
+            if (s.n == 0) continue;
+            const bool vec = aligned16(s.pid) && aligned16(s.toa);
+            long long g = (s.n / 4 + 255) / 256;
+            g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 8));
+            Timed tm(h, LDE_K_ATOMIC);
+            HIPCALL(h, lde::launch_bin_atomic(s.pid, s.toa, s.n, lut, h->pid_off, (unsigned)h->L,
+                                              h->d_thr, h->d_bp, h->tp, h->d_win32, vec, (int)g,
+                                              h->stream));
+        }
+        return LDE_OK;
+    }
+    // PARTITION
+    long long chunks = 0;
+    for (const Segment &s : segs) chunks += (s.n + lde::kChunk - 1) / lde::kChunk;
+    if (chunks == 0) return LDE_OK;
+    long long item_events = h->item_events_override > 0
+                                ? h->item_events_override
+                                : std::max<long long>(32768, (total + 2LL * h->cus - 1) / (2LL * h->cus));
+    if (item_events > 0x7fffffffLL) item_events = 0x7fffffffLL;
+    const long long max_items = (total + item_events - 1) / item_events + h->n_tiles;
+    if (int rc = ensure_partition_capacity(h, chunks, max_items)) return rc;
+    const int grid_a = (int)std::min<long long>(chunks, (long long)h->part_rows);
+    HIPCALL(h, hipMemsetAsync(h->d_part, 0, (size_t)grid_a * h->n_tiles * 4, h->stream));
+    long long chunk0 = 0;
+    for (const Segment &s : segs) {
+        if (s.n == 0) continue;
+        const long long nc = (s.n + lde::kChunk - 1) / lde::kChunk;
+        const bool vec = aligned16(s.pid) && aligned16(s.toa);
+        Timed tm(h, LDE_K_PARTITION);
+        HIPCALL(h, lde::launch_partition(h->tile_bits, s.pid, s.toa, s.n, lut, h->pid_off,
+                                         (unsigned)h->L, h->d_thr, h->d_bp, h->tp, h->n_tiles,
+                                         chunk0, nc, h->d_payload, h->d_starts, h->d_part, vec,
+                                         grid_a, h->stream));
+        chunk0 += nc;
+    }
+    {
+        Timed tm(h, LDE_K_PLAN);
+        HIPCALL(h, lde::launch_plan(h->d_part, grid_a, h->n_tiles, (uint32_t)item_events,
+                                    h->d_ttot, h->d_tile_items, h->d_items, h->d_item_count,
+                                    (uint32_t)max_items, h->stream));
+    }
+    {
+        Timed tm(h, LDE_K_TILE);
+        HIPCALL(h, lde::launch_tile_accumulate(h->tile_bits, h->d_payload, h->d_starts,
+                                               h->n_tiles, chunks, h->d_items, h->d_item_count,
+                                               h->d_tile_items, h->d_win32, h->nbins,
+                                               (int)max_items, h->stream));
+    }
+    return LDE_OK;
+}
+
+int ensure_win64(lde_handle *h) {
+    if (h->d_win64) return LDE_OK;
+    if (int rc = dev_alloc(h, &h->d_win64, (size_t)h->nbins)) return rc;
+    HIPCALL(h, hipMemsetAsync(h->d_win64, 0, (size_t)h->nbins * 8, h->stream));
+    return LDE_OK;
+}
+
+int zero_state(lde_handle *h) {
+    const size_t nb = (size_t)h->nbins;
+    HIPCALL(h, hipMemsetAsync(h->d_win32, 0, nb * 4, h->stream));
+    HIPCALL(h, hipMemsetAsync(h->d_cum, 0, nb * 8, h->stream));
+    if (h->d_win64) HIPCALL(h, hipMemsetAsync(h->d_win64, 0, nb * 8, h->stream));
+    if (h->d_winf) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
+    if (h->d_cumf) HIPCALL(h, hipMemsetAsync(h->d_cumf, 0, nb * 4, h->stream));
+    h->window_has_data = false;
+    h->cum_has_data = false;
+    h->win64_dirty = false;
+    h->win_events = 0;
+    return LDE_OK;
+}
+
+void convert_u64(const unsigned long long *src, void *dst, long long n, int dtype) {
+    if (dtype == LDE_F32) {
+        float *d = (float *)dst;
+        for (long long i = 0; i < n; ++i) d[i] = (float)src[i];
+    } else {
+        double *d = (double *)dst;
+        for (long long i = 0; i < n; ++i) d[i] = (double)src[i];
+    }
+}
+
+void release(lde_handle *h) {
+    if (!h) return;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (auto &l : h->launches) {
+        (void)hipEventDestroy(l.a);
+        (void)hipEventDestroy(l.b);
+    }
+    for (auto e : h->event_pool) (void)hipEventDestroy(e);
+    dev_free(h->d_lut);
+    dev_free(h->d_thr);
+    dev_free(h->d_bp);
+    dev_free(h->d_win32);
+    dev_free(h->d_win64);
+    dev_free(h->d_cum);
+    dev_free(h->d_winf);
+    dev_free(h->d_cumf);
+    dev_free(h->d_spid);
+    dev_free(h->d_stoa);
+    if (h->h_ppid) (void)hipHostFree(h->h_ppid);
+    if (h->h_ptoa) (void)hipHostFree(h->h_ptoa);
+    if (h->pin_done) (void)hipEventDestroy(h->pin_done);
+    dev_free(h->d_payload);
+    dev_free(h->d_starts);
+    dev_free(h->d_part);
+    dev_free(h->d_ttot);
+    dev_free(h->d_tile_items);
+    dev_free(h->d_item_count);
+    dev_free(h->d_items);
+    dev_free(h->d_tot4);
+    dev_free(h->d_img_cur);
+    dev_free(h->d_img_cum);
+    dev_free(h->d_snap);
+    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int lde_abi_version(void) { return LDE_ABI_VERSION; }
+
+const char *lde_last_error(const lde_handle *h) {
+    return h ? h->err.c_str() : g_create_error.c_str();
+}
+
+int lde_create(const lde_config *cfg, lde_handle **out) {
+    if (!out) return fail(nullptr, LDE_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (!cfg) return fail(nullptr, LDE_EINVAL, "config is NULL");
+    if (cfg->abi_version != LDE_ABI_VERSION)
+        return fail(nullptr, LDE_EINVAL, "abi_version %d != %d", cfg->abi_version, LDE_ABI_VERSION);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(nullptr, LDE_EHIP, "no HIP device available");
+    if (cfg->device_id < 0 || cfg->device_id >= ndev)
+        return fail(nullptr, LDE_EINVAL, "device_id %d out of range (%d devices)", cfg->device_id, ndev);
+    if (cfg->n_screen < 1) return fail(nullptr, LDE_EINVAL, "n_screen must be >= 1");
+    if (cfg->n_replicas < 1) return fail(nullptr, LDE_EINVAL, "n_replicas must be >= 1");
+    if (cfg->out_dtype != LDE_F64 && cfg->out_dtype != LDE_F32)
+        return fail(nullptr, LDE_EINVAL, "out_dtype must be LDE_F64 or LDE_F32");
+    const bool monitor = cfg->out_lut == nullptr;
+    if (monitor && (cfg->n_screen != 1 || cfg->n_replicas != 1))
+        return fail(nullptr, LDE_EINVAL, "a NULL out_lut (monitor) requires n_screen = n_replicas = 1");
+    if (!monitor && (cfg->lut_len < 1 || cfg->lut_len > 0x7fffffffLL))
+        return fail(nullptr, LDE_EINVAL, "lut_len must be in [1, 2^31)");
+    const long long nbins = cfg->n_screen * (long long)cfg->n_toa_bins;
+    if (cfg->n_toa_bins < 1 || nbins > 0x7fffffffLL)
+        return fail(nullptr, LDE_EINVAL, "n_screen * n_toa_bins must be in [1, 2^31)");
+
+    lde_handle *h = new (std::nothrow) lde_handle();
+    if (!h) return fail(nullptr, LDE_ENOMEM, "out of host memory");
+    h->device = cfg->device_id;
+    DeviceGuard guard(h->device);
+    std::vector<long long> thr;
+    std::vector<uint32_t> bp;
+    int rc = build_toa_tables(h, cfg->toa_edges, cfg->n_toa_bins, thr, bp, h->tp);
+    if (rc) {
+        g_create_error = h->err;
+        release(h);
+        return rc;
+    }
+#define CREATE_CHECK(expr)                          \
+    do {                                            \
+        int rc_ = (expr);                           \
+        if (rc_) {                                  \
+            g_create_error = h->err;                \
+            release(h);                             \
+            return rc_;                             \
+        }                                           \
+    } while (0)
+#define CREATE_HIP(expr) CREATE_CHECK(((expr) == hipSuccess) ? 0 : fail(h, LDE_EHIP, "%s failed", #expr))
+
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, h->device) == hipSuccess && prop.multiProcessorCount > 0)
+        h->cus = prop.multiProcessorCount;
+    if (cfg->stream) {
+        h->stream = (hipStream_t)cfg->stream;
+    } else {
+        CREATE_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        h->own_stream = true;
+    }
+    h->pid_off = cfg->pid_offset;
+    h->R = cfg->n_replicas;
+    h->L = monitor ? 0 : cfg->lut_len;
+    h->monitor = monitor;
+    h->S = cfg->n_screen;
+    h->T = cfg->n_toa_bins;
+    h->nbins = nbins;
+    h->out_dtype = cfg->out_dtype;
+    h->strategy = cfg->strategy;
+    if (cfg->range_lo < 0 && cfg->range_hi < 0) {
+        h->range_lo = 0;
+        h->range_hi = h->T;
+    } else {
+        if (cfg->range_lo < 0 || cfg->range_hi > h->T || cfg->range_lo > cfg->range_hi) {
+            int r = fail(h, LDE_EINVAL, "range [%d, %d) invalid for %d bins", cfg->range_lo,
+                         cfg->range_hi, h->T);
+            g_create_error = h->err;
+            release(h);
+            return r;
+        }
+        h->range_lo = cfg->range_lo;
+        h->range_hi = cfg->range_hi;
+    }
+
+    // LUT: screen index -> screen*T (premultiplied), validated
+    if (!monitor) {
+        const long long n = (long long)h->R * h->L;
+        std::vector<int> lut((size_t)n);
+        for (long long i = 0; i < n; ++i) {
+            const int v = cfg->out_lut[i];
+            if (v < -1 || v >= h->S) {
+                int r = fail(h, LDE_EINVAL, "out_lut[%lld] = %d outside [-1, %lld)", i, v, h->S);
+                g_create_error = h->err;
+                release(h);
+                return r;
+            }
+            lut[(size_t)i] = v < 0 ? -1 : (int)((long long)v * h->T);
+        }
+        CREATE_CHECK(dev_alloc(h, &h->d_lut, (size_t)n));
+        CREATE_HIP(hipMemcpy(h->d_lut, lut.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    }
+    CREATE_CHECK(dev_alloc(h, &h->d_thr, thr.size()));
+    CREATE_HIP(hipMemcpy(h->d_thr, thr.data(), thr.size() * 8, hipMemcpyHostToDevice));
+    CREATE_CHECK(dev_alloc(h, &h->d_bp, bp.size()));
+    CREATE_HIP(hipMemcpy(h->d_bp, bp.data(), bp.size() * 4, hipMemcpyHostToDevice));
+
+    // histograms
+    CREATE_CHECK(dev_alloc(h, &h->d_win32, (size_t)nbins));
+    CREATE_CHECK(dev_alloc(h, &h->d_cum, (size_t)nbins));
+    if (h->out_dtype == LDE_F32) {
+        CREATE_CHECK(dev_alloc(h, &h->d_winf, (size_t)nbins));
+        CREATE_CHECK(dev_alloc(h, &h->d_cumf, (size_t)nbins));
+        CREATE_CHECK(ensure_win64(h));
+    }
+    CREATE_CHECK(dev_alloc(h, &h->d_tot4, 4));
+    CREATE_CHECK(dev_alloc(h, (double **)&h->d_img_cur, (size_t)h->S));
+    CREATE_CHECK(dev_alloc(h, (double **)&h->d_img_cum, (size_t)h->S));
+    CREATE_CHECK(zero_state(h));
+
+    // partition workspace: choose the smallest tile that keeps <= kMaxTiles tiles
+    if (!monitor) {
+        int tb = (int)env_ll("LDE_TILE_BITS", 13);
+        tb = std::max(13, std::min(tb, 15));
+        while (tb < 15 && (nbins + (1LL << tb) - 1) >> tb > lde::kMaxTiles) ++tb;
+        const long long nt = (nbins + (1LL << tb) - 1) >> tb;
+        const bool smem_ok = lde::partition_smem((int)nt, h->tp) <= 160 * 1024;
+        if (nt <= lde::kMaxTiles && smem_ok) {
+            h->tile_bits = tb;
+            h->n_tiles = (int)nt;
+            h->part_rows = 2 * h->cus;
+            CREATE_CHECK(dev_alloc(h, &h->d_part, (size_t)h->part_rows * h->n_tiles));
+            CREATE_CHECK(dev_alloc(h, &h->d_ttot, (size_t)h->n_tiles));
+            CREATE_CHECK(dev_alloc(h, &h->d_tile_items, (size_t)h->n_tiles));
+            CREATE_CHECK(dev_alloc(h, &h->d_item_count, 1));
+        } else {
+            h->n_tiles = 0;  // partition unavailable -> atomic strategy
+        }
+        h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
+        h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);
+    }
+    CREATE_HIP(hipEventCreateWithFlags(&h->pin_done, hipEventDisableTiming));
+    CREATE_HIP(hipStreamSynchronize(h->stream));
+#undef CREATE_CHECK
+#undef CREATE_HIP
+    *out = h;
+    return LDE_OK;
+}
+
+void lde_destroy(lde_handle *h) {
+    if (!h) return;
+    DeviceGuard guard(h->device);
+    release(h);
+}
+
+int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (n < 0) return fail(h, LDE_EINVAL, "negative event count");
+    if (n == 0) return LDE_OK;
+    if (!toa || (!h->monitor && !pid))
+        return fail(h, LDE_EINVAL, "event arrays must not be NULL");
+    DeviceGuard guard(h->device);
+    // the pinned ring is reused batch to batch: wait for the previous batch's copies
+    if (h->staged_host == 0 && h->pin_pending) {
+        HIPCALL(h, hipEventSynchronize(h->pin_done));
+        h->pin_pending = false;
+    }
+    if (int rc = ensure_stage_capacity(h, h->staged_host + n)) return rc;
+    const long long off = h->staged_host;
+    std::memcpy(h->h_ptoa + off, toa, (size_t)n * 4);
+    HIPCALL(h, hipMemcpyAsync(h->d_stoa + off, h->h_ptoa + off, (size_t)n * 4,
+                              hipMemcpyHostToDevice, h->stream));
+    if (!h->monitor) {
+        std::memcpy(h->h_ppid + off, pid, (size_t)n * 4);
+        HIPCALL(h, hipMemcpyAsync(h->d_spid + off, h->h_ppid + off, (size_t)n * 4,
+                                  hipMemcpyHostToDevice, h->stream));
+    }
+    HIPCALL(h, hipEventRecord(h->pin_done, h->stream));
+    h->pin_pending = true;
+    h->staged_host += n;
+    return LDE_OK;
+}
+
+int lde_stage_device(lde_handle *h, const void *d_pid, const void *d_toa, int64_t n) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (n < 0) return fail(h, LDE_EINVAL, "negative event count");
+    if (n == 0) return LDE_OK;
+    if (!d_toa || (!h->monitor && !d_pid))
+        return fail(h, LDE_EINVAL, "event arrays must not be NULL");
+    h->dev_segments.push_back({(const int *)d_pid, (const int *)d_toa, (long long)n});
+    return LDE_OK;
+}
+
+int lde_accumulate(lde_handle *h, int32_t replica) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (replica < 0 || replica >= h->R)
+        return fail(h, LDE_EINVAL, "replica %d out of range [0, %d)", replica, h->R);
+    DeviceGuard guard(h->device);
+    std::vector<Segment> segs;
+    if (h->staged_host > 0) segs.push_back({h->d_spid, h->d_stoa, h->staged_host});
+    for (const Segment &s : h->dev_segments) segs.push_back(s);
+    long long total = 0;
+    for (const Segment &s : segs) total += s.n;
+
+    // split into pieces that cannot overflow a u32 window bin
+    const long long piece_max = 1LL << 31;
+    std::vector<std::vector<Segment>> pieces;
+    {
+        std::vector<Segment> cur;
+        long long in_cur = 0;
+        for (Segment s : segs) {
+            while (s.n > 0) {
+                const long long take = std::min(s.n, piece_max - in_cur);
+                cur.push_back({s.pid ? s.pid : nullptr, s.toa, take});
+                in_cur += take;
+                s.pid = s.pid ? s.pid + take : nullptr;
+                s.toa += take;
+                s.n -= take;
+                if (in_cur == piece_max) {
+                    pieces.push_back(cur);
+                    cur.clear();
+                    in_cur = 0;
+                }
+            }
+        }
+        if (!cur.empty()) pieces.push_back(cur);
+    }
+    const bool f32 = h->out_dtype == LDE_F32;
+    {
+        Timed all(h, LDE_K_BINNING);
+        for (auto &p : pieces) {
+            long long n = 0;
+            for (auto &s : p) n += s.n;
+            if (!f32 && h->win_events + (unsigned long long)n > 0xffffffffULL) {
+                if (int rc = ensure_win64(h)) return rc;
+                HIPCALL(h, lde::launch_fold_window(h->d_win32, h->d_win64, h->nbins, h->stream));
+                h->win64_dirty = true;
+                h->win_events = 0;
+            }
+            if (int rc = bin_segments(h, p, n, replica)) return rc;
+            h->win_events += (unsigned long long)n;
+        }
+    }
+    if (f32) {
+        Timed tm(h, LDE_K_FINALIZE);
+        HIPCALL(h, lde::launch_merge_f32(h->d_win32, h->d_win64, h->d_winf, h->d_cumf, h->nbins,
+                                         h->window_has_data ? 0 : 1, h->cum_has_data ? 0 : 1,
+                                         h->stream));
+        h->win64_dirty = true;
+        h->win_events = 0;
+    }
+    h->events_binned += total;
+    h->window_has_data = true;
+    h->cum_has_data = true;
+    h->staged_host = 0;
+    h->dev_segments.clear();
+    return LDE_OK;
+}
+
+int lde_finalize(lde_handle *h, lde_outputs *out) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!h->window_has_data) return fail(h, LDE_ENODATA, "No data has been added");
+    DeviceGuard guard(h->device);
+    const bool f32 = h->out_dtype == LDE_F32;
+    const size_t nb = (size_t)h->nbins;
+    lde_outputs dummy;
+    std::memset(&dummy, 0, sizeof dummy);
+    if (!out) out = &dummy;
+    const bool want_cur_hist = out->current_hist != nullptr;
+    const bool want_cum_hist = out->cumulative_hist != nullptr;
+    if (want_cur_hist && !f32 && !h->d_snap)
+        if (int rc = dev_alloc(h, &h->d_snap, nb)) return rc;
+    if (f32) {
+        // images/hists come from the f32 accumulators (mirrors f32 += order)
+        if (out->current_image)
+            HIPCALL(h, lde::launch_rows_f32(h->d_winf, h->S, h->T, h->range_lo, h->range_hi,
+                                            (float *)h->d_img_cur, h->stream));
+        if (out->cumulative_image)
+            HIPCALL(h, lde::launch_rows_f32(h->d_cumf, h->S, h->T, h->range_lo, h->range_hi,
+                                            (float *)h->d_img_cum, h->stream));
+        if (want_cur_hist)
+            HIPCALL(h, hipMemcpyAsync(out->current_hist, h->d_winf, nb * 4, hipMemcpyDeviceToHost,
+                                      h->stream));
+        if (want_cum_hist)
+            HIPCALL(h, hipMemcpyAsync(out->cumulative_hist, h->d_cumf, nb * 4,
+                                      hipMemcpyDeviceToHost, h->stream));
+    }
+    HIPCALL(h, hipMemsetAsync(h->d_tot4, 0, 32, h->stream));
+    {
+        Timed tm(h, LDE_K_FINALIZE);
+        HIPCALL(h, lde::launch_finalize(
+                       f32, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
+                       (want_cur_hist && !f32) ? h->d_snap : nullptr, h->S, h->T, h->range_lo,
+                       h->range_hi, (!f32 && out->current_image) ? h->d_img_cur : nullptr,
+                       (!f32 && out->cumulative_image) ? h->d_img_cum : nullptr, h->d_tot4,
+                       h->stream));
+    }
+    const size_t isz = f32 ? 4 : 8;
+    if (out->current_image)
+        HIPCALL(h, hipMemcpyAsync(out->current_image, h->d_img_cur, (size_t)h->S * isz,
+                                  hipMemcpyDeviceToHost, h->stream));
+    if (out->cumulative_image)
+        HIPCALL(h, hipMemcpyAsync(out->cumulative_image, h->d_img_cum, (size_t)h->S * isz,
+                                  hipMemcpyDeviceToHost, h->stream));
+    unsigned long long tot[4] = {0, 0, 0, 0};
+    HIPCALL(h, hipMemcpyAsync(tot, h->d_tot4, 32, hipMemcpyDeviceToHost, h->stream));
+    std::vector<unsigned long long> tmp;
+    if (!f32 && (want_cur_hist || want_cum_hist)) tmp.resize(nb);
+    if (!f32 && want_cur_hist) {
+        HIPCALL(h, hipMemcpyAsync(tmp.data(), h->d_snap, nb * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        convert_u64(tmp.data(), out->current_hist, (long long)nb, LDE_F64);
+    }
+    if (!f32 && want_cum_hist) {
+        HIPCALL(h, hipMemcpyAsync(tmp.data(), h->d_cum, nb * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        convert_u64(tmp.data(), out->cumulative_hist, (long long)nb, LDE_F64);
+    }
+    if (f32) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    for (int q = 0; q < 4; ++q) out->totals[q] = tot[q];
+    h->window_has_data = false;
+    h->win64_dirty = false;
+    h->win_events = 0;
+    return LDE_OK;
+}
+
+int lde_read_histogram(lde_handle *h, int32_t which, void *host_out) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!host_out) return fail(h, LDE_EINVAL, "host_out is NULL");
+    if (which != LDE_CURRENT && which != LDE_CUMULATIVE)
+        return fail(h, LDE_EINVAL, "which must be LDE_CURRENT or LDE_CUMULATIVE");
+    if (which == LDE_CURRENT && !h->window_has_data)
+        return fail(h, LDE_ENODATA, "No data has been added");
+    if (which == LDE_CUMULATIVE && !h->cum_has_data)
+        return fail(h, LDE_ENODATA, "No data has been added");
+    DeviceGuard guard(h->device);
+    const size_t nb = (size_t)h->nbins;
+    if (h->out_dtype == LDE_F32) {
+        HIPCALL(h, hipMemcpyAsync(host_out, which == LDE_CURRENT ? h->d_winf : h->d_cumf, nb * 4,
+                                  hipMemcpyDeviceToHost, h->stream));
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        return LDE_OK;
+    }
+    if (!h->d_snap)
+        if (int rc = dev_alloc(h, &h->d_snap, nb)) return rc;
+    const unsigned long long *w64 = h->win64_dirty ? h->d_win64 : nullptr;
+    if (which == LDE_CURRENT)
+        HIPCALL(h, lde::launch_sum3(w64, nullptr, h->d_win32, h->d_snap, h->nbins, h->stream));
+    else
+        HIPCALL(h, lde::launch_sum3(h->d_cum, w64, h->d_win32, h->d_snap, h->nbins, h->stream));
+    std::vector<unsigned long long> tmp(nb);
+    HIPCALL(h, hipMemcpyAsync(tmp.data(), h->d_snap, nb * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    convert_u64(tmp.data(), host_out, (long long)nb, LDE_F64);
+    return LDE_OK;
+}
+
+int lde_clear(lde_handle *h) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    DeviceGuard guard(h->device);
+    h->staged_host = 0;
+    h->dev_segments.clear();
+    return zero_state(h);
+}
+
+int lde_reset_cumulative(lde_handle *h) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    DeviceGuard guard(h->device);
+    return zero_state(h);
+}
+
+int lde_export_window(lde_handle *h, void *d_dst) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!d_dst) return fail(h, LDE_EINVAL, "destination is NULL");
+    if (h->out_dtype == LDE_F32 || h->win64_dirty)
+        return fail(h, LDE_ESTATE, "window is not in uint32 form (f32 view or folded window)");
+    DeviceGuard guard(h->device);
+    HIPCALL(h, hipMemcpyAsync(d_dst, h->d_win32, (size_t)h->nbins * 4, hipMemcpyDeviceToDevice,
+                              h->stream));
+    return LDE_OK;
+}
+
+int lde_import_window(lde_handle *h, const void *d_src) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!d_src) return fail(h, LDE_EINVAL, "source is NULL");
+    if (h->out_dtype == LDE_F32 || h->win64_dirty)
+        return fail(h, LDE_ESTATE, "window is not in uint32 form (f32 view or folded window)");
+    DeviceGuard guard(h->device);
+    HIPCALL(h, hipMemcpyAsync(h->d_win32, d_src, (size_t)h->nbins * 4, hipMemcpyDeviceToDevice,
+                              h->stream));
+    h->window_has_data = true;
+    h->cum_has_data = true;
+    return LDE_OK;
+}
+
+int lde_synchronize(lde_handle *h) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    DeviceGuard guard(h->device);
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    return LDE_OK;
+}
+
+int lde_timing_enable(lde_handle *h, int32_t enable) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    DeviceGuard guard(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    resolve_timing(h);
+    for (int k = 0; k < LDE_K_COUNT; ++k) {
+        h->kms[k] = 0.0;
+        h->kcount[k] = 0;
+    }
+    h->timing = enable != 0;
+    return LDE_OK;
+}
+
+int lde_kernel_stats(lde_handle *h, int32_t kernel_id, double *ms, int64_t *launches) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (kernel_id < 0 || kernel_id >= LDE_K_COUNT)
+        return fail(h, LDE_EINVAL, "kernel id %d out of range", kernel_id);
+    DeviceGuard guard(h->device);
+    resolve_timing(h);
+    if (ms) *ms = h->kms[kernel_id];
+    if (launches) *launches = h->kcount[kernel_id];
+    return LDE_OK;
+}
+
+int lde_info(lde_handle *h, int64_t *n_screen, int32_t *n_toa_bins, int64_t *staged,
+             int32_t *tile_bits, int32_t *n_tiles, int64_t *events_binned,
+             int32_t *last_strategy) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    long long st = h->staged_host;
+    for (const Segment &s : h->dev_segments) st += s.n;
+    if (n_screen) *n_screen = h->S;
+    if (n_toa_bins) *n_toa_bins = h->T;
+    if (staged) *staged = st;
+    if (tile_bits) *tile_bits = h->tile_bits;
+    if (n_tiles) *n_tiles = h->n_tiles;
+    if (events_binned) *events_binned = h->events_binned;
+    if (last_strategy) *last_strategy = h->last_strategy;
+    return LDE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,72 @@
+// lde_internal.h -- shared constants and launch prototypes (not part of the ABI)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace lde {
+
+constexpr int kPartThreads = 1024;                 // pass A block
+constexpr int kPartEventsPerThread = 16;           // 4 x int4 per array
+constexpr int kChunk = kPartThreads * kPartEventsPerThread;  // 16384 events
+constexpr int kMaxTilesPerThread = 4;              // pass A/plan scan width
+constexpr int kMaxTiles = kPartThreads * kMaxTilesPerThread;  // 4096 tiles
+constexpr int kTileThreads = 512;                  // pass B block
+constexpr int kMonitorColumnsMaxT = 512;           // conflict-free monitor layout
+constexpr int kMaxBuckets = 4096;                  // TOA bucket table
+
+struct ToaParams {
+    long long lo;  // ceil(edge[0])  (clamped to the int32 domain)
+    long long hi;  // ceil(edge[T])
+    int shift;     // bucket width = 2^shift
+    int G;         // number of buckets
+    int T;         // number of TOA bins
+    int pad;
+};
+
+__host__ __device__ constexpr inline int align4(int x) { return (x + 3) & ~3; }
+__host__ __device__ constexpr inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+__host__ __device__ constexpr inline size_t thr_bytes(int T) { return align16((size_t)(T + 1) * 8); }
+
+inline unsigned grid_for(long long n) {
+    long long g = (n + 255) / 256;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+
+size_t partition_smem(int n_tiles, const ToaParams &tp);
+
+hipError_t launch_bin_atomic(const int *pid, const int *toa, long long n, const int *lut,
+                             int pid_off, unsigned L, const long long *thr, const uint32_t *bp,
+                             const ToaParams &tp, uint32_t *hist, bool vec, int grid,
+                             hipStream_t st);
+hipError_t launch_partition(int tile_bits, const int *pid, const int *toa, long long n,
+                            const int *lut, int pid_off, unsigned L, const long long *thr,
+                            const uint32_t *bp, const ToaParams &tp, int n_tiles, long long chunk0,
+                            long long n_chunks, uint16_t *payload, uint32_t *starts,
+                            uint32_t *part, bool vec, int grid, hipStream_t st);
+hipError_t launch_plan(const uint32_t *part, int part_rows, int n_tiles, uint32_t item_events,
+                       uint32_t *totals, uint32_t *tile_items, uint2 *items,
+                       uint32_t *item_count, uint32_t max_items, hipStream_t st);
+hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const uint32_t *starts,
+                                  int n_tiles, long long n_chunks, const uint2 *items,
+                                  const uint32_t *item_count, const uint32_t *tile_items,
+                                  uint32_t *hist, long long n_bins, int grid, hipStream_t st);
+hipError_t launch_monitor(const int *toa, long long n, const long long *thr, const uint32_t *bp,
+                          const ToaParams &tp, uint32_t *hist, bool vec, int grid,
+                          hipStream_t st);
+hipError_t launch_fold_window(uint32_t *win32, unsigned long long *win64, long long n,
+                              hipStream_t st);
+hipError_t launch_merge_f32(uint32_t *batch, unsigned long long *win64, float *winf, float *cumf,
+                            long long n, int first_win, int first_cum, hipStream_t st);
+hipError_t launch_sum3(const unsigned long long *a, const unsigned long long *b, const uint32_t *c,
+                       unsigned long long *out, long long n, hipStream_t st);
+hipError_t launch_finalize(bool f32_images, uint32_t *win32, unsigned long long *win64,
+                           unsigned long long *cum, unsigned long long *snap, long long S, int T,
+                           int lo, int hi, void *cur_img, void *cum_img,
+                           unsigned long long *totals, hipStream_t st);
+hipError_t launch_rows_f32(const float *h, long long S, int T, int lo, int hi, float *img,
+                           hipStream_t st);
+
+}  // namespace lde

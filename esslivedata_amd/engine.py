@@ -1,0 +1,253 @@
+"""Python handle of one HIP binning engine (thin wrapper over the C ABI).
+
+One :class:`BinningEngine` holds the device state of one detector view or
+monitor histogram: LUT, TOA thresholds, window and cumulative counts.  It is
+single-thread-affine like the reference's jobs (SRC/core/job_manager.py:698-701).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native
+from ._native import check
+
+
+@dataclass
+class FinalizeResult:
+    current_image: np.ndarray | None
+    cumulative_image: np.ndarray | None
+    current_hist: np.ndarray | None
+    cumulative_hist: np.ndarray | None
+    current_total: int
+    current_in_range: int
+    cumulative_total: int
+    cumulative_in_range: int
+
+
+def _as_i32(a) -> np.ndarray:
+    a = np.asarray(a)
+    if a.dtype != np.int32:
+        if a.dtype.kind not in 'iu':
+            raise TypeError(f'event arrays must be integer, got {a.dtype}')
+        a = a.astype(np.int32)
+    return np.ascontiguousarray(a)
+
+
+class BinningEngine:
+    """Device-resident event binning for one view (see include/lde.h)."""
+
+    def __init__(
+        self,
+        *,
+        toa_edges_ns: np.ndarray,
+        out_lut: np.ndarray | None,
+        pid_offset: int = 0,
+        n_screen: int = 1,
+        out_dtype: str = 'float64',
+        strategy: str = 'auto',
+        toa_range: tuple[int, int] | None = None,
+        device: int = 0,
+        stream: int | None = None,
+    ) -> None:
+        lib = _native.lib()
+        edges = np.ascontiguousarray(np.asarray(toa_edges_ns, dtype=np.float64))
+        if edges.ndim != 1 or len(edges) < 2:
+            raise ValueError('toa edges need at least two values')
+        self._T = len(edges) - 1
+        self._S = int(n_screen)
+        self._dtype = np.dtype(out_dtype)
+        if self._dtype not in (np.dtype('float64'), np.dtype('float32')):
+            raise ValueError('out_dtype must be float64 or float32')
+        if strategy not in _native.STRATEGIES:
+            raise ValueError(f'unknown strategy {strategy!r}')
+        cfg = _native.LdeConfig()
+        cfg.abi_version = _native.ABI_VERSION
+        cfg.device_id = int(device)
+        cfg.stream = ctypes.c_void_p(stream) if stream else None
+        cfg.pid_offset = int(pid_offset)
+        self._lut = None
+        if out_lut is None:
+            cfg.n_replicas = 1
+            cfg.lut_len = 0
+            cfg.out_lut = None
+        else:
+            lut = np.ascontiguousarray(np.asarray(out_lut, dtype=np.int32))
+            if lut.ndim == 1:
+                lut = lut[None, :]
+            self._lut = lut
+            cfg.n_replicas = lut.shape[0]
+            cfg.lut_len = lut.shape[1]
+            cfg.out_lut = lut.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        cfg.n_screen = self._S
+        cfg.n_toa_bins = self._T
+        cfg.toa_edges = edges.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        cfg.out_dtype = _native.LDE_F32 if self._dtype == np.float32 else _native.LDE_F64
+        cfg.strategy = _native.STRATEGIES[strategy]
+        if toa_range is None:
+            cfg.range_lo, cfg.range_hi = -1, -1
+        else:
+            cfg.range_lo, cfg.range_hi = int(toa_range[0]), int(toa_range[1])
+        self._n_replicas = cfg.n_replicas
+        h = ctypes.c_void_p()
+        rc = lib.lde_create(ctypes.byref(cfg), ctypes.byref(h))
+        check(rc, None)
+        self._h = h
+        self._lib = lib
+        self._keepalive: list = []
+
+    # ------------------------------------------------------------------
+    @classmethod
+    def monitor(cls, toa_edges_ns: np.ndarray, **kwargs) -> 'BinningEngine':
+        return cls(toa_edges_ns=toa_edges_ns, out_lut=None, n_screen=1, **kwargs)
+
+    @property
+    def n_screen(self) -> int:
+        return self._S
+
+    @property
+    def n_toa_bins(self) -> int:
+        return self._T
+
+    @property
+    def n_replicas(self) -> int:
+        return self._n_replicas
+
+    @property
+    def dtype(self) -> np.dtype:
+        return self._dtype
+
+    def _call(self, fn, *args) -> None:
+        check(fn(self._h, *args), self._h)
+
+    # ------------------------------------------------------------------
+    def stage(self, pid, toa) -> None:
+        """Stage one message of host events (ToNXevent_data.add equivalent)."""
+        t = _as_i32(toa)
+        if pid is None:
+            self._call(self._lib.lde_stage, None, t.ctypes.data, len(t))
+            return
+        p = _as_i32(pid)
+        if len(p) != len(t):
+            raise ValueError(
+                f'pixel_id and time_of_arrival must have the same length, '
+                f'got {len(p)} and {len(t)}'
+            )
+        self._call(self._lib.lde_stage, p.ctypes.data, t.ctypes.data, len(t))
+
+    def stage_device(self, pid_ptr: int | None, toa_ptr: int, n: int, keepalive=None) -> None:
+        """Stage events already in HBM (device pointers, int32)."""
+        if keepalive is not None:
+            self._keepalive.append(keepalive)
+        self._call(self._lib.lde_stage_device, pid_ptr, toa_ptr, int(n))
+
+    def stage_tensors(self, pid, toa) -> None:
+        """Stage int32 torch tensors resident on this engine's device."""
+        if pid is not None and pid.numel() != toa.numel():
+            raise ValueError('pixel_id and time_of_arrival must have the same length')
+        for t in (pid, toa):
+            if t is not None and (t.dtype.itemsize != 4 or not t.is_contiguous()):
+                raise ValueError('device event tensors must be contiguous int32')
+        self.stage_device(
+            None if pid is None else pid.data_ptr(), toa.data_ptr(), toa.numel(), (pid, toa)
+        )
+
+    def accumulate(self, replica: int = 0) -> None:
+        self._call(self._lib.lde_accumulate, int(replica))
+        self._keepalive.clear()
+
+    def finalize(self, *, images: bool = True, hists: bool = False) -> FinalizeResult:
+        out = _native.LdeOutputs()
+        arrs = {}
+        if images:
+            arrs['current_image'] = np.empty(self._S, dtype=self._dtype)
+            arrs['cumulative_image'] = np.empty(self._S, dtype=self._dtype)
+        if hists:
+            arrs['current_hist'] = np.empty(self._S * self._T, dtype=self._dtype)
+            arrs['cumulative_hist'] = np.empty(self._S * self._T, dtype=self._dtype)
+        for k, a in arrs.items():
+            setattr(out, k, a.ctypes.data)
+        self._call(self._lib.lde_finalize, ctypes.byref(out))
+        tot = list(out.totals)
+        shape = (self._S, self._T)
+        return FinalizeResult(
+            current_image=arrs.get('current_image'),
+            cumulative_image=arrs.get('cumulative_image'),
+            current_hist=arrs['current_hist'].reshape(shape) if hists else None,
+            cumulative_hist=arrs['cumulative_hist'].reshape(shape) if hists else None,
+            current_total=int(tot[0]),
+            current_in_range=int(tot[1]),
+            cumulative_total=int(tot[2]),
+            cumulative_in_range=int(tot[3]),
+        )
+
+    def read_histogram(self, which: str = 'current') -> np.ndarray:
+        w = {'current': _native.LDE_CURRENT, 'cumulative': _native.LDE_CUMULATIVE}[which]
+        out = np.empty(self._S * self._T, dtype=self._dtype)
+        self._call(self._lib.lde_read_histogram, w, out.ctypes.data)
+        return out.reshape(self._S, self._T)
+
+    def clear(self) -> None:
+        self._keepalive.clear()
+        self._call(self._lib.lde_clear)
+
+    def reset_cumulative(self) -> None:
+        self._call(self._lib.lde_reset_cumulative)
+
+    def export_window(self, dst_ptr: int) -> None:
+        self._call(self._lib.lde_export_window, dst_ptr)
+
+    def import_window(self, src_ptr: int) -> None:
+        self._call(self._lib.lde_import_window, src_ptr)
+
+    def synchronize(self) -> None:
+        self._call(self._lib.lde_synchronize)
+
+    def timing_enable(self, enable: bool = True) -> None:
+        self._call(self._lib.lde_timing_enable, 1 if enable else 0)
+
+    def kernel_stats(self, kernel: str) -> tuple[float, int]:
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        self._call(
+            self._lib.lde_kernel_stats, _native.KERNELS[kernel], ctypes.byref(ms), ctypes.byref(n)
+        )
+        return ms.value, n.value
+
+    def info(self) -> dict:
+        s, st, eb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        t, tb, nt, ls = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        self._call(
+            self._lib.lde_info,
+            ctypes.byref(s),
+            ctypes.byref(t),
+            ctypes.byref(st),
+            ctypes.byref(tb),
+            ctypes.byref(nt),
+            ctypes.byref(eb),
+            ctypes.byref(ls),
+        )
+        return {
+            'n_screen': s.value,
+            'n_toa_bins': t.value,
+            'staged': st.value,
+            'tile_bits': tb.value,
+            'n_tiles': nt.value,
+            'events_binned': eb.value,
+            'last_strategy': {0: 'monitor', 1: 'atomic', 2: 'partition'}.get(ls.value, '?'),
+        }
+
+    def close(self) -> None:
+        h = getattr(self, '_h', None)
+        if h:
+            self._lib.lde_destroy(h)
+            self._h = None
+
+    def __del__(self) -> None:
+        try:
+            self.close()
+        except Exception:
+            pass

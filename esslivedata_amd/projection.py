@@ -1,0 +1,192 @@
+"""Setup-time construction of the engine's pid -> screen lookup tables.
+
+This is host code that runs once per job / geometry (like the reference's
+projector construction at job creation); the per-event work runs
+on the GPU.  It folds three reference steps into one int32 table per noise
+replica:
+
+* ``group_event_data`` membership and pixel index
+  (SRC/preprocessors/group_by_pixel.py:36-54): ids not in ``detector_number``
+  map to -1 (dropped); pixel index = row-major position.
+* geometric projection (SRC/workflows/detector_view/projectors.py:306-352):
+  per-replica screen coordinates binned with scipp's int-bin-count edge rule
+  ``linspace(nanmin, nextafter(nanmax, +inf), res + 1)``; half-open bins; NaN
+  and out-of-range -> -1; ``flip_x`` negates ``x``; screen dims follow the
+  order of the ``resolution`` dict.
+* logical projection (projectors.py:243-270): a reshape/slice transform of
+  the detector array followed by merging of reduction dims; computed by
+  applying the transform to an index array.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Sequence
+
+import numpy as np
+
+MAX_LUT_LEN = 1 << 28
+
+
+@dataclass
+class ViewLUT:
+    """Per-replica pid -> flat screen index table for :class:`BinningEngine`."""
+
+    pid_offset: int
+    lut: np.ndarray  # (R, L) int32, -1 = dropped
+    screen_shape: tuple[int, ...]
+    screen_dims: tuple[str, ...]
+    screen_coords: dict[str, np.ndarray] = field(default_factory=dict)
+    screen_edges: dict[str, np.ndarray] = field(default_factory=dict)
+    pixel_weights: np.ndarray | None = None
+
+    @property
+    def n_screen(self) -> int:
+        return int(np.prod(self.screen_shape)) if self.screen_shape else 1
+
+    @property
+    def n_replicas(self) -> int:
+        return self.lut.shape[0]
+
+
+def pid_pixel_table(detector_number: np.ndarray) -> tuple[int, np.ndarray]:
+    """Dense ``pid - pid_offset -> pixel index`` table (-1 = unknown id)."""
+    dn = np.asarray(detector_number).ravel().astype(np.int64)
+    if dn.size == 0:
+        raise ValueError('detector_number is empty')
+    lo, hi = int(dn.min()), int(dn.max())
+    length = hi - lo + 1
+    if length > MAX_LUT_LEN:
+        raise ValueError(f'detector_number range {length} too large for a dense LUT')
+    if lo < -(2**31) or hi >= 2**31:
+        raise ValueError('detector numbers must fit in int32')
+    table = np.full(length, -1, dtype=np.int64)
+    pos = dn - lo
+    if len(np.unique(pos)) != len(pos):
+        raise ValueError('detector_number contains duplicate ids')
+    table[pos] = np.arange(dn.size, dtype=np.int64)
+    return lo, table
+
+
+def scipp_hist_edges(values: np.ndarray, res: int) -> np.ndarray:
+    """scipp's edges for ``hist({dim: res})`` with an integer bin count."""
+    lo = float(np.nanmin(values))
+    hi = float(np.nanmax(values))
+    return np.linspace(lo, np.nextafter(hi, np.inf), int(res) + 1)
+
+
+def _bin_half_open(values: np.ndarray, edges: np.ndarray) -> np.ndarray:
+    idx = np.searchsorted(edges, values, side='right') - 1
+    bad = (idx < 0) | (idx >= len(edges) - 1) | np.isnan(values)
+    idx = idx.astype(np.int64)
+    idx[bad] = -1
+    return idx
+
+
+def _compose(detector_number, pixel_screen: np.ndarray) -> tuple[int, np.ndarray]:
+    """LUT[r][pid - off] = pixel_screen[r][pixel(pid)]."""
+    off, table = pid_pixel_table(detector_number)
+    known = table >= 0
+    lut = np.full((pixel_screen.shape[0], len(table)), -1, dtype=np.int32)
+    lut[:, known] = pixel_screen[:, table[known]]
+    return off, lut
+
+
+def geometric_lut(
+    detector_number: np.ndarray,
+    coords: dict[str, np.ndarray],
+    resolution: dict[str, int],
+    *,
+    flip_x: bool = False,
+) -> ViewLUT:
+    """LUT for a geometric view from per-replica projected coordinates.
+
+    ``coords[dim]`` has shape ``(R, P)`` (replica, detector pixel), as produced
+    by essreduce's ``make_xy_plane_coords`` / ``make_cylinder_mantle_coords``
+    on ``CalibratedPositionWithNoisyReplicas``.
+    """
+    coords = {k: np.atleast_2d(np.asarray(v, dtype=np.float64)) for k, v in coords.items()}
+    if flip_x and 'x' in coords:
+        coords['x'] = -coords['x']
+    dims = tuple(resolution)
+    p = int(np.asarray(detector_number).size)
+    for d in dims:
+        if d not in coords:
+            raise ValueError(f'no projected coordinate for screen dim {d!r}')
+        if coords[d].shape[1] != p:
+            raise ValueError(f'coordinate {d!r} has {coords[d].shape[1]} pixels, expected {p}')
+    edges = {d: scipp_hist_edges(coords[d], resolution[d]) for d in dims}
+    shape = tuple(int(resolution[d]) for d in dims)
+    r = coords[dims[0]].shape[0]
+    pixel_screen = np.empty((r, p), dtype=np.int64)
+    for rep in range(r):
+        flat = None
+        for d, n in zip(dims, shape):
+            b = _bin_half_open(coords[d][rep], edges[d])
+            if flat is None:
+                flat = b
+            else:
+                bad = (flat < 0) | (b < 0)
+                flat = flat * n + b
+                flat[bad] = -1
+        pixel_screen[rep] = flat
+    off, lut = _compose(detector_number, pixel_screen)
+    # pixel weights: mean number of pixels per screen bin over replicas
+    # (GeometricProjector.compute_weights, projectors.py:154-172), float32
+    w = np.zeros(int(np.prod(shape)), dtype=np.float64)
+    for rep in range(r):
+        ok = pixel_screen[rep] >= 0
+        w += np.bincount(pixel_screen[rep][ok], minlength=len(w))
+    weights = (w.astype(np.float32) / np.float32(r)).reshape(shape)
+    return ViewLUT(
+        pid_offset=off,
+        lut=lut,
+        screen_shape=shape,
+        screen_dims=dims,
+        screen_coords={d: 0.5 * (edges[d][1:] + edges[d][:-1]) for d in dims},
+        screen_edges=edges,
+        pixel_weights=weights,
+    )
+
+
+def logical_lut(
+    detector_number: np.ndarray,
+    *,
+    dims: Sequence[str] | None = None,
+    transform: Callable[[np.ndarray], np.ndarray] | None = None,
+    output_dims: Sequence[str] | None = None,
+    reduction_axes: Sequence[int] = (),
+) -> ViewLUT:
+    """LUT for a logical view (identity, fold/flatten/slice, reduction).
+
+    ``transform`` receives an index array shaped like ``detector_number`` and
+    returns the reshaped/sliced array; pixels it drops map to -1; axes listed
+    in ``reduction_axes`` (of the transformed array) are merged.
+    """
+    dn = np.asarray(detector_number)
+    p = dn.size
+    idx = np.arange(p, dtype=np.int64).reshape(dn.shape)
+    t = np.asarray(idx if transform is None else transform(idx))
+    red = set(int(a) % t.ndim for a in reduction_axes) if t.ndim else set()
+    kept = [a for a in range(t.ndim) if a not in red]
+    out_shape = tuple(t.shape[a] for a in kept)
+    moved = np.moveaxis(t, kept, list(range(len(kept)))) if t.ndim else t
+    n_out = int(np.prod(out_shape)) if out_shape else 1
+    moved = moved.reshape(n_out, -1)
+    pix_out = np.full(p, -1, dtype=np.int64)
+    out_ids = np.repeat(np.arange(n_out, dtype=np.int64), moved.shape[1])
+    pix_out[moved.ravel()] = out_ids
+    off, lut = _compose(dn, pix_out[None, :])
+    weights = np.bincount(pix_out[pix_out >= 0], minlength=n_out).astype(np.float32)
+    if output_dims is None:
+        if dims is not None and transform is None and not red:
+            output_dims = tuple(dims)
+        else:
+            output_dims = tuple(f'dim_{i}' for i in range(len(out_shape)))
+    return ViewLUT(
+        pid_offset=off,
+        lut=lut,
+        screen_shape=out_shape,
+        screen_dims=tuple(output_dims),
+        pixel_weights=weights.reshape(out_shape),
+    )

@@ -1,0 +1,202 @@
+"""Synthetic instrument shapes and ev44-like event streams.
+
+No geometry files or recorded streams are available offline, so benchmark and
+test inputs are generated here with fixed seeds.  Shapes and distributions
+follow the reference's instrument configs and fakes:
+
+* dummy ``panel_0``: pids 1..16384 (dummy/streams.py:11), identity logical view
+  128 x 128 (dummy/factories.py:40-51); TOA ``uniform(0, 70e6)``
+  (tests/helpers/livedata_app.py:189) or ``normal(30e6, 1e7)``
+  (services/fake_detectors.py:98-99, 142-145).
+* LOKI bank 0: pids 1..802816 (loki/streams.py:18), xy_plane 144 x 144
+  (loki/factories.py:101-121); TOA ``uniform(0, 71e6)``.
+* DREAM mantle: pids 229377..720896 (dream/streams.py:19), cylinder_mantle_z
+  80 x 320 (dream/factories.py:59-66), sigma 4 mm noise, 4 noisy replicas + the
+  original; Zipf(1.2) pixel skew over a random permutation; TOA 80 % normal(30 ms,
+  10 ms) + 20 % in 3 hot bins; ``geomspace(0.5, 71.43, 101)`` ms edges.
+* BIFROST unified detector: pids 1..13500 folded (arc 5, tube 3, channel 9,
+  pixel 100) (bifrost/streams.py:46-48), logical 15 x 900, float32.
+
+Projected per-replica coordinates stand in for essreduce's
+``make_cylinder_mantle_coords`` / ``make_xy_plane_coords`` output; the engine
+takes them as input, exactly like the reference's own projector tests
+(tests/workflows/detector_view/projectors_test.py:19-51).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .edges import ESS_PULSE_PERIOD_MS, TOAEdges
+
+
+@dataclass
+class Instrument:
+    name: str
+    detector_number: np.ndarray
+    coords: dict[str, np.ndarray] | None  # (R, P) per screen dim, geometric views
+    resolution: dict[str, int] | None
+    edges: TOAEdges
+    out_dtype: str = 'float64'
+
+
+def dream_mantle(n_replicas: int = 5, seed: int = 7) -> Instrument:
+    rng = np.random.default_rng(seed)
+    first, last = 229377, 720896
+    p = last - first + 1  # 491520
+    n_phi, n_z = 1280, 384
+    phi = np.linspace(-2.4, 2.4, n_phi)
+    zz = np.linspace(-0.8, 0.8, n_z)
+    pp, zz2 = np.meshgrid(phi, zz, indexing='ij')
+    radius = 1.1
+    x = radius * np.cos(pp).ravel()
+    y = radius * np.sin(pp).ravel()
+    z = zz2.ravel()
+    arcs, zs = [], []
+    for r in range(n_replicas):
+        s = 0.0 if r == 0 else 0.004
+        xn = x + rng.normal(0, s, p) if s else x
+        yn = y + rng.normal(0, s, p) if s else y
+        zn = z + rng.normal(0, s, p) if s else z
+        arcs.append(np.hypot(xn, yn) * np.arctan2(yn, xn))
+        zs.append(zn)
+    return Instrument(
+        name='dream_mantle',
+        detector_number=np.arange(first, last + 1, dtype=np.int32),
+        coords={'arc_length': np.stack(arcs), 'z': np.stack(zs)},
+        resolution={'arc_length': 80, 'z': 320},
+        edges=TOAEdges(start=0.5, stop=ESS_PULSE_PERIOD_MS, num_bins=100, scale='log'),
+    )
+
+
+def loki_bank0(n_replicas: int = 5, seed: int = 42) -> Instrument:
+    rng = np.random.default_rng(seed)
+    p = 802816
+    side = 896
+    xs = np.linspace(-0.5, 0.5, side)
+    xx, yy = np.meshgrid(xs, xs, indexing='ij')
+    x, y = xx.ravel(), yy.ravel()
+    cx, cy = [], []
+    for r in range(n_replicas):
+        s = 0.0 if r == 0 else 0.002
+        cx.append(x + (rng.normal(0, s, p) if s else 0))
+        cy.append(y + (rng.uniform(-s, s, p) if s else 0))
+    return Instrument(
+        name='loki_bank0',
+        detector_number=np.arange(1, p + 1, dtype=np.int32),
+        coords={'x': np.stack(cx), 'y': np.stack(cy)},
+        resolution={'y': 144, 'x': 144},
+        edges=TOAEdges(),
+    )
+
+
+def dummy_panel() -> Instrument:
+    return Instrument(
+        name='dummy',
+        detector_number=np.arange(1, 128**2 + 1, dtype=np.int32).reshape(128, 128),
+        coords=None,
+        resolution=None,
+        edges=TOAEdges(),
+    )
+
+
+def bifrost_unified() -> Instrument:
+    return Instrument(
+        name='bifrost',
+        detector_number=np.arange(1, 5 * 3 * 9 * 100 + 1, dtype=np.int32).reshape(5, 3, 9, 100),
+        coords=None,
+        resolution=None,
+        edges=TOAEdges(),
+        out_dtype='float32',
+    )
+
+
+def bifrost_transform(idx: np.ndarray) -> np.ndarray:
+    """``_logical_view`` (bifrost/specs.py:285-299): flatten (arc, tube) and
+    (channel, pixel) -> (15, 900)."""
+    return idx.reshape(15, 900)
+
+
+# ---------------------------------------------------------------------------
+# event streams (numpy, for tests and the CPU baseline)
+# ---------------------------------------------------------------------------
+def zipf_pixel_weights(p: int, s: float = 1.2, seed: int = 7) -> np.ndarray:
+    rng = np.random.default_rng(seed + 1000)
+    w = np.arange(1, p + 1, dtype=np.float64) ** (-s)
+    w = w[rng.permutation(p)]
+    return w / w.sum()
+
+
+def dream_hot_bins(edges_ns: np.ndarray) -> list[tuple[float, float]]:
+    return [(edges_ns[b], edges_ns[b + 1]) for b in (40, 62, 85)]
+
+
+def dream_events(n: int, inst: Instrument, seed: int = 7, cdf: np.ndarray | None = None):
+    rng = np.random.default_rng(seed)
+    dn = inst.detector_number.ravel()
+    if cdf is None:
+        cdf = np.cumsum(zipf_pixel_weights(len(dn)))
+    pix = np.minimum(np.searchsorted(cdf, rng.random(n)), len(dn) - 1)
+    pid = dn[pix].astype(np.int32)
+    edges = inst.edges.edges_ns()
+    toa = rng.normal(30e6, 10e6, n)
+    hot = rng.random(n) < 0.2
+    which = rng.integers(0, 3, n)
+    hb = np.array(dream_hot_bins(edges))
+    lo, hi = hb[which, 0], hb[which, 1]
+    toa = np.where(hot, lo + rng.random(n) * (hi - lo), toa)
+    return pid, toa.astype(np.int32)
+
+
+def uniform_events(n: int, first: int, last: int, seed: int = 42, toa_max: float = 71e6):
+    rng = np.random.default_rng(seed)
+    pid = rng.integers(first, last + 1, n, dtype=np.int64).astype(np.int32)
+    toa = rng.uniform(0, toa_max, n).astype(np.int32)
+    return pid, toa
+
+
+def fake_detector_events(n: int, first: int, last: int, seed: int = 1234):
+    """fake_detectors.py:98-103: normal(30e6, 1e7) TOA, uniform pixel ids."""
+    rng = np.random.default_rng(seed)
+    toa = rng.normal(loc=30_000_000, scale=10_000_000, size=n).astype(np.int64).astype(np.int32)
+    pid = rng.integers(low=first, high=last + 1, size=n).astype(np.int32)
+    return pid, toa
+
+
+# ---------------------------------------------------------------------------
+# device-side generators (torch, for the benchmark: inputs resident in HBM)
+# ---------------------------------------------------------------------------
+def torch_dream_events(n: int, inst: Instrument, seed: int, device):
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    dn = torch.as_tensor(inst.detector_number.ravel(), device=device)
+    cdf = torch.as_tensor(np.cumsum(zipf_pixel_weights(len(dn))), device=device)
+    u = torch.rand(n, generator=g, device=device, dtype=torch.float64)
+    pix = torch.clamp(torch.searchsorted(cdf, u), max=len(dn) - 1)
+    pid = dn[pix].to(torch.int32)
+    del pix, u
+    edges = inst.edges.edges_ns()
+    toa = torch.randn(n, generator=g, device=device, dtype=torch.float32) * 10e6 + 30e6
+    hot = torch.rand(n, generator=g, device=device) < 0.2
+    which = torch.randint(0, 3, (n,), generator=g, device=device)
+    hb = torch.as_tensor(np.array(dream_hot_bins(edges)), device=device, dtype=torch.float64)
+    lo, hi = hb[which, 0], hb[which, 1]
+    hot_toa = lo + torch.rand(n, generator=g, device=device, dtype=torch.float64) * (hi - lo)
+    toa = torch.where(hot, hot_toa, toa.to(torch.float64)).to(torch.int32)
+    return pid.contiguous(), toa.contiguous()
+
+
+def torch_uniform_events(n: int, first: int, last: int, seed: int, device, toa_max: float = 71e6):
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    pid = torch.randint(first, last + 1, (n,), generator=g, device=device, dtype=torch.int32)
+    toa = (torch.rand(n, generator=g, device=device, dtype=torch.float64) * toa_max).to(
+        torch.int32
+    )
+    return pid.contiguous(), toa.contiguous()

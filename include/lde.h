@@ -1,0 +1,171 @@
+/*
+ * lde.h -- C ABI of the MI355X live-data event-binning engine ("lde").
+ *
+ * The engine replaces the per-event work the reference runs inside scipp on
+ * the detector-view and monitor-histogram path (reference = scipp/esslivedata,
+ * SRC = src/ess/livedata):
+ *
+ *   ToNXevent_data.add/get          SRC/preprocessors/to_nxevent_data.py:127-208
+ *   GroupByPixel.get (group_event_data)   SRC/preprocessors/group_by_pixel.py:43-54
+ *   GeometricProjector.project_events     SRC/workflows/detector_view/projectors.py:80-152
+ *   LogicalProjector.project_events       SRC/workflows/detector_view/projectors.py:243-270
+ *   compute_detector_histogram (hist)     SRC/workflows/detector_view/providers.py:169-214
+ *   _histogram_monitor (event mode)       SRC/workflows/monitor_workflow.py:65-112
+ *   NoCopyAccumulator / window pair       SRC/preprocessors/accumulators.py:86-195
+ *   detector_image/counts_total/counts_in_range  providers.py:236-357
+ *
+ * Plain C types only: host pointers, device pointers as void*, sizes as
+ * int64_t.  No C++ exceptions cross this boundary.  Every entry point returns
+ * LDE_OK (0) or a negative error code; lde_last_error() gives the message.
+ * The Python host maps LDE_EINVAL to ValueError and everything else to
+ * RuntimeError, matching the reference's error conventions.
+ *
+ * Threading: a handle is single-thread-affine (one job per worker thread in
+ * the reference, SRC/core/job_manager.py:698-701); distinct handles are
+ * independent and may be driven from different threads concurrently.  Each
+ * handle owns its HIP stream unless the caller passes one.
+ */
+#ifndef LDE_H
+#define LDE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDE_ABI_VERSION 1
+
+/* error codes */
+#define LDE_OK 0
+#define LDE_EINVAL (-1)   /* invalid argument  -> ValueError   */
+#define LDE_ESTATE (-2)   /* invalid call order -> RuntimeError */
+#define LDE_ENOMEM (-3)   /* allocation failed  -> RuntimeError */
+#define LDE_EHIP (-4)     /* HIP runtime error  -> RuntimeError */
+#define LDE_ENODATA (-5)  /* nothing accumulated -> ValueError ("No data has been added") */
+
+/* output element types */
+#define LDE_F64 0 /* float64 counts (reference default, unit 'counts') */
+#define LDE_F32 1 /* float32 counts (BIFROST logical view, bifrost/specs.py:295) */
+
+/* binning strategies (LDE_AUTO lets the engine choose per batch) */
+#define LDE_STRATEGY_AUTO 0
+#define LDE_STRATEGY_ATOMIC 1      /* one pass, global atomics             */
+#define LDE_STRATEGY_PARTITION 2   /* tile partition + LDS sub-histograms  */
+
+/* histogram selectors for lde_read_histogram */
+#define LDE_CURRENT 0    /* window since the last finalize  (accumulators.py:138-163) */
+#define LDE_CUMULATIVE 1 /* since job start / last reset     (accumulators.py:86-135)  */
+
+typedef struct lde_handle lde_handle;
+
+/*
+ * Engine configuration.  The pid -> output LUT folds the reference's
+ * group_event_data membership test (unknown ids dropped), the pixel index and
+ * the per-replica geometric/logical projection into one table:
+ *
+ *   out_lut[r * lut_len + (pid - pid_offset)] = flat screen index, or -1.
+ *
+ * A monitor is the special case n_screen = 1, n_replicas = 1 with a NULL
+ * out_lut: every event maps to screen 0 and pixel ids are ignored.
+ */
+typedef struct lde_config {
+    int32_t abi_version;      /* must be LDE_ABI_VERSION */
+    int32_t device_id;        /* HIP device ordinal */
+    void *stream;             /* hipStream_t to run on, or NULL = engine-owned */
+    int32_t pid_offset;       /* smallest pixel id the LUT covers */
+    int32_t n_replicas;       /* R >= 1 (noise replicas, projectors.py:105-113) */
+    int64_t lut_len;          /* L: pixel ids pid_offset .. pid_offset+L-1 */
+    const int32_t *out_lut;   /* host [R*L] screen index or -1; NULL for monitors */
+    int64_t n_screen;         /* S >= 1 */
+    int32_t n_toa_bins;       /* T >= 1 */
+    const double *toa_edges;  /* host [T+1] float64 edges in the event unit (ns) */
+    int32_t out_dtype;        /* LDE_F64 or LDE_F32 */
+    int32_t strategy;         /* LDE_STRATEGY_* */
+    int32_t range_lo;         /* TOA-range bin slice [range_lo, range_hi) used for */
+    int32_t range_hi;         /*  detector_image / counts_in_range (-1,-1 = all)   */
+} lde_config;
+
+/* Finalize outputs.  Every pointer is an optional host buffer (NULL = skip).
+ * Image element type = out_dtype; totals are exact integer counts. */
+typedef struct lde_outputs {
+    void *current_image;       /* [S]   sum over TOA range of the window     */
+    void *cumulative_image;    /* [S]   sum over TOA range of the cumulative */
+    void *current_hist;        /* [S*T] full window histogram                */
+    void *cumulative_hist;     /* [S*T] full cumulative histogram            */
+    uint64_t totals[4];        /* current total, current in-range,
+                                  cumulative total, cumulative in-range      */
+} lde_outputs;
+
+/* Create / destroy.  On failure *out is NULL and lde_last_error(NULL) holds
+ * the message (thread-local). */
+int lde_create(const lde_config *cfg, lde_handle **out);
+void lde_destroy(lde_handle *h);
+const char *lde_last_error(const lde_handle *h);
+int lde_abi_version(void);
+
+/* Stage one ev44 message worth of events (replaces ToNXevent_data.add).
+ * Host pointers; copied H2D asynchronously on the handle's stream before the
+ * call returns (the caller may reuse its buffers).  pid may be NULL for a
+ * monitor.  n == 0 is accepted (empty message). */
+int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n);
+
+/* Stage events already resident in HBM.  No copy: the device buffers must
+ * stay valid until the next lde_accumulate returns. */
+int lde_stage_device(lde_handle *h, const void *d_pid, const void *d_toa, int64_t n);
+
+/* Bin everything staged since the last call into the current window using
+ * noise replica `replica` (0 <= replica < R).  Replaces
+ * GroupByPixel.get + project_events + hist + accumulator push. */
+int lde_accumulate(lde_handle *h, int32_t replica);
+
+/* Finalize: cumulative += window, fill the requested outputs, clear the
+ * window (window accumulator on_finalize).  Returns LDE_ENODATA when nothing
+ * was accumulated since the last finalize (the reference's empty window
+ * accumulator raises ValueError). */
+int lde_finalize(lde_handle *h, lde_outputs *out);
+
+/* Read a full histogram (LDE_CURRENT or LDE_CUMULATIVE) without finalizing. */
+int lde_read_histogram(lde_handle *h, int32_t which, void *host_out);
+
+/* Reset semantics: clear both (workflow.clear / Job.reset) or drop the
+ * cumulative and window because the geometry coord changed
+ * (NoCopyAccumulator._reset_if_geometry_changed, accumulators.py:116-131). */
+int lde_clear(lde_handle *h);
+int lde_reset_cumulative(lde_handle *h);
+
+/* Multi-GPU merge support (no reference counterpart): export the window
+ * counts (uint32 [S*T]) into a caller device buffer, and import merged
+ * counts back (e.g. after an RCCL reduce over xGMI). */
+int lde_export_window(lde_handle *h, void *d_dst);
+int lde_import_window(lde_handle *h, const void *d_src);
+
+/* Wait for all work queued on the handle's stream. */
+int lde_synchronize(lde_handle *h);
+
+/* Kernel timing, measured with HIP events recorded on the handle's stream
+ * around each launch of the engine's kernels (ids LDE_K_*).  Recording is off
+ * until lde_timing_enable(h, 1); enabling again resets the statistics.
+ * lde_kernel_stats synchronizes the stream and returns the summed kernel
+ * milliseconds and the launch count for one kernel id. */
+#define LDE_K_ATOMIC 0    /* k_bin_atomic: one-pass global-atomic binning   */
+#define LDE_K_PARTITION 1 /* k_partition: pass A, tile partition            */
+#define LDE_K_PLAN 2      /* k_tile_totals + k_plan                          */
+#define LDE_K_TILE 3      /* k_tile_accumulate: pass B, LDS sub-histograms   */
+#define LDE_K_MONITOR 4   /* k_monitor: 1-D TOA histogram                    */
+#define LDE_K_FINALIZE 5  /* k_finalize / merge kernels                      */
+#define LDE_K_BINNING 6   /* whole binning sequence of one accumulate        */
+#define LDE_K_COUNT 7
+int lde_timing_enable(lde_handle *h, int32_t enable);
+int lde_kernel_stats(lde_handle *h, int32_t kernel_id, double *ms, int64_t *launches);
+
+/* Introspection for tests and reports. */
+int lde_info(lde_handle *h, int64_t *n_screen, int32_t *n_toa_bins, int64_t *staged,
+             int32_t *tile_bits, int32_t *n_tiles, int64_t *events_binned,
+             int32_t *last_strategy);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LDE_H */

@@ -1,0 +1,352 @@
+"""CPU oracle: a NumPy restatement of the reference's event-binning hot path.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the
+checker / CPU baseline.  The product path (``esslivedata_amd``) never imports
+it: binning always runs on the HIP engine and fails loudly without it.
+
+What is restated (reference = /root/reference, SRC = src/ess/livedata):
+
+* TOA edges: ``make_edges`` -> ``sc.linspace``/``sc.geomspace`` (numpy under the
+  hood), SRC/parameter_models.py:290-295; converted to the event unit with
+  ``bins.to(unit=event_unit)`` (ms -> ns, one f64 multiply by 1e6),
+  SRC/workflows/detector_view/providers.py:205-207 and
+  SRC/workflows/monitor_workflow.py:93-95.
+* scipp ``hist``: half-open bins ``[e_i, e_{i+1})`` including the last one,
+  int32 event coordinate compared against float64 edges, out-of-range and NaN
+  dropped (providers.py:208, monitor_workflow.py:97).
+* ``group_event_data``: events whose ``event_id`` is not a value of the
+  flattened ``detector_number`` are dropped; pixel index = row-major position
+  (SRC/preprocessors/group_by_pixel.py:36-54, _patch_group_event_data.py:23-35).
+* ``GeometricProjector``: one replica per ``project_events`` call, cycling
+  ``counter % R`` (SRC/workflows/detector_view/projectors.py:105-113); per-event
+  screen coordinate gather (:123-143) then ``bin(edges)`` (:152); screen edges
+  ``coords[dim].hist({dim: res}).coords[dim]`` (:344-350) = scipp's
+  int-bin-count rule ``linspace(nanmin, nextafter(nanmax, +inf), res + 1)``;
+  ``flip_x`` negates x (:341-342).
+* ``LogicalProjector``: transform (reshape/slice) then ``bins.concat`` over the
+  reduction dims (projectors.py:243-270); restated as an index-array transform.
+* Accumulators: cumulative ``NoCopyAccumulator`` (first push copies, then
+  ``+=``, reset when the scalar reset coord changes) and the window
+  accumulator cleared on finalize (SRC/preprocessors/accumulators.py:86-195).
+* Finalize outputs: ``detector_image`` (sum over the spectral dim, optional
+  label slice), ``counts_total``, ``counts_in_range``
+  (providers.py:236-357); monitor ``counts_total``/``counts_in_range``
+  (monitor_workflow.py:147-167); output target names
+  (detector_view/factory.py:208-215, monitor_workflow.py:318-325).
+
+Scipp rules that cannot be verified offline (scipp is not installed) are pinned
+by the hand-derived known-answer tests in ``tests/test_oracle_kat.py`` and by
+the reference's own test expectations; see DESIGN.md "Parity".
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Sequence
+
+import numpy as np
+
+# ESS_PULSE_PERIOD_MS, SRC/parameter_models.py:26
+ESS_PULSE_PERIOD_MS = float(np.ceil(1000.0 / 14 * 100) / 100)
+
+# scipp unit conversion factors for time units -> ns (f64 multiply).
+_TO_NS = {'ns': 1.0, 'us': 1e3, 'μs': 1e3, 'ms': 1e6, 's': 1e9}
+
+
+# --------------------------------------------------------------------------
+# Edges
+# --------------------------------------------------------------------------
+def make_edges(start: float, stop: float, num_bins: int, scale: str = 'linear'):
+    """``make_edges`` (SRC/parameter_models.py:290-295): linspace/geomspace."""
+    if scale == 'linear':
+        return np.linspace(start, stop, num_bins + 1)
+    if scale == 'log':
+        return np.geomspace(start, stop, num_bins + 1)
+    raise ValueError(f"unknown scale {scale!r}")
+
+
+def to_ns(edges: np.ndarray, unit: str) -> np.ndarray:
+    """``edges.to(unit='ns')`` as one f64 multiply (providers.py:207)."""
+    factor = _TO_NS[unit]
+    edges = np.asarray(edges, dtype=np.float64)
+    return edges if factor == 1.0 else edges * factor
+
+
+def hist_bin_index(values: np.ndarray, edges: np.ndarray) -> np.ndarray:
+    """Bin index of each value under scipp's ``hist`` rule; -1 = dropped.
+
+    Half-open ``[e_i, e_{i+1})`` for every bin including the last, comparison
+    in float64 (int32 TOA promoted exactly), NaN dropped.
+    """
+    v = np.asarray(values)
+    vf = v.astype(np.float64, copy=False)
+    idx = np.searchsorted(edges, vf, side='right') - 1
+    nb = len(edges) - 1
+    bad = (idx < 0) | (idx >= nb)
+    if vf.dtype.kind == 'f':
+        bad |= np.isnan(vf)
+    idx = idx.astype(np.int64)
+    idx[bad] = -1
+    return idx
+
+
+def label_slice(edges: np.ndarray, low: float, high: float) -> tuple[int, int]:
+    """Bin range selected by scipp label slicing ``da[dim, low:high]`` on a
+    bin-edge coordinate: from the bin containing ``low`` to the bins that
+    overlap ``[low, high)``.  Pinned by the KAT at
+    tests/workflows/monitor_workflow_test.py:233-243 (edges 0..10 ns / 6,
+    [2 ns, 8 ns) -> bins 1..3)."""
+    nb = len(edges) - 1
+    begin = int(np.searchsorted(edges, low, side='right')) - 1
+    end = int(np.searchsorted(edges, high, side='left'))
+    return max(begin, 0), min(max(end, 0), nb)
+
+
+def screen_edges(coord_all_replicas: np.ndarray, res: int) -> np.ndarray:
+    """scipp ``Variable.hist({dim: res})`` edge rule (projectors.py:344-350):
+    ``linspace(nanmin, nextafter(nanmax, +inf), res + 1)`` over all replicas."""
+    lo = float(np.nanmin(coord_all_replicas))
+    hi = float(np.nanmax(coord_all_replicas))
+    return np.linspace(lo, np.nextafter(hi, np.inf), res + 1)
+
+
+# --------------------------------------------------------------------------
+# Pixel grouping and projection (LUT construction is setup-time)
+# --------------------------------------------------------------------------
+def pixel_index(event_id: np.ndarray, detector_number: np.ndarray) -> np.ndarray:
+    """``group_event_data`` membership: row-major pixel index or -1 (dropped)."""
+    dn = np.asarray(detector_number).ravel()
+    order = np.argsort(dn, kind='stable')
+    sdn = dn[order]
+    pos = np.searchsorted(sdn, event_id)
+    pos_c = np.minimum(pos, len(sdn) - 1)
+    hit = (pos < len(sdn)) & (sdn[pos_c] == event_id)
+    out = np.full(len(event_id), -1, dtype=np.int64)
+    out[hit] = order[pos_c[hit]]
+    return out
+
+
+def geometric_screen_index(
+    coords: dict[str, np.ndarray], edges: dict[str, np.ndarray], replica: int
+) -> np.ndarray:
+    """Flat screen index per pixel for one replica (-1 = outside / NaN).
+
+    ``coords[dim]`` has shape ``(R, P)``; dims in ``edges`` order (the order of
+    the ``resolution`` dict, projectors.py:345-350) are row-major.
+    """
+    dims = list(edges)
+    flat = None
+    for dim in dims:
+        b = hist_bin_index(np.asarray(coords[dim])[replica], edges[dim])
+        n = len(edges[dim]) - 1
+        if flat is None:
+            flat = b.copy()
+        else:
+            bad = (flat < 0) | (b < 0)
+            flat = flat * n + b
+            flat[bad] = -1
+    return flat
+
+
+def logical_screen_index(
+    detector_shape: Sequence[int],
+    transform: Callable[[np.ndarray], np.ndarray] | None,
+    reduction_axes: Sequence[int] = (),
+) -> tuple[np.ndarray, tuple[int, ...]]:
+    """Output index per pixel for a logical view (projectors.py:243-270).
+
+    The transform is applied to an index-valued array shaped like the
+    detector; pixels that the transform drops (slicing) get -1; reduced axes
+    are merged (``bins.concat``).  Returns ``(lut[P], output_shape)``.
+    """
+    p = int(np.prod(detector_shape))
+    idx = np.arange(p, dtype=np.int64).reshape(detector_shape)
+    t = idx if transform is None else transform(idx)
+    t = np.asarray(t)
+    kept = [a for a in range(t.ndim) if a not in set(reduction_axes)]
+    out_shape = tuple(t.shape[a] for a in kept)
+    moved = np.moveaxis(t, kept, list(range(len(kept))))
+    n_out = int(np.prod(out_shape)) if out_shape else 1
+    moved = moved.reshape(n_out, -1)
+    lut = np.full(p, -1, dtype=np.int64)
+    for o in range(n_out):
+        lut[moved[o]] = o
+    return lut, out_shape
+
+
+# --------------------------------------------------------------------------
+# Histograms
+# --------------------------------------------------------------------------
+def detector_histogram(
+    pixel_screen: np.ndarray,
+    n_screen: int,
+    event_pixel: np.ndarray,
+    toa: np.ndarray,
+    toa_edges_ns: np.ndarray,
+    dtype=np.float64,
+) -> np.ndarray:
+    """One batch: group -> project -> ``hist`` over TOA (providers.py:169-214).
+
+    ``event_pixel`` is the pixel index per event (-1 = unknown id) and
+    ``pixel_screen`` the screen index per pixel (-1 = off screen).
+    Returns ``(n_screen, T)`` counts in ``dtype`` (f64, or f32 for BIFROST).
+    """
+    t = len(toa_edges_ns) - 1
+    ok = event_pixel >= 0
+    scr = np.full(len(event_pixel), -1, dtype=np.int64)
+    scr[ok] = pixel_screen[event_pixel[ok]]
+    tb = hist_bin_index(toa, toa_edges_ns)
+    keep = (scr >= 0) & (tb >= 0)
+    flat = scr[keep] * t + tb[keep]
+    counts = np.bincount(flat, minlength=n_screen * t)
+    return counts.reshape(n_screen, t).astype(dtype)
+
+
+def monitor_histogram(toa: np.ndarray, toa_edges_ns: np.ndarray) -> np.ndarray:
+    """``_histogram_monitor`` event mode (monitor_workflow.py:90-100)."""
+    tb = hist_bin_index(toa, toa_edges_ns)
+    tb = tb[tb >= 0]
+    return np.bincount(tb, minlength=len(toa_edges_ns) - 1).astype(np.float64)
+
+
+# --------------------------------------------------------------------------
+# Accumulator pair (accumulators.py:86-195)
+# --------------------------------------------------------------------------
+@dataclass
+class AccumulatorPair:
+    """Cumulative (copy on first push, ``+=``) + window (cleared on finalize),
+    both resetting when the pushed value's geometry coord differs."""
+
+    cumulative: np.ndarray | None = None
+    window: np.ndarray | None = None
+    cum_geom: object = None
+    win_geom: object = None
+
+    @staticmethod
+    def _changed(stored, new) -> bool:
+        return stored is not None and new is not None and stored != new
+
+    def push(self, value: np.ndarray, geometry=None) -> None:
+        if self.cumulative is not None and self._changed(self.cum_geom, geometry):
+            self.cumulative = None
+        if self.cumulative is None:
+            self.cumulative = value.copy()
+        else:
+            self.cumulative += value
+        self.cum_geom = geometry
+        if self.window is not None and self._changed(self.win_geom, geometry):
+            self.window = None
+        if self.window is None:
+            self.window = value.copy()
+        else:
+            self.window += value
+        self.win_geom = geometry
+
+    def on_finalize(self) -> None:
+        self.window = None
+        self.win_geom = None
+
+    def clear(self) -> None:
+        self.cumulative = None
+        self.window = None
+        self.cum_geom = None
+        self.win_geom = None
+
+
+# --------------------------------------------------------------------------
+# Workflow-level restatements
+# --------------------------------------------------------------------------
+@dataclass
+class OracleDetectorView:
+    """Detector-view workflow semantics (factory.py:95-276, providers.py)."""
+
+    detector_number: np.ndarray
+    pixel_screen: np.ndarray  # (R, P) screen index per replica and pixel
+    screen_shape: tuple[int, ...]
+    toa_edges_ns: np.ndarray
+    toa_slice: tuple[int, int] | None = None  # bin range of HistogramSlice
+    dtype: type = np.float64
+    _counter: int = 0
+    _acc: AccumulatorPair = field(default_factory=AccumulatorPair)
+
+    @property
+    def n_screen(self) -> int:
+        return int(np.prod(self.screen_shape))
+
+    def batch_histogram(self, pid, toa, replica: int) -> np.ndarray:
+        pix = pixel_index(np.asarray(pid), self.detector_number)
+        return detector_histogram(
+            self.pixel_screen[replica],
+            self.n_screen,
+            pix,
+            np.asarray(toa),
+            self.toa_edges_ns,
+            self.dtype,
+        )
+
+    def accumulate(self, pid, toa, geometry=None) -> None:
+        r = self._counter % self.pixel_screen.shape[0]
+        self._counter += 1
+        self._acc.push(self.batch_histogram(pid, toa, r), geometry)
+
+    def _outputs(self, hist: np.ndarray) -> dict:
+        lo, hi = self.toa_slice if self.toa_slice else (0, hist.shape[-1])
+        img = hist[:, lo:hi].sum(axis=-1).reshape(self.screen_shape)
+        return {
+            'image': img,
+            'total': hist.sum(),
+            'in_range': hist[:, lo:hi].sum(),
+        }
+
+    def finalize(self) -> dict:
+        if self._acc.cumulative is None:
+            raise ValueError("No data has been added")
+        cum = self._outputs(self._acc.cumulative)
+        cur = self._outputs(self._acc.window)
+        out = {
+            'cumulative': cum['image'],
+            'current': cur['image'],
+            'counts_total': cur['total'],
+            'counts_in_toa_range': cur['in_range'],
+            'counts_total_cumulative': cum['total'],
+            'counts_in_toa_range_cumulative': cum['in_range'],
+            'histogram_cumulative': self._acc.cumulative.copy(),
+            'histogram_current': self._acc.window.copy(),
+        }
+        self._acc.on_finalize()
+        return out
+
+    def clear(self) -> None:
+        self._acc.clear()
+
+
+@dataclass
+class OracleMonitor:
+    """Monitor-histogram workflow semantics (monitor_workflow.py:65-331)."""
+
+    toa_edges_ns: np.ndarray
+    range_slice: tuple[int, int] | None = None
+    _acc: AccumulatorPair = field(default_factory=AccumulatorPair)
+
+    def accumulate(self, toa, geometry=None) -> None:
+        self._acc.push(monitor_histogram(np.asarray(toa), self.toa_edges_ns), geometry)
+
+    def finalize(self) -> dict:
+        if self._acc.cumulative is None:
+            raise ValueError("No data has been added")
+        lo, hi = self.range_slice if self.range_slice else (0, len(self.toa_edges_ns) - 1)
+        cum, cur = self._acc.cumulative, self._acc.window
+        out = {
+            'cumulative': cum.copy(),
+            'current': cur.copy(),
+            'counts_total': cur.sum(),
+            'counts_in_toa_range': cur[lo:hi].sum(),
+            'counts_total_cumulative': cum.sum(),
+            'counts_in_toa_range_cumulative': cum[lo:hi].sum(),
+        }
+        self._acc.on_finalize()
+        return out
+
+    def clear(self) -> None:
+        self._acc.clear()

@@ -1,0 +1,280 @@
+"""GPU parity: HIP engine (through the C ABI) vs the CPU oracle, bit-exact.
+
+Counts are integers, so every comparison here is exact equality of the f64
+(or f32) arrays the reference would produce.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import scipp_semantics as ora
+
+pytestmark = pytest.mark.gpu
+
+STRATEGIES = ['atomic', 'partition']
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu(engine_lib):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+
+
+def _engine(view, edges_ns, strategy='auto', **kw):
+    from esslivedata_amd.engine import BinningEngine
+
+    return BinningEngine(
+        toa_edges_ns=edges_ns,
+        out_lut=view.lut,
+        pid_offset=view.pid_offset,
+        n_screen=view.n_screen,
+        strategy=strategy,
+        **kw,
+    )
+
+
+def _oracle_pixel_screen_geometric(inst):
+    edges = {d: ora.screen_edges(inst.coords[d], r) for d, r in inst.resolution.items()}
+    r = next(iter(inst.coords.values())).shape[0]
+    return np.stack([ora.geometric_screen_index(inst.coords, edges, k) for k in range(r)])
+
+
+# ---------------------------------------------------------------------------
+def test_monitor_kat_reference_fixture():
+    """monitor_workflow_test.py:176-183: TOA 1..5 ns, edges linspace(0,10,6) ns."""
+    from esslivedata_amd.engine import BinningEngine
+
+    edges = np.linspace(0, 10, 6)
+    eng = BinningEngine.monitor(edges)
+    eng.stage(None, np.array([1, 2, 3, 4, 5], dtype=np.int32))
+    eng.accumulate()
+    res = eng.finalize(hists=True)
+    np.testing.assert_array_equal(res.current_hist.ravel(), [1, 2, 2, 0, 0])
+    assert res.current_total == 5
+    np.testing.assert_array_equal(
+        res.current_hist.ravel(), ora.monitor_histogram(np.arange(1, 6), edges)
+    )
+
+
+@pytest.mark.parametrize('n_bins', [100, 7, 1000, 3000])
+def test_monitor_matches_oracle(n_bins):
+    from esslivedata_amd.engine import BinningEngine
+
+    rng = np.random.default_rng(n_bins)
+    edges = np.geomspace(0.5, 71.43, n_bins + 1) * 1e6
+    toa = np.concatenate(
+        [
+            rng.normal(30e6, 10e6, 200_000).astype(np.int32),
+            np.ceil(edges).astype(np.int32),
+            np.ceil(edges).astype(np.int32) - 1,
+            np.full(50_000, int(np.ceil(edges[3])), dtype=np.int32),  # hot bin
+        ]
+    )
+    eng = BinningEngine.monitor(edges)
+    eng.stage(None, toa)
+    eng.accumulate()
+    res = eng.finalize(hists=True)
+    np.testing.assert_array_equal(res.current_hist.ravel(), ora.monitor_histogram(toa, edges))
+
+
+@pytest.mark.parametrize('strategy', STRATEGIES)
+def test_dummy_logical_view_multi_batch(strategy):
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.dummy_panel()
+    view = projection.logical_lut(inst.detector_number, dims=('y', 'x'))
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, strategy)
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=ora.logical_screen_index(inst.detector_number.shape, None)[0][None, :],
+        screen_shape=(128, 128),
+        toa_edges_ns=edges,
+    )
+    for batch, size in enumerate([2000, 3000, 1000, 1000, 250_000]):
+        pid, toa = synthetic.fake_detector_events(size, 0, 16384 + 5, seed=batch)
+        eng.stage(pid, toa)
+        eng.accumulate(0)
+        o.accumulate(pid, toa)
+        if batch in (0, 1, 3, 4):
+            res = eng.finalize(hists=True)
+            exp = o.finalize()
+            np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
+            np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
+            np.testing.assert_array_equal(res.current_image.reshape(128, 128), exp['current'])
+            np.testing.assert_array_equal(
+                res.cumulative_image.reshape(128, 128), exp['cumulative']
+            )
+            assert res.current_total == exp['counts_total']
+            assert res.cumulative_total == exp['counts_total_cumulative']
+
+
+@pytest.mark.parametrize('strategy', STRATEGIES)
+def test_dream_mantle_geometric_skewed(strategy):
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.dream_mantle()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    lo, hi = 10, 90
+    eng = _engine(view, edges, strategy, toa_range=(lo, hi))
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=_oracle_pixel_screen_geometric(inst),
+        screen_shape=(80, 320),
+        toa_edges_ns=edges,
+        toa_slice=(lo, hi),
+    )
+    for batch in range(3):  # replicas cycle 0, 1, 2
+        pid, toa = synthetic.dream_events(1_500_000, inst, seed=100 + batch)
+        # unknown ids on both sides of the LUT
+        pid[:1000] = 229376
+        pid[1000:2000] = 720897
+        eng.stage(pid[: len(pid) // 2], toa[: len(toa) // 2])
+        eng.stage(pid[len(pid) // 2 :], toa[len(toa) // 2 :])
+        eng.accumulate(batch % view.n_replicas)
+        o.accumulate(pid, toa)
+    res = eng.finalize(hists=True)
+    exp = o.finalize()
+    assert eng.info()['last_strategy'] == strategy
+    np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
+    np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
+    np.testing.assert_array_equal(res.current_image.reshape(80, 320), exp['current'])
+    assert res.current_in_range == exp['counts_in_toa_range']
+    assert res.cumulative_in_range == exp['counts_in_toa_range_cumulative']
+
+
+@pytest.mark.parametrize('strategy', STRATEGIES)
+def test_edge_ties_are_bit_exact(strategy):
+    """Integer TOAs on, just below and just above every float64 edge."""
+    from esslivedata_amd import projection
+
+    dn = np.arange(1, 65, dtype=np.int32)
+    view = projection.logical_lut(dn)
+    for edges in (
+        np.linspace(0, 71.43, 101) * 1e6,
+        np.geomspace(0.5, 71.43, 101) * 1e6,
+        np.array([-5.5, -0.5, 0.0, 0.5, 1.0, 1.0, 2.5, 3.0, 1e6 + 0.25]),
+    ):
+        c = np.ceil(edges).astype(np.int64)
+        toa = np.concatenate([c - 1, c, c + 1, np.floor(edges).astype(np.int64)])
+        toa = np.clip(toa, -(2**31), 2**31 - 1).astype(np.int32)
+        pid = np.resize(dn, len(toa))
+        eng = _engine(view, edges, strategy)
+        eng.stage(pid, toa)
+        eng.accumulate(0)
+        got = eng.finalize(hists=True).current_hist
+        pix = ora.pixel_index(pid, dn)
+        exp = ora.detector_histogram(np.arange(64), 64, pix, toa, edges)
+        np.testing.assert_array_equal(got, exp)
+
+
+def test_bifrost_float32_accumulation():
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.bifrost_unified()
+    view = projection.logical_lut(inst.detector_number, transform=synthetic.bifrost_transform)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, 'auto', out_dtype='float32')
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=ora.logical_screen_index((5, 3, 9, 100), synthetic.bifrost_transform)[0][
+            None, :
+        ],
+        screen_shape=(15, 900),
+        toa_edges_ns=edges,
+        dtype=np.float32,
+    )
+    for batch in range(20):
+        pid, toa = synthetic.fake_detector_events(45_000, 1, 13500, seed=batch)
+        eng.stage(pid, toa)
+        eng.accumulate(0)
+        o.accumulate(pid, toa)
+        if batch % 5 == 4:
+            res = eng.finalize(hists=True)
+            exp = o.finalize()
+            assert res.current_hist.dtype == np.float32
+            np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
+            np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
+
+
+def test_empty_and_all_dropped_batches():
+    from esslivedata_amd import projection
+
+    dn = np.arange(10, 20, dtype=np.int32)
+    view = projection.logical_lut(dn)
+    edges = np.linspace(0, 100, 11)
+    eng = _engine(view, edges)
+    with pytest.raises(ValueError, match='No data'):
+        eng.finalize()
+    eng.accumulate(0)  # empty batch still produces (zero) outputs
+    res = eng.finalize(hists=True)
+    assert res.current_total == 0 and res.cumulative_total == 0
+    eng.stage(np.array([1, 2, 30], np.int32), np.array([5, 5, 5], np.int32))  # unknown ids
+    eng.stage(np.array([10, 11], np.int32), np.array([-1, 100], np.int32))  # out of range TOA
+    eng.accumulate(0)
+    res = eng.finalize(hists=True)
+    assert res.current_total == 0
+    with pytest.raises(ValueError):
+        eng.accumulate(1)  # replica out of range
+    with pytest.raises(ValueError):
+        eng.stage(np.array([1, 2], np.int32), np.array([1], np.int32))
+
+
+def test_reset_and_clear_semantics():
+    from esslivedata_amd import projection
+
+    dn = np.arange(1, 5, dtype=np.int32)
+    view = projection.logical_lut(dn)
+    edges = np.linspace(0, 10, 3)
+    eng = _engine(view, edges)
+    eng.stage(np.array([1, 2], np.int32), np.array([1, 6], np.int32))
+    eng.accumulate(0)
+    eng.finalize()
+    eng.stage(np.array([3], np.int32), np.array([1], np.int32))
+    eng.accumulate(0)
+    assert eng.read_histogram('cumulative').sum() == 3
+    eng.reset_cumulative()  # geometry changed: drop cumulative and window
+    eng.stage(np.array([4], np.int32), np.array([7], np.int32))
+    eng.accumulate(0)
+    res = eng.finalize(hists=True)
+    assert res.cumulative_total == 1 and res.current_total == 1
+    eng.clear()
+    with pytest.raises(ValueError):
+        eng.finalize()
+
+
+@pytest.mark.parametrize('strategy', STRATEGIES)
+def test_device_staging_matches_host_staging(strategy):
+    import torch
+
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.loki_bank0()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution, flip_x=True)
+    edges = inst.edges.edges_ns()
+    pid, toa = synthetic.uniform_events(3_000_001, 1, 802816 + 100, seed=5)
+    a = _engine(view, edges, strategy)
+    a.stage(pid, toa)
+    a.accumulate(1)
+    b = _engine(view, edges, strategy)
+    dp = torch.as_tensor(pid, device='cuda')
+    dt = torch.as_tensor(toa, device='cuda')
+    b.stage_tensors(dp[:1_000_003], dt[:1_000_003])  # misaligned second segment
+    b.stage_tensors(dp[1_000_003:], dt[1_000_003:])
+    b.accumulate(1)
+    np.testing.assert_array_equal(a.read_histogram(), b.read_histogram())
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=_oracle_pixel_screen_geometric(
+            synthetic.Instrument(
+                'l', inst.detector_number, {'x': -inst.coords['x'], 'y': inst.coords['y']},
+                inst.resolution, inst.edges,
+            )
+        ),
+        screen_shape=(144, 144),
+        toa_edges_ns=edges,
+    )
+    np.testing.assert_array_equal(a.read_histogram(), o.batch_histogram(pid, toa, 1))
