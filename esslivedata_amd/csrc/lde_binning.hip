@@ -1,0 +1,652 @@
+// lde_binning.hip -- CDNA4 (gfx950) event-binning kernels.
+//
+// Hot path, per event:
+//   pid -> LUT[replica][pid - pid_offset]   screen index or invalid; folds
+//          group_event_data membership + pixel index + projection
+//          (group_by_pixel.py:46-54, projectors.py:118-152 / 243-270)
+//   toa -> TOA bin under scipp's half-open float64-edge rule (providers.py:205-210)
+//   count[screen*T + bin] += 1
+//
+// Exact integer TOA binning: for int32 t and float64 edge e, t >= e <=> t >= ceil(e).
+// The host turns the f64 edges into integer thresholds and builds the LDS
+// image of a lookup table; two layouts:
+//   FAST    : u32 thresholds relative to lo + u16 bucket table whose buckets are
+//             narrower than every bin, so bin = bst[d >> shift] + (d >= rthr[b+1])
+//             (one LDS gather, one compare, no branch).
+//   general : int64 thresholds + (first, last) candidate pairs per bucket with a
+//             binary search inside the bucket (any sorted edges).
+//
+// Strategies (bit-identical integer counts):
+//   ATOMIC    : one pass, one agent-scope u32 atomic per event.
+//   PARTITION : pass A partitions events into LDS-sized tiles of the (S, T)
+//               histogram (chunk-major tile-sorted runs, no global atomics);
+//               k_plan splits tiles into balanced work items; pass B
+//               accumulates each item in an LDS sub-histogram and flushes the
+//               non-zero bins with coalesced atomics.
+//   monitors  : conflict-free per-lane-column LDS histogram.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lde_internal.h"
+
+namespace lde {
+
+// ---------------------------------------------------------------------------
+// TOA lookup
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_toa_tables(unsigned char *s_tab,
+                                                const unsigned char *__restrict__ g_tab,
+                                                const ToaParams &tp) {
+    const int n16 = (int)(toa_lds_bytes(tp) / 16);
+    for (int i = threadIdx.x; i < n16; i += blockDim.x)
+        reinterpret_cast<uint4 *>(s_tab)[i] = reinterpret_cast<const uint4 *>(g_tab)[i];
+}
+
+template <bool FAST>
+__device__ __forceinline__ int toa_bin(int t, const unsigned char *s_tab, const ToaParams &tp) {
+    if (FAST) {
+        const unsigned d = (unsigned)t - (unsigned)tp.lo;
+        if (d >= tp.span) return -1;
+        const uint32_t *rthr = reinterpret_cast<const uint32_t *>(s_tab);
+        const uint16_t *bst =
+            reinterpret_cast<const uint16_t *>(s_tab + align16((size_t)(tp.T + 1) * 4));
+        const int b = bst[d >> tp.shift];
+        return b + (d >= rthr[b + 1] ? 1 : 0);
+    } else {
+        const long long tt = t;
+        if (tt < tp.lo || tt >= tp.hi) return -1;
+        const long long *thr = reinterpret_cast<const long long *>(s_tab);
+        const uint32_t *bp =
+            reinterpret_cast<const uint32_t *>(s_tab + align16((size_t)(tp.T + 1) * 8));
+        const uint32_t pr = bp[(unsigned)((unsigned long long)(tt - tp.lo) >> tp.shift)];
+        int b = (int)(pr & 0xFFFFu);
+        int e = (int)(pr >> 16);
+        while (b < e) {
+            const int m = (b + e + 1) >> 1;
+            if (tt >= thr[m]) b = m; else e = m - 1;
+        }
+        return b;
+    }
+}
+
+// LUT entry -> flat histogram base (screen * T) or -1
+__device__ __forceinline__ int lut_base(const uint16_t *__restrict__ lut, unsigned p, int T) {
+    const unsigned v = lut[p];
+    return v == 0xFFFFu ? -1 : (int)(v * (unsigned)T);
+}
+__device__ __forceinline__ int lut_base(const int *__restrict__ lut, unsigned p, int) {
+    return lut[p];
+}
+
+template <typename LT, bool FAST>
+__device__ __forceinline__ int event_key(int pid, int t, const LT *__restrict__ lut, int pid_off,
+                                        unsigned L, const unsigned char *s_tab,
+                                        const ToaParams &tp) {
+    const unsigned p = (unsigned)pid - (unsigned)pid_off;
+    if (p >= L) return -1;
+    const int base = lut_base(lut, p, tp.T);
+    if (base < 0) return -1;
+    const int b = toa_bin<FAST>(t, s_tab, tp);
+    return b < 0 ? -1 : base + b;
+}
+
+// ---------------------------------------------------------------------------
+// wave / block helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// exclusive prefix of v across the block; *total = block sum.  s_w >= 17
+// uint32; contains two __syncthreads().
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *s_w,
+                                                         uint32_t *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nw = blockDim.x >> 6;
+    const uint32_t inc = wave_inclusive_scan(v);
+    if (lane == 63) s_w[wid] = inc;
+    __syncthreads();
+    if (wid == 0) {
+        const uint32_t w = lane < nw ? s_w[lane] : 0u;
+        const uint32_t wi = wave_inclusive_scan(w);
+        if (lane < nw) s_w[lane] = wi - w;
+        if (lane == nw - 1) s_w[16] = wi;
+    }
+    __syncthreads();
+    *total = s_w[16];
+    return inc - v + s_w[wid];
+}
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// ATOMIC strategy: one pass, global u32 atomics (agent scope)
+// ---------------------------------------------------------------------------
+template <typename LT, bool FAST>
+__global__ __launch_bounds__(256) void k_bin_atomic(const SegDesc seg, const LT *__restrict__ lut,
+                                                    int pid_off, unsigned L,
+                                                    const unsigned char *__restrict__ g_tab,
+                                                    ToaParams tp, uint32_t *__restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    load_toa_tables(smem, g_tab, tp);
+    __syncthreads();
+    const long long n = seg.n;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long tail = 0;
+    if ((((uintptr_t)seg.pid | (uintptr_t)seg.toa) & 15u) == 0) {
+        const long long n4 = n >> 2;
+        for (long long i = i0; i < n4; i += stride) {
+            const v4i p = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(seg.pid) + i);
+            const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(seg.toa) + i);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = event_key<LT, FAST>(p[q], t[q], lut, pid_off, L, smem, tp);
+                if (k >= 0) atomicAdd(hist + k, 1u);
+            }
+        }
+        tail = n4 << 2;
+    }
+    for (long long i = tail + i0; i < n; i += stride) {
+        const int k = event_key<LT, FAST>(seg.pid[i], seg.toa[i], lut, pid_off, L, smem, tp);
+        if (k >= 0) atomicAdd(hist + k, 1u);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// PARTITION strategy, pass A: chunk-major tile partition
+//   One launch covers up to kMaxSegs staged segments (ev44 messages); global
+//   chunk c maps to the segment with segs[s].chunk0 <= c < segs[s+1].chunk0.
+//   The valid events of chunk c are written tile-sorted to payload[c*CH ...]
+//   as u16 offsets inside their tile, with per-tile run starts
+//   starts[c*(NT+1) + t].  The next chunk's events are prefetched into
+//   registers while the current chunk runs its LDS phases.
+// ---------------------------------------------------------------------------
+struct ChunkRegs {
+    int p[kPartEventsPerThread];
+    int t[kPartEventsPerThread];
+};
+
+__device__ __forceinline__ void load_chunk(const SegDesc *s_seg, int n_segs, long long c,
+                                           int pid_off, ChunkRegs &r) {
+    int s = 0;
+    while (s + 1 < n_segs && s_seg[s + 1].chunk0 <= c) ++s;
+    const SegDesc sd = s_seg[s];
+    const long long base = (c - sd.chunk0) * kChunk;
+    const bool vec = (((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kPartEventsPerThread / 4; ++j) {
+        const long long e0 = base + ((long long)j * kPartThreads + tid) * 4;
+        if (vec && e0 + 3 < sd.n) {
+            const v4i p = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.pid + e0));
+            const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.toa + e0));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                r.p[j * 4 + q] = p[q];
+                r.t[j * 4 + q] = t[q];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool ok = e0 + q < sd.n;
+                r.p[j * 4 + q] = ok ? sd.pid[e0 + q] : pid_off - 1;  // outside the LUT: dropped
+                r.t[j * 4 + q] = ok ? sd.toa[e0 + q] : 0;
+            }
+        }
+    }
+}
+
+template <int TILE_BITS, typename LT, bool FAST, bool PEEL>
+__global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_partition(
+    const SegDesc *__restrict__ segs, int n_segs, long long c_begin, long long n_chunks,
+    const LT *__restrict__ lut, int pid_off, unsigned L, const unsigned char *__restrict__ g_tab,
+    ToaParams tp, int n_tiles, uint16_t *__restrict__ payload, uint32_t *__restrict__ starts,
+    uint32_t *__restrict__ part) {
+    constexpr int EPT = kPartEventsPerThread;
+    constexpr int CH = kChunk;
+    constexpr int TPT = kMaxTiles / kPartThreads;  // tiles per thread in the scan
+    constexpr uint32_t MASK = (1u << TILE_BITS) - 1u;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // LDS carve: staging | counts | totals | scan | segments | TOA tables
+    uint16_t *s_stg = reinterpret_cast<uint16_t *>(smem);
+    uint32_t *s_cnt = reinterpret_cast<uint32_t *>(smem + CH * 2);
+    uint32_t *s_tot = s_cnt + align4(n_tiles + 1);
+    uint32_t *s_w = s_tot + align4(n_tiles);
+    SegDesc *s_seg = reinterpret_cast<SegDesc *>(s_w + 32);
+    unsigned char *s_tab = reinterpret_cast<unsigned char *>(s_seg + kMaxSegs);
+    load_toa_tables(s_tab, g_tab, tp);
+    for (int i = threadIdx.x; i < n_segs; i += blockDim.x) s_seg[i] = segs[i];
+    for (int i = threadIdx.x; i <= n_tiles; i += blockDim.x) s_cnt[i] = 0;
+    for (int i = threadIdx.x; i < n_tiles; i += blockDim.x) s_tot[i] = 0;
+    __syncthreads();
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    ChunkRegs nxt;
+    if (c_begin + blockIdx.x < n_chunks)
+        load_chunk(s_seg, n_segs, c_begin + blockIdx.x, pid_off, nxt);
+    for (long long c = c_begin + blockIdx.x; c < n_chunks; c += gridDim.x) {
+        const ChunkRegs cur = nxt;
+        if (c + gridDim.x < n_chunks) load_chunk(s_seg, n_segs, c + gridDim.x, pid_off, nxt);
+        int key[EPT];
+        uint32_t rank[EPT];
+        if (tp.pad == 0) {
+#pragma unroll
+            for (int e = 0; e < EPT; ++e)
+                key[e] = event_key<LT, FAST>(cur.p[e], cur.t[e], lut, pid_off, L, s_tab, tp);
+        } else {  // LDE_ABLATE diagnostics: timing only, results are wrong by design
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) {
+                const unsigned p = (unsigned)cur.p[e] - (unsigned)pid_off;
+                const int base = (tp.pad & 1) ? (int)((p & 16383u) * (unsigned)tp.T)
+                                              : (p < L ? lut_base(lut, p, tp.T) : -1);
+                const int b = (tp.pad & 2) ? (int)((unsigned)cur.t[e] & 63u) : toa_bin<FAST>(cur.t[e], s_tab, tp);
+                key[e] = (p >= L || base < 0 || b < 0) ? -1 : base + b;
+            }
+        }
+        // ---- rank inside tile: LDS returning atomics; with PEEL the most
+        // common tile of the wave (sampled lane) is ranked with one atomic
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+            const int tile = key[e] >= 0 ? (key[e] >> TILE_BITS) : -1;
+            rank[e] = 0;
+            if (tp.pad & 4) {
+                rank[e] = (uint32_t)(e * 64 + lane) & 255u;
+            } else if (PEEL) {
+                const int lead = __builtin_amdgcn_readlane(tile, (e * 5) & 63);
+                const unsigned long long m = __ballot(tile == lead);
+                if (lead >= 0) {
+                    const int first = __builtin_ctzll(m);
+                    uint32_t base = 0;
+                    if (lane == first) base = atomicAdd(&s_cnt[lead], (uint32_t)__popcll(m));
+                    base = __builtin_amdgcn_readlane(base, first);
+                    if (tile == lead) rank[e] = base + lanes_below(m);
+                }
+                if (tile >= 0 && tile != lead) rank[e] = atomicAdd(&s_cnt[tile], 1u);
+            } else {
+                if (tile >= 0) rank[e] = atomicAdd(&s_cnt[tile], 1u);
+            }
+        }
+        __syncthreads();
+        // ---- exclusive scan of the tile counts
+        uint32_t loc[TPT];
+        uint32_t sum = 0;
+        const int t0 = tid * TPT;
+#pragma unroll
+        for (int q = 0; q < TPT; ++q) {
+            const int t = t0 + q;
+            loc[q] = t < n_tiles ? s_cnt[t] : 0u;
+            sum += loc[q];
+        }
+        uint32_t total;
+        uint32_t run = block_exclusive_scan(sum, s_w, &total);
+        uint32_t *g_starts = starts + c * (long long)(n_tiles + 1);
+#pragma unroll
+        for (int q = 0; q < TPT; ++q) {
+            const int t = t0 + q;
+            if (t < n_tiles) {
+                s_cnt[t] = run;  // becomes the run start
+                g_starts[t] = run;
+                s_tot[t] += loc[q];
+            }
+            run += loc[q];
+        }
+        if (tid == 0) g_starts[n_tiles] = total;
+        __syncthreads();
+        // ---- scatter into LDS staging (tile-sorted)
+        if (!(tp.pad & 8)) {
+#pragma unroll
+            for (int e = 0; e < EPT; ++e)
+                if (key[e] >= 0) s_stg[s_cnt[key[e] >> TILE_BITS] + rank[e]] = (uint16_t)(key[e] & MASK);
+        } else {
+            int acc = 0;
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) acc += key[e];
+            if (acc == 0x7fffffff) s_stg[tid] = 1;
+        }
+        __syncthreads();
+        // ---- coalesced write-out of the valid prefix (16 B per lane)
+        uint16_t *g_out = payload + c * (long long)CH;
+        if (!(tp.pad & 8))
+            for (int i = tid * 8; i < (int)total; i += kPartThreads * 8)
+                *reinterpret_cast<uint4 *>(g_out + i) = *reinterpret_cast<const uint4 *>(s_stg + i);
+        for (int i = tid; i <= n_tiles; i += blockDim.x) s_cnt[i] = 0;
+        __syncthreads();
+    }
+    // per-block tile totals (row blockIdx.x is owned by this block; accumulates
+    // across the launches of one accumulate, which run in stream order)
+    uint32_t *g_part = part + (long long)blockIdx.x * n_tiles;
+    for (int t = threadIdx.x; t < n_tiles; t += blockDim.x) g_part[t] += s_tot[t];
+}
+
+// ---------------------------------------------------------------------------
+// PARTITION strategy, plan: per-tile totals -> balanced work items
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_tile_totals(const uint32_t *__restrict__ part,
+                                                     int part_rows, int n_tiles,
+                                                     uint32_t *__restrict__ totals) {
+    __shared__ uint32_t s_r[4];
+    const int t = blockIdx.x;
+    uint32_t v = 0;
+    for (int r = threadIdx.x; r < part_rows; r += blockDim.x) v += part[(long long)r * n_tiles + t];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    if ((threadIdx.x & 63) == 0) s_r[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) totals[t] = s_r[0] + s_r[1] + s_r[2] + s_r[3];
+}
+
+__global__ __launch_bounds__(1024) void k_plan(const uint32_t *__restrict__ totals, int n_tiles,
+                                               long long n_chunks, uint32_t item_events,
+                                               uint32_t *__restrict__ tile_items,
+                                               uint2 *__restrict__ items,
+                                               uint32_t *__restrict__ item_count,
+                                               uint32_t max_items) {
+    __shared__ uint32_t s_w[32];
+    constexpr int TPT = kMaxTiles / 1024;
+    const int tid = threadIdx.x;
+    uint32_t ni[TPT];
+    uint32_t lane_mode[TPT];
+    uint32_t sum = 0;
+    const int t0 = tid * TPT;
+#pragma unroll
+    for (int q = 0; q < TPT; ++q) {
+        const int t = t0 + q;
+        const uint32_t tot = t < n_tiles ? totals[t] : 0u;
+        ni[q] = tot == 0 ? 0u : (tot + item_events - 1) / item_events;
+        // short average runs per chunk: one lane per chunk in pass B
+        lane_mode[q] = (long long)tot < (long long)kLaneModeRun * n_chunks ? 0x80000000u : 0u;
+        sum += ni[q];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(sum, s_w, &total);
+#pragma unroll
+    for (int q = 0; q < TPT; ++q) {
+        const int t = t0 + q;
+        if (t < n_tiles) {
+            tile_items[t] = ni[q];
+            for (uint32_t j = 0; j < ni[q] && run + j < max_items; ++j)
+                items[run + j] = make_uint2((uint32_t)t, j | lane_mode[q]);
+        }
+        run += ni[q];
+    }
+    if (tid == 0) *item_count = total < max_items ? total : max_items;
+}
+
+// ---------------------------------------------------------------------------
+// PARTITION strategy, pass B: LDS sub-histogram per work item
+//   item = (tile t, slice j of n_t of the chunk range).  Tiles whose runs are
+//   short on average (cold tiles) walk chunks one LANE per chunk so a wave
+//   covers 64 chunks per step; hot tiles walk one WAVE per chunk run with
+//   16-byte loads (8 events per lane).
+// ---------------------------------------------------------------------------
+template <int TILE_BITS>
+__global__ __launch_bounds__(kTileThreads) void k_tile_accumulate(
+    const uint16_t *__restrict__ payload, const uint32_t *__restrict__ starts, int n_tiles,
+    long long n_chunks, const uint2 *__restrict__ items, const uint32_t *__restrict__ item_count,
+    const uint32_t *__restrict__ tile_items, uint32_t *__restrict__ hist, long long n_bins) {
+    constexpr int TB = 1 << TILE_BITS;
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[TB];
+    if (blockIdx.x >= *item_count) return;
+    const uint2 it = items[blockIdx.x];
+    const int t = (int)it.x;
+    const bool lane_mode = (it.y & 0x80000000u) != 0;
+    const long long j = it.y & 0x7fffffffu;
+    const long long nt = tile_items[t];
+    const long long c0 = j * n_chunks / nt;
+    const long long c1 = (j + 1) * n_chunks / nt;
+    for (int i = threadIdx.x * 4; i < TB; i += kTileThreads * 4)
+        *reinterpret_cast<uint4 *>(s_tile + i) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int NW = kTileThreads / 64;
+    const long long stride = (long long)(n_tiles + 1);
+    if (lane_mode) {
+        // one lane per chunk run; each lane reads its run with aligned 16-byte
+        // loads (8 entries), masking entries outside [s, e)
+        long long g = c0 + (long long)wid * 64;
+        uint32_t ns = 0, ne = 0;
+        if (g + lane < c1) {
+            ns = starts[(g + lane) * stride + t];
+            ne = starts[(g + lane) * stride + t + 1];
+        }
+        for (; g < c1; g += (long long)NW * 64) {
+            const long long c = g + lane;
+            const uint32_t s = ns, e = ne;
+            const long long gn = g + (long long)NW * 64;  // prefetch the next group's run bounds
+            ns = ne = 0;
+            if (gn + lane < c1) {
+                ns = starts[(gn + lane) * stride + t];
+                ne = starts[(gn + lane) * stride + t + 1];
+            }
+            const uint16_t *p = payload + c * kChunk;
+            for (uint32_t i = s & ~7u;; i += 16u) {
+                if (!__any(i < e)) break;
+                uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+                if (i < e) v0 = *reinterpret_cast<const uint4 *>(p + i);
+                if (i + 8u < e) v1 = *reinterpret_cast<const uint4 *>(p + i + 8u);
+                const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const uint32_t k = i + (uint32_t)q;
+                    if (k >= s && k < e) atomicAdd(&s_tile[(w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu], 1u);
+                }
+            }
+        }
+    } else {
+        for (long long c = c0 + wid; c < c1; c += NW) {
+            const uint32_t s = starts[c * stride + t];
+            const uint32_t e = starts[c * stride + t + 1];
+            const uint16_t *p = payload + c * kChunk;
+            const uint32_t a0 = (s + 7u) & ~7u;  // 16-byte aligned body [a0, a1)
+            const uint32_t a1 = e & ~7u;
+            if (a0 >= a1) {
+                for (uint32_t i = s + lane; i < e; i += 64) atomicAdd(&s_tile[p[i]], 1u);
+                continue;
+            }
+            if (s + lane < a0) atomicAdd(&s_tile[p[s + lane]], 1u);
+            if (a1 + lane < e) atomicAdd(&s_tile[p[a1 + lane]], 1u);
+            for (uint32_t i = a0 + lane * 8u; i < a1; i += 512u) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(p + i);
+                atomicAdd(&s_tile[v.x & 0xFFFFu], 1u);
+                atomicAdd(&s_tile[v.x >> 16], 1u);
+                atomicAdd(&s_tile[v.y & 0xFFFFu], 1u);
+                atomicAdd(&s_tile[v.y >> 16], 1u);
+                atomicAdd(&s_tile[v.z & 0xFFFFu], 1u);
+                atomicAdd(&s_tile[v.z >> 16], 1u);
+                atomicAdd(&s_tile[v.w & 0xFFFFu], 1u);
+                atomicAdd(&s_tile[v.w >> 16], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    const long long base = (long long)t << TILE_BITS;
+    for (int i = threadIdx.x; i < TB; i += kTileThreads) {
+        const uint32_t v = s_tile[i];
+        if (v != 0u && base + i < n_bins) atomicAdd(hist + base + i, v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Monitor: 1-D TOA histogram, LDS layout [bin][32 columns] so the 32 lanes of
+// each half-wave always hit 32 distinct banks (conflict-free for any skew).
+// ---------------------------------------------------------------------------
+template <bool FAST, bool COLUMNS>
+__global__ __launch_bounds__(256) void k_monitor(const SegDesc seg,
+                                                 const unsigned char *__restrict__ g_tab,
+                                                 ToaParams tp, uint32_t *__restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *s_h = reinterpret_cast<uint32_t *>(smem);
+    const int HB = COLUMNS ? tp.T * 32 : tp.T;
+    unsigned char *s_tab = smem + align16((size_t)HB * 4);
+    load_toa_tables(s_tab, g_tab, tp);
+    for (int i = threadIdx.x; i < HB; i += blockDim.x) s_h[i] = 0;
+    __syncthreads();
+    const int col = threadIdx.x & 31;
+    const long long n = seg.n;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    auto add = [&](int t) {
+        const int b = toa_bin<FAST>(t, s_tab, tp);
+        if (b >= 0) atomicAdd(&s_h[COLUMNS ? b * 32 + col : b], 1u);
+    };
+    long long tail = 0;
+    if (((uintptr_t)seg.toa & 15u) == 0) {
+        const long long n4 = n >> 2;
+        for (long long i = i0; i < n4; i += stride) {
+            const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(seg.toa) + i);
+            add(t[0]);
+            add(t[1]);
+            add(t[2]);
+            add(t[3]);
+        }
+        tail = n4 << 2;
+    }
+    for (long long i = tail + i0; i < n; i += stride) add(seg.toa[i]);
+    __syncthreads();
+    for (int b = threadIdx.x; b < tp.T; b += blockDim.x) {
+        uint32_t v = 0;
+        if (COLUMNS) {
+            for (int c = 0; c < 32; ++c) v += s_h[b * 32 + ((c + b) & 31)];
+        } else {
+            v = s_h[b];
+        }
+        if (v) atomicAdd(hist + b, v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launch wrappers
+// ---------------------------------------------------------------------------
+size_t partition_smem(int n_tiles, const ToaParams &tp) {
+    return (size_t)kChunk * 2 + 4 * ((size_t)align4(n_tiles + 1) + align4(n_tiles) + 32) +
+           sizeof(SegDesc) * kMaxSegs + toa_lds_bytes(tp);
+}
+
+template <typename LT>
+static hipError_t launch_bin_atomic_t(const SegDesc &seg, const LT *lut, int pid_off, unsigned L,
+                                      const unsigned char *tab, const ToaParams &tp,
+                                      uint32_t *hist, int grid, hipStream_t st) {
+    const size_t sm = toa_lds_bytes(tp);
+    if (tp.fast) {
+        (void)hipFuncSetAttribute((const void *)k_bin_atomic<LT, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL((k_bin_atomic<LT, true>), dim3(grid), dim3(256), sm, st, seg, lut,
+                           pid_off, L, tab, tp, hist);
+    } else {
+        (void)hipFuncSetAttribute((const void *)k_bin_atomic<LT, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL((k_bin_atomic<LT, false>), dim3(grid), dim3(256), sm, st, seg, lut,
+                           pid_off, L, tab, tp, hist);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_atomic(const SegDesc &seg, const void *lut, bool lut16, int pid_off,
+                             unsigned L, const unsigned char *tab, const ToaParams &tp,
+                             uint32_t *hist, int grid, hipStream_t st) {
+    return lut16 ? launch_bin_atomic_t(seg, (const uint16_t *)lut, pid_off, L, tab, tp, hist, grid, st)
+                 : launch_bin_atomic_t(seg, (const int *)lut, pid_off, L, tab, tp, hist, grid, st);
+}
+
+template <int TB, typename LT, bool FAST, bool PEEL>
+static hipError_t launch_partition_t(const PartitionArgs &a, const LT *lut, hipStream_t st) {
+    const size_t sm = partition_smem(a.n_tiles, a.tp);
+    (void)hipFuncSetAttribute((const void *)k_partition<TB, LT, FAST, PEEL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    hipLaunchKernelGGL((k_partition<TB, LT, FAST, PEEL>), dim3(a.grid), dim3(kPartThreads), sm,
+                       st, a.segs, a.n_segs, a.c_begin, a.n_chunks, lut, a.pid_off, a.L, a.tab,
+                       a.tp, a.n_tiles, a.payload, a.starts, a.part);
+    return hipGetLastError();
+}
+
+template <int TB, typename LT>
+static hipError_t launch_partition_tl(const PartitionArgs &a, const LT *lut, hipStream_t st) {
+    if (a.tp.fast)
+        return a.peel ? launch_partition_t<TB, LT, true, true>(a, lut, st)
+                      : launch_partition_t<TB, LT, true, false>(a, lut, st);
+    return a.peel ? launch_partition_t<TB, LT, false, true>(a, lut, st)
+                  : launch_partition_t<TB, LT, false, false>(a, lut, st);
+}
+
+template <int TB>
+static hipError_t launch_partition_tb(const PartitionArgs &a, hipStream_t st) {
+    return a.lut16 ? launch_partition_tl<TB>(a, (const uint16_t *)a.lut, st)
+                   : launch_partition_tl<TB>(a, (const int *)a.lut, st);
+}
+
+hipError_t launch_partition(const PartitionArgs &a, hipStream_t st) {
+    switch (a.tile_bits) {
+    case 13: return launch_partition_tb<13>(a, st);
+    case 14: return launch_partition_tb<14>(a, st);
+    case 15: return launch_partition_tb<15>(a, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_plan(const uint32_t *part, int part_rows, int n_tiles, long long n_chunks,
+                       uint32_t item_events, uint32_t *totals, uint32_t *tile_items, uint2 *items,
+                       uint32_t *item_count, uint32_t max_items, hipStream_t st) {
+    hipLaunchKernelGGL(k_tile_totals, dim3(n_tiles), dim3(256), 0, st, part, part_rows, n_tiles,
+                       totals);
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, totals, n_tiles, n_chunks, item_events,
+                       tile_items, items, item_count, max_items);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const uint32_t *starts,
+                                  int n_tiles, long long n_chunks, const uint2 *items,
+                                  const uint32_t *item_count, const uint32_t *tile_items,
+                                  uint32_t *hist, long long n_bins, int grid, hipStream_t st) {
+    switch (tile_bits) {
+    case 13:
+        hipLaunchKernelGGL(k_tile_accumulate<13>, dim3(grid), dim3(kTileThreads), 0, st, payload,
+                           starts, n_tiles, n_chunks, items, item_count, tile_items, hist, n_bins);
+        break;
+    case 14:
+        hipLaunchKernelGGL(k_tile_accumulate<14>, dim3(grid), dim3(kTileThreads), 0, st, payload,
+                           starts, n_tiles, n_chunks, items, item_count, tile_items, hist, n_bins);
+        break;
+    case 15:
+        hipLaunchKernelGGL(k_tile_accumulate<15>, dim3(grid), dim3(kTileThreads), 0, st, payload,
+                           starts, n_tiles, n_chunks, items, item_count, tile_items, hist, n_bins);
+        break;
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_monitor(const SegDesc &seg, const unsigned char *tab, const ToaParams &tp,
+                          uint32_t *hist, int grid, hipStream_t st) {
+    const bool columns = tp.T <= kMonitorColumnsMaxT;
+    const size_t hb = align16((size_t)(columns ? tp.T * 32 : tp.T) * 4);
+    const size_t sm = hb + toa_lds_bytes(tp);
+#define LDE_MON(F, C)                                                                          \
+    do {                                                                                       \
+        (void)hipFuncSetAttribute((const void *)k_monitor<F, C>,                               \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);        \
+        hipLaunchKernelGGL((k_monitor<F, C>), dim3(grid), dim3(256), sm, st, seg, tab, tp, hist); \
+    } while (0)
+    if (tp.fast && columns) LDE_MON(true, true);
+    else if (tp.fast) LDE_MON(true, false);
+    else if (columns) LDE_MON(false, true);
+    else LDE_MON(false, false);
+#undef LDE_MON
+    return hipGetLastError();
+}
+
+}  // namespace lde

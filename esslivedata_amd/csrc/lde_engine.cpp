@@ -59,9 +59,10 @@ struct lde_handle {
     int range_lo = 0, range_hi = 1;
     lde::ToaParams tp{};
 
-    int *d_lut = nullptr;
-    long long *d_thr = nullptr;
-    uint32_t *d_bp = nullptr;
+    void *d_lut = nullptr;
+    bool lut16 = false;
+    unsigned char *d_tab = nullptr;
+    bool peel = true;
 
     uint32_t *d_win32 = nullptr;
     unsigned long long *d_win64 = nullptr;
@@ -85,9 +86,14 @@ struct lde_handle {
     long long chunk_cap = 0;
     uint32_t *d_part = nullptr;
     int part_rows = 0;
+    int part_grid = 0;
     uint32_t *d_ttot = nullptr, *d_tile_items = nullptr, *d_item_count = nullptr;
     uint2 *d_items = nullptr;
     long long items_cap = 0;
+    lde::SegDesc *d_segs = nullptr, *h_segs = nullptr;
+    long long segs_cap = 0;
+    hipEvent_t segs_done = nullptr;
+    bool segs_pending = false;
     long long item_events_override = 0;
     long long atomic_threshold = -1;
 
@@ -180,8 +186,15 @@ long long ceil_clamped(double e) {
     return (long long)std::ceil(e);
 }
 
-int build_toa_tables(lde_handle *h, const double *edges, int T, std::vector<long long> &thr,
-                     std::vector<uint32_t> &bp, lde::ToaParams &tp) {
+// bin(x) = largest b in [0, T-1] with thr[b] <= x (x in [lo, hi))
+static int bin_of(const std::vector<long long> &thr, int T, long long x) {
+    int b = (int)(std::upper_bound(thr.begin(), thr.begin() + T, x) - thr.begin()) - 1;
+    return std::max(0, std::min(b, T - 1));
+}
+
+// Builds the LDS image of the TOA lookup (layouts documented in lde_binning.hip).
+int build_toa_tables(lde_handle *h, const double *edges, int T, std::vector<unsigned char> &img,
+                     lde::ToaParams &tp) {
     if (!edges) return fail(h, LDE_EINVAL, "toa_edges is NULL");
     if (T < 1 || T > 65535) return fail(h, LDE_EINVAL, "n_toa_bins=%d out of range [1, 65535]", T);
     for (int i = 0; i <= T; ++i) {
@@ -190,28 +203,59 @@ int build_toa_tables(lde_handle *h, const double *edges, int T, std::vector<long
         if (i > 0 && edges[i] < edges[i - 1])
             return fail(h, LDE_EINVAL, "toa edges must be sorted (edge %d < edge %d)", i, i - 1);
     }
-    thr.resize(T + 1);
+    std::vector<long long> thr(T + 1);
     for (int i = 0; i <= T; ++i) thr[i] = ceil_clamped(edges[i]);
+    std::memset(&tp, 0, sizeof tp);
     tp.T = T;
     tp.lo = thr[0];
     tp.hi = thr[T];
     const long long span = tp.hi - tp.lo;  // 0 .. 2^32
+    // fast layout: u32 relative thresholds, buckets narrower than every bin
+    if (span >= 1 && span <= 0xffffffffLL && tp.lo <= 0x7fffffffLL &&
+        std::getenv("LDE_TOA_GENERAL") == nullptr) {
+        long long min_width = span;
+        for (int i = 0; i < T; ++i)
+            if (thr[i + 1] > thr[i]) min_width = std::min(min_width, thr[i + 1] - thr[i]);
+        int shift = 0;
+        while ((2LL << shift) <= min_width) ++shift;  // 2^shift <= min non-empty bin width
+        while (((span - 1) >> shift) >= lde::kMaxFastBuckets) ++shift;
+        const int G = (int)(((span - 1) >> shift) + 1);
+        std::vector<uint16_t> bst(G);
+        bool one_step = true;
+        for (int g = 0; g < G && one_step; ++g) {
+            const long long x0 = tp.lo + ((long long)g << shift);
+            long long x1 = std::min(tp.lo + (((long long)g + 1) << shift) - 1, tp.hi - 1);
+            const int b0 = bin_of(thr, T, x0), b1 = bin_of(thr, T, x1);
+            if (b1 - b0 > 1) one_step = false;
+            bst[g] = (uint16_t)b0;
+        }
+        if (one_step) {
+            tp.fast = 1;
+            tp.span = (unsigned)span;
+            tp.shift = shift;
+            tp.G = G;
+            img.assign(lde::toa_lds_bytes(tp), 0);
+            uint32_t *rthr = reinterpret_cast<uint32_t *>(img.data());
+            for (int i = 0; i <= T; ++i) rthr[i] = (uint32_t)(thr[i] - tp.lo);
+            std::memcpy(img.data() + lde::align16((size_t)(T + 1) * 4), bst.data(), (size_t)G * 2);
+            return LDE_OK;
+        }
+    }
+    // general layout: int64 thresholds + (first, last) candidate bins per bucket
     int shift = 0;
     while (span > 0 && ((span - 1) >> shift) >= lde::kMaxBuckets) ++shift;
+    tp.fast = 0;
     tp.shift = shift;
     tp.G = span > 0 ? (int)(((span - 1) >> shift) + 1) : 1;
-    bp.assign(tp.G, 0u);
-    // bin(x) = largest b in [0, T-1] with thr[b] <= x, for x in [lo, hi)
-    auto bin_of = [&](long long x) {
-        int b = (int)(std::upper_bound(thr.begin(), thr.begin() + T, x) - thr.begin()) - 1;
-        return std::max(0, std::min(b, T - 1));
-    };
+    img.assign(lde::toa_lds_bytes(tp), 0);
+    std::memcpy(img.data(), thr.data(), (size_t)(T + 1) * 8);
+    uint32_t *bp = reinterpret_cast<uint32_t *>(img.data() + lde::align16((size_t)(T + 1) * 8));
     for (int g = 0; g < tp.G; ++g) {
         const long long x0 = tp.lo + ((long long)g << shift);
         long long x1 = tp.lo + (((long long)g + 1) << shift) - 1;
         if (x1 > tp.hi - 1) x1 = tp.hi - 1;
-        const int b0 = span > 0 ? bin_of(x0) : 0;
-        const int b1 = span > 0 ? bin_of(std::max(x0, x1)) : 0;
+        const int b0 = span > 0 ? bin_of(thr, T, x0) : 0;
+        const int b1 = span > 0 ? bin_of(thr, T, std::max(x0, x1)) : 0;
         bp[g] = (uint32_t)b0 | ((uint32_t)b1 << 16);
     }
     return LDE_OK;
@@ -324,16 +368,18 @@ bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
 // ---- binning ---------------------------------------------------------------
 int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long total, int replica) {
-    const int *lut = h->monitor ? nullptr : h->d_lut + (long long)replica * h->L;
+    const size_t lut_es = h->lut16 ? 2 : 4;
+    const void *lut = h->monitor ? nullptr
+                                 : (const void *)((const unsigned char *)h->d_lut +
+                                                  (size_t)replica * h->L * lut_es);
     if (h->monitor) {
         h->last_strategy = LDE_STRATEGY_AUTO;
         for (const Segment &s : segs) {
             if (s.n == 0) continue;
-            const bool vec = aligned16(s.toa);
             long long g = (s.n / 4 + 255) / 256;
             g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 4));
             Timed tm(h, LDE_K_MONITOR);
-            HIPCALL(h, lde::launch_monitor(s.toa, s.n, h->d_thr, h->d_bp, h->tp, h->d_win32, vec,
+            HIPCALL(h, lde::launch_monitor({nullptr, s.toa, s.n, 0}, h->d_tab, h->tp, h->d_win32,
                                            (int)g, h->stream));
         }
         return LDE_OK;
@@ -350,19 +396,23 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
     if (strat == LDE_STRATEGY_ATOMIC) {
         for (const Segment &s : segs) {
             if (s.n == 0) continue;
-            const bool vec = aligned16(s.pid) && aligned16(s.toa);
             long long g = (s.n / 4 + 255) / 256;
             g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 8));
             Timed tm(h, LDE_K_ATOMIC);
-            HIPCALL(h, lde::launch_bin_atomic(s.pid, s.toa, s.n, lut, h->pid_off, (unsigned)h->L,
-                                              h->d_thr, h->d_bp, h->tp, h->d_win32, vec, (int)g,
+            HIPCALL(h, lde::launch_bin_atomic({s.pid, s.toa, s.n, 0}, lut, h->lut16, h->pid_off,
+                                              (unsigned)h->L, h->d_tab, h->tp, h->d_win32, (int)g,
                                               h->stream));
         }
         return LDE_OK;
     }
     // PARTITION
     long long chunks = 0;
-    for (const Segment &s : segs) chunks += (s.n + lde::kChunk - 1) / lde::kChunk;
+    std::vector<lde::SegDesc> sd;
+    for (const Segment &s : segs) {
+        if (s.n == 0) continue;
+        sd.push_back({s.pid, s.toa, s.n, chunks});
+        chunks += (s.n + lde::kChunk - 1) / lde::kChunk;
+    }
     if (chunks == 0) return LDE_OK;
     long long item_events = h->item_events_override > 0
                                 ? h->item_events_override
@@ -370,23 +420,60 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
     if (item_events > 0x7fffffffLL) item_events = 0x7fffffffLL;
     const long long max_items = (total + item_events - 1) / item_events + h->n_tiles;
     if (int rc = ensure_partition_capacity(h, chunks, max_items)) return rc;
-    const int grid_a = (int)std::min<long long>(chunks, (long long)h->part_rows);
+    // segment table -> device (pinned staging, reused once the previous copy landed)
+    if (h->segs_pending) {
+        HIPCALL(h, hipEventSynchronize(h->segs_done));
+        h->segs_pending = false;
+    }
+    if ((long long)sd.size() > h->segs_cap) {
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        dev_free(h->d_segs);
+        if (h->h_segs) (void)hipHostFree(h->h_segs);
+        h->h_segs = nullptr;
+        h->segs_cap = 0;
+        const long long cap = std::max<long long>((long long)sd.size(), 256);
+        if (int rc = dev_alloc(h, &h->d_segs, (size_t)cap)) return rc;
+        HIPCALL(h, hipHostMalloc((void **)&h->h_segs, cap * sizeof(lde::SegDesc), hipHostMallocDefault));
+        h->segs_cap = cap;
+    }
+    std::memcpy(h->h_segs, sd.data(), sd.size() * sizeof(lde::SegDesc));
+    HIPCALL(h, hipMemcpyAsync(h->d_segs, h->h_segs, sd.size() * sizeof(lde::SegDesc),
+                              hipMemcpyHostToDevice, h->stream));
+    HIPCALL(h, hipEventRecord(h->segs_done, h->stream));
+    h->segs_pending = true;
+    const int grid_a = (int)std::min<long long>(chunks, (long long)h->part_grid);
     HIPCALL(h, hipMemsetAsync(h->d_part, 0, (size_t)grid_a * h->n_tiles * 4, h->stream));
-    long long chunk0 = 0;
-    for (const Segment &s : segs) {
-        if (s.n == 0) continue;
-        const long long nc = (s.n + lde::kChunk - 1) / lde::kChunk;
-        const bool vec = aligned16(s.pid) && aligned16(s.toa);
+    for (size_t s0 = 0; s0 < sd.size(); s0 += lde::kMaxSegs) {
+        const int ns = (int)std::min<size_t>(lde::kMaxSegs, sd.size() - s0);
+        // chunk ids are global: launch the whole range, segments outside this
+        // group are skipped by clamping the chunk window
+        const long long c_lo = sd[s0].chunk0;
+        const long long c_hi = (s0 + ns < sd.size()) ? sd[s0 + ns].chunk0 : chunks;
+        lde::PartitionArgs pa;
+        pa.tile_bits = h->tile_bits;
+        pa.lut16 = h->lut16;
+        pa.peel = h->peel;
+        pa.segs = h->d_segs + s0;
+        pa.n_segs = ns;
+        pa.c_begin = c_lo;
+        pa.n_chunks = c_hi;
+        pa.lut = lut;
+        pa.pid_off = h->pid_off;
+        pa.L = (unsigned)h->L;
+        pa.tab = h->d_tab;
+        pa.tp = h->tp;
+        pa.tp.pad = (int)env_ll("LDE_ABLATE", 0);
+        pa.n_tiles = h->n_tiles;
+        pa.payload = h->d_payload;
+        pa.starts = h->d_starts;
+        pa.part = h->d_part;
+        pa.grid = (int)std::min<long long>(grid_a, c_hi - c_lo);
         Timed tm(h, LDE_K_PARTITION);
-        HIPCALL(h, lde::launch_partition(h->tile_bits, s.pid, s.toa, s.n, lut, h->pid_off,
-                                         (unsigned)h->L, h->d_thr, h->d_bp, h->tp, h->n_tiles,
-                                         chunk0, nc, h->d_payload, h->d_starts, h->d_part, vec,
-                                         grid_a, h->stream));
-        chunk0 += nc;
+        HIPCALL(h, lde::launch_partition(pa, h->stream));
     }
     {
         Timed tm(h, LDE_K_PLAN);
-        HIPCALL(h, lde::launch_plan(h->d_part, grid_a, h->n_tiles, (uint32_t)item_events,
+        HIPCALL(h, lde::launch_plan(h->d_part, grid_a, h->n_tiles, chunks, (uint32_t)item_events,
                                     h->d_ttot, h->d_tile_items, h->d_items, h->d_item_count,
                                     (uint32_t)max_items, h->stream));
     }
@@ -440,8 +527,7 @@ void release(lde_handle *h) {
     }
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
     dev_free(h->d_lut);
-    dev_free(h->d_thr);
-    dev_free(h->d_bp);
+    dev_free(h->d_tab);
     dev_free(h->d_win32);
     dev_free(h->d_win64);
     dev_free(h->d_cum);
@@ -459,6 +545,9 @@ void release(lde_handle *h) {
     dev_free(h->d_tile_items);
     dev_free(h->d_item_count);
     dev_free(h->d_items);
+    dev_free(h->d_segs);
+    if (h->h_segs) (void)hipHostFree(h->h_segs);
+    if (h->segs_done) (void)hipEventDestroy(h->segs_done);
     dev_free(h->d_tot4);
     dev_free(h->d_img_cur);
     dev_free(h->d_img_cum);
@@ -508,9 +597,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     if (!h) return fail(nullptr, LDE_ENOMEM, "out of host memory");
     h->device = cfg->device_id;
     DeviceGuard guard(h->device);
-    std::vector<long long> thr;
-    std::vector<uint32_t> bp;
-    int rc = build_toa_tables(h, cfg->toa_edges, cfg->n_toa_bins, thr, bp, h->tp);
+    std::vector<unsigned char> tab;
+    int rc = build_toa_tables(h, cfg->toa_edges, cfg->n_toa_bins, tab, h->tp);
     if (rc) {
         g_create_error = h->err;
         release(h);
@@ -560,10 +648,14 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->range_hi = cfg->range_hi;
     }
 
-    // LUT: screen index -> screen*T (premultiplied), validated
+    // LUT: u16 screen index (0xFFFF = dropped) when S < 65535, else int32
+    // screen*T premultiplied (-1 = dropped); validated here
     if (!monitor) {
         const long long n = (long long)h->R * h->L;
-        std::vector<int> lut((size_t)n);
+        h->lut16 = h->S < 0xFFFF && env_ll("LDE_LUT32", 0) == 0;
+        std::vector<uint16_t> l16;
+        std::vector<int> l32;
+        if (h->lut16) l16.resize((size_t)n); else l32.resize((size_t)n);
         for (long long i = 0; i < n; ++i) {
             const int v = cfg->out_lut[i];
             if (v < -1 || v >= h->S) {
@@ -572,15 +664,20 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 release(h);
                 return r;
             }
-            lut[(size_t)i] = v < 0 ? -1 : (int)((long long)v * h->T);
+            if (h->lut16) l16[(size_t)i] = v < 0 ? (uint16_t)0xFFFF : (uint16_t)v;
+            else l32[(size_t)i] = v < 0 ? -1 : (int)((long long)v * h->T);
         }
-        CREATE_CHECK(dev_alloc(h, &h->d_lut, (size_t)n));
-        CREATE_HIP(hipMemcpy(h->d_lut, lut.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+        if (h->lut16) {
+            CREATE_CHECK(dev_alloc(h, (uint16_t **)&h->d_lut, (size_t)n));
+            CREATE_HIP(hipMemcpy(h->d_lut, l16.data(), (size_t)n * 2, hipMemcpyHostToDevice));
+        } else {
+            CREATE_CHECK(dev_alloc(h, (int **)&h->d_lut, (size_t)n));
+            CREATE_HIP(hipMemcpy(h->d_lut, l32.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+        }
     }
-    CREATE_CHECK(dev_alloc(h, &h->d_thr, thr.size()));
-    CREATE_HIP(hipMemcpy(h->d_thr, thr.data(), thr.size() * 8, hipMemcpyHostToDevice));
-    CREATE_CHECK(dev_alloc(h, &h->d_bp, bp.size()));
-    CREATE_HIP(hipMemcpy(h->d_bp, bp.data(), bp.size() * 4, hipMemcpyHostToDevice));
+    CREATE_CHECK(dev_alloc(h, &h->d_tab, tab.size()));
+    CREATE_HIP(hipMemcpy(h->d_tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
+    h->peel = env_ll("LDE_PEEL", 1) != 0;
 
     // histograms
     CREATE_CHECK(dev_alloc(h, &h->d_win32, (size_t)nbins));
@@ -601,11 +698,13 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         tb = std::max(13, std::min(tb, 15));
         while (tb < 15 && (nbins + (1LL << tb) - 1) >> tb > lde::kMaxTiles) ++tb;
         const long long nt = (nbins + (1LL << tb) - 1) >> tb;
-        const bool smem_ok = lde::partition_smem((int)nt, h->tp) <= 160 * 1024;
+        const bool smem_ok = lde::partition_smem((int)nt, h->tp) <= 64 * 1024;
         if (nt <= lde::kMaxTiles && smem_ok) {
             h->tile_bits = tb;
             h->n_tiles = (int)nt;
             h->part_rows = 2 * h->cus;
+            h->part_grid = (int)std::min<long long>(
+                h->part_rows, std::max<long long>(1, env_ll("LDE_PART_GRID", 2LL * h->cus)));
             CREATE_CHECK(dev_alloc(h, &h->d_part, (size_t)h->part_rows * h->n_tiles));
             CREATE_CHECK(dev_alloc(h, &h->d_ttot, (size_t)h->n_tiles));
             CREATE_CHECK(dev_alloc(h, &h->d_tile_items, (size_t)h->n_tiles));
@@ -617,6 +716,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);
     }
     CREATE_HIP(hipEventCreateWithFlags(&h->pin_done, hipEventDisableTiming));
+    CREATE_HIP(hipEventCreateWithFlags(&h->segs_done, hipEventDisableTiming));
     CREATE_HIP(hipStreamSynchronize(h->stream));
 #undef CREATE_CHECK
 #undef CREATE_HIP

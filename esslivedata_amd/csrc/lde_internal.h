@@ -6,27 +6,62 @@
 
 namespace lde {
 
-constexpr int kPartThreads = 1024;                 // pass A block
+constexpr int kPartThreads = 512;                  // pass A block
+constexpr int kPartMinWavesPerEU = 4;              // 2 pass-A blocks per CU
 constexpr int kPartEventsPerThread = 16;           // 4 x int4 per array
-constexpr int kChunk = kPartThreads * kPartEventsPerThread;  // 16384 events
-constexpr int kMaxTilesPerThread = 4;              // pass A/plan scan width
-constexpr int kMaxTiles = kPartThreads * kMaxTilesPerThread;  // 4096 tiles
+constexpr int kChunk = kPartThreads * kPartEventsPerThread;  // 8192 events
+constexpr int kMaxTiles = 4096;                    // tiles of the (S,T) histogram
 constexpr int kTileThreads = 512;                  // pass B block
 constexpr int kMonitorColumnsMaxT = 512;           // conflict-free monitor layout
-constexpr int kMaxBuckets = 4096;                  // TOA bucket table
+constexpr int kMaxBuckets = 4096;                  // TOA bucket table (general layout)
+constexpr int kMaxFastBuckets = 16384;             // TOA bucket table (fast layout)
+constexpr int kMaxSegs = 64;                       // segments per pass-A launch
+constexpr int kLaneModeRun = 48;                   // pass B: lane-per-chunk below this avg run
+
+struct SegDesc {  // one staged ev44 message (device pointers)
+    const int *pid;
+    const int *toa;
+    long long n;
+    long long chunk0;  // first global chunk of this segment
+};
 
 struct ToaParams {
-    long long lo;  // ceil(edge[0])  (clamped to the int32 domain)
-    long long hi;  // ceil(edge[T])
-    int shift;     // bucket width = 2^shift
-    int G;         // number of buckets
-    int T;         // number of TOA bins
+    long long lo;   // ceil(edge[0])  (clamped to [INT32_MIN, INT32_MAX + 1])
+    long long hi;   // ceil(edge[T])
+    unsigned span;  // hi - lo (fast layout only)
+    int shift;      // bucket width = 2^shift
+    int G;          // number of buckets
+    int T;          // number of TOA bins
+    int fast;       // 1: u32 relative thresholds + one-step u16 buckets
     int pad;
 };
 
 __host__ __device__ constexpr inline int align4(int x) { return (x + 3) & ~3; }
 __host__ __device__ constexpr inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
-__host__ __device__ constexpr inline size_t thr_bytes(int T) { return align16((size_t)(T + 1) * 8); }
+// bytes of the TOA lookup image copied verbatim into LDS
+__host__ __device__ inline size_t toa_lds_bytes(const ToaParams &tp) {
+    return tp.fast ? align16((size_t)(tp.T + 1) * 4) + align16((size_t)tp.G * 2)
+                   : align16((size_t)(tp.T + 1) * 8) + align16((size_t)tp.G * 4);
+}
+
+struct PartitionArgs {
+    int tile_bits;
+    bool lut16;
+    bool peel;
+    const SegDesc *segs;
+    int n_segs;
+    long long c_begin, n_chunks;
+    const void *lut;
+    int pid_off;
+    unsigned L;
+    const unsigned char *tab;
+    ToaParams tp;
+    int n_tiles;
+    uint16_t *payload;
+    uint32_t *starts;
+    uint32_t *part;
+    int grid;
+};
 
 inline unsigned grid_for(long long n) {
     long long g = (n + 255) / 256;
@@ -37,25 +72,19 @@ inline unsigned grid_for(long long n) {
 
 size_t partition_smem(int n_tiles, const ToaParams &tp);
 
-hipError_t launch_bin_atomic(const int *pid, const int *toa, long long n, const int *lut,
-                             int pid_off, unsigned L, const long long *thr, const uint32_t *bp,
-                             const ToaParams &tp, uint32_t *hist, bool vec, int grid,
-                             hipStream_t st);
-hipError_t launch_partition(int tile_bits, const int *pid, const int *toa, long long n,
-                            const int *lut, int pid_off, unsigned L, const long long *thr,
-                            const uint32_t *bp, const ToaParams &tp, int n_tiles, long long chunk0,
-                            long long n_chunks, uint16_t *payload, uint32_t *starts,
-                            uint32_t *part, bool vec, int grid, hipStream_t st);
-hipError_t launch_plan(const uint32_t *part, int part_rows, int n_tiles, uint32_t item_events,
-                       uint32_t *totals, uint32_t *tile_items, uint2 *items,
+hipError_t launch_bin_atomic(const SegDesc &seg, const void *lut, bool lut16, int pid_off,
+                             unsigned L, const unsigned char *tab, const ToaParams &tp,
+                             uint32_t *hist, int grid, hipStream_t st);
+hipError_t launch_partition(const PartitionArgs &a, hipStream_t st);
+hipError_t launch_plan(const uint32_t *part, int part_rows, int n_tiles, long long n_chunks,
+                       uint32_t item_events, uint32_t *totals, uint32_t *tile_items, uint2 *items,
                        uint32_t *item_count, uint32_t max_items, hipStream_t st);
 hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const uint32_t *starts,
                                   int n_tiles, long long n_chunks, const uint2 *items,
                                   const uint32_t *item_count, const uint32_t *tile_items,
                                   uint32_t *hist, long long n_bins, int grid, hipStream_t st);
-hipError_t launch_monitor(const int *toa, long long n, const long long *thr, const uint32_t *bp,
-                          const ToaParams &tp, uint32_t *hist, bool vec, int grid,
-                          hipStream_t st);
+hipError_t launch_monitor(const SegDesc &seg, const unsigned char *tab, const ToaParams &tp,
+                          uint32_t *hist, int grid, hipStream_t st);
 hipError_t launch_fold_window(uint32_t *win32, unsigned long long *win64, long long n,
                               hipStream_t st);
 hipError_t launch_merge_f32(uint32_t *batch, unsigned long long *win64, float *winf, float *cumf,

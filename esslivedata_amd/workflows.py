@@ -1,0 +1,384 @@
+"""Workflow-protocol side of the drop-in boundary (GPU detector view / monitor).
+
+``GpuDetectorViewWorkflow`` and ``GpuMonitorWorkflow`` implement the
+reference's ``Workflow`` protocol (SRC/workflows/workflow_factory.py:22-34:
+``accumulate(data, *, start_time, end_time)``, ``finalize() -> dict``,
+``clear()``) plus ``SupportsContext.build`` (:37-57), with the same output
+names (SRC/workflows/detector_view/factory.py:208-215,
+SRC/workflows/monitor_workflow.py:318-325) and window time coords
+(SRC/workflows/stream_processor_workflow.py:225-244).  Every per-event step
+runs in the HIP engine (``BinningEngine``); the host only stages message
+arrays and assembles the small finalize outputs.
+
+Semantics mirrored:
+* replica cycling ``counter % R`` per accumulate (projectors.py:105-113);
+* cumulative/current pair with reset-on-geometry-change
+  (SRC/preprocessors/accumulators.py:86-195);
+* ``detector_image``: sum over the TOA slice, optional ``/ weights``;
+  ``counts_total``; ``counts_in_range`` (providers.py:236-357);
+* monitor histogram coord: edges converted to ns and back to the edge unit
+  (monitor_workflow.py:93-100), ranges by label slicing (:154-167).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Callable, Iterable, Mapping, Sequence
+
+import numpy as np
+
+from .dataarray import DataArray, Variable
+from .edges import TOAEdges, convert_time, label_slice
+from .engine import BinningEngine
+from .preprocessors import DetectorEvents, MonitorEvents, StagedEvents, Timestamp
+from .projection import ViewLUT, geometric_lut, logical_lut
+
+DETECTOR_TRANSFORM = 'detector_transform'
+MONITOR_TRANSFORM = 'monitor_transform'
+
+DETECTOR_WINDOW_OUTPUTS = ('current', 'counts_total', 'counts_in_toa_range')
+MONITOR_WINDOW_OUTPUTS = ('current', 'counts_total', 'counts_in_toa_range')
+
+
+# ---------------------------------------------------------------------------
+# parameters and view configuration
+# ---------------------------------------------------------------------------
+@dataclass
+class DetectorViewParams:
+    """Subset of ``DetectorViewParams`` (SRC/workflows/detector_view_specs.py:53-124)
+    relevant in TOA mode."""
+
+    toa_edges: TOAEdges = field(default_factory=TOAEdges)
+    toa_range: tuple[float, float] | None = None  # in toa_edges.unit; None = disabled
+    pixel_weighting: bool = False
+
+
+@dataclass(frozen=True)
+class GeometricViewConfig:
+    """``GeometricViewConfig`` (SRC/workflows/detector_view/types.py:94-131)."""
+
+    projection_type: str
+    resolution: dict[str, int]
+    pixel_noise: Any = None
+    flip_x: bool = False
+
+
+@dataclass(frozen=True)
+class LogicalViewConfig:
+    """``LogicalViewConfig`` (types.py:134-162); ``transform`` maps an
+    index-valued array shaped like ``detector_number`` (and the source name) to
+    the reshaped/sliced view; ``reduction_axes`` are merged."""
+
+    transform: Callable[[np.ndarray, str], np.ndarray] | None = None
+    reduction_axes: Sequence[int] = ()
+    output_dims: tuple[str, ...] | None = None
+
+
+def _histogram_slice(edges: TOAEdges, toa_range) -> tuple[int, int] | None:
+    if toa_range is None:
+        return None
+    return label_slice(edges.get_edges(), float(toa_range[0]), float(toa_range[1]))
+
+
+def _events_of(data) -> tuple[list, list | None]:
+    """Normalise the accepted inputs into per-message (pid, toa) lists."""
+    if isinstance(data, StagedEvents):
+        return data.time_of_arrival, data.pixel_id
+    if isinstance(data, DetectorEvents):
+        return [data.time_of_arrival], [data.pixel_id]
+    if isinstance(data, MonitorEvents):
+        return [data.time_of_arrival], None
+    if isinstance(data, tuple) and len(data) == 2:
+        pid, toa = data
+        return [toa], None if pid is None else [pid]
+    raise TypeError(f'unsupported event payload {type(data).__name__}')
+
+
+def _stage(engine: BinningEngine, toas: list, pids: list | None) -> None:
+    for i, toa in enumerate(toas):
+        pid = None if pids is None else pids[i]
+        if hasattr(toa, 'data_ptr'):  # device tensors: no copy
+            engine.stage_tensors(pid, toa)
+        else:
+            engine.stage(pid, toa)
+
+
+class _ContextState:
+    """Tracks the geometry signal context (reset-on-move)."""
+
+    def __init__(self, key: str | None) -> None:
+        self.key = key
+        self.value = None
+
+    def changed(self, data: Mapping[str, Any]) -> bool:
+        if self.key is None or self.key not in data:
+            return False
+        new = data[self.key]
+        old, self.value = self.value, new
+        if old is None or new is None:
+            return False
+        return not np.array_equal(np.asarray(old), np.asarray(new))
+
+
+# ---------------------------------------------------------------------------
+# detector view
+# ---------------------------------------------------------------------------
+class GpuDetectorViewWorkflow:
+    """Detector view in TOA mode on the MI355X engine."""
+
+    def __init__(
+        self,
+        source_name: str,
+        view: ViewLUT,
+        params: DetectorViewParams | None = None,
+        *,
+        out_dtype: str = 'float64',
+        device: int = 0,
+        stream: int | None = None,
+        geometry_key: str | None = DETECTOR_TRANSFORM,
+        strategy: str = 'auto',
+    ) -> None:
+        self._source = source_name
+        self._view = view
+        self._params = params or DetectorViewParams()
+        self._edges_unit = self._params.toa_edges.get_edges()
+        self._slice = _histogram_slice(self._params.toa_edges, self._params.toa_range)
+        self._engine = BinningEngine(
+            toa_edges_ns=self._params.toa_edges.edges_ns(),
+            out_lut=view.lut,
+            pid_offset=view.pid_offset,
+            n_screen=view.n_screen,
+            out_dtype=out_dtype,
+            strategy=strategy,
+            toa_range=self._slice,
+            device=device,
+            stream=stream,
+        )
+        self._counter = 0
+        self._geometry = _ContextState(geometry_key)
+        self._context_keys: dict[str, Any] = {}
+        self._built = False
+        self._start: Timestamp | None = None
+        self._end: Timestamp | None = None
+
+    @property
+    def engine(self) -> BinningEngine:
+        return self._engine
+
+    @property
+    def view(self) -> ViewLUT:
+        return self._view
+
+    # SupportsContext
+    def build(self, *, context_keys: Mapping[str, Any] | None = None,
+              chain_patch_bindings: Iterable = ()) -> None:
+        bindings = list(chain_patch_bindings)
+        if self._built:
+            if context_keys or bindings:
+                raise RuntimeError('Cannot inject bindings: the workflow is already built.')
+            return
+        if context_keys:
+            self._context_keys.update(context_keys)
+        self._built = True
+
+    def accumulate(self, data: dict[str, Any], *, start_time: Timestamp,
+                   end_time: Timestamp) -> None:
+        if self._start is None:
+            self._start = start_time
+        self._end = end_time
+        if self._geometry.changed(data):
+            self._engine.reset_cumulative()
+        if self._source not in data:
+            return
+        toas, pids = _events_of(data[self._source])
+        if pids is None:
+            raise ValueError('detector events need pixel ids')
+        _stage(self._engine, toas, pids)
+        replica = self._counter % self._view.n_replicas
+        self._counter += 1
+        self._engine.accumulate(replica)
+
+    def _image(self, values: np.ndarray) -> DataArray:
+        img = values.reshape(self._view.screen_shape)
+        if self._params.pixel_weighting and self._view.pixel_weights is not None:
+            with np.errstate(divide='ignore', invalid='ignore'):
+                img = img / self._view.pixel_weights
+        coords = {d: Variable((d,), c) for d, c in self._view.screen_coords.items()}
+        return DataArray(img, self._view.screen_dims, 'counts', coords)
+
+    def finalize(self) -> dict[str, Any]:
+        res = self._engine.finalize(images=True)
+        dt = self._engine.dtype.type
+        out = {
+            'cumulative': self._image(res.cumulative_image),
+            'current': self._image(res.current_image),
+            'counts_total': DataArray(np.asarray(dt(res.current_total)), (), 'counts'),
+            'counts_in_toa_range': DataArray(np.asarray(dt(res.current_in_range)), (), 'counts'),
+            'counts_total_cumulative': DataArray(np.asarray(dt(res.cumulative_total)), (), 'counts'),
+            'counts_in_toa_range_cumulative': DataArray(
+                np.asarray(dt(res.cumulative_in_range)), (), 'counts'
+            ),
+        }
+        if self._start is not None:
+            st = Variable((), self._start.to_ns(), 'ns')
+            tt = Variable((), self._end.to_ns(), 'ns')
+            for name in DETECTOR_WINDOW_OUTPUTS:
+                out[name] = out[name].assign_coords(start_time=st, time=tt)
+        self._start = self._end = None
+        return out
+
+    def read_histogram(self, which: str = 'cumulative') -> DataArray:
+        h = self._engine.read_histogram(which)
+        dims = (*self._view.screen_dims, 'time_of_arrival')
+        shape = (*self._view.screen_shape, h.shape[-1])
+        return DataArray(
+            h.reshape(shape), dims, 'counts',
+            {'time_of_arrival': Variable(('time_of_arrival',), self._edges_unit,
+                                         self._params.toa_edges.unit)},
+        )
+
+    def clear(self) -> None:
+        self._engine.clear()
+        self._start = self._end = None
+
+
+class GpuDetectorViewFactory:
+    """``DetectorViewFactory.make_workflow`` (detector_view/factory.py:95-276).
+
+    ``detector_numbers`` supplies each source's ``detector_number`` (as
+    ``Instrument.get_detector_number`` does); geometric views additionally
+    need per-replica projected coordinates ``projected_coords[source][dim]`` of
+    shape (replica, pixel), the output of essreduce's projection of
+    ``CalibratedPositionWithNoisyReplicas`` (setup-time input).
+    """
+
+    def __init__(
+        self,
+        *,
+        detector_numbers: Mapping[str, np.ndarray],
+        view_config: GeometricViewConfig | LogicalViewConfig | Mapping[str, Any],
+        projected_coords: Mapping[str, Mapping[str, np.ndarray]] | None = None,
+        out_dtype: str = 'float64',
+        device: int = 0,
+    ) -> None:
+        self._dn = dict(detector_numbers)
+        self._cfg = view_config
+        self._coords = dict(projected_coords or {})
+        self._dtype = out_dtype
+        self._device = device
+
+    def _config(self, source: str):
+        if isinstance(self._cfg, Mapping):
+            return self._cfg[source]
+        return self._cfg
+
+    def make_view(self, source_name: str) -> ViewLUT:
+        cfg = self._config(source_name)
+        dn = np.asarray(self._dn[source_name])
+        if isinstance(cfg, GeometricViewConfig):
+            if source_name not in self._coords:
+                raise ValueError(f'no projected coordinates for {source_name!r}')
+            return geometric_lut(dn, self._coords[source_name], cfg.resolution, flip_x=cfg.flip_x)
+        if isinstance(cfg, LogicalViewConfig):
+            tf = None if cfg.transform is None else (lambda a: cfg.transform(a, source_name))
+            return logical_lut(dn, transform=tf, reduction_axes=cfg.reduction_axes,
+                               output_dims=cfg.output_dims)
+        raise TypeError(f'unknown view config {type(cfg).__name__}')
+
+    def make_workflow(self, source_name: str, params: DetectorViewParams | None = None,
+                      aux_source_names: Mapping[str, str] | None = None) -> GpuDetectorViewWorkflow:
+        _ = aux_source_names
+        return GpuDetectorViewWorkflow(
+            source_name, self.make_view(source_name), params, out_dtype=self._dtype,
+            device=self._device,
+        )
+
+
+# ---------------------------------------------------------------------------
+# monitor histogram
+# ---------------------------------------------------------------------------
+class GpuMonitorWorkflow:
+    """Monitor TOA histogram (``create_monitor_workflow`` TOA/event mode,
+    monitor_workflow.py:225-331)."""
+
+    def __init__(
+        self,
+        source_name: str,
+        edges: TOAEdges,
+        *,
+        range_filter: tuple[float, float] | None = None,
+        device: int = 0,
+        stream: int | None = None,
+        geometry_key: str | None = MONITOR_TRANSFORM,
+    ) -> None:
+        self._source = source_name
+        self._edges = edges
+        e_unit = edges.get_edges()
+        e_ns = edges.edges_ns()
+        # output coord: edges converted to ns and back (monitor_workflow.py:100)
+        self._coord = convert_time(e_ns, 'ns', edges.unit)
+        lo, hi = range_filter if range_filter is not None else (e_unit[0], e_unit[-1])
+        self._slice = label_slice(self._coord, float(lo), float(hi))
+        self._engine = BinningEngine.monitor(e_ns, toa_range=self._slice, device=device,
+                                             stream=stream)
+        self._geometry = _ContextState(geometry_key)
+        self._start: Timestamp | None = None
+        self._end: Timestamp | None = None
+        self._built = False
+
+    @property
+    def engine(self) -> BinningEngine:
+        return self._engine
+
+    def build(self, *, context_keys=None, chain_patch_bindings: Iterable = ()) -> None:
+        if self._built and (context_keys or list(chain_patch_bindings)):
+            raise RuntimeError('Cannot inject bindings: the workflow is already built.')
+        self._built = True
+
+    def accumulate(self, data: dict[str, Any], *, start_time: Timestamp,
+                   end_time: Timestamp) -> None:
+        if self._start is None:
+            self._start = start_time
+        self._end = end_time
+        if self._geometry.changed(data):
+            self._engine.reset_cumulative()
+        if self._source not in data:
+            return
+        toas, _ = _events_of(data[self._source])
+        _stage(self._engine, toas, None)
+        self._engine.accumulate(0)
+
+    def _hist(self, values: np.ndarray) -> DataArray:
+        dim = 'time_of_arrival'
+        return DataArray(values.reshape(-1), (dim,), 'counts',
+                         {dim: Variable((dim,), self._coord, self._edges.unit)})
+
+    def finalize(self) -> dict[str, Any]:
+        res = self._engine.finalize(images=False, hists=True)
+        out = {
+            'cumulative': self._hist(res.cumulative_hist),
+            'current': self._hist(res.current_hist),
+            'counts_total': DataArray(np.asarray(float(res.current_total)), (), 'counts'),
+            'counts_in_toa_range': DataArray(np.asarray(float(res.current_in_range)), (), 'counts'),
+            'counts_total_cumulative': DataArray(np.asarray(float(res.cumulative_total)), (), 'counts'),
+            'counts_in_toa_range_cumulative': DataArray(
+                np.asarray(float(res.cumulative_in_range)), (), 'counts'
+            ),
+        }
+        if self._start is not None:
+            st = Variable((), self._start.to_ns(), 'ns')
+            tt = Variable((), self._end.to_ns(), 'ns')
+            for name in MONITOR_WINDOW_OUTPUTS:
+                out[name] = out[name].assign_coords(start_time=st, time=tt)
+        self._start = self._end = None
+        return out
+
+    def clear(self) -> None:
+        self._engine.clear()
+        self._start = self._end = None
+
+
+def create_gpu_monitor_workflow(source_name: str, edges: TOAEdges, *,
+                                range_filter: tuple[float, float] | None = None,
+                                device: int = 0) -> GpuMonitorWorkflow:
+    return GpuMonitorWorkflow(source_name, edges, range_filter=range_filter, device=device)

@@ -1,0 +1,170 @@
+"""Generate the committed golden fixtures under tests/golden/.
+
+Run from the repo root:  python tests/golden/make_golden.py
+
+Three kinds of fixtures (see DESIGN.md "Parity"):
+
+1. ``reference_kats.json`` -- known answers transcribed from the reference's own
+   tests (inputs and expected outputs as data; file:line cited per case).  The
+   reference cannot be imported here (Python 3.10 vs >=3.12, scipp/essreduce
+   absent), so these literals are the reference's pinned behaviour.
+2. ``tie_kats.json`` -- hand-derived edge-tie cases: integer TOAs exactly on,
+   below and above float64 edges produced by ``linspace``/``geomspace`` in ms and
+   converted to ns with one f64 multiply.  Expected bins were worked out by
+   hand from the f64 values printed next to them (e.g. 5.0001 ms * 1e6 =
+   5000100.000000001 ns, so TOA 5000100 ns is in bin 6, not 7).
+3. ``dream_small.npz`` -- a restatement-generated regression vector (DREAM
+   mantle shape, skewed pixels, geomspace edges; 200k events, replica 1) with
+   the oracle's histogram, used to pin the GPU engine and to catch oracle drift.
+"""
+
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parents[1]
+sys.path.insert(0, str(ROOT))
+
+REFERENCE_KATS = [
+    {
+        'name': 'group_by_pixel_sizes',
+        'source': 'tests/preprocessors/group_by_pixel_test.py:24-45',
+        'detector_number': [1, 2, 3],
+        'messages': [{'pixel_id': [1, 2, 3, 1, 3], 'toa': [100, 200, 300, 400, 500]}],
+        'expected_sizes': [2, 1, 2],
+    },
+    {
+        'name': 'group_by_pixel_two_messages',
+        'source': 'tests/preprocessors/group_by_pixel_test.py:47-63',
+        'detector_number': [1, 2],
+        'messages': [
+            {'pixel_id': [1, 2], 'toa': [100, 200]},
+            {'pixel_id': [1, 1], 'toa': [300, 400]},
+        ],
+        'expected_sizes': [3, 1],
+    },
+    {
+        'name': 'group_by_pixel_after_get',
+        'source': 'tests/preprocessors/group_by_pixel_test.py:81-93',
+        'detector_number': [1, 2],
+        'messages': [{'pixel_id': [2], 'toa': [200]}],
+        'expected_sizes': [0, 1],
+    },
+    {
+        'name': 'monitor_event_histogram',
+        'source': 'tests/workflows/monitor_workflow_test.py:161-183',
+        'toa_ns': [1, 2, 3, 4, 5],
+        'edges_ns': [0.0, 2.0, 4.0, 6.0, 8.0, 10.0],
+        'expected_sum': 5,
+        'expected_hist': [1, 2, 2, 0, 0],
+    },
+    {
+        'name': 'monitor_counts_in_range',
+        'source': 'tests/workflows/monitor_workflow_test.py:232-243',
+        'edges_ns': [0.0, 2.0, 4.0, 6.0, 8.0, 10.0],
+        'hist': [1.0, 2.0, 3.0, 4.0, 5.0],
+        'range_ns': [2.0, 8.0],
+        'expected': 9.0,
+    },
+    {
+        'name': 'monitor_counts_total',
+        'source': 'tests/workflows/monitor_workflow_test.py:222-230',
+        'hist': [1.0, 2.0, 3.0],
+        'expected': 6.0,
+    },
+    {
+        'name': 'detector_service_cumulative_current',
+        'source': 'tests/services/detector_data_test.py:57-131',
+        'note': 'uniform(0, 70e6) ns TOA (tests/helpers/livedata_app.py:189) is inside the '
+        'default 0..71.43 ms edges, so every event with a known pixel id is counted',
+        'batches': [[2000], [3000], [1000, 1000]],
+        'expected_cumulative': [2000, 5000, 7000],
+        'expected_current': [2000, 3000, 2000],
+    },
+]
+
+# hand-derived: toa -> expected bin (-1 = dropped)
+TIE_KATS = [
+    {
+        'name': 'default_linear_edges_ms',
+        'edges_ms': {'op': 'linspace', 'start': 0.0, 'stop': 71.43, 'num': 101},
+        'f64_edges_ns_used': {'1': 714300.0, '7': 5000100.000000001, '10': 7143000.000000001,
+                              '100': 71430000.0},
+        'cases': [
+            [-1, -1], [0, 0], [714299, 0], [714300, 1], [714301, 1],
+            [5000099, 6], [5000100, 6], [5000101, 7],
+            [7142999, 9], [7143000, 9], [7143001, 10],
+            [71429999, 99], [71430000, -1], [71430001, -1],
+        ],
+    },
+    {
+        'name': 'geomspace_edges_ms',
+        'edges_ms': {'op': 'geomspace', 'start': 0.5, 'stop': 71.43, 'num': 101},
+        'f64_edges_ns_used': {'0': 500000.0, '1': 525435.1359694994, '50': 5976202.807803631,
+                              '99': 67972233.9734684, '100': 71430000.0},
+        'cases': [
+            [499999, -1], [500000, 0], [525435, 0], [525436, 1],
+            [5976202, 49], [5976203, 50], [67972233, 98], [67972234, 99],
+            [71429999, 99], [71430000, -1],
+        ],
+    },
+    {
+        'name': 'fractional_and_duplicate_edges_ns',
+        'edges_ns': [-5.5, -0.5, 0.0, 0.5, 1.0, 1.0, 2.5, 3.0],
+        'cases': [
+            [-6, -1], [-5, 0], [-1, 0], [0, 2], [1, 5], [2, 5], [3, -1],
+        ],
+    },
+]
+
+SCREEN_EDGE_KATS = [
+    {
+        'name': 'int_bin_count_includes_max',
+        'note': 'scipp hist({dim: res}) edges = linspace(nanmin, nextafter(nanmax, +inf), res+1)',
+        'values': [0.0, 1.0, 2.0, 3.0],
+        'res': 2,
+        'expected_bins': [0, 0, 1, 1],
+    },
+    {
+        'name': 'nan_dropped',
+        'values': [0.0, float('nan'), 4.0],
+        'res': 4,
+        'expected_bins': [0, -1, 3],
+    },
+]
+
+
+def main() -> None:
+    (HERE / 'reference_kats.json').write_text(json.dumps(REFERENCE_KATS, indent=1))
+    (HERE / 'tie_kats.json').write_text(
+        json.dumps({'toa': TIE_KATS, 'screen': SCREEN_EDGE_KATS}, indent=1)
+    )
+    from esslivedata_amd import synthetic
+    from oracle import scipp_semantics as ora
+
+    inst = synthetic.dream_mantle()
+    edges = {d: ora.screen_edges(inst.coords[d], r) for d, r in inst.resolution.items()}
+    pid, toa = synthetic.dream_events(200_000, inst, seed=11)
+    pid[:500] = 100  # unknown ids
+    ps = ora.geometric_screen_index(inst.coords, edges, 1)
+    pix = ora.pixel_index(pid, inst.detector_number)
+    hist = ora.detector_histogram(ps, 25600, pix, toa, inst.edges.edges_ns())
+    nz = np.nonzero(hist.ravel())[0]
+    np.savez_compressed(
+        HERE / 'dream_small.npz',
+        pid=pid,
+        toa=toa,
+        replica=np.int32(1),
+        hist_index=nz.astype(np.int32),
+        hist_value=hist.ravel()[nz].astype(np.int32),
+    )
+    print('wrote', sorted(p.name for p in HERE.iterdir() if p.suffix in ('.json', '.npz')))
+
+
+if __name__ == '__main__':
+    main()

@@ -13,6 +13,15 @@ pytestmark = pytest.mark.gpu
 
 STRATEGIES = ['atomic', 'partition']
 
+# internal kernel variants that must all be bit-identical
+VARIANTS = [
+    {},
+    {'LDE_LUT32': '1'},
+    {'LDE_TOA_GENERAL': '1'},
+    {'LDE_PEEL': '0'},
+    {'LDE_TILE_BITS': '15', 'LDE_PART_GRID': '7'},
+]
+
 
 @pytest.fixture(scope='module', autouse=True)
 def _gpu(engine_lib):
@@ -111,8 +120,11 @@ def test_dummy_logical_view_multi_batch(strategy):
             assert res.cumulative_total == exp['counts_total_cumulative']
 
 
+@pytest.mark.parametrize('variant', range(len(VARIANTS)))
 @pytest.mark.parametrize('strategy', STRATEGIES)
-def test_dream_mantle_geometric_skewed(strategy):
+def test_dream_mantle_geometric_skewed(strategy, variant, monkeypatch):
+    for k, v in VARIANTS[variant].items():
+        monkeypatch.setenv(k, v)
     from esslivedata_amd import projection, synthetic
 
     inst = synthetic.dream_mantle()
@@ -146,9 +158,12 @@ def test_dream_mantle_geometric_skewed(strategy):
     assert res.cumulative_in_range == exp['counts_in_toa_range_cumulative']
 
 
+@pytest.mark.parametrize('general', [False, True])
 @pytest.mark.parametrize('strategy', STRATEGIES)
-def test_edge_ties_are_bit_exact(strategy):
+def test_edge_ties_are_bit_exact(strategy, general, monkeypatch):
     """Integer TOAs on, just below and just above every float64 edge."""
+    if general:
+        monkeypatch.setenv('LDE_TOA_GENERAL', '1')
     from esslivedata_amd import projection
 
     dn = np.arange(1, 65, dtype=np.int32)
@@ -157,6 +172,9 @@ def test_edge_ties_are_bit_exact(strategy):
         np.linspace(0, 71.43, 101) * 1e6,
         np.geomspace(0.5, 71.43, 101) * 1e6,
         np.array([-5.5, -0.5, 0.0, 0.5, 1.0, 1.0, 2.5, 3.0, 1e6 + 0.25]),
+        np.array([-3e9, -2.0**31, -1.5, 7.0, 2.0**31 - 1, 2.0**31, 5e9]),
+        np.array([10.0, 10.0, 10.0]),
+        np.sort(np.random.default_rng(3).uniform(-1e5, 1e5, 2001)),
     ):
         c = np.ceil(edges).astype(np.int64)
         toa = np.concatenate([c - 1, c, c + 1, np.floor(edges).astype(np.int64)])

@@ -1,0 +1,148 @@
+"""Pin the CPU oracle against the reference's known answers (CPU only).
+
+The reference itself cannot be imported in this container (it needs Python
+>= 3.12 and scipp/essreduce, which are absent -- ordinary errors, not a
+permission denial), so the oracle is pinned by the KATs transcribed from the
+reference's own tests (tests/golden/reference_kats.json) and by hand-derived
+edge-tie cases (tests/golden/tie_kats.json).
+"""
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import scipp_semantics as ora
+
+GOLDEN = Path(__file__).resolve().parent / 'golden'
+REF = {k['name']: k for k in json.loads((GOLDEN / 'reference_kats.json').read_text())}
+TIES = json.loads((GOLDEN / 'tie_kats.json').read_text())
+
+
+@pytest.mark.parametrize(
+    'name', ['group_by_pixel_sizes', 'group_by_pixel_two_messages', 'group_by_pixel_after_get']
+)
+def test_group_by_pixel_kats(name):
+    kat = REF[name]
+    dn = np.array(kat['detector_number'])
+    pid = np.concatenate([m['pixel_id'] for m in kat['messages']])
+    pix = ora.pixel_index(pid, dn)
+    sizes = np.bincount(pix[pix >= 0], minlength=len(dn))
+    np.testing.assert_array_equal(sizes, kat['expected_sizes'])
+
+
+def test_group_by_pixel_drops_unknown_and_noncontiguous_ids():
+    dn = np.array([[7, 3], [11, 100]])  # folded, non-contiguous (dream high-res style)
+    pid = np.array([3, 3, 4, 100, 7, 0, 11, 101])
+    np.testing.assert_array_equal(ora.pixel_index(pid, dn), [1, 1, -1, 3, 0, -1, 2, -1])
+
+
+def test_monitor_histogram_kat():
+    kat = REF['monitor_event_histogram']
+    h = ora.monitor_histogram(np.array(kat['toa_ns'], np.int32), np.array(kat['edges_ns']))
+    assert h.sum() == kat['expected_sum']
+    np.testing.assert_array_equal(h, kat['expected_hist'])
+
+
+def test_counts_in_range_kat():
+    kat = REF['monitor_counts_in_range']
+    lo, hi = ora.label_slice(np.array(kat['edges_ns']), *kat['range_ns'])
+    assert (lo, hi) == (1, 4)
+    assert np.sum(np.array(kat['hist'])[lo:hi]) == kat['expected']
+    assert np.sum(REF['monitor_counts_total']['hist']) == REF['monitor_counts_total']['expected']
+
+
+def test_label_slice_rule():
+    edges = np.array([0.0, 2.0, 4.0, 6.0, 8.0, 10.0])
+    assert ora.label_slice(edges, 1.0, 7.0) == (0, 4)  # bins containing / overlapping
+    assert ora.label_slice(edges, 0.0, 10.0) == (0, 5)
+    assert ora.label_slice(edges, -5.0, 50.0) == (0, 5)
+    assert ora.label_slice(edges, 4.0, 4.0) == (2, 2)
+
+
+def test_accumulator_pair_service_kat():
+    """detector_data_test.py:57-131: 2000 -> 2000/2000, +3000 -> 5000/3000,
+    +1000+1000 -> 7000/2000 on the dummy panel."""
+    kat = REF['detector_service_cumulative_current']
+    dn = np.arange(1, 128**2 + 1).reshape(128, 128)
+    edges = np.linspace(0, ora.ESS_PULSE_PERIOD_MS, 101) * 1e6
+    o = ora.OracleDetectorView(
+        detector_number=dn,
+        pixel_screen=np.arange(128**2)[None, :],
+        screen_shape=(128, 128),
+        toa_edges_ns=edges,
+    )
+    rng = np.random.default_rng(1234)
+    for sizes, cum, cur in zip(kat['batches'], kat['expected_cumulative'], kat['expected_current']):
+        for n in sizes:  # each message is its own accumulate call in the service
+            toa = rng.uniform(0, 70_000_000, n).astype(np.int32)
+            pid = rng.integers(1, 128**2 + 1, n, dtype=np.int32)
+            o.accumulate(pid, toa)
+        out = o.finalize()
+        assert np.nansum(out['cumulative']) == cum
+        assert np.nansum(out['current']) == cur
+        assert out['counts_total'] == cur and out['counts_total_cumulative'] == cum
+
+
+def test_accumulator_reset_on_geometry_change():
+    """accumulators.py:116-131: a changed reset coord restarts the cumulative."""
+    acc = ora.AccumulatorPair()
+    acc.push(np.array([1.0, 2.0]), geometry='g1')
+    acc.on_finalize()
+    acc.push(np.array([1.0, 1.0]), geometry='g1')
+    np.testing.assert_array_equal(acc.cumulative, [2.0, 3.0])
+    acc.on_finalize()
+    acc.push(np.array([5.0, 0.0]), geometry='g2')
+    np.testing.assert_array_equal(acc.cumulative, [5.0, 0.0])
+    np.testing.assert_array_equal(acc.window, [5.0, 0.0])
+    acc.push(np.array([1.0, 1.0]), geometry=None)  # absent coord: no reset
+    np.testing.assert_array_equal(acc.cumulative, [6.0, 1.0])
+
+
+@pytest.mark.parametrize('kat', TIES['toa'], ids=lambda k: k['name'])
+def test_toa_edge_ties(kat):
+    if 'edges_ms' in kat:
+        spec = kat['edges_ms']
+        op = {'linspace': np.linspace, 'geomspace': np.geomspace}[spec['op']]
+        edges = ora.to_ns(op(spec['start'], spec['stop'], spec['num']), 'ms')
+        for i, v in kat['f64_edges_ns_used'].items():
+            assert edges[int(i)] == v  # pins linspace/geomspace + ms->ns f64 arithmetic
+    else:
+        edges = np.array(kat['edges_ns'])
+    toa = np.array([c[0] for c in kat['cases']], dtype=np.int32)
+    exp = np.array([c[1] for c in kat['cases']])
+    np.testing.assert_array_equal(ora.hist_bin_index(toa, edges), exp)
+
+
+@pytest.mark.parametrize('kat', TIES['screen'], ids=lambda k: k['name'])
+def test_screen_edge_rule(kat):
+    v = np.array(kat['values'], dtype=np.float64)
+    e = ora.screen_edges(v, kat['res'])
+    np.testing.assert_array_equal(ora.hist_bin_index(v, e), kat['expected_bins'])
+
+
+def test_oracle_regression_vector():
+    """Restatement-generated golden vector (tests/golden/dream_small.npz)."""
+    from esslivedata_amd import synthetic
+
+    g = np.load(GOLDEN / 'dream_small.npz')
+    inst = synthetic.dream_mantle()
+    edges = {d: ora.screen_edges(inst.coords[d], r) for d, r in inst.resolution.items()}
+    ps = ora.geometric_screen_index(inst.coords, edges, int(g['replica']))
+    pix = ora.pixel_index(g['pid'], inst.detector_number)
+    hist = ora.detector_histogram(ps, 25600, pix, g['toa'], inst.edges.edges_ns()).ravel()
+    nz = np.nonzero(hist)[0]
+    np.testing.assert_array_equal(nz, g['hist_index'])
+    np.testing.assert_array_equal(hist[nz], g['hist_value'])
+
+
+def test_logical_view_reduction_and_slicing():
+    # fold 4x6 -> transpose, drop column 0, merge axis 0
+    lut, shape = ora.logical_screen_index((4, 6), lambda a: a.T[1:], reduction_axes=(1,))
+    assert shape == (5,)
+    idx = np.arange(24).reshape(4, 6)
+    for r in range(4):
+        assert lut[idx[r, 0]] == -1
+        for c in range(1, 6):
+            assert lut[idx[r, c]] == c - 1
