@@ -46,43 +46,50 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(inst, view_coords_screen, seconds: float) -> dict:
-    """Time the oracle (NumPy restatement of the scipp pipeline) on host cores."""
+def cpu_baseline(inst, pixel_screen, seconds: float) -> dict:
+    """Time the CPU restatement of the scipp pipeline on the host cores.
+
+    Main figure: oracle/binning_ref.c (group -> project -> hist -> +=, OpenMP
+    over the host cores, the way scipp's TBB kernels run).  The single-thread
+    NumPy oracle is reported beside it.
+    """
     from esslivedata_amd import synthetic
+    from oracle import c_oracle
     from oracle import scipp_semantics as ora
 
-    n = 2_000_000
-    o = ora.OracleDetectorView(
-        detector_number=inst.detector_number,
-        pixel_screen=view_coords_screen,
-        screen_shape=tuple(inst.resolution.values()),
-        toa_edges_ns=inst.edges.edges_ns(),
-    )
-    done = 0
-    batches = 0
-    t_total = 0.0
-    seed = 1
-    while t_total < seconds and batches < 64:
-        if inst.name == 'dream_mantle':
-            pid, toa = synthetic.dream_events(n, inst, seed=seed)
-        else:
-            pid, toa = synthetic.uniform_events(n, 1, 802816, seed=seed)
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, 16))
+    n = 4_000_000
+    gen = (lambda s: synthetic.dream_events(n, inst, seed=s)) if inst.name == 'dream_mantle' else (
+        lambda s: synthetic.uniform_events(n, 1, 802816, seed=s))
+    batches = [gen(s) for s in (1, 2, 3)]
+    c = c_oracle.CDetectorView(inst.detector_number, pixel_screen,
+                               int(np.prod(list(inst.resolution.values()))),
+                               inst.edges.edges_ns(), threads=threads)
+    done, t_total, k = 0, 0.0, 0
+    while t_total < seconds and k < 400:
+        pid, toa = batches[k % 3]
         t0 = time.perf_counter()
-        o.accumulate(pid, toa)
+        c.accumulate(pid, toa, k % pixel_screen.shape[0])
         t_total += time.perf_counter() - t0
         done += n
-        batches += 1
-        seed += 1
+        k += 1
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number, pixel_screen=pixel_screen,
+        screen_shape=tuple(inst.resolution.values()), toa_edges_ns=inst.edges.edges_ns())
     t0 = time.perf_counter()
-    o.finalize()
-    t_total += time.perf_counter() - t0
+    for j in range(2):
+        o.accumulate(*batches[j])
+    t_np = time.perf_counter() - t0
     return {
         'value': done / t_total,
         'unit': 'events/s',
-        'cores': 1,
+        'cores': c.threads_used,
         'kind': 'port',
-        'sample': f'{batches} batches x {n} events of the same workload through '
-        f'oracle/scipp_semantics.py (group -> project -> hist -> +=), {t_total:.1f} s',
+        'sample': f'{k} batches x {n} events of the same workload (3 distinct seeded batches, '
+        f'cycling replicas) through oracle/binning_ref.c with {c.threads_used} OpenMP threads, '
+        f'{t_total:.1f} s; NumPy oracle (1 core): {2 * n / t_np:.3e} events/s',
+        'numpy_1core': 2 * n / t_np,
     }
 
 
@@ -126,18 +133,16 @@ def main():
         pid, toa = synthetic.torch_uniform_events(n_step, 1, 802816, seed, dev)
     torch.cuda.synchronize(dev)
     nbins = view.n_screen * eng.n_toa_bins
-    merged = torch.zeros(nbins, dtype=torch.int32, device=dev) if world > 1 else None
+    from esslivedata_amd.distributed import WindowReducer
+
+    reducer = WindowReducer(eng, dev) if world > 1 else None
 
     def step(i: int):
         for p in range(args.pulses):
             eng.stage_tensors(pid[p * n_pulse : (p + 1) * n_pulse], toa[p * n_pulse : (p + 1) * n_pulse])
         eng.accumulate(i % view.n_replicas)
-        if world > 1:
-            eng.export_window(merged.data_ptr())
-            dist.reduce(merged, dst=0, op=dist.ReduceOp.SUM)
-            if rank == 0:
-                eng.import_window(merged.data_ptr())
-        if rank == 0 or world == 1:
+        root = reducer.reduce() if reducer is not None else True
+        if root:
             eng.finalize(images=True)
         else:
             eng.clear()
@@ -172,13 +177,11 @@ def main():
     # dominant kernel and its roofline (algorithmic bytes per launch / avg duration)
     dom = max(('atomic', 'partition', 'tile_accumulate'), key=lambda k: stats[k][0])
     ms, launches = stats[dom]
-    if dom == 'partition':
-        events_per_launch = n_pulse  # one launch per staged pulse segment
-    else:
-        events_per_launch = n_step
+    # every binning kernel processes all events of the timed steps across its launches
+    events_per_launch = n_step * args.steps / max(launches, 1)
     alg_bytes = BYTES_PER_EVENT * events_per_launch
     if dom == 'tile_accumulate':
-        alg_bytes += 4 * nbins  # window written once per batch
+        alg_bytes += 4 * nbins * args.steps / max(launches, 1)  # window written once per batch
     avg_s = (ms / max(launches, 1)) / 1e3
     achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
     bin_ms, bin_n = stats['binning']
@@ -228,10 +231,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import scipp_semantics as ora
 
-        edges_s = {d: ora.screen_edges(inst.coords[d] if d != 'x' or args.workload != 'loki' else -inst.coords[d], r) for d, r in inst.resolution.items()}
         coords = dict(inst.coords)
         if args.workload == 'loki':
             coords['x'] = -coords['x']
+        edges_s = {d: ora.screen_edges(coords[d], r) for d, r in inst.resolution.items()}
         ps = np.stack([ora.geometric_screen_index(coords, edges_s, k) for k in range(view.n_replicas)])
         result['cpu_baseline'] = cpu_baseline(inst, ps, args.cpu_baseline_seconds)
     if rank == 0:

@@ -1,0 +1,179 @@
+"""Workflow-protocol parity on the GPU: the drop-in detector-view and monitor
+workflows against the oracle's workflow restatement and the reference KATs."""
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import scipp_semantics as ora
+
+pytestmark = pytest.mark.gpu
+GOLDEN = Path(__file__).resolve().parent / 'golden'
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu(engine_lib):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+
+
+def _ts(s):
+    from esslivedata_amd.preprocessors import Timestamp
+
+    return Timestamp.from_seconds(s)
+
+
+def test_detector_service_kat_through_staging_and_workflow():
+    """detector_data_test.py:57-131 driven through EventStaging + workflow:
+    2000 -> 2000/2000; +3000 -> 5000/3000; +1000 +1000 -> 7000/2000."""
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.preprocessors import DetectorEvents, EventStaging
+    from esslivedata_amd.workflows import GpuDetectorViewWorkflow
+
+    kat = {k['name']: k for k in json.loads((GOLDEN / 'reference_kats.json').read_text())}[
+        'detector_service_cumulative_current'
+    ]
+    inst = synthetic.dummy_panel()
+    view = projection.logical_lut(inst.detector_number, dims=('y', 'x'))
+    wf = GpuDetectorViewWorkflow('panel_0', view)
+    wf.build()
+    pre = EventStaging(inst.detector_number)
+    rng = np.random.default_rng(1234)
+    t = 0
+    for sizes, cum, cur in zip(kat['batches'], kat['expected_cumulative'], kat['expected_current']):
+        for n in sizes:
+            t += 1
+            toa = rng.uniform(0, 70_000_000, n).astype(np.int32)
+            pid = rng.integers(1, 128**2 + 1, n, dtype=np.int32)
+            pre.add(_ts(t), DetectorEvents(pixel_id=pid, time_of_arrival=toa, unit='ns'))
+            wf.accumulate({'panel_0': pre.get()}, start_time=_ts(t), end_time=_ts(t + 1))
+            pre.release_buffers()
+        out = wf.finalize()
+        assert out['cumulative'].nansum().value == cum
+        assert out['current'].nansum().value == cur
+        assert out['counts_total'].value == cur
+        assert out['counts_total_cumulative'].value == cum
+        assert out['current'].dims == ('y', 'x') and out['current'].dtype == np.float64
+        assert 'start_time' in out['current'].coords and 'time' in out['counts_total'].coords
+        assert 'start_time' not in out['cumulative'].coords
+    with pytest.raises(ValueError):
+        wf.finalize()  # empty window: "No data has been added"
+
+
+def test_geometric_workflow_matches_oracle_with_replicas_range_and_reset():
+    from esslivedata_amd import synthetic
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.workflows import (
+        DetectorViewParams,
+        GeometricViewConfig,
+        GpuDetectorViewFactory,
+    )
+
+    inst = synthetic.dream_mantle()
+    params = DetectorViewParams(
+        toa_edges=TOAEdges(start=0.5, stop=71.43, num_bins=100, scale='log'),
+        toa_range=(10.0, 40.0),
+        pixel_weighting=True,
+    )
+    factory = GpuDetectorViewFactory(
+        detector_numbers={'mantle_detector': inst.detector_number},
+        view_config=GeometricViewConfig('cylinder_mantle_z', {'arc_length': 80, 'z': 320}),
+        projected_coords={'mantle_detector': inst.coords},
+    )
+    wf = factory.make_workflow('mantle_detector', params, {})
+    wf.build(context_keys={'mantle_detector/transform': 'detector_transform'})
+    edges_ms = params.toa_edges.get_edges()
+    sl = ora.label_slice(edges_ms, 10.0, 40.0)
+    oedges = {d: ora.screen_edges(inst.coords[d], r) for d, r in inst.resolution.items()}
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=np.stack([ora.geometric_screen_index(inst.coords, oedges, k) for k in range(5)]),
+        screen_shape=(80, 320),
+        toa_edges_ns=ora.to_ns(edges_ms, 'ms'),
+        toa_slice=sl,
+    )
+    geom = ['A', 'A', 'A', 'B', 'B', 'B', 'B']
+    for b, g in enumerate(geom):
+        pid, toa = synthetic.dream_events(300_000, inst, seed=b)
+        wf.accumulate(
+            {'mantle_detector': (pid, toa), 'detector_transform': g},
+            start_time=_ts(b),
+            end_time=_ts(b + 1),
+        )
+        o.accumulate(pid, toa, geometry=g)
+        if b in (1, 4, 6):
+            out = wf.finalize()
+            exp = o.finalize()
+            with np.errstate(divide='ignore', invalid='ignore'):
+                w = wf.view.pixel_weights
+                np.testing.assert_array_equal(out['current'].values, exp['current'] / w)
+                np.testing.assert_array_equal(out['cumulative'].values, exp['cumulative'] / w)
+            assert out['counts_in_toa_range'].value == exp['counts_in_toa_range']
+            assert out['counts_total_cumulative'].value == exp['counts_total_cumulative']
+
+
+def test_monitor_workflow_kats_and_range():
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.preprocessors import EventStaging, MonitorEvents
+    from esslivedata_amd.workflows import create_gpu_monitor_workflow
+
+    edges = TOAEdges(start=0.0, stop=10.0, num_bins=5, unit='ns')
+    wf = create_gpu_monitor_workflow('monitor_1', edges, range_filter=(2.0, 8.0))
+    wf.build()
+    pre = EventStaging()
+    pre.add(_ts(1), MonitorEvents([1, 2, 3, 4, 5], unit='ns'))
+    wf.accumulate({'monitor_1': pre.get()}, start_time=_ts(1), end_time=_ts(2))
+    pre.release_buffers()
+    out = wf.finalize()
+    np.testing.assert_array_equal(out['current'].values, [1, 2, 2, 0, 0])
+    assert out['counts_total'].value == 5
+    assert out['counts_in_toa_range'].value == 4  # bins [2,4),[4,6),[6,8)
+    # cumulative 10 vs current 5 over two batches (monitor_workflow_test.py:484-516)
+    pre.add(_ts(2), MonitorEvents([1, 2, 3, 4, 5], unit='ns'))
+    wf.accumulate({'monitor_1': pre.get()}, start_time=_ts(2), end_time=_ts(3))
+    out = wf.finalize()
+    assert out['counts_total_cumulative'].value == 10 and out['counts_total'].value == 5
+    assert out['current'].coords['time_of_arrival'].unit == 'ns'
+
+
+def test_monitor_workflow_ms_edges_match_oracle():
+    from esslivedata_amd import synthetic
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.workflows import GpuMonitorWorkflow
+
+    edges = TOAEdges()
+    wf = GpuMonitorWorkflow('monitor_2', edges, range_filter=(5.0, 30.0))
+    o = ora.OracleMonitor(
+        toa_edges_ns=edges.edges_ns(),
+        range_slice=ora.label_slice(edges.edges_ns() * 1e-6, 5.0, 30.0),
+    )
+    for b in range(4):
+        _, toa = synthetic.fake_detector_events(100_000, 1, 2, seed=b)
+        wf.accumulate({'monitor_2': (None, toa)}, start_time=_ts(b), end_time=_ts(b + 1))
+        o.accumulate(toa)
+    out, exp = wf.finalize(), o.finalize()
+    np.testing.assert_array_equal(out['current'].values, exp['current'])
+    np.testing.assert_array_equal(out['cumulative'].values, exp['cumulative'])
+    assert out['counts_in_toa_range'].value == exp['counts_in_toa_range']
+
+
+def test_golden_regression_vector_on_gpu():
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.engine import BinningEngine
+
+    g = np.load(GOLDEN / 'dream_small.npz')
+    inst = synthetic.dream_mantle()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    for strategy in ('atomic', 'partition'):
+        eng = BinningEngine(toa_edges_ns=inst.edges.edges_ns(), out_lut=view.lut,
+                            pid_offset=view.pid_offset, n_screen=view.n_screen, strategy=strategy)
+        eng.stage(g['pid'], g['toa'])
+        eng.accumulate(int(g['replica']))
+        h = eng.read_histogram().ravel()
+        nz = np.nonzero(h)[0]
+        np.testing.assert_array_equal(nz, g['hist_index'])
+        np.testing.assert_array_equal(h[nz], g['hist_value'])

@@ -146,3 +146,29 @@ def test_logical_view_reduction_and_slicing():
         assert lut[idx[r, 0]] == -1
         for c in range(1, 6):
             assert lut[idx[r, c]] == c - 1
+
+
+def test_c_oracle_matches_numpy_oracle():
+    """oracle/binning_ref.c (the CPU baseline) restates the same rules."""
+    from esslivedata_amd import synthetic
+    from oracle import c_oracle
+
+    g = np.load(GOLDEN / 'dream_small.npz')
+    inst = synthetic.dream_mantle()
+    edges = {d: ora.screen_edges(inst.coords[d], r) for d, r in inst.resolution.items()}
+    ps = np.stack([ora.geometric_screen_index(inst.coords, edges, k) for k in range(2)])
+    c = c_oracle.CDetectorView(inst.detector_number, ps, 25600, inst.edges.edges_ns(), threads=4)
+    h = c.accumulate(g['pid'], g['toa'], int(g['replica']))
+    nz = np.nonzero(h)[0]
+    np.testing.assert_array_equal(nz, g['hist_index'])
+    np.testing.assert_array_equal(h[nz], g['hist_value'])
+    # edge-tie KATs through the C binary search
+    for kat in TIES['toa']:
+        if 'edges_ns' not in kat:
+            continue
+        e = np.array(kat['edges_ns'])
+        cv = c_oracle.CDetectorView(np.array([1]), np.array([[0]]), 1, e, threads=1)
+        toa = np.array([x[0] for x in kat['cases']], dtype=np.int32)
+        exp = np.array([x[1] for x in kat['cases']])
+        got = cv.accumulate(np.ones(len(toa), np.int32), toa)
+        np.testing.assert_array_equal(got, np.bincount(exp[exp >= 0], minlength=len(e) - 1))
