@@ -27,108 +27,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lde_device.h"
 #include "lde_internal.h"
 
 namespace lde {
-
-// ---------------------------------------------------------------------------
-// TOA lookup
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void load_toa_tables(unsigned char *s_tab,
-                                                const unsigned char *__restrict__ g_tab,
-                                                const ToaParams &tp) {
-    const int n16 = (int)(toa_lds_bytes(tp) / 16);
-    for (int i = threadIdx.x; i < n16; i += blockDim.x)
-        reinterpret_cast<uint4 *>(s_tab)[i] = reinterpret_cast<const uint4 *>(g_tab)[i];
-}
-
-template <bool FAST>
-__device__ __forceinline__ int toa_bin(int t, const unsigned char *s_tab, const ToaParams &tp) {
-    if (FAST) {
-        const unsigned d = (unsigned)t - (unsigned)tp.lo;
-        if (d >= tp.span) return -1;
-        const uint32_t *rthr = reinterpret_cast<const uint32_t *>(s_tab);
-        const uint16_t *bst =
-            reinterpret_cast<const uint16_t *>(s_tab + align16((size_t)(tp.T + 1) * 4));
-        const int b = bst[d >> tp.shift];
-        return b + (d >= rthr[b + 1] ? 1 : 0);
-    } else {
-        const long long tt = t;
-        if (tt < tp.lo || tt >= tp.hi) return -1;
-        const long long *thr = reinterpret_cast<const long long *>(s_tab);
-        const uint32_t *bp =
-            reinterpret_cast<const uint32_t *>(s_tab + align16((size_t)(tp.T + 1) * 8));
-        const uint32_t pr = bp[(unsigned)((unsigned long long)(tt - tp.lo) >> tp.shift)];
-        int b = (int)(pr & 0xFFFFu);
-        int e = (int)(pr >> 16);
-        while (b < e) {
-            const int m = (b + e + 1) >> 1;
-            if (tt >= thr[m]) b = m; else e = m - 1;
-        }
-        return b;
-    }
-}
-
-// LUT entry -> flat histogram base (screen * T) or -1
-__device__ __forceinline__ int lut_base(const uint16_t *__restrict__ lut, unsigned p, int T) {
-    const unsigned v = lut[p];
-    return v == 0xFFFFu ? -1 : (int)(v * (unsigned)T);
-}
-__device__ __forceinline__ int lut_base(const int *__restrict__ lut, unsigned p, int) {
-    return lut[p];
-}
-
-template <typename LT, bool FAST>
-__device__ __forceinline__ int event_key(int pid, int t, const LT *__restrict__ lut, int pid_off,
-                                        unsigned L, const unsigned char *s_tab,
-                                        const ToaParams &tp) {
-    const unsigned p = (unsigned)pid - (unsigned)pid_off;
-    if (p >= L) return -1;
-    const int base = lut_base(lut, p, tp.T);
-    if (base < 0) return -1;
-    const int b = toa_bin<FAST>(t, s_tab, tp);
-    return b < 0 ? -1 : base + b;
-}
-
-// ---------------------------------------------------------------------------
-// wave / block helpers
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    return x;
-}
-
-// exclusive prefix of v across the block; *total = block sum.  s_w >= 17
-// uint32; contains two __syncthreads().
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *s_w,
-                                                         uint32_t *total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int nw = blockDim.x >> 6;
-    const uint32_t inc = wave_inclusive_scan(v);
-    if (lane == 63) s_w[wid] = inc;
-    __syncthreads();
-    if (wid == 0) {
-        const uint32_t w = lane < nw ? s_w[lane] : 0u;
-        const uint32_t wi = wave_inclusive_scan(w);
-        if (lane < nw) s_w[lane] = wi - w;
-        if (lane == nw - 1) s_w[16] = wi;
-    }
-    __syncthreads();
-    *total = s_w[16];
-    return inc - v + s_w[wid];
-}
-
-typedef int v4i __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
 // ATOMIC strategy: one pass, global u32 atomics (agent scope)
@@ -173,41 +75,6 @@ __global__ __launch_bounds__(256) void k_bin_atomic(const SegDesc seg, const LT 
 //   starts[c*(NT+1) + t].  The next chunk's events are prefetched into
 //   registers while the current chunk runs its LDS phases.
 // ---------------------------------------------------------------------------
-struct ChunkRegs {
-    int p[kPartEventsPerThread];
-    int t[kPartEventsPerThread];
-};
-
-__device__ __forceinline__ void load_chunk(const SegDesc *s_seg, int n_segs, long long c,
-                                           int pid_off, ChunkRegs &r) {
-    int s = 0;
-    while (s + 1 < n_segs && s_seg[s + 1].chunk0 <= c) ++s;
-    const SegDesc sd = s_seg[s];
-    const long long base = (c - sd.chunk0) * kChunk;
-    const bool vec = (((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0;
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int j = 0; j < kPartEventsPerThread / 4; ++j) {
-        const long long e0 = base + ((long long)j * kPartThreads + tid) * 4;
-        if (vec && e0 + 3 < sd.n) {
-            const v4i p = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.pid + e0));
-            const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.toa + e0));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                r.p[j * 4 + q] = p[q];
-                r.t[j * 4 + q] = t[q];
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const bool ok = e0 + q < sd.n;
-                r.p[j * 4 + q] = ok ? sd.pid[e0 + q] : pid_off - 1;  // outside the LUT: dropped
-                r.t[j * 4 + q] = ok ? sd.toa[e0 + q] : 0;
-            }
-        }
-    }
-}
-
 template <int TILE_BITS, typename LT, bool FAST, bool PEEL>
 __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_partition(
     const SegDesc *__restrict__ segs, int n_segs, long long c_begin, long long n_chunks,

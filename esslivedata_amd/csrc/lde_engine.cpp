@@ -90,12 +90,23 @@ struct lde_handle {
     uint32_t *d_ttot = nullptr, *d_tile_items = nullptr, *d_item_count = nullptr;
     uint2 *d_items = nullptr;
     long long items_cap = 0;
+    // PAGED workspace
+    uint16_t *d_pages = nullptr;
+    size_t pages_cap = 0;  // entries
+    uint32_t *d_page_tile = nullptr, *d_page_cnt = nullptr, *d_list = nullptr;
+    size_t page_meta_cap = 0;  // pages
+    uint32_t *d_pool_used = nullptr, *d_cntp = nullptr, *d_evp = nullptr;
+    uint32_t *d_tile_pages = nullptr, *d_tile_events = nullptr, *d_tile_base = nullptr;
+    uint32_t *d_overflow = nullptr;
+    uint4 *d_items4 = nullptr;
+    long long items4_cap = 0;
     lde::SegDesc *d_segs = nullptr, *h_segs = nullptr;
     long long segs_cap = 0;
     hipEvent_t segs_done = nullptr;
     bool segs_pending = false;
     long long item_events_override = 0;
     long long atomic_threshold = -1;
+    int auto_partition = LDE_STRATEGY_PAGED;
 
     // finalize scratch
     unsigned long long *d_tot4 = nullptr;
@@ -367,6 +378,121 @@ int ensure_partition_capacity(lde_handle *h, long long chunks, long long max_ite
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
 // ---- binning ---------------------------------------------------------------
+int upload_segments(lde_handle *h, const std::vector<lde::SegDesc> &sd) {
+    if (h->segs_pending) {
+        HIPCALL(h, hipEventSynchronize(h->segs_done));
+        h->segs_pending = false;
+    }
+    if ((long long)sd.size() > h->segs_cap) {
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        dev_free(h->d_segs);
+        if (h->h_segs) (void)hipHostFree(h->h_segs);
+        h->h_segs = nullptr;
+        h->segs_cap = 0;
+        const long long cap = std::max<long long>((long long)sd.size(), 256);
+        if (int rc = dev_alloc(h, &h->d_segs, (size_t)cap)) return rc;
+        HIPCALL(h, hipHostMalloc((void **)&h->h_segs, cap * sizeof(lde::SegDesc), hipHostMallocDefault));
+        h->segs_cap = cap;
+    }
+    std::memcpy(h->h_segs, sd.data(), sd.size() * sizeof(lde::SegDesc));
+    HIPCALL(h, hipMemcpyAsync(h->d_segs, h->h_segs, sd.size() * sizeof(lde::SegDesc),
+                              hipMemcpyHostToDevice, h->stream));
+    HIPCALL(h, hipEventRecord(h->segs_done, h->stream));
+    h->segs_pending = true;
+    return LDE_OK;
+}
+
+template <typename T>
+int grow(lde_handle *h, T **p, size_t &cap, size_t need) {
+    if (need <= cap && *p) return LDE_OK;
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    dev_free(*p);
+    const size_t n = std::max(need, cap * 2);
+    if (int rc = dev_alloc(h, p, n)) return rc;
+    cap = n;
+    return LDE_OK;
+}
+
+int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks,
+              long long total, const void *lut) {
+    const int grid = (int)std::min<long long>(chunks, (long long)h->part_grid);
+    const long long per_block = (chunks + grid - 1) / grid;
+    const int cap = (int)((per_block * lde::kChunk + lde::kPage - 1) / lde::kPage) + 2 * h->n_tiles;
+    const size_t pages = (size_t)grid * (size_t)cap;
+    if (pages > 0xffffffffULL) return fail(h, LDE_EINVAL, "batch too large for the page pool");
+    long long item_events = h->item_events_override > 0
+                                ? h->item_events_override
+                                : std::max<long long>(32768, (total + 2LL * h->cus - 1) / (2LL * h->cus));
+    if (item_events > 0x7fffffffLL) item_events = 0x7fffffffLL;
+    const long long max_items = (total + item_events - 1) / item_events + h->n_tiles;
+    if (int rc = grow(h, &h->d_pages, h->pages_cap, pages * lde::kPage)) return rc;
+    if (pages > h->page_meta_cap || !h->d_page_tile) {
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        const size_t n = std::max(pages, h->page_meta_cap * 2);
+        dev_free(h->d_page_tile);
+        dev_free(h->d_page_cnt);
+        dev_free(h->d_list);
+        h->page_meta_cap = 0;
+        if (int rc = dev_alloc(h, &h->d_page_tile, n)) return rc;
+        if (int rc = dev_alloc(h, &h->d_page_cnt, n)) return rc;
+        if (int rc = dev_alloc(h, &h->d_list, n)) return rc;
+        h->page_meta_cap = n;
+    }
+    if (!h->d_pool_used) {
+        const size_t rows = (size_t)h->part_rows;
+        if (int rc = dev_alloc(h, &h->d_pool_used, rows)) return rc;
+        if (int rc = dev_alloc(h, &h->d_cntp, rows * h->n_tiles)) return rc;
+        if (int rc = dev_alloc(h, &h->d_evp, rows * h->n_tiles)) return rc;
+        if (int rc = dev_alloc(h, &h->d_tile_pages, (size_t)h->n_tiles)) return rc;
+        if (int rc = dev_alloc(h, &h->d_tile_events, (size_t)h->n_tiles)) return rc;
+        if (int rc = dev_alloc(h, &h->d_tile_base, (size_t)h->n_tiles)) return rc;
+        if (int rc = dev_alloc(h, &h->d_overflow, 1)) return rc;
+        HIPCALL(h, hipMemsetAsync(h->d_overflow, 0, 4, h->stream));
+    }
+    size_t icap = (size_t)h->items4_cap;
+    if (int rc = grow(h, &h->d_items4, icap, (size_t)max_items)) return rc;
+    h->items4_cap = (long long)icap;
+    if (int rc = upload_segments(h, sd)) return rc;
+    lde::PagedArgs a;
+    a.tile_bits = h->tile_bits;
+    a.lut16 = h->lut16;
+    a.peel = h->peel;
+    a.segs = h->d_segs;
+    a.n_segs = (int)sd.size();
+    a.n_chunks = chunks;
+    a.lut = lut;
+    a.pid_off = h->pid_off;
+    a.L = (unsigned)h->L;
+    a.tab = h->d_tab;
+    a.tp = h->tp;
+    a.n_tiles = h->n_tiles;
+    a.pages = h->d_pages;
+    a.page_tile = h->d_page_tile;
+    a.page_cnt = h->d_page_cnt;
+    a.pool_used = h->d_pool_used;
+    a.cap = cap;
+    a.overflow = h->d_overflow;
+    a.grid = grid;
+    {
+        Timed tm(h, LDE_K_PAGED);
+        HIPCALL(h, lde::launch_paged_partition(a, h->stream));
+    }
+    {
+        Timed tm(h, LDE_K_PAGE_PLAN);
+        HIPCALL(h, lde::launch_page_plan(a, (uint32_t)item_events, h->d_cntp, h->d_evp,
+                                         h->d_tile_pages, h->d_tile_events, h->d_tile_base,
+                                         h->d_items4, h->d_item_count, (uint32_t)max_items,
+                                         h->d_list, h->stream));
+    }
+    {
+        Timed tm(h, LDE_K_PAGE_ACC);
+        HIPCALL(h, lde::launch_page_accumulate(h->tile_bits, a, h->d_list, h->d_items4,
+                                               h->d_item_count, h->d_win32, h->nbins,
+                                               (int)max_items, h->stream));
+    }
+    return LDE_OK;
+}
+
 int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long total, int replica) {
     const size_t lut_es = h->lut16 ? 2 : 4;
     const void *lut = h->monitor ? nullptr
@@ -389,9 +515,10 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
         const long long thr = h->atomic_threshold >= 0
                                   ? h->atomic_threshold
                                   : std::max<long long>(1 << 20, h->nbins / 2);
-        strat = (h->n_tiles > 0 && total >= thr) ? LDE_STRATEGY_PARTITION : LDE_STRATEGY_ATOMIC;
+        strat = (h->n_tiles > 0 && total >= thr) ? h->auto_partition : LDE_STRATEGY_ATOMIC;
     }
-    if (strat == LDE_STRATEGY_PARTITION && h->n_tiles == 0) strat = LDE_STRATEGY_ATOMIC;
+    if ((strat == LDE_STRATEGY_PARTITION || strat == LDE_STRATEGY_PAGED) && h->n_tiles == 0)
+        strat = LDE_STRATEGY_ATOMIC;
     h->last_strategy = strat;
     if (strat == LDE_STRATEGY_ATOMIC) {
         for (const Segment &s : segs) {
@@ -405,7 +532,7 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
         }
         return LDE_OK;
     }
-    // PARTITION
+    // PARTITION / PAGED
     long long chunks = 0;
     std::vector<lde::SegDesc> sd;
     for (const Segment &s : segs) {
@@ -414,33 +541,14 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
         chunks += (s.n + lde::kChunk - 1) / lde::kChunk;
     }
     if (chunks == 0) return LDE_OK;
+    if (strat == LDE_STRATEGY_PAGED) return bin_paged(h, sd, chunks, total, lut);
     long long item_events = h->item_events_override > 0
                                 ? h->item_events_override
                                 : std::max<long long>(32768, (total + 2LL * h->cus - 1) / (2LL * h->cus));
     if (item_events > 0x7fffffffLL) item_events = 0x7fffffffLL;
     const long long max_items = (total + item_events - 1) / item_events + h->n_tiles;
     if (int rc = ensure_partition_capacity(h, chunks, max_items)) return rc;
-    // segment table -> device (pinned staging, reused once the previous copy landed)
-    if (h->segs_pending) {
-        HIPCALL(h, hipEventSynchronize(h->segs_done));
-        h->segs_pending = false;
-    }
-    if ((long long)sd.size() > h->segs_cap) {
-        HIPCALL(h, hipStreamSynchronize(h->stream));
-        dev_free(h->d_segs);
-        if (h->h_segs) (void)hipHostFree(h->h_segs);
-        h->h_segs = nullptr;
-        h->segs_cap = 0;
-        const long long cap = std::max<long long>((long long)sd.size(), 256);
-        if (int rc = dev_alloc(h, &h->d_segs, (size_t)cap)) return rc;
-        HIPCALL(h, hipHostMalloc((void **)&h->h_segs, cap * sizeof(lde::SegDesc), hipHostMallocDefault));
-        h->segs_cap = cap;
-    }
-    std::memcpy(h->h_segs, sd.data(), sd.size() * sizeof(lde::SegDesc));
-    HIPCALL(h, hipMemcpyAsync(h->d_segs, h->h_segs, sd.size() * sizeof(lde::SegDesc),
-                              hipMemcpyHostToDevice, h->stream));
-    HIPCALL(h, hipEventRecord(h->segs_done, h->stream));
-    h->segs_pending = true;
+    if (int rc = upload_segments(h, sd)) return rc;
     const int grid_a = (int)std::min<long long>(chunks, (long long)h->part_grid);
     HIPCALL(h, hipMemsetAsync(h->d_part, 0, (size_t)grid_a * h->n_tiles * 4, h->stream));
     for (size_t s0 = 0; s0 < sd.size(); s0 += lde::kMaxSegs) {
@@ -548,6 +656,18 @@ void release(lde_handle *h) {
     dev_free(h->d_segs);
     if (h->h_segs) (void)hipHostFree(h->h_segs);
     if (h->segs_done) (void)hipEventDestroy(h->segs_done);
+    dev_free(h->d_pages);
+    dev_free(h->d_page_tile);
+    dev_free(h->d_page_cnt);
+    dev_free(h->d_list);
+    dev_free(h->d_pool_used);
+    dev_free(h->d_cntp);
+    dev_free(h->d_evp);
+    dev_free(h->d_tile_pages);
+    dev_free(h->d_tile_events);
+    dev_free(h->d_tile_base);
+    dev_free(h->d_overflow);
+    dev_free(h->d_items4);
     dev_free(h->d_tot4);
     dev_free(h->d_img_cur);
     dev_free(h->d_img_cum);
@@ -698,7 +818,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         tb = std::max(13, std::min(tb, 15));
         while (tb < 15 && (nbins + (1LL << tb) - 1) >> tb > lde::kMaxTiles) ++tb;
         const long long nt = (nbins + (1LL << tb) - 1) >> tb;
-        const bool smem_ok = lde::partition_smem((int)nt, h->tp) <= 64 * 1024;
+        const bool smem_ok = lde::partition_smem((int)nt, h->tp) <= 64 * 1024 &&
+                             lde::paged_smem((int)nt, h->tp) <= 64 * 1024;
         if (nt <= lde::kMaxTiles && smem_ok) {
             h->tile_bits = tb;
             h->n_tiles = (int)nt;
@@ -714,6 +835,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         }
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);
+        h->auto_partition = (int)env_ll("LDE_AUTO_PARTITION", LDE_STRATEGY_PAGED);
     }
     CREATE_HIP(hipEventCreateWithFlags(&h->pin_done, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&h->segs_done, hipEventDisableTiming));
@@ -894,7 +1016,11 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
         convert_u64(tmp.data(), out->cumulative_hist, (long long)nb, LDE_F64);
     }
     if (f32) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
+    uint32_t ovf = 0;
+    if (h->d_overflow)
+        HIPCALL(h, hipMemcpyAsync(&ovf, h->d_overflow, 4, hipMemcpyDeviceToHost, h->stream));
     HIPCALL(h, hipStreamSynchronize(h->stream));
+    if (ovf) return fail(h, LDE_ESTATE, "page pool overflow (internal error)");
     for (int q = 0; q < 4; ++q) out->totals[q] = tot[q];
     h->window_has_data = false;
     h->win64_dirty = false;

@@ -17,6 +17,8 @@ constexpr int kMaxBuckets = 4096;                  // TOA bucket table (general 
 constexpr int kMaxFastBuckets = 16384;             // TOA bucket table (fast layout)
 constexpr int kMaxSegs = 64;                       // segments per pass-A launch
 constexpr int kLaneModeRun = 48;                   // pass B: lane-per-chunk below this avg run
+constexpr int kPageBits = 10;                      // PAGED strategy: 1024-entry (2 KB) pages
+constexpr int kPage = 1 << kPageBits;
 
 struct SegDesc {  // one staged ev44 message (device pointers)
     const int *pid;
@@ -76,6 +78,37 @@ hipError_t launch_bin_atomic(const SegDesc &seg, const void *lut, bool lut16, in
                              unsigned L, const unsigned char *tab, const ToaParams &tp,
                              uint32_t *hist, int grid, hipStream_t st);
 hipError_t launch_partition(const PartitionArgs &a, hipStream_t st);
+struct PagedArgs {
+    int tile_bits;
+    bool lut16;
+    bool peel;
+    const SegDesc *segs;  // device segment table (all staged segments)
+    int n_segs;
+    long long n_chunks;
+    const void *lut;
+    int pid_off;
+    unsigned L;
+    const unsigned char *tab;
+    ToaParams tp;
+    int n_tiles;
+    uint16_t *pages;
+    uint32_t *page_tile;
+    uint32_t *page_cnt;
+    uint32_t *pool_used;
+    int cap;  // pages per block pool
+    uint32_t *overflow;
+    int grid;
+};
+
+size_t paged_smem(int n_tiles, const ToaParams &tp);
+hipError_t launch_paged_partition(const PagedArgs &a, hipStream_t st);
+hipError_t launch_page_plan(const PagedArgs &a, uint32_t item_events, uint32_t *cntp,
+                            uint32_t *evp, uint32_t *tile_pages, uint32_t *tile_events,
+                            uint32_t *tile_base, uint4 *items, uint32_t *item_count,
+                            uint32_t max_items, uint32_t *list, hipStream_t st);
+hipError_t launch_page_accumulate(int tile_bits, const PagedArgs &a, const uint32_t *list,
+                                  const uint4 *items, const uint32_t *item_count, uint32_t *hist,
+                                  long long n_bins, int grid, hipStream_t st);
 hipError_t launch_plan(const uint32_t *part, int part_rows, int n_tiles, long long n_chunks,
                        uint32_t item_events, uint32_t *totals, uint32_t *tile_items, uint2 *items,
                        uint32_t *item_count, uint32_t max_items, hipStream_t st);

@@ -51,7 +51,8 @@ extern "C" {
 /* binning strategies (LDE_AUTO lets the engine choose per batch) */
 #define LDE_STRATEGY_AUTO 0
 #define LDE_STRATEGY_ATOMIC 1      /* one pass, global atomics             */
-#define LDE_STRATEGY_PARTITION 2   /* tile partition + LDS sub-histograms  */
+#define LDE_STRATEGY_PARTITION 2   /* tile partition (chunk-major runs) + LDS sub-histograms */
+#define LDE_STRATEGY_PAGED 3       /* tile partition into per-block page chains + LDS sub-histograms */
 
 /* histogram selectors for lde_read_histogram */
 #define LDE_CURRENT 0    /* window since the last finalize  (accumulators.py:138-163) */
@@ -155,7 +156,10 @@ int lde_synchronize(lde_handle *h);
 #define LDE_K_MONITOR 4   /* k_monitor: 1-D TOA histogram                    */
 #define LDE_K_FINALIZE 5  /* k_finalize / merge kernels                      */
 #define LDE_K_BINNING 6   /* whole binning sequence of one accumulate        */
-#define LDE_K_COUNT 7
+#define LDE_K_PAGED 7     /* k_paged_partition: PAGED pass A                  */
+#define LDE_K_PAGE_PLAN 8 /* k_page_count/scan/plan/scatter                   */
+#define LDE_K_PAGE_ACC 9  /* k_page_accumulate: PAGED pass B                  */
+#define LDE_K_COUNT 10
 int lde_timing_enable(lde_handle *h, int32_t enable);
 int lde_kernel_stats(lde_handle *h, int32_t kernel_id, double *ms, int64_t *launches);
 

@@ -11,7 +11,7 @@ from oracle import scipp_semantics as ora
 
 pytestmark = pytest.mark.gpu
 
-STRATEGIES = ['atomic', 'partition']
+STRATEGIES = ['atomic', 'partition', 'paged']
 
 # internal kernel variants that must all be bit-identical
 VARIANTS = [

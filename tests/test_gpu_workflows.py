@@ -168,7 +168,7 @@ def test_golden_regression_vector_on_gpu():
     g = np.load(GOLDEN / 'dream_small.npz')
     inst = synthetic.dream_mantle()
     view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
-    for strategy in ('atomic', 'partition'):
+    for strategy in ('atomic', 'partition', 'paged'):
         eng = BinningEngine(toa_edges_ns=inst.edges.edges_ns(), out_lut=view.lut,
                             pid_offset=view.pid_offset, n_screen=view.n_screen, strategy=strategy)
         eng.stage(g['pid'], g['toa'])

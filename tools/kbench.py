@@ -46,7 +46,7 @@ def run(workload, strategy, env, pulses=14, n_pulse=10_000_000, reps=5, check=No
         step(i)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
-    st = {k: eng.kernel_stats(k) for k in ('atomic', 'partition', 'plan', 'tile_accumulate', 'binning')}
+    st = {k: eng.kernel_stats(k) for k in ('atomic', 'partition', 'plan', 'tile_accumulate', 'paged', 'page_plan', 'page_accumulate', 'binning')}
     eng.close()
     for k in env:
         del os.environ[k]
@@ -65,12 +65,13 @@ if __name__ == '__main__':
     if mode == 'prof':  # one config for rocprof
         run(sys.argv[2] if len(sys.argv) > 2 else 'dream', 'partition', {}, reps=3)
         sys.exit(0)
-    variants = [dict(LDE_TILE_BITS=14), dict(LDE_TILE_BITS=15)]
-    ablations = [dict(LDE_ABLATE=a) for a in (1, 2, 3, 4, 8, 12, 15)]
+    variants = [dict(LDE_TILE_BITS=14), dict(LDE_TILE_BITS=15), dict(LDE_PEEL=0)]
+    ablations = [dict(LDE_ABLATE=a) for a in (1, 3, 4, 8, 15)]
     for wl in ('dream', 'loki'):
         base = run(wl, 'partition', {})
         for v in variants:
-            run(wl, 'partition', v, check=base)
+            run(wl, 'paged', v, check=base)
+        run(wl, 'paged', {}, check=base)
         for v in ablations:
             run(wl, 'partition', v)
         run(wl, 'atomic', {}, reps=1, pulses=14, check=base)
