@@ -105,24 +105,24 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_partition(
     if (c_begin + blockIdx.x < n_chunks)
         load_chunk(s_seg, n_segs, c_begin + blockIdx.x, pid_off, nxt);
     for (long long c = c_begin + blockIdx.x; c < n_chunks; c += gridDim.x) {
-        const ChunkRegs cur = nxt;
-        if (c + gridDim.x < n_chunks) load_chunk(s_seg, n_segs, c + gridDim.x, pid_off, nxt);
         int key[EPT];
         uint32_t rank[EPT];
         if (tp.pad == 0) {
 #pragma unroll
             for (int e = 0; e < EPT; ++e)
-                key[e] = event_key<LT, FAST>(cur.p[e], cur.t[e], lut, pid_off, L, s_tab, tp);
+                key[e] = event_key<LT, FAST>(nxt.p[e], nxt.t[e], lut, pid_off, L, s_tab, tp);
         } else {  // LDE_ABLATE diagnostics: timing only, results are wrong by design
 #pragma unroll
             for (int e = 0; e < EPT; ++e) {
-                const unsigned p = (unsigned)cur.p[e] - (unsigned)pid_off;
+                const unsigned p = (unsigned)nxt.p[e] - (unsigned)pid_off;
                 const int base = (tp.pad & 1) ? (int)((p & 16383u) * (unsigned)tp.T)
                                               : (p < L ? lut_base(lut, p, tp.T) : -1);
-                const int b = (tp.pad & 2) ? (int)((unsigned)cur.t[e] & 63u) : toa_bin<FAST>(cur.t[e], s_tab, tp);
+                const int b = (tp.pad & 2) ? (int)((unsigned)nxt.t[e] & 63u) : toa_bin<FAST>(nxt.t[e], s_tab, tp);
                 key[e] = (p >= L || base < 0 || b < 0) ? -1 : base + b;
             }
         }
+        // the next chunk's events load while this chunk runs its LDS phases
+        if (c + gridDim.x < n_chunks) load_chunk(s_seg, n_segs, c + gridDim.x, pid_off, nxt);
         // ---- rank inside tile: LDS returning atomics; with PEEL the most
         // common tile of the wave (sampled lane) is ranked with one atomic
 #pragma unroll

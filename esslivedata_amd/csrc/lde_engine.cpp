@@ -63,6 +63,7 @@ struct lde_handle {
     bool lut16 = false;
     unsigned char *d_tab = nullptr;
     bool peel = true;
+    int subc = 4;
 
     uint32_t *d_win32 = nullptr;
     unsigned long long *d_win64 = nullptr;
@@ -456,7 +457,7 @@ int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     lde::PagedArgs a;
     a.tile_bits = h->tile_bits;
     a.lut16 = h->lut16;
-    a.peel = h->peel;
+    a.subc = h->subc;
     a.segs = h->d_segs;
     a.n_segs = (int)sd.size();
     a.n_chunks = chunks;
@@ -797,7 +798,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     }
     CREATE_CHECK(dev_alloc(h, &h->d_tab, tab.size()));
     CREATE_HIP(hipMemcpy(h->d_tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
-    h->peel = env_ll("LDE_PEEL", 1) != 0;
+    h->peel = env_ll("LDE_PEEL", 0) != 0;
 
     // histograms
     CREATE_CHECK(dev_alloc(h, &h->d_win32, (size_t)nbins));
@@ -819,7 +820,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         while (tb < 15 && (nbins + (1LL << tb) - 1) >> tb > lde::kMaxTiles) ++tb;
         const long long nt = (nbins + (1LL << tb) - 1) >> tb;
         const bool smem_ok = lde::partition_smem((int)nt, h->tp) <= 64 * 1024 &&
-                             lde::paged_smem((int)nt, h->tp) <= 64 * 1024;
+                             lde::paged_smem((int)nt, 1, h->tp) <= 64 * 1024;
+        h->subc = (env_ll("LDE_SUBC", 4) == 4 && lde::paged_smem((int)nt, 4, h->tp) <= 64 * 1024) ? 4 : 1;
         if (nt <= lde::kMaxTiles && smem_ok) {
             h->tile_bits = tb;
             h->n_tiles = (int)nt;

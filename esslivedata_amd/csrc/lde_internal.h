@@ -81,7 +81,7 @@ hipError_t launch_partition(const PartitionArgs &a, hipStream_t st);
 struct PagedArgs {
     int tile_bits;
     bool lut16;
-    bool peel;
+    int subc;  // LDS rank sub-counters per tile (1 or 4)
     const SegDesc *segs;  // device segment table (all staged segments)
     int n_segs;
     long long n_chunks;
@@ -100,7 +100,7 @@ struct PagedArgs {
     int grid;
 };
 
-size_t paged_smem(int n_tiles, const ToaParams &tp);
+size_t paged_smem(int n_tiles, int subc, const ToaParams &tp);
 hipError_t launch_paged_partition(const PagedArgs &a, hipStream_t st);
 hipError_t launch_page_plan(const PagedArgs &a, uint32_t item_events, uint32_t *cntp,
                             uint32_t *evp, uint32_t *tile_pages, uint32_t *tile_events,

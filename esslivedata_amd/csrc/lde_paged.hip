@@ -56,12 +56,15 @@ __device__ __forceinline__ void load_chunk_global(const SegDesc *__restrict__ se
     }
 }
 
-size_t paged_smem(int n_tiles, const ToaParams &tp) {
-    return (size_t)kChunk * 4 + 4 * ((size_t)align4(n_tiles + 1) + 3 * (size_t)align4(n_tiles) + 36) +
+// staging holds every tile run padded to a multiple of 8 entries (sentinel
+// 0xFFFF offsets), so runs start 16-byte aligned in LDS and in their pages
+size_t paged_smem(int n_tiles, int subc, const ToaParams &tp) {
+    return 4 * ((size_t)kChunk + 8 * (size_t)n_tiles) +
+           4 * ((size_t)align4(n_tiles * subc + 1) + 4 * (size_t)align4(n_tiles) + 36) +
            toa_lds_bytes(tp);
 }
 
-template <int TILE_BITS, typename LT, bool FAST, bool PEEL>
+template <int TILE_BITS, typename LT, bool FAST, int SUBC>
 __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_partition(
     const SegDesc *__restrict__ segs, int n_segs, long long n_chunks, const LT *__restrict__ lut,
     int pid_off, unsigned L, const unsigned char *__restrict__ g_tab, ToaParams tp, int n_tiles,
@@ -71,83 +74,79 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_part
     constexpr int TPT = kMaxTiles / kPartThreads;
     constexpr uint32_t MASK = (1u << TILE_BITS) - 1u;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // LDS carve: staging (tile<<16 | offset) | counts/starts | fill | cur | new | scan | pool | TOA
+    // LDS carve: staging (tile<<16 | offset) | sub-counters/starts | fill | cur | new | scan | pool | TOA
     uint32_t *s_stg = reinterpret_cast<uint32_t *>(smem);
-    uint32_t *s_cnt = s_stg + kChunk;
-    uint32_t *s_fill = s_cnt + align4(n_tiles + 1);
+    uint32_t *s_cnt = s_stg + kChunk + 8 * n_tiles;
+    uint32_t *s_fill = s_cnt + align4(n_tiles * SUBC + 1);
     uint32_t *s_cur = s_fill + align4(n_tiles);
     uint32_t *s_new = s_cur + align4(n_tiles);
-    uint32_t *s_w = s_new + align4(n_tiles);
+    uint32_t *s_loc = s_new + align4(n_tiles);
+    uint32_t *s_w = s_loc + align4(n_tiles);
     uint32_t *s_pool = s_w + 32;
     unsigned char *s_tab = reinterpret_cast<unsigned char *>(s_pool + 4);
     const uint32_t pool_base = (uint32_t)blockIdx.x * (uint32_t)cap;
     load_toa_tables(s_tab, g_tab, tp);
+    for (int i = threadIdx.x; i < n_tiles * SUBC; i += blockDim.x) s_cnt[i] = 0;
     for (int t = threadIdx.x; t < n_tiles; t += blockDim.x) {
-        s_cnt[t] = 0;
         s_fill[t] = 0;
         s_cur[t] = pool_base + t;  // first page of every tile, pre-assigned
         s_new[t] = 0;
         page_tile[pool_base + t] = (uint32_t)t;
     }
-    if (threadIdx.x == 0) {
-        s_cnt[n_tiles] = 0;
-        s_pool[0] = (uint32_t)n_tiles;
-    }
+    if (threadIdx.x == 0) s_pool[0] = (uint32_t)n_tiles;
     __syncthreads();
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    const int sub = lane & (SUBC - 1);
     ChunkRegs nxt;
     if ((long long)blockIdx.x < n_chunks) load_chunk_global(segs, n_segs, blockIdx.x, pid_off, nxt);
     for (long long c = blockIdx.x; c < n_chunks; c += gridDim.x) {
-        const ChunkRegs cur = nxt;
-        if (c + gridDim.x < n_chunks) load_chunk_global(segs, n_segs, c + gridDim.x, pid_off, nxt);
         int key[EPT];
         uint32_t rank[EPT];
 #pragma unroll
         for (int e = 0; e < EPT; ++e)
-            key[e] = event_key<LT, FAST>(cur.p[e], cur.t[e], lut, pid_off, L, s_tab, tp);
+            key[e] = event_key<LT, FAST>(nxt.p[e], nxt.t[e], lut, pid_off, L, s_tab, tp);
+        // the next chunk's events load while this chunk runs its LDS phases
+        if (c + gridDim.x < n_chunks) load_chunk_global(segs, n_segs, c + gridDim.x, pid_off, nxt);
+        // ---- rank inside (tile, sub-counter): SUBC counters per tile spread a hot
+        // tile's same-address LDS atomics over SUBC banks
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
-            const int tile = key[e] >= 0 ? (key[e] >> TILE_BITS) : -1;
             rank[e] = 0;
-            if (PEEL) {
-                const int lead = __builtin_amdgcn_readlane(tile, (e * 5) & 63);
-                const unsigned long long m = __ballot(tile == lead);
-                if (lead >= 0) {
-                    const int first = __builtin_ctzll(m);
-                    uint32_t base = 0;
-                    if (lane == first) base = atomicAdd(&s_cnt[lead], (uint32_t)__popcll(m));
-                    base = __builtin_amdgcn_readlane(base, first);
-                    if (tile == lead) rank[e] = base + lanes_below(m);
-                }
-                if (tile >= 0 && tile != lead) rank[e] = atomicAdd(&s_cnt[tile], 1u);
-            } else if (tile >= 0) {
-                rank[e] = atomicAdd(&s_cnt[tile], 1u);
-            }
+            if (key[e] >= 0) rank[e] = atomicAdd(&s_cnt[(key[e] >> TILE_BITS) * SUBC + sub], 1u);
         }
         __syncthreads();
-        // ---- scan of tile counts + page allocation for the owned tiles
-        uint32_t loc[TPT];
+        // ---- scan of padded tile totals, sub-run starts, padding, page allocation
+        // (thread tid owns tiles [tid*TPT, tid*TPT + TPT))
         uint32_t sum = 0;
         const int t0 = tid * TPT;
+        for (int t = t0; t < t0 + TPT && t < n_tiles; ++t) {
+            uint32_t n = 0;
 #pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-            const int t = t0 + q;
-            loc[q] = t < n_tiles ? s_cnt[t] : 0u;
-            sum += loc[q];
+            for (int s2 = 0; s2 < SUBC; ++s2) n += s_cnt[t * SUBC + s2];
+            s_loc[t] = n;
+            sum += (n + 7u) & ~7u;
         }
         uint32_t total;
         uint32_t run = block_exclusive_scan(sum, s_w, &total);
+        for (int t = t0; t < t0 + TPT && t < n_tiles; ++t) {
+            const uint32_t n_t = s_loc[t];
+            const uint32_t padded = (n_t + 7u) & ~7u;
+            if (n_t > 0) {
+                uint32_t st = run;
 #pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-            const int t = t0 + q;
-            if (t < n_tiles) {
-                s_cnt[t] = run;
+                for (int s2 = 0; s2 < SUBC; ++s2) {
+                    const uint32_t n = s_cnt[t * SUBC + s2];
+                    s_cnt[t * SUBC + s2] = st;
+                    st += n;
+                }
+                for (uint32_t k = run + n_t; k < run + padded; ++k)
+                    s_stg[k] = ((uint32_t)t << 16) | 0xFFFFu;  // sentinel padding
                 const uint32_t fill = s_fill[t];
                 const uint32_t room = (uint32_t)kPage - fill;
-                if (loc[q] > room) {
-                    const uint32_t n_new = (loc[q] - room + kPage - 1) >> kPageBits;
+                if (padded > room) {
+                    const uint32_t n_new = (padded - room + kPage - 1) >> kPageBits;
                     const uint32_t off = atomicAdd(s_pool, n_new);
                     if (off + n_new > (uint32_t)cap) {  // cannot happen by construction
                         atomicOr(overflow, 1u);
@@ -163,40 +162,46 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_part
                     }
                 }
             }
-            run += loc[q];
+            run += padded;
         }
         __syncthreads();
-        // ---- scatter into LDS staging (tile-sorted), tile id kept beside the offset
+        // ---- scatter into LDS staging (tile-sorted), tile id beside the offset
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
             if (key[e] >= 0) {
                 const uint32_t t = (uint32_t)key[e] >> TILE_BITS;
-                s_stg[s_cnt[t] + rank[e]] = (t << 16) | ((uint32_t)key[e] & MASK);
+                s_stg[s_cnt[t * SUBC + sub] + rank[e]] = (t << 16) | ((uint32_t)key[e] & MASK);
             }
         }
         __syncthreads();
-        // ---- write-out into the page chains (consecutive lanes -> consecutive entries)
-        for (int i = tid; i < (int)total; i += kPartThreads) {
-            const uint32_t v = s_stg[i];
-            const uint32_t t = v >> 16;
-            const uint32_t pos = s_fill[t] + ((uint32_t)i - s_cnt[t]);
+        // ---- write-out: one 16-byte store per 8-entry group (runs are 8-aligned)
+        for (uint32_t g = (uint32_t)tid * 8u; g < total; g += kPartThreads * 8u) {
+            const uint4 v0 = *reinterpret_cast<const uint4 *>(s_stg + g);
+            const uint4 v1 = *reinterpret_cast<const uint4 *>(s_stg + g + 4);
+            const uint32_t t = v0.x >> 16;
+            const uint32_t pos = s_fill[t] + (g - s_cnt[t * SUBC]);
             const uint32_t k = pos >> kPageBits;
             const uint32_t page = k == 0 ? s_cur[t] : s_new[t] + k - 1;
+            uint4 w;
+            w.x = (v0.x & 0xFFFFu) | (v0.y << 16);
+            w.y = (v0.z & 0xFFFFu) | (v0.w << 16);
+            w.z = (v1.x & 0xFFFFu) | (v1.y << 16);
+            w.w = (v1.z & 0xFFFFu) | (v1.w << 16);
             if (page - pool_base < (uint32_t)cap)  // always true unless the pool overflowed
-                pages[(size_t)page * kPage + (pos & (kPage - 1))] = (uint16_t)(v & 0xFFFFu);
+                *reinterpret_cast<uint4 *>(pages + (size_t)page * kPage + (pos & (kPage - 1))) = w;
         }
         __syncthreads();
-        // ---- advance the open page of the owned tiles
-#pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-            const int t = t0 + q;
-            if (t < n_tiles && loc[q] > 0) {
-                const uint32_t end = s_fill[t] + loc[q];
+        // ---- advance the open page of the owned tiles, reset the counters
+        for (int t = t0; t < t0 + TPT && t < n_tiles; ++t) {
+            const uint32_t n_t = s_loc[t];
+            if (n_t > 0) {
+                const uint32_t end = s_fill[t] + ((n_t + 7u) & ~7u);
                 const uint32_t k_end = (end - 1) >> kPageBits;
                 if (k_end > 0) s_cur[t] = s_new[t] + k_end - 1;
                 s_fill[t] = end - (k_end << kPageBits);
             }
-            if (t < n_tiles) s_cnt[t] = 0;
+#pragma unroll
+            for (int s2 = 0; s2 < SUBC; ++s2) s_cnt[t * SUBC + s2] = 0;
         }
         __syncthreads();
     }
@@ -370,15 +375,10 @@ __global__ __launch_bounds__(kTileThreads) void k_page_accumulate(
             if (e0 + 8u < ncnt) nb = src[1];
         }
         const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        if (e0 + 16u <= cnt) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                atomicAdd(&s_tile[(w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu], 1u);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 16; ++q)
-                if (e0 + (uint32_t)q < cnt)
-                    atomicAdd(&s_tile[(w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu], 1u);
+        for (int q = 0; q < 16; ++q) {
+            const uint32_t v = (w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu;
+            if (e0 + (uint32_t)q < cnt && v != 0xFFFFu) atomicAdd(&s_tile[v], 1u);
         }
         idx = nidx;
         page = npage;
@@ -397,12 +397,12 @@ __global__ __launch_bounds__(kTileThreads) void k_page_accumulate(
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
-template <int TB, typename LT, bool FAST, bool PEEL>
+template <int TB, typename LT, bool FAST, int SUBC>
 static hipError_t launch_paged_t(const PagedArgs &a, const LT *lut, hipStream_t st) {
-    const size_t sm = paged_smem(a.n_tiles, a.tp);
-    (void)hipFuncSetAttribute((const void *)k_paged_partition<TB, LT, FAST, PEEL>,
+    const size_t sm = paged_smem(a.n_tiles, SUBC, a.tp);
+    (void)hipFuncSetAttribute((const void *)k_paged_partition<TB, LT, FAST, SUBC>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipLaunchKernelGGL((k_paged_partition<TB, LT, FAST, PEEL>), dim3(a.grid), dim3(kPartThreads),
+    hipLaunchKernelGGL((k_paged_partition<TB, LT, FAST, SUBC>), dim3(a.grid), dim3(kPartThreads),
                        sm, st, a.segs, a.n_segs, a.n_chunks, lut, a.pid_off, a.L, a.tab, a.tp,
                        a.n_tiles, a.pages, a.page_tile, a.page_cnt, a.pool_used, a.cap, a.overflow);
     return hipGetLastError();
@@ -411,10 +411,10 @@ static hipError_t launch_paged_t(const PagedArgs &a, const LT *lut, hipStream_t 
 template <int TB, typename LT>
 static hipError_t launch_paged_tl(const PagedArgs &a, const LT *lut, hipStream_t st) {
     if (a.tp.fast)
-        return a.peel ? launch_paged_t<TB, LT, true, true>(a, lut, st)
-                      : launch_paged_t<TB, LT, true, false>(a, lut, st);
-    return a.peel ? launch_paged_t<TB, LT, false, true>(a, lut, st)
-                  : launch_paged_t<TB, LT, false, false>(a, lut, st);
+        return a.subc == 4 ? launch_paged_t<TB, LT, true, 4>(a, lut, st)
+                           : launch_paged_t<TB, LT, true, 1>(a, lut, st);
+    return a.subc == 4 ? launch_paged_t<TB, LT, false, 4>(a, lut, st)
+                       : launch_paged_t<TB, LT, false, 1>(a, lut, st);
 }
 
 template <int TB>

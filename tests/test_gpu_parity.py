@@ -18,7 +18,8 @@ VARIANTS = [
     {},
     {'LDE_LUT32': '1'},
     {'LDE_TOA_GENERAL': '1'},
-    {'LDE_PEEL': '0'},
+    {'LDE_PEEL': '1'},
+    {'LDE_SUBC': '1'},
     {'LDE_TILE_BITS': '15', 'LDE_PART_GRID': '7'},
 ]
 

@@ -65,8 +65,8 @@ if __name__ == '__main__':
     if mode == 'prof':  # one config for rocprof
         run(sys.argv[2] if len(sys.argv) > 2 else 'dream', 'partition', {}, reps=3)
         sys.exit(0)
-    variants = [dict(LDE_TILE_BITS=14), dict(LDE_TILE_BITS=15), dict(LDE_PEEL=0)]
-    ablations = [dict(LDE_ABLATE=a) for a in (1, 3, 4, 8, 15)]
+    variants = [dict(LDE_TILE_BITS=14), dict(LDE_SUBC=1), dict(LDE_PART_GRID=1024)]
+    ablations = []
     for wl in ('dream', 'loki'):
         base = run(wl, 'partition', {})
         for v in variants:
