@@ -28,6 +28,15 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+PROFILE_ROUND = 'r1'  # profiles/<round>_<workload>_bench.json (tools/prof_round.sh)
+# bench kernel name -> device symbol in the rocprofv3 summary
+KERNEL_SYMBOL = {
+    'atomic': 'k_bin_atomic',
+    'partition': 'k_partition',
+    'tile_accumulate': 'k_tile_accumulate',
+    'paged': 'k_paged_partition',
+    'page_accumulate': 'k_page_accumulate',
+}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_EVENT = 8  # int32 pixel_id + int32 time_of_flight
 
@@ -40,7 +49,7 @@ def parse():
     ap.add_argument('--workload', default='dream', choices=['dream', 'loki'])
     ap.add_argument('--pulses', type=int, default=14)
     ap.add_argument('--events-per-pulse', type=int, default=10_000_000)
-    ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition'])
+    ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition', 'paged'])
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     return ap.parse_args()
@@ -91,6 +100,25 @@ def cpu_baseline(inst, pixel_screen, seconds: float) -> dict:
         f'{t_total:.1f} s; NumPy oracle (1 core): {2 * n / t_np:.3e} events/s',
         'numpy_1core': 2 * n / t_np,
     }
+
+
+def profiled_traffic(workload: str, kernel: str, events_per_launch: float):
+    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC
+    summary of this same bench command (2 x FETCH_SIZE + WRITE_SIZE, the gfx950
+    correction of MI355X_MICROARCH.md), or None when no profile is committed."""
+    path = ROOT / 'profiles' / f'{PROFILE_ROUND}_{workload}_bench.json'
+    try:
+        prof = json.loads(path.read_text())
+        e = prof[KERNEL_SYMBOL[kernel]]
+        return {
+            'bytes': e['hbm_traffic_bytes'],
+            'read': e['hbm_read_bytes'],
+            'write': e['hbm_write_bytes'],
+            'profiled_avg_ms': e['avg_ms'],
+            'source': str(path.relative_to(ROOT)),
+        }
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def main():
@@ -168,22 +196,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    stats = {k: eng.kernel_stats(k) for k in ('atomic', 'partition', 'tile_accumulate', 'plan', 'binning', 'finalize')}
+    stats = {
+        k: eng.kernel_stats(k)
+        for k in ('atomic', 'partition', 'tile_accumulate', 'plan', 'paged', 'page_plan',
+                  'page_accumulate', 'binning', 'finalize')
+    }
     info = eng.info()
     total_events = n_step * args.steps * world
     value = total_events / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
     # dominant kernel and its roofline (algorithmic bytes per launch / avg duration)
-    dom = max(('atomic', 'partition', 'tile_accumulate'), key=lambda k: stats[k][0])
+    dom = max(('atomic', 'partition', 'tile_accumulate', 'paged', 'page_accumulate'), key=lambda k: stats[k][0])
     ms, launches = stats[dom]
     # every binning kernel processes all events of the timed steps across its launches
     events_per_launch = n_step * args.steps / max(launches, 1)
     alg_bytes = BYTES_PER_EVENT * events_per_launch
-    if dom == 'tile_accumulate':
-        alg_bytes += 4 * nbins * args.steps / max(launches, 1)  # window written once per batch
+    if dom in ('tile_accumulate', 'page_accumulate'):
+        # pass B reads one 16-bit tile-local key per event and writes the window once per batch
+        alg_bytes = 2 * events_per_launch + 4 * nbins * args.steps / max(launches, 1)
     avg_s = (ms / max(launches, 1)) / 1e3
     achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
+    traffic = profiled_traffic(args.workload, dom, events_per_launch)
     bin_ms, bin_n = stats['binning']
     pipeline_gbs = BYTES_PER_EVENT * n_step / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0
 
@@ -220,7 +254,8 @@ def main():
             'peak': HBM_PEAK_GBS,
             'unit': 'GB/s',
             'frac': achieved / HBM_PEAK_GBS,
-            'traffic': None,
+            'traffic': traffic['bytes'] if traffic else None,
+            'traffic_detail': traffic,
             'avg_launch_ms': ms / max(launches, 1),
             'launches': launches,
             'pipeline_achieved': pipeline_gbs,

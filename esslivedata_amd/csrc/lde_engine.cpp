@@ -418,7 +418,7 @@ int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
               long long total, const void *lut) {
     const int grid = (int)std::min<long long>(chunks, (long long)h->part_grid);
     const long long per_block = (chunks + grid - 1) / grid;
-    const int cap = (int)((per_block * lde::kChunk + lde::kPage - 1) / lde::kPage) + 2 * h->n_tiles;
+    const int cap = (int)((per_block * lde::kChunk + lde::kPage - 1) / lde::kPage) + 2 * h->n_tiles + 2;
     const size_t pages = (size_t)grid * (size_t)cap;
     if (pages > 0xffffffffULL) return fail(h, LDE_EINVAL, "batch too large for the page pool");
     long long item_events = h->item_events_override > 0
@@ -815,13 +815,19 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
 
     // partition workspace: choose the smallest tile that keeps <= kMaxTiles tiles
     if (!monitor) {
-        int tb = (int)env_ll("LDE_TILE_BITS", 13);
+        int tb = (int)env_ll("LDE_TILE_BITS", 14);
         tb = std::max(13, std::min(tb, 15));
-        while (tb < 15 && (nbins + (1LL << tb) - 1) >> tb > lde::kMaxTiles) ++tb;
-        const long long nt = (nbins + (1LL << tb) - 1) >> tb;
-        const bool smem_ok = lde::partition_smem((int)nt, h->tp) <= 64 * 1024 &&
-                             lde::paged_smem((int)nt, 1, h->tp) <= 64 * 1024;
-        h->subc = (env_ll("LDE_SUBC", 4) == 4 && lde::paged_smem((int)nt, 4, h->tp) <= 64 * 1024) ? 4 : 1;
+        auto tiles = [&](int b) { return (nbins + (1LL << b) - 1) >> b; };
+        while (tb < 15 && (tiles(tb) > lde::kMaxTiles ||
+                           lde::paged_smem((int)std::min<long long>(tiles(tb), lde::kMaxTiles), 1,
+                                           h->tp) > lde::kPagedSmemMax))
+            ++tb;
+        const long long nt = tiles(tb);
+        const bool smem_ok = nt <= lde::kMaxTiles &&
+                             lde::partition_smem((int)nt, h->tp) <= 64 * 1024 &&
+                             lde::paged_smem((int)nt, 1, h->tp) <= lde::kPagedSmemMax;
+        h->subc = (env_ll("LDE_SUBC", 4) == 4 && smem_ok &&
+                   lde::paged_smem((int)nt, 4, h->tp) <= lde::kPagedSmemMax) ? 4 : 1;
         if (nt <= lde::kMaxTiles && smem_ok) {
             h->tile_bits = tb;
             h->n_tiles = (int)nt;

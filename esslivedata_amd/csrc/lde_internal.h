@@ -19,6 +19,7 @@ constexpr int kMaxSegs = 64;                       // segments per pass-A launch
 constexpr int kLaneModeRun = 48;                   // pass B: lane-per-chunk below this avg run
 constexpr int kPageBits = 10;                      // PAGED strategy: 1024-entry (2 KB) pages
 constexpr int kPage = 1 << kPageBits;
+constexpr size_t kPagedSmemMax = 80 * 1024;        // two pass-A blocks per CU (160 KB LDS)
 
 struct SegDesc {  // one staged ev44 message (device pointers)
     const int *pid;

@@ -56,14 +56,43 @@ __device__ __forceinline__ void load_chunk_global(const SegDesc *__restrict__ se
     }
 }
 
-// staging holds every tile run padded to a multiple of 8 entries (sentinel
-// 0xFFFF offsets), so runs start 16-byte aligned in LDS and in their pages
+// LDS carve of k_paged_partition (u32 words):
+//   staging   kChunk + 16 * NT   tile runs, each [carry | new entries] rounded up to 8
+//   counters  2 x align4(NT * SUBC + 1)   rank sub-counters, double-buffered by chunk parity
+//   tile info 7 x align4(NT)    run, end, write fill, write page, new page, fill, page
+//   carry     4 x NT            <= 7 pending u16 offsets per tile (one 16-byte group)
+//   scan + pool 36, then the TOA lookup image
 size_t paged_smem(int n_tiles, int subc, const ToaParams &tp) {
-    return 4 * ((size_t)kChunk + 8 * (size_t)n_tiles) +
-           4 * ((size_t)align4(n_tiles * subc + 1) + 4 * (size_t)align4(n_tiles) + 36) +
+    const size_t nt4 = (size_t)align4(n_tiles);
+    return 4 * ((size_t)kChunk + 16 * (size_t)n_tiles + 2 * (size_t)align4(n_tiles * subc + 1) +
+                7 * nt4 + 4 * nt4 + 36) +
            toa_lds_bytes(tp);
 }
 
+// raw LUT entry of one event (the gather); p >= L reads nothing
+__device__ __forceinline__ int lut_raw(const uint16_t *__restrict__ lut, unsigned p, unsigned L) {
+    return p < L ? (int)lut[p] : 0xFFFF;
+}
+__device__ __forceinline__ int lut_raw(const int *__restrict__ lut, unsigned p, unsigned L) {
+    return p < L ? lut[p] : -1;
+}
+__device__ __forceinline__ int raw_base(const uint16_t *, int v, int T) {
+    return v == 0xFFFF ? -1 : v * T;
+}
+__device__ __forceinline__ int raw_base(const int *, int v, int) { return v; }
+
+// Pass A.  Per 8192-event chunk:
+//   R  rank every event inside its (tile, sub-counter)                 | sync
+//   S  owner threads (tile t -> thread t mod 512): run sizes incl. the  |
+//      tile's carried tail, block scan, sub-run starts, carry copied    |
+//      to the head of the run, page allocation for the full 8-groups    | sync
+//   P  scatter (tile << 16 | offset) into staging; then the NEXT chunk's |
+//      LUT gathers + TOA bins are issued and its successor's events     |
+//      are requested                                                    | sync
+//   W  16-byte page stores of every full 8-group; owners keep the tail  |
+//      (< 8 entries) in LDS for the next chunk and reset the counters   |
+// so only whole 16-byte groups reach the pages; the tails are flushed once
+// per launch, padded with 0xFFFF sentinels.
 template <int TILE_BITS, typename LT, bool FAST, int SUBC>
 __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_partition(
     const SegDesc *__restrict__ segs, int n_segs, long long n_chunks, const LT *__restrict__ lut,
@@ -71,101 +100,130 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_part
     uint16_t *__restrict__ pages, uint32_t *__restrict__ page_tile, uint32_t *__restrict__ page_cnt,
     uint32_t *__restrict__ pool_used, int cap, uint32_t *__restrict__ overflow) {
     constexpr int EPT = kPartEventsPerThread;
-    constexpr int TPT = kMaxTiles / kPartThreads;
     constexpr uint32_t MASK = (1u << TILE_BITS) - 1u;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // LDS carve: staging (tile<<16 | offset) | sub-counters/starts | fill | cur | new | scan | pool | TOA
+    const int nt4 = align4(n_tiles);
+    const int ncnt = align4(n_tiles * SUBC + 1);
     uint32_t *s_stg = reinterpret_cast<uint32_t *>(smem);
-    uint32_t *s_cnt = s_stg + kChunk + 8 * n_tiles;
-    uint32_t *s_fill = s_cnt + align4(n_tiles * SUBC + 1);
-    uint32_t *s_cur = s_fill + align4(n_tiles);
-    uint32_t *s_new = s_cur + align4(n_tiles);
-    uint32_t *s_loc = s_new + align4(n_tiles);
-    uint32_t *s_w = s_loc + align4(n_tiles);
+    uint32_t *s_cnt0 = s_stg + kChunk + 16 * n_tiles;
+    uint32_t *s_run = s_cnt0 + 2 * ncnt;
+    uint32_t *s_end = s_run + nt4;
+    uint32_t *s_wfill = s_end + nt4;
+    uint32_t *s_wcur = s_wfill + nt4;
+    uint32_t *s_new = s_wcur + nt4;
+    uint32_t *s_fill = s_new + nt4;
+    uint32_t *s_cur = s_fill + nt4;
+    uint32_t *s_carry = s_cur + nt4;  // 4 words per tile; word 3 bits 16..31 hold the count
+    uint32_t *s_w = s_carry + 4 * nt4;
     uint32_t *s_pool = s_w + 32;
     unsigned char *s_tab = reinterpret_cast<unsigned char *>(s_pool + 4);
     const uint32_t pool_base = (uint32_t)blockIdx.x * (uint32_t)cap;
     load_toa_tables(s_tab, g_tab, tp);
-    for (int i = threadIdx.x; i < n_tiles * SUBC; i += blockDim.x) s_cnt[i] = 0;
+    for (int i = threadIdx.x; i < 2 * ncnt; i += blockDim.x) s_cnt0[i] = 0;
     for (int t = threadIdx.x; t < n_tiles; t += blockDim.x) {
         s_fill[t] = 0;
         s_cur[t] = pool_base + t;  // first page of every tile, pre-assigned
-        s_new[t] = 0;
+        s_carry[4 * t + 3] = 0;
         page_tile[pool_base + t] = (uint32_t)t;
     }
     if (threadIdx.x == 0) s_pool[0] = (uint32_t)n_tiles;
     __syncthreads();
 
     const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int sub = lane & (SUBC - 1);
+    const int sub = tid & (SUBC - 1);
+    int key[EPT];
+    uint32_t rank[EPT];
     ChunkRegs nxt;
-    if ((long long)blockIdx.x < n_chunks) load_chunk_global(segs, n_segs, blockIdx.x, pid_off, nxt);
-    for (long long c = blockIdx.x; c < n_chunks; c += gridDim.x) {
-        int key[EPT];
-        uint32_t rank[EPT];
-#pragma unroll
-        for (int e = 0; e < EPT; ++e)
-            key[e] = event_key<LT, FAST>(nxt.p[e], nxt.t[e], lut, pid_off, L, s_tab, tp);
-        // the next chunk's events load while this chunk runs its LDS phases
-        if (c + gridDim.x < n_chunks) load_chunk_global(segs, n_segs, c + gridDim.x, pid_off, nxt);
-        // ---- rank inside (tile, sub-counter): SUBC counters per tile spread a hot
-        // tile's same-address LDS atomics over SUBC banks
+    // prologue: keys of the first chunk, events of the second in flight
+    if ((long long)blockIdx.x < n_chunks) {
+        load_chunk_global(segs, n_segs, blockIdx.x, pid_off, nxt);
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
+            key[e] = lut_raw(lut, (unsigned)nxt.p[e] - (unsigned)pid_off, L);
+            rank[e] = (uint32_t)toa_bin<FAST>(nxt.t[e], s_tab, tp);
+        }
+        if ((long long)blockIdx.x + gridDim.x < n_chunks)
+            load_chunk_global(segs, n_segs, blockIdx.x + gridDim.x, pid_off, nxt);
+    }
+    int parity = 0;
+    for (long long c = blockIdx.x; c < n_chunks; c += gridDim.x, parity ^= 1) {
+        uint32_t *s_cnt = s_cnt0 + parity * ncnt;
+        // ---- R: finish the keys (the gathers were issued one phase earlier), rank
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+            const int base = raw_base(lut, key[e], tp.T);
+            const int b = (int)rank[e];
+            key[e] = (base < 0 || b < 0) ? -1 : base + b;
             rank[e] = 0;
             if (key[e] >= 0) rank[e] = atomicAdd(&s_cnt[(key[e] >> TILE_BITS) * SUBC + sub], 1u);
         }
         __syncthreads();
-        // ---- scan of padded tile totals, sub-run starts, padding, page allocation
-        // (thread tid owns tiles [tid*TPT, tid*TPT + TPT))
+        // ---- S: owner threads
         uint32_t sum = 0;
-        const int t0 = tid * TPT;
-        for (int t = t0; t < t0 + TPT && t < n_tiles; ++t) {
-            uint32_t n = 0;
+        for (int t = tid; t < n_tiles; t += kPartThreads) {
+            uint32_t n = s_carry[4 * t + 3] >> 16;
 #pragma unroll
             for (int s2 = 0; s2 < SUBC; ++s2) n += s_cnt[t * SUBC + s2];
-            s_loc[t] = n;
+            s_end[t] = n;  // run length for now; the run end after the scan
             sum += (n + 7u) & ~7u;
         }
         uint32_t total;
         uint32_t run = block_exclusive_scan(sum, s_w, &total);
-        for (int t = t0; t < t0 + TPT && t < n_tiles; ++t) {
-            const uint32_t n_t = s_loc[t];
-            const uint32_t padded = (n_t + 7u) & ~7u;
-            if (n_t > 0) {
-                uint32_t st = run;
+        for (int t = tid; t < n_tiles; t += kPartThreads) {
+            const uint32_t mt = s_end[t];
+            if (mt > 0) {
+                const uint4 cw = *reinterpret_cast<const uint4 *>(s_carry + 4 * t);
+                const uint32_t cn = cw.w >> 16;
+                uint32_t st = run + cn;
 #pragma unroll
                 for (int s2 = 0; s2 < SUBC; ++s2) {
                     const uint32_t n = s_cnt[t * SUBC + s2];
                     s_cnt[t * SUBC + s2] = st;
                     st += n;
                 }
-                for (uint32_t k = run + n_t; k < run + padded; ++k)
-                    s_stg[k] = ((uint32_t)t << 16) | 0xFFFFu;  // sentinel padding
+                const uint32_t hi = (uint32_t)t << 16;
+                const uint32_t cv[7] = {cw.x & 0xFFFFu, cw.x >> 16, cw.y & 0xFFFFu, cw.y >> 16,
+                                        cw.z & 0xFFFFu, cw.z >> 16, cw.w & 0xFFFFu};
+#pragma unroll
+                for (int j = 0; j < 7; ++j)
+                    if ((uint32_t)j < cn) s_stg[run + j] = hi | cv[j];
+                const uint32_t full = mt & ~7u;
                 const uint32_t fill = s_fill[t];
-                const uint32_t room = (uint32_t)kPage - fill;
-                if (padded > room) {
-                    const uint32_t n_new = (padded - room + kPage - 1) >> kPageBits;
-                    const uint32_t off = atomicAdd(s_pool, n_new);
-                    if (off + n_new > (uint32_t)cap) {  // cannot happen by construction
-                        atomicOr(overflow, 1u);
-                        s_new[t] = s_cur[t];
-                    } else {
-                        const uint32_t first = pool_base + off;
-                        s_new[t] = first;
-                        page_cnt[s_cur[t]] = kPage;  // the open page is now full
-                        for (uint32_t k = 0; k < n_new; ++k) {
-                            page_tile[first + k] = (uint32_t)t;
-                            page_cnt[first + k] = kPage;
+                const uint32_t cur = s_cur[t];
+                s_run[t] = run;
+                s_end[t] = run + mt;
+                s_wfill[t] = fill;
+                s_wcur[t] = cur;
+                if (full > 0) {
+                    const uint32_t room = (uint32_t)kPage - fill;
+                    uint32_t first = cur;
+                    if (full > room) {
+                        const uint32_t n_new = (full - room + kPage - 1) >> kPageBits;
+                        const uint32_t off = atomicAdd(s_pool, n_new);
+                        if (off + n_new > (uint32_t)cap) {  // cannot happen by construction
+                            atomicOr(overflow, 1u);
+                        } else {
+                            first = pool_base + off;
+                            page_cnt[cur] = kPage;  // the open page is now full
+                            for (uint32_t q = 0; q < n_new; ++q) {
+                                page_tile[first + q] = (uint32_t)t;
+                                page_cnt[first + q] = kPage;
+                            }
                         }
                     }
+                    s_new[t] = first;
+                    const uint32_t end = fill + full;
+                    const uint32_t k_end = (end - 1) >> kPageBits;
+                    if (k_end > 0) s_cur[t] = first + k_end - 1;
+                    s_fill[t] = end - (k_end << kPageBits);
                 }
+                run += (mt + 7u) & ~7u;
+            } else {
+                s_run[t] = 0;  // s_end[t] == 0: empty run
             }
-            run += padded;
         }
         __syncthreads();
-        // ---- scatter into LDS staging (tile-sorted), tile id beside the offset
+        // ---- P: scatter, then start the next chunk's keys
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
             if (key[e] >= 0) {
@@ -173,39 +231,88 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_part
                 s_stg[s_cnt[t * SUBC + sub] + rank[e]] = (t << 16) | ((uint32_t)key[e] & MASK);
             }
         }
+        if (c + gridDim.x < n_chunks) {
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) {
+                key[e] = lut_raw(lut, (unsigned)nxt.p[e] - (unsigned)pid_off, L);
+                rank[e] = (uint32_t)toa_bin<FAST>(nxt.t[e], s_tab, tp);
+            }
+            if (c + 2LL * gridDim.x < n_chunks)
+                load_chunk_global(segs, n_segs, c + 2LL * gridDim.x, pid_off, nxt);
+        }
         __syncthreads();
-        // ---- write-out: one 16-byte store per 8-entry group (runs are 8-aligned)
+        // ---- W: full 8-groups to the pages (runs start 8-aligned in staging)
         for (uint32_t g = (uint32_t)tid * 8u; g < total; g += kPartThreads * 8u) {
             const uint4 v0 = *reinterpret_cast<const uint4 *>(s_stg + g);
-            const uint4 v1 = *reinterpret_cast<const uint4 *>(s_stg + g + 4);
             const uint32_t t = v0.x >> 16;
-            const uint32_t pos = s_fill[t] + (g - s_cnt[t * SUBC]);
-            const uint32_t k = pos >> kPageBits;
-            const uint32_t page = k == 0 ? s_cur[t] : s_new[t] + k - 1;
-            uint4 w;
-            w.x = (v0.x & 0xFFFFu) | (v0.y << 16);
-            w.y = (v0.z & 0xFFFFu) | (v0.w << 16);
-            w.z = (v1.x & 0xFFFFu) | (v1.y << 16);
-            w.w = (v1.z & 0xFFFFu) | (v1.w << 16);
-            if (page - pool_base < (uint32_t)cap)  // always true unless the pool overflowed
-                *reinterpret_cast<uint4 *>(pages + (size_t)page * kPage + (pos & (kPage - 1))) = w;
-        }
-        __syncthreads();
-        // ---- advance the open page of the owned tiles, reset the counters
-        for (int t = t0; t < t0 + TPT && t < n_tiles; ++t) {
-            const uint32_t n_t = s_loc[t];
-            if (n_t > 0) {
-                const uint32_t end = s_fill[t] + ((n_t + 7u) & ~7u);
-                const uint32_t k_end = (end - 1) >> kPageBits;
-                if (k_end > 0) s_cur[t] = s_new[t] + k_end - 1;
-                s_fill[t] = end - (k_end << kPageBits);
+            if (g + 8u <= s_end[t]) {
+                const uint4 v1 = *reinterpret_cast<const uint4 *>(s_stg + g + 4);
+                const uint32_t pos = s_wfill[t] + (g - s_run[t]);
+                const uint32_t k = pos >> kPageBits;
+                const uint32_t page = k == 0 ? s_wcur[t] : s_new[t] + k - 1;
+                uint4 w;
+                w.x = (v0.x & 0xFFFFu) | (v0.y << 16);
+                w.y = (v0.z & 0xFFFFu) | (v0.w << 16);
+                w.z = (v1.x & 0xFFFFu) | (v1.y << 16);
+                w.w = (v1.z & 0xFFFFu) | (v1.w << 16);
+                if (page - pool_base < (uint32_t)cap)  // always true unless the pool overflowed
+                    *reinterpret_cast<uint4 *>(pages + (size_t)page * kPage + (pos & (kPage - 1))) = w;
             }
-#pragma unroll
-            for (int s2 = 0; s2 < SUBC; ++s2) s_cnt[t * SUBC + s2] = 0;
         }
-        __syncthreads();
+        // owners: keep the tail, reset this parity's counters
+        for (int t = tid; t < n_tiles; t += kPartThreads) {
+            {
+                const uint32_t mt = s_end[t] - s_run[t];
+                if (mt > 0) {
+                    const uint32_t cn = mt & 7u;
+                    const uint32_t b = s_run[t] + (mt & ~7u);
+                    uint32_t v[7];
+#pragma unroll
+                    for (int j = 0; j < 7; ++j) v[j] = (uint32_t)j < cn ? (s_stg[b + j] & 0xFFFFu) : 0u;
+                    *reinterpret_cast<uint4 *>(s_carry + 4 * t) =
+                        make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16),
+                                   v[6] | (cn << 16));
+                }
+#pragma unroll
+                for (int s2 = 0; s2 < SUBC; ++s2) s_cnt[t * SUBC + s2] = 0;
+            }
+        }
     }
-    for (int t = threadIdx.x; t < n_tiles; t += blockDim.x) page_cnt[s_cur[t]] = s_fill[t];
+    __syncthreads();
+    // flush: every tile's tail as one sentinel-padded group
+    for (int t = threadIdx.x; t < n_tiles; t += blockDim.x) {
+        const uint4 cw = *reinterpret_cast<const uint4 *>(s_carry + 4 * t);
+        const uint32_t cn = cw.w >> 16;
+        uint32_t fill = s_fill[t], cur = s_cur[t];
+        if (cn > 0) {
+            bool ok = true;
+            if (fill == (uint32_t)kPage) {
+                const uint32_t off = atomicAdd(s_pool, 1u);
+                if (off + 1 > (uint32_t)cap) {
+                    atomicOr(overflow, 1u);
+                    ok = false;
+                } else {
+                    page_cnt[cur] = kPage;
+                    cur = pool_base + off;
+                    page_tile[cur] = (uint32_t)t;
+                    fill = 0;
+                }
+            }
+            if (ok) {
+                uint32_t v[8];
+                const uint32_t cv[7] = {cw.x & 0xFFFFu, cw.x >> 16, cw.y & 0xFFFFu, cw.y >> 16,
+                                        cw.z & 0xFFFFu, cw.z >> 16, cw.w & 0xFFFFu};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (j < 7 && (uint32_t)j < cn) ? cv[j] : 0xFFFFu;
+                *reinterpret_cast<uint4 *>(pages + (size_t)cur * kPage + fill) =
+                    make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16),
+                               v[6] | (v[7] << 16));
+                fill += 8;
+            }
+        }
+        page_cnt[cur] = fill;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) pool_used[blockIdx.x] = min(s_pool[0], (uint32_t)cap);
 }
 
@@ -265,7 +372,14 @@ __global__ __launch_bounds__(256) void k_page_scan(uint32_t *__restrict__ cntp,
     }
 }
 
-// tile list bases + work items (t, first list index, last list index)
+// tile list bases + work items (t, first list index, last list index).  Tile
+// prefixes go to LDS, then every thread emits items independently (binary
+// search of its item's tile), so a hot tile's items are not written serially.
+__device__ __forceinline__ uint32_t split_point(uint32_t j, uint32_t np, uint32_t ni) {
+    const unsigned long long x = (unsigned long long)j * np;
+    return x <= 0xffffffffULL ? (uint32_t)x / ni : (uint32_t)(x / ni);
+}
+
 __global__ __launch_bounds__(1024) void k_page_plan(const uint32_t *__restrict__ tile_pages,
                                                     const uint32_t *__restrict__ tile_events,
                                                     int n_tiles, uint32_t item_events,
@@ -274,6 +388,8 @@ __global__ __launch_bounds__(1024) void k_page_plan(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ item_count,
                                                     uint32_t max_items) {
     __shared__ uint32_t s_w[32];
+    __shared__ uint32_t s_ib[kMaxTiles + 1];  // item prefix per tile
+    __shared__ uint32_t s_pb[kMaxTiles];      // page-list prefix per tile
     constexpr int TPT = kMaxTiles / 1024;
     const int tid = threadIdx.x;
     const int t0 = tid * TPT;
@@ -299,16 +415,28 @@ __global__ __launch_bounds__(1024) void k_page_plan(const uint32_t *__restrict__
         const int t = t0 + q;
         if (t < n_tiles) {
             tile_base[t] = pbase;
-            for (uint32_t j = 0; j < ni[q] && ibase + j < max_items; ++j) {
-                const uint32_t lo = pbase + (uint32_t)((unsigned long long)j * np[q] / ni[q]);
-                const uint32_t hi = pbase + (uint32_t)((unsigned long long)(j + 1) * np[q] / ni[q]);
-                items[ibase + j] = make_uint4((uint32_t)t, lo, hi, 0u);
-            }
+            s_pb[t] = pbase;
+            s_ib[t] = ibase;
         }
         pbase += np[q];
         ibase += ni[q];
     }
-    if (tid == 0) *item_count = itot < max_items ? itot : max_items;
+    if (tid == 0) s_ib[n_tiles] = itot;
+    __syncthreads();
+    const uint32_t n_items = itot < max_items ? itot : max_items;
+    for (uint32_t i = (uint32_t)tid; i < n_items; i += 1024u) {
+        int lo = 0, hi = n_tiles - 1;  // last tile with s_ib[t] <= i
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_ib[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        const uint32_t nt_items = s_ib[lo + 1] - s_ib[lo];
+        const uint32_t j = i - s_ib[lo];
+        const uint32_t pages_t = (lo + 1 < n_tiles ? s_pb[lo + 1] : ptot) - s_pb[lo];
+        items[i] = make_uint4((uint32_t)lo, s_pb[lo] + split_point(j, pages_t, nt_items),
+                              s_pb[lo] + split_point(j + 1, pages_t, nt_items), 0u);
+    }
+    if (tid == 0) *item_count = n_items;
 }
 
 // per-tile page lists

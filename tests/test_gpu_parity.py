@@ -21,6 +21,7 @@ VARIANTS = [
     {'LDE_PEEL': '1'},
     {'LDE_SUBC': '1'},
     {'LDE_TILE_BITS': '15', 'LDE_PART_GRID': '7'},
+    {'LDE_TILE_BITS': '13', 'LDE_PART_GRID': '3'},  # long per-block page chains + tails
 ]
 
 

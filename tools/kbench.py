@@ -65,7 +65,7 @@ if __name__ == '__main__':
     if mode == 'prof':  # one config for rocprof
         run(sys.argv[2] if len(sys.argv) > 2 else 'dream', 'partition', {}, reps=3)
         sys.exit(0)
-    variants = [dict(LDE_TILE_BITS=14), dict(LDE_SUBC=1), dict(LDE_PART_GRID=1024)]
+    variants = [dict(LDE_TILE_BITS=13), dict(LDE_TILE_BITS=15), dict(LDE_SUBC=1)]
     ablations = []
     for wl in ('dream', 'loki'):
         base = run(wl, 'partition', {})

@@ -1,18 +1,25 @@
 #!/bin/bash
-# rocprofv3: kernel trace + separate PMC passes for one workload (diagnostic)
+# rocprofv3 on the bench command itself: one kernel-trace/--stats pass, then
+# separate PMC passes (no tracing domains combined with --pmc), then the
+# summary into profiles/${TAG}_${WL}_bench{.json,_kernel_stats.csv}.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 WL=${WL:-dream}
-OUT=gpurun_out/prof_${TAG:-r1}_${WL}
+TAG=${TAG:-r1}
+OUT=gpurun_out/prof_${TAG}_${WL}
+ARGS="bench.py --workload $WL --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline ${BENCH_ARGS}"
+rm -rf $OUT
 mkdir -p $OUT
-rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 tools/kbench.py prof $WL > $OUT/kt.log 2>&1 || { echo "kt failed $?"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 $ARGS > $OUT/kt.log 2>&1
+rc=$?
+echo "kernel trace rc=$rc"
+if [ $rc -ne 0 ]; then tail -20 $OUT/kt.log; exit $rc; fi
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD" "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum" "GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY"; do
   name=$(echo $pmc | tr ' ' '_' | cut -c1-40)
-  timeout -k 10 300 rocprofv3 --pmc $pmc -d $OUT/pmc_$name -o run --output-format csv -- python3 tools/kbench.py prof $WL > $OUT/pmc_$name.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $pmc -d $OUT/pmc_$name -o run --output-format csv -- python3 $ARGS > $OUT/pmc_$name.log 2>&1
   rc=$?
   echo "pmc $pmc rc=$rc"
-  if [ $rc -ne 0 ]; then tail -5 $OUT/pmc_$name.log; fi
-  if [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
+  if [ $rc -ne 0 ]; then tail -5 $OUT/pmc_$name.log; exit $rc; fi
 done
+python3 tools/prof_summary.py $OUT profiles/${TAG}_${WL}_bench > $OUT/summary.log 2>&1 || { cat $OUT/summary.log; exit 1; }
 echo done

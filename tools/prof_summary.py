@@ -1,0 +1,80 @@
+"""Condense one rocprofv3 round (kernel trace + separate PMC passes) into a
+committed summary under profiles/ (diagnostic tool, not the product).
+
+Usage: python tools/prof_summary.py <prof_dir> <out_stem>
+
+<prof_dir> is what tools/prof_round.sh wrote (kt/ and pmc_*/ subdirectories).
+Writes <out_stem>.json (per engine kernel: calls, average duration, PMC
+counters per dispatch, HBM traffic per dispatch) and <out_stem>_kernel_stats.csv
+(the rocprofv3 --stats table restricted to the engine's kernels + torch's top
+kernels).
+
+HBM traffic per dispatch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950
+FETCH_SIZE counts half the bytes of wide streaming reads (MI355X_MICROARCH.md
+section "HBM [CDNA4]"), WRITE_SIZE counts 16-B stores exactly.
+"""
+
+from __future__ import annotations
+
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def short(name: str) -> str:
+    m = re.search(r'lde::(k_\w+)', name)
+    return m.group(1) if m else name.split('(')[0][:80]
+
+
+def main(prof: Path, stem: Path) -> None:
+    stats = list(csv.DictReader(open(prof / 'kt' / 'run_kernel_stats.csv')))
+    kernels: dict[str, dict] = {}
+    for r in stats:
+        k = short(r['Name'])
+        d = kernels.setdefault(k, {'calls': 0, 'total_ns': 0.0})
+        d['calls'] += int(r['Calls'])
+        d['total_ns'] += float(r['TotalDurationNs'])
+    for d in kernels.values():
+        d['avg_ms'] = d['total_ns'] / max(d['calls'], 1) / 1e6
+    counters: dict[str, dict[str, list[float]]] = defaultdict(lambda: defaultdict(list))
+    for sub in sorted(prof.glob('pmc_*')):
+        f = sub / 'run_counter_collection.csv'
+        if not f.exists():
+            continue
+        per = defaultdict(float)  # (kernel, dispatch, counter) -> value summed over dims
+        for r in csv.DictReader(open(f)):
+            per[(short(r['Kernel_Name']), r['Dispatch_Id'], r['Counter_Name'])] += float(r['Counter_Value'])
+        for (k, _, c), v in per.items():
+            counters[k][c].append(v)
+    out = {}
+    for k, d in kernels.items():
+        if not k.startswith('k_'):
+            continue
+        e = {'calls': d['calls'], 'avg_ms': d['avg_ms']}
+        pm = {c: sum(v) / len(v) for c, v in counters.get(k, {}).items()}
+        # the first dispatches of each kernel include warm-up sizes; use the median-like mean
+        e['pmc_per_dispatch'] = pm
+        if 'FETCH_SIZE' in pm and 'WRITE_SIZE' in pm:
+            e['hbm_read_bytes'] = 2 * pm['FETCH_SIZE'] * 1024
+            e['hbm_write_bytes'] = pm['WRITE_SIZE'] * 1024
+            e['hbm_traffic_bytes'] = e['hbm_read_bytes'] + e['hbm_write_bytes']
+            e['hbm_GBs_at_avg'] = e['hbm_traffic_bytes'] / (d['avg_ms'] * 1e-3) / 1e9
+        out[k] = e
+    stem.parent.mkdir(parents=True, exist_ok=True)
+    Path(str(stem) + '.json').write_text(json.dumps(out, indent=1, sort_keys=True) + '\n')
+    rows = sorted(stats, key=lambda r: -float(r['TotalDurationNs']))
+    with open(str(stem) + '_kernel_stats.csv', 'w', newline='') as f:
+        w = csv.writer(f)
+        w.writerow(['Name', 'Calls', 'TotalDurationNs', 'AverageNs', 'Percentage', 'MinNs', 'MaxNs'])
+        for r in rows:
+            if 'lde::' in r['Name'] or rows.index(r) < 8:
+                w.writerow([short(r['Name']), r['Calls'], r['TotalDurationNs'], r['AverageNs'],
+                            r['Percentage'], r['MinNs'], r['MaxNs']])
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == '__main__':
+    main(Path(sys.argv[1]), Path(sys.argv[2]))
