@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 ${TEST_TIMEOUT:-600} python -m pytest tests -x -q -m gpu ${PYTEST_ARGS} > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/gpu_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 tail -40 gpurun_out/gpu_tests.log

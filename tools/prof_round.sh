@@ -16,10 +16,10 @@ echo "kernel trace rc=$rc"
 if [ $rc -ne 0 ]; then tail -20 $OUT/kt.log; exit $rc; fi
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD" "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum" "GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY"; do
   name=$(echo $pmc | tr ' ' '_' | cut -c1-40)
-  timeout -k 10 300 rocprofv3 --pmc $pmc -d $OUT/pmc_$name -o run --output-format csv -- python3 $ARGS > $OUT/pmc_$name.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $pmc -d $OUT/pmc_$name -o run --output-format csv -- python3 $ARGS > $OUT/pmc_$name.log 2>&1
   rc=$?
   echo "pmc $pmc rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/pmc_$name.log; exit $rc; fi
 done
-python3 tools/prof_summary.py $OUT profiles/${TAG}_${WL}_bench > $OUT/summary.log 2>&1 || { cat $OUT/summary.log; exit 1; }
+python3 tools/prof_summary.py $OUT $OUT/${TAG}_${WL}_bench > $OUT/summary.log 2>&1 || { cat $OUT/summary.log; exit 1; }
 echo done
