@@ -36,6 +36,7 @@ KERNEL_SYMBOL = {
     'tile_accumulate': 'k_tile_accumulate',
     'paged': 'k_paged_partition',
     'page_accumulate': 'k_page_accumulate',
+    'split': 'k_split',
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_EVENT = 8  # int32 pixel_id + int32 time_of_flight
@@ -49,7 +50,7 @@ def parse():
     ap.add_argument('--workload', default='dream', choices=['dream', 'loki'])
     ap.add_argument('--pulses', type=int, default=14)
     ap.add_argument('--events-per-pulse', type=int, default=10_000_000)
-    ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition', 'paged'])
+    ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition', 'paged', 'split'])
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     return ap.parse_args()
@@ -199,7 +200,7 @@ def main():
     stats = {
         k: eng.kernel_stats(k)
         for k in ('atomic', 'partition', 'tile_accumulate', 'plan', 'paged', 'page_plan',
-                  'page_accumulate', 'binning', 'finalize')
+                  'page_accumulate', 'split', 'split_aux', 'binning', 'finalize')
     }
     info = eng.info()
     total_events = n_step * args.steps * world
@@ -207,7 +208,8 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
 
     # dominant kernel and its roofline (algorithmic bytes per launch / avg duration)
-    dom = max(('atomic', 'partition', 'tile_accumulate', 'paged', 'page_accumulate'), key=lambda k: stats[k][0])
+    dom = max(('atomic', 'partition', 'tile_accumulate', 'paged', 'page_accumulate', 'split'),
+              key=lambda k: stats[k][0])
     ms, launches = stats[dom]
     # every binning kernel processes all events of the timed steps across its launches
     events_per_launch = n_step * args.steps / max(launches, 1)

@@ -25,7 +25,7 @@ LDE_ENODATA = -5
 LDE_F64 = 0
 LDE_F32 = 1
 
-STRATEGIES = {'auto': 0, 'atomic': 1, 'partition': 2, 'paged': 3}
+STRATEGIES = {'auto': 0, 'atomic': 1, 'partition': 2, 'paged': 3, 'split': 4}
 
 LDE_CURRENT = 0
 LDE_CUMULATIVE = 1
@@ -41,6 +41,8 @@ KERNELS = {
     'paged': 7,
     'page_plan': 8,
     'page_accumulate': 9,
+    'split': 10,
+    'split_aux': 11,
 }
 
 # every symbol include/lde.h declares (checked by tests/test_abi.py)

@@ -38,25 +38,7 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > mtime for p in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    if not force and not needs_build():
-        return LIB
-    tmp = LIB.with_suffix('.so.tmp')
-    cmd = [
-        _hipcc(),
-        f'--offload-arch={ARCH}',
-        '-O3',
-        '-std=c++17',
-        '-fPIC',
-        '-shared',
-        '-Wall',
-        '-Wno-unused-function',
-        '-Wno-unused-result',
-        f'-I{ROOT / "include"}',
-        *[str(s) for s in sources()],
-        '-o',
-        str(tmp),
-    ]
+def _run(cmd: list[str], verbose: bool) -> None:
     if verbose:
         print(' '.join(cmd), file=sys.stderr)
     res = subprocess.run(cmd, capture_output=True, text=True)
@@ -64,6 +46,37 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         raise RuntimeError(f'hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}')
     if verbose and res.stderr.strip():
         print(res.stderr, file=sys.stderr)
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile every source to an object in parallel, then link the library."""
+    if not force and not needs_build():
+        return LIB
+    from concurrent.futures import ThreadPoolExecutor
+
+    flags = [
+        f'--offload-arch={ARCH}',
+        '-O3',
+        '-std=c++17',
+        '-fPIC',
+        '-Wall',
+        '-Wno-unused-function',
+        '-Wno-unused-result',
+        f'-I{ROOT / "include"}',
+    ]
+    objdir = PKG / 'build'
+    objdir.mkdir(exist_ok=True)
+    srcs = sources()
+    objs = [objdir / (s.name + '.o') for s in srcs]
+    jobs = min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(jobs) as ex:
+        futs = [ex.submit(_run, [_hipcc(), *flags, '-c', str(s), '-o', str(o)], verbose)
+                for s, o in zip(srcs, objs)]
+        for f in futs:
+            f.result()
+    tmp = LIB.with_suffix('.so.tmp')
+    _run([_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', *[str(o) for o in objs], '-o',
+          str(tmp)], verbose)
     os.replace(tmp, LIB)
     return LIB
 

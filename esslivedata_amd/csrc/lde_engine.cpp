@@ -108,6 +108,28 @@ struct lde_handle {
     long long item_events_override = 0;
     long long atomic_threshold = -1;
     int auto_partition = LDE_STRATEGY_PAGED;
+    // SPLIT workspace (hot rows in LDS + cold keys through the paged path)
+    bool split_ok = false;
+    int hot_rows = 0;
+    int split_grid = 0;
+    int cache_bits = 0, row_bits = 0, screen_bits = 0;
+    int hot_refresh = 256;      // re-select a replica's hot set after this many batches
+    double split_min_cov = 0.3; // sampled hot fraction below which AUTO stays PAGED
+    uint32_t *d_hlut = nullptr;        // [R][L] (row + 1) << 22 | screen * T
+    uint32_t *d_row_screen = nullptr;  // [R][kHotMaxRows]
+    uint32_t *d_sel_stats = nullptr;   // [R][4]
+    uint32_t *d_sample_part = nullptr, *d_screen_cnt = nullptr;
+    uint16_t *d_screen_row = nullptr;
+    uint32_t *h_sel_stats = nullptr;   // pinned
+    std::vector<int> hot_uses;         // per replica: -1 = not selected yet
+    std::vector<double> hot_cov;
+    uint32_t *d_hot_part = nullptr;
+    size_t hot_part_cap = 0;
+    uint32_t *d_cold = nullptr;
+    size_t cold_total_cap = 0;
+    uint32_t *d_cold_cnt = nullptr;
+    lde::SegDesc *d_cold_segs = nullptr;
+    long long *d_cold_chunks = nullptr;
 
     // finalize scratch
     unsigned long long *d_tot4 = nullptr;
@@ -414,8 +436,13 @@ int grow(lde_handle *h, T **p, size_t &cap, size_t need) {
     return LDE_OK;
 }
 
-int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks,
-              long long total, const void *lut) {
+// PAGED pass A + plan + pass B over `segs` (device table).  Key mode (cold keys
+// of the SPLIT strategy) when n_chunks_dev != nullptr: `chunks` is then an
+// upper bound and the real count is read on the device.  `events` sizes the
+// pass-B work items.
+int paged_core(lde_handle *h, const lde::SegDesc *segs, int n_segs, long long chunks,
+               long long total, long long events, const void *lut,
+               const long long *n_chunks_dev) {
     const int grid = (int)std::min<long long>(chunks, (long long)h->part_grid);
     const long long per_block = (chunks + grid - 1) / grid;
     const int cap = (int)((per_block * lde::kChunk + lde::kPage - 1) / lde::kPage) + 2 * h->n_tiles + 2;
@@ -423,7 +450,7 @@ int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     if (pages > 0xffffffffULL) return fail(h, LDE_EINVAL, "batch too large for the page pool");
     long long item_events = h->item_events_override > 0
                                 ? h->item_events_override
-                                : std::max<long long>(32768, (total + 2LL * h->cus - 1) / (2LL * h->cus));
+                                : std::max<long long>(32768, (events + 2LL * h->cus - 1) / (2LL * h->cus));
     if (item_events > 0x7fffffffLL) item_events = 0x7fffffffLL;
     const long long max_items = (total + item_events - 1) / item_events + h->n_tiles;
     if (int rc = grow(h, &h->d_pages, h->pages_cap, pages * lde::kPage)) return rc;
@@ -453,13 +480,12 @@ int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     size_t icap = (size_t)h->items4_cap;
     if (int rc = grow(h, &h->d_items4, icap, (size_t)max_items)) return rc;
     h->items4_cap = (long long)icap;
-    if (int rc = upload_segments(h, sd)) return rc;
     lde::PagedArgs a;
     a.tile_bits = h->tile_bits;
     a.lut16 = h->lut16;
     a.subc = h->subc;
-    a.segs = h->d_segs;
-    a.n_segs = (int)sd.size();
+    a.segs = segs;
+    a.n_segs = n_segs;
     a.n_chunks = chunks;
     a.lut = lut;
     a.pid_off = h->pid_off;
@@ -476,7 +502,8 @@ int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.grid = grid;
     {
         Timed tm(h, LDE_K_PAGED);
-        HIPCALL(h, lde::launch_paged_partition(a, h->stream));
+        if (n_chunks_dev) HIPCALL(h, lde::launch_paged_keys(a, n_chunks_dev, h->stream));
+        else HIPCALL(h, lde::launch_paged_partition(a, h->stream));
     }
     {
         Timed tm(h, LDE_K_PAGE_PLAN);
@@ -492,6 +519,76 @@ int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                                                (int)max_items, h->stream));
     }
     return LDE_OK;
+}
+
+int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks,
+              long long total, const void *lut) {
+    if (int rc = upload_segments(h, sd)) return rc;
+    return paged_core(h, h->d_segs, (int)sd.size(), chunks, total, total, lut, nullptr);
+}
+
+// SPLIT: hot rows of this replica in LDS, cold keys through paged_core.
+// Returns 1 (nothing launched) when AUTO should fall back to PAGED.
+int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks,
+              long long total, int replica, bool forced) {
+    if (int rc = upload_segments(h, sd)) return rc;
+    lde::SplitArgs a;
+    a.segs = h->d_segs;
+    a.n_segs = (int)sd.size();
+    a.n_chunks = chunks;
+    a.lut = h->d_lut;
+    a.lut16 = h->lut16;
+    a.L = h->L;
+    a.pid_off = h->pid_off;
+    a.S = (int)h->S;
+    a.tab = h->d_tab;
+    a.tp = h->tp;
+    a.rows = h->hot_rows;
+    a.sample_blocks = (int)std::min<long long>(lde::kSampleBlocks, chunks);
+    a.sample_part = h->d_sample_part;
+    a.screen_cnt = h->d_screen_cnt;
+    a.stats = h->d_sel_stats + 4 * replica;
+    a.screen_row = h->d_screen_row;
+    a.row_screen = h->d_row_screen + (size_t)lde::kHotMaxRows * replica;
+    a.hlut = h->d_hlut + (size_t)h->L * replica;
+    a.grid = (int)std::min<long long>(chunks, (long long)h->split_grid);
+    a.ablate = (int)env_ll("LDE_ABLATE", 0);
+    int &uses = h->hot_uses[replica];
+    if (uses < 0 || uses >= h->hot_refresh) {
+        {
+            Timed tm(h, LDE_K_SPLIT_AUX);
+            HIPCALL(h, lde::launch_hot_select(a, replica, h->stream));
+        }
+        HIPCALL(h, hipMemcpyAsync(h->h_sel_stats, a.stats, 16, hipMemcpyDeviceToHost, h->stream));
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        const double sampled = (double)h->h_sel_stats[0];
+        h->hot_cov[replica] = sampled > 0 ? (double)h->h_sel_stats[1] / sampled : 0.0;
+        uses = 0;
+    }
+    ++uses;
+    if (!forced && h->hot_cov[replica] < h->split_min_cov) return 1;
+    const long long per_block = (chunks + a.grid - 1) / a.grid;
+    a.cold_cap = per_block * lde::kChunk;
+    a.cache_bits = h->cache_bits;
+    a.row_bits = h->row_bits;
+    a.screen_bits = h->screen_bits;
+    const int ht4 = lde::align4(h->hot_rows * h->T);
+    if (int rc = grow(h, &h->d_hot_part, h->hot_part_cap, (size_t)a.grid * ht4)) return rc;
+    if (int rc = grow(h, &h->d_cold, h->cold_total_cap, (size_t)a.grid * a.cold_cap)) return rc;
+    a.hot_part = h->d_hot_part;
+    a.cold = h->d_cold;
+    a.cold_cnt = h->d_cold_cnt;
+    {
+        Timed tm(h, LDE_K_SPLIT);
+        HIPCALL(h, lde::launch_split(a, h->stream));
+    }
+    {
+        Timed tm(h, LDE_K_SPLIT_AUX);
+        HIPCALL(h, lde::launch_split_tail(a, h->d_win32, h->d_cold_segs, h->d_cold_chunks, h->stream));
+    }
+    const double cold_frac = std::min(1.0, std::max(0.05, 1.0 - h->hot_cov[replica]));
+    return paged_core(h, h->d_cold_segs, a.grid, chunks, total, (long long)(cold_frac * total),
+                      nullptr, h->d_cold_chunks);
 }
 
 int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long total, int replica) {
@@ -518,6 +615,8 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
                                   : std::max<long long>(1 << 20, h->nbins / 2);
         strat = (h->n_tiles > 0 && total >= thr) ? h->auto_partition : LDE_STRATEGY_ATOMIC;
     }
+    const bool auto_split = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && h->split_ok;
+    if (strat == LDE_STRATEGY_SPLIT && !h->split_ok) strat = LDE_STRATEGY_PAGED;
     if ((strat == LDE_STRATEGY_PARTITION || strat == LDE_STRATEGY_PAGED) && h->n_tiles == 0)
         strat = LDE_STRATEGY_ATOMIC;
     h->last_strategy = strat;
@@ -542,6 +641,14 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
         chunks += (s.n + lde::kChunk - 1) / lde::kChunk;
     }
     if (chunks == 0) return LDE_OK;
+    if (strat == LDE_STRATEGY_SPLIT || auto_split) {
+        const int rc = bin_split(h, sd, chunks, total, replica, strat == LDE_STRATEGY_SPLIT);
+        if (rc != 1) {
+            if (rc == LDE_OK) h->last_strategy = LDE_STRATEGY_SPLIT;
+            return rc;
+        }
+        return paged_core(h, h->d_segs, (int)sd.size(), chunks, total, total, lut, nullptr);
+    }
     if (strat == LDE_STRATEGY_PAGED) return bin_paged(h, sd, chunks, total, lut);
     long long item_events = h->item_events_override > 0
                                 ? h->item_events_override
@@ -669,6 +776,18 @@ void release(lde_handle *h) {
     dev_free(h->d_tile_base);
     dev_free(h->d_overflow);
     dev_free(h->d_items4);
+    dev_free(h->d_hlut);
+    dev_free(h->d_row_screen);
+    dev_free(h->d_sel_stats);
+    dev_free(h->d_sample_part);
+    dev_free(h->d_screen_cnt);
+    dev_free(h->d_screen_row);
+    if (h->h_sel_stats) (void)hipHostFree(h->h_sel_stats);
+    dev_free(h->d_hot_part);
+    dev_free(h->d_cold);
+    dev_free(h->d_cold_cnt);
+    dev_free(h->d_cold_segs);
+    dev_free(h->d_cold_chunks);
     dev_free(h->d_tot4);
     dev_free(h->d_img_cur);
     dev_free(h->d_img_cum);
@@ -840,6 +959,51 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
             CREATE_CHECK(dev_alloc(h, &h->d_item_count, 1));
         } else {
             h->n_tiles = 0;  // partition unavailable -> atomic strategy
+        }
+        // SPLIT: needs the paged path for its cold keys and the sampled screen
+        // histogram in LDS; the pixel cache needs tag + row + screen <= 31 bits
+        if (h->n_tiles > 0 && h->S * 4 <= 160 * 1024 && env_ll("LDE_SPLIT", 1) != 0) {
+            auto bits = [](long long n) { int b = 0; while ((1LL << b) < n) ++b; return b; };
+            int cbits = (int)std::max<long long>(0, std::min<long long>(16, env_ll("LDE_PIXEL_CACHE_BITS", 14)));
+            if ((1LL << cbits) >= 2 * h->L) cbits = std::max(0, bits(h->L));  // whole LUT fits
+            auto rows_for = [&](int cb) {
+                const size_t fixed = lde::split_smem(0, cb ? (1 << cb) : 0, h->tp);
+                int H = 0;
+                if (fixed < lde::kSplitSmemMax)
+                    H = (int)std::min<long long>(lde::kHotMaxRows, (long long)((lde::kSplitSmemMax - fixed) / (4 * (size_t)h->T)));
+                while (H > 0 && lde::split_smem(lde::align4(H * h->T), cb ? (1 << cb) : 0, h->tp) > lde::kSplitSmemMax) --H;
+                return H;
+            };
+            // the cache never takes the room of the last 64 hot rows
+            while (cbits > 8 && rows_for(cbits) < std::min<long long>(64, h->S)) --cbits;
+            int H = rows_for(cbits);
+            H = (int)std::min<long long>(H, h->S);
+            const long long hmax = env_ll("LDE_HOT_ROWS", 0);
+            if (hmax > 0) H = (int)std::min<long long>(H, hmax);
+            h->row_bits = bits(H + 2);
+            h->screen_bits = std::max(1, bits(h->S));
+            const int tag_bits = std::max(0, bits(h->L) - cbits);
+            if (cbits > 0 && tag_bits + h->row_bits + h->screen_bits > 31) cbits = 0;
+            h->cache_bits = cbits;
+            if (H >= 8) {
+                h->split_ok = true;
+                h->hot_rows = H;
+                h->split_grid = (int)std::max<long long>(1, env_ll("LDE_SPLIT_GRID", h->cus));
+                h->hot_refresh = (int)std::max<long long>(1, env_ll("LDE_HOT_REFRESH", 256));
+                h->split_min_cov = (double)env_ll("LDE_SPLIT_MIN_COV_PCT", 30) / 100.0;
+                h->hot_uses.assign((size_t)h->R, -1);
+                h->hot_cov.assign((size_t)h->R, 0.0);
+                CREATE_CHECK(dev_alloc(h, &h->d_hlut, (size_t)h->R * h->L));
+                CREATE_CHECK(dev_alloc(h, &h->d_row_screen, (size_t)h->R * lde::kHotMaxRows));
+                CREATE_CHECK(dev_alloc(h, &h->d_sel_stats, (size_t)h->R * 4));
+                CREATE_CHECK(dev_alloc(h, &h->d_sample_part, (size_t)lde::kSampleBlocks * h->S));
+                CREATE_CHECK(dev_alloc(h, &h->d_screen_cnt, (size_t)h->S));
+                CREATE_CHECK(dev_alloc(h, &h->d_screen_row, (size_t)h->S));
+                CREATE_CHECK(dev_alloc(h, &h->d_cold_cnt, (size_t)h->split_grid));
+                CREATE_CHECK(dev_alloc(h, &h->d_cold_segs, (size_t)h->split_grid));
+                CREATE_CHECK(dev_alloc(h, &h->d_cold_chunks, 1));
+                CREATE_HIP(hipHostMalloc((void **)&h->h_sel_stats, 16, hipHostMallocDefault));
+            }
         }
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);

@@ -20,6 +20,14 @@ constexpr int kLaneModeRun = 48;                   // pass B: lane-per-chunk bel
 constexpr int kPageBits = 10;                      // PAGED strategy: 1024-entry (2 KB) pages
 constexpr int kPage = 1 << kPageBits;
 constexpr size_t kPagedSmemMax = 80 * 1024;        // two pass-A blocks per CU (160 KB LDS)
+constexpr int kSplitThreads = 1024;                // SPLIT event pass block (one per CU)
+constexpr int kSplitEPT = kChunk / kSplitThreads;  // 8 events per thread per chunk
+constexpr size_t kSplitSmemMax = 160 * 1024;       // hot rows + TOA image, one block per CU
+constexpr uint32_t kHotDrop = 0xFFFFFFFFu;         // hot-LUT entry of a dropped pixel
+constexpr int kHotRowShift = 22;                   // hot LUT: (row + 1) << 22 | screen
+constexpr uint32_t kHotBaseMask = (1u << kHotRowShift) - 1u;
+constexpr int kHotMaxRows = 1022;
+constexpr int kSampleBlocks = 64;                  // sampled chunks per hot-set selection
 
 struct SegDesc {  // one staged ev44 message (device pointers)
     const int *pid;
@@ -103,6 +111,39 @@ struct PagedArgs {
 
 size_t paged_smem(int n_tiles, int subc, const ToaParams &tp);
 hipError_t launch_paged_partition(const PagedArgs &a, hipStream_t st);
+// key mode: segments hold u32 (screen * T + bin) keys, chunk count read on the device
+hipError_t launch_paged_keys(const PagedArgs &a, const long long *n_chunks_dev, hipStream_t st);
+
+struct SplitArgs {
+    const SegDesc *segs;  // staged event segments
+    int n_segs;
+    long long n_chunks;
+    const void *lut;  // d_lut (all replicas)
+    bool lut16;
+    long long L;
+    int pid_off;
+    int S;
+    const unsigned char *tab;
+    ToaParams tp;
+    int rows;  // hot rows H
+    int sample_blocks;
+    uint32_t *sample_part, *screen_cnt, *stats;
+    uint16_t *screen_row;
+    uint32_t *row_screen;  // this replica's row -> screen
+    uint32_t *hlut;        // this replica's hot LUT
+    int grid;
+    uint32_t *hot_part;
+    uint32_t *cold;
+    long long cold_cap;  // keys per block region
+    uint32_t *cold_cnt;
+    int ablate;  // timing ablations (LDE_ABLATE), never set in production
+    int cache_bits, row_bits, screen_bits;  // LDS pixel cache (cache_bits 0: off)
+};
+size_t split_smem(int ht4, int cache_words, const ToaParams &tp);
+hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st);
+hipError_t launch_split(const SplitArgs &a, hipStream_t st);
+hipError_t launch_split_tail(const SplitArgs &a, uint32_t *win, SegDesc *cold_segs,
+                             long long *n_cold_chunks, hipStream_t st);
 hipError_t launch_page_plan(const PagedArgs &a, uint32_t item_events, uint32_t *cntp,
                             uint32_t *evp, uint32_t *tile_pages, uint32_t *tile_events,
                             uint32_t *tile_base, uint4 *items, uint32_t *item_count,

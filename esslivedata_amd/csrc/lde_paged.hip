@@ -22,6 +22,7 @@
 
 namespace lde {
 
+template <bool KEYS>
 __device__ __forceinline__ void load_chunk_global(const SegDesc *__restrict__ segs, int n_segs,
                                                   long long c, int pid_off, ChunkRegs &r) {
     // segment of chunk c: binary search over chunk0 (uniform per block)
@@ -32,25 +33,29 @@ __device__ __forceinline__ void load_chunk_global(const SegDesc *__restrict__ se
     }
     const SegDesc sd = segs[lo];
     const long long base = (c - sd.chunk0) * kChunk;
-    const bool vec = (((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0;
+    const uintptr_t al = KEYS ? (uintptr_t)sd.pid : ((uintptr_t)sd.pid | (uintptr_t)sd.toa);
+    const bool vec = (al & 15u) == 0;
+    // key mode: sd.pid holds u32 keys; padding entries are -1 (dropped)
+    const int fill = KEYS ? -1 : pid_off - 1;  // pid_off - 1 is outside the LUT: dropped
     const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < kPartEventsPerThread / 4; ++j) {
         const long long e0 = base + ((long long)j * kPartThreads + tid) * 4;
         if (vec && e0 + 3 < sd.n) {
             const v4i p = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.pid + e0));
-            const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.toa + e0));
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                r.p[j * 4 + q] = p[q];
-                r.t[j * 4 + q] = t[q];
+            for (int q = 0; q < 4; ++q) r.p[j * 4 + q] = p[q];
+            if (!KEYS) {
+                const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.toa + e0));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) r.t[j * 4 + q] = t[q];
             }
         } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const bool ok = e0 + q < sd.n;
-                r.p[j * 4 + q] = ok ? sd.pid[e0 + q] : pid_off - 1;  // outside the LUT: dropped
-                r.t[j * 4 + q] = ok ? sd.toa[e0 + q] : 0;
+                r.p[j * 4 + q] = ok ? sd.pid[e0 + q] : fill;
+                if (!KEYS) r.t[j * 4 + q] = ok ? sd.toa[e0 + q] : 0;
             }
         }
     }
@@ -93,9 +98,13 @@ __device__ __forceinline__ int raw_base(const int *, int v, int) { return v; }
 //      (< 8 entries) in LDS for the next chunk and reset the counters   |
 // so only whole 16-byte groups reach the pages; the tails are flushed once
 // per launch, padded with 0xFFFF sentinels.
-template <int TILE_BITS, typename LT, bool FAST, int SUBC>
+//
+// KEYS: the segments hold ready (screen * T + bin) keys (the cold events of the
+// SPLIT strategy) and the chunk count is read from n_chunks_dev.
+template <int TILE_BITS, typename LT, bool FAST, int SUBC, bool KEYS>
 __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_partition(
-    const SegDesc *__restrict__ segs, int n_segs, long long n_chunks, const LT *__restrict__ lut,
+    const SegDesc *__restrict__ segs, int n_segs, long long n_chunks,
+    const long long *__restrict__ n_chunks_dev, const LT *__restrict__ lut,
     int pid_off, unsigned L, const unsigned char *__restrict__ g_tab, ToaParams tp, int n_tiles,
     uint16_t *__restrict__ pages, uint32_t *__restrict__ page_tile, uint32_t *__restrict__ page_cnt,
     uint32_t *__restrict__ pool_used, int cap, uint32_t *__restrict__ overflow) {
@@ -118,7 +127,8 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_part
     uint32_t *s_pool = s_w + 32;
     unsigned char *s_tab = reinterpret_cast<unsigned char *>(s_pool + 4);
     const uint32_t pool_base = (uint32_t)blockIdx.x * (uint32_t)cap;
-    load_toa_tables(s_tab, g_tab, tp);
+    if (KEYS) n_chunks = *n_chunks_dev;
+    else load_toa_tables(s_tab, g_tab, tp);
     for (int i = threadIdx.x; i < 2 * ncnt; i += blockDim.x) s_cnt0[i] = 0;
     for (int t = threadIdx.x; t < n_tiles; t += blockDim.x) {
         s_fill[t] = 0;
@@ -136,14 +146,19 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_part
     ChunkRegs nxt;
     // prologue: keys of the first chunk, events of the second in flight
     if ((long long)blockIdx.x < n_chunks) {
-        load_chunk_global(segs, n_segs, blockIdx.x, pid_off, nxt);
+        load_chunk_global<KEYS>(segs, n_segs, blockIdx.x, pid_off, nxt);
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
-            key[e] = lut_raw(lut, (unsigned)nxt.p[e] - (unsigned)pid_off, L);
-            rank[e] = (uint32_t)toa_bin<FAST>(nxt.t[e], s_tab, tp);
+            if (KEYS) {
+                key[e] = nxt.p[e];
+                rank[e] = 0;
+            } else {
+                key[e] = lut_raw(lut, (unsigned)nxt.p[e] - (unsigned)pid_off, L);
+                rank[e] = (uint32_t)toa_bin<FAST>(nxt.t[e], s_tab, tp);
+            }
         }
         if ((long long)blockIdx.x + gridDim.x < n_chunks)
-            load_chunk_global(segs, n_segs, blockIdx.x + gridDim.x, pid_off, nxt);
+            load_chunk_global<KEYS>(segs, n_segs, blockIdx.x + gridDim.x, pid_off, nxt);
     }
     int parity = 0;
     for (long long c = blockIdx.x; c < n_chunks; c += gridDim.x, parity ^= 1) {
@@ -151,9 +166,11 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_part
         // ---- R: finish the keys (the gathers were issued one phase earlier), rank
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
-            const int base = raw_base(lut, key[e], tp.T);
-            const int b = (int)rank[e];
-            key[e] = (base < 0 || b < 0) ? -1 : base + b;
+            if (!KEYS) {
+                const int base = raw_base(lut, key[e], tp.T);
+                const int b = (int)rank[e];
+                key[e] = (base < 0 || b < 0) ? -1 : base + b;
+            }
             rank[e] = 0;
             if (key[e] >= 0) rank[e] = atomicAdd(&s_cnt[(key[e] >> TILE_BITS) * SUBC + sub], 1u);
         }
@@ -234,11 +251,15 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_part
         if (c + gridDim.x < n_chunks) {
 #pragma unroll
             for (int e = 0; e < EPT; ++e) {
-                key[e] = lut_raw(lut, (unsigned)nxt.p[e] - (unsigned)pid_off, L);
-                rank[e] = (uint32_t)toa_bin<FAST>(nxt.t[e], s_tab, tp);
+                if (KEYS) {
+                    key[e] = nxt.p[e];
+                } else {
+                    key[e] = lut_raw(lut, (unsigned)nxt.p[e] - (unsigned)pid_off, L);
+                    rank[e] = (uint32_t)toa_bin<FAST>(nxt.t[e], s_tab, tp);
+                }
             }
             if (c + 2LL * gridDim.x < n_chunks)
-                load_chunk_global(segs, n_segs, c + 2LL * gridDim.x, pid_off, nxt);
+                load_chunk_global<KEYS>(segs, n_segs, c + 2LL * gridDim.x, pid_off, nxt);
         }
         __syncthreads();
         // ---- W: full 8-groups to the pages (runs start 8-aligned in staging)
@@ -525,14 +546,16 @@ __global__ __launch_bounds__(kTileThreads) void k_page_accumulate(
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
-template <int TB, typename LT, bool FAST, int SUBC>
-static hipError_t launch_paged_t(const PagedArgs &a, const LT *lut, hipStream_t st) {
+template <int TB, typename LT, bool FAST, int SUBC, bool KEYS = false>
+static hipError_t launch_paged_t(const PagedArgs &a, const LT *lut, hipStream_t st,
+                                 const long long *n_chunks_dev = nullptr) {
     const size_t sm = paged_smem(a.n_tiles, SUBC, a.tp);
-    (void)hipFuncSetAttribute((const void *)k_paged_partition<TB, LT, FAST, SUBC>,
+    (void)hipFuncSetAttribute((const void *)k_paged_partition<TB, LT, FAST, SUBC, KEYS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipLaunchKernelGGL((k_paged_partition<TB, LT, FAST, SUBC>), dim3(a.grid), dim3(kPartThreads),
-                       sm, st, a.segs, a.n_segs, a.n_chunks, lut, a.pid_off, a.L, a.tab, a.tp,
-                       a.n_tiles, a.pages, a.page_tile, a.page_cnt, a.pool_used, a.cap, a.overflow);
+    hipLaunchKernelGGL((k_paged_partition<TB, LT, FAST, SUBC, KEYS>), dim3(a.grid),
+                       dim3(kPartThreads), sm, st, a.segs, a.n_segs, a.n_chunks, n_chunks_dev, lut,
+                       a.pid_off, a.L, a.tab, a.tp, a.n_tiles, a.pages, a.page_tile, a.page_cnt,
+                       a.pool_used, a.cap, a.overflow);
     return hipGetLastError();
 }
 
@@ -556,6 +579,21 @@ hipError_t launch_paged_partition(const PagedArgs &a, hipStream_t st) {
     case 13: return launch_paged_tb<13>(a, st);
     case 14: return launch_paged_tb<14>(a, st);
     case 15: return launch_paged_tb<15>(a, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int TB>
+static hipError_t launch_paged_keys_tb(const PagedArgs &a, const long long *nc, hipStream_t st) {
+    return a.subc == 4 ? launch_paged_t<TB, uint16_t, true, 4, true>(a, nullptr, st, nc)
+                       : launch_paged_t<TB, uint16_t, true, 1, true>(a, nullptr, st, nc);
+}
+
+hipError_t launch_paged_keys(const PagedArgs &a, const long long *n_chunks_dev, hipStream_t st) {
+    switch (a.tile_bits) {
+    case 13: return launch_paged_keys_tb<13>(a, n_chunks_dev, st);
+    case 14: return launch_paged_keys_tb<14>(a, n_chunks_dev, st);
+    case 15: return launch_paged_keys_tb<15>(a, n_chunks_dev, st);
     default: return hipErrorInvalidValue;
     }
 }

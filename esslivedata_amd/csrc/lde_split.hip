@@ -1,0 +1,441 @@
+// lde_split.hip -- SPLIT strategy: hot screen rows privatized in LDS, cold
+// remainder through the paged partition in key mode.
+//
+// Detector event streams are skewed (DREAM: Zipf pixel intensities; the top
+// 1 % of pixels carry more than half of the events).
+// The screen pixels that receive most events get a full TOA row (T u32
+// counters) in every block's LDS, so their events cost one LDS atomic and
+// nothing else.  Everything else ("cold") is appended as a 4-byte
+// (screen*T + bin) key to a block-private region and binned by the PAGED pass
+// A in key mode + the usual page plan and pass B.
+//
+//   k_sample_screens : per-screen event counts of a few sampled chunks (LDS)
+//   k_screen_sum     : column sums of the samples
+//   k_select_hot     : top-H screens -> row numbers (single block)
+//   k_build_hot_lut  : u32 LUT of one replica: (hot row + 1) << 22 | screen
+//   k_split          : the event pass (one read of pid + toa per event)
+//   k_hot_reduce     : per-block hot rows summed into the window
+//   k_cold_segs      : segment table of the cold regions for pass A (keys)
+//
+// The hot set is a performance hint only: every event lands in the same bin
+// whether its row is hot or cold, so the counts stay bit-exact whatever the
+// sample picked.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lde_device.h"
+#include "lde_internal.h"
+
+namespace lde {
+
+namespace {
+
+template <int THREADS, int EPT, bool WITH_TOA>
+__device__ __forceinline__ void load_chunk_t(const SegDesc *__restrict__ segs, int n_segs,
+                                             long long c, int fill, int (&p)[EPT], int (&t)[EPT]) {
+    int lo = 0, hi = n_segs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+    }
+    const SegDesc sd = segs[lo];
+    const long long base = (c - sd.chunk0) * kChunk;
+    const uintptr_t align = WITH_TOA ? ((uintptr_t)sd.pid | (uintptr_t)sd.toa) : (uintptr_t)sd.pid;
+    const bool vec = (align & 15u) == 0;
+#pragma unroll
+    for (int j = 0; j < EPT / 4; ++j) {
+        const long long e0 = base + ((long long)j * THREADS + threadIdx.x) * 4;
+        if (vec && e0 + 3 < sd.n) {
+            const v4i pv = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.pid + e0));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) p[j * 4 + q] = pv[q];
+            if (WITH_TOA) {
+                const v4i tv = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.toa + e0));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) t[j * 4 + q] = tv[q];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool ok = e0 + q < sd.n;
+                p[j * 4 + q] = ok ? sd.pid[e0 + q] : fill;
+                if (WITH_TOA) t[j * 4 + q] = ok ? sd.toa[e0 + q] : 0;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ int screen_of(const uint16_t *__restrict__ lut, unsigned p, int) {
+    const unsigned v = lut[p];
+    return v == 0xFFFFu ? -1 : (int)v;
+}
+__device__ __forceinline__ int screen_of(const int *__restrict__ lut, unsigned p, int T) {
+    const int v = lut[p];
+    return v < 0 ? -1 : v / T;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// hot-set selection
+// ---------------------------------------------------------------------------
+template <typename LT>
+__global__ __launch_bounds__(kSplitThreads) void k_sample_screens(
+    const SegDesc *__restrict__ segs, int n_segs, long long n_chunks, const LT *__restrict__ lut,
+    int pid_off, unsigned L, int T, int S, uint32_t *__restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_cnt[];
+    for (int i = threadIdx.x; i < S; i += kSplitThreads) s_cnt[i] = 0;
+    __syncthreads();
+    const long long c = (long long)blockIdx.x * n_chunks / gridDim.x;
+    int p[kSplitEPT], t[kSplitEPT];
+    load_chunk_t<kSplitThreads, kSplitEPT, false>(segs, n_segs, c, pid_off - 1, p, t);
+#pragma unroll
+    for (int e = 0; e < kSplitEPT; ++e) {
+        const unsigned q = (unsigned)p[e] - (unsigned)pid_off;
+        const int s = q < L ? screen_of(lut, q, T) : -1;
+        if (s >= 0) atomicAdd(&s_cnt[s], 1u);
+    }
+    __syncthreads();
+    uint32_t *dst = part + (size_t)blockIdx.x * S;
+    for (int i = threadIdx.x; i < S; i += kSplitThreads) dst[i] = s_cnt[i];
+}
+
+__global__ __launch_bounds__(256) void k_screen_sum(const uint32_t *__restrict__ part, int rows,
+                                                    int S, uint32_t *__restrict__ cnt) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    uint32_t v = 0;
+    for (int r = 0; r < rows; ++r) v += part[(size_t)r * S + s];
+    cnt[s] = v;
+}
+
+// Top-H screens by sampled count.  Counts fall into log2 classes; every class
+// above the one that overflows H is taken whole, the overflowing class is
+// taken in screen order.  stats = {sampled events, events in hot rows, rows}.
+__global__ __launch_bounds__(1024) void k_select_hot(const uint32_t *__restrict__ cnt, int S,
+                                                     int H, uint16_t *__restrict__ screen_row,
+                                                     uint32_t *__restrict__ row_screen,
+                                                     uint32_t *__restrict__ stats) {
+    __shared__ uint32_t s_cls[33];
+    __shared__ uint32_t s_w[32];
+    __shared__ uint32_t s_sel[4];
+    const int tid = threadIdx.x;
+    if (tid < 33) s_cls[tid] = 0;
+    __syncthreads();
+    const int per = (S + 1023) / 1024;
+    const int s0 = min(S, tid * per), s1 = min(S, s0 + per);
+    uint32_t tot = 0;
+    for (int s = s0; s < s1; ++s) {
+        const uint32_t c = cnt[s];
+        tot += c;
+        if (c) atomicAdd(&s_cls[32 - __clz(c)], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        int k = 32;
+        for (; k >= 1; --k) {
+            if (acc + s_cls[k] > (uint32_t)H) break;
+            acc += s_cls[k];
+        }
+        s_sel[0] = (uint32_t)(k < 1 ? 0 : k);  // class taken partially (0: none)
+        s_sel[1] = acc;                        // screens taken in full
+    }
+    __syncthreads();
+    const uint32_t kpart = s_sel[0], full = s_sel[1];
+    auto cls = [](uint32_t c) { return c ? (uint32_t)(32 - __clz(c)) : 0u; };
+    uint32_t n1 = 0, n2 = 0;
+    for (int s = s0; s < s1; ++s) {
+        const uint32_t k = cls(cnt[s]);
+        n1 += (k > kpart && k > 0) ? 1u : 0u;
+        n2 += (kpart > 0 && k == kpart) ? 1u : 0u;
+    }
+    uint32_t t1, t2;
+    uint32_t o1 = block_exclusive_scan(n1, s_w, &t1);
+    __syncthreads();
+    uint32_t o2 = block_exclusive_scan(n2, s_w, &t2);
+    const uint32_t room = (uint32_t)H - full;
+    uint32_t hot = 0;
+    for (int s = s0; s < s1; ++s) {
+        const uint32_t c = cnt[s];
+        const uint32_t k = cls(c);
+        uint32_t row = 0xFFFFFFFFu;
+        if (k > kpart && k > 0) {
+            row = o1++;
+        } else if (kpart > 0 && k == kpart) {
+            if (o2 < room) row = full + o2;
+            ++o2;
+        }
+        if (row != 0xFFFFFFFFu) {
+            screen_row[s] = (uint16_t)(row + 1);
+            row_screen[row] = (uint32_t)s;
+            hot += c;
+        } else {
+            screen_row[s] = 0;
+        }
+    }
+    __syncthreads();
+    uint32_t ht;
+    (void)block_exclusive_scan(hot, s_w, &ht);
+    __syncthreads();
+    uint32_t tt;
+    (void)block_exclusive_scan(tot, s_w, &tt);
+    if (tid == 0) {
+        stats[0] = tt;
+        stats[1] = ht;
+        stats[2] = min(t1 + min(t2, room), (uint32_t)H);
+    }
+}
+
+template <typename LT>
+__global__ __launch_bounds__(256) void k_build_hot_lut(const LT *__restrict__ lut, long long L,
+                                                       int T, const uint16_t *__restrict__ screen_row,
+                                                       uint32_t *__restrict__ hlut) {
+    const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (p >= L) return;
+    const int s = screen_of(lut, (unsigned)p, T);
+    hlut[p] = s < 0 ? kHotDrop : (((uint32_t)screen_row[s] << kHotRowShift) | (uint32_t)s);
+}
+
+// ---------------------------------------------------------------------------
+// the event pass
+// ---------------------------------------------------------------------------
+// Pixel cache: a direct-mapped LDS cache of hot-LUT entries, private to the
+// block and filled by the block itself.  Slot = q mod C, one u32 word:
+//   tag (q / C) << (row_bits + screen_bits) | (row + 1) << screen_bits | screen
+// (0xFFFFFFFF = empty; a valid word keeps bit 31 clear).  A miss reads the
+// global hot LUT and installs the entry with probability 1/8, so the pixels
+// that miss most often (the hot ones of a skewed stream) end up resident and
+// the L2 gather rate stops bounding the pass.
+struct PixelCache {
+    int cbits;        // log2 C (0: no cache)
+    int screen_bits;
+    int tag_shift;    // row_bits + screen_bits
+};
+
+template <bool FAST, bool CACHE>
+__global__ __launch_bounds__(kSplitThreads) void k_split(
+    const SegDesc *__restrict__ segs, int n_segs, long long n_chunks,
+    const uint32_t *__restrict__ hlut, int pid_off, unsigned L,
+    const unsigned char *__restrict__ g_tab, ToaParams tp, int ht4, PixelCache pc,
+    uint32_t *__restrict__ hot_part, uint32_t *__restrict__ cold, long long cold_cap,
+    uint32_t *__restrict__ cold_cnt, int ablate) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *s_hot = reinterpret_cast<uint32_t *>(smem);
+    uint32_t *s_pc = s_hot + ht4;
+    const int n_pc = CACHE ? (1 << pc.cbits) : 0;
+    uint32_t *s_cur = s_pc + n_pc;
+    unsigned char *s_tab = reinterpret_cast<unsigned char *>(s_cur + 4);
+    const int tid = threadIdx.x;
+    for (int i = tid * 4; i < ht4; i += kSplitThreads * 4)
+        *reinterpret_cast<uint4 *>(s_hot + i) = make_uint4(0, 0, 0, 0);
+    if (CACHE)
+        for (int i = tid * 4; i < n_pc; i += kSplitThreads * 4)
+            *reinterpret_cast<uint4 *>(s_pc + i) =
+                make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    if (tid == 0) s_cur[0] = 0;
+    load_toa_tables(s_tab, g_tab, tp);
+    __syncthreads();
+    uint32_t *my_cold = cold + (size_t)blockIdx.x * (size_t)cold_cap;
+    const int T = tp.T;
+    const uint32_t cmask = (uint32_t)n_pc - 1u;
+    const uint32_t smask = (1u << pc.screen_bits) - 1u;
+    const uint32_t rmask = (1u << (pc.tag_shift - pc.screen_bits)) - 1u;
+
+    // stage 2 of the pipeline: LUT entry (cache, else global gather) + TOA bin
+    auto lookup = [&](const int (&p)[kSplitEPT], const int (&t)[kSplitEPT], long long salt,
+                      uint32_t (&v)[kSplitEPT], int (&b)[kSplitEPT]) {
+#pragma unroll
+        for (int e = 0; e < kSplitEPT; ++e) {
+            const unsigned q = (unsigned)p[e] - (unsigned)pid_off;
+            const bool inr = q < L;
+            if (ablate & 1) {  // timing ablation only: no gather
+                v[e] = (q & 1023u) < 768u ? ((1u + q % 300u) << kHotRowShift) : (q & 0x3FFFu);
+            } else if (CACHE) {
+                const uint32_t w = s_pc[q & cmask];
+                const bool hit = inr && w != 0xFFFFFFFFu && (w >> pc.tag_shift) == (q >> pc.cbits);
+                if (hit) {
+                    v[e] = (((w >> pc.screen_bits) & rmask) << kHotRowShift) | (w & smask);
+                } else {
+                    v[e] = inr ? hlut[q] : kHotDrop;
+                    if (inr && v[e] != kHotDrop &&
+                        ((q * 0x9E3779B1u + (uint32_t)salt * 0x85EBCA6Bu) >> 29) == 0u)
+                        s_pc[q & cmask] = ((q >> pc.cbits) << pc.tag_shift) |
+                                          ((v[e] >> kHotRowShift) << pc.screen_bits) |
+                                          (v[e] & kHotBaseMask);
+                }
+            } else {
+                v[e] = inr ? hlut[q] : kHotDrop;
+            }
+            b[e] = (ablate & 8) ? (t[e] & 63) : toa_bin<FAST>(t[e], s_tab, tp);
+        }
+    };
+
+    // pipeline: events of chunk c+2G stream in while c+G is looked up and c is binned
+    int p[kSplitEPT], t[kSplitEPT];
+    uint32_t v[kSplitEPT];
+    int b[kSplitEPT];
+    const long long G = gridDim.x;
+    long long c = blockIdx.x;
+    if (c < n_chunks) {
+        load_chunk_t<kSplitThreads, kSplitEPT, true>(segs, n_segs, c, pid_off - 1, p, t);
+        lookup(p, t, c, v, b);
+        if (c + G < n_chunks)
+            load_chunk_t<kSplitThreads, kSplitEPT, true>(segs, n_segs, c + G, pid_off - 1, p, t);
+    }
+    for (; c < n_chunks; c += G) {
+        uint32_t key[kSplitEPT];
+        unsigned long long bal[kSplitEPT];
+        uint32_t pre[kSplitEPT];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int e = 0; e < kSplitEPT; ++e) {
+            const bool ok = v[e] != kHotDrop && b[e] >= 0;
+            const uint32_t row = v[e] >> kHotRowShift;
+            key[e] = (v[e] & kHotBaseMask) * (uint32_t)T + (uint32_t)b[e];
+            if (ok && row != 0u && !(ablate & 2))
+                atomicAdd(&s_hot[(row - 1u) * (uint32_t)T + (uint32_t)b[e]], 1u);
+            bal[e] = __ballot(ok && row == 0u);
+            pre[e] = tot;
+            tot += (uint32_t)__popcll(bal[e]);
+        }
+        if (tot && !(ablate & 4)) {
+            uint32_t wbase = 0;
+            if ((tid & 63) == 0) wbase = atomicAdd(s_cur, tot);
+            wbase = (uint32_t)__builtin_amdgcn_readfirstlane(wbase);
+#pragma unroll
+            for (int e = 0; e < kSplitEPT; ++e)
+                if ((bal[e] >> (tid & 63)) & 1ull) my_cold[wbase + pre[e] + lanes_below(bal[e])] = key[e];
+        }
+        if (c + G < n_chunks) {
+            lookup(p, t, c + G, v, b);
+            if (c + 2 * G < n_chunks)
+                load_chunk_t<kSplitThreads, kSplitEPT, true>(segs, n_segs, c + 2 * G, pid_off - 1, p, t);
+        }
+    }
+    __syncthreads();
+    uint32_t *dst = hot_part + (size_t)blockIdx.x * ht4;
+    for (int i = tid * 4; i < ht4; i += kSplitThreads * 4)
+        *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(s_hot + i);
+    if (tid == 0) cold_cnt[blockIdx.x] = s_cur[0];
+}
+
+// window[row_screen[row] * T + b] += sum over blocks of hot_part[.][row * T + b]
+__global__ __launch_bounds__(256) void k_hot_reduce(const uint32_t *__restrict__ hot_part,
+                                                    int rows, int ht, int ht4, int T,
+                                                    int rows_per_slice,
+                                                    const uint32_t *__restrict__ row_screen,
+                                                    uint32_t *__restrict__ win) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= ht) return;
+    const int j0 = blockIdx.y * rows_per_slice;
+    const int j1 = min(rows, j0 + rows_per_slice);
+    uint32_t sum = 0;
+    for (int j = j0; j < j1; ++j) sum += hot_part[(size_t)j * ht4 + i];
+    if (sum) {
+        const int row = i / T;
+        atomicAdd(win + (size_t)row_screen[row] * T + (i - row * T), sum);
+    }
+}
+
+// segment table of the cold regions (one per split block) for pass A in key mode
+__global__ __launch_bounds__(1024) void k_cold_segs(const uint32_t *__restrict__ cold_cnt, int rows,
+                                                    const uint32_t *__restrict__ cold,
+                                                    long long cold_cap, SegDesc *__restrict__ segs,
+                                                    long long *__restrict__ n_chunks) {
+    __shared__ uint32_t s_w[32];
+    uint32_t carry = 0;
+    for (int r0 = 0; r0 < rows; r0 += 1024) {
+        const int r = r0 + threadIdx.x;
+        const uint32_t n = r < rows ? cold_cnt[r] : 0u;
+        const uint32_t ch = (n + kChunk - 1) / kChunk;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(ch, s_w, &tot);
+        if (r < rows) {
+            SegDesc d;
+            d.pid = reinterpret_cast<const int *>(cold + (size_t)r * (size_t)cold_cap);
+            d.toa = nullptr;
+            d.n = n;
+            d.chunk0 = carry + ex;
+            segs[r] = d;
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *n_chunks = carry;
+}
+
+// ---------------------------------------------------------------------------
+// launch wrappers
+// ---------------------------------------------------------------------------
+size_t split_smem(int ht4, int cache_words, const ToaParams &tp) {
+    return (size_t)ht4 * 4 + (size_t)cache_words * 4 + 16 + toa_lds_bytes(tp);
+}
+
+hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st) {
+    const size_t sm = (size_t)a.S * 4;
+    const void *lut_r = a.lut16 ? (const void *)((const uint16_t *)a.lut + (size_t)replica * a.L)
+                                : (const void *)((const int *)a.lut + (size_t)replica * a.L);
+    if (a.lut16) {
+        (void)hipFuncSetAttribute((const void *)k_sample_screens<uint16_t>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL(k_sample_screens<uint16_t>, dim3(a.sample_blocks), dim3(kSplitThreads), sm,
+                           st, a.segs, a.n_segs, a.n_chunks, (const uint16_t *)lut_r, a.pid_off,
+                           (unsigned)a.L, a.tp.T, a.S, a.sample_part);
+    } else {
+        (void)hipFuncSetAttribute((const void *)k_sample_screens<int>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL(k_sample_screens<int>, dim3(a.sample_blocks), dim3(kSplitThreads), sm, st,
+                           a.segs, a.n_segs, a.n_chunks, (const int *)lut_r, a.pid_off,
+                           (unsigned)a.L, a.tp.T, a.S, a.sample_part);
+    }
+    hipLaunchKernelGGL(k_screen_sum, dim3((a.S + 255) / 256), dim3(256), 0, st, a.sample_part,
+                       a.sample_blocks, a.S, a.screen_cnt);
+    hipLaunchKernelGGL(k_select_hot, dim3(1), dim3(1024), 0, st, a.screen_cnt, a.S, a.rows,
+                       a.screen_row, a.row_screen, a.stats);
+    const unsigned g = (unsigned)((a.L + 255) / 256);
+    if (a.lut16)
+        hipLaunchKernelGGL(k_build_hot_lut<uint16_t>, dim3(g), dim3(256), 0, st,
+                           (const uint16_t *)lut_r, a.L, a.tp.T, a.screen_row, a.hlut);
+    else
+        hipLaunchKernelGGL(k_build_hot_lut<int>, dim3(g), dim3(256), 0, st, (const int *)lut_r, a.L,
+                           a.tp.T, a.screen_row, a.hlut);
+    return hipGetLastError();
+}
+
+template <bool FAST, bool CACHE>
+static hipError_t launch_split_t(const SplitArgs &a, hipStream_t st) {
+    const int ht4 = align4(a.rows * a.tp.T);
+    PixelCache pc;
+    pc.cbits = a.cache_bits;
+    pc.screen_bits = a.screen_bits;
+    pc.tag_shift = a.screen_bits + a.row_bits;
+    const size_t sm = split_smem(ht4, CACHE ? (1 << a.cache_bits) : 0, a.tp);
+    (void)hipFuncSetAttribute((const void *)k_split<FAST, CACHE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    hipLaunchKernelGGL((k_split<FAST, CACHE>), dim3(a.grid), dim3(kSplitThreads), sm, st, a.segs,
+                       a.n_segs, a.n_chunks, a.hlut, a.pid_off, (unsigned)a.L, a.tab, a.tp, ht4, pc,
+                       a.hot_part, a.cold, a.cold_cap, a.cold_cnt, a.ablate);
+    return hipGetLastError();
+}
+
+hipError_t launch_split(const SplitArgs &a, hipStream_t st) {
+    if (a.tp.fast)
+        return a.cache_bits > 0 ? launch_split_t<true, true>(a, st) : launch_split_t<true, false>(a, st);
+    return a.cache_bits > 0 ? launch_split_t<false, true>(a, st) : launch_split_t<false, false>(a, st);
+}
+
+hipError_t launch_split_tail(const SplitArgs &a, uint32_t *win, SegDesc *cold_segs,
+                             long long *n_cold_chunks, hipStream_t st) {
+    const int ht = a.rows * a.tp.T;
+    const int ht4 = align4(ht);
+    const int slices = 8;
+    const int per = (a.grid + slices - 1) / slices;
+    hipLaunchKernelGGL(k_hot_reduce, dim3((ht + 255) / 256, slices), dim3(256), 0, st, a.hot_part,
+                       a.grid, ht, ht4, a.tp.T, per, a.row_screen, win);
+    hipLaunchKernelGGL(k_cold_segs, dim3(1), dim3(1024), 0, st, a.cold_cnt, a.grid, a.cold,
+                       a.cold_cap, cold_segs, n_cold_chunks);
+    return hipGetLastError();
+}
+
+}  // namespace lde

@@ -53,6 +53,7 @@ extern "C" {
 #define LDE_STRATEGY_ATOMIC 1      /* one pass, global atomics             */
 #define LDE_STRATEGY_PARTITION 2   /* tile partition (chunk-major runs) + LDS sub-histograms */
 #define LDE_STRATEGY_PAGED 3       /* tile partition into per-block page chains + LDS sub-histograms */
+#define LDE_STRATEGY_SPLIT 4       /* hot screen rows in LDS + cold remainder through PAGED (skewed streams) */
 
 /* histogram selectors for lde_read_histogram */
 #define LDE_CURRENT 0    /* window since the last finalize  (accumulators.py:138-163) */
@@ -159,7 +160,9 @@ int lde_synchronize(lde_handle *h);
 #define LDE_K_PAGED 7     /* k_paged_partition: PAGED pass A                  */
 #define LDE_K_PAGE_PLAN 8 /* k_page_count/scan/plan/scatter                   */
 #define LDE_K_PAGE_ACC 9  /* k_page_accumulate: PAGED pass B                  */
-#define LDE_K_COUNT 10
+#define LDE_K_SPLIT 10    /* k_split: SPLIT event pass (hot rows in LDS, cold keys out) */
+#define LDE_K_SPLIT_AUX 11 /* hot-set selection, hot-row reduce, cold segment table */
+#define LDE_K_COUNT 12
 int lde_timing_enable(lde_handle *h, int32_t enable);
 int lde_kernel_stats(lde_handle *h, int32_t kernel_id, double *ms, int64_t *launches);
 

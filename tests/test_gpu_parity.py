@@ -11,7 +11,7 @@ from oracle import scipp_semantics as ora
 
 pytestmark = pytest.mark.gpu
 
-STRATEGIES = ['atomic', 'partition', 'paged']
+STRATEGIES = ['atomic', 'partition', 'paged', 'split']
 
 # internal kernel variants that must all be bit-identical
 VARIANTS = [
@@ -22,6 +22,13 @@ VARIANTS = [
     {'LDE_SUBC': '1'},
     {'LDE_TILE_BITS': '15', 'LDE_PART_GRID': '7'},
     {'LDE_TILE_BITS': '13', 'LDE_PART_GRID': '3'},  # long per-block page chains + tails
+    # SPLIT: few hot rows (mostly cold keys), few split blocks (long cold regions),
+    # hot set re-selected every batch
+    {'LDE_HOT_ROWS': '8', 'LDE_SPLIT_GRID': '3', 'LDE_HOT_REFRESH': '1'},
+    # SPLIT pixel cache: off, tiny (constant tag conflicts), large
+    {'LDE_PIXEL_CACHE_BITS': '0'},
+    {'LDE_PIXEL_CACHE_BITS': '6', 'LDE_SPLIT_GRID': '17'},
+    {'LDE_PIXEL_CACHE_BITS': '15'},
 ]
 
 
@@ -298,3 +305,32 @@ def test_device_staging_matches_host_staging(strategy):
         toa_edges_ns=edges,
     )
     np.testing.assert_array_equal(a.read_histogram(), o.batch_histogram(pid, toa, 1))
+
+
+def test_auto_picks_split_for_skewed_and_paged_for_uniform():
+    """AUTO: the sampled hot-row coverage decides (performance only; counts exact)."""
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.dream_mantle()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges)
+    pid, toa = synthetic.dream_events(3_000_000, inst, seed=11)
+    eng.stage(pid, toa)
+    eng.accumulate(3)
+    assert eng.info()['last_strategy'] == 'split'
+    exp = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=_oracle_pixel_screen_geometric(inst),
+        screen_shape=(80, 320),
+        toa_edges_ns=edges,
+    ).batch_histogram(pid, toa, 3)
+    np.testing.assert_array_equal(eng.read_histogram(), exp)
+
+    inst = synthetic.loki_bank0()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    eng = _engine(view, inst.edges.edges_ns())
+    pid, toa = synthetic.uniform_events(3_000_000, 1, 802816, seed=5)
+    eng.stage(pid, toa)
+    eng.accumulate(0)
+    assert eng.info()['last_strategy'] == 'paged'
