@@ -50,8 +50,8 @@ __global__ __launch_bounds__(256) void k_bin_atomic(const SegDesc seg, const LT 
     if ((((uintptr_t)seg.pid | (uintptr_t)seg.toa) & 15u) == 0) {
         const long long n4 = n >> 2;
         for (long long i = i0; i < n4; i += stride) {
-            const v4i p = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(seg.pid) + i);
-            const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(seg.toa) + i);
+            const v4i p = ld_stream4(seg.pid + 4 * i);
+            const v4i t = ld_stream4(seg.toa + 4 * i);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int k = event_key<LT, FAST>(p[q], t[q], lut, pid_off, L, smem, tp);
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_bin_atomic(const SegDesc seg, const LT 
         tail = n4 << 2;
     }
     for (long long i = tail + i0; i < n; i += stride) {
-        const int k = event_key<LT, FAST>(seg.pid[i], seg.toa[i], lut, pid_off, L, smem, tp);
+        const int k = event_key<LT, FAST>(ld_global(seg.pid + i), ld_global(seg.toa + i), lut, pid_off, L, smem, tp);
         if (k >= 0) atomicAdd(hist + k, 1u);
     }
 }
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(256) void k_monitor(const SegDesc seg,
     if (((uintptr_t)seg.toa & 15u) == 0) {
         const long long n4 = n >> 2;
         for (long long i = i0; i < n4; i += stride) {
-            const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(seg.toa) + i);
+            const v4i t = ld_stream4(seg.toa + 4 * i);
             add(t[0]);
             add(t[1]);
             add(t[2]);
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256) void k_monitor(const SegDesc seg,
         }
         tail = n4 << 2;
     }
-    for (long long i = tail + i0; i < n; i += stride) add(seg.toa[i]);
+    for (long long i = tail + i0; i < n; i += stride) add(ld_global(seg.toa + i));
     __syncthreads();
     for (int b = threadIdx.x; b < tp.T; b += blockDim.x) {
         uint32_t v = 0;

@@ -10,6 +10,17 @@ namespace lde {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
+// Event arrays arrive as generic pointers inside segment descriptors; loads
+// through them would compile to flat_load, which the waitcnt logic cannot
+// order (every use waits for vmcnt(0) and lgkmcnt(0), which serializes the
+// chunk prefetch).  These casts make them global_load.
+typedef __attribute__((address_space(1))) const v4i g_v4i;
+typedef __attribute__((address_space(1))) const int g_int;
+__device__ __forceinline__ v4i ld_stream4(const int *p) {
+    return __builtin_nontemporal_load((const g_v4i *)p);
+}
+__device__ __forceinline__ int ld_global(const int *p) { return *(const g_int *)p; }
+
 // ---------------------------------------------------------------------------
 // TOA lookup
 // ---------------------------------------------------------------------------
@@ -128,8 +139,8 @@ __device__ __forceinline__ void load_chunk(const SegDesc *s_seg, int n_segs, lon
     for (int j = 0; j < kPartEventsPerThread / 4; ++j) {
         const long long e0 = base + ((long long)j * kPartThreads + tid) * 4;
         if (vec && e0 + 3 < sd.n) {
-            const v4i p = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.pid + e0));
-            const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.toa + e0));
+            const v4i p = ld_stream4(sd.pid + e0);
+            const v4i t = ld_stream4(sd.toa + e0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 r.p[j * 4 + q] = p[q];
@@ -139,8 +150,8 @@ __device__ __forceinline__ void load_chunk(const SegDesc *s_seg, int n_segs, lon
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const bool ok = e0 + q < sd.n;
-                r.p[j * 4 + q] = ok ? sd.pid[e0 + q] : pid_off - 1;  // outside the LUT: dropped
-                r.t[j * 4 + q] = ok ? sd.toa[e0 + q] : 0;
+                r.p[j * 4 + q] = ok ? ld_global(sd.pid + e0 + q) : pid_off - 1;  // outside the LUT: dropped
+                r.t[j * 4 + q] = ok ? ld_global(sd.toa + e0 + q) : 0;
             }
         }
     }

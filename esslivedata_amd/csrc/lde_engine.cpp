@@ -130,6 +130,7 @@ struct lde_handle {
     uint32_t *d_cold_cnt = nullptr;
     lde::SegDesc *d_cold_segs = nullptr;
     long long *d_cold_chunks = nullptr;
+    int *d_dummy = nullptr;  // 64 zero bytes
 
     // finalize scratch
     unsigned long long *d_tot4 = nullptr;
@@ -552,7 +553,6 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.row_screen = h->d_row_screen + (size_t)lde::kHotMaxRows * replica;
     a.hlut = h->d_hlut + (size_t)h->L * replica;
     a.grid = (int)std::min<long long>(chunks, (long long)h->split_grid);
-    a.ablate = (int)env_ll("LDE_ABLATE", 0);
     int &uses = h->hot_uses[replica];
     if (uses < 0 || uses >= h->hot_refresh) {
         {
@@ -574,7 +574,10 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.screen_bits = h->screen_bits;
     const int ht4 = lde::align4(h->hot_rows * h->T);
     if (int rc = grow(h, &h->d_hot_part, h->hot_part_cap, (size_t)a.grid * ht4)) return rc;
-    if (int rc = grow(h, &h->d_cold, h->cold_total_cap, (size_t)a.grid * a.cold_cap)) return rc;
+    if (int rc = grow(h, &h->d_cold, h->cold_total_cap,
+                      (size_t)a.grid * (size_t)(a.cold_cap + lde::kSplitThreads / 64)))
+        return rc;
+    a.dummy = h->d_dummy;
     a.hot_part = h->d_hot_part;
     a.cold = h->d_cold;
     a.cold_cnt = h->d_cold_cnt;
@@ -788,6 +791,7 @@ void release(lde_handle *h) {
     dev_free(h->d_cold_cnt);
     dev_free(h->d_cold_segs);
     dev_free(h->d_cold_chunks);
+    dev_free(h->d_dummy);
     dev_free(h->d_tot4);
     dev_free(h->d_img_cur);
     dev_free(h->d_img_cum);
@@ -966,12 +970,14 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
             auto bits = [](long long n) { int b = 0; while ((1LL << b) < n) ++b; return b; };
             int cbits = (int)std::max<long long>(0, std::min<long long>(16, env_ll("LDE_PIXEL_CACHE_BITS", 14)));
             if ((1LL << cbits) >= 2 * h->L) cbits = std::max(0, bits(h->L));  // whole LUT fits
+            // LDS budget per split block: 160 KB = one block per CU; 80 KB = two
+            const size_t budget = (size_t)std::max<long long>(32, std::min<long long>(160, env_ll("LDE_SPLIT_SMEM_KB", 160))) * 1024;
             auto rows_for = [&](int cb) {
                 const size_t fixed = lde::split_smem(0, cb ? (1 << cb) : 0, h->tp);
                 int H = 0;
-                if (fixed < lde::kSplitSmemMax)
-                    H = (int)std::min<long long>(lde::kHotMaxRows, (long long)((lde::kSplitSmemMax - fixed) / (4 * (size_t)h->T)));
-                while (H > 0 && lde::split_smem(lde::align4(H * h->T), cb ? (1 << cb) : 0, h->tp) > lde::kSplitSmemMax) --H;
+                if (fixed < budget)
+                    H = (int)std::min<long long>(lde::kHotMaxRows, (long long)((budget - fixed) / (4 * (size_t)h->T)));
+                while (H > 0 && lde::split_smem(lde::align4(H * h->T), cb ? (1 << cb) : 0, h->tp) > budget) --H;
                 return H;
             };
             // the cache never takes the room of the last 64 hot rows
@@ -988,7 +994,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
             if (H >= 8) {
                 h->split_ok = true;
                 h->hot_rows = H;
-                h->split_grid = (int)std::max<long long>(1, env_ll("LDE_SPLIT_GRID", h->cus));
+                h->split_grid = (int)std::max<long long>(
+                    1, env_ll("LDE_SPLIT_GRID", (long long)h->cus * (long long)std::max<size_t>(1, (160 * 1024) / budget)));
                 h->hot_refresh = (int)std::max<long long>(1, env_ll("LDE_HOT_REFRESH", 256));
                 h->split_min_cov = (double)env_ll("LDE_SPLIT_MIN_COV_PCT", 30) / 100.0;
                 h->hot_uses.assign((size_t)h->R, -1);
@@ -1002,6 +1009,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 CREATE_CHECK(dev_alloc(h, &h->d_cold_cnt, (size_t)h->split_grid));
                 CREATE_CHECK(dev_alloc(h, &h->d_cold_segs, (size_t)h->split_grid));
                 CREATE_CHECK(dev_alloc(h, &h->d_cold_chunks, 1));
+                CREATE_CHECK(dev_alloc(h, &h->d_dummy, 16));
+                CREATE_HIP(hipMemset(h->d_dummy, 0, 64));
                 CREATE_HIP(hipHostMalloc((void **)&h->h_sel_stats, 16, hipHostMallocDefault));
             }
         }

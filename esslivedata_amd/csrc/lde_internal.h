@@ -136,8 +136,8 @@ struct SplitArgs {
     uint32_t *cold;
     long long cold_cap;  // keys per block region
     uint32_t *cold_cnt;
-    int ablate;  // timing ablations (LDE_ABLATE), never set in production
     int cache_bits, row_bits, screen_bits;  // LDS pixel cache (cache_bits 0: off)
+    const int *dummy;  // 16-byte aligned zeros: load target of non-live chunk slots
 };
 size_t split_smem(int ht4, int cache_words, const ToaParams &tp);
 hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st);

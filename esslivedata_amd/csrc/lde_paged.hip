@@ -42,11 +42,11 @@ __device__ __forceinline__ void load_chunk_global(const SegDesc *__restrict__ se
     for (int j = 0; j < kPartEventsPerThread / 4; ++j) {
         const long long e0 = base + ((long long)j * kPartThreads + tid) * 4;
         if (vec && e0 + 3 < sd.n) {
-            const v4i p = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.pid + e0));
+            const v4i p = ld_stream4(sd.pid + e0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) r.p[j * 4 + q] = p[q];
             if (!KEYS) {
-                const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.toa + e0));
+                const v4i t = ld_stream4(sd.toa + e0);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) r.t[j * 4 + q] = t[q];
             }
@@ -54,8 +54,8 @@ __device__ __forceinline__ void load_chunk_global(const SegDesc *__restrict__ se
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const bool ok = e0 + q < sd.n;
-                r.p[j * 4 + q] = ok ? sd.pid[e0 + q] : fill;
-                if (!KEYS) r.t[j * 4 + q] = ok ? sd.toa[e0 + q] : 0;
+                r.p[j * 4 + q] = ok ? ld_global(sd.pid + e0 + q) : fill;
+                if (!KEYS) r.t[j * 4 + q] = ok ? ld_global(sd.toa + e0 + q) : 0;
             }
         }
     }

@@ -30,6 +30,9 @@ namespace lde {
 
 namespace {
 
+// Loads one chunk's events.  The vector/element choice is block-uniform (a
+// scalar branch), so no divergent control flow sits between these loads and
+// their uses.
 template <int THREADS, int EPT, bool WITH_TOA>
 __device__ __forceinline__ void load_chunk_t(const SegDesc *__restrict__ segs, int n_segs,
                                              long long c, int fill, int (&p)[EPT], int (&t)[EPT]) {
@@ -41,28 +44,54 @@ __device__ __forceinline__ void load_chunk_t(const SegDesc *__restrict__ segs, i
     const SegDesc sd = segs[lo];
     const long long base = (c - sd.chunk0) * kChunk;
     const uintptr_t align = WITH_TOA ? ((uintptr_t)sd.pid | (uintptr_t)sd.toa) : (uintptr_t)sd.pid;
-    const bool vec = (align & 15u) == 0;
+    if ((align & 15u) == 0 && base + kChunk <= sd.n) {
 #pragma unroll
-    for (int j = 0; j < EPT / 4; ++j) {
-        const long long e0 = base + ((long long)j * THREADS + threadIdx.x) * 4;
-        if (vec && e0 + 3 < sd.n) {
-            const v4i pv = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.pid + e0));
+        for (int j = 0; j < EPT / 4; ++j) {
+            const long long e0 = base + ((long long)j * THREADS + threadIdx.x) * 4;
+            const v4i pv = ld_stream4(sd.pid + e0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) p[j * 4 + q] = pv[q];
             if (WITH_TOA) {
-                const v4i tv = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(sd.toa + e0));
+                const v4i tv = ld_stream4(sd.toa + e0);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) t[j * 4 + q] = tv[q];
             }
-        } else {
+        }
+    } else {
+        // tail chunk or misaligned segment: element loads of a clamped index
+#pragma unroll
+        for (int j = 0; j < EPT / 4; ++j) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const bool ok = e0 + q < sd.n;
-                p[j * 4 + q] = ok ? sd.pid[e0 + q] : fill;
-                if (WITH_TOA) t[j * 4 + q] = ok ? sd.toa[e0 + q] : 0;
+                const long long e = base + ((long long)j * THREADS + threadIdx.x) * 4 + q;
+                const bool ok = e < sd.n;
+                const long long ec = ok ? e : 0;
+                const int pv = ld_global(sd.pid + ec);
+                p[j * 4 + q] = ok ? pv : fill;
+                if (WITH_TOA) {
+                    const int tv = ld_global(sd.toa + ec);
+                    t[j * 4 + q] = ok ? tv : 0;
+                }
             }
         }
     }
+}
+
+// branch-free TOA bin (no early return, so no divergent flow around loads)
+template <bool FAST>
+__device__ __forceinline__ int toa_bin_nb(int t, const unsigned char *s_tab, const ToaParams &tp) {
+    if (FAST) {
+        const unsigned d = (unsigned)t - (unsigned)tp.lo;
+        const bool in = d < tp.span;
+        const unsigned dc = in ? d : 0u;
+        const uint32_t *rthr = reinterpret_cast<const uint32_t *>(s_tab);
+        const uint16_t *bst =
+            reinterpret_cast<const uint16_t *>(s_tab + align16((size_t)(tp.T + 1) * 4));
+        const int b = bst[dc >> tp.shift];
+        const int r = b + (dc >= rthr[b + 1] ? 1 : 0);
+        return in ? r : -1;
+    }
+    return toa_bin<false>(t, s_tab, tp);
 }
 
 __device__ __forceinline__ int screen_of(const uint16_t *__restrict__ lut, unsigned p, int) {
@@ -213,13 +242,23 @@ struct PixelCache {
     int tag_shift;    // row_bits + screen_bits
 };
 
+// The main loop keeps the number of vector-memory instructions per
+// iteration fixed (every chunk slot loads, every lookup gathers, every bin
+// stores), so the compiler's in-order vmcnt accounting can wait for exactly
+// the operation a value comes from instead of draining the queue:
+//   * a chunk that is not a full 16-byte-aligned chunk of its segment (or is
+//     past the end) loads a 16-byte dummy and is binned afterwards by a plain
+//     per-element pass ("deferred");
+//   * cache hits and out-of-range pixels gather entry 0 of the hot LUT (one
+//     shared line) and discard it;
+//   * lanes without a cold key store to a per-wave scratch word.
 template <bool FAST, bool CACHE>
 __global__ __launch_bounds__(kSplitThreads) void k_split(
     const SegDesc *__restrict__ segs, int n_segs, long long n_chunks,
     const uint32_t *__restrict__ hlut, int pid_off, unsigned L,
     const unsigned char *__restrict__ g_tab, ToaParams tp, int ht4, PixelCache pc,
     uint32_t *__restrict__ hot_part, uint32_t *__restrict__ cold, long long cold_cap,
-    uint32_t *__restrict__ cold_cnt, int ablate) {
+    uint32_t *__restrict__ cold_cnt, const int *__restrict__ dummy) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *s_hot = reinterpret_cast<uint32_t *>(smem);
     uint32_t *s_pc = s_hot + ht4;
@@ -236,82 +275,154 @@ __global__ __launch_bounds__(kSplitThreads) void k_split(
     if (tid == 0) s_cur[0] = 0;
     load_toa_tables(s_tab, g_tab, tp);
     __syncthreads();
-    uint32_t *my_cold = cold + (size_t)blockIdx.x * (size_t)cold_cap;
+    // cold region of this block: cold_cap keys, then one scratch word per wave
+    uint32_t *my_cold = cold + (size_t)blockIdx.x * (size_t)(cold_cap + kSplitThreads / 64);
+    uint32_t *my_dump = my_cold + cold_cap + (tid >> 6);
     const int T = tp.T;
     const uint32_t cmask = (uint32_t)n_pc - 1u;
     const uint32_t smask = (1u << pc.screen_bits) - 1u;
     const uint32_t rmask = (1u << (pc.tag_shift - pc.screen_bits)) - 1u;
 
-    // stage 2 of the pipeline: LUT entry (cache, else global gather) + TOA bin
-    auto lookup = [&](const int (&p)[kSplitEPT], const int (&t)[kSplitEPT], long long salt,
-                      uint32_t (&v)[kSplitEPT], int (&b)[kSplitEPT]) {
-#pragma unroll
-        for (int e = 0; e < kSplitEPT; ++e) {
-            const unsigned q = (unsigned)p[e] - (unsigned)pid_off;
-            const bool inr = q < L;
-            if (ablate & 1) {  // timing ablation only: no gather
-                v[e] = (q & 1023u) < 768u ? ((1u + q % 300u) << kHotRowShift) : (q & 0x3FFFu);
-            } else if (CACHE) {
-                const uint32_t w = s_pc[q & cmask];
-                const bool hit = inr && w != 0xFFFFFFFFu && (w >> pc.tag_shift) == (q >> pc.cbits);
-                if (hit) {
-                    v[e] = (((w >> pc.screen_bits) & rmask) << kHotRowShift) | (w & smask);
-                } else {
-                    v[e] = inr ? hlut[q] : kHotDrop;
-                    if (inr && v[e] != kHotDrop &&
-                        ((q * 0x9E3779B1u + (uint32_t)salt * 0x85EBCA6Bu) >> 29) == 0u)
-                        s_pc[q & cmask] = ((q >> pc.cbits) << pc.tag_shift) |
-                                          ((v[e] >> kHotRowShift) << pc.screen_bits) |
-                                          (v[e] & kHotBaseMask);
-                }
-            } else {
-                v[e] = inr ? hlut[q] : kHotDrop;
+    // chunk c -> base pointers of its events (block-uniform); !clean -> dummy
+    auto locate = [&](long long c, const int *&pp, const int *&tq) __attribute__((always_inline)) {
+        bool clean = false;
+        pp = dummy;
+        tq = dummy;
+        if (c < n_chunks) {
+            int lo = 0, hi = n_segs - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
             }
-            b[e] = (ablate & 8) ? (t[e] & 63) : toa_bin<FAST>(t[e], s_tab, tp);
+            const SegDesc sd = segs[lo];
+            const long long base = (c - sd.chunk0) * kChunk;
+            clean = ((((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0) && base + kChunk <= sd.n;
+            if (clean) {
+                pp = sd.pid + base;
+                tq = sd.toa + base;
+            }
+        }
+        return clean;
+    };
+    auto load = [&](const int *pp, const int *tq, bool clean, int (&p)[kSplitEPT],
+                    int (&t)[kSplitEPT]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < kSplitEPT / 4; ++j) {
+            const int off = clean ? (j * kSplitThreads + tid) * 4 : 0;
+            const v4i pv = ld_stream4(pp + off);
+            const v4i tv = ld_stream4(tq + off);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                p[j * 4 + q] = pv[q];
+                t[j * 4 + q] = tv[q];
+            }
         }
     };
 
-    // pipeline: events of chunk c+2G stream in while c+G is looked up and c is binned
-    int p[kSplitEPT], t[kSplitEPT];
-    uint32_t v[kSplitEPT];
+    uint32_t v[kSplitEPT], qq[kSplitEPT], ins = 0;
     int b[kSplitEPT];
-    const long long G = gridDim.x;
-    long long c = blockIdx.x;
-    if (c < n_chunks) {
-        load_chunk_t<kSplitThreads, kSplitEPT, true>(segs, n_segs, c, pid_off - 1, p, t);
-        lookup(p, t, c, v, b);
-        if (c + G < n_chunks)
-            load_chunk_t<kSplitThreads, kSplitEPT, true>(segs, n_segs, c + G, pid_off - 1, p, t);
-    }
-    for (; c < n_chunks; c += G) {
+    // stage 2: TOA bins and cache probes (LDS), then one gather per event (a
+    // miss reads its pixel, everything else entry 0).  Misses that pass the
+    // 1/8 install test are flagged in `ins` and installed by stage 3.
+    auto lookup = [&](const int (&p)[kSplitEPT], const int (&t)[kSplitEPT], long long salt)
+                      __attribute__((always_inline)) {
+        ins = 0;
+        uint32_t w[kSplitEPT];
+#pragma unroll
+        for (int e = 0; e < kSplitEPT; ++e) {
+            const unsigned q = (unsigned)p[e] - (unsigned)pid_off;
+            qq[e] = q;
+            b[e] = toa_bin_nb<FAST>(t[e], s_tab, tp);
+            if (CACHE) w[e] = s_pc[q & cmask];
+        }
+#pragma unroll
+        for (int e = 0; e < kSplitEPT; ++e) {
+            const unsigned q = qq[e];
+            const bool inr = q < L;
+            bool hit = false;
+            uint32_t dec = kHotDrop;
+            if (CACHE) {
+                hit = inr && w[e] != 0xFFFFFFFFu && (w[e] >> pc.tag_shift) == (q >> pc.cbits);
+                dec = (((w[e] >> pc.screen_bits) & rmask) << kHotRowShift) | (w[e] & smask);
+                if (!hit && inr && ((q * 0x9E3779B1u + (uint32_t)salt * 0x85EBCA6Bu) >> 29) == 0u)
+                    ins |= 1u << e;
+            }
+            const bool need = inr && !hit;
+            const uint32_t g = hlut[need ? q : 0u];
+            v[e] = need ? g : (hit ? dec : kHotDrop);
+        }
+    };
+    // stage 3: bin the looked-up chunk (hot rows in LDS, cold keys out); a
+    // chunk that is not live bins nothing but issues the same stores
+    auto bin = [&](bool live) __attribute__((always_inline)) {
         uint32_t key[kSplitEPT];
         unsigned long long bal[kSplitEPT];
         uint32_t pre[kSplitEPT];
+        bool cold_e[kSplitEPT];
         uint32_t tot = 0;
 #pragma unroll
         for (int e = 0; e < kSplitEPT; ++e) {
-            const bool ok = v[e] != kHotDrop && b[e] >= 0;
+            const bool ok = live && v[e] != kHotDrop && b[e] >= 0;
             const uint32_t row = v[e] >> kHotRowShift;
+            if (CACHE && live && ((ins >> e) & 1u) && v[e] != kHotDrop)
+                s_pc[qq[e] & cmask] = ((qq[e] >> pc.cbits) << pc.tag_shift) |
+                                      (row << pc.screen_bits) | (v[e] & kHotBaseMask);
             key[e] = (v[e] & kHotBaseMask) * (uint32_t)T + (uint32_t)b[e];
-            if (ok && row != 0u && !(ablate & 2))
-                atomicAdd(&s_hot[(row - 1u) * (uint32_t)T + (uint32_t)b[e]], 1u);
-            bal[e] = __ballot(ok && row == 0u);
+            if (ok && row != 0u) atomicAdd(&s_hot[(row - 1u) * (uint32_t)T + (uint32_t)b[e]], 1u);
+            cold_e[e] = ok && row == 0u;
+            bal[e] = __ballot(cold_e[e]);
             pre[e] = tot;
             tot += (uint32_t)__popcll(bal[e]);
         }
-        if (tot && !(ablate & 4)) {
-            uint32_t wbase = 0;
-            if ((tid & 63) == 0) wbase = atomicAdd(s_cur, tot);
-            wbase = (uint32_t)__builtin_amdgcn_readfirstlane(wbase);
+        uint32_t wbase = 0;
+        if ((tid & 63) == 0) wbase = atomicAdd(s_cur, tot);
+        wbase = (uint32_t)__builtin_amdgcn_readfirstlane(wbase);
 #pragma unroll
-            for (int e = 0; e < kSplitEPT; ++e)
-                if ((bal[e] >> (tid & 63)) & 1ull) my_cold[wbase + pre[e] + lanes_below(bal[e])] = key[e];
+        for (int e = 0; e < kSplitEPT; ++e) {
+            uint32_t *dst = cold_e[e] ? my_cold + (wbase + pre[e] + lanes_below(bal[e])) : my_dump;
+            *dst = key[e];
         }
-        if (c + G < n_chunks) {
-            lookup(p, t, c + G, v, b);
-            if (c + 2 * G < n_chunks)
-                load_chunk_t<kSplitThreads, kSplitEPT, true>(segs, n_segs, c + 2 * G, pid_off - 1, p, t);
+    };
+
+    // Pipeline over this block's chunks c0, c0 + G, ...: chunk i is binned
+    // while chunk i+1 is looked up and chunks i+2, i+3 stream in (register
+    // sets A and B alternate).
+    int pA[kSplitEPT], tA[kSplitEPT], pB[kSplitEPT], tB[kSplitEPT];
+    const long long G = gridDim.x;
+    const long long c0 = blockIdx.x;
+    const int *ppA, *tqA, *ppB, *tqB;
+    bool clA, clB, clV;
+    if (c0 < n_chunks) {
+        clA = locate(c0, ppA, tqA);
+        load(ppA, tqA, clA, pA, tA);
+        clB = locate(c0 + G, ppB, tqB);
+        load(ppB, tqB, clB, pB, tB);
+        lookup(pA, tA, c0);
+        clV = clA;
+        clA = locate(c0 + 2 * G, ppA, tqA);
+        load(ppA, tqA, clA, pA, tA);
+        for (long long c = c0; c < n_chunks; c += 2 * G) {
+            bin(clV);  // chunk c
+            lookup(pB, tB, c + G);
+            clV = clB;
+            clB = locate(c + 3 * G, ppB, tqB);
+            load(ppB, tqB, clB, pB, tB);
+            if (c + G >= n_chunks) break;
+            bin(clV);  // chunk c + G
+            lookup(pA, tA, c + 2 * G);
+            clV = clA;
+            clA = locate(c + 4 * G, ppA, tqA);
+            load(ppA, tqA, clA, pA, tA);
         }
+    }
+    // deferred chunks (tails, misaligned segments): plain per-element pass
+    for (long long c = c0; c < n_chunks; c += G) {
+        const int *pp, *tq;
+        if (locate(c, pp, tq)) continue;
+        int p[kSplitEPT], t[kSplitEPT];
+        load_chunk_t<kSplitThreads, kSplitEPT, true>(segs, n_segs, c, pid_off - 1, p, t);
+        lookup(p, t, c);
+        bin(true);
     }
     __syncthreads();
     uint32_t *dst = hot_part + (size_t)blockIdx.x * ht4;
@@ -353,7 +464,7 @@ __global__ __launch_bounds__(1024) void k_cold_segs(const uint32_t *__restrict__
         const uint32_t ex = block_exclusive_scan(ch, s_w, &tot);
         if (r < rows) {
             SegDesc d;
-            d.pid = reinterpret_cast<const int *>(cold + (size_t)r * (size_t)cold_cap);
+            d.pid = reinterpret_cast<const int *>(cold + (size_t)r * (size_t)(cold_cap + kSplitThreads / 64));
             d.toa = nullptr;
             d.n = n;
             d.chunk0 = carry + ex;
@@ -415,7 +526,7 @@ static hipError_t launch_split_t(const SplitArgs &a, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     hipLaunchKernelGGL((k_split<FAST, CACHE>), dim3(a.grid), dim3(kSplitThreads), sm, st, a.segs,
                        a.n_segs, a.n_chunks, a.hlut, a.pid_off, (unsigned)a.L, a.tab, a.tp, ht4, pc,
-                       a.hot_part, a.cold, a.cold_cap, a.cold_cnt, a.ablate);
+                       a.hot_part, a.cold, a.cold_cap, a.cold_cnt, a.dummy);
     return hipGetLastError();
 }
 
