@@ -116,6 +116,8 @@ struct lde_handle {
     int hot_refresh = 256;      // re-select a replica's hot set after this many batches
     double split_min_cov = 0.3; // sampled hot fraction below which AUTO stays PAGED
     uint32_t *d_hlut = nullptr;        // [R][L] (row + 1) << 22 | screen * T
+    uint32_t *d_pix_cnt = nullptr;     // [L] sampled events per pixel
+    uint32_t *d_pix_tab = nullptr;     // [R][1 << cache_bits] LDS pixel table images
     uint32_t *d_row_screen = nullptr;  // [R][kHotMaxRows]
     uint32_t *d_sel_stats = nullptr;   // [R][4]
     uint32_t *d_sample_part = nullptr, *d_screen_cnt = nullptr;
@@ -553,6 +555,11 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.row_screen = h->d_row_screen + (size_t)lde::kHotMaxRows * replica;
     a.hlut = h->d_hlut + (size_t)h->L * replica;
     a.grid = (int)std::min<long long>(chunks, (long long)h->split_grid);
+    a.cache_bits = h->cache_bits;
+    a.row_bits = h->row_bits;
+    a.screen_bits = h->screen_bits;
+    a.pix_cnt = h->d_pix_cnt;
+    a.pix_tab = h->d_pix_tab + ((size_t)replica << h->cache_bits);
     int &uses = h->hot_uses[replica];
     if (uses < 0 || uses >= h->hot_refresh) {
         {
@@ -563,15 +570,16 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         HIPCALL(h, hipStreamSynchronize(h->stream));
         const double sampled = (double)h->h_sel_stats[0];
         h->hot_cov[replica] = sampled > 0 ? (double)h->h_sel_stats[1] / sampled : 0.0;
+        if (env_ll("LDE_VERBOSE", 0))
+            fprintf(stderr, "lde split: replica %d sampled %u, hot rows %u cover %.3f, pixel table covers %.3f\n",
+                    replica, h->h_sel_stats[0], h->h_sel_stats[2], h->hot_cov[replica],
+                    sampled > 0 && h->cache_bits ? (double)h->h_sel_stats[3] / sampled : 0.0);
         uses = 0;
     }
     ++uses;
     if (!forced && h->hot_cov[replica] < h->split_min_cov) return 1;
     const long long per_block = (chunks + a.grid - 1) / a.grid;
     a.cold_cap = per_block * lde::kChunk;
-    a.cache_bits = h->cache_bits;
-    a.row_bits = h->row_bits;
-    a.screen_bits = h->screen_bits;
     const int ht4 = lde::align4(h->hot_rows * h->T);
     if (int rc = grow(h, &h->d_hot_part, h->hot_part_cap, (size_t)a.grid * ht4)) return rc;
     if (int rc = grow(h, &h->d_cold, h->cold_total_cap,
@@ -780,6 +788,8 @@ void release(lde_handle *h) {
     dev_free(h->d_overflow);
     dev_free(h->d_items4);
     dev_free(h->d_hlut);
+    dev_free(h->d_pix_cnt);
+    dev_free(h->d_pix_tab);
     dev_free(h->d_row_screen);
     dev_free(h->d_sel_stats);
     dev_free(h->d_sample_part);
@@ -968,7 +978,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         // histogram in LDS; the pixel cache needs tag + row + screen <= 31 bits
         if (h->n_tiles > 0 && h->S * 4 <= 160 * 1024 && env_ll("LDE_SPLIT", 1) != 0) {
             auto bits = [](long long n) { int b = 0; while ((1LL << b) < n) ++b; return b; };
-            int cbits = (int)std::max<long long>(0, std::min<long long>(16, env_ll("LDE_PIXEL_CACHE_BITS", 14)));
+            int cbits = (int)std::max<long long>(0, std::min<long long>(16, env_ll("LDE_PIXEL_CACHE_BITS", 13)));
             if ((1LL << cbits) >= 2 * h->L) cbits = std::max(0, bits(h->L));  // whole LUT fits
             // LDS budget per split block: 160 KB = one block per CU; 80 KB = two
             const size_t budget = (size_t)std::max<long long>(32, std::min<long long>(160, env_ll("LDE_SPLIT_SMEM_KB", 160))) * 1024;
@@ -1001,6 +1011,10 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 h->hot_uses.assign((size_t)h->R, -1);
                 h->hot_cov.assign((size_t)h->R, 0.0);
                 CREATE_CHECK(dev_alloc(h, &h->d_hlut, (size_t)h->R * h->L));
+                if (cbits > 0) {
+                    CREATE_CHECK(dev_alloc(h, &h->d_pix_cnt, (size_t)h->L));
+                    CREATE_CHECK(dev_alloc(h, &h->d_pix_tab, (size_t)h->R << cbits));
+                }
                 CREATE_CHECK(dev_alloc(h, &h->d_row_screen, (size_t)h->R * lde::kHotMaxRows));
                 CREATE_CHECK(dev_alloc(h, &h->d_sel_stats, (size_t)h->R * 4));
                 CREATE_CHECK(dev_alloc(h, &h->d_sample_part, (size_t)lde::kSampleBlocks * h->S));

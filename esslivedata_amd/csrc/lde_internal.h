@@ -136,7 +136,9 @@ struct SplitArgs {
     uint32_t *cold;
     long long cold_cap;  // keys per block region
     uint32_t *cold_cnt;
-    int cache_bits, row_bits, screen_bits;  // LDS pixel cache (cache_bits 0: off)
+    int cache_bits, row_bits, screen_bits;  // LDS pixel table (cache_bits 0: off)
+    uint32_t *pix_cnt;  // [L] sampled events per pixel (zeroed before each selection)
+    uint32_t *pix_tab;  // this replica's pixel table image (1 << cache_bits words)
     const int *dummy;  // 16-byte aligned zeros: load target of non-live chunk slots
 };
 size_t split_smem(int ht4, int cache_words, const ToaParams &tp);

@@ -111,7 +111,8 @@ __device__ __forceinline__ int screen_of(const int *__restrict__ lut, unsigned p
 template <typename LT>
 __global__ __launch_bounds__(kSplitThreads) void k_sample_screens(
     const SegDesc *__restrict__ segs, int n_segs, long long n_chunks, const LT *__restrict__ lut,
-    int pid_off, unsigned L, int T, int S, uint32_t *__restrict__ part) {
+    int pid_off, unsigned L, int T, int S, uint32_t *__restrict__ part,
+    uint32_t *__restrict__ pix_cnt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_cnt[];
     for (int i = threadIdx.x; i < S; i += kSplitThreads) s_cnt[i] = 0;
     __syncthreads();
@@ -122,7 +123,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_sample_screens(
     for (int e = 0; e < kSplitEPT; ++e) {
         const unsigned q = (unsigned)p[e] - (unsigned)pid_off;
         const int s = q < L ? screen_of(lut, q, T) : -1;
-        if (s >= 0) atomicAdd(&s_cnt[s], 1u);
+        if (s >= 0) {
+            atomicAdd(&s_cnt[s], 1u);
+            if (pix_cnt) atomicAdd(pix_cnt + q, 1u);
+        }
     }
     __syncthreads();
     uint32_t *dst = part + (size_t)blockIdx.x * S;
@@ -213,6 +217,7 @@ __global__ __launch_bounds__(1024) void k_select_hot(const uint32_t *__restrict_
         stats[0] = tt;
         stats[1] = ht;
         stats[2] = min(t1 + min(t2, room), (uint32_t)H);
+        stats[3] = 0;  // k_build_pix_table: sampled events of the table's pixels
     }
 }
 
@@ -226,16 +231,48 @@ __global__ __launch_bounds__(256) void k_build_hot_lut(const LT *__restrict__ lu
     hlut[p] = s < 0 ? kHotDrop : (((uint32_t)screen_row[s] << kHotRowShift) | (uint32_t)s);
 }
 
+// Pixel table image of one replica: slot j holds the most-sampled pixel q with
+// q mod C == j (C = 1 << cbits), as
+//   tag (q >> cbits) << tag_shift | (row + 1) << screen_bits | screen
+// or 0xFFFFFFFF when no sampled pixel maps there.
+__global__ __launch_bounds__(256) void k_build_pix_table(const uint32_t *__restrict__ cnt,
+                                                         const uint32_t *__restrict__ hlut,
+                                                         long long L, int cbits, int screen_bits,
+                                                         int tag_shift, uint32_t *__restrict__ tab,
+                                                         uint32_t *__restrict__ stats) {
+    const long long C = 1LL << cbits;
+    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (j >= C) return;
+    uint32_t best = 0;
+    long long bq = -1;
+    for (long long q = j; q < L; q += C) {
+        const uint32_t c = cnt[q];
+        if (c > best && hlut[q] != kHotDrop) {
+            best = c;
+            bq = q;
+        }
+    }
+    uint32_t w = 0xFFFFFFFFu;
+    if (bq >= 0) {
+        atomicAdd(stats + 3, best);
+        const uint32_t v = hlut[bq];
+        w = ((uint32_t)(bq >> cbits) << tag_shift) | ((v >> kHotRowShift) << screen_bits) |
+            (v & kHotBaseMask);
+    }
+    tab[j] = w;
+}
+
 // ---------------------------------------------------------------------------
 // the event pass
 // ---------------------------------------------------------------------------
-// Pixel cache: a direct-mapped LDS cache of hot-LUT entries, private to the
-// block and filled by the block itself.  Slot = q mod C, one u32 word:
+// Pixel table: a direct-mapped LDS table of hot-LUT entries for the pixels
+// the hot-set sample saw most (k_build_pix_table), copied into every block's
+// LDS at start.  Slot = q mod C, one u32 word:
 //   tag (q / C) << (row_bits + screen_bits) | (row + 1) << screen_bits | screen
-// (0xFFFFFFFF = empty; a valid word keeps bit 31 clear).  A miss reads the
-// global hot LUT and installs the entry with probability 1/8, so the pixels
-// that miss most often (the hot ones of a skewed stream) end up resident and
-// the L2 gather rate stops bounding the pass.
+// (0xFFFFFFFF = empty; a valid word keeps bit 31 clear).  A hit costs one LDS
+// read; a miss reads the global hot LUT, so on a skewed stream the L2 gather
+// rate (one random request per event, ~2.7e11/s chip-wide) stops bounding the
+// pass.
 struct PixelCache {
     int cbits;        // log2 C (0: no cache)
     int screen_bits;
@@ -258,7 +295,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_split(
     const uint32_t *__restrict__ hlut, int pid_off, unsigned L,
     const unsigned char *__restrict__ g_tab, ToaParams tp, int ht4, PixelCache pc,
     uint32_t *__restrict__ hot_part, uint32_t *__restrict__ cold, long long cold_cap,
-    uint32_t *__restrict__ cold_cnt, const int *__restrict__ dummy) {
+    uint32_t *__restrict__ cold_cnt, const uint32_t *__restrict__ pix_tab,
+    const int *__restrict__ dummy) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *s_hot = reinterpret_cast<uint32_t *>(smem);
     uint32_t *s_pc = s_hot + ht4;
@@ -270,8 +308,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_split(
         *reinterpret_cast<uint4 *>(s_hot + i) = make_uint4(0, 0, 0, 0);
     if (CACHE)
         for (int i = tid * 4; i < n_pc; i += kSplitThreads * 4)
-            *reinterpret_cast<uint4 *>(s_pc + i) =
-                make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+            *reinterpret_cast<uint4 *>(s_pc + i) = *reinterpret_cast<const uint4 *>(pix_tab + i);
     if (tid == 0) s_cur[0] = 0;
     load_toa_tables(s_tab, g_tab, tp);
     __syncthreads();
@@ -319,14 +356,12 @@ __global__ __launch_bounds__(kSplitThreads) void k_split(
         }
     };
 
-    uint32_t v[kSplitEPT], qq[kSplitEPT], ins = 0;
+    uint32_t v[kSplitEPT], qq[kSplitEPT];
     int b[kSplitEPT];
-    // stage 2: TOA bins and cache probes (LDS), then one gather per event (a
-    // miss reads its pixel, everything else entry 0).  Misses that pass the
-    // 1/8 install test are flagged in `ins` and installed by stage 3.
-    auto lookup = [&](const int (&p)[kSplitEPT], const int (&t)[kSplitEPT], long long salt)
+    // stage 2: TOA bins and table probes (LDS), then one gather per event (a
+    // miss reads its pixel, everything else entry 0)
+    auto lookup = [&](const int (&p)[kSplitEPT], const int (&t)[kSplitEPT])
                       __attribute__((always_inline)) {
-        ins = 0;
         uint32_t w[kSplitEPT];
 #pragma unroll
         for (int e = 0; e < kSplitEPT; ++e) {
@@ -344,8 +379,6 @@ __global__ __launch_bounds__(kSplitThreads) void k_split(
             if (CACHE) {
                 hit = inr && w[e] != 0xFFFFFFFFu && (w[e] >> pc.tag_shift) == (q >> pc.cbits);
                 dec = (((w[e] >> pc.screen_bits) & rmask) << kHotRowShift) | (w[e] & smask);
-                if (!hit && inr && ((q * 0x9E3779B1u + (uint32_t)salt * 0x85EBCA6Bu) >> 29) == 0u)
-                    ins |= 1u << e;
             }
             const bool need = inr && !hit;
             const uint32_t g = hlut[need ? q : 0u];
@@ -364,9 +397,6 @@ __global__ __launch_bounds__(kSplitThreads) void k_split(
         for (int e = 0; e < kSplitEPT; ++e) {
             const bool ok = live && v[e] != kHotDrop && b[e] >= 0;
             const uint32_t row = v[e] >> kHotRowShift;
-            if (CACHE && live && ((ins >> e) & 1u) && v[e] != kHotDrop)
-                s_pc[qq[e] & cmask] = ((qq[e] >> pc.cbits) << pc.tag_shift) |
-                                      (row << pc.screen_bits) | (v[e] & kHotBaseMask);
             key[e] = (v[e] & kHotBaseMask) * (uint32_t)T + (uint32_t)b[e];
             if (ok && row != 0u) atomicAdd(&s_hot[(row - 1u) * (uint32_t)T + (uint32_t)b[e]], 1u);
             cold_e[e] = ok && row == 0u;
@@ -397,19 +427,19 @@ __global__ __launch_bounds__(kSplitThreads) void k_split(
         load(ppA, tqA, clA, pA, tA);
         clB = locate(c0 + G, ppB, tqB);
         load(ppB, tqB, clB, pB, tB);
-        lookup(pA, tA, c0);
+        lookup(pA, tA);
         clV = clA;
         clA = locate(c0 + 2 * G, ppA, tqA);
         load(ppA, tqA, clA, pA, tA);
         for (long long c = c0; c < n_chunks; c += 2 * G) {
             bin(clV);  // chunk c
-            lookup(pB, tB, c + G);
+            lookup(pB, tB);
             clV = clB;
             clB = locate(c + 3 * G, ppB, tqB);
             load(ppB, tqB, clB, pB, tB);
             if (c + G >= n_chunks) break;
             bin(clV);  // chunk c + G
-            lookup(pA, tA, c + 2 * G);
+            lookup(pA, tA);
             clV = clA;
             clA = locate(c + 4 * G, ppA, tqA);
             load(ppA, tqA, clA, pA, tA);
@@ -421,7 +451,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_split(
         if (locate(c, pp, tq)) continue;
         int p[kSplitEPT], t[kSplitEPT];
         load_chunk_t<kSplitThreads, kSplitEPT, true>(segs, n_segs, c, pid_off - 1, p, t);
-        lookup(p, t, c);
+        lookup(p, t);
         bin(true);
     }
     __syncthreads();
@@ -484,6 +514,10 @@ size_t split_smem(int ht4, int cache_words, const ToaParams &tp) {
 }
 
 hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st) {
+    if (a.cache_bits > 0) {
+        const hipError_t e = hipMemsetAsync(a.pix_cnt, 0, (size_t)a.L * 4, st);
+        if (e != hipSuccess) return e;
+    }
     const size_t sm = (size_t)a.S * 4;
     const void *lut_r = a.lut16 ? (const void *)((const uint16_t *)a.lut + (size_t)replica * a.L)
                                 : (const void *)((const int *)a.lut + (size_t)replica * a.L);
@@ -492,13 +526,15 @@ hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL(k_sample_screens<uint16_t>, dim3(a.sample_blocks), dim3(kSplitThreads), sm,
                            st, a.segs, a.n_segs, a.n_chunks, (const uint16_t *)lut_r, a.pid_off,
-                           (unsigned)a.L, a.tp.T, a.S, a.sample_part);
+                           (unsigned)a.L, a.tp.T, a.S, a.sample_part,
+                           a.cache_bits > 0 ? a.pix_cnt : nullptr);
     } else {
         (void)hipFuncSetAttribute((const void *)k_sample_screens<int>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL(k_sample_screens<int>, dim3(a.sample_blocks), dim3(kSplitThreads), sm, st,
                            a.segs, a.n_segs, a.n_chunks, (const int *)lut_r, a.pid_off,
-                           (unsigned)a.L, a.tp.T, a.S, a.sample_part);
+                           (unsigned)a.L, a.tp.T, a.S, a.sample_part,
+                           a.cache_bits > 0 ? a.pix_cnt : nullptr);
     }
     hipLaunchKernelGGL(k_screen_sum, dim3((a.S + 255) / 256), dim3(256), 0, st, a.sample_part,
                        a.sample_blocks, a.S, a.screen_cnt);
@@ -511,6 +547,10 @@ hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st) {
     else
         hipLaunchKernelGGL(k_build_hot_lut<int>, dim3(g), dim3(256), 0, st, (const int *)lut_r, a.L,
                            a.tp.T, a.screen_row, a.hlut);
+    if (a.cache_bits > 0)
+        hipLaunchKernelGGL(k_build_pix_table, dim3((unsigned)(((1LL << a.cache_bits) + 255) / 256)),
+                           dim3(256), 0, st, a.pix_cnt, a.hlut, a.L, a.cache_bits, a.screen_bits,
+                           a.screen_bits + a.row_bits, a.pix_tab, a.stats);
     return hipGetLastError();
 }
 
@@ -526,7 +566,7 @@ static hipError_t launch_split_t(const SplitArgs &a, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     hipLaunchKernelGGL((k_split<FAST, CACHE>), dim3(a.grid), dim3(kSplitThreads), sm, st, a.segs,
                        a.n_segs, a.n_chunks, a.hlut, a.pid_off, (unsigned)a.L, a.tab, a.tp, ht4, pc,
-                       a.hot_part, a.cold, a.cold_cap, a.cold_cnt, a.dummy);
+                       a.hot_part, a.cold, a.cold_cap, a.cold_cnt, a.pix_tab, a.dummy);
     return hipGetLastError();
 }
 
