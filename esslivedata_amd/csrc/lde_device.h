@@ -20,6 +20,9 @@ __device__ __forceinline__ v4i ld_stream4(const int *p) {
     return __builtin_nontemporal_load((const g_v4i *)p);
 }
 __device__ __forceinline__ int ld_global(const int *p) { return *(const g_int *)p; }
+__device__ __forceinline__ uint32_t ld_global_u32(const uint32_t *p) {
+    return *(const __attribute__((address_space(1))) uint32_t *)p;
+}
 
 // ---------------------------------------------------------------------------
 // TOA lookup

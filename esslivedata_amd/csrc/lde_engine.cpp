@@ -133,6 +133,17 @@ struct lde_handle {
     lde::SegDesc *d_cold_segs = nullptr;
     long long *d_cold_chunks = nullptr;
     int *d_dummy = nullptr;  // 64 zero bytes
+    // SIEVE: lean event pass of SPLIT (lde_sieve.hip), used when its encodings fit
+    bool sieve_ok = false;
+    uint32_t *d_glut = nullptr;       // [R][L + 1] pixel words
+    uint32_t *d_sieve_tab = nullptr;  // [R][1 << cache_bits] LDS table images
+    std::vector<uint32_t> ttab;       // TOA bucket words (host copy)
+    uint32_t *d_ttab = nullptr;
+    uint32_t ttab_cap = 0;
+    int ttab_shift = 0;
+    lde::ChunkPtrs *d_chunk_tab = nullptr;
+    size_t chunk_tab_cap = 0;
+    int *d_sieve_dummy = nullptr;     // kChunk x (pid_off - 1): the all-invalid chunk
 
     // finalize scratch
     unsigned long long *d_tot4 = nullptr;
@@ -298,6 +309,33 @@ int build_toa_tables(lde_handle *h, const double *edges, int T, std::vector<unsi
     return LDE_OK;
 }
 
+// SIEVE TOA image: one u32 per 2^shift2-wide bucket of the fast layout,
+// (offset of the next threshold inside the bucket, capped at 2^shift2) << 8 |
+// bin of the bucket start, then a sentinel bucket (bin 255 -> 256, dropped).
+// Buckets inherit the one-step property of the fast layout (at most one
+// threshold inside), so bin = (w & 0xFF) + ((d & (2^shift2 - 1)) >= (w >> 8)).
+bool build_sieve_toa(const lde::ToaParams &tp, const std::vector<unsigned char> &img,
+                     std::vector<uint32_t> &words, int &shift2, uint32_t &cap) {
+    if (!tp.fast || tp.T > lde::kSieveMaxT || tp.span == 0) return false;
+    const uint32_t *rthr = reinterpret_cast<const uint32_t *>(img.data());
+    shift2 = std::min(tp.shift, 23);
+    const unsigned long long span = tp.span;
+    const unsigned long long G = ((span - 1) >> shift2) + 1;
+    if (G > (unsigned long long)lde::kMaxFastBuckets) return false;
+    const unsigned long long W = 1ULL << shift2;
+    words.assign((size_t)lde::align4((int)G + 1), 0u);
+    int b = 0;
+    for (unsigned long long g = 0; g < G; ++g) {
+        const unsigned long long start = g << shift2;
+        while (b + 1 < tp.T && rthr[b + 1] <= start) ++b;
+        const unsigned long long off = std::min<unsigned long long>(rthr[b + 1] - start, W);
+        words[(size_t)g] = (uint32_t)(off << 8) | (uint32_t)b;
+    }
+    words[(size_t)G] = 0xFFu;
+    cap = (G << shift2) > 0xffffffffULL ? 0xffffffffu : (uint32_t)(G << shift2);
+    return true;
+}
+
 // ---- timing ----------------------------------------------------------------
 hipEvent_t pool_event(lde_handle *h) {
     if (!h->event_pool.empty()) {
@@ -451,9 +489,13 @@ int paged_core(lde_handle *h, const lde::SegDesc *segs, int n_segs, long long ch
     const int cap = (int)((per_block * lde::kChunk + lde::kPage - 1) / lde::kPage) + 2 * h->n_tiles + 2;
     const size_t pages = (size_t)grid * (size_t)cap;
     if (pages > 0xffffffffULL) return fail(h, LDE_EINVAL, "batch too large for the page pool");
+    // pass-B work items: ~2 per CU for a full batch; the (smaller) cold-key
+    // stream of SPLIT gets ~1 per 2 CUs, since every item pays a flush of its
+    // whole tile (measured: 64K -> 256K events per item, pass B -23 %)
+    const long long per_items = n_chunks_dev ? std::max(1, h->cus / 2) : 2LL * h->cus;
     long long item_events = h->item_events_override > 0
                                 ? h->item_events_override
-                                : std::max<long long>(32768, (events + 2LL * h->cus - 1) / (2LL * h->cus));
+                                : std::max<long long>(32768, (events + per_items - 1) / per_items);
     if (item_events > 0x7fffffffLL) item_events = 0x7fffffffLL;
     const long long max_items = (total + item_events - 1) / item_events + h->n_tiles;
     if (int rc = grow(h, &h->d_pages, h->pages_cap, pages * lde::kPage)) return rc;
@@ -560,26 +602,51 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.screen_bits = h->screen_bits;
     a.pix_cnt = h->d_pix_cnt;
     a.pix_tab = h->d_pix_tab + ((size_t)replica << h->cache_bits);
+    // Hot-set selection samples this batch.  The first time any replica is
+    // needed, every replica is selected from the same batch (one host sync in
+    // all, instead of one per replica on its first batch); afterwards each
+    // replica is re-selected after hot_refresh of its own batches.  The SIEVE
+    // tables are built right after each selection, while d_screen_row holds
+    // that replica's rows.
     int &uses = h->hot_uses[replica];
     if (uses < 0 || uses >= h->hot_refresh) {
-        {
+        std::vector<int> todo;
+        for (int r = 0; r < h->R; ++r)
+            if (r == replica || h->hot_uses[(size_t)r] < 0) todo.push_back(r);
+        for (int r : todo) {
+            lde::SplitArgs b = a;
+            b.stats = h->d_sel_stats + 4 * r;
+            b.row_screen = h->d_row_screen + (size_t)lde::kHotMaxRows * r;
+            b.hlut = h->d_hlut + (size_t)h->L * r;
+            b.pix_tab = h->d_pix_tab + ((size_t)r << h->cache_bits);
             Timed tm(h, LDE_K_SPLIT_AUX);
-            HIPCALL(h, lde::launch_hot_select(a, replica, h->stream));
+            HIPCALL(h, lde::launch_hot_select(b, r, h->stream));
+            if (h->sieve_ok)
+                HIPCALL(h, lde::launch_sieve_tables(
+                               (const unsigned char *)h->d_lut + (size_t)r * h->L * (h->lut16 ? 2 : 4),
+                               h->lut16, h->L, h->T, h->d_screen_row, h->d_pix_cnt, h->cache_bits,
+                               h->d_glut + (size_t)(h->L + 1) * r,
+                               h->d_sieve_tab + ((size_t)r << h->cache_bits), h->stream));
         }
-        HIPCALL(h, hipMemcpyAsync(h->h_sel_stats, a.stats, 16, hipMemcpyDeviceToHost, h->stream));
+        HIPCALL(h, hipMemcpyAsync(h->h_sel_stats, h->d_sel_stats, (size_t)h->R * 16,
+                                  hipMemcpyDeviceToHost, h->stream));
         HIPCALL(h, hipStreamSynchronize(h->stream));
-        const double sampled = (double)h->h_sel_stats[0];
-        h->hot_cov[replica] = sampled > 0 ? (double)h->h_sel_stats[1] / sampled : 0.0;
-        if (env_ll("LDE_VERBOSE", 0))
-            fprintf(stderr, "lde split: replica %d sampled %u, hot rows %u cover %.3f, pixel table covers %.3f\n",
-                    replica, h->h_sel_stats[0], h->h_sel_stats[2], h->hot_cov[replica],
-                    sampled > 0 && h->cache_bits ? (double)h->h_sel_stats[3] / sampled : 0.0);
-        uses = 0;
+        for (int r : todo) {
+            const uint32_t *st = h->h_sel_stats + 4 * r;
+            const double sampled = (double)st[0];
+            h->hot_cov[(size_t)r] = sampled > 0 ? (double)st[1] / sampled : 0.0;
+            h->hot_uses[(size_t)r] = 0;
+            if (env_ll("LDE_VERBOSE", 0))
+                fprintf(stderr, "lde split: replica %d sampled %u, hot rows %u cover %.3f, pixel table covers %.3f\n",
+                        r, st[0], st[2], h->hot_cov[(size_t)r],
+                        sampled > 0 && h->cache_bits ? (double)st[3] / sampled : 0.0);
+        }
     }
     ++uses;
     if (!forced && h->hot_cov[replica] < h->split_min_cov) return 1;
     const long long per_block = (chunks + a.grid - 1) / a.grid;
-    a.cold_cap = per_block * lde::kChunk;
+    // SIEVE reserves cold slots in multiples of 4 per wave and half chunk
+    a.cold_cap = per_block * (lde::kChunk + (h->sieve_ok ? 4 * 2 * (lde::kSplitThreads / 64) : 0));
     const int ht4 = lde::align4(h->hot_rows * h->T);
     if (int rc = grow(h, &h->d_hot_part, h->hot_part_cap, (size_t)a.grid * ht4)) return rc;
     if (int rc = grow(h, &h->d_cold, h->cold_total_cap,
@@ -589,7 +656,44 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.hot_part = h->d_hot_part;
     a.cold = h->d_cold;
     a.cold_cnt = h->d_cold_cnt;
-    {
+    const bool sieve = h->sieve_ok && (unsigned long long)a.cold_cap * 4ULL < 0x80000000ULL &&
+                       env_ll("LDE_SIEVE", 1) != 0;
+    if (sieve) {
+        if ((size_t)chunks + 1 > h->chunk_tab_cap) {
+            HIPCALL(h, hipStreamSynchronize(h->stream));
+            dev_free(h->d_chunk_tab);
+            h->chunk_tab_cap = 0;
+            const size_t cap = std::max<size_t>((size_t)chunks + 1, 2 * h->chunk_tab_cap);
+            if (int rc = dev_alloc(h, &h->d_chunk_tab, cap)) return rc;
+            h->chunk_tab_cap = cap;
+        }
+        lde::SieveArgs sa;
+        sa.segs = h->d_segs;
+        sa.n_segs = a.n_segs;
+        sa.n_chunks = chunks;
+        sa.chunk_tab = h->d_chunk_tab;
+        sa.glut = h->d_glut + (size_t)(h->L + 1) * replica;
+        sa.L = (uint32_t)h->L;
+        sa.pid_off = h->pid_off;
+        sa.ttab = h->d_ttab;
+        sa.toa_lo = (uint32_t)h->tp.lo;
+        sa.toa_cap = h->ttab_cap;
+        sa.toa_shift = h->ttab_shift;
+        sa.toa_words4 = (int)h->ttab.size();
+        sa.T = h->T;
+        sa.pix_tab = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
+        sa.cbits = h->cache_bits;
+        sa.hot_words = ht4;
+        sa.hot_part = h->d_hot_part;
+        sa.cold = h->d_cold;
+        sa.cold_cap = a.cold_cap;
+        sa.cold_cnt = h->d_cold_cnt;
+        sa.ablate = (int)env_ll("LDE_SIEVE_ABLATE", 0);
+        Timed tm(h, LDE_K_SPLIT);
+        HIPCALL(h, lde::launch_chunk_tab(h->d_segs, a.n_segs, chunks, h->d_sieve_dummy,
+                                         h->d_chunk_tab, h->stream));
+        HIPCALL(h, lde::launch_sieve(sa, a.grid, h->stream));
+    } else {
         Timed tm(h, LDE_K_SPLIT);
         HIPCALL(h, lde::launch_split(a, h->stream));
     }
@@ -790,6 +894,11 @@ void release(lde_handle *h) {
     dev_free(h->d_hlut);
     dev_free(h->d_pix_cnt);
     dev_free(h->d_pix_tab);
+    dev_free(h->d_glut);
+    dev_free(h->d_sieve_tab);
+    dev_free(h->d_ttab);
+    dev_free(h->d_chunk_tab);
+    dev_free(h->d_sieve_dummy);
     dev_free(h->d_row_screen);
     dev_free(h->d_sel_stats);
     dev_free(h->d_sample_part);
@@ -1001,6 +1110,31 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
             const int tag_bits = std::max(0, bits(h->L) - cbits);
             if (cbits > 0 && tag_bits + h->row_bits + h->screen_bits > 31) cbits = 0;
             h->cache_bits = cbits;
+            // SIEVE: needs the pixel table, the fast TOA layout with T <= 254,
+            // keys below 2^22 and table tags below 255; its LDS carve bounds H
+            {
+                std::vector<uint32_t> tt;
+                int tsh = 0;
+                uint32_t tcap = 0;
+                if (cbits > 0 && env_ll("LDE_SIEVE", 1) != 0 && build_sieve_toa(h->tp, tab, tt, tsh, tcap) &&
+                    (unsigned long long)h->S * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL &&
+                    ((h->L - 1) >> cbits) < 255 && h->L < 0x3fffffffLL) {
+                    int Hs = 0;
+                    const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size());
+                    if (fixed < budget)
+                        Hs = (int)std::min<long long>(lde::kHotMaxRows, (long long)((budget - fixed) / (4 * (size_t)h->T)));
+                    while (Hs > 0 && lde::sieve_smem(lde::align4(Hs * h->T), cbits, (int)tt.size()) > budget) --Hs;
+                    Hs = (int)std::min<long long>(Hs, h->S);
+                    if (hmax > 0) Hs = (int)std::min<long long>(Hs, hmax);
+                    if (Hs >= 8 && (unsigned long long)Hs * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL) {
+                        h->sieve_ok = true;
+                        H = std::min(H, Hs);
+                        h->ttab = std::move(tt);
+                        h->ttab_shift = tsh;
+                        h->ttab_cap = tcap;
+                    }
+                }
+            }
             if (H >= 8) {
                 h->split_ok = true;
                 h->hot_rows = H;
@@ -1015,6 +1149,15 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                     CREATE_CHECK(dev_alloc(h, &h->d_pix_cnt, (size_t)h->L));
                     CREATE_CHECK(dev_alloc(h, &h->d_pix_tab, (size_t)h->R << cbits));
                 }
+                if (h->sieve_ok) {
+                    CREATE_CHECK(dev_alloc(h, &h->d_glut, (size_t)h->R * (size_t)(h->L + 1)));
+                    CREATE_CHECK(dev_alloc(h, &h->d_sieve_tab, (size_t)h->R << cbits));
+                    CREATE_CHECK(dev_alloc(h, &h->d_ttab, h->ttab.size()));
+                    CREATE_HIP(hipMemcpy(h->d_ttab, h->ttab.data(), h->ttab.size() * 4, hipMemcpyHostToDevice));
+                    std::vector<int> dum((size_t)lde::kChunk, (int)((unsigned)h->pid_off - 1u));
+                    CREATE_CHECK(dev_alloc(h, &h->d_sieve_dummy, dum.size()));
+                    CREATE_HIP(hipMemcpy(h->d_sieve_dummy, dum.data(), dum.size() * 4, hipMemcpyHostToDevice));
+                }
                 CREATE_CHECK(dev_alloc(h, &h->d_row_screen, (size_t)h->R * lde::kHotMaxRows));
                 CREATE_CHECK(dev_alloc(h, &h->d_sel_stats, (size_t)h->R * 4));
                 CREATE_CHECK(dev_alloc(h, &h->d_sample_part, (size_t)lde::kSampleBlocks * h->S));
@@ -1025,7 +1168,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 CREATE_CHECK(dev_alloc(h, &h->d_cold_chunks, 1));
                 CREATE_CHECK(dev_alloc(h, &h->d_dummy, 16));
                 CREATE_HIP(hipMemset(h->d_dummy, 0, 64));
-                CREATE_HIP(hipHostMalloc((void **)&h->h_sel_stats, 16, hipHostMallocDefault));
+                CREATE_HIP(hipHostMalloc((void **)&h->h_sel_stats, (size_t)h->R * 16, hipHostMallocDefault));
             }
         }
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);

@@ -141,6 +141,50 @@ struct SplitArgs {
     uint32_t *pix_tab;  // this replica's pixel table image (1 << cache_bits words)
     const int *dummy;  // 16-byte aligned zeros: load target of non-live chunk slots
 };
+// SIEVE: the lean SPLIT event pass (lde_sieve.hip).  Pixel word, in the LDS
+// table and in the HBM LUT: valid | hot | tag (table only) | value, where
+// value = row * T (hot) or screen * T (cold).
+constexpr uint32_t kSieveValid = 0x80000000u;
+constexpr uint32_t kSieveHot = 0x40000000u;
+constexpr int kSieveTagShift = 22;
+constexpr uint32_t kSieveValueMask = (1u << kSieveTagShift) - 1u;
+constexpr uint32_t kSieveEmpty = 0xFFu << kSieveTagShift;  // tag 255, not valid
+constexpr int kSieveMaxT = 254;
+
+struct ChunkPtrs {  // one 8192-event chunk of the staged batch (or the dummy chunk)
+    const int *pid;
+    const int *toa;
+};
+
+struct SieveArgs {
+    const SegDesc *segs;
+    int n_segs;
+    long long n_chunks;
+    const ChunkPtrs *chunk_tab;  // [n_chunks + 1]; deferred chunks and entry n_chunks: dummy
+    const uint32_t *glut;  // this replica's pixel words, L + 1 entries (entry L = 0)
+    uint32_t L;
+    int pid_off;
+    const uint32_t *ttab;  // TOA bucket words (+ sentinel), padded to toa_words4
+    uint32_t toa_lo, toa_cap;
+    int toa_shift, toa_words4;
+    int T;
+    const uint32_t *pix_tab;  // this replica's LDS table image (1 << cbits words)
+    int cbits;
+    int hot_words;  // align4(rows * T)
+    uint32_t *hot_part;
+    uint32_t *cold;
+    long long cold_cap;  // keys per block region (region stride cold_cap + 16)
+    uint32_t *cold_cnt;
+    int ablate;  // benchmark ablation variant (0 = the real pass)
+};
+size_t sieve_smem(int hot_words, int cbits, int toa_words4);
+hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
+                               const uint16_t *screen_row, const uint32_t *pix_cnt, int cbits,
+                               uint32_t *glut, uint32_t *tab, hipStream_t st);
+// dummy: kChunk x (pid_off - 1), the all-invalid chunk
+hipError_t launch_chunk_tab(const SegDesc *segs, int n_segs, long long n_chunks, const int *dummy,
+                            ChunkPtrs *tab, hipStream_t st);
+hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st);
 size_t split_smem(int ht4, int cache_words, const ToaParams &tp);
 hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st);
 hipError_t launch_split(const SplitArgs &a, hipStream_t st);

@@ -1,0 +1,402 @@
+// lde_sieve.hip -- lean event pass of the SPLIT strategy ("sieve").
+//
+// Same contract as k_split (lde_split.hip): every event of the batch is
+// binned either into a hot screen row privatized in LDS or emitted as a cold
+// (screen * T + bin) key for the paged pass, so the counts are bit-exact
+// whatever the hot set is.  What changes is the per-event instruction stream,
+// which in k_split was ~66 VALU operations per event with a vmcnt(0) drain per
+// chunk (rocprofv3 SQ_INSTS_VALU, round 1):
+//
+//   * one 32-bit word per pixel, in LDS (direct-mapped table of the sampled
+//     hottest pixels) and in HBM (the replica's LUT), with the same payload:
+//         bit 31 valid | bit 30 hot | bits 22..29 tag (table only) | bits 0..21 value
+//     value = row * T for a hot screen, screen * T for a cold one;
+//   * table misses gather the HBM word with a raw buffer load; hits (and
+//     out-of-range pixels, clamped to the zero sentinel at index L) load at an
+//     out-of-range offset, which returns 0 without a memory request, so
+//     word = table_hit_word | gathered_word needs no per-event branch;
+//   * one LDS read bins the TOA: bucket word = offset-of-next-edge << 8 | bin,
+//     bin = word & 0xFF + (low bits >= word >> 8); a sentinel bucket past the
+//     last edge gives bin 256 (dropped);
+//   * hot lanes add 1 to their LDS row, the others to a lane-private dummy
+//     word; cold keys are compacted per wave in LDS and leave as one 16-byte
+//     store per lane per half chunk (lanes past the count store out of range,
+//     which is discarded) -- so every iteration issues the same memory
+//     operations and the compiler's in-order vmcnt / lgkmcnt accounting can
+//     wait for exactly the operation a value comes from;
+//   * each block walks a contiguous chunk range; the {pid, toa} pointers of
+//     every chunk come from a small descriptor table (k_chunk_tab) read with a
+//     vector load, so the loop has no segment search and no scalar loads.
+//
+// Deferred chunks (partial tails, segments that are not 16-byte aligned) are
+// replaced by an all-invalid dummy chunk in the pipeline and binned afterwards
+// by a plain element-wise pass.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lde_device.h"
+#include "lde_internal.h"
+
+namespace lde {
+
+namespace {
+
+constexpr uint32_t kOOB = 0x80000000u;        // buffer offset past every num_records
+constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data format
+constexpr int kEPT = kSplitEPT;               // 8 events per thread per chunk
+constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (half a chunk)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes,
+                                             (int)kRsrcWord3);
+}
+
+__device__ __forceinline__ int screen_of_lut(const uint16_t *__restrict__ lut, long long q, int) {
+    const unsigned v = lut[q];
+    return v == 0xFFFFu ? -1 : (int)v;
+}
+__device__ __forceinline__ int screen_of_lut(const int *__restrict__ lut, long long q, int T) {
+    const int v = lut[q];
+    return v < 0 ? -1 : v / T;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// tables (rebuilt with the hot set, i.e. every hot_refresh batches)
+// ---------------------------------------------------------------------------
+template <typename LT>
+__global__ __launch_bounds__(256) void k_sieve_glut(const LT *__restrict__ lut, long long L, int T,
+                                                    const uint16_t *__restrict__ screen_row,
+                                                    uint32_t *__restrict__ glut) {
+    const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (q > L) return;
+    uint32_t w = 0;  // q == L: the zero sentinel of clamped out-of-range pixels
+    if (q < L) {
+        const int s = screen_of_lut(lut, q, T);
+        if (s >= 0) {
+            const uint32_t r1 = screen_row[s];
+            w = r1 ? (kSieveValid | kSieveHot | ((r1 - 1u) * (uint32_t)T))
+                   : (kSieveValid | ((uint32_t)s * (uint32_t)T));
+        }
+    }
+    glut[q] = w;
+}
+
+// slot j of the LDS pixel table: the most-sampled valid pixel q = j (mod C)
+__global__ __launch_bounds__(256) void k_sieve_table(const uint32_t *__restrict__ cnt,
+                                                     const uint32_t *__restrict__ glut, long long L,
+                                                     int cbits, uint32_t *__restrict__ tab) {
+    const long long C = 1LL << cbits;
+    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (j >= C) return;
+    uint32_t best = 0;
+    long long bq = -1;
+    for (long long q = j; q < L; q += C) {
+        const uint32_t c = cnt[q];
+        if (c > best && glut[q] != 0u) {
+            best = c;
+            bq = q;
+        }
+    }
+    tab[j] = bq < 0 ? kSieveEmpty
+                    : (glut[bq] | ((uint32_t)(bq >> cbits) << kSieveTagShift));
+}
+
+// chunk c -> its event pointers, or the dummy chunk (deferred / past the end)
+__global__ __launch_bounds__(256) void k_chunk_tab(const SegDesc *__restrict__ segs, int n_segs,
+                                                   long long n_chunks, const int *dummy,
+                                                   ChunkPtrs *__restrict__ tab) {
+    const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (c > n_chunks) return;
+    ChunkPtrs r{dummy, dummy};
+    if (c < n_chunks) {
+        int lo = 0, hi = n_segs - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+        }
+        const SegDesc sd = segs[lo];
+        const long long base = (c - sd.chunk0) * kChunk;
+        if (((((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0) && base + kChunk <= sd.n) {
+            r.pid = sd.pid + base;
+            r.toa = sd.toa + base;
+        }
+    }
+    tab[c] = r;
+}
+
+// ---------------------------------------------------------------------------
+// the event pass
+// ---------------------------------------------------------------------------
+// ABL (benchmark ablations only, results are wrong when nonzero): 1 no hot
+// LDS atomics, 2 no gathers, 4 no cold stores, 8 no LDS probes
+template <int ABL>
+__global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t C = 1u << a.cbits;
+    // LDS carve (words): hot rows | pixel table | TOA buckets | 64 dummies |
+    // cursor (4) | cold staging (256 per wave)
+    const uint32_t o_pc = (uint32_t)a.hot_words;
+    const uint32_t o_tt = o_pc + C;
+    const uint32_t o_dum = o_tt + (uint32_t)a.toa_words4;
+    const uint32_t o_cur = o_dum + 64u;
+    const uint32_t o_stg = o_cur + 4u;
+    for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.hot_words; i += kSplitThreads * 4u)
+        *reinterpret_cast<uint4 *>(sm + i) = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = (uint32_t)tid * 4u; i < C; i += kSplitThreads * 4u)
+        *reinterpret_cast<uint4 *>(sm + o_pc + i) = *reinterpret_cast<const uint4 *>(a.pix_tab + i);
+    for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.toa_words4; i += kSplitThreads * 4u)
+        *reinterpret_cast<uint4 *>(sm + o_tt + i) = *reinterpret_cast<const uint4 *>(a.ttab + i);
+    if (tid < 64) sm[o_dum + tid] = 0;
+    if (tid == 0) sm[o_cur] = 0;
+    for (uint32_t i = (uint32_t)tid; i < kSieveStage * (kSplitThreads / 64); i += kSplitThreads)
+        sm[o_stg + i] = 0xFFFFFFFFu;
+    __syncthreads();
+
+    const __amdgpu_buffer_rsrc_t glut = make_rsrc(a.glut, (a.L + 1u) * 4u);
+    uint32_t *my_cold = a.cold + (size_t)blockIdx.x * (size_t)(a.cold_cap + kSplitThreads / 64);
+    const __amdgpu_buffer_rsrc_t cold = make_rsrc(my_cold, (uint32_t)a.cold_cap * 4u);  // 16-B aligned
+    const uint32_t cmask = C - 1u;
+    const uint32_t pid_off = (uint32_t)a.pid_off;
+    const uint32_t Lc = a.L;
+    const uint32_t toa_lo = a.toa_lo, toa_cap = a.toa_cap;
+    const uint32_t wmask = (1u << a.toa_shift) - 1u;
+    const uint32_t T = (uint32_t)a.T;
+    const uint32_t dum_idx = o_dum + (uint32_t)lane;
+    const uint32_t o_stg_w = o_stg + kSieveStage * (uint32_t)(tid >> 6);
+
+    // ---- contiguous chunk range of this block
+    const long long n = a.n_chunks;
+    const long long cb = (long long)blockIdx.x * n / gridDim.x;
+    const long long ce = ((long long)blockIdx.x + 1) * n / gridDim.x;
+    // chunk descriptor {pid, toa} pointers, fetched by four lanes with a
+    // vector load (in-order vmcnt) and read back with readlane; chunks outside
+    // [cb, ce) and deferred chunks map to the all-invalid dummy chunk
+    const uint32_t *ctab = reinterpret_cast<const uint32_t *>(a.chunk_tab);
+    auto fetch = [&](long long c) __attribute__((always_inline)) {
+        const long long ci = c < ce ? c : n;
+        return ld_global_u32(ctab + (size_t)ci * 4 + (lane & 3));
+    };
+    auto ptrs = [&](uint32_t dv, const int *&pp, const int *&tq) __attribute__((always_inline)) {
+        const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)dv, 0);
+        const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)dv, 1);
+        const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)dv, 2);
+        const uint32_t w3 = (uint32_t)__builtin_amdgcn_readlane((int)dv, 3);
+        pp = reinterpret_cast<const int *>(((unsigned long long)w1 << 32) | w0);
+        tq = reinterpret_cast<const int *>(((unsigned long long)w3 << 32) | w2);
+    };
+    auto load = [&](uint32_t dv, int (&p)[kEPT], int (&t)[kEPT]) __attribute__((always_inline)) {
+        const int *pp, *tq;
+        ptrs(dv, pp, tq);
+#pragma unroll
+        for (int j = 0; j < kEPT / 4; ++j) {
+            const int off = (j * kSplitThreads + tid) * 4;
+            const v4i pv = ld_stream4(pp + off);
+            const v4i tv = ld_stream4(tq + off);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                p[j * 4 + q] = pv[q];
+                t[j * 4 + q] = tv[q];
+            }
+        }
+    };
+    // stage 2: table probe + TOA bucket (LDS), one gather per event
+    auto lookup = [&](const int (&p)[kEPT], const int (&t)[kEPT], uint32_t (&ws)[kEPT],
+                      uint32_t (&g)[kEPT], uint32_t (&dc)[kEPT], uint32_t (&tw)[kEPT])
+                      __attribute__((always_inline)) {
+        uint32_t w[kEPT], qs[kEPT];
+#pragma unroll
+        for (int e = 0; e < kEPT; ++e) {
+            const uint32_t q = (uint32_t)p[e] - pid_off;
+            qs[e] = q;
+            const uint32_t d = min((uint32_t)t[e] - toa_lo, toa_cap);
+            dc[e] = d;
+            if (ABL & 8) {
+                w[e] = q ^ d;
+                tw[e] = d & 0xFFFu;
+            } else {
+                w[e] = sm[o_pc + (q & cmask)];
+                tw[e] = sm[o_tt + (d >> a.toa_shift)];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < kEPT; ++e) {
+            const bool hit = ((w[e] >> kSieveTagShift) & 0xFFu) == (qs[e] >> a.cbits);
+            ws[e] = hit ? w[e] : 0u;
+            const uint32_t off = hit ? kOOB : (min(qs[e], Lc) << 2);
+            g[e] = (ABL & 2) ? (off & 0x3u) : __builtin_amdgcn_raw_buffer_load_b32(glut, (int)off, 0, 0);
+        }
+    };
+    // stage 3: bin, in two halves of four events per lane.  Hot lanes add 1
+    // to their LDS row (the others to a lane-private dummy); cold keys are
+    // compacted into the wave's 256-word LDS staging area (the others write a
+    // dummy), the wave reserves round4(count) slots of the block's cold region
+    // with one LDS atomic, and every lane stores 16 staged bytes at once (lanes
+    // past the reservation store out of range).  Staging words are reset to
+    // -1, so the <= 3 pad keys of a reservation are dropped by the key pass.
+    auto bin = [&](const uint32_t (&ws)[kEPT], const uint32_t (&g)[kEPT], const uint32_t (&dc)[kEPT],
+                   const uint32_t (&tw)[kEPT]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint32_t tot = 0;
+#pragma unroll
+            for (int e = h * kEPT / 2; e < (h + 1) * kEPT / 2; ++e) {
+                const uint32_t v = ws[e] | g[e];
+                const uint32_t b = (tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u);
+                const uint32_t fl = v >> 30;
+                const bool inb = b < T;
+                const uint32_t k = (v & kSieveValueMask) + b;
+                const bool cm = inb && fl == 2u;
+                const unsigned long long bal = __ballot(cm);
+                const uint32_t sidx = cm ? (o_stg_w + tot + lanes_below(bal)) : dum_idx;
+                tot += (uint32_t)__popcll(bal);
+                const uint32_t hidx = (inb && fl == 3u) ? k : dum_idx;
+                if (!(ABL & 1))
+                    __hip_atomic_fetch_add(sm + hidx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    tot += hidx & 1u;
+                sm[sidx] = k;
+            }
+            const uint32_t res = (tot + 3u) & ~3u;
+            uint32_t wbase = 0;
+            if (lane == 0)
+                wbase = __hip_atomic_fetch_add(sm + o_cur, res, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+            wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)wbase);
+            __builtin_amdgcn_wave_barrier();
+            uint4 *slot = reinterpret_cast<uint4 *>(sm + o_stg_w + 4u * (uint32_t)lane);
+            const uint4 kv = *slot;
+            *slot = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t off = 4u * (uint32_t)lane < res ? (wbase + 4u * (uint32_t)lane) << 2 : kOOB;
+            v4u kk = {kv.x, kv.y, kv.z, kv.w};
+            if (!(ABL & 4)) __builtin_amdgcn_raw_buffer_store_b128(kk, cold, (int)off, 0, 0);
+            else sm[o_dum + lane] += kv.x ^ off;
+        }
+    };
+
+    // ---- pipeline: chunk i is binned while chunk i+1 is looked up, chunks
+    // i+2, i+3 stream in and the descriptor of i+4 is fetched (register sets
+    // A and B alternate)
+    int pA[kEPT], tA[kEPT], pB[kEPT], tB[kEPT];
+    uint32_t wsX[kEPT], gX[kEPT], dX[kEPT], twX[kEPT];
+    uint32_t wsY[kEPT], gY[kEPT], dY[kEPT], twY[kEPT];
+    if (cb < ce) {
+        uint32_t dA = fetch(cb), dB = fetch(cb + 1);
+        load(dA, pA, tA);
+        load(dB, pB, tB);
+        dA = fetch(cb + 2);
+        dB = fetch(cb + 3);
+        lookup(pA, tA, wsX, gX, dX, twX);
+        load(dA, pA, tA);
+        dA = fetch(cb + 4);
+        for (long long c = cb; c < ce; c += 2) {
+            bin(wsX, gX, dX, twX);  // chunk c
+            lookup(pB, tB, wsY, gY, dY, twY);
+            load(dB, pB, tB);  // chunk c + 3
+            dB = fetch(c + 5);
+            if (c + 1 >= ce) break;
+            bin(wsY, gY, dY, twY);  // chunk c + 1
+            lookup(pA, tA, wsX, gX, dX, twX);
+            load(dA, pA, tA);  // chunk c + 4
+            dA = fetch(c + 6);
+        }
+    }
+
+    // ---- deferred chunks: element-wise loads of a clamped index
+    if (cb < ce) {
+        int si = 0;
+        {
+            int lo = 0, hi = a.n_segs - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (a.segs[mid].chunk0 <= cb) lo = mid; else hi = mid - 1;
+            }
+            si = lo;
+        }
+        for (long long c = cb; c < ce; ++c) {
+            while (si + 1 < a.n_segs && a.segs[si + 1].chunk0 <= c) ++si;
+            const SegDesc sd = a.segs[si];
+            const long long base = (c - sd.chunk0) * kChunk;
+            if (((((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0) && base + kChunk <= sd.n)
+                continue;
+            int p[kEPT], t[kEPT];
+#pragma unroll
+            for (int j = 0; j < kEPT / 4; ++j) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const long long ei = base + ((long long)j * kSplitThreads + tid) * 4 + q;
+                    const bool ok = ei < sd.n;
+                    const long long ec = ok ? ei : 0;
+                    const int pv = ld_global(sd.pid + ec);
+                    const int tv = ld_global(sd.toa + ec);
+                    p[j * 4 + q] = ok ? pv : a.pid_off - 1;  // outside the LUT: dropped
+                    t[j * 4 + q] = tv;
+                }
+            }
+            lookup(p, t, wsX, gX, dX, twX);
+            bin(wsX, gX, dX, twX);
+        }
+    }
+    __syncthreads();
+    uint32_t *dst = a.hot_part + (size_t)blockIdx.x * a.hot_words;
+    for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4)
+        *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(sm + i);
+    if (tid == 0) a.cold_cnt[blockIdx.x] = sm[o_cur];
+}
+
+// ---------------------------------------------------------------------------
+// launch wrappers
+// ---------------------------------------------------------------------------
+size_t sieve_smem(int hot_words, int cbits, int toa_words4) {
+    return 4 * ((size_t)hot_words + ((size_t)1 << cbits) + (size_t)toa_words4 + 64 + 4 +
+                (size_t)kSieveStage * (kSplitThreads / 64));
+}
+
+hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
+                               const uint16_t *screen_row, const uint32_t *pix_cnt, int cbits,
+                               uint32_t *glut, uint32_t *tab, hipStream_t st) {
+    const unsigned g = (unsigned)((L + 1 + 255) / 256);
+    if (lut16)
+        hipLaunchKernelGGL(k_sieve_glut<uint16_t>, dim3(g), dim3(256), 0, st,
+                           (const uint16_t *)lut, L, T, screen_row, glut);
+    else
+        hipLaunchKernelGGL(k_sieve_glut<int>, dim3(g), dim3(256), 0, st, (const int *)lut, L, T,
+                           screen_row, glut);
+    hipLaunchKernelGGL(k_sieve_table, dim3((unsigned)(((1LL << cbits) + 255) / 256)), dim3(256), 0,
+                       st, pix_cnt, glut, L, cbits, tab);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_tab(const SegDesc *segs, int n_segs, long long n_chunks, const int *dummy,
+                            ChunkPtrs *tab, hipStream_t st) {
+    hipLaunchKernelGGL(k_chunk_tab, dim3((unsigned)((n_chunks + 1 + 255) / 256)), dim3(256), 0, st,
+                       segs, n_segs, n_chunks, dummy, tab);
+    return hipGetLastError();
+}
+
+template <int ABL>
+static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st) {
+    const size_t sm = sieve_smem(a.hot_words, a.cbits, a.toa_words4);
+    (void)hipFuncSetAttribute((const void *)k_sieve<ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
+    hipLaunchKernelGGL(k_sieve<ABL>, dim3(grid), dim3(kSplitThreads), sm, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st) {
+    switch (a.ablate) {
+    case 1: return launch_sieve_t<1>(a, grid, st);
+    case 2: return launch_sieve_t<2>(a, grid, st);
+    case 4: return launch_sieve_t<4>(a, grid, st);
+    case 7: return launch_sieve_t<7>(a, grid, st);
+    case 15: return launch_sieve_t<15>(a, grid, st);
+    default: return launch_sieve_t<0>(a, grid, st);
+    }
+}
+
+}  // namespace lde

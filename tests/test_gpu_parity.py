@@ -29,6 +29,9 @@ VARIANTS = [
     {'LDE_PIXEL_CACHE_BITS': '0'},
     {'LDE_PIXEL_CACHE_BITS': '6', 'LDE_SPLIT_GRID': '17'},
     {'LDE_PIXEL_CACHE_BITS': '15'},
+    # SPLIT with the original event pass instead of the SIEVE pass
+    {'LDE_SIEVE': '0'},
+    {'LDE_SIEVE': '0', 'LDE_PIXEL_CACHE_BITS': '6', 'LDE_SPLIT_GRID': '17'},
 ]
 
 
