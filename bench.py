@@ -36,8 +36,12 @@ KERNEL_SYMBOL = {
     'tile_accumulate': 'k_tile_accumulate',
     'paged': 'k_paged_partition',
     'page_accumulate': 'k_page_accumulate',
-    'split': 'k_split',
+    'split': 'k_sieve',  # SPLIT's event pass (k_split when LDE_SIEVE=0)
 }
+# engine timing buckets (include/lde.h LDE_K_*) as they are used by the SPLIT
+# strategy's SIEVE pass: 'split' = k_chunk_tab + k_sieve, 'split_aux' = hot-set
+# selection + k_hot_reduce, 'paged' = the cold-key pipeline (k_cold_scan,
+# k_cold_plan, k_cold_sort, k_cold_accumulate)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_EVENT = 8  # int32 pixel_id + int32 time_of_flight
 

@@ -144,6 +144,14 @@ struct lde_handle {
     lde::ChunkPtrs *d_chunk_tab = nullptr;
     size_t chunk_tab_cap = 0;
     int *d_sieve_dummy = nullptr;     // kChunk x (pid_off - 1): the all-invalid chunk
+    // SIEVE cold keys: per (block, tile) counts and offsets, tile-major u16 keys, items
+    uint32_t *d_cold_tcnt = nullptr, *d_cold_boff = nullptr;
+    size_t cold_tcnt_cap = 0, cold_boff_cap = 0;
+    uint16_t *d_cold_keys = nullptr;
+    size_t cold_keys_cap = 0;
+    uint4 *d_cold_items = nullptr;
+    size_t cold_items_cap = 0;
+    uint32_t *d_cold_ttot = nullptr, *d_cold_tbase = nullptr;  // [n_tiles]
 
     // finalize scratch
     unsigned long long *d_tot4 = nullptr;
@@ -659,14 +667,20 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     const bool sieve = h->sieve_ok && (unsigned long long)a.cold_cap * 4ULL < 0x80000000ULL &&
                        env_ll("LDE_SIEVE", 1) != 0;
     if (sieve) {
-        if ((size_t)chunks + 1 > h->chunk_tab_cap) {
-            HIPCALL(h, hipStreamSynchronize(h->stream));
-            dev_free(h->d_chunk_tab);
-            h->chunk_tab_cap = 0;
-            const size_t cap = std::max<size_t>((size_t)chunks + 1, 2 * h->chunk_tab_cap);
-            if (int rc = dev_alloc(h, &h->d_chunk_tab, cap)) return rc;
-            h->chunk_tab_cap = cap;
-        }
+        if (int rc = grow(h, &h->d_chunk_tab, h->chunk_tab_cap, (size_t)chunks + 1)) return rc;
+        const size_t nt = (size_t)h->n_tiles;
+        if (int rc = grow(h, &h->d_cold_tcnt, h->cold_tcnt_cap, (size_t)a.grid * nt)) return rc;
+        if (int rc = grow(h, &h->d_cold_boff, h->cold_boff_cap, (size_t)a.grid * nt)) return rc;
+        // tile-major u16 keys: at most every staged slot, + slack for pass B's 16-byte loads
+        if (int rc = grow(h, &h->d_cold_keys, h->cold_keys_cap,
+                          (size_t)a.grid * (size_t)a.cold_cap + 64))
+            return rc;
+        const double cold_est = std::min(1.0, std::max(0.05, 1.0 - h->hot_cov[replica])) * (double)total;
+        const long long item_keys = h->item_events_override > 0
+                                        ? h->item_events_override
+                                        : std::max<long long>(32768, (long long)(cold_est / std::max(1, h->cus / 2)));
+        const long long max_items = ((long long)a.grid * a.cold_cap) / item_keys + h->n_tiles + 1;
+        if (int rc = grow(h, &h->d_cold_items, h->cold_items_cap, (size_t)max_items)) return rc;
         lde::SieveArgs sa;
         sa.segs = h->d_segs;
         sa.n_segs = a.n_segs;
@@ -688,11 +702,42 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         sa.cold = h->d_cold;
         sa.cold_cap = a.cold_cap;
         sa.cold_cnt = h->d_cold_cnt;
+        sa.tile_bits = h->tile_bits;
+        sa.n_tiles = h->n_tiles;
+        sa.cold_tcnt = h->d_cold_tcnt;
         sa.ablate = (int)env_ll("LDE_SIEVE_ABLATE", 0);
-        Timed tm(h, LDE_K_SPLIT);
-        HIPCALL(h, lde::launch_chunk_tab(h->d_segs, a.n_segs, chunks, h->d_sieve_dummy,
-                                         h->d_chunk_tab, h->stream));
-        HIPCALL(h, lde::launch_sieve(sa, a.grid, h->stream));
+        {
+            Timed tm(h, LDE_K_SPLIT);
+            HIPCALL(h, lde::launch_chunk_tab(h->d_segs, a.n_segs, chunks, h->d_sieve_dummy,
+                                             h->d_chunk_tab, h->stream));
+            HIPCALL(h, lde::launch_sieve(sa, a.grid, h->stream));
+        }
+        {
+            Timed tm(h, LDE_K_SPLIT_AUX);
+            HIPCALL(h, lde::launch_hot_reduce(a, h->d_win32, h->stream));
+        }
+        lde::ColdArgs c;
+        c.tile_bits = h->tile_bits;
+        c.n_tiles = h->n_tiles;
+        c.rows = a.grid;
+        c.cold = h->d_cold;
+        c.stride = a.cold_cap + lde::kSplitThreads / 64;
+        c.cap = a.cold_cap;
+        c.cold_cnt = h->d_cold_cnt;
+        c.tcnt = h->d_cold_tcnt;
+        c.boff = h->d_cold_boff;
+        c.tile_total = h->d_cold_ttot;
+        c.tile_base = h->d_cold_tbase;
+        c.item_keys = (uint32_t)std::min<long long>(item_keys, 0x7fffffffLL);
+        c.max_items = (uint32_t)max_items;
+        c.items = h->d_cold_items;
+        c.item_count = h->d_item_count;
+        c.keys = h->d_cold_keys;
+        c.hist = h->d_win32;
+        c.n_bins = h->nbins;
+        Timed tm(h, LDE_K_PAGED);
+        HIPCALL(h, lde::launch_cold_pipeline(c, h->stream));
+        return LDE_OK;
     } else {
         Timed tm(h, LDE_K_SPLIT);
         HIPCALL(h, lde::launch_split(a, h->stream));
@@ -899,6 +944,12 @@ void release(lde_handle *h) {
     dev_free(h->d_ttab);
     dev_free(h->d_chunk_tab);
     dev_free(h->d_sieve_dummy);
+    dev_free(h->d_cold_tcnt);
+    dev_free(h->d_cold_boff);
+    dev_free(h->d_cold_keys);
+    dev_free(h->d_cold_items);
+    dev_free(h->d_cold_ttot);
+    dev_free(h->d_cold_tbase);
     dev_free(h->d_row_screen);
     dev_free(h->d_sel_stats);
     dev_free(h->d_sample_part);
@@ -1120,10 +1171,10 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                     (unsigned long long)h->S * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL &&
                     ((h->L - 1) >> cbits) < 255 && h->L < 0x3fffffffLL) {
                     int Hs = 0;
-                    const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size());
+                    const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size(), h->n_tiles);
                     if (fixed < budget)
                         Hs = (int)std::min<long long>(lde::kHotMaxRows, (long long)((budget - fixed) / (4 * (size_t)h->T)));
-                    while (Hs > 0 && lde::sieve_smem(lde::align4(Hs * h->T), cbits, (int)tt.size()) > budget) --Hs;
+                    while (Hs > 0 && lde::sieve_smem(lde::align4(Hs * h->T), cbits, (int)tt.size(), h->n_tiles) > budget) --Hs;
                     Hs = (int)std::min<long long>(Hs, h->S);
                     if (hmax > 0) Hs = (int)std::min<long long>(Hs, hmax);
                     if (Hs >= 8 && (unsigned long long)Hs * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL) {
@@ -1156,6 +1207,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                     CREATE_HIP(hipMemcpy(h->d_ttab, h->ttab.data(), h->ttab.size() * 4, hipMemcpyHostToDevice));
                     std::vector<int> dum((size_t)lde::kChunk, (int)((unsigned)h->pid_off - 1u));
                     CREATE_CHECK(dev_alloc(h, &h->d_sieve_dummy, dum.size()));
+                    CREATE_CHECK(dev_alloc(h, &h->d_cold_ttot, (size_t)h->n_tiles));
+                    CREATE_CHECK(dev_alloc(h, &h->d_cold_tbase, (size_t)h->n_tiles));
                     CREATE_HIP(hipMemcpy(h->d_sieve_dummy, dum.data(), dum.size() * 4, hipMemcpyHostToDevice));
                 }
                 CREATE_CHECK(dev_alloc(h, &h->d_row_screen, (size_t)h->R * lde::kHotMaxRows));

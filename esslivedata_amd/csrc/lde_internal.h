@@ -175,9 +175,30 @@ struct SieveArgs {
     uint32_t *cold;
     long long cold_cap;  // keys per block region (region stride cold_cap + 16)
     uint32_t *cold_cnt;
+    int tile_bits, n_tiles;  // cold keys are counted per tile of 2^tile_bits bins
+    uint32_t *cold_tcnt;     // [grid][n_tiles]
     int ablate;  // benchmark ablation variant (0 = the real pass)
 };
-size_t sieve_smem(int hot_words, int cbits, int toa_words4);
+size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);
+// cold keys of SIEVE: per-tile scan, plan, exact counting sort into a
+// tile-major u16 array, pass B
+struct ColdArgs {
+    int tile_bits, n_tiles;
+    int rows;  // sieve blocks
+    const uint32_t *cold;
+    long long stride, cap;  // region stride and capacity (keys)
+    const uint32_t *cold_cnt, *tcnt;
+    uint32_t *boff, *tile_total, *tile_base;
+    uint32_t item_keys, max_items;
+    uint4 *items;
+    uint32_t *item_count;
+    uint16_t *keys;  // tile-major, 16-byte aligned, >= total + 8 entries
+    uint32_t *hist;
+    long long n_bins;
+};
+size_t cold_sort_smem(int n_tiles);
+hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st);
+hipError_t launch_hot_reduce(const SplitArgs &a, uint32_t *win, hipStream_t st);
 hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
                                const uint16_t *screen_row, const uint32_t *pix_cnt, int cbits,
                                uint32_t *glut, uint32_t *tab, hipStream_t st);

@@ -131,7 +131,8 @@ __global__ __launch_bounds__(256) void k_chunk_tab(const SegDesc *__restrict__ s
 // the event pass
 // ---------------------------------------------------------------------------
 // ABL (benchmark ablations only, results are wrong when nonzero): 1 no hot
-// LDS atomics, 2 no gathers, 4 no cold stores, 8 no LDS probes
+// LDS atomics, 2 no gathers, 4 no cold stores, 8 no LDS probes, 16 every
+// gather lane out of range, 32 every gather lane on the first two words
 template <int ABL>
 __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
@@ -139,12 +140,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const int lane = tid & 63;
     const uint32_t C = 1u << a.cbits;
     // LDS carve (words): hot rows | pixel table | TOA buckets | 64 dummies |
-    // cursor (4) | cold staging (256 per wave)
+    // cursor (4) | cold staging (256 per wave) | cold keys per tile
     const uint32_t o_pc = (uint32_t)a.hot_words;
     const uint32_t o_tt = o_pc + C;
     const uint32_t o_dum = o_tt + (uint32_t)a.toa_words4;
     const uint32_t o_cur = o_dum + 64u;
     const uint32_t o_stg = o_cur + 4u;
+    const uint32_t o_tcnt = o_stg + kSieveStage * (kSplitThreads / 64);
     for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.hot_words; i += kSplitThreads * 4u)
         *reinterpret_cast<uint4 *>(sm + i) = make_uint4(0, 0, 0, 0);
     for (uint32_t i = (uint32_t)tid * 4u; i < C; i += kSplitThreads * 4u)
@@ -155,6 +157,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     if (tid == 0) sm[o_cur] = 0;
     for (uint32_t i = (uint32_t)tid; i < kSieveStage * (kSplitThreads / 64); i += kSplitThreads)
         sm[o_stg + i] = 0xFFFFFFFFu;
+    for (int i = tid; i < a.n_tiles; i += kSplitThreads) sm[o_tcnt + i] = 0;
     __syncthreads();
 
     const __amdgpu_buffer_rsrc_t glut = make_rsrc(a.glut, (a.L + 1u) * 4u);
@@ -227,7 +230,9 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         for (int e = 0; e < kEPT; ++e) {
             const bool hit = ((w[e] >> kSieveTagShift) & 0xFFu) == (qs[e] >> a.cbits);
             ws[e] = hit ? w[e] : 0u;
-            const uint32_t off = hit ? kOOB : (min(qs[e], Lc) << 2);
+            uint32_t off = hit ? kOOB : (min(qs[e], Lc) << 2);
+            if (ABL & 16) off = kOOB | (off & 4u);
+            if (ABL & 32) off = off & 4u;
             g[e] = (ABL & 2) ? (off & 0x3u) : __builtin_amdgcn_raw_buffer_load_b32(glut, (int)off, 0, 0);
         }
     };
@@ -260,6 +265,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 else
                     tot += hidx & 1u;
                 sm[sidx] = k;
+                const uint32_t tidx = cm ? o_tcnt + (k >> a.tile_bits) : dum_idx;
+                __hip_atomic_fetch_add(sm + tidx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             const uint32_t res = (tot + 3u) & ~3u;
             uint32_t wbase = 0;
@@ -347,14 +354,229 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4)
         *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(sm + i);
     if (tid == 0) a.cold_cnt[blockIdx.x] = sm[o_cur];
+    for (int i = tid; i < a.n_tiles; i += kSplitThreads)
+        a.cold_tcnt[(size_t)blockIdx.x * a.n_tiles + i] = sm[o_tcnt + i];
+}
+
+// ---------------------------------------------------------------------------
+// cold keys: exact counting sort into a tile-major u16 array, then pass B
+// ---------------------------------------------------------------------------
+// per tile: exclusive scan over sieve blocks of their key counts
+__global__ __launch_bounds__(256) void k_cold_scan(const uint32_t *__restrict__ tcnt, int rows,
+                                                   int n_tiles, uint32_t *__restrict__ boff,
+                                                   uint32_t *__restrict__ tile_total) {
+    __shared__ uint32_t s_w[32];
+    const int t = blockIdx.x;
+    uint32_t carry = 0;
+    for (int r0 = 0; r0 < rows; r0 += 256) {
+        const int r = r0 + threadIdx.x;
+        const uint32_t v = r < rows ? tcnt[(size_t)r * n_tiles + t] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(v, s_w, &tot);
+        if (r < rows) boff[(size_t)r * n_tiles + t] = carry + ex;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tile_total[t] = carry;
+}
+
+// tile bases of the tile-major key array + balanced pass-B items
+// (tile, first key, end key); a tile with n keys gets ceil(n / item_keys) items
+__global__ __launch_bounds__(1024) void k_cold_plan(const uint32_t *__restrict__ tile_total,
+                                                    int n_tiles, uint32_t item_keys,
+                                                    uint32_t *__restrict__ tile_base,
+                                                    uint4 *__restrict__ items,
+                                                    uint32_t *__restrict__ item_count,
+                                                    uint32_t max_items) {
+    __shared__ uint32_t s_w[32];
+    __shared__ uint32_t s_ib[kMaxTiles + 1];
+    __shared__ uint32_t s_kb[kMaxTiles + 1];
+    constexpr int TPT = kMaxTiles / 1024;
+    const int tid = threadIdx.x;
+    uint32_t nk[TPT], ni[TPT], ksum = 0, isum = 0;
+#pragma unroll
+    for (int q = 0; q < TPT; ++q) {
+        const int t = tid * TPT + q;
+        nk[q] = t < n_tiles ? tile_total[t] : 0u;
+        ni[q] = (nk[q] + item_keys - 1) / item_keys;
+        ksum += nk[q];
+        isum += ni[q];
+    }
+    uint32_t ktot, itot;
+    uint32_t kb = block_exclusive_scan(ksum, s_w, &ktot);
+    __syncthreads();
+    uint32_t ib = block_exclusive_scan(isum, s_w, &itot);
+#pragma unroll
+    for (int q = 0; q < TPT; ++q) {
+        const int t = tid * TPT + q;
+        if (t < n_tiles) {
+            tile_base[t] = kb;
+            s_kb[t] = kb;
+            s_ib[t] = ib;
+        }
+        kb += nk[q];
+        ib += ni[q];
+    }
+    if (tid == 0) {
+        s_ib[n_tiles] = itot;
+        s_kb[n_tiles] = ktot;
+    }
+    __syncthreads();
+    const uint32_t n_items = itot < max_items ? itot : max_items;
+    for (uint32_t i = (uint32_t)tid; i < n_items; i += 1024u) {
+        int lo = 0, hi = n_tiles - 1;  // last tile with s_ib[t] <= i
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_ib[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        const uint32_t j = i - s_ib[lo], nt = s_ib[lo + 1] - s_ib[lo];
+        const uint32_t k0 = s_kb[lo], kn = s_kb[lo + 1] - k0;
+        const uint32_t b0 = k0 + (uint32_t)((unsigned long long)j * kn / nt);
+        const uint32_t b1 = k0 + (uint32_t)((unsigned long long)(j + 1) * kn / nt);
+        items[i] = make_uint4((uint32_t)lo, b0, b1, 0u);
+    }
+    if (tid == 0) *item_count = n_items;
+}
+
+// One block per sieve block: its cold region is sorted by tile in 16K-key
+// pieces in LDS (rank by LDS atomics, scan over tiles, scatter), and each
+// piece's tile runs are written as u16 tile-local keys at the block's exact
+// offsets of the tile-major array.  Pad keys (-1) are skipped.
+constexpr int kSortThreads = 1024;
+constexpr int kSortPiece = 16384;
+size_t cold_sort_smem(int n_tiles) {
+    return 4 * ((size_t)kSortPiece + 3 * (size_t)align4(n_tiles) + 32);
+}
+
+template <int TB>
+__global__ __launch_bounds__(kSortThreads) void k_cold_sort(
+    const uint32_t *__restrict__ cold, long long stride, long long cap,
+    const uint32_t *__restrict__ cold_cnt, const uint32_t *__restrict__ boff,
+    const uint32_t *__restrict__ tile_base, int n_tiles, uint16_t *__restrict__ out) {
+    constexpr int KPT = kSortPiece / kSortThreads;  // 16 keys per thread
+    constexpr uint32_t MASK = (1u << TB) - 1u;
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    const int nt4 = align4(n_tiles);
+    uint32_t *s_sorted = sm;
+    uint32_t *s_cnt = sm + kSortPiece;
+    uint32_t *s_start = s_cnt + nt4;
+    uint32_t *s_cur = s_start + nt4;
+    uint32_t *s_w = s_cur + nt4;
+    const int tid = threadIdx.x;
+    const int b = blockIdx.x;
+    const uint32_t n = cold_cnt[b];
+    const uint32_t *src = cold + (size_t)b * (size_t)stride;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, (uint32_t)(cap * 4));
+    for (int t = tid; t < n_tiles; t += kSortThreads)
+        s_cur[t] = tile_base[t] + boff[(size_t)b * n_tiles + t];
+    constexpr int TPT = kMaxTiles / kSortThreads;
+    // the next piece's keys are requested before the current piece is sorted
+    v4u nk[KPT / 4];
+    auto fetch = [&](uint32_t p0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < KPT / 4; ++j) {
+            const uint32_t e0 = p0 + ((uint32_t)j * kSortThreads + (uint32_t)tid) * 4u;
+            nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
+        }
+    };
+    if (n > 0) fetch(0);
+    for (uint32_t p0 = 0; p0 < n; p0 += kSortPiece) {
+        for (int t = tid; t < n_tiles; t += kSortThreads) s_cnt[t] = 0;
+        uint32_t key[KPT], rank[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT / 4; ++j) {
+            const uint32_t e0 = p0 + ((uint32_t)j * kSortThreads + (uint32_t)tid) * 4u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n ? nk[j][q] : 0xFFFFFFFFu;
+        }
+        if (p0 + kSortPiece < n) fetch(p0 + kSortPiece);
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < KPT; ++e) {
+            rank[e] = 0;
+            if (key[e] != 0xFFFFFFFFu)
+                rank[e] = __hip_atomic_fetch_add(s_cnt + (key[e] >> TB), 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+        uint32_t c[TPT], sum = 0;
+#pragma unroll
+        for (int q = 0; q < TPT; ++q) {
+            const int t = tid * TPT + q;
+            c[q] = t < n_tiles ? s_cnt[t] : 0u;
+            sum += c[q];
+        }
+        uint32_t total;
+        uint32_t run = block_exclusive_scan(sum, s_w, &total);
+#pragma unroll
+        for (int q = 0; q < TPT; ++q) {
+            const int t = tid * TPT + q;
+            if (t < n_tiles) s_start[t] = run;
+            run += c[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < KPT; ++e)
+            if (key[e] != 0xFFFFFFFFu) s_sorted[s_start[key[e] >> TB] + rank[e]] = key[e];
+        __syncthreads();
+        for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
+            const uint32_t k = s_sorted[i];
+            const uint32_t t = k >> TB;
+            out[s_cur[t] + (i - s_start[t])] = (uint16_t)(k & MASK);
+        }
+        __syncthreads();
+        for (int t = tid; t < n_tiles; t += kSortThreads) s_cur[t] += s_cnt[t];
+    }
+}
+
+// pass B: one item = a contiguous key range of one tile
+template <int TB>
+__global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
+    const uint16_t *__restrict__ keys, const uint4 *__restrict__ items,
+    const uint32_t *__restrict__ item_count, uint32_t *__restrict__ hist, long long n_bins) {
+    constexpr int NB = 1 << TB;
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[NB];
+    if (blockIdx.x >= *item_count) return;
+    const uint4 it = items[blockIdx.x];
+    for (int i = threadIdx.x * 4; i < NB; i += kTileThreads * 4)
+        *reinterpret_cast<uint4 *>(s_tile + i) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    // four 16-byte loads (32 keys) per thread in flight per iteration
+    const uint32_t k0 = it.y & ~7u;
+    for (uint32_t i0 = k0 + (uint32_t)threadIdx.x * 8u; i0 < it.z; i0 += kTileThreads * 32u) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * kTileThreads * 8u;
+            v[u] = i < it.z ? *reinterpret_cast<const uint4 *>(keys + i) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * kTileThreads * 8u;
+            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t idx = i + (uint32_t)q;
+                if (idx >= it.y && idx < it.z)
+                    __hip_atomic_fetch_add(s_tile + ((w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu), 1u,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    }
+    __syncthreads();
+    const long long base = (long long)it.x << TB;
+    for (int i = threadIdx.x; i < NB; i += kTileThreads) {
+        const uint32_t v = s_tile[i];
+        if (v != 0u && base + i < n_bins) atomicAdd(hist + base + i, v);
+    }
 }
 
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
-size_t sieve_smem(int hot_words, int cbits, int toa_words4) {
+size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles) {
     return 4 * ((size_t)hot_words + ((size_t)1 << cbits) + (size_t)toa_words4 + 64 + 4 +
-                (size_t)kSieveStage * (kSplitThreads / 64));
+                (size_t)kSieveStage * (kSplitThreads / 64) + (size_t)align4(n_tiles));
 }
 
 hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
@@ -379,9 +601,37 @@ hipError_t launch_chunk_tab(const SegDesc *segs, int n_segs, long long n_chunks,
     return hipGetLastError();
 }
 
+hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st) {
+    hipLaunchKernelGGL(k_cold_scan, dim3(c.n_tiles), dim3(256), 0, st, c.tcnt, c.rows, c.n_tiles,
+                       c.boff, c.tile_total);
+    hipLaunchKernelGGL(k_cold_plan, dim3(1), dim3(1024), 0, st, c.tile_total, c.n_tiles, c.item_keys,
+                       c.tile_base, c.items, c.item_count, c.max_items);
+    const size_t sm = cold_sort_smem(c.n_tiles);
+    hipError_t e = hipSuccess;
+    switch (c.tile_bits) {
+#define LDE_COLD(TB)                                                                              \
+    case TB:                                                                                      \
+        (void)hipFuncSetAttribute((const void *)k_cold_sort<TB>,                                  \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);           \
+        hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows), dim3(kSortThreads), sm, st, c.cold,     \
+                           c.stride, c.cap, c.cold_cnt, c.boff, c.tile_base, c.n_tiles, c.keys);  \
+        hipLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, st,   \
+                           c.keys, c.items, c.item_count, c.hist, c.n_bins);                      \
+        break;
+        LDE_COLD(13)
+        LDE_COLD(14)
+        LDE_COLD(15)
+#undef LDE_COLD
+    default:
+        e = hipErrorInvalidValue;
+    }
+    if (e != hipSuccess) return e;
+    return hipGetLastError();
+}
+
 template <int ABL>
 static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st) {
-    const size_t sm = sieve_smem(a.hot_words, a.cbits, a.toa_words4);
+    const size_t sm = sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles);
     (void)hipFuncSetAttribute((const void *)k_sieve<ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)sm);
     hipLaunchKernelGGL(k_sieve<ABL>, dim3(grid), dim3(kSplitThreads), sm, st, a);
@@ -395,6 +645,8 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st) {
     case 4: return launch_sieve_t<4>(a, grid, st);
     case 7: return launch_sieve_t<7>(a, grid, st);
     case 15: return launch_sieve_t<15>(a, grid, st);
+    case 16: return launch_sieve_t<16>(a, grid, st);
+    case 32: return launch_sieve_t<32>(a, grid, st);
     default: return launch_sieve_t<0>(a, grid, st);
     }
 }

@@ -576,6 +576,16 @@ hipError_t launch_split(const SplitArgs &a, hipStream_t st) {
     return a.cache_bits > 0 ? launch_split_t<false, true>(a, st) : launch_split_t<false, false>(a, st);
 }
 
+hipError_t launch_hot_reduce(const SplitArgs &a, uint32_t *win, hipStream_t st) {
+    const int ht = a.rows * a.tp.T;
+    const int ht4 = align4(ht);
+    const int slices = 8;
+    const int per = (a.grid + slices - 1) / slices;
+    hipLaunchKernelGGL(k_hot_reduce, dim3((ht + 255) / 256, slices), dim3(256), 0, st, a.hot_part,
+                       a.grid, ht, ht4, a.tp.T, per, a.row_screen, win);
+    return hipGetLastError();
+}
+
 hipError_t launch_split_tail(const SplitArgs &a, uint32_t *win, SegDesc *cold_segs,
                              long long *n_cold_chunks, hipStream_t st) {
     const int ht = a.rows * a.tp.T;
