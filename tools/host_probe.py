@@ -1,0 +1,36 @@
+"""Host-side cost of one bench step (diagnostic): wall time of the staging
+calls, accumulate and finalize, with and without kernel timing events."""
+import sys, time
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import torch
+from esslivedata_amd import projection, synthetic
+from esslivedata_amd.engine import BinningEngine
+
+dev = torch.device('cuda', 0)
+inst = synthetic.dream_mantle()
+view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+eng = BinningEngine(toa_edges_ns=inst.edges.edges_ns(), out_lut=view.lut, pid_offset=view.pid_offset,
+                    n_screen=view.n_screen, strategy='auto', device=0,
+                    stream=torch.cuda.current_stream(dev).cuda_stream)
+n_pulse, pulses = 10_000_000, 14
+pid, toa = synthetic.torch_dream_events(n_pulse * pulses, inst, 7, dev)
+torch.cuda.synchronize()
+for timing in (False, True):
+    eng.timing_enable(timing)
+    acc = {'stage': 0.0, 'accumulate': 0.0, 'finalize': 0.0}
+    for i in range(25):
+        t0 = time.perf_counter()
+        for p in range(pulses):
+            eng.stage_tensors(pid[p * n_pulse:(p + 1) * n_pulse], toa[p * n_pulse:(p + 1) * n_pulse])
+        t1 = time.perf_counter()
+        eng.accumulate(i % view.n_replicas)
+        t2 = time.perf_counter()
+        eng.finalize(images=True)
+        t3 = time.perf_counter()
+        if i >= 5:
+            acc['stage'] += t1 - t0
+            acc['accumulate'] += t2 - t1
+            acc['finalize'] += t3 - t2
+    print('timing' if timing else 'no timing', {k: round(v / 20 * 1e3, 4) for k, v in acc.items()},
+          'ms/step total', round(sum(acc.values()) / 20 * 1e3, 4), flush=True)
