@@ -170,9 +170,15 @@ def main():
 
     reducer = WindowReducer(eng, dev) if world > 1 else None
 
+    # one device buffer view per ev44 message, made once: in the service each
+    # message arrives as its own buffer, slicing here is only how the
+    # synthetic stream is laid out
+    messages = [(pid[p * n_pulse : (p + 1) * n_pulse], toa[p * n_pulse : (p + 1) * n_pulse])
+                for p in range(args.pulses)]
+
     def step(i: int):
-        for p in range(args.pulses):
-            eng.stage_tensors(pid[p * n_pulse : (p + 1) * n_pulse], toa[p * n_pulse : (p + 1) * n_pulse])
+        for mp, mt in messages:
+            eng.stage_tensors(mp, mt)
         eng.accumulate(i % view.n_replicas)
         root = reducer.reduce() if reducer is not None else True
         if root:

@@ -1101,7 +1101,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         CREATE_CHECK(dev_alloc(h, &h->d_cumf, (size_t)nbins));
         CREATE_CHECK(ensure_win64(h));
     }
-    CREATE_CHECK(dev_alloc(h, &h->d_tot4, 4));
+    CREATE_CHECK(dev_alloc(h, &h->d_tot4, 4 + 4 * 8192));  // totals + per-block partials
     CREATE_CHECK(dev_alloc(h, (double **)&h->d_img_cur, (size_t)h->S));
     CREATE_CHECK(dev_alloc(h, (double **)&h->d_img_cum, (size_t)h->S));
     CREATE_CHECK(zero_state(h));
@@ -1375,7 +1375,6 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
             HIPCALL(h, hipMemcpyAsync(out->cumulative_hist, h->d_cumf, nb * 4,
                                       hipMemcpyDeviceToHost, h->stream));
     }
-    HIPCALL(h, hipMemsetAsync(h->d_tot4, 0, 32, h->stream));
     {
         Timed tm(h, LDE_K_FINALIZE);
         HIPCALL(h, lde::launch_finalize(

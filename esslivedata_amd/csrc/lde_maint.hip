@@ -107,10 +107,103 @@ __global__ __launch_bounds__(256) void k_finalize(uint32_t *__restrict__ win32,
     if (lane == 0)
         for (int q = 0; q < 4; ++q) s_tot[wid][q] = acc[q];
     __syncthreads();
+    // per-block partials (summed by k_sum_totals): thousands of same-word
+    // atomics would serialize at the memory side
+    if (threadIdx.x < 4)
+        totals[4 + (size_t)blockIdx.x * 4 + threadIdx.x] =
+            s_tot[0][threadIdx.x] + s_tot[1][threadIdx.x] + s_tot[2][threadIdx.x] + s_tot[3][threadIdx.x];
+}
+
+// Same as k_finalize for T % 4 == 0 and T <= 128: a 32-lane group per screen
+// row (two rows per wave), 4 bins per lane with 16-byte loads and stores, and
+// 5-step group reductions instead of 6-step wave reductions per row.
+template <typename OUT>
+__global__ __launch_bounds__(256) void k_finalize_v4(uint32_t *__restrict__ win32,
+                                                     unsigned long long *__restrict__ win64,
+                                                     unsigned long long *__restrict__ cum,
+                                                     unsigned long long *__restrict__ snap,
+                                                     long long S, int T, int lo, int hi,
+                                                     OUT *__restrict__ cur_img,
+                                                     OUT *__restrict__ cum_img,
+                                                     unsigned long long *__restrict__ totals) {
+    typedef unsigned long long u64;
+    __shared__ u64 s_tot[8][4];
+    const int gl = threadIdx.x & 31, grp = threadIdx.x >> 5;  // 8 row groups per block
+    u64 acc[4] = {0, 0, 0, 0};
+    const int i0 = gl * 4;
+    const bool act = i0 < T;
+    for (long long s = (long long)blockIdx.x * 8 + grp; s < S; s += (long long)gridDim.x * 8) {
+        u64 rw = 0, rc = 0, tw = 0, tc = 0;
+        if (act) {
+            const long long k = s * T + i0;
+            const uint4 w4 = *reinterpret_cast<const uint4 *>(win32 + k);
+            u64 w[4] = {w4.x, w4.y, w4.z, w4.w};
+            if (win64) {
+                const ulonglong2 a = *reinterpret_cast<const ulonglong2 *>(win64 + k);
+                const ulonglong2 b = *reinterpret_cast<const ulonglong2 *>(win64 + k + 2);
+                w[0] += a.x; w[1] += a.y; w[2] += b.x; w[3] += b.y;
+                *reinterpret_cast<ulonglong2 *>(win64 + k) = make_ulonglong2(0, 0);
+                *reinterpret_cast<ulonglong2 *>(win64 + k + 2) = make_ulonglong2(0, 0);
+            }
+            const ulonglong2 c01 = *reinterpret_cast<const ulonglong2 *>(cum + k);
+            const ulonglong2 c23 = *reinterpret_cast<const ulonglong2 *>(cum + k + 2);
+            const u64 c[4] = {c01.x + w[0], c01.y + w[1], c23.x + w[2], c23.y + w[3]};
+            *reinterpret_cast<ulonglong2 *>(cum + k) = make_ulonglong2(c[0], c[1]);
+            *reinterpret_cast<ulonglong2 *>(cum + k + 2) = make_ulonglong2(c[2], c[3]);
+            if (snap) {
+                *reinterpret_cast<ulonglong2 *>(snap + k) = make_ulonglong2(w[0], w[1]);
+                *reinterpret_cast<ulonglong2 *>(snap + k + 2) = make_ulonglong2(w[2], w[3]);
+            }
+            *reinterpret_cast<uint4 *>(win32 + k) = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                tw += w[q];
+                tc += c[q];
+                if (i0 + q >= lo && i0 + q < hi) {
+                    rw += w[q];
+                    rc += c[q];
+                }
+            }
+        }
+#pragma unroll
+        for (int d = 16; d > 0; d >>= 1) {
+            rw += __shfl_xor(rw, d, 32);
+            rc += __shfl_xor(rc, d, 32);
+            tw += __shfl_xor(tw, d, 32);
+            tc += __shfl_xor(tc, d, 32);
+        }
+        if (gl == 0) {
+            if (cur_img) cur_img[s] = (OUT)rw;
+            if (cum_img) cum_img[s] = (OUT)rc;
+            acc[0] += tw;
+            acc[1] += rw;
+            acc[2] += tc;
+            acc[3] += rc;
+        }
+    }
+    if (gl == 0)
+        for (int q = 0; q < 4; ++q) s_tot[grp][q] = acc[q];
+    __syncthreads();
     if (threadIdx.x < 4) {
-        const unsigned long long v = s_tot[0][threadIdx.x] + s_tot[1][threadIdx.x] +
-                                     s_tot[2][threadIdx.x] + s_tot[3][threadIdx.x];
-        if (v) atomicAdd(totals + threadIdx.x, v);
+        u64 v = 0;
+        for (int g = 0; g < 8; ++g) v += s_tot[g][threadIdx.x];
+        totals[4 + (size_t)blockIdx.x * 4 + threadIdx.x] = v;
+    }
+}
+
+// totals[q] = sum over blocks of the partials at totals[4 + 4 * block + q]
+__global__ __launch_bounds__(256) void k_sum_totals(unsigned long long *__restrict__ totals,
+                                                    int blocks) {
+    __shared__ unsigned long long s[4][64];
+    const int q = threadIdx.x & 3, r = threadIdx.x >> 2;
+    unsigned long long v = 0;
+    for (int b = r; b < blocks; b += 64) v += totals[4 + (size_t)b * 4 + q];
+    s[q][r] = v;
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        unsigned long long t = 0;
+        for (int i = 0; i < 64; ++i) t += s[threadIdx.x][i];
+        totals[threadIdx.x] = t;
     }
 }
 
@@ -153,6 +246,21 @@ hipError_t launch_finalize(bool f32_images, uint32_t *win32, unsigned long long 
                            unsigned long long *cum, unsigned long long *snap, long long S, int T,
                            int lo, int hi, void *cur_img, void *cum_img,
                            unsigned long long *totals, hipStream_t st) {
+    if (T % 4 == 0 && T <= 128) {
+        long long b8 = (S + 7) / 8;
+        if (b8 > 8192) b8 = 8192;
+        if (b8 < 1) b8 = 1;
+        if (f32_images)
+            hipLaunchKernelGGL(k_finalize_v4<float>, dim3((unsigned)b8), dim3(256), 0, st, win32,
+                               win64, cum, snap, S, T, lo, hi, (float *)cur_img, (float *)cum_img,
+                               totals);
+        else
+            hipLaunchKernelGGL(k_finalize_v4<double>, dim3((unsigned)b8), dim3(256), 0, st, win32,
+                               win64, cum, snap, S, T, lo, hi, (double *)cur_img,
+                               (double *)cum_img, totals);
+        hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(256), 0, st, totals, (int)b8);
+        return hipGetLastError();
+    }
     long long blocks = (S + 3) / 4;
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
@@ -164,6 +272,7 @@ hipError_t launch_finalize(bool f32_images, uint32_t *win32, unsigned long long 
         hipLaunchKernelGGL(k_finalize<double>, dim3((unsigned)blocks), dim3(256), 0, st, win32,
                            win64, cum, snap, S, T, lo, hi, (double *)cur_img, (double *)cum_img,
                            totals);
+    hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(256), 0, st, totals, (int)blocks);
     return hipGetLastError();
 }
 

@@ -42,6 +42,7 @@ namespace lde {
 namespace {
 
 constexpr uint32_t kOOB = 0x80000000u;        // buffer offset past every num_records
+constexpr uint32_t kOOBi = 0xFFFFFFF0u;       // same, as an inline constant (-16): loads only
 constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data format
 constexpr int kEPT = kSplitEPT;               // 8 events per thread per chunk
 constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (half a chunk)
@@ -59,6 +60,19 @@ __device__ __forceinline__ int screen_of_lut(const uint16_t *__restrict__ lut, l
 __device__ __forceinline__ int screen_of_lut(const int *__restrict__ lut, long long q, int T) {
     const int v = lut[q];
     return v < 0 ? -1 : v / T;
+}
+
+// v_cndmask on a wave mask: m's lane bit ? t : f.  Written as asm so the
+// compiler cannot turn a select between LDS addresses into a branch.
+__device__ __forceinline__ uint32_t vsel(unsigned long long m, uint32_t t, uint32_t f) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;
+}
+
+// LDS word at a byte offset (the sieve keeps its LDS indices pre-scaled)
+__device__ __forceinline__ uint32_t &lds_at(uint32_t *sm, uint32_t byte_off) {
+    return *reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(sm) + byte_off);
 }
 
 }  // namespace
@@ -135,7 +149,8 @@ __global__ __launch_bounds__(256) void k_chunk_tab(const SegDesc *__restrict__ s
 // gather lane out of range, 32 every gather lane on the first two words
 template <int ABL>
 __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    // static, so LDS addresses need no runtime base (one block per CU anyway)
+    __shared__ __attribute__((aligned(16))) uint32_t sm[kSplitSmemMax / 4];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const uint32_t C = 1u << a.cbits;
@@ -170,7 +185,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t wmask = (1u << a.toa_shift) - 1u;
     const uint32_t T = (uint32_t)a.T;
     const uint32_t dum_idx = o_dum + (uint32_t)lane;
+    const uint32_t dum4 = dum_idx * 4u;
     const uint32_t o_stg_w = o_stg + kSieveStage * (uint32_t)(tid >> 6);
+    const uint32_t o_pc4 = o_pc * 4u, o_tt4 = o_tt * 4u, o_tcnt4 = o_tcnt * 4u;
+    const int tsh = a.tile_bits + 2;
 
     // ---- contiguous chunk range of this block
     const long long n = a.n_chunks;
@@ -222,15 +240,16 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 w[e] = q ^ d;
                 tw[e] = d & 0xFFFu;
             } else {
-                w[e] = sm[o_pc + (q & cmask)];
-                tw[e] = sm[o_tt + (d >> a.toa_shift)];
+                w[e] = lds_at(sm, o_pc4 + ((q & cmask) << 2));
+                tw[e] = lds_at(sm, o_tt4 + ((d >> a.toa_shift) << 2));
             }
         }
 #pragma unroll
         for (int e = 0; e < kEPT; ++e) {
-            const bool hit = ((w[e] >> kSieveTagShift) & 0xFFu) == (qs[e] >> a.cbits);
-            ws[e] = hit ? w[e] : 0u;
-            uint32_t off = hit ? kOOB : (min(qs[e], Lc) << 2);
+            const unsigned long long hit =
+                __builtin_amdgcn_ballot_w64(((w[e] >> kSieveTagShift) & 0xFFu) == (qs[e] >> a.cbits));
+            ws[e] = vsel(hit, w[e], 0u);
+            uint32_t off = vsel(hit, kOOBi, min(qs[e], Lc) << 2);
             if (ABL & 16) off = kOOB | (off & 4u);
             if (ABL & 32) off = off & 4u;
             g[e] = (ABL & 2) ? (off & 0x3u) : __builtin_amdgcn_raw_buffer_load_b32(glut, (int)off, 0, 0);
@@ -253,20 +272,25 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 const uint32_t v = ws[e] | g[e];
                 const uint32_t b = (tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u);
                 const uint32_t fl = v >> 30;
-                const bool inb = b < T;
-                const uint32_t k = (v & kSieveValueMask) + b;
-                const bool cm = inb && fl == 2u;
-                const unsigned long long bal = __ballot(cm);
-                const uint32_t sidx = cm ? (o_stg_w + tot + lanes_below(bal)) : dum_idx;
+                // hot rows start at LDS byte 0, so the scaled key is the hot
+                // counter's address; cold keys leave scaled by 4 as well
+                const uint32_t k4 = ((v & kSieveValueMask) + b) << 2;
+                // lane masks straight from the compares (no bool round trip)
+                const unsigned long long inb = __builtin_amdgcn_ballot_w64(b < T);
+                const unsigned long long bal = inb & __builtin_amdgcn_ballot_w64(fl == 2u);
+                const unsigned long long hm = inb & __builtin_amdgcn_ballot_w64(fl == 3u);
+                const uint32_t pos4 = (lanes_below(bal) + o_stg_w + tot) << 2;
                 tot += (uint32_t)__popcll(bal);
-                const uint32_t hidx = (inb && fl == 3u) ? k : dum_idx;
+                const uint32_t hidx4 = vsel(hm, k4, dum4);
                 if (!(ABL & 1))
-                    __hip_atomic_fetch_add(sm + hidx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&lds_at(sm, hidx4), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                 else
-                    tot += hidx & 1u;
-                sm[sidx] = k;
-                const uint32_t tidx = cm ? o_tcnt + (k >> a.tile_bits) : dum_idx;
-                __hip_atomic_fetch_add(sm + tidx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    tot += hidx4 & 1u;
+                lds_at(sm, vsel(bal, pos4, dum4)) = k4;
+                const uint32_t tidx4 = vsel(bal, ((k4 >> tsh) << 2) + o_tcnt4, dum4);
+                __hip_atomic_fetch_add(&lds_at(sm, tidx4), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             const uint32_t res = (tot + 3u) & ~3u;
             uint32_t wbase = 0;
@@ -438,7 +462,7 @@ __global__ __launch_bounds__(1024) void k_cold_plan(const uint32_t *__restrict__
     if (tid == 0) *item_count = n_items;
 }
 
-// One block per sieve block: its cold region is sorted by tile in 16K-key
+// One block per sieve block: its cold region (keys scaled by 4, -1 pads) is sorted by tile in 16K-key
 // pieces in LDS (rank by LDS atomics, scan over tiles, scatter), and each
 // piece's tile runs are written as u16 tile-local keys at the block's exact
 // offsets of the tile-major array.  Pad keys (-1) are skipped.
@@ -495,7 +519,7 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
         for (int e = 0; e < KPT; ++e) {
             rank[e] = 0;
             if (key[e] != 0xFFFFFFFFu)
-                rank[e] = __hip_atomic_fetch_add(s_cnt + (key[e] >> TB), 1u, __ATOMIC_RELAXED,
+                rank[e] = __hip_atomic_fetch_add(s_cnt + (key[e] >> (TB + 2)), 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         __syncthreads();
@@ -517,12 +541,12 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
         __syncthreads();
 #pragma unroll
         for (int e = 0; e < KPT; ++e)
-            if (key[e] != 0xFFFFFFFFu) s_sorted[s_start[key[e] >> TB] + rank[e]] = key[e];
+            if (key[e] != 0xFFFFFFFFu) s_sorted[s_start[key[e] >> (TB + 2)] + rank[e]] = key[e];
         __syncthreads();
         for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
             const uint32_t k = s_sorted[i];
-            const uint32_t t = k >> TB;
-            out[s_cur[t] + (i - s_start[t])] = (uint16_t)(k & MASK);
+            const uint32_t t = k >> (TB + 2);
+            out[s_cur[t] + (i - s_start[t])] = (uint16_t)((k >> 2) & MASK);
         }
         __syncthreads();
         for (int t = tid; t < n_tiles; t += kSortThreads) s_cur[t] += s_cnt[t];
@@ -631,10 +655,9 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st) {
 
 template <int ABL>
 static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st) {
-    const size_t sm = sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles);
-    (void)hipFuncSetAttribute((const void *)k_sieve<ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sm);
-    hipLaunchKernelGGL(k_sieve<ABL>, dim3(grid), dim3(kSplitThreads), sm, st, a);
+    if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles) > kSplitSmemMax)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_sieve<ABL>, dim3(grid), dim3(kSplitThreads), 0, st, a);  // static LDS
     return hipGetLastError();
 }
 
