@@ -1216,7 +1216,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 CREATE_CHECK(dev_alloc(h, &h->d_sample_part, (size_t)lde::kSampleBlocks * h->S));
                 CREATE_CHECK(dev_alloc(h, &h->d_screen_cnt, (size_t)h->S));
                 CREATE_CHECK(dev_alloc(h, &h->d_screen_row, (size_t)h->S));
-                CREATE_CHECK(dev_alloc(h, &h->d_cold_cnt, (size_t)h->split_grid));
+                CREATE_CHECK(dev_alloc(h, &h->d_cold_cnt, (size_t)h->split_grid * (lde::kSplitThreads / 64)));  // SIEVE: per wave
                 CREATE_CHECK(dev_alloc(h, &h->d_cold_segs, (size_t)h->split_grid));
                 CREATE_CHECK(dev_alloc(h, &h->d_cold_chunks, 1));
                 CREATE_CHECK(dev_alloc(h, &h->d_dummy, 16));

@@ -189,6 +189,9 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t o_stg_w = o_stg + kSieveStage * (uint32_t)(tid >> 6);
     const uint32_t o_pc4 = o_pc * 4u, o_tt4 = o_tt * 4u, o_tcnt4 = o_tcnt * 4u;
     const int tsh = a.tile_bits + 2;
+    // this wave's sub-region of the block's cold region (keys), 16-B aligned
+    const uint32_t capw = (uint32_t)(a.cold_cap / (kSplitThreads / 64));
+    const uint32_t wave_base = capw * (uint32_t)(tid >> 6);
 
     // ---- contiguous chunk range of this block
     const long long n = a.n_chunks;
@@ -225,11 +228,11 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             }
         }
     };
-    // stage 2: table probe + TOA bucket (LDS), one gather per event
-    auto lookup = [&](const int (&p)[kEPT], const int (&t)[kEPT], uint32_t (&ws)[kEPT],
-                      uint32_t (&g)[kEPT], uint32_t (&dc)[kEPT], uint32_t (&tw)[kEPT])
-                      __attribute__((always_inline)) {
-        uint32_t w[kEPT], qs[kEPT];
+    // stage 2a: table probe + TOA bucket, LDS reads only (issued before the
+    // previous chunk's LDS atomics, so their latency hides behind its binning)
+    auto probe = [&](const int (&p)[kEPT], const int (&t)[kEPT], uint32_t (&w)[kEPT],
+                     uint32_t (&qs)[kEPT], uint32_t (&dc)[kEPT], uint32_t (&tw)[kEPT])
+                     __attribute__((always_inline)) {
 #pragma unroll
         for (int e = 0; e < kEPT; ++e) {
             const uint32_t q = (uint32_t)p[e] - pid_off;
@@ -244,24 +247,33 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 tw[e] = lds_at(sm, o_tt4 + ((d >> a.toa_shift) << 2));
             }
         }
+    };
+    // stage 2b: tag check, one gather per event (a table hit or an
+    // out-of-range pixel loads out of range: no request, returns 0); w -> the
+    // table word of hits (0 otherwise), qs -> the gathered word
+    auto finish = [&](uint32_t (&w)[kEPT], uint32_t (&qs)[kEPT]) __attribute__((always_inline)) {
 #pragma unroll
         for (int e = 0; e < kEPT; ++e) {
             const unsigned long long hit =
                 __builtin_amdgcn_ballot_w64(((w[e] >> kSieveTagShift) & 0xFFu) == (qs[e] >> a.cbits));
-            ws[e] = vsel(hit, w[e], 0u);
             uint32_t off = vsel(hit, kOOBi, min(qs[e], Lc) << 2);
             if (ABL & 16) off = kOOB | (off & 4u);
             if (ABL & 32) off = off & 4u;
-            g[e] = (ABL & 2) ? (off & 0x3u) : __builtin_amdgcn_raw_buffer_load_b32(glut, (int)off, 0, 0);
+            w[e] = vsel(hit, w[e], 0u);
+            qs[e] = (ABL & 2) ? (off & 0x3u) : __builtin_amdgcn_raw_buffer_load_b32(glut, (int)off, 0, 0);
         }
     };
     // stage 3: bin, in two halves of four events per lane.  Hot lanes add 1
     // to their LDS row (the others to a lane-private dummy); cold keys are
     // compacted into the wave's 256-word LDS staging area (the others write a
-    // dummy), the wave reserves round4(count) slots of the block's cold region
-    // with one LDS atomic, and every lane stores 16 staged bytes at once (lanes
-    // past the reservation store out of range).  Staging words are reset to
-    // -1, so the <= 3 pad keys of a reservation are dropped by the key pass.
+    // dummy) and leave as one 16-byte store per lane into the wave's own
+    // sub-region of the block's cold region, at an SGPR cursor (no atomics).
+    // The staged words are read back right away but stored one half later,
+    // so that read's LDS latency is not waited for.  Staging words are reset
+    // to -1, so the <= 3 pad keys of round4(count) are dropped by the sort.
+    v4u pend_kv = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    uint32_t pend_off = kOOB;
+    uint32_t wcur = 0;  // this wave's cold keys so far (wave-uniform)
     auto bin = [&](const uint32_t (&ws)[kEPT], const uint32_t (&g)[kEPT], const uint32_t (&dc)[kEPT],
                    const uint32_t (&tw)[kEPT]) __attribute__((always_inline)) {
 #pragma unroll
@@ -293,26 +305,23 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             const uint32_t res = (tot + 3u) & ~3u;
-            uint32_t wbase = 0;
-            if (lane == 0)
-                wbase = __hip_atomic_fetch_add(sm + o_cur, res, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-            wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)wbase);
+            // the previous half's keys leave now (their LDS read is long done)
+            if (!(ABL & 4)) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+            else sm[o_dum + lane] += pend_kv[0] ^ pend_off;
             __builtin_amdgcn_wave_barrier();
             uint4 *slot = reinterpret_cast<uint4 *>(sm + o_stg_w + 4u * (uint32_t)lane);
             const uint4 kv = *slot;
             *slot = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
             __builtin_amdgcn_wave_barrier();
-            const uint32_t off = 4u * (uint32_t)lane < res ? (wbase + 4u * (uint32_t)lane) << 2 : kOOB;
-            v4u kk = {kv.x, kv.y, kv.z, kv.w};
-            if (!(ABL & 4)) __builtin_amdgcn_raw_buffer_store_b128(kk, cold, (int)off, 0, 0);
-            else sm[o_dum + lane] += kv.x ^ off;
+            pend_kv = v4u{kv.x, kv.y, kv.z, kv.w};
+            pend_off = 4u * (uint32_t)lane < res ? (wave_base + wcur + 4u * (uint32_t)lane) << 2 : kOOB;
+            wcur += res;
         }
     };
 
-    // ---- pipeline: chunk i is binned while chunk i+1 is looked up, chunks
-    // i+2, i+3 stream in and the descriptor of i+4 is fetched (register sets
-    // A and B alternate)
+    // ---- pipeline: chunk i is binned while chunk i+1 is probed (before) and
+    // gathered (after), chunks i+2, i+3 stream in and the descriptor of i+4 is
+    // fetched (register sets A/B and X/Y alternate)
     int pA[kEPT], tA[kEPT], pB[kEPT], tB[kEPT];
     uint32_t wsX[kEPT], gX[kEPT], dX[kEPT], twX[kEPT];
     uint32_t wsY[kEPT], gY[kEPT], dY[kEPT], twY[kEPT];
@@ -322,17 +331,20 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         load(dB, pB, tB);
         dA = fetch(cb + 2);
         dB = fetch(cb + 3);
-        lookup(pA, tA, wsX, gX, dX, twX);
+        probe(pA, tA, wsX, gX, dX, twX);
+        finish(wsX, gX);
         load(dA, pA, tA);
         dA = fetch(cb + 4);
         for (long long c = cb; c < ce; c += 2) {
-            bin(wsX, gX, dX, twX);  // chunk c
-            lookup(pB, tB, wsY, gY, dY, twY);
+            probe(pB, tB, wsY, gY, dY, twY);  // chunk c + 1
+            bin(wsX, gX, dX, twX);             // chunk c
+            finish(wsY, gY);
             load(dB, pB, tB);  // chunk c + 3
             dB = fetch(c + 5);
             if (c + 1 >= ce) break;
-            bin(wsY, gY, dY, twY);  // chunk c + 1
-            lookup(pA, tA, wsX, gX, dX, twX);
+            probe(pA, tA, wsX, gX, dX, twX);  // chunk c + 2
+            bin(wsY, gY, dY, twY);             // chunk c + 1
+            finish(wsX, gX);
             load(dA, pA, tA);  // chunk c + 4
             dA = fetch(c + 6);
         }
@@ -369,15 +381,18 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                     t[j * 4 + q] = tv;
                 }
             }
-            lookup(p, t, wsX, gX, dX, twX);
+            probe(p, t, wsX, gX, dX, twX);
+            finish(wsX, gX);
             bin(wsX, gX, dX, twX);
         }
     }
+    // the last half's keys
+    if (!(ABL & 4)) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+    if (lane == 0) a.cold_cnt[(size_t)blockIdx.x * (kSplitThreads / 64) + (tid >> 6)] = wcur;
     __syncthreads();
     uint32_t *dst = a.hot_part + (size_t)blockIdx.x * a.hot_words;
     for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4)
         *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(sm + i);
-    if (tid == 0) a.cold_cnt[blockIdx.x] = sm[o_cur];
     for (int i = tid; i < a.n_tiles; i += kSplitThreads)
         a.cold_tcnt[(size_t)blockIdx.x * a.n_tiles + i] = sm[o_tcnt + i];
 }
@@ -462,7 +477,8 @@ __global__ __launch_bounds__(1024) void k_cold_plan(const uint32_t *__restrict__
     if (tid == 0) *item_count = n_items;
 }
 
-// One block per sieve block: its cold region (keys scaled by 4, -1 pads) is sorted by tile in 16K-key
+// One block per sieve block: its cold region (keys scaled by 4, -1 pads; 16
+// wave sub-regions) is sorted by tile in 16K-key
 // pieces in LDS (rank by LDS atomics, scan over tiles, scatter), and each
 // piece's tile runs are written as u16 tile-local keys at the block's exact
 // offsets of the tile-major array.  Pad keys (-1) are skipped.
@@ -488,7 +504,31 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
     uint32_t *s_w = s_cur + nt4;
     const int tid = threadIdx.x;
     const int b = blockIdx.x;
-    const uint32_t n = cold_cnt[b];
+    // the sieve block's cold region = 16 wave sub-regions of cap / 16 keys,
+    // each filled to a multiple of 4; logical key i lives in the sub-region
+    // of the last wave whose prefix is <= i
+    constexpr int NW = kSplitThreads / 64;
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int w = 0; w < NW; ++w) {
+            s_w[w] = acc;
+            acc += cold_cnt[(size_t)b * NW + w];
+        }
+        s_w[NW] = acc;
+    }
+    __syncthreads();
+    uint32_t pre[NW + 1];
+#pragma unroll
+    for (int w = 0; w <= NW; ++w) pre[w] = s_w[w];
+    __syncthreads();
+    const uint32_t n = pre[NW];
+    const uint32_t capw = (uint32_t)(cap / NW);
+    auto phys = [&](uint32_t i) __attribute__((always_inline)) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int q = 1; q < NW; ++q) w = i >= pre[q] ? (uint32_t)q : w;
+        return i < n ? (w * capw + (i - pre[w])) * 4u : 0x80000000u;
+    };
     const uint32_t *src = cold + (size_t)b * (size_t)stride;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, (uint32_t)(cap * 4));
     for (int t = tid; t < n_tiles; t += kSortThreads)
@@ -500,7 +540,7 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
 #pragma unroll
         for (int j = 0; j < KPT / 4; ++j) {
             const uint32_t e0 = p0 + ((uint32_t)j * kSortThreads + (uint32_t)tid) * 4u;
-            nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
+            nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)phys(e0), 0, 0);
         }
     };
     if (n > 0) fetch(0);
