@@ -8,8 +8,9 @@ geomspace TOA bins, Zipf(1.2) pixel skew + 3 hot TOA bins.  One step = one 1 Hz
 service batch: 14 ev44 pulses of 1e7 events each (1.4e8 events) staged from
 HBM, binned into the current window (accumulate), then finalized (cumulative
 += window, images and totals to the host).  With N > 1 ranks every rank bins
-its own batch (event-batch sharding, weak scaling) and the window histograms
-are summed onto rank 0 with an RCCL reduce over xGMI before rank 0 finalizes.
+its own batch (event-batch sharding, weak scaling) into its own histograms, and
+each finalize RCCL-reduces the ranks' exact partial outputs (u64 images and
+totals) onto rank 0 over xGMI.
 
 Prints ONE JSON line on rank 0.
 """
@@ -166,9 +167,12 @@ def main():
         pid, toa = synthetic.torch_uniform_events(n_step, 1, 802816, seed, dev)
     torch.cuda.synchronize(dev)
     nbins = view.n_screen * eng.n_toa_bins
-    from esslivedata_amd.distributed import WindowReducer
+    from esslivedata_amd.distributed import OutputReducer
 
-    reducer = WindowReducer(eng, dev) if world > 1 else None
+    # N > 1: every rank keeps its own histograms; per finalize only the
+    # published outputs (u64 partial images + totals, 2*S + 4 words) are
+    # RCCL-reduced onto rank 0 (bit-exact integer sums)
+    reducer = OutputReducer(eng, dev) if world > 1 else None
 
     # one device buffer view per ev44 message, made once: in the service each
     # message arrives as its own buffer, slicing here is only how the
@@ -180,11 +184,10 @@ def main():
         for mp, mt in messages:
             eng.stage_tensors(mp, mt)
         eng.accumulate(i % view.n_replicas)
-        root = reducer.reduce() if reducer is not None else True
-        if root:
-            eng.finalize(images=True)
+        if reducer is not None:
+            reducer.finalize()
         else:
-            eng.clear()
+            eng.finalize(images=True)
 
     for i in range(args.warmup):
         step(i)
@@ -257,7 +260,7 @@ def main():
             'pulses_per_step': args.pulses,
             'strategy': info['last_strategy'],
             'tile_bits': info['tile_bits'],
-            'parallelism': f'event-batch sharding x{world} + RCCL reduce' if world > 1 else 'single GPU',
+            'parallelism': f'event-batch sharding x{world} + RCCL reduce of partial outputs' if world > 1 else 'single GPU',
         },
         'roofline': {
             'bound': 'hbm',

@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     'lde_clear',
     'lde_reset_cumulative',
     'lde_export_window',
+    'lde_finalize_partials',
     'lde_import_window',
     'lde_synchronize',
     'lde_timing_enable',
@@ -117,6 +118,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_clear': (ctypes.c_int, [H]),
         'lde_reset_cumulative': (ctypes.c_int, [H]),
         'lde_export_window': (ctypes.c_int, [H, P]),
+        'lde_finalize_partials': (ctypes.c_int, [H, P]),
         'lde_import_window': (ctypes.c_int, [H, P]),
         'lde_synchronize': (ctypes.c_int, [H]),
         'lde_timing_enable': (ctypes.c_int, [H, i32]),

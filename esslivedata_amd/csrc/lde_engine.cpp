@@ -1378,7 +1378,7 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
     {
         Timed tm(h, LDE_K_FINALIZE);
         HIPCALL(h, lde::launch_finalize(
-                       f32, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
+                       f32 ? 1 : 0, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
                        (want_cur_hist && !f32) ? h->d_snap : nullptr, h->S, h->T, h->range_lo,
                        h->range_hi, (!f32 && out->current_image) ? h->d_img_cur : nullptr,
                        (!f32 && out->cumulative_image) ? h->d_img_cum : nullptr, h->d_tot4,
@@ -1412,6 +1412,26 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
     HIPCALL(h, hipStreamSynchronize(h->stream));
     if (ovf) return fail(h, LDE_ESTATE, "page pool overflow (internal error)");
     for (int q = 0; q < 4; ++q) out->totals[q] = tot[q];
+    h->window_has_data = false;
+    h->win64_dirty = false;
+    h->win_events = 0;
+    return LDE_OK;
+}
+
+int lde_finalize_partials(lde_handle *h, void *d_out) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!d_out) return fail(h, LDE_EINVAL, "output buffer is NULL");
+    if (h->out_dtype == LDE_F32)
+        return fail(h, LDE_EINVAL, "partial outputs need an integer-exact (float64) view");
+    DeviceGuard guard(h->device);
+    unsigned long long *o = (unsigned long long *)d_out;
+    {
+        Timed tm(h, LDE_K_FINALIZE);
+        HIPCALL(h, lde::launch_finalize(2, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr,
+                                        h->d_cum, nullptr, h->S, h->T, h->range_lo, h->range_hi,
+                                        o, o + h->S, h->d_tot4, h->stream));
+    }
+    HIPCALL(h, hipMemcpyAsync(o + 2 * h->S, h->d_tot4, 32, hipMemcpyDeviceToDevice, h->stream));
     h->window_has_data = false;
     h->win64_dirty = false;
     h->win_events = 0;

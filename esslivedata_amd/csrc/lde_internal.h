@@ -233,7 +233,7 @@ hipError_t launch_merge_f32(uint32_t *batch, unsigned long long *win64, float *w
                             long long n, int first_win, int first_cum, hipStream_t st);
 hipError_t launch_sum3(const unsigned long long *a, const unsigned long long *b, const uint32_t *c,
                        unsigned long long *out, long long n, hipStream_t st);
-hipError_t launch_finalize(bool f32_images, uint32_t *win32, unsigned long long *win64,
+hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *win64,
                            unsigned long long *cum, unsigned long long *snap, long long S, int T,
                            int lo, int hi, void *cur_img, void *cum_img,
                            unsigned long long *totals, hipStream_t st);

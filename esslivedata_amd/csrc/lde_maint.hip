@@ -242,37 +242,40 @@ hipError_t launch_sum3(const unsigned long long *a, const unsigned long long *b,
     return hipGetLastError();
 }
 
-hipError_t launch_finalize(bool f32_images, uint32_t *win32, unsigned long long *win64,
-                           unsigned long long *cum, unsigned long long *snap, long long S, int T,
-                           int lo, int hi, void *cur_img, void *cum_img,
-                           unsigned long long *totals, hipStream_t st) {
+template <typename OUT>
+static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsigned long long *cum,
+                              unsigned long long *snap, long long S, int T, int lo, int hi,
+                              void *cur_img, void *cum_img, unsigned long long *totals,
+                              hipStream_t st) {
     if (T % 4 == 0 && T <= 128) {
         long long b8 = (S + 7) / 8;
         if (b8 > 8192) b8 = 8192;
         if (b8 < 1) b8 = 1;
-        if (f32_images)
-            hipLaunchKernelGGL(k_finalize_v4<float>, dim3((unsigned)b8), dim3(256), 0, st, win32,
-                               win64, cum, snap, S, T, lo, hi, (float *)cur_img, (float *)cum_img,
-                               totals);
-        else
-            hipLaunchKernelGGL(k_finalize_v4<double>, dim3((unsigned)b8), dim3(256), 0, st, win32,
-                               win64, cum, snap, S, T, lo, hi, (double *)cur_img,
-                               (double *)cum_img, totals);
+        hipLaunchKernelGGL(k_finalize_v4<OUT>, dim3((unsigned)b8), dim3(256), 0, st, win32, win64,
+                           cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, totals);
         hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(256), 0, st, totals, (int)b8);
-        return hipGetLastError();
+        return;
     }
     long long blocks = (S + 3) / 4;
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
-    if (f32_images)
-        hipLaunchKernelGGL(k_finalize<float>, dim3((unsigned)blocks), dim3(256), 0, st, win32,
-                           win64, cum, snap, S, T, lo, hi, (float *)cur_img, (float *)cum_img,
-                           totals);
-    else
-        hipLaunchKernelGGL(k_finalize<double>, dim3((unsigned)blocks), dim3(256), 0, st, win32,
-                           win64, cum, snap, S, T, lo, hi, (double *)cur_img, (double *)cum_img,
-                           totals);
+    hipLaunchKernelGGL(k_finalize<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
+                       cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, totals);
     hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(256), 0, st, totals, (int)blocks);
+}
+
+// image element type: 0 f64, 1 f32, 2 u64 (exact partial sums for multi-GPU)
+hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *win64,
+                           unsigned long long *cum, unsigned long long *snap, long long S, int T,
+                           int lo, int hi, void *cur_img, void *cum_img,
+                           unsigned long long *totals, hipStream_t st) {
+    if (img_kind == 1)
+        launch_finalize_t<float>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals, st);
+    else if (img_kind == 2)
+        launch_finalize_t<unsigned long long>(win32, win64, cum, snap, S, T, lo, hi, cur_img,
+                                              cum_img, totals, st);
+    else
+        launch_finalize_t<double>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals, st);
     return hipGetLastError();
 }
 

@@ -1,12 +1,18 @@
-"""Multi-GPU event-batch sharding with an RCCL window merge (no reference
-counterpart: the reference has no GPU or collective code).
+"""Multi-GPU event-batch sharding (no reference counterpart: the reference
+has no GPU or collective code).
 
 One process per GPU.  Every rank bins its own share of the event batches into
-its own uint32 window; at each finalize the windows are summed onto the root
-with ``torch.distributed.reduce`` (backend ``nccl`` = RCCL over xGMI on ROCm).
-Integer sums are order-independent, so the merged counts are bit-identical to
-a single-GPU run over all events.  The root then finalizes (cumulative +=
-window, images, totals); the other ranks drop their window.
+its own histograms.  Two merge modes, both bit-identical to a single GPU that
+binned every event (integer sums are order-independent):
+
+* ``OutputReducer`` (default): every rank keeps its own window and cumulative;
+  at each finalize only the outputs the detector view publishes are summed
+  onto the root -- uint64 partial images (current, cumulative) and totals,
+  2*S + 4 words (400 KB for DREAM) instead of the 10 MB window -- with one
+  ``torch.distributed.reduce`` (backend ``nccl`` = RCCL over xGMI on ROCm).
+* ``WindowReducer``: sums the uint32 windows onto the root, which then
+  finalizes as a single GPU would; needed when the full (S, T) histogram is
+  published.
 """
 
 from __future__ import annotations
@@ -32,6 +38,33 @@ def dist_env() -> tuple[int, int, int]:
     )
 
 
+class OutputReducer:
+    """Sums every rank's finalize outputs onto the root (see module doc)."""
+
+    def __init__(self, engine, device, *, dst: int = 0, group=None) -> None:
+        import torch
+
+        self.engine = engine
+        self.dst = dst
+        self.group = group
+        self.S = engine.n_screen
+        self.buf = torch.zeros(2 * self.S + 4, dtype=torch.int64, device=device)
+
+    def finalize(self):
+        """Collective.  On the root: (current image, cumulative image, totals)
+        as float64 numpy arrays and a list of 4 ints; elsewhere None."""
+        import torch.distributed as dist
+
+        self.engine.finalize_partials(self.buf.data_ptr())
+        self.engine.synchronize()  # the engine may run on its own stream
+        dist.reduce(self.buf, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group)
+        if dist.get_rank(self.group) != self.dst:
+            return None
+        h = self.buf.cpu().numpy()
+        S = self.S
+        return h[:S].astype('float64'), h[S : 2 * S].astype('float64'), [int(x) for x in h[2 * S :]]
+
+
 class WindowReducer:
     """Sums every rank's window into the root's window (SUM over uint32)."""
 
@@ -49,8 +82,13 @@ class WindowReducer:
         import torch.distributed as dist
 
         self.engine.export_window(self.buf.data_ptr())
+        self.engine.synchronize()  # the engine may run on its own stream
         dist.reduce(self.buf, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group)
         root = dist.get_rank(self.group) == self.dst
         if root:
+            if self.buf.is_cuda:
+                import torch
+
+                torch.cuda.synchronize(self.buf.device)  # reduce result before the engine's stream reads it
             self.engine.import_window(self.buf.data_ptr())
         return root

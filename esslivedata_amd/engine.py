@@ -197,6 +197,11 @@ class BinningEngine:
     def reset_cumulative(self) -> None:
         self._call(self._lib.lde_reset_cumulative)
 
+    def finalize_partials(self, dst_ptr: int) -> None:
+        """Finalize into device memory: uint64 [S] current image, [S]
+        cumulative image, [4] totals (this rank's exact share, for a reduce)."""
+        self._call(self._lib.lde_finalize_partials, dst_ptr)
+
     def export_window(self, dst_ptr: int) -> None:
         self._call(self._lib.lde_export_window, dst_ptr)
 

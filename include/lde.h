@@ -140,6 +140,15 @@ int lde_reset_cumulative(lde_handle *h);
  * counts (uint32 [S*T]) into a caller device buffer, and import merged
  * counts back (e.g. after an RCCL reduce over xGMI). */
 int lde_export_window(lde_handle *h, void *d_dst);
+/* Multi-GPU finalize without moving the histogram: cumulative += window,
+ * window cleared (as lde_finalize), and this rank's exact partial outputs
+ * written to caller device memory, uint64 [S] current image | [S] cumulative
+ * image | [4] totals (lde_outputs.totals order), asynchronously on the
+ * handle's stream.  Summed over ranks (RCCL reduce) they equal the outputs of
+ * one handle that binned every rank's events.  An empty window is allowed
+ * (zeros for the current outputs).  float64 views only (LDE_EINVAL for f32,
+ * whose per-push rounding is order dependent). */
+int lde_finalize_partials(lde_handle *h, void *d_out);
 int lde_import_window(lde_handle *h, const void *d_src);
 
 /* Wait for all work queued on the handle's stream. */

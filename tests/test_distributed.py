@@ -34,6 +34,25 @@ class _HostEngine:
     def import_window(self, ptr):
         ctypes.memmove(self.window.ctypes.data, ptr, self.window.nbytes)
 
+    # OutputReducer interface: u64 [S] current image | [S] cumulative | [4] totals
+    cum = None
+    lo, hi = 2, 7  # TOA bin range of the images
+
+    def finalize_partials(self, ptr):
+        if self.cum is None:
+            self.cum = np.zeros_like(self.window, dtype=np.int64)
+        w = self.window.astype(np.int64).reshape(self.n_screen, self.n_toa_bins)
+        self.cum += w.ravel()
+        c = self.cum.reshape(self.n_screen, self.n_toa_bins)
+        out = np.concatenate([w[:, self.lo:self.hi].sum(1), c[:, self.lo:self.hi].sum(1),
+                              [w.sum(), w[:, self.lo:self.hi].sum(), c.sum(),
+                               c[:, self.lo:self.hi].sum()]]).astype(np.int64)
+        ctypes.memmove(ptr, out.ctypes.data, out.nbytes)
+        self.window[:] = 0
+
+    def synchronize(self):
+        pass
+
 
 def _free_port():
     s = socket.socket()
@@ -68,6 +87,62 @@ def _worker(rank, world, port, q):
             q.put(bool(np.array_equal(eng.window, full.window)) and int(eng.window.sum()) > 0)
     finally:
         dist.destroy_process_group()
+
+
+def _worker_outputs(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from esslivedata_amd.distributed import OutputReducer, shard_bounds
+
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        edges = np.linspace(0, 100, 11)
+        eng = _HostEngine(64, edges)
+        full = _HostEngine(64, edges)
+        red = OutputReducer(eng, torch.device('cpu'))
+        ok = True
+        for batch in range(3):  # cumulative outputs across finalizes
+            rng = np.random.default_rng(10 + batch)
+            n = 50_001 + batch
+            pid = rng.integers(0, 70, n).astype(np.int32)
+            toa = rng.integers(-10, 110, n).astype(np.int32)
+            lo, hi = shard_bounds(n, rank, world)
+            if batch != 1 or rank == 0:  # batch 1: rank 1 gets no events at all
+                eng.bin(pid[lo:hi], toa[lo:hi])
+                if batch == 1:
+                    eng.bin(pid[hi:], toa[hi:])
+            res = red.finalize()
+            full.bin(pid, toa)
+            buf = np.zeros(2 * 64 + 4, dtype=np.int64)
+            full.finalize_partials(buf.ctypes.data)
+            if rank == 0:
+                cur, cum, tot = res
+                ok &= np.array_equal(cur, buf[:64].astype(np.float64))
+                ok &= np.array_equal(cum, buf[64:128].astype(np.float64))
+                ok &= tot == [int(x) for x in buf[128:]] and tot[0] > 0
+            else:
+                ok &= res is None
+        q.put(bool(ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_output_reducer_matches_single_process():
+    """Sharded binning + reduce of partial outputs == one process over all events."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_outputs, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(results)
 
 
 def test_shard_bounds_cover_all_events():

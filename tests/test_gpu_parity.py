@@ -337,3 +337,37 @@ def test_auto_picks_split_for_skewed_and_paged_for_uniform():
     eng.stage(pid, toa)
     eng.accumulate(0)
     assert eng.info()['last_strategy'] == 'paged'
+
+
+def test_finalize_partials_match_finalize():
+    """lde_finalize_partials (multi-GPU outputs) == lde_finalize, over batches,
+    including an empty window (a rank that received no events)."""
+    import torch
+
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.dream_mantle()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    a = _engine(view, edges)
+    b = _engine(view, edges)
+    S = view.n_screen
+    buf = torch.zeros(2 * S + 4, dtype=torch.int64, device='cuda')
+    for batch, n in enumerate([300_000, 0, 2_000_000]):
+        pid, toa = synthetic.dream_events(n, inst, seed=30 + batch)
+        if n:
+            a.stage(pid, toa)
+            a.accumulate(batch % view.n_replicas)
+            b.stage(pid, toa)
+            b.accumulate(batch % view.n_replicas)
+            ref = a.finalize(images=True)
+        b.finalize_partials(buf.data_ptr())
+        b.synchronize()  # b runs on its own stream
+        h = buf.cpu().numpy()
+        if n:
+            np.testing.assert_array_equal(h[:S].astype(np.float64), ref.current_image)
+            np.testing.assert_array_equal(h[S:2 * S].astype(np.float64), ref.cumulative_image)
+            assert [int(x) for x in h[2 * S:]] == [ref.current_total, ref.current_in_range,
+                                                   ref.cumulative_total, ref.cumulative_in_range]
+        else:
+            assert not h[:S].any() and int(h[2 * S]) == 0 and int(h[2 * S + 2]) > 0

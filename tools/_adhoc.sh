@@ -5,4 +5,3 @@ run() { tag=$1; shift; env "$@" timeout -k 10 120 python bench.py --steps 20 --w
 python3 -c "import json;D=json.load(open('gpurun_out/k_$tag.json'));d=D['roofline']['kernel_ms'];print('$tag', '%.4g'%D['value'], D['ms_per_step'], D['config']['strategy'], ' '.join('%s=%.4f'%(k,v) for k,v in d.items() if v))"; }
 BA=()
 run default LDE_X=0
-run default2 LDE_X=0
