@@ -63,6 +63,7 @@ EXPORTED_SYMBOLS = (
     'lde_import_window',
     'lde_synchronize',
     'lde_timing_enable',
+    'lde_timing_select',
     'lde_kernel_stats',
     'lde_info',
 )
@@ -122,6 +123,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_import_window': (ctypes.c_int, [H, P]),
         'lde_synchronize': (ctypes.c_int, [H]),
         'lde_timing_enable': (ctypes.c_int, [H, i32]),
+        'lde_timing_select': (ctypes.c_int, [H, ctypes.c_uint32]),
         'lde_kernel_stats': (
             ctypes.c_int,
             [H, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)],

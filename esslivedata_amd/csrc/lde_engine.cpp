@@ -168,6 +168,7 @@ struct lde_handle {
 
     // timing
     bool timing = false;
+    uint32_t timing_mask = 0xffffffffu;  // LDE_K_* ids recorded while timing
     std::vector<TimedLaunch> launches;
     std::vector<hipEvent_t> event_pool;
     double kms[LDE_K_COUNT] = {};
@@ -344,6 +345,15 @@ bool build_sieve_toa(const lde::ToaParams &tp, const std::vector<unsigned char> 
     return true;
 }
 
+// SIEVE cold keys are counted per tile for this many wave groups per block
+// (the sort then runs that many blocks per sieve block); <= 8 KB of LDS
+int sieve_groups(int n_tiles) {
+    const long long g = env_ll("LDE_SIEVE_GROUPS", 1);
+    for (int k : {4, 2})
+        if (g >= k && (long long)n_tiles * k * 4 <= 8192) return k;
+    return 1;
+}
+
 // ---- timing ----------------------------------------------------------------
 hipEvent_t pool_event(lde_handle *h) {
     if (!h->event_pool.empty()) {
@@ -361,13 +371,13 @@ struct Timed {
     int kid;
     hipEvent_t a = nullptr;
     Timed(lde_handle *h_, int kid_) : h(h_), kid(kid_) {
-        if (h->timing) {
+        if (h->timing && ((h->timing_mask >> kid) & 1u)) {
             a = pool_event(h);
             if (a) (void)hipEventRecord(a, h->stream);
         }
     }
     ~Timed() {
-        if (h->timing && a) {
+        if (a) {
             hipEvent_t b = pool_event(h);
             if (b) {
                 (void)hipEventRecord(b, h->stream);
@@ -669,8 +679,9 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     if (sieve) {
         if (int rc = grow(h, &h->d_chunk_tab, h->chunk_tab_cap, (size_t)chunks + 1)) return rc;
         const size_t nt = (size_t)h->n_tiles;
-        if (int rc = grow(h, &h->d_cold_tcnt, h->cold_tcnt_cap, (size_t)a.grid * nt)) return rc;
-        if (int rc = grow(h, &h->d_cold_boff, h->cold_boff_cap, (size_t)a.grid * nt)) return rc;
+        const int tg = sieve_groups(h->n_tiles);
+        if (int rc = grow(h, &h->d_cold_tcnt, h->cold_tcnt_cap, (size_t)a.grid * tg * nt)) return rc;
+        if (int rc = grow(h, &h->d_cold_boff, h->cold_boff_cap, (size_t)a.grid * tg * nt)) return rc;
         // tile-major u16 keys: at most every staged slot, + slack for pass B's 16-byte loads
         if (int rc = grow(h, &h->d_cold_keys, h->cold_keys_cap,
                           (size_t)a.grid * (size_t)a.cold_cap + 64))
@@ -704,6 +715,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         sa.cold_cnt = h->d_cold_cnt;
         sa.tile_bits = h->tile_bits;
         sa.n_tiles = h->n_tiles;
+        sa.tgroups = tg;
         sa.cold_tcnt = h->d_cold_tcnt;
         sa.ablate = (int)env_ll("LDE_SIEVE_ABLATE", 0);
         {
@@ -720,6 +732,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         c.tile_bits = h->tile_bits;
         c.n_tiles = h->n_tiles;
         c.rows = a.grid;
+        c.groups = tg;
         c.cold = h->d_cold;
         c.stride = a.cold_cap + lde::kSplitThreads / 64;
         c.cap = a.cold_cap;
@@ -1171,10 +1184,10 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                     (unsigned long long)h->S * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL &&
                     ((h->L - 1) >> cbits) < 255 && h->L < 0x3fffffffLL) {
                     int Hs = 0;
-                    const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size(), h->n_tiles);
+                    const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size(), h->n_tiles, sieve_groups(h->n_tiles));
                     if (fixed < budget)
                         Hs = (int)std::min<long long>(lde::kHotMaxRows, (long long)((budget - fixed) / (4 * (size_t)h->T)));
-                    while (Hs > 0 && lde::sieve_smem(lde::align4(Hs * h->T), cbits, (int)tt.size(), h->n_tiles) > budget) --Hs;
+                    while (Hs > 0 && lde::sieve_smem(lde::align4(Hs * h->T), cbits, (int)tt.size(), h->n_tiles, sieve_groups(h->n_tiles)) > budget) --Hs;
                     Hs = (int)std::min<long long>(Hs, h->S);
                     if (hmax > 0) Hs = (int)std::min<long long>(Hs, hmax);
                     if (Hs >= 8 && (unsigned long long)Hs * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL) {
@@ -1511,6 +1524,12 @@ int lde_synchronize(lde_handle *h) {
     if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
     DeviceGuard guard(h->device);
     HIPCALL(h, hipStreamSynchronize(h->stream));
+    return LDE_OK;
+}
+
+int lde_timing_select(lde_handle *h, uint32_t mask) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    h->timing_mask = mask;
     return LDE_OK;
 }
 

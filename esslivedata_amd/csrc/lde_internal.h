@@ -176,15 +176,17 @@ struct SieveArgs {
     long long cold_cap;  // keys per block region (region stride cold_cap + 16)
     uint32_t *cold_cnt;
     int tile_bits, n_tiles;  // cold keys are counted per tile of 2^tile_bits bins
-    uint32_t *cold_tcnt;     // [grid][n_tiles]
+    int tgroups;             // ... for each of tgroups groups of waves (1, 2, 4)
+    uint32_t *cold_tcnt;     // [grid][tgroups][n_tiles]
     int ablate;  // benchmark ablation variant (0 = the real pass)
 };
-size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);
+size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles, int tgroups);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a
 // tile-major u16 array, pass B
 struct ColdArgs {
     int tile_bits, n_tiles;
-    int rows;  // sieve blocks
+    int rows;    // sieve blocks
+    int groups;  // wave groups per sieve block (sort blocks per sieve block)
     const uint32_t *cold;
     long long stride, cap;  // region stride and capacity (keys)
     const uint32_t *cold_cnt, *tcnt;

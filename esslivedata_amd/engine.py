@@ -211,6 +211,11 @@ class BinningEngine:
     def synchronize(self) -> None:
         self._call(self._lib.lde_synchronize)
 
+    def timing_select(self, kernels=None) -> None:
+        """Record only these kernel ids (names of _native.KERNELS); None = all."""
+        mask = 0xFFFFFFFF if kernels is None else sum(1 << _native.KERNELS[k] for k in kernels)
+        self._call(self._lib.lde_timing_select, mask)
+
     def timing_enable(self, enable: bool = True) -> None:
         self._call(self._lib.lde_timing_enable, 1 if enable else 0)
 

@@ -173,6 +173,9 @@ int lde_synchronize(lde_handle *h);
 #define LDE_K_SPLIT_AUX 11 /* hot-set selection, hot-row reduce, cold segment table */
 #define LDE_K_COUNT 12
 int lde_timing_enable(lde_handle *h, int32_t enable);
+/* Record only the kernels whose bit (1 << LDE_K_*) is set in mask (default:
+ * all).  Fewer recorded events = less host work per batch. */
+int lde_timing_select(lde_handle *h, uint32_t mask);
 int lde_kernel_stats(lde_handle *h, int32_t kernel_id, double *ms, int64_t *launches);
 
 /* Introspection for tests and reports. */

@@ -15,14 +15,16 @@ eng = BinningEngine(toa_edges_ns=inst.edges.edges_ns(), out_lut=view.lut, pid_of
                     stream=torch.cuda.current_stream(dev).cuda_stream)
 n_pulse, pulses = 10_000_000, 14
 pid, toa = synthetic.torch_dream_events(n_pulse * pulses, inst, 7, dev)
+msgs = [(pid[p * n_pulse:(p + 1) * n_pulse], toa[p * n_pulse:(p + 1) * n_pulse]) for p in range(pulses)]
 torch.cuda.synchronize()
+import os
 for timing in (False, True):
     eng.timing_enable(timing)
     acc = {'stage': 0.0, 'accumulate': 0.0, 'finalize': 0.0}
     for i in range(25):
         t0 = time.perf_counter()
-        for p in range(pulses):
-            eng.stage_tensors(pid[p * n_pulse:(p + 1) * n_pulse], toa[p * n_pulse:(p + 1) * n_pulse])
+        for mp, mt in msgs:
+            eng.stage_tensors(mp, mt)
         t1 = time.perf_counter()
         eng.accumulate(i % view.n_replicas)
         t2 = time.perf_counter()
@@ -34,3 +36,18 @@ for timing in (False, True):
             acc['finalize'] += t3 - t2
     print('timing' if timing else 'no timing', {k: round(v / 20 * 1e3, 4) for k, v in acc.items()},
           'ms/step total', round(sum(acc.values()) / 20 * 1e3, 4), flush=True)
+
+# GPU-side span of one step (events around the whole step on the engine stream)
+eng.timing_enable(False)
+s0 = torch.cuda.Event(enable_timing=True); s1 = torch.cuda.Event(enable_timing=True)
+tot = 0.0
+for i in range(20):
+    s0.record()
+    for mp, mt in msgs:
+        eng.stage_tensors(mp, mt)
+    eng.accumulate(i % view.n_replicas)
+    eng.finalize(images=True)
+    s1.record()
+    s1.synchronize()
+    tot += s0.elapsed_time(s1)
+print('gpu span per step (ms)', round(tot / 20, 4))
