@@ -75,7 +75,8 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         for f in futs:
             f.result()
     tmp = LIB.with_suffix('.so.tmp')
-    _run([_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', *[str(o) for o in objs], '-o',
+    _run([_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-Wl,--no-undefined',
+          *[str(o) for o in objs], '-o',
           str(tmp)], verbose)
     os.replace(tmp, LIB)
     return LIB

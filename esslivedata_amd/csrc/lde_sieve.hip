@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     if (tid == 0) sm[o_cur] = 0;
     for (uint32_t i = (uint32_t)tid; i < kSieveStage * (kSplitThreads / 64); i += kSplitThreads)
         sm[o_stg + i] = 0xFFFFFFFFu;
-    for (int i = tid; i < a.n_tiles; i += kSplitThreads) sm[o_tcnt + i] = 0;
+    for (int i = tid; i < a.n_tiles * a.tgroups; i += kSplitThreads) sm[o_tcnt + i] = 0;
     __syncthreads();
 
     const __amdgpu_buffer_rsrc_t glut = make_rsrc(a.glut, (a.L + 1u) * 4u);
@@ -187,7 +187,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t dum_idx = o_dum + (uint32_t)lane;
     const uint32_t dum4 = dum_idx * 4u;
     const uint32_t o_stg_w = o_stg + kSieveStage * (uint32_t)(tid >> 6);
-    const uint32_t o_pc4 = o_pc * 4u, o_tt4 = o_tt * 4u, o_tcnt4 = o_tcnt * 4u;
+    // cold keys are counted per tile for each group of 16 / tgroups waves
+    const uint32_t grp = (uint32_t)(tid >> 6) / (uint32_t)((kSplitThreads / 64) / a.tgroups);
+    const uint32_t o_pc4 = o_pc * 4u, o_tt4 = o_tt * 4u;
+    const uint32_t o_tcnt4 = (o_tcnt + grp * (uint32_t)a.n_tiles) * 4u;
     const int tsh = a.tile_bits + 2;
     // this wave's sub-region of the block's cold region (keys), 16-B aligned
     const uint32_t capw = (uint32_t)(a.cold_cap / (kSplitThreads / 64));
@@ -393,8 +396,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     uint32_t *dst = a.hot_part + (size_t)blockIdx.x * a.hot_words;
     for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4)
         *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(sm + i);
-    for (int i = tid; i < a.n_tiles; i += kSplitThreads)
-        a.cold_tcnt[(size_t)blockIdx.x * a.n_tiles + i] = sm[o_tcnt + i];
+    for (int i = tid; i < a.n_tiles * a.tgroups; i += kSplitThreads)
+        a.cold_tcnt[(size_t)blockIdx.x * a.tgroups * a.n_tiles + i] = sm[o_tcnt + i];
 }
 
 // ---------------------------------------------------------------------------
@@ -492,7 +495,8 @@ template <int TB>
 __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
     const uint32_t *__restrict__ cold, long long stride, long long cap,
     const uint32_t *__restrict__ cold_cnt, const uint32_t *__restrict__ boff,
-    const uint32_t *__restrict__ tile_base, int n_tiles, uint16_t *__restrict__ out) {
+    const uint32_t *__restrict__ tile_base, int n_tiles, int groups,
+    uint16_t *__restrict__ out) {
     constexpr int KPT = kSortPiece / kSortThreads;  // 16 keys per thread
     constexpr uint32_t MASK = (1u << TB) - 1u;
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
@@ -503,16 +507,18 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
     uint32_t *s_cur = s_start + nt4;
     uint32_t *s_w = s_cur + nt4;
     const int tid = threadIdx.x;
-    const int b = blockIdx.x;
-    // the sieve block's cold region = 16 wave sub-regions of cap / 16 keys,
-    // each filled to a multiple of 4; logical key i lives in the sub-region
-    // of the last wave whose prefix is <= i
+    // block = (sieve block b, wave group g): waves [g * WPG, (g + 1) * WPG) of
+    // the sieve block's cold region, which is 16 wave sub-regions of cap / 16
+    // keys, each filled to a multiple of 4; logical key i lives in the
+    // sub-region of the last wave whose prefix is <= i
     constexpr int NW = kSplitThreads / 64;
+    const int b = blockIdx.x / groups, g = blockIdx.x % groups;
+    const int WPG = NW / groups;
     if (tid == 0) {
         uint32_t acc = 0;
         for (int w = 0; w < NW; ++w) {
             s_w[w] = acc;
-            acc += cold_cnt[(size_t)b * NW + w];
+            if (w >= g * WPG && w < (g + 1) * WPG) acc += cold_cnt[(size_t)b * NW + w];
         }
         s_w[NW] = acc;
     }
@@ -532,7 +538,7 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
     const uint32_t *src = cold + (size_t)b * (size_t)stride;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, (uint32_t)(cap * 4));
     for (int t = tid; t < n_tiles; t += kSortThreads)
-        s_cur[t] = tile_base[t] + boff[(size_t)b * n_tiles + t];
+        s_cur[t] = tile_base[t] + boff[(size_t)blockIdx.x * n_tiles + t];
     constexpr int TPT = kMaxTiles / kSortThreads;
     // the next piece's keys are requested before the current piece is sorted
     v4u nk[KPT / 4];
@@ -638,9 +644,9 @@ __global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
-size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles) {
+size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles, int tgroups) {
     return 4 * ((size_t)hot_words + ((size_t)1 << cbits) + (size_t)toa_words4 + 64 + 4 +
-                (size_t)kSieveStage * (kSplitThreads / 64) + (size_t)align4(n_tiles));
+                (size_t)kSieveStage * (kSplitThreads / 64) + (size_t)align4(n_tiles * tgroups));
 }
 
 hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
@@ -666,8 +672,8 @@ hipError_t launch_chunk_tab(const SegDesc *segs, int n_segs, long long n_chunks,
 }
 
 hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st) {
-    hipLaunchKernelGGL(k_cold_scan, dim3(c.n_tiles), dim3(256), 0, st, c.tcnt, c.rows, c.n_tiles,
-                       c.boff, c.tile_total);
+    hipLaunchKernelGGL(k_cold_scan, dim3(c.n_tiles), dim3(256), 0, st, c.tcnt, c.rows * c.groups,
+                       c.n_tiles, c.boff, c.tile_total);
     hipLaunchKernelGGL(k_cold_plan, dim3(1), dim3(1024), 0, st, c.tile_total, c.n_tiles, c.item_keys,
                        c.tile_base, c.items, c.item_count, c.max_items);
     const size_t sm = cold_sort_smem(c.n_tiles);
@@ -677,8 +683,9 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st) {
     case TB:                                                                                      \
         (void)hipFuncSetAttribute((const void *)k_cold_sort<TB>,                                  \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);           \
-        hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows), dim3(kSortThreads), sm, st, c.cold,     \
-                           c.stride, c.cap, c.cold_cnt, c.boff, c.tile_base, c.n_tiles, c.keys);  \
+        hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * c.groups), dim3(kSortThreads), sm, st,  \
+                           c.cold, c.stride, c.cap, c.cold_cnt, c.boff, c.tile_base, c.n_tiles,  \
+                           c.groups, c.keys);                                                     \
         hipLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, st,   \
                            c.keys, c.items, c.item_count, c.hist, c.n_bins);                      \
         break;
@@ -695,7 +702,7 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st) {
 
 template <int ABL>
 static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st) {
-    if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles) > kSplitSmemMax)
+    if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles, a.tgroups) > kSplitSmemMax)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_sieve<ABL>, dim3(grid), dim3(kSplitThreads), 0, st, a);  // static LDS
     return hipGetLastError();
