@@ -191,20 +191,22 @@ __global__ __launch_bounds__(256) void k_finalize_v4(uint32_t *__restrict__ win3
     }
 }
 
-// totals[q] = sum over blocks of the partials at totals[4 + 4 * block + q]
-__global__ __launch_bounds__(256) void k_sum_totals(unsigned long long *__restrict__ totals,
-                                                    int blocks) {
-    __shared__ unsigned long long s[4][64];
-    const int q = threadIdx.x & 3, r = threadIdx.x >> 2;
+// totals[q] = sum over blocks of the partials at totals[4 + 4 * block + q].
+// Thread i sums the partials i, i + 1024, ... (all of quantity i & 3) with
+// independent loads, then the 256 threads of each quantity reduce in LDS.
+__global__ __launch_bounds__(1024) void k_sum_totals(unsigned long long *__restrict__ totals,
+                                                     int blocks) {
+    __shared__ unsigned long long s[1024];
+    const int n = 4 * blocks;
     unsigned long long v = 0;
-    for (int b = r; b < blocks; b += 64) v += totals[4 + (size_t)b * 4 + q];
-    s[q][r] = v;
+    for (int j = threadIdx.x; j < n; j += 1024) v += totals[4 + j];
+    s[threadIdx.x] = v;
     __syncthreads();
-    if (threadIdx.x < 4) {
-        unsigned long long t = 0;
-        for (int i = 0; i < 64; ++i) t += s[threadIdx.x][i];
-        totals[threadIdx.x] = t;
+    for (int d = 512; d >= 4; d >>= 1) {
+        if ((int)threadIdx.x < d) s[threadIdx.x] += s[threadIdx.x + d];
+        __syncthreads();
     }
+    if (threadIdx.x < 4) totals[threadIdx.x] = s[threadIdx.x];
 }
 
 // f32-mode image rows: sum of f32 values over the TOA range in f64, rounded once
@@ -253,7 +255,7 @@ static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsign
         if (b8 < 1) b8 = 1;
         hipLaunchKernelGGL(k_finalize_v4<OUT>, dim3((unsigned)b8), dim3(256), 0, st, win32, win64,
                            cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, totals);
-        hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(256), 0, st, totals, (int)b8);
+        hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(1024), 0, st, totals, (int)b8);
         return;
     }
     long long blocks = (S + 3) / 4;
@@ -261,7 +263,7 @@ static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsign
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_finalize<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
                        cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, totals);
-    hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(256), 0, st, totals, (int)blocks);
+    hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(1024), 0, st, totals, (int)blocks);
 }
 
 // image element type: 0 f64, 1 f32, 2 u64 (exact partial sums for multi-GPU)
