@@ -155,7 +155,11 @@ struct lde_handle {
 
     // finalize scratch
     unsigned long long *d_tot4 = nullptr;
-    void *d_img_cur = nullptr, *d_img_cum = nullptr;
+    void *d_img_cur = nullptr, *d_img_cum = nullptr;  // inside d_pack
+    // finalize outputs leave in one D2H copy: [current image S x 8 B]
+    // [cumulative image S x 8 B][totals 32 B][overflow flag 16 B]
+    unsigned char *d_pack = nullptr, *h_pack = nullptr;  // h_pack pinned
+    size_t pack_bytes = 0;
     unsigned long long *d_snap = nullptr;
 
     // state
@@ -976,8 +980,9 @@ void release(lde_handle *h) {
     dev_free(h->d_cold_chunks);
     dev_free(h->d_dummy);
     dev_free(h->d_tot4);
-    dev_free(h->d_img_cur);
-    dev_free(h->d_img_cum);
+    dev_free(h->d_pack);
+    if (h->h_pack) (void)hipHostFree(h->h_pack);
+    h->h_pack = nullptr;
     dev_free(h->d_snap);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -1115,8 +1120,11 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         CREATE_CHECK(ensure_win64(h));
     }
     CREATE_CHECK(dev_alloc(h, &h->d_tot4, 4 + 4 * 8192));  // totals + per-block partials
-    CREATE_CHECK(dev_alloc(h, (double **)&h->d_img_cur, (size_t)h->S));
-    CREATE_CHECK(dev_alloc(h, (double **)&h->d_img_cum, (size_t)h->S));
+    h->pack_bytes = (size_t)h->S * 16 + 48;
+    CREATE_CHECK(dev_alloc(h, &h->d_pack, h->pack_bytes));
+    CREATE_HIP(hipHostMalloc((void **)&h->h_pack, h->pack_bytes, hipHostMallocDefault));
+    h->d_img_cur = h->d_pack;
+    h->d_img_cum = h->d_pack + (size_t)h->S * 8;
     CREATE_CHECK(zero_state(h));
 
     // partition workspace: choose the smallest tile that keeps <= kMaxTiles tiles
@@ -1398,14 +1406,15 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
                        h->stream));
     }
     const size_t isz = f32 ? 4 : 8;
-    if (out->current_image)
-        HIPCALL(h, hipMemcpyAsync(out->current_image, h->d_img_cur, (size_t)h->S * isz,
-                                  hipMemcpyDeviceToHost, h->stream));
-    if (out->cumulative_image)
-        HIPCALL(h, hipMemcpyAsync(out->cumulative_image, h->d_img_cum, (size_t)h->S * isz,
-                                  hipMemcpyDeviceToHost, h->stream));
-    unsigned long long tot[4] = {0, 0, 0, 0};
-    HIPCALL(h, hipMemcpyAsync(tot, h->d_tot4, 32, hipMemcpyDeviceToHost, h->stream));
+    // images, totals and the overflow flag leave in one pinned D2H copy
+    // (separate copies into pageable memory cost ~25 us each)
+    unsigned char *d_tail = h->d_pack + (size_t)h->S * 16;
+    HIPCALL(h, hipMemcpyAsync(d_tail, h->d_tot4, 32, hipMemcpyDeviceToDevice, h->stream));
+    if (h->d_overflow)
+        HIPCALL(h, hipMemcpyAsync(d_tail + 32, h->d_overflow, 4, hipMemcpyDeviceToDevice, h->stream));
+    else
+        HIPCALL(h, hipMemsetAsync(d_tail + 32, 0, 4, h->stream));
+    HIPCALL(h, hipMemcpyAsync(h->h_pack, h->d_pack, h->pack_bytes, hipMemcpyDeviceToHost, h->stream));
     std::vector<unsigned long long> tmp;
     if (!f32 && (want_cur_hist || want_cum_hist)) tmp.resize(nb);
     if (!f32 && want_cur_hist) {
@@ -1419,11 +1428,16 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
         convert_u64(tmp.data(), out->cumulative_hist, (long long)nb, LDE_F64);
     }
     if (f32) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
-    uint32_t ovf = 0;
-    if (h->d_overflow)
-        HIPCALL(h, hipMemcpyAsync(&ovf, h->d_overflow, 4, hipMemcpyDeviceToHost, h->stream));
     HIPCALL(h, hipStreamSynchronize(h->stream));
+    const unsigned char *h_tail = h->h_pack + (size_t)h->S * 16;
+    uint32_t ovf = 0;
+    std::memcpy(&ovf, h_tail + 32, 4);
     if (ovf) return fail(h, LDE_ESTATE, "page pool overflow (internal error)");
+    if (out->current_image) std::memcpy(out->current_image, h->h_pack, (size_t)h->S * isz);
+    if (out->cumulative_image)
+        std::memcpy(out->cumulative_image, h->h_pack + (size_t)h->S * 8, (size_t)h->S * isz);
+    unsigned long long tot[4];
+    std::memcpy(tot, h_tail, 32);
     for (int q = 0; q < 4; ++q) out->totals[q] = tot[q];
     h->window_has_data = false;
     h->win64_dirty = false;
