@@ -66,7 +66,11 @@ EXPORTED_SYMBOLS = (
     'lde_timing_select',
     'lde_kernel_stats',
     'lde_info',
+    'lde_set_groups',
+    'lde_group_spectra',
 )
+
+MAX_GROUP_SETS = 4
 
 
 class LdeConfig(ctypes.Structure):
@@ -122,6 +126,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_finalize_partials': (ctypes.c_int, [H, P]),
         'lde_import_window': (ctypes.c_int, [H, P]),
         'lde_synchronize': (ctypes.c_int, [H]),
+        'lde_set_groups': (ctypes.c_int, [H, i32, i64, P, P]),
+        'lde_group_spectra': (ctypes.c_int, [H, i32, i32, P]),
         'lde_timing_enable': (ctypes.c_int, [H, i32]),
         'lde_timing_select': (ctypes.c_int, [H, ctypes.c_uint32]),
         'lde_kernel_stats': (

@@ -162,6 +162,16 @@ struct lde_handle {
     size_t pack_bytes = 0;
     unsigned long long *d_snap = nullptr;
 
+    // screen groupings (ROI spectra, spectrum views), lde_set_groups
+    struct GroupSet {
+        long long n_groups = 0;
+        int n_items = 0;
+        bool all_single = true;
+        int4 *d_items = nullptr;
+        int *d_screens = nullptr;
+        unsigned long long *d_out = nullptr;  // [n_groups * T]
+    } groups[LDE_MAX_GROUP_SETS];
+
     // state
     bool window_has_data = false;
     bool cum_has_data = false;
@@ -984,6 +994,11 @@ void release(lde_handle *h) {
     if (h->h_pack) (void)hipHostFree(h->h_pack);
     h->h_pack = nullptr;
     dev_free(h->d_snap);
+    for (auto &g : h->groups) {
+        dev_free(g.d_items);
+        dev_free(g.d_screens);
+        dev_free(g.d_out);
+    }
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1493,6 +1508,93 @@ int lde_read_histogram(lde_handle *h, int32_t which, void *host_out) {
     HIPCALL(h, hipMemcpyAsync(tmp.data(), h->d_snap, nb * 8, hipMemcpyDeviceToHost, h->stream));
     HIPCALL(h, hipStreamSynchronize(h->stream));
     convert_u64(tmp.data(), host_out, (long long)nb, LDE_F64);
+    return LDE_OK;
+}
+
+int lde_set_groups(lde_handle *h, int32_t slot, int64_t n_groups, const int64_t *offsets,
+                   const int32_t *screens) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (slot < 0 || slot >= LDE_MAX_GROUP_SETS)
+        return fail(h, LDE_EINVAL, "group slot %d out of range [0, %d)", slot, LDE_MAX_GROUP_SETS);
+    if (n_groups < 0 || n_groups > (1LL << 24))
+        return fail(h, LDE_EINVAL, "n_groups %lld out of range", (long long)n_groups);
+    if (n_groups > 0 && !offsets) return fail(h, LDE_EINVAL, "offsets is NULL");
+    const long long n_ref = n_groups > 0 ? (long long)offsets[n_groups] : 0;
+    if (n_ref > 0 && !screens) return fail(h, LDE_EINVAL, "screens is NULL");
+    if (n_groups > 0 && offsets[0] != 0) return fail(h, LDE_EINVAL, "offsets[0] must be 0");
+    if (n_ref > (1LL << 30)) return fail(h, LDE_EINVAL, "too many group members");
+    for (long long g = 0; g < n_groups; ++g)
+        if (offsets[g + 1] < offsets[g]) return fail(h, LDE_EINVAL, "offsets must be non-decreasing");
+    for (long long k = 0; k < n_ref; ++k)
+        if (screens[k] < 0 || screens[k] >= h->S)
+            return fail(h, LDE_EINVAL, "screen index %d out of range [0, %lld)", screens[k],
+                        (long long)h->S);
+    // work items of at most GROUP_ITEM screens; empty groups get no item (zeros)
+    std::vector<int4> items;
+    bool all_single = true;
+    for (long long g = 0; g < n_groups; ++g) {
+        const long long b = offsets[g], e = offsets[g + 1];
+        if (e == b) {
+            all_single = false;
+            continue;
+        }
+        const bool single = e - b <= lde::GROUP_ITEM;
+        if (!single) all_single = false;
+        for (long long k = b; k < e; k += lde::GROUP_ITEM)
+            items.push_back(make_int4((int)g, (int)k, (int)std::min(e, k + lde::GROUP_ITEM), single ? 1 : 0));
+    }
+    if (items.size() > 0x7fffffffULL) return fail(h, LDE_EINVAL, "too many group items");
+    DeviceGuard guard(h->device);
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    auto &gs = h->groups[slot];
+    dev_free(gs.d_items);
+    dev_free(gs.d_screens);
+    dev_free(gs.d_out);
+    gs = lde_handle::GroupSet{};
+    if (n_groups == 0) return LDE_OK;
+    if (int rc = dev_alloc(h, &gs.d_items, items.size())) return rc;
+    if (int rc = dev_alloc(h, &gs.d_screens, (size_t)n_ref)) return rc;
+    if (int rc = dev_alloc(h, &gs.d_out, (size_t)n_groups * h->T)) return rc;
+    if (!items.empty())
+        HIPCALL(h, hipMemcpy(gs.d_items, items.data(), items.size() * sizeof(int4),
+                             hipMemcpyHostToDevice));
+    if (n_ref > 0)
+        HIPCALL(h, hipMemcpy(gs.d_screens, screens, (size_t)n_ref * 4, hipMemcpyHostToDevice));
+    gs.n_groups = n_groups;
+    gs.n_items = (int)items.size();
+    gs.all_single = all_single;
+    return LDE_OK;
+}
+
+int lde_group_spectra(lde_handle *h, int32_t slot, int32_t which, void *host_out) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (slot < 0 || slot >= LDE_MAX_GROUP_SETS)
+        return fail(h, LDE_EINVAL, "group slot %d out of range [0, %d)", slot, LDE_MAX_GROUP_SETS);
+    if (which != LDE_CURRENT && which != LDE_CUMULATIVE)
+        return fail(h, LDE_EINVAL, "which must be LDE_CURRENT or LDE_CUMULATIVE");
+    if (which == LDE_CURRENT && !h->window_has_data)
+        return fail(h, LDE_ENODATA, "No data has been added");
+    if (which == LDE_CUMULATIVE && !h->cum_has_data)
+        return fail(h, LDE_ENODATA, "No data has been added");
+    auto &gs = h->groups[slot];
+    if (gs.n_groups == 0) return LDE_OK;
+    if (!host_out) return fail(h, LDE_EINVAL, "host_out is NULL");
+    DeviceGuard guard(h->device);
+    const size_t n = (size_t)gs.n_groups * h->T;
+    const bool f32 = h->out_dtype == LDE_F32;
+    if (!gs.all_single) HIPCALL(h, hipMemsetAsync(gs.d_out, 0, n * 8, h->stream));
+    {
+        Timed tm(h, LDE_K_FINALIZE);
+        HIPCALL(h, lde::launch_group_spectra(
+                       f32 ? 2 : (which == LDE_CUMULATIVE ? 1 : 0), gs.d_items, gs.n_items,
+                       gs.d_screens, h->T, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr,
+                       h->d_cum, f32 ? (which == LDE_CUMULATIVE ? h->d_cumf : h->d_winf) : nullptr,
+                       gs.d_out, h->stream));
+    }
+    std::vector<unsigned long long> tmp(n);
+    HIPCALL(h, hipMemcpyAsync(tmp.data(), gs.d_out, n * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    convert_u64(tmp.data(), host_out, (long long)n, h->out_dtype);
     return LDE_OK;
 }
 

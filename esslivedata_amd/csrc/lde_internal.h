@@ -241,5 +241,12 @@ hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *wi
                            unsigned long long *totals, hipStream_t st);
 hipError_t launch_rows_f32(const float *h, long long S, int T, int lo, int hi, float *img,
                            hipStream_t st);
+// items: {group, begin, end, group has a single item}; out zeroed unless every
+// group is a single item
+constexpr int GROUP_ITEM = 64;  // screens per work item of k_group_spectra
+hipError_t launch_group_spectra(int mode, const int4 *items, int n_items, const int *screens,
+                                int T, const uint32_t *win32, const unsigned long long *win64,
+                                const unsigned long long *cum, const float *fsrc,
+                                unsigned long long *out, hipStream_t st);
 
 }  // namespace lde

@@ -222,6 +222,57 @@ __global__ __launch_bounds__(256) void k_rows_f32(const float *__restrict__ h, l
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Screen-group spectra: ROI spectra (SRC/workflows/detector_view/roi.py:188-266)
+// and spectrum views (SRC/workflows/detector_view/providers.py:300-325).
+// out[g][t] = sum over the screens s of group g of H[s][t], H = the window
+// (mode 0: win32 + win64), the cumulative as finalize would publish it
+// (mode 1: cum + win32 + win64) or an integer-valued f32 accumulator (mode 2).
+// One block per work item (<= GROUP_ITEM screens of one group); a thread owns
+// TOA bins t, t + blockDim, ... and reads the item's rows coalesced along t.
+// Groups may overlap (ROIs do), so items of one group add with u64 atomics into
+// the zeroed output; integer sums make the result order independent.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void k_group_spectra(
+    int mode, const int4 *__restrict__ items, const int *__restrict__ screens, int T,
+    const uint32_t *__restrict__ win32, const unsigned long long *__restrict__ win64,
+    const unsigned long long *__restrict__ cum, const float *__restrict__ fsrc,
+    unsigned long long *__restrict__ out) {
+    const int4 it = items[blockIdx.x];  // {group, begin, end, single}
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        unsigned long long acc = 0;
+        int k = it.y;
+        for (; k + 4 <= it.z; k += 4) {
+            size_t i0 = (size_t)screens[k] * T + t, i1 = (size_t)screens[k + 1] * T + t;
+            size_t i2 = (size_t)screens[k + 2] * T + t, i3 = (size_t)screens[k + 3] * T + t;
+            if (mode == 2) {
+                acc += (unsigned long long)fsrc[i0] + (unsigned long long)fsrc[i1] +
+                       (unsigned long long)fsrc[i2] + (unsigned long long)fsrc[i3];
+            } else {
+                acc += (unsigned long long)win32[i0] + win32[i1] + win32[i2] + win32[i3];
+                if (win64) acc += win64[i0] + win64[i1] + win64[i2] + win64[i3];
+                if (mode == 1) acc += cum[i0] + cum[i1] + cum[i2] + cum[i3];
+            }
+        }
+        for (; k < it.z; ++k) {
+            const size_t i = (size_t)screens[k] * T + t;
+            if (mode == 2) {
+                acc += (unsigned long long)fsrc[i];
+            } else {
+                acc += win32[i];
+                if (win64) acc += win64[i];
+                if (mode == 1) acc += cum[i];
+            }
+        }
+        unsigned long long *o = out + (size_t)it.x * T + t;
+        if (it.w)
+            *o = acc;  // the group's only item: plain store
+        else
+            atomicAdd(o, acc);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
@@ -287,6 +338,16 @@ hipError_t launch_rows_f32(const float *h, long long S, int T, int lo, int hi, f
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_rows_f32, dim3((unsigned)blocks), dim3(256), 0, st, h, S, T, lo, hi, img);
+    return hipGetLastError();
+}
+
+hipError_t launch_group_spectra(int mode, const int4 *items, int n_items, const int *screens,
+                                int T, const uint32_t *win32, const unsigned long long *win64,
+                                const unsigned long long *cum, const float *fsrc,
+                                unsigned long long *out, hipStream_t st) {
+    if (n_items <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_group_spectra, dim3((unsigned)n_items), dim3(128), 0, st, mode, items,
+                       screens, T, win32, win64, cum, fsrc, out);
     return hipGetLastError();
 }
 

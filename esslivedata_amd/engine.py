@@ -98,6 +98,7 @@ class BinningEngine:
         self._h = h
         self._lib = lib
         self._keepalive: list = []
+        self._n_groups: dict[int, int] = {}
 
     # ------------------------------------------------------------------
     @classmethod
@@ -210,6 +211,29 @@ class BinningEngine:
 
     def synchronize(self) -> None:
         self._call(self._lib.lde_synchronize)
+
+    def set_groups(self, slot: int, groups) -> None:
+        """Register screen groups (ROIs, spectrum-view output pixels) in ``slot``:
+        ``groups`` is a sequence of flat screen-index arrays (may overlap)."""
+        groups = [np.asarray(g, dtype=np.int32).ravel() for g in groups]
+        offsets = np.zeros(len(groups) + 1, dtype=np.int64)
+        if groups:
+            offsets[1:] = np.cumsum([g.size for g in groups])
+        screens = (np.concatenate(groups) if groups else np.zeros(0, np.int32)).astype(np.int32)
+        screens = np.ascontiguousarray(screens)
+        self._call(self._lib.lde_set_groups, int(slot), len(groups),
+                   offsets.ctypes.data if groups else None,
+                   screens.ctypes.data if screens.size else None)
+        self._n_groups[int(slot)] = len(groups)
+
+    def group_spectra(self, slot: int, which: str = 'current') -> np.ndarray:
+        """``(n_groups, T)`` spectra of the groups in ``slot`` from the window
+        (``'current'``) or the cumulative including the window."""
+        w = {'current': _native.LDE_CURRENT, 'cumulative': _native.LDE_CUMULATIVE}[which]
+        n = self._n_groups.get(int(slot), 0)
+        out = np.zeros((n, self._T), dtype=self._dtype)
+        self._call(self._lib.lde_group_spectra, int(slot), w, out.ctypes.data if n else None)
+        return out
 
     def timing_select(self, kernels=None) -> None:
         """Record only these kernel ids (names of _native.KERNELS); None = all."""

@@ -39,6 +39,7 @@ class ViewLUT:
     screen_coords: dict[str, np.ndarray] = field(default_factory=dict)
     screen_edges: dict[str, np.ndarray] = field(default_factory=dict)
     pixel_weights: np.ndarray | None = None
+    screen_units: dict[str, str | None] = field(default_factory=dict)
 
     @property
     def n_screen(self) -> int:
@@ -98,6 +99,7 @@ def geometric_lut(
     resolution: dict[str, int],
     *,
     flip_x: bool = False,
+    unit: str = 'm',
 ) -> ViewLUT:
     """LUT for a geometric view from per-replica projected coordinates.
 
@@ -146,6 +148,7 @@ def geometric_lut(
         screen_coords={d: 0.5 * (edges[d][1:] + edges[d][:-1]) for d in dims},
         screen_edges=edges,
         pixel_weights=weights,
+        screen_units={d: unit for d in dims},
     )
 
 
@@ -190,3 +193,27 @@ def logical_lut(
         screen_dims=tuple(output_dims),
         pixel_weights=weights.reshape(out_shape),
     )
+
+
+def index_groups(
+    shape: Sequence[int],
+    transform: Callable[[np.ndarray], np.ndarray] | None = None,
+    reduction_axes: Sequence[int] = (),
+) -> tuple[tuple[int, ...], list[np.ndarray]]:
+    """Output groups of a sum-preserving regrouping of a ``shape`` grid.
+
+    ``transform`` gets the flat-index array of shape ``shape`` and returns it
+    folded / transposed / sliced; ``reduction_axes`` of the result are summed.
+    Returns the output shape and, per output element (row-major), the flat
+    input indices it sums.  Used for spectrum views, whose transforms
+    fold + sum + flatten the screen dims (SRC/workflows/detector_view/
+    providers.py:300-325, bifrost/specs.py:311-329).
+    """
+    idx = np.arange(int(np.prod(shape)), dtype=np.int64).reshape(tuple(shape))
+    t = np.asarray(idx if transform is None else transform(idx))
+    red = set(int(a) % t.ndim for a in reduction_axes) if t.ndim else set()
+    kept = [a for a in range(t.ndim) if a not in red]
+    out_shape = tuple(t.shape[a] for a in kept)
+    n_out = int(np.prod(out_shape)) if out_shape else 1
+    moved = np.moveaxis(t, kept, list(range(len(kept)))).reshape(n_out, -1)
+    return out_shape, [row.astype(np.int32) for row in moved]

@@ -200,3 +200,20 @@ def torch_uniform_events(n: int, first: int, last: int, seed: int, device, toa_m
         torch.int32
     )
     return pid.contiguous(), toa.contiguous()
+
+
+def bifrost_spectrum_config(pixels_per_tube: int = 10):
+    """BIFROST ``spectrum_view`` (bifrost/specs.py:311-349) in index form: the
+    (15, 900) screen folded to (arc 5, tube 3, channel 9, pixel, subpixel),
+    subpixel summed, (tube, channel, pixel) flattened -> (arc, detector_number)."""
+    from .workflows import SpectrumViewConfig
+
+    if 100 % pixels_per_tube:
+        raise ValueError('pixels_per_tube must divide 100')
+    sub = 100 // pixels_per_tube
+
+    def transform(idx: np.ndarray) -> np.ndarray:
+        return idx.reshape(5, 3, 9, pixels_per_tube, sub).reshape(5, 3 * 9 * pixels_per_tube, sub)
+
+    return SpectrumViewConfig(transform=transform, output_dims=('arc', 'detector_number'),
+                              reduction_axes=(2,))

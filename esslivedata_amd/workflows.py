@@ -31,12 +31,19 @@ from .dataarray import DataArray, Variable
 from .edges import TOAEdges, convert_time, label_slice
 from .engine import BinningEngine
 from .preprocessors import DetectorEvents, MonitorEvents, StagedEvents, Timestamp
-from .projection import ViewLUT, geometric_lut, logical_lut
+from .projection import ViewLUT, geometric_lut, index_groups, logical_lut
+from . import roi as _roi
 
 DETECTOR_TRANSFORM = 'detector_transform'
 MONITOR_TRANSFORM = 'monitor_transform'
 
 DETECTOR_WINDOW_OUTPUTS = ('current', 'counts_total', 'counts_in_toa_range')
+# with ROI support the current ROI spectra are window outputs too
+# (DetectorViewOutputs.fields_with(Temporality.window), detector_view/factory.py:262-276)
+ROI_WINDOW_OUTPUTS = ('roi_spectra_current',)
+TOA_DIM = 'time_of_arrival'
+_ROI_SLOT = 0
+_SPECTRUM_SLOT = 1
 MONITOR_WINDOW_OUTPUTS = ('current', 'counts_total', 'counts_in_toa_range')
 
 
@@ -72,6 +79,25 @@ class LogicalViewConfig:
     transform: Callable[[np.ndarray, str], np.ndarray] | None = None
     reduction_axes: Sequence[int] = ()
     output_dims: tuple[str, ...] | None = None
+    roi_support: bool = True
+    spectrum_view: 'SpectrumViewConfig | None' = None
+
+
+@dataclass(frozen=True)
+class SpectrumViewConfig:
+    """``SpectrumViewSpec`` (SRC/workflows/detector_view/types.py) in index form.
+
+    The reference's transform folds / sums / flattens the cumulative
+    ``(screen..., toa)`` histogram (providers.py:300-325; BIFROST
+    bifrost/specs.py:311-329).  Here ``transform`` receives the flat screen
+    index array of shape ``screen_shape`` and returns it folded / transposed;
+    ``reduction_axes`` of the result are summed; ``output_dims`` name the kept
+    axes.  The regrouping then runs on the GPU (``lde_group_spectra``).
+    """
+
+    transform: Callable[[np.ndarray], np.ndarray] | None
+    output_dims: tuple[str, ...]
+    reduction_axes: Sequence[int] = ()
 
 
 def _histogram_slice(edges: TOAEdges, toa_range) -> tuple[int, int] | None:
@@ -137,6 +163,9 @@ class GpuDetectorViewWorkflow:
         stream: int | None = None,
         geometry_key: str | None = DETECTOR_TRANSFORM,
         strategy: str = 'auto',
+        roi_support: bool = False,
+        roi_keys: Mapping[str, str] | None = None,
+        spectrum_view: SpectrumViewConfig | None = None,
     ) -> None:
         self._source = source_name
         self._view = view
@@ -160,6 +189,24 @@ class GpuDetectorViewWorkflow:
         self._built = False
         self._start: Timestamp | None = None
         self._end: Timestamp | None = None
+        # ROI requests arrive as context streams keyed by their wire names
+        # (aux_source_names, detector_view/factory.py:234-246)
+        self._roi_support = roi_support
+        keys = dict(roi_keys or {})
+        self._roi_keys = {'roi_rectangle': keys.get('roi_rectangle', 'roi_rectangle'),
+                          'roi_polygon': keys.get('roi_polygon', 'roi_polygon')}
+        self._roi_requests: dict[str, Any] = {'roi_rectangle': None, 'roi_polygon': None}
+        self._roi_index: list[int] = []
+        self._spectrum = spectrum_view
+        self._spectrum_shape: tuple[int, ...] = ()
+        if spectrum_view is not None:
+            shape, groups = index_groups(view.screen_shape, spectrum_view.transform,
+                                         spectrum_view.reduction_axes)
+            if len(shape) != len(spectrum_view.output_dims):
+                raise ValueError(f'spectrum view output_dims {spectrum_view.output_dims} do not '
+                                 f'match the transformed shape {shape}')
+            self._spectrum_shape = shape
+            self._engine.set_groups(_SPECTRUM_SLOT, groups)
 
     @property
     def engine(self) -> BinningEngine:
@@ -188,6 +235,8 @@ class GpuDetectorViewWorkflow:
         self._end = end_time
         if self._geometry.changed(data):
             self._engine.reset_cumulative()
+        if self._roi_support:
+            self._update_rois(data)
         if self._source not in data:
             return
         toas, pids = _events_of(data[self._source])
@@ -198,6 +247,49 @@ class GpuDetectorViewWorkflow:
         self._counter += 1
         self._engine.accumulate(replica)
 
+    def _update_rois(self, data: Mapping[str, Any]) -> None:
+        """New ROI requests -> screen groups on the device (the reference's
+        precompute_roi_rectangle_bounds / precompute_roi_polygon_masks, roi.py:31-125)."""
+        changed = False
+        for name, wire in self._roi_keys.items():
+            if wire in data:
+                self._roi_requests[name] = data[wire]
+                changed = True
+        if not changed:
+            return
+        rects = _roi.from_concatenated(self._roi_requests['roi_rectangle'])
+        polys = _roi.from_concatenated(self._roi_requests['roi_polygon'])
+        self._roi_index, groups = _roi.roi_groups(self._view, rects, polys)
+        self._engine.set_groups(_ROI_SLOT, groups)
+
+    def _toa_coord(self) -> Variable:
+        return Variable((TOA_DIM,), self._edges_unit, self._params.toa_edges.unit)
+
+    def _roi_spectra(self, which: str) -> DataArray:
+        """``roi_spectra`` (roi.py:188-266): dims (roi, toa), int32 roi coord."""
+        n = len(self._roi_index)
+        if n:
+            values = self._engine.group_spectra(_ROI_SLOT, which)
+        else:
+            values = np.zeros((0, self._engine.n_toa_bins), dtype=self._engine.dtype)
+        return DataArray(values, ('roi', TOA_DIM), 'counts', {
+            'roi': Variable(('roi',), np.asarray(self._roi_index, dtype=np.int32)),
+            TOA_DIM: self._toa_coord(),
+        })
+
+    def _roi_readback(self, name: str) -> DataArray:
+        """``roi_rectangle_readback`` / ``roi_polygon_readback`` (roi.py:293-353):
+        the request unchanged, or an empty one carrying the screen coord units."""
+        req = self._roi_requests[name]
+        kind = 'rectangle' if name == 'roi_rectangle' else 'polygon'
+        if isinstance(req, DataArray) and len(np.atleast_1d(req.values)) > 0:
+            return req
+        if isinstance(req, Mapping) and req:
+            return _roi.to_concatenated(req, kind)
+        y_dim, x_dim = (self._view.screen_dims + (None, None))[:2]
+        units = {'x': self._view.screen_units.get(x_dim), 'y': self._view.screen_units.get(y_dim)}
+        return _roi.to_concatenated({}, kind, coord_units=units)
+
     def _image(self, values: np.ndarray) -> DataArray:
         img = values.reshape(self._view.screen_shape)
         if self._params.pixel_weighting and self._view.pixel_weights is not None:
@@ -207,6 +299,19 @@ class GpuDetectorViewWorkflow:
         return DataArray(img, self._view.screen_dims, 'counts', coords)
 
     def finalize(self) -> dict[str, Any]:
+        # grouped spectra read the window before finalize clears it; with an
+        # empty window they raise the same ValueError finalize would
+        extra: dict[str, Any] = {}
+        if self._roi_support:
+            extra['roi_spectra_current'] = self._roi_spectra('current')
+            extra['roi_spectra_cumulative'] = self._roi_spectra('cumulative')
+        if self._spectrum is not None:
+            vals = self._engine.group_spectra(_SPECTRUM_SLOT, 'cumulative')
+            extra['spectrum_view'] = DataArray(
+                vals.reshape(*self._spectrum_shape, -1),
+                (*self._spectrum.output_dims, TOA_DIM), 'counts',
+                {TOA_DIM: self._toa_coord()},
+            )
         res = self._engine.finalize(images=True)
         dt = self._engine.dtype.type
         out = {
@@ -219,23 +324,24 @@ class GpuDetectorViewWorkflow:
                 np.asarray(dt(res.cumulative_in_range)), (), 'counts'
             ),
         }
+        out.update(extra)
+        if self._roi_support:
+            out['roi_rectangle'] = self._roi_readback('roi_rectangle')
+            out['roi_polygon'] = self._roi_readback('roi_polygon')
         if self._start is not None:
             st = Variable((), self._start.to_ns(), 'ns')
             tt = Variable((), self._end.to_ns(), 'ns')
-            for name in DETECTOR_WINDOW_OUTPUTS:
+            names = DETECTOR_WINDOW_OUTPUTS + (ROI_WINDOW_OUTPUTS if self._roi_support else ())
+            for name in names:
                 out[name] = out[name].assign_coords(start_time=st, time=tt)
         self._start = self._end = None
         return out
 
     def read_histogram(self, which: str = 'cumulative') -> DataArray:
         h = self._engine.read_histogram(which)
-        dims = (*self._view.screen_dims, 'time_of_arrival')
+        dims = (*self._view.screen_dims, TOA_DIM)
         shape = (*self._view.screen_shape, h.shape[-1])
-        return DataArray(
-            h.reshape(shape), dims, 'counts',
-            {'time_of_arrival': Variable(('time_of_arrival',), self._edges_unit,
-                                         self._params.toa_edges.unit)},
-        )
+        return DataArray(h.reshape(shape), dims, 'counts', {TOA_DIM: self._toa_coord()})
 
     def clear(self) -> None:
         self._engine.clear()
@@ -287,10 +393,14 @@ class GpuDetectorViewFactory:
 
     def make_workflow(self, source_name: str, params: DetectorViewParams | None = None,
                       aux_source_names: Mapping[str, str] | None = None) -> GpuDetectorViewWorkflow:
-        _ = aux_source_names
+        cfg = self._config(source_name)
+        # geometric views always support ROIs (factory.py:187); logical views per config
+        roi_support = isinstance(cfg, GeometricViewConfig) or bool(cfg.roi_support)
+        spectrum = cfg.spectrum_view if isinstance(cfg, LogicalViewConfig) else None
         return GpuDetectorViewWorkflow(
             source_name, self.make_view(source_name), params, out_dtype=self._dtype,
-            device=self._device,
+            device=self._device, roi_support=roi_support, roi_keys=aux_source_names,
+            spectrum_view=spectrum,
         )
 
 

@@ -151,6 +151,23 @@ int lde_export_window(lde_handle *h, void *d_dst);
 int lde_finalize_partials(lde_handle *h, void *d_out);
 int lde_import_window(lde_handle *h, const void *d_src);
 
+/* Screen groupings: per-group TOA spectra summed on the device, replacing the
+ * host-side reductions of the finalize outputs
+ *   roi_spectra (rectangle slices / polygon masks)  SRC/workflows/detector_view/roi.py:188-266
+ *   spectrum_view (per-instrument regrouping)       SRC/workflows/detector_view/providers.py:300-325
+ *                                                   (BIFROST: config/instruments/bifrost/specs.py:311-329)
+ * Group g holds the flat screen indices screens[offsets[g] .. offsets[g+1]);
+ * groups may overlap and may be empty.  n_groups == 0 clears the slot.
+ * lde_group_spectra writes out[g * T + t] (out_dtype) for LDE_CURRENT (the
+ * window since the last finalize) or LDE_CUMULATIVE (the cumulative as the
+ * next finalize publishes it, i.e. including the window).  Call it before
+ * lde_finalize to get the current-window spectra of that finalize.  Sums are
+ * exact integers on the device; an empty slot writes nothing. */
+#define LDE_MAX_GROUP_SETS 4
+int lde_set_groups(lde_handle *h, int32_t slot, int64_t n_groups, const int64_t *offsets,
+                   const int32_t *screens);
+int lde_group_spectra(lde_handle *h, int32_t slot, int32_t which, void *host_out);
+
 /* Wait for all work queued on the handle's stream. */
 int lde_synchronize(lde_handle *h);
 

@@ -255,6 +255,58 @@ class AccumulatorPair:
 
 
 # --------------------------------------------------------------------------
+# ROI spectra and spectrum views (finalize-side regroupings)
+# --------------------------------------------------------------------------
+def roi_rectangle_slice(n: int, bounds, edges: np.ndarray | None) -> slice:
+    """One axis of ``histogram[dim, low:high]`` (roi.py:221-228): integer bounds
+    (``Interval.to_bounds`` without unit, SRC/config/models.py:274-290) slice
+    positionally, physical bounds slice by label on the bin-edge coord."""
+    low, high, unit = bounds
+    if unit is None:
+        return slice(int(low), int(high))
+    b, e = label_slice(edges, low, high)
+    return slice(b, e)
+
+
+def polygon_inside(xs, ys, x_centers: np.ndarray, y_centers: np.ndarray) -> np.ndarray:
+    """``_compute_polygon_mask`` (roi.py:128-185) without the inversion:
+    matplotlib ``Path.contains_points`` on the (y, x) grid of bin centers."""
+    from matplotlib.path import Path
+
+    xx, yy = np.meshgrid(x_centers, y_centers)
+    path = Path(list(zip(xs, ys)))
+    return path.contains_points(np.column_stack([xx.ravel(), yy.ravel()])).reshape(xx.shape)
+
+
+def roi_spectra(hist: np.ndarray, rectangles: Sequence, polygons: Sequence,
+                y_edges: np.ndarray | None = None, x_edges: np.ndarray | None = None) -> np.ndarray:
+    """``roi_spectra`` (roi.py:188-266) on a dense ``(y, x, spectral)`` array:
+    rectangles (``(y_bounds, x_bounds)`` with bounds ``(low, high, unit)``)
+    first, then polygons (``(y, x)`` boolean inside masks), each summed over
+    both screen dims -> ``(n_roi, spectral)``."""
+    ny, nx, nt = hist.shape
+    out = []
+    for yb, xb in rectangles:
+        sy = roi_rectangle_slice(ny, yb, y_edges)
+        sx = roi_rectangle_slice(nx, xb, x_edges)
+        out.append(hist[sy][:, sx].sum(axis=(0, 1)))
+    for inside in polygons:
+        out.append(hist[inside].sum(axis=0))  # masked sum: outside bins excluded
+    return np.asarray(out, dtype=hist.dtype).reshape(len(out), nt)
+
+
+def bifrost_spectrum_view(hist: np.ndarray, pixels_per_tube: int = 10) -> np.ndarray:
+    """``_bifrost_spectrum_transform`` (bifrost/specs.py:311-329) on a dense
+    ``(arc/tube=15, channel/pixel=900, toa)`` array: fold arc/tube -> (arc 5,
+    tube 3), channel/pixel -> (channel 9, pixel 100), pixel -> (pixel,
+    subpixel), sum subpixel, flatten (tube, channel, pixel) -> detector_number."""
+    sub = 100 // pixels_per_tube
+    nt = hist.shape[-1]
+    h = hist.reshape(5, 3, 9, pixels_per_tube, sub, nt).sum(axis=4)
+    return h.reshape(5, 3 * 9 * pixels_per_tube, nt)
+
+
+# --------------------------------------------------------------------------
 # Workflow-level restatements
 # --------------------------------------------------------------------------
 @dataclass

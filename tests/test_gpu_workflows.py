@@ -177,3 +177,139 @@ def test_golden_regression_vector_on_gpu():
         nz = np.nonzero(h)[0]
         np.testing.assert_array_equal(nz, g['hist_index'])
         np.testing.assert_array_equal(h[nz], g['hist_value'])
+
+
+def test_group_spectra_engine_overlapping_large_and_empty_groups():
+    """lde_group_spectra vs numpy group sums of the engine's own histograms:
+    overlapping groups, groups larger than one work item, empty groups, both
+    selectors, a folded (u64) window and the cumulative pending fold."""
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.engine import BinningEngine
+
+    inst = synthetic.dream_mantle()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    rng = np.random.default_rng(11)
+    groups = [rng.choice(view.n_screen, k, replace=False) for k in (1, 63, 64, 65, 700, 25600)]
+    groups.insert(2, np.zeros(0, np.int32))
+    groups.append(groups[3][:10])  # overlaps another group
+    for strategy in ('atomic', 'split'):
+        eng = BinningEngine(toa_edges_ns=inst.edges.edges_ns(), out_lut=view.lut,
+                            pid_offset=view.pid_offset, n_screen=view.n_screen, strategy=strategy)
+        eng.set_groups(0, groups)
+        eng.set_groups(3, [np.arange(view.n_screen)])
+        for b in range(3):
+            pid, toa = synthetic.dream_events(400_000, inst, seed=20 + b)
+            eng.stage(pid, toa)
+            eng.accumulate(b % 5)
+            cur, cum = eng.read_histogram('current'), eng.read_histogram('cumulative')
+            for which, h in (('current', cur), ('cumulative', cum)):
+                got = eng.group_spectra(0, which)
+                exp = np.asarray([h[g].sum(axis=0) for g in groups])
+                np.testing.assert_array_equal(got, exp)
+                np.testing.assert_array_equal(eng.group_spectra(3, which)[0], h.sum(axis=0))
+            if b == 1:
+                eng.finalize()
+        eng.set_groups(0, [])  # cleared slot -> empty result
+        assert eng.group_spectra(0, 'current').shape == (0, 100)
+        with pytest.raises(ValueError):
+            eng.set_groups(1, [np.array([view.n_screen])])  # out of range
+        eng.close()
+
+
+def test_geometric_workflow_roi_spectra_match_oracle():
+    """roi_spectra_current/cumulative (roi.py:188-266) for rectangles (label and
+    index bounds) and polygons on the DREAM view, across finalizes and an ROI
+    update, against the oracle on the oracle's histograms."""
+    from esslivedata_amd import roi, synthetic
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.workflows import DetectorViewParams, GeometricViewConfig, GpuDetectorViewFactory
+
+    inst = synthetic.dream_mantle()
+    params = DetectorViewParams(toa_edges=TOAEdges(start=0.5, stop=71.43, num_bins=100, scale='log'))
+    factory = GpuDetectorViewFactory(
+        detector_numbers={'mantle_detector': inst.detector_number},
+        view_config=GeometricViewConfig('cylinder_mantle_z', {'arc_length': 80, 'z': 320}),
+        projected_coords={'mantle_detector': inst.coords},
+    )
+    aux = {'roi_rectangle': 'job1/roi_rectangle', 'roi_polygon': 'job1/roi_polygon'}
+    wf = factory.make_workflow('mantle_detector', params, aux)
+    view = wf.view
+    ye, xe = view.screen_edges['arc_length'], view.screen_edges['z']
+    yc, xc = view.screen_coords['arc_length'], view.screen_coords['z']
+    ylo, yhi, xlo, xhi = ye[0], ye[-1], xe[0], xe[-1]
+    rects = {0: roi.RectangleROI(x=roi.Interval(xlo + 0.1 * (xhi - xlo), xlo + 0.6 * (xhi - xlo), 'm'),
+                                 y=roi.Interval(ylo + 0.2 * (yhi - ylo), ylo + 0.9 * (yhi - ylo), 'm')),
+             5: roi.RectangleROI(x=roi.Interval(xlo, xlo + 0.3 * (xhi - xlo), 'm'),
+                                 y=roi.Interval(ylo - 1.0, ylo + 0.4 * (yhi - ylo), 'm'))}
+    polys = {2: roi.PolygonROI(x=[xlo, xhi, 0.5 * (xlo + xhi)], y=[ylo, ylo, yhi], x_unit='m', y_unit='m')}
+    oedges = {d: ora.screen_edges(inst.coords[d], r) for d, r in inst.resolution.items()}
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=np.stack([ora.geometric_screen_index(inst.coords, oedges, k) for k in range(5)]),
+        screen_shape=(80, 320), toa_edges_ns=params.toa_edges.edges_ns(),
+    )
+
+    def expected(h, rr, pp):
+        o_r = [((r.y.min, r.y.max, r.y.unit), (r.x.min, r.x.max, r.x.unit)) for r in rr.values()]
+        o_p = [ora.polygon_inside(p.x, p.y, xc, yc) for p in pp.values()]
+        return ora.roi_spectra(h.reshape(80, 320, -1), o_r, o_p, oedges['arc_length'], oedges['z'])
+
+    t = 0
+    for phase in range(3):
+        data = {}
+        if phase == 0:
+            data = {aux['roi_rectangle']: roi.to_concatenated(rects, 'rectangle'),
+                    aux['roi_polygon']: roi.to_concatenated(polys, 'polygon')}
+        if phase == 2:  # ROI update: index-based rectangles replace the physical ones
+            rects = {1: roi.RectangleROI(x=roi.Interval(10, 250), y=roi.Interval(0, 40)),
+                     4: roi.RectangleROI(x=roi.Interval(0, 320), y=roi.Interval(79, 200))}
+            data = {aux['roi_rectangle']: roi.to_concatenated(rects, 'rectangle')}
+        for b in range(2):
+            pid, toa = synthetic.dream_events(300_000, inst, seed=100 + t)
+            wf.accumulate({'mantle_detector': (pid, toa), **(data if b == 0 else {})},
+                          start_time=_ts(t), end_time=_ts(t + 1))
+            o.accumulate(pid, toa)
+            t += 1
+        out, exp = wf.finalize(), o.finalize()
+        ids = list(rects) + list(polys)
+        cur, cum = out['roi_spectra_current'], out['roi_spectra_cumulative']
+        assert cur.dims == ('roi', 'time_of_arrival') and list(cur.coords['roi'].values) == ids
+        np.testing.assert_array_equal(cur.values, expected(exp['histogram_current'], rects, polys))
+        np.testing.assert_array_equal(cum.values, expected(exp['histogram_cumulative'], rects, polys))
+        assert 'start_time' in cur.coords and 'start_time' not in cum.coords
+        assert roi.from_concatenated(out['roi_rectangle']) == rects
+        assert roi.from_concatenated(out['roi_polygon']) == polys
+
+
+def test_bifrost_spectrum_view_float32_matches_oracle():
+    """BIFROST unified view: f32 outputs and spectrum_view (bifrost/specs.py:311-349)
+    from the cumulative histogram; ROI readbacks of a logical view carry no units."""
+    from esslivedata_amd import synthetic
+    from esslivedata_amd.workflows import GpuDetectorViewFactory, LogicalViewConfig
+
+    inst = synthetic.bifrost_unified()
+    cfg = LogicalViewConfig(transform=lambda a, _s: synthetic.bifrost_transform(a),
+                            output_dims=('arc/tube', 'channel/pixel'),
+                            spectrum_view=synthetic.bifrost_spectrum_config(10))
+    factory = GpuDetectorViewFactory(detector_numbers={'unified_detector': inst.detector_number},
+                                     view_config=cfg, out_dtype='float32')
+    wf = factory.make_workflow('unified_detector', None, {})
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=ora.logical_screen_index((5, 3, 9, 100), synthetic.bifrost_transform)[0][None, :],
+        screen_shape=(15, 900), toa_edges_ns=inst.edges.edges_ns(), dtype=np.float32,
+    )
+    for b in range(25):
+        pid, toa = synthetic.uniform_events(45_000, 1, 13_500, seed=300 + b)
+        wf.accumulate({'unified_detector': (pid, toa)}, start_time=_ts(b), end_time=_ts(b + 1))
+        o.accumulate(pid, toa)
+        if b % 10 == 9 or b == 24:
+            out, exp = wf.finalize(), o.finalize()
+            sv = out['spectrum_view']
+            assert sv.dims == ('arc', 'detector_number', 'time_of_arrival')
+            assert sv.values.dtype == np.float32 and sv.shape == (5, 270, 100)
+            np.testing.assert_array_equal(
+                sv.values, ora.bifrost_spectrum_view(exp['histogram_cumulative'].reshape(15, 900, -1)
+                                                     .astype(np.float64), 10))
+            assert out['roi_spectra_current'].shape == (0, 100)
+            assert out['roi_rectangle'].coords['x'].unit is None
