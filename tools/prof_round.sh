@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 WL=${WL:-dream}
 TAG=${TAG:-r1}
 OUT=gpurun_out/prof_${TAG}_${WL}
-ARGS="bench.py --workload $WL --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline ${BENCH_ARGS}"
+ARGS="bench.py --workload $WL --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline --e2e-steps 0 ${BENCH_ARGS}"
 rm -rf $OUT
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 $ARGS > $OUT/kt.log 2>&1
