@@ -183,8 +183,7 @@ def main():
                 for p in range(args.pulses)]
 
     def step(i: int):
-        for mp, mt in messages:
-            eng.stage_tensors(mp, mt)
+        eng.stage_tensors_batch(messages)
         eng.accumulate(i % view.n_replicas)
         if reducer is not None:
             reducer.finalize()

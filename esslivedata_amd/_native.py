@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = (
     'lde_destroy',
     'lde_stage',
     'lde_stage_device',
+    'lde_stage_device_batch',
     'lde_accumulate',
     'lde_finalize',
     'lde_read_histogram',
@@ -117,6 +118,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_destroy': (None, [H]),
         'lde_stage': (ctypes.c_int, [H, P, P, i64]),
         'lde_stage_device': (ctypes.c_int, [H, P, P, i64]),
+        'lde_stage_device_batch': (ctypes.c_int, [H, i64, P, P, P]),
         'lde_accumulate': (ctypes.c_int, [H, i32]),
         'lde_finalize': (ctypes.c_int, [H, ctypes.POINTER(LdeOutputs)]),
         'lde_read_histogram': (ctypes.c_int, [H, i32, P]),

@@ -181,6 +181,8 @@ struct lde_handle {
     int last_strategy = 0;
 
     // timing
+    hipEvent_t bin_stop_ext = nullptr;  // BINNING stop event for the last kernel to stamp
+    bool bin_stop_used = false;
     bool timing = false;
     uint32_t timing_mask = 0xffffffffu;  // LDE_K_* ids recorded while timing
     std::vector<TimedLaunch> launches;
@@ -733,10 +735,21 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         sa.cold_tcnt = h->d_cold_tcnt;
         sa.ablate = (int)env_ll("LDE_SIEVE_ABLATE", 0);
         {
-            Timed tm(h, LDE_K_SPLIT);
+            // k_sieve is timed by its own dispatch (start/stop events stamped
+            // by hipExtLaunchKernelGGL): no marker packets around it
+            hipEvent_t ea = nullptr, eb = nullptr;
+            if (h->timing && ((h->timing_mask >> LDE_K_SPLIT) & 1u)) {
+                ea = pool_event(h);
+                eb = ea ? pool_event(h) : nullptr;
+                if (!eb && ea) {
+                    h->event_pool.push_back(ea);
+                    ea = nullptr;
+                }
+            }
             HIPCALL(h, lde::launch_chunk_tab(h->d_segs, a.n_segs, chunks, h->d_sieve_dummy,
                                              h->d_chunk_tab, h->stream));
-            HIPCALL(h, lde::launch_sieve(sa, a.grid, h->stream));
+            HIPCALL(h, lde::launch_sieve(sa, a.grid, h->stream, ea, eb));
+            if (ea) h->launches.push_back({LDE_K_SPLIT, ea, eb});
         }
         {
             Timed tm(h, LDE_K_SPLIT_AUX);
@@ -763,7 +776,8 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         c.hist = h->d_win32;
         c.n_bins = h->nbins;
         Timed tm(h, LDE_K_PAGED);
-        HIPCALL(h, lde::launch_cold_pipeline(c, h->stream));
+        HIPCALL(h, lde::launch_cold_pipeline(c, h->stream, h->bin_stop_ext));
+        if (h->bin_stop_ext) h->bin_stop_used = true;
         return LDE_OK;
     } else {
         Timed tm(h, LDE_K_SPLIT);
@@ -1317,6 +1331,24 @@ int lde_stage_device(lde_handle *h, const void *d_pid, const void *d_toa, int64_
     return LDE_OK;
 }
 
+int lde_stage_device_batch(lde_handle *h, int64_t count, const void *const *d_pids,
+                           const void *const *d_toas, const int64_t *ns) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (count < 0) return fail(h, LDE_EINVAL, "negative message count");
+    if (count > 0 && (!d_toas || !ns || (!h->monitor && !d_pids)))
+        return fail(h, LDE_EINVAL, "message arrays must not be NULL");
+    for (int64_t i = 0; i < count; ++i) {
+        if (ns[i] < 0) return fail(h, LDE_EINVAL, "negative event count in message %lld", (long long)i);
+        if (ns[i] > 0 && (!d_toas[i] || (!h->monitor && !d_pids[i])))
+            return fail(h, LDE_EINVAL, "event arrays of message %lld must not be NULL", (long long)i);
+    }
+    for (int64_t i = 0; i < count; ++i)
+        if (ns[i] > 0)
+            h->dev_segments.push_back({h->monitor ? nullptr : (const int *)d_pids[i],
+                                       (const int *)d_toas[i], (long long)ns[i]});
+    return LDE_OK;
+}
+
 int lde_accumulate(lde_handle *h, int32_t replica) {
     if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
     if (replica < 0 || replica >= h->R)
@@ -1353,8 +1385,33 @@ int lde_accumulate(lde_handle *h, int32_t replica) {
     }
     const bool f32 = h->out_dtype == LDE_F32;
     {
-        Timed all(h, LDE_K_BINNING);
-        for (auto &p : pieces) {
+        // BINNING range: a start marker (the GPU waits for the host here
+        // anyway) and, on the sieve path, a stop stamped by the last kernel's
+        // own dispatch instead of a marker in front of the finalize kernels
+        hipEvent_t bin_a = nullptr, bin_b = nullptr;
+        if (h->timing && ((h->timing_mask >> LDE_K_BINNING) & 1u)) {
+            bin_a = pool_event(h);
+            bin_b = bin_a ? pool_event(h) : nullptr;
+            if (bin_a && !bin_b) {
+                h->event_pool.push_back(bin_a);
+                bin_a = nullptr;
+            }
+            if (bin_a) (void)hipEventRecord(bin_a, h->stream);
+        }
+        struct BinRange {
+            lde_handle *h;
+            hipEvent_t a, b;
+            ~BinRange() {
+                h->bin_stop_ext = nullptr;
+                if (!a) return;
+                if (!h->bin_stop_used) (void)hipEventRecord(b, h->stream);
+                h->launches.push_back({LDE_K_BINNING, a, b});
+            }
+        } bin_range{h, bin_a, bin_b};
+        h->bin_stop_used = false;
+        for (size_t pi = 0; pi < pieces.size(); ++pi) {
+            auto &p = pieces[pi];
+            h->bin_stop_ext = pi + 1 == pieces.size() ? bin_b : nullptr;
             long long n = 0;
             for (auto &s : p) n += s.n;
             if (!f32 && h->win_events + (unsigned long long)n > 0xffffffffULL) {
@@ -1413,22 +1470,19 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
     }
     {
         Timed tm(h, LDE_K_FINALIZE);
+        // totals and the overflow flag land in the pack tail from k_sum_totals
+        unsigned char *d_tail = h->d_pack + (size_t)h->S * 16;
         HIPCALL(h, lde::launch_finalize(
                        f32 ? 1 : 0, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
                        (want_cur_hist && !f32) ? h->d_snap : nullptr, h->S, h->T, h->range_lo,
                        h->range_hi, (!f32 && out->current_image) ? h->d_img_cur : nullptr,
                        (!f32 && out->cumulative_image) ? h->d_img_cum : nullptr, h->d_tot4,
+                       (unsigned long long *)d_tail, h->d_overflow, (uint32_t *)(d_tail + 32),
                        h->stream));
     }
     const size_t isz = f32 ? 4 : 8;
     // images, totals and the overflow flag leave in one pinned D2H copy
     // (separate copies into pageable memory cost ~25 us each)
-    unsigned char *d_tail = h->d_pack + (size_t)h->S * 16;
-    HIPCALL(h, hipMemcpyAsync(d_tail, h->d_tot4, 32, hipMemcpyDeviceToDevice, h->stream));
-    if (h->d_overflow)
-        HIPCALL(h, hipMemcpyAsync(d_tail + 32, h->d_overflow, 4, hipMemcpyDeviceToDevice, h->stream));
-    else
-        HIPCALL(h, hipMemsetAsync(d_tail + 32, 0, 4, h->stream));
     HIPCALL(h, hipMemcpyAsync(h->h_pack, h->d_pack, h->pack_bytes, hipMemcpyDeviceToHost, h->stream));
     std::vector<unsigned long long> tmp;
     if (!f32 && (want_cur_hist || want_cum_hist)) tmp.resize(nb);
@@ -1471,9 +1525,9 @@ int lde_finalize_partials(lde_handle *h, void *d_out) {
         Timed tm(h, LDE_K_FINALIZE);
         HIPCALL(h, lde::launch_finalize(2, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr,
                                         h->d_cum, nullptr, h->S, h->T, h->range_lo, h->range_hi,
-                                        o, o + h->S, h->d_tot4, h->stream));
+                                        o, o + h->S, h->d_tot4, o + 2 * h->S, nullptr, nullptr,
+                                        h->stream));
     }
-    HIPCALL(h, hipMemcpyAsync(o + 2 * h->S, h->d_tot4, 32, hipMemcpyDeviceToDevice, h->stream));
     h->window_has_data = false;
     h->win64_dirty = false;
     h->win_events = 0;

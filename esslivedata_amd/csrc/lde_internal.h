@@ -199,15 +199,19 @@ struct ColdArgs {
     long long n_bins;
 };
 size_t cold_sort_smem(int n_tiles);
-hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st);
+// start/stop: optional HIP events stamped by the kernel dispatch itself
+// (hipExtLaunchKernelGGL), so timing adds no marker packets between kernels
+hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t stop = nullptr);
 hipError_t launch_hot_reduce(const SplitArgs &a, uint32_t *win, hipStream_t st);
 hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
                                const uint16_t *screen_row, const uint32_t *pix_cnt, int cbits,
                                uint32_t *glut, uint32_t *tab, hipStream_t st);
 // dummy: kChunk x (pid_off - 1), the all-invalid chunk
 hipError_t launch_chunk_tab(const SegDesc *segs, int n_segs, long long n_chunks, const int *dummy,
-                            ChunkPtrs *tab, hipStream_t st);
-hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st);
+                            ChunkPtrs *tab, hipStream_t st,
+                            hipEvent_t start = nullptr);
+hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start = nullptr,
+                        hipEvent_t stop = nullptr);
 size_t split_smem(int ht4, int cache_words, const ToaParams &tp);
 hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st);
 hipError_t launch_split(const SplitArgs &a, hipStream_t st);
@@ -238,7 +242,8 @@ hipError_t launch_sum3(const unsigned long long *a, const unsigned long long *b,
 hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *win64,
                            unsigned long long *cum, unsigned long long *snap, long long S, int T,
                            int lo, int hi, void *cur_img, void *cum_img,
-                           unsigned long long *totals, hipStream_t st);
+                           unsigned long long *totals, unsigned long long *tot_copy,
+                           const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st);
 hipError_t launch_rows_f32(const float *h, long long S, int T, int lo, int hi, float *img,
                            hipStream_t st);
 // items: {group, begin, end, group has a single item}; out zeroed unless every

@@ -194,8 +194,13 @@ __global__ __launch_bounds__(256) void k_finalize_v4(uint32_t *__restrict__ win3
 // totals[q] = sum over blocks of the partials at totals[4 + 4 * block + q].
 // Thread i sums the partials i, i + 1024, ... (all of quantity i & 3) with
 // independent loads, then the 256 threads of each quantity reduce in LDS.
+// The four sums also go to `copy` (the finalize pack / a partials buffer) and
+// the page-pool overflow flag is carried along to `ovf_dst`, so finalize needs
+// no separate device-to-device copies (each a ~5 us blit).
 __global__ __launch_bounds__(1024) void k_sum_totals(unsigned long long *__restrict__ totals,
-                                                     int blocks) {
+                                                     int blocks, unsigned long long *__restrict__ copy,
+                                                     const uint32_t *__restrict__ ovf_src,
+                                                     uint32_t *__restrict__ ovf_dst) {
     __shared__ unsigned long long s[1024];
     const int n = 4 * blocks;
     unsigned long long v = 0;
@@ -206,7 +211,11 @@ __global__ __launch_bounds__(1024) void k_sum_totals(unsigned long long *__restr
         if ((int)threadIdx.x < d) s[threadIdx.x] += s[threadIdx.x + d];
         __syncthreads();
     }
-    if (threadIdx.x < 4) totals[threadIdx.x] = s[threadIdx.x];
+    if (threadIdx.x < 4) {
+        totals[threadIdx.x] = s[threadIdx.x];
+        if (copy) copy[threadIdx.x] = s[threadIdx.x];
+    }
+    if (ovf_dst && threadIdx.x == 4) *ovf_dst = ovf_src ? *ovf_src : 0u;
 }
 
 // f32-mode image rows: sum of f32 values over the TOA range in f64, rounded once
@@ -299,14 +308,16 @@ template <typename OUT>
 static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsigned long long *cum,
                               unsigned long long *snap, long long S, int T, int lo, int hi,
                               void *cur_img, void *cum_img, unsigned long long *totals,
-                              hipStream_t st) {
+                              unsigned long long *tot_copy, const uint32_t *ovf_src,
+                              uint32_t *ovf_dst, hipStream_t st) {
     if (T % 4 == 0 && T <= 128) {
         long long b8 = (S + 7) / 8;
         if (b8 > 8192) b8 = 8192;
         if (b8 < 1) b8 = 1;
         hipLaunchKernelGGL(k_finalize_v4<OUT>, dim3((unsigned)b8), dim3(256), 0, st, win32, win64,
                            cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, totals);
-        hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(1024), 0, st, totals, (int)b8);
+        hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(1024), 0, st, totals, (int)b8, tot_copy,
+                           ovf_src, ovf_dst);
         return;
     }
     long long blocks = (S + 3) / 4;
@@ -314,21 +325,25 @@ static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsign
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_finalize<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
                        cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, totals);
-    hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(1024), 0, st, totals, (int)blocks);
+    hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(1024), 0, st, totals, (int)blocks, tot_copy,
+                       ovf_src, ovf_dst);
 }
 
 // image element type: 0 f64, 1 f32, 2 u64 (exact partial sums for multi-GPU)
 hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *win64,
                            unsigned long long *cum, unsigned long long *snap, long long S, int T,
                            int lo, int hi, void *cur_img, void *cum_img,
-                           unsigned long long *totals, hipStream_t st) {
+                           unsigned long long *totals, unsigned long long *tot_copy,
+                           const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st) {
     if (img_kind == 1)
-        launch_finalize_t<float>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals, st);
+        launch_finalize_t<float>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals,
+                                 tot_copy, ovf_src, ovf_dst, st);
     else if (img_kind == 2)
         launch_finalize_t<unsigned long long>(win32, win64, cum, snap, S, T, lo, hi, cur_img,
-                                              cum_img, totals, st);
+                                              cum_img, totals, tot_copy, ovf_src, ovf_dst, st);
     else
-        launch_finalize_t<double>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals, st);
+        launch_finalize_t<double>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals,
+                                  tot_copy, ovf_src, ovf_dst, st);
     return hipGetLastError();
 }
 

@@ -31,6 +31,7 @@
 // Deferred chunks (partial tails, segments that are not 16-byte aligned) are
 // replaced by an all-invalid dummy chunk in the pipeline and binned afterwards
 // by a plain element-wise pass.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -665,13 +666,15 @@ hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
 }
 
 hipError_t launch_chunk_tab(const SegDesc *segs, int n_segs, long long n_chunks, const int *dummy,
-                            ChunkPtrs *tab, hipStream_t st) {
-    hipLaunchKernelGGL(k_chunk_tab, dim3((unsigned)((n_chunks + 1 + 255) / 256)), dim3(256), 0, st,
+                            ChunkPtrs *tab, hipStream_t st,
+                            hipEvent_t start) {
+    hipExtLaunchKernelGGL(k_chunk_tab, dim3((unsigned)((n_chunks + 1 + 255) / 256)), dim3(256), 0, st,
+                          start, nullptr, 0,
                        segs, n_segs, n_chunks, dummy, tab);
     return hipGetLastError();
 }
 
-hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st) {
+hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t stop) {
     hipLaunchKernelGGL(k_cold_scan, dim3(c.n_tiles), dim3(256), 0, st, c.tcnt, c.rows * c.groups,
                        c.n_tiles, c.boff, c.tile_total);
     hipLaunchKernelGGL(k_cold_plan, dim3(1), dim3(1024), 0, st, c.tile_total, c.n_tiles, c.item_keys,
@@ -686,8 +689,8 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st) {
         hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * c.groups), dim3(kSortThreads), sm, st,  \
                            c.cold, c.stride, c.cap, c.cold_cnt, c.boff, c.tile_base, c.n_tiles,  \
                            c.groups, c.keys);                                                     \
-        hipLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, st,   \
-                           c.keys, c.items, c.item_count, c.hist, c.n_bins);                      \
+        hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, st,\
+                              nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist, c.n_bins); \
         break;
         LDE_COLD(13)
         LDE_COLD(14)
@@ -701,23 +704,26 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st) {
 }
 
 template <int ABL>
-static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st) {
+static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
+                                 hipEvent_t stop) {
     if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles, a.tgroups) > kSplitSmemMax)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_sieve<ABL>, dim3(grid), dim3(kSplitThreads), 0, st, a);  // static LDS
+    hipExtLaunchKernelGGL(k_sieve<ABL>, dim3(grid), dim3(kSplitThreads), 0, st, start, stop, 0,
+                          a);  // static LDS
     return hipGetLastError();
 }
 
-hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st) {
+hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
+                        hipEvent_t stop) {
     switch (a.ablate) {
-    case 1: return launch_sieve_t<1>(a, grid, st);
-    case 2: return launch_sieve_t<2>(a, grid, st);
-    case 4: return launch_sieve_t<4>(a, grid, st);
-    case 7: return launch_sieve_t<7>(a, grid, st);
-    case 15: return launch_sieve_t<15>(a, grid, st);
-    case 16: return launch_sieve_t<16>(a, grid, st);
-    case 32: return launch_sieve_t<32>(a, grid, st);
-    default: return launch_sieve_t<0>(a, grid, st);
+    case 1: return launch_sieve_t<1>(a, grid, st, start, stop);
+    case 2: return launch_sieve_t<2>(a, grid, st, start, stop);
+    case 4: return launch_sieve_t<4>(a, grid, st, start, stop);
+    case 7: return launch_sieve_t<7>(a, grid, st, start, stop);
+    case 15: return launch_sieve_t<15>(a, grid, st, start, stop);
+    case 16: return launch_sieve_t<16>(a, grid, st, start, stop);
+    case 32: return launch_sieve_t<32>(a, grid, st, start, stop);
+    default: return launch_sieve_t<0>(a, grid, st, start, stop);
     }
 }
 

@@ -156,6 +156,26 @@ class BinningEngine:
             None if pid is None else pid.data_ptr(), toa.data_ptr(), toa.numel(), (pid, toa)
         )
 
+    def stage_tensors_batch(self, messages) -> None:
+        """Stage a batch of ``(pid, toa)`` int32 device tensors in one call
+        (``pid`` may be None for a monitor)."""
+        n = len(messages)
+        if n == 0:
+            return
+        ptrs = np.zeros((3, n), dtype=np.int64)
+        for i, (pid, toa) in enumerate(messages):
+            if pid is not None and pid.numel() != toa.numel():
+                raise ValueError('pixel_id and time_of_arrival must have the same length')
+            for t in (pid, toa):
+                if t is not None and (t.dtype.itemsize != 4 or not t.is_contiguous()):
+                    raise ValueError('device event tensors must be contiguous int32')
+            ptrs[0, i] = 0 if pid is None else pid.data_ptr()
+            ptrs[1, i] = toa.data_ptr()
+            ptrs[2, i] = toa.numel()
+        self._call(self._lib.lde_stage_device_batch, n, ptrs[0].ctypes.data, ptrs[1].ctypes.data,
+                   ptrs[2].ctypes.data)
+        self._keepalive.append(messages)
+
     def accumulate(self, replica: int = 0) -> None:
         self._call(self._lib.lde_accumulate, int(replica))
         self._keepalive.clear()

@@ -121,6 +121,9 @@ def _events_of(data) -> tuple[list, list | None]:
 
 
 def _stage(engine: BinningEngine, toas: list, pids: list | None) -> None:
+    if toas and all(hasattr(t, 'data_ptr') for t in toas):  # device tensors: one call, no copy
+        engine.stage_tensors_batch([(None if pids is None else pids[i], t) for i, t in enumerate(toas)])
+        return
     for i, toa in enumerate(toas):
         pid = None if pids is None else pids[i]
         if hasattr(toa, 'data_ptr'):  # device tensors: no copy

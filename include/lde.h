@@ -116,6 +116,13 @@ int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n);
  * stay valid until the next lde_accumulate returns. */
 int lde_stage_device(lde_handle *h, const void *d_pid, const void *d_toa, int64_t n);
 
+/* Stage a whole batch of device-resident messages in one call (the batch
+ * ToNXevent_data.get hands over, to_nxevent_data.py:155-200): message i is
+ * d_pids[i] / d_toas[i] with ns[i] events, same rules as lde_stage_device.
+ * Nothing is staged unless every message is valid. */
+int lde_stage_device_batch(lde_handle *h, int64_t count, const void *const *d_pids,
+                           const void *const *d_toas, const int64_t *ns);
+
 /* Bin everything staged since the last call into the current window using
  * noise replica `replica` (0 <= replica < R).  Replaces
  * GroupByPixel.get + project_events + hist + accumulator push. */

@@ -308,6 +308,14 @@ def test_device_staging_matches_host_staging(strategy):
         toa_edges_ns=edges,
     )
     np.testing.assert_array_equal(a.read_histogram(), o.batch_histogram(pid, toa, 1))
+    # the same batch through lde_stage_device_batch (one call, an empty message in it)
+    c = _engine(view, edges, strategy)
+    cuts = [0, 7, 1_000_003, 1_000_003, 2_500_000, len(pid)]
+    c.stage_tensors_batch([(dp[x:y], dt[x:y]) for x, y in zip(cuts[:-1], cuts[1:])])
+    c.accumulate(1)
+    np.testing.assert_array_equal(a.read_histogram(), c.read_histogram())
+    with pytest.raises(ValueError):
+        c.stage_tensors_batch([(dp[:5], dt[:4])])
 
 
 def test_auto_picks_split_for_skewed_and_paged_for_uniform():

@@ -23,8 +23,7 @@ for timing in (False, True):
     acc = {'stage': 0.0, 'accumulate': 0.0, 'finalize': 0.0}
     for i in range(25):
         t0 = time.perf_counter()
-        for mp, mt in msgs:
-            eng.stage_tensors(mp, mt)
+        eng.stage_tensors_batch(msgs)
         t1 = time.perf_counter()
         eng.accumulate(i % view.n_replicas)
         t2 = time.perf_counter()
@@ -43,8 +42,7 @@ s0 = torch.cuda.Event(enable_timing=True); s1 = torch.cuda.Event(enable_timing=T
 tot = 0.0
 for i in range(20):
     s0.record()
-    for mp, mt in msgs:
-        eng.stage_tensors(mp, mt)
+    eng.stage_tensors_batch(msgs)
     eng.accumulate(i % view.n_replicas)
     eng.finalize(images=True)
     s1.record()
