@@ -234,11 +234,18 @@ def main():
     # ring + async H2D on the engine stream), binned and finalized
     e2e = None
     if args.e2e_steps > 0:
-        host_msgs = [(mp.cpu().numpy(), mt.cpu().numpy()) for mp, mt in messages]
+        from esslivedata_amd.ev44 import serialise_ev44
+
+        t_pulse = 1_767_225_600 * 10**9
+        host_msgs = [
+            np.frombuffer(serialise_ev44(args.workload, k, [t_pulse + k * 71_428_571], 0,
+                                         mt.cpu().numpy(), mp.cpu().numpy()), dtype=np.uint8)
+            for k, (mp, mt) in enumerate(messages)
+        ]
 
         def host_step(i: int):
-            for hp, ht in host_msgs:
-                eng.stage(hp, ht)
+            for payload in host_msgs:
+                eng.stage_ev44(payload)
             eng.accumulate(i % view.n_replicas)
             if reducer is not None:
                 reducer.finalize()
@@ -263,9 +270,10 @@ def main():
             'unit': 'events/s',
             'ms_per_step': 1e3 * e2e_s / args.e2e_steps,
             'steps': args.e2e_steps,
-            'note': 'PCIe-inclusive: each step stages its 14 messages from pageable host '
-                    'arrays through lde_stage (memcpy into the pinned ring + async H2D), '
-                    'then accumulate + finalize; not `value`',
+            'note': 'PCIe-inclusive: each step hands its 14 serialized ev44 payloads '
+                    '(pageable host bytes) to lde_stage_ev44 (in-place flatbuffer decode, '
+                    'memcpy into the pinned ring + async H2D), then accumulate + finalize; '
+                    'not `value`',
         }
         del host_msgs
     total_events = n_step * args.steps * world

@@ -21,6 +21,7 @@ LDE_ESTATE = -2
 LDE_ENOMEM = -3
 LDE_EHIP = -4
 LDE_ENODATA = -5
+LDE_ENOTSUP = -6
 
 LDE_F64 = 0
 LDE_F32 = 1
@@ -54,6 +55,8 @@ EXPORTED_SYMBOLS = (
     'lde_stage',
     'lde_stage_device',
     'lde_stage_device_batch',
+    'lde_ev44_decode',
+    'lde_stage_ev44',
     'lde_accumulate',
     'lde_finalize',
     'lde_read_histogram',
@@ -119,6 +122,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_stage': (ctypes.c_int, [H, P, P, i64]),
         'lde_stage_device': (ctypes.c_int, [H, P, P, i64]),
         'lde_stage_device_batch': (ctypes.c_int, [H, i64, P, P, P]),
+        'lde_ev44_decode': (ctypes.c_int, [P, i64, P]),
+        'lde_stage_ev44': (ctypes.c_int, [H, P, i64, i64, i32, ctypes.POINTER(i64)]),
         'lde_accumulate': (ctypes.c_int, [H, i32]),
         'lde_finalize': (ctypes.c_int, [H, ctypes.POINTER(LdeOutputs)]),
         'lde_read_histogram': (ctypes.c_int, [H, i32, P]),
@@ -191,4 +196,6 @@ def check(rc: int, handle=None) -> None:
     msg = last_error(handle)
     if rc in (LDE_EINVAL, LDE_ENODATA):
         raise ValueError(msg)
+    if rc == LDE_ENOTSUP:
+        raise NotImplementedError(msg)
     raise RuntimeError(msg or f'lde error {rc}')

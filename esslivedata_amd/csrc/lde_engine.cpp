@@ -1321,6 +1321,31 @@ int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n) 
     return LDE_OK;
 }
 
+int lde_ev44_decode(const uint8_t *buf, int64_t len, lde_ev44_view *out) {
+    std::string err;
+    const int rc = lde::ev44_parse(buf, len, out, &err);
+    if (rc) return fail(nullptr, rc, "%s", err.c_str());
+    return LDE_OK;
+}
+
+int lde_stage_ev44(lde_handle *h, const uint8_t *buf, int64_t len, int64_t kafka_timestamp_ms,
+                   int32_t flags, int64_t *timestamp_ns) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (flags & ~(LDE_EV44_SINGLE_PULSE | LDE_EV44_MONITOR))
+        return fail(h, LDE_EINVAL, "unknown ev44 flags 0x%x", (unsigned)flags);
+    if ((flags & LDE_EV44_MONITOR) && !h->monitor)
+        return fail(h, LDE_EINVAL, "LDE_EV44_MONITOR on a detector handle");
+    if (h->monitor) flags |= LDE_EV44_MONITOR;
+    lde_ev44_view v;
+    std::string err;
+    int rc = lde::ev44_parse(buf, len, &v, &err);
+    if (!rc) rc = lde::ev44_events(&v, kafka_timestamp_ms, flags, timestamp_ns, &err);
+    if (rc) return fail(h, rc, "%s", err.c_str());
+    // the vectors may be unaligned inside the payload: lde_stage only memcpy's them
+    return lde_stage(h, h->monitor ? nullptr : (const int32_t *)v.pixel_id,
+                     (const int32_t *)v.time_of_flight, v.n_time_of_flight);
+}
+
 int lde_stage_device(lde_handle *h, const void *d_pid, const void *d_toa, int64_t n) {
     if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
     if (n < 0) return fail(h, LDE_EINVAL, "negative event count");

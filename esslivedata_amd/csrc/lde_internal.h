@@ -4,6 +4,10 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
+
+struct lde_ev44_view;  // include/lde.h
+
 namespace lde {
 
 constexpr int kPartThreads = 512;                  // pass A block
@@ -253,5 +257,11 @@ hipError_t launch_group_spectra(int mode, const int4 *items, int n_items, const 
                                 int T, const uint32_t *win32, const unsigned long long *win64,
                                 const unsigned long long *cum, const float *fsrc,
                                 unsigned long long *out, hipStream_t st);
+
+// ev44 flatbuffer decode (lde_ev44.cpp): in-place parse with bounds checks,
+// then the adapter rules (timestamp fallback, single pulse, lengths).
+int ev44_parse(const uint8_t *buf, int64_t len, ::lde_ev44_view *v, std::string *err);
+int ev44_events(const ::lde_ev44_view *v, int64_t kafka_timestamp_ms, int32_t flags,
+                int64_t *timestamp_ns, std::string *err);
 
 }  // namespace lde

@@ -14,6 +14,7 @@ import numpy as np
 
 from . import _native
 from ._native import check
+from .preprocessors import Timestamp
 
 
 @dataclass
@@ -138,6 +139,17 @@ class BinningEngine:
                 f'got {len(p)} and {len(t)}'
             )
         self._call(self._lib.lde_stage, p.ctypes.data, t.ctypes.data, len(t))
+
+    def stage_ev44(self, payload, kafka_timestamp_ms: int = 0, *, single_pulse: bool = True):
+        """Decode one ev44 payload in the engine and stage its events
+        (``lde_stage_ev44``): the adapter chain plus ``ToNXevent_data.add`` in
+        one native call.  Returns the message ``Timestamp``."""
+        raw = np.frombuffer(payload, dtype=np.uint8) if not isinstance(payload, np.ndarray) else payload
+        ts = ctypes.c_int64()
+        flags = 1 if single_pulse else 0
+        self._call(self._lib.lde_stage_ev44, raw.ctypes.data if raw.size else None, raw.size,
+                   int(kafka_timestamp_ms), flags, ctypes.byref(ts))
+        return Timestamp.from_ns(ts.value)
 
     def stage_device(self, pid_ptr: int | None, toa_ptr: int, n: int, keepalive=None) -> None:
         """Stage events already in HBM (device pointers, int32)."""

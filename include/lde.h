@@ -112,6 +112,55 @@ int lde_abi_version(void);
  * monitor.  n == 0 is accepted (empty message). */
 int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n);
 
+/* ev44 messages (ess-streaming-data-types ev44 flatbuffer, file identifier
+ * "ev44").  lde_ev44_decode decodes one payload in place, replacing
+ * eventdata_ev44.deserialise_ev44 / Event44Message.GetRootAs as called by
+ *   KafkaToEv44Adapter.adapt           SRC/kafka/message_adapter.py:192-204
+ *   KafkaToMonitorEventsAdapter.adapt  SRC/kafka/message_adapter.py:380-409
+ * Every offset and extent is checked against len: garbage, empty, truncated
+ * or wrong-schema payloads return LDE_EINVAL (message in
+ * lde_last_error(NULL), thread-local) where the reference raises and drops
+ * the message.  Vector pointers point into buf (zero copy, possibly
+ * unaligned); `present` flags which fields the payload carries. */
+#define LDE_EV44_HAS_SOURCE_NAME (1u << 0)
+#define LDE_EV44_HAS_MESSAGE_ID (1u << 1)
+#define LDE_EV44_HAS_REFERENCE_TIME (1u << 2)
+#define LDE_EV44_HAS_REFERENCE_TIME_INDEX (1u << 3)
+#define LDE_EV44_HAS_TIME_OF_FLIGHT (1u << 4)
+#define LDE_EV44_HAS_PIXEL_ID (1u << 5)
+typedef struct lde_ev44_view {
+    const char *source_name;           /* UTF-8, not NUL-terminated */
+    int64_t source_name_len;
+    int64_t message_id;
+    const void *reference_time;        /* int64 [n_reference_time], ns since epoch */
+    int64_t n_reference_time;
+    const void *reference_time_index;  /* int32 [n_reference_time_index] */
+    int64_t n_reference_time_index;
+    const void *time_of_flight;        /* int32 [n_time_of_flight], ns */
+    int64_t n_time_of_flight;
+    const void *pixel_id;              /* int32 [n_pixel_id] */
+    int64_t n_pixel_id;
+    uint32_t present;                  /* LDE_EV44_HAS_* bits */
+} lde_ev44_view;
+int lde_ev44_decode(const uint8_t *buf, int64_t len, lde_ev44_view *out);
+
+/* Decode one ev44 payload and stage its events (lde_stage semantics) in one
+ * call: the adapter chain KafkaToEv44Adapter -> Ev44ToDetectorEventsAdapter ->
+ * DetectorEvents.from_ev44 (message_adapter.py:192-204, 412-437;
+ * to_nxevent_data.py:16-19, 57-69) for detector handles, and
+ * KafkaToMonitorEventsAdapter (time_of_flight only, pixel_id ignored) for
+ * monitor handles.  flags: LDE_EV44_SINGLE_PULSE applies
+ * _require_single_pulse (-> LDE_ENOTSUP, NotImplementedError in Python);
+ * LDE_EV44_MONITOR selects the monitor rules on a detector handle is invalid
+ * and is implied by a monitor handle.  *timestamp_ns (optional) receives
+ * reference_time[-1], or kafka_timestamp_ms * 1e6 when that vector is empty.
+ * A rejected payload stages nothing. */
+#define LDE_ENOTSUP (-6) /* unsupported message -> NotImplementedError */
+#define LDE_EV44_SINGLE_PULSE 1
+#define LDE_EV44_MONITOR 2
+int lde_stage_ev44(lde_handle *h, const uint8_t *buf, int64_t len, int64_t kafka_timestamp_ms,
+                   int32_t flags, int64_t *timestamp_ns);
+
 /* Stage events already resident in HBM.  No copy: the device buffers must
  * stay valid until the next lde_accumulate returns. */
 int lde_stage_device(lde_handle *h, const void *d_pid, const void *d_toa, int64_t n);
