@@ -18,7 +18,9 @@
 #include <cstring>
 #include <limits>
 #include <new>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lde.h"
@@ -1307,13 +1309,43 @@ int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n) 
     }
     if (int rc = ensure_stage_capacity(h, h->staged_host + n)) return rc;
     const long long off = h->staged_host;
-    std::memcpy(h->h_ptoa + off, toa, (size_t)n * 4);
-    HIPCALL(h, hipMemcpyAsync(h->d_stoa + off, h->h_ptoa + off, (size_t)n * 4,
-                              hipMemcpyHostToDevice, h->stream));
-    if (!h->monitor) {
-        std::memcpy(h->h_ppid + off, pid, (size_t)n * 4);
-        HIPCALL(h, hipMemcpyAsync(h->d_spid + off, h->h_ppid + off, (size_t)n * 4,
-                                  hipMemcpyHostToDevice, h->stream));
+    // Large messages: split into chunks; worker threads each memcpy a chunk
+    // into the pinned ring and queue its H2D right away, so the host copies
+    // run in parallel and overlap the PCIe transfers of earlier chunks.  The
+    // single-thread memcpy, not PCIe, bounded the end-to-end rate.
+    const long long chunk = std::max<long long>(1 << 18, env_ll("LDE_STAGE_CHUNK", 1 << 20));
+    const int arrays = h->monitor ? 1 : 2;
+    const long long n_chunks = (n + chunk - 1) / chunk;
+    const int workers = (int)std::min<long long>(
+        std::max<long long>(1, env_ll("LDE_STAGE_THREADS", 8)), n_chunks * arrays);
+    auto copy_chunk = [&](long long item) -> hipError_t {
+        const int a = (int)(item % arrays);
+        const long long c0 = (item / arrays) * chunk;
+        const long long cn = std::min(chunk, n - c0);
+        int *hp = (a == 0 ? h->h_ptoa : h->h_ppid) + off + c0;
+        int *dp = (a == 0 ? h->d_stoa : h->d_spid) + off + c0;
+        const int32_t *src = (a == 0 ? toa : pid) + c0;
+        std::memcpy(hp, src, (size_t)cn * 4);
+        return hipMemcpyAsync(dp, hp, (size_t)cn * 4, hipMemcpyHostToDevice, h->stream);
+    };
+    if (workers <= 1) {
+        for (long long it = 0; it < n_chunks * arrays; ++it) HIPCALL(h, copy_chunk(it));
+    } else {
+        std::atomic<long long> next{0};
+        std::atomic<int> err{(int)hipSuccess};
+        auto work = [&]() {
+            (void)hipSetDevice(h->device);
+            for (long long it; (it = next.fetch_add(1)) < n_chunks * arrays;) {
+                const hipError_t e = copy_chunk(it);
+                if (e != hipSuccess) err.store((int)e);
+            }
+        };
+        std::vector<std::thread> pool;
+        pool.reserve(workers - 1);
+        for (int w = 1; w < workers; ++w) pool.emplace_back(work);
+        work();
+        for (auto &t : pool) t.join();
+        HIPCALL(h, (hipError_t)err.load());
     }
     HIPCALL(h, hipEventRecord(h->pin_done, h->stream));
     h->pin_pending = true;
