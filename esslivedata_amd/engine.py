@@ -174,16 +174,25 @@ class BinningEngine:
         n = len(messages)
         if n == 0:
             return
-        ptrs = np.zeros((3, n), dtype=np.int64)
-        for i, (pid, toa) in enumerate(messages):
-            if pid is not None and pid.numel() != toa.numel():
+        # host time here is GPU idle time between batches: one pass over the
+        # messages, identity dtype test first (torch attribute calls dominate)
+        import torch
+
+        i32 = torch.int32
+        rows = []
+        for pid, toa in messages:
+            nn = toa.numel()
+            if (toa.dtype is not i32 and toa.dtype.itemsize != 4) or not toa.is_contiguous():
+                raise ValueError('device event tensors must be contiguous int32')
+            if pid is None:
+                rows.append((0, toa.data_ptr(), nn))
+                continue
+            if (pid.dtype is not i32 and pid.dtype.itemsize != 4) or not pid.is_contiguous():
+                raise ValueError('device event tensors must be contiguous int32')
+            if pid.numel() != nn:
                 raise ValueError('pixel_id and time_of_arrival must have the same length')
-            for t in (pid, toa):
-                if t is not None and (t.dtype.itemsize != 4 or not t.is_contiguous()):
-                    raise ValueError('device event tensors must be contiguous int32')
-            ptrs[0, i] = 0 if pid is None else pid.data_ptr()
-            ptrs[1, i] = toa.data_ptr()
-            ptrs[2, i] = toa.numel()
+            rows.append((pid.data_ptr(), toa.data_ptr(), nn))
+        ptrs = np.array(rows, dtype=np.int64).T.copy()
         self._call(self._lib.lde_stage_device_batch, n, ptrs[0].ctypes.data, ptrs[1].ctypes.data,
                    ptrs[2].ctypes.data)
         self._keepalive.append(messages)
