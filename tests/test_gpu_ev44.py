@@ -88,3 +88,33 @@ def test_monitor_ev44_staging_ignores_pixel_id():
     b.accumulate(0)
     np.testing.assert_array_equal(a.read_histogram(), b.read_histogram())
     np.testing.assert_array_equal(b.read_histogram().ravel(), np.histogram(toa, edges)[0])
+
+
+@pytest.mark.parametrize('chunk', ['262144', '1048576'])
+def test_threaded_host_staging_large_messages(monkeypatch, chunk):
+    """lde_stage splits large messages over worker threads (each chunk's H2D
+    queued by the thread that copied it): detector and monitor handles, ragged
+    chunk tails, a message that starts mid-ring."""
+    from esslivedata_amd import ev44, projection, synthetic
+    from esslivedata_amd.engine import BinningEngine
+
+    monkeypatch.setenv('LDE_STAGE_CHUNK', chunk)
+    inst = synthetic.dummy_panel()
+    view = projection.logical_lut(inst.detector_number)
+    edges = inst.edges.edges_ns()
+    pid, toa = synthetic.fake_detector_events(3_333_337, 1, 16384 + 50, seed=9)
+    eng = BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                        n_screen=view.n_screen)
+    eng.stage(pid[:7], toa[:7])
+    eng.stage_ev44(ev44.serialise_ev44('panel_0', 0, [1], 0, toa[7:], pid[7:]))
+    eng.accumulate(0)
+    o = ora.OracleDetectorView(detector_number=inst.detector_number,
+                               pixel_screen=np.arange(16384)[None, :], screen_shape=(128, 128),
+                               toa_edges_ns=edges)
+    got = eng.read_histogram()
+    np.testing.assert_array_equal(got, o.batch_histogram(pid, toa, 0).reshape(got.shape))
+    mon = BinningEngine.monitor(np.linspace(0.0, 80_000_000.5, 101))
+    mon.stage(None, toa)
+    mon.accumulate(0)
+    np.testing.assert_array_equal(mon.read_histogram().ravel(),
+                                  np.histogram(toa, np.linspace(0.0, 80_000_000.5, 101))[0])
