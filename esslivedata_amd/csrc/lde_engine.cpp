@@ -492,22 +492,32 @@ int ensure_partition_capacity(lde_handle *h, long long chunks, long long max_ite
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
 // ---- binning ---------------------------------------------------------------
-int upload_segments(lde_handle *h, const std::vector<lde::SegDesc> &sd) {
+int ensure_segs_cap(lde_handle *h, long long n) {
+    if (n <= h->segs_cap && h->d_segs) return LDE_OK;
     if (h->segs_pending) {
         HIPCALL(h, hipEventSynchronize(h->segs_done));
         h->segs_pending = false;
     }
-    if ((long long)sd.size() > h->segs_cap) {
+    {
         HIPCALL(h, hipStreamSynchronize(h->stream));
         dev_free(h->d_segs);
         if (h->h_segs) (void)hipHostFree(h->h_segs);
         h->h_segs = nullptr;
         h->segs_cap = 0;
-        const long long cap = std::max<long long>((long long)sd.size(), 256);
+        const long long cap = std::max<long long>(n, 256);
         if (int rc = dev_alloc(h, &h->d_segs, (size_t)cap)) return rc;
         HIPCALL(h, hipHostMalloc((void **)&h->h_segs, cap * sizeof(lde::SegDesc), hipHostMallocDefault));
         h->segs_cap = cap;
     }
+    return LDE_OK;
+}
+
+int upload_segments(lde_handle *h, const std::vector<lde::SegDesc> &sd) {
+    if (h->segs_pending) {
+        HIPCALL(h, hipEventSynchronize(h->segs_done));
+        h->segs_pending = false;
+    }
+    if (int rc = ensure_segs_cap(h, (long long)sd.size())) return rc;
     std::memcpy(h->h_segs, sd.data(), sd.size() * sizeof(lde::SegDesc));
     HIPCALL(h, hipMemcpyAsync(h->d_segs, h->h_segs, sd.size() * sizeof(lde::SegDesc),
                               hipMemcpyHostToDevice, h->stream));
@@ -626,7 +636,15 @@ int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
 // Returns 1 (nothing launched) when AUTO should fall back to PAGED.
 int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks,
               long long total, int replica, bool forced) {
-    if (int rc = upload_segments(h, sd)) return rc;
+    // the descriptor table is uploaded lazily: the SIEVE pass of a batch of
+    // at most kKargSegs messages passes it as kernel arguments instead
+    if (int rc = ensure_segs_cap(h, (long long)sd.size())) return rc;  // d_segs fixed from here
+    bool uploaded = false;
+    auto upload = [&]() -> int {
+        if (uploaded) return LDE_OK;
+        uploaded = true;
+        return upload_segments(h, sd);
+    };
     lde::SplitArgs a;
     a.segs = h->d_segs;
     a.n_segs = (int)sd.size();
@@ -660,6 +678,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     // that replica's rows.
     int &uses = h->hot_uses[replica];
     if (uses < 0 || uses >= h->hot_refresh) {
+        if (int rc = upload()) return rc;
         std::vector<int> todo;
         for (int r = 0; r < h->R; ++r)
             if (r == replica || h->hot_uses[(size_t)r] < 0) todo.push_back(r);
@@ -762,8 +781,14 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                     ea = nullptr;
                 }
             }
-            HIPCALL(h, lde::launch_chunk_tab(h->d_segs, a.n_segs, chunks, h->d_sieve_dummy,
-                                             h->d_chunk_tab, h->stream));
+            if (!uploaded && (long long)sd.size() <= lde::kKargSegs && env_ll("LDE_KARG_SEGS", 1)) {
+                HIPCALL(h, lde::launch_chunk_tab_karg(sd.data(), a.n_segs, chunks, h->d_sieve_dummy,
+                                                      h->d_chunk_tab, h->d_segs, h->stream));
+            } else {
+                if (int rc = upload()) return rc;
+                HIPCALL(h, lde::launch_chunk_tab(h->d_segs, a.n_segs, chunks, h->d_sieve_dummy,
+                                                 h->d_chunk_tab, h->stream));
+            }
             HIPCALL(h, lde::launch_sieve(sa, a.grid, h->stream, ea, eb));
             if (ea) h->launches.push_back({LDE_K_SPLIT, ea, eb});
         }
@@ -796,6 +821,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         if (h->bin_stop_ext) h->bin_stop_used = true;
         return LDE_OK;
     } else {
+        if (int rc = upload()) return rc;
         Timed tm(h, LDE_K_SPLIT);
         HIPCALL(h, lde::launch_split(a, h->stream));
     }

@@ -214,6 +214,16 @@ hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
 hipError_t launch_chunk_tab(const SegDesc *segs, int n_segs, long long n_chunks, const int *dummy,
                             ChunkPtrs *tab, hipStream_t st,
                             hipEvent_t start = nullptr);
+// Batches of up to kKargSegs messages: the descriptors travel as kernel
+// arguments (no pinned staging + H2D copy before the event pass); the kernel
+// also writes them to segs_out for the kernels that read the device table.
+constexpr int kKargSegs = 24;
+struct SegKarg {
+    SegDesc s[kKargSegs];
+};
+hipError_t launch_chunk_tab_karg(const SegDesc *host_segs, int n_segs, long long n_chunks,
+                                 const int *dummy, ChunkPtrs *tab, SegDesc *segs_out,
+                                 hipStream_t st);
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start = nullptr,
                         hipEvent_t stop = nullptr);
 size_t split_smem(int ht4, int cache_words, const ToaParams &tp);

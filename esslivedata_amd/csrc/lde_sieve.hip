@@ -142,6 +142,35 @@ __global__ __launch_bounds__(256) void k_chunk_tab(const SegDesc *__restrict__ s
     tab[c] = r;
 }
 
+// k_chunk_tab with the descriptors in kernel arguments: every index into the
+// argument array is static (unrolled), so the reads stay scalar kernarg loads
+__global__ __launch_bounds__(256) void k_chunk_tab_karg(SegKarg sk, int n_segs, long long n_chunks,
+                                                        const int *dummy,
+                                                        ChunkPtrs *__restrict__ tab,
+                                                        SegDesc *__restrict__ segs_out) {
+    if (blockIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < kKargSegs; ++i)
+            if ((int)threadIdx.x == i && i < n_segs) segs_out[i] = sk.s[i];
+    }
+    const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (c > n_chunks) return;
+    ChunkPtrs r{dummy, dummy};
+    if (c < n_chunks) {
+        // last segment whose first chunk is <= c (chunk0 ascending)
+        SegDesc sd = sk.s[0];
+#pragma unroll
+        for (int i = 1; i < kKargSegs; ++i)
+            if (i < n_segs && sk.s[i].chunk0 <= c) sd = sk.s[i];
+        const long long base = (c - sd.chunk0) * kChunk;
+        if (((((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0) && base + kChunk <= sd.n) {
+            r.pid = sd.pid + base;
+            r.toa = sd.toa + base;
+        }
+    }
+    tab[c] = r;
+}
+
 // ---------------------------------------------------------------------------
 // the event pass
 // ---------------------------------------------------------------------------
@@ -671,6 +700,17 @@ hipError_t launch_chunk_tab(const SegDesc *segs, int n_segs, long long n_chunks,
     hipExtLaunchKernelGGL(k_chunk_tab, dim3((unsigned)((n_chunks + 1 + 255) / 256)), dim3(256), 0, st,
                           start, nullptr, 0,
                        segs, n_segs, n_chunks, dummy, tab);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_tab_karg(const SegDesc *host_segs, int n_segs, long long n_chunks,
+                                 const int *dummy, ChunkPtrs *tab, SegDesc *segs_out,
+                                 hipStream_t st) {
+    if (n_segs < 1 || n_segs > kKargSegs) return hipErrorInvalidValue;
+    SegKarg sk{};
+    for (int i = 0; i < n_segs; ++i) sk.s[i] = host_segs[i];
+    hipLaunchKernelGGL(k_chunk_tab_karg, dim3((unsigned)((n_chunks + 1 + 255) / 256)), dim3(256), 0,
+                       st, sk, n_segs, n_chunks, dummy, tab, segs_out);
     return hipGetLastError();
 }
 

@@ -379,3 +379,42 @@ def test_finalize_partials_match_finalize():
                                                    ref.cumulative_total, ref.cumulative_in_range]
         else:
             assert not h[:S].any() and int(h[2 * S]) == 0 and int(h[2 * S + 2]) > 0
+
+
+@pytest.mark.parametrize('karg', ['1', '0'])
+@pytest.mark.parametrize('n_msgs', [1, 14, 24, 25, 40])
+def test_split_many_device_messages(n_msgs, karg, monkeypatch):
+    """SIEVE with the message descriptors passed as kernel arguments (<= 24
+    messages) or uploaded (more, or LDE_KARG_SEGS=0): ragged, misaligned
+    device segments, replica cycling, hot-set refresh every batch."""
+    import torch
+
+    monkeypatch.setenv('LDE_KARG_SEGS', karg)
+    monkeypatch.setenv('LDE_HOT_REFRESH', '2')
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.dream_mantle()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, 'split')
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=_oracle_pixel_screen_geometric(inst),
+        screen_shape=(80, 320),
+        toa_edges_ns=edges,
+    )
+    rng = np.random.default_rng(n_msgs)
+    for batch in range(3):
+        pid, toa = synthetic.dream_events(1_000_003, inst, seed=200 + batch)
+        dp = torch.as_tensor(pid, device='cuda')
+        dt = torch.as_tensor(toa, device='cuda')
+        cuts = np.sort(rng.choice(np.arange(1, len(pid)), n_msgs - 1, replace=False))
+        bounds = [0, *cuts.tolist(), len(pid)]
+        eng.stage_tensors_batch([(dp[a:b], dt[a:b]) for a, b in zip(bounds[:-1], bounds[1:])])
+        eng.accumulate(batch % view.n_replicas)
+        o.accumulate(pid, toa)
+    res = eng.finalize(hists=True)
+    exp = o.finalize()
+    assert eng.info()['last_strategy'] == 'split'
+    np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
+    np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
