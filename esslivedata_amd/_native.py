@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     'lde_stage_device_batch',
     'lde_ev44_decode',
     'lde_stage_ev44',
+    'lde_rebin_f64',
     'lde_accumulate',
     'lde_finalize',
     'lde_read_histogram',
@@ -123,6 +124,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_stage_device': (ctypes.c_int, [H, P, P, i64]),
         'lde_stage_device_batch': (ctypes.c_int, [H, i64, P, P, P]),
         'lde_ev44_decode': (ctypes.c_int, [P, i64, P]),
+        'lde_rebin_f64': (ctypes.c_int, [P, P, i64, P, i64, P, P, P]),
         'lde_stage_ev44': (ctypes.c_int, [H, P, i64, i64, i32, ctypes.POINTER(i64)]),
         'lde_accumulate': (ctypes.c_int, [H, i32]),
         'lde_finalize': (ctypes.c_int, [H, ctypes.POINTER(LdeOutputs)]),

@@ -1393,6 +1393,19 @@ int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n) 
     return LDE_OK;
 }
 
+int lde_rebin_f64(const double *d_src_edges, const double *d_src_values, int64_t n_src,
+                  const double *d_dst_edges, int64_t n_dst, double *d_out_a, double *d_out_b,
+                  void *stream) {
+    if (n_src < 1 || n_dst < 1) return fail(nullptr, LDE_EINVAL, "rebin needs at least one bin");
+    if (!d_src_edges || !d_src_values || !d_dst_edges)
+        return fail(nullptr, LDE_EINVAL, "rebin arrays must not be NULL");
+    if (!d_out_a && !d_out_b) return LDE_OK;
+    const hipError_t e = lde::launch_rebin_f64(d_src_edges, d_src_values, n_src, d_dst_edges, n_dst,
+                                               d_out_a, d_out_b, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(nullptr, LDE_EHIP, "k_rebin_f64: %s", hipGetErrorString(e));
+    return LDE_OK;
+}
+
 int lde_ev44_decode(const uint8_t *buf, int64_t len, lde_ev44_view *out) {
     std::string err;
     const int rc = lde::ev44_parse(buf, len, out, &err);

@@ -268,6 +268,9 @@ hipError_t launch_group_spectra(int mode, const int4 *items, int n_items, const 
                                 const unsigned long long *cum, const float *fsrc,
                                 unsigned long long *out, hipStream_t st);
 
+hipError_t launch_rebin_f64(const double *se, const double *sv, long long ns, const double *de,
+                            long long nd, double *out_a, double *out_b, hipStream_t st);
+
 // ev44 flatbuffer decode (lde_ev44.cpp): in-place parse with bounds checks,
 // then the adapter rules (timestamp fallback, single pulse, lengths).
 int ev44_parse(const uint8_t *buf, int64_t len, ::lde_ev44_view *v, std::string *err);

@@ -366,4 +366,39 @@ hipError_t launch_group_spectra(int mode, const int4 *items, int n_items, const 
     return hipGetLastError();
 }
 
+// Histogram-mode monitors: rebin a float64 histogram onto the view's edges
+// and add it into the window and the cumulative accumulator in one pass
+// (monitor_workflow.py:101-108 `rebin`, then the accumulator pushes of
+// accumulators.py:129-160).  One thread per output bin; source bins in
+// ascending order, each adding value * overlap / width (uniform density
+// inside a source bin, as scipp's rebin).
+__global__ void k_rebin_f64(const double *__restrict__ se, const double *__restrict__ sv, long long ns,
+                            const double *__restrict__ de, long long nd, double *__restrict__ out_a,
+                            double *__restrict__ out_b) {
+    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nd) return;
+    const double lo = de[j], hi = de[j + 1];
+    // first source bin whose upper edge is above lo
+    long long a = 0, b = ns;
+    while (a < b) {
+        const long long m = (a + b) >> 1;
+        if (se[m + 1] <= lo) a = m + 1; else b = m;
+    }
+    double acc = 0.0;
+    for (long long i = a; i < ns && se[i] < hi; ++i) {
+        const double xl = se[i], xh = se[i + 1];
+        const double ov = fmin(xh, hi) - fmax(xl, lo);
+        if (ov > 0.0) acc += sv[i] * ov / (xh - xl);
+    }
+    if (out_a) out_a[j] += acc;
+    if (out_b) out_b[j] += acc;
+}
+
+hipError_t launch_rebin_f64(const double *se, const double *sv, long long ns, const double *de,
+                            long long nd, double *out_a, double *out_b, hipStream_t st) {
+    hipLaunchKernelGGL(k_rebin_f64, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, st, se, sv, ns,
+                       de, nd, out_a, out_b);
+    return hipGetLastError();
+}
+
 }  // namespace lde

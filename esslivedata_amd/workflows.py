@@ -438,10 +438,48 @@ class GpuMonitorWorkflow:
         self._start: Timestamp | None = None
         self._end: Timestamp | None = None
         self._built = False
+        self._device = device
+        # histogram mode (da00 monitor histograms): float64 window and
+        # cumulative on the device, fed by lde_rebin_f64
+        self._hist_mode = False
+        self._hcur = self._hcum = self._hedges = None
+        self._hslice = label_slice(e_unit, float(lo), float(hi))
+        self._hdata = False
 
     @property
     def engine(self) -> BinningEngine:
         return self._engine
+
+    def _push_histogram(self, hist: DataArray) -> None:
+        """Histogram mode (monitor_workflow.py:101-108): convert the coord to
+        the edges' unit, rebin onto the edges and push into both accumulators
+        on the GPU (one ``lde_rebin_f64`` launch)."""
+        import torch
+
+        from ._native import check, lib
+
+        dim = hist.dims[0]
+        coord = hist.coords[dim]
+        src_edges = convert_time(np.asarray(coord.values, dtype=np.float64), coord.unit,
+                                 self._edges.unit)
+        vals = np.ascontiguousarray(hist.values, dtype=np.float64).reshape(-1)
+        if src_edges.shape != (vals.size + 1,):
+            raise ValueError(f'histogram coord {dim!r} must hold bin edges')
+        dev = torch.device('cuda', self._device)
+        if self._hcur is None:
+            e = self._edges.get_edges()
+            self._hedges = torch.as_tensor(np.asarray(e, dtype=np.float64), device=dev)
+            self._hcur = torch.zeros(len(e) - 1, dtype=torch.float64, device=dev)
+            self._hcum = torch.zeros_like(self._hcur)
+        se = torch.as_tensor(src_edges, device=dev)
+        sv = torch.as_tensor(vals, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        check(lib().lde_rebin_f64(se.data_ptr(), sv.data_ptr(), vals.size, self._hedges.data_ptr(),
+                                  self._hcur.numel(), self._hcur.data_ptr(), self._hcum.data_ptr(),
+                                  stream))
+        torch.cuda.current_stream(dev).synchronize()  # se/sv are freed on return
+        self._hist_mode = True
+        self._hdata = True
 
     def build(self, *, context_keys=None, chain_patch_bindings: Iterable = ()) -> None:
         if self._built and (context_keys or list(chain_patch_bindings)):
@@ -455,9 +493,17 @@ class GpuMonitorWorkflow:
         self._end = end_time
         if self._geometry.changed(data):
             self._engine.reset_cumulative()
+            if self._hcum is not None:
+                self._hcum.zero_()
+                self._hcur.zero_()
         if self._source not in data:
             return
-        toas, _ = _events_of(data[self._source])
+        value = data[self._source]
+        if isinstance(value, DataArray) and np.ndim(value.values) == 1 and value.dims \
+                and value.dims[0] in value.coords:
+            self._push_histogram(value)
+            return
+        toas, _ = _events_of(value)
         _stage(self._engine, toas, None)
         self._engine.accumulate(0)
 
@@ -466,7 +512,43 @@ class GpuMonitorWorkflow:
         return DataArray(values.reshape(-1), (dim,), 'counts',
                          {dim: Variable((dim,), self._coord, self._edges.unit)})
 
+    def _finalize_histogram_mode(self) -> dict[str, Any]:
+        if not self._hdata:
+            raise ValueError('No data has been added')
+        cur = self._hcur.cpu().numpy()
+        cum = self._hcum.cpu().numpy()
+        self._hcur.zero_()
+        self._hdata = False
+        dim = 'time_of_arrival'
+        coord = Variable((dim,), np.asarray(self._edges.get_edges(), dtype=np.float64),
+                         self._edges.unit)
+        lo, hi = self._hslice
+
+        def h(v):
+            return DataArray(v, (dim,), 'counts', {dim: coord})
+
+        def scalar(x):
+            return DataArray(np.asarray(float(x)), (), 'counts')
+
+        return {
+            'cumulative': h(cum),
+            'current': h(cur),
+            'counts_total': scalar(cur.sum()),
+            'counts_in_toa_range': scalar(cur[lo:hi].sum()),
+            'counts_total_cumulative': scalar(cum.sum()),
+            'counts_in_toa_range_cumulative': scalar(cum[lo:hi].sum()),
+        }
+
     def finalize(self) -> dict[str, Any]:
+        if self._hist_mode:
+            out = self._finalize_histogram_mode()
+            if self._start is not None:
+                st = Variable((), self._start.to_ns(), 'ns')
+                tt = Variable((), self._end.to_ns(), 'ns')
+                for name in MONITOR_WINDOW_OUTPUTS:
+                    out[name] = out[name].assign_coords(start_time=st, time=tt)
+            self._start = self._end = None
+            return out
         res = self._engine.finalize(images=False, hists=True)
         out = {
             'cumulative': self._hist(res.cumulative_hist),
@@ -488,6 +570,10 @@ class GpuMonitorWorkflow:
 
     def clear(self) -> None:
         self._engine.clear()
+        if self._hcur is not None:
+            self._hcur.zero_()
+            self._hcum.zero_()
+        self._hdata = False
         self._start = self._end = None
 
 

@@ -151,8 +151,8 @@ int lde_ev44_decode(const uint8_t *buf, int64_t len, lde_ev44_view *out);
  * KafkaToMonitorEventsAdapter (time_of_flight only, pixel_id ignored) for
  * monitor handles.  flags: LDE_EV44_SINGLE_PULSE applies
  * _require_single_pulse (-> LDE_ENOTSUP, NotImplementedError in Python);
- * LDE_EV44_MONITOR selects the monitor rules on a detector handle is invalid
- * and is implied by a monitor handle.  *timestamp_ns (optional) receives
+ * LDE_EV44_MONITOR (the monitor rules) is implied by a monitor handle and
+ * invalid on a detector handle.  *timestamp_ns (optional) receives
  * reference_time[-1], or kafka_timestamp_ms * 1e6 when that vector is empty.
  * A rejected payload stages nothing. */
 #define LDE_ENOTSUP (-6) /* unsupported message -> NotImplementedError */
@@ -223,6 +223,16 @@ int lde_import_window(lde_handle *h, const void *d_src);
 int lde_set_groups(lde_handle *h, int32_t slot, int64_t n_groups, const int64_t *offsets,
                    const int32_t *screens);
 int lde_group_spectra(lde_handle *h, int32_t slot, int32_t which, void *host_out);
+
+/* Histogram-mode monitors (monitor_workflow.py:101-108): rebin a float64
+ * histogram (n_src bins, n_src + 1 ascending edges, already in the target
+ * unit) onto n_dst bins and ADD the result into d_out_a and d_out_b (either
+ * may be NULL), i.e. the window and cumulative pushes of one message.  All
+ * arrays are device memory; runs on `stream` (hipStream_t, NULL = default).
+ * Errors: LDE_EINVAL, message in lde_last_error(NULL). */
+int lde_rebin_f64(const double *d_src_edges, const double *d_src_values, int64_t n_src,
+                  const double *d_dst_edges, int64_t n_dst, double *d_out_a, double *d_out_b,
+                  void *stream);
 
 /* Wait for all work queued on the handle's stream. */
 int lde_synchronize(lde_handle *h);

@@ -210,6 +210,29 @@ def monitor_histogram(toa: np.ndarray, toa_edges_ns: np.ndarray) -> np.ndarray:
     return np.bincount(tb, minlength=len(toa_edges_ns) - 1).astype(np.float64)
 
 
+def rebin(src_edges: np.ndarray, values: np.ndarray, dst_edges: np.ndarray) -> np.ndarray:
+    """``_histogram_monitor`` histogram mode (monitor_workflow.py:101-108):
+    scipp ``rebin`` of a 1-D float64 histogram, uniform density inside each
+    source bin; each new bin sums ``value * overlap / width`` over the source
+    bins in ascending order.  Pinned by the reference's KATs
+    (tests/workflows/monitor_workflow_test.py:190-216, 518-548); the exact
+    rounding order beyond them is parity unpinned (scipp's C++ rebin)."""
+    se = np.asarray(src_edges, dtype=np.float64)
+    sv = np.asarray(values, dtype=np.float64)
+    de = np.asarray(dst_edges, dtype=np.float64)
+    out = np.zeros(len(de) - 1)
+    for j in range(len(de) - 1):
+        lo, hi = de[j], de[j + 1]
+        acc = 0.0
+        for i in range(len(sv)):
+            xl, xh = se[i], se[i + 1]
+            ov = min(xh, hi) - max(xl, lo)
+            if ov > 0.0:
+                acc += sv[i] * ov / (xh - xl)
+        out[j] = acc
+    return out
+
+
 # --------------------------------------------------------------------------
 # Accumulator pair (accumulators.py:86-195)
 # --------------------------------------------------------------------------

@@ -313,3 +313,50 @@ def test_bifrost_spectrum_view_float32_matches_oracle():
                                                      .astype(np.float64), 10))
             assert out['roi_spectra_current'].shape == (0, 100)
             assert out['roi_rectangle'].coords['x'].unit is None
+
+
+def test_monitor_workflow_histogram_mode_rebin():
+    """Histogram-mode monitors (monitor_workflow.py:101-108) through
+    lde_rebin_f64: the reference KATs (monitor_workflow_test.py:190-216,
+    518-548), then random histograms in another unit vs the oracle rebin."""
+    from esslivedata_amd.dataarray import DataArray, Variable
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.workflows import GpuMonitorWorkflow
+
+    def hist(edges, values, dim='tof', unit='ns'):
+        return DataArray(np.asarray(values, dtype=np.float64), (dim,), 'counts',
+                         {dim: Variable((dim,), np.asarray(edges, dtype=np.float64), unit)})
+
+    edges = TOAEdges(start=0.0, stop=10.0, num_bins=5, unit='ns')
+    wf = GpuMonitorWorkflow('monitor_1', edges)
+    wf.build()
+    vals = [1.0, 2.0, 3.0, 4.0, 5.0, 4.0, 3.0, 2.0, 1.0, 0.0]
+    wf.accumulate({'monitor_1': hist(np.linspace(0, 10, 11), vals)}, start_time=_ts(0),
+                  end_time=_ts(1000))
+    out = wf.finalize()
+    np.testing.assert_array_equal(out['current'].values, [3.0, 7.0, 9.0, 5.0, 1.0])
+    assert out['current'].dims == ('time_of_arrival',)
+    wf.accumulate({'monitor_1': hist(np.linspace(0, 10, 11), [1.0] * 10, 'time_of_arrival')},
+                  start_time=_ts(1000), end_time=_ts(2000))
+    out = wf.finalize()
+    assert out['current'].sum().value == 10.0 and out['counts_total'].value == 10.0
+    assert out['counts_in_toa_range'].value == 10.0
+    assert out['cumulative'].sum().value == 35.0
+    with pytest.raises(ValueError):
+        wf.finalize()
+
+    # ms target edges, ns input histograms with ragged random edges
+    edges = TOAEdges()  # 0..71.43 ms, 100 bins
+    wf = GpuMonitorWorkflow('monitor_2', edges, range_filter=(5.0, 30.0))
+    rng = np.random.default_rng(4)
+    e = edges.get_edges()
+    cum = np.zeros(len(e) - 1)
+    for _ in range(3):
+        src = np.sort(rng.uniform(-5e6, 80e6, 3001))
+        v = rng.uniform(0, 100, 3000)
+        exp = ora.rebin(src * 1e-6, v, e)
+        wf.accumulate({'monitor_2': hist(src, v)}, start_time=_ts(0), end_time=_ts(1))
+        cum += exp
+        out = wf.finalize()
+        np.testing.assert_allclose(out['current'].values, exp, rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(out['cumulative'].values, cum, rtol=1e-12, atol=1e-9)

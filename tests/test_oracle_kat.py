@@ -172,3 +172,17 @@ def test_c_oracle_matches_numpy_oracle():
         exp = np.array([x[1] for x in kat['cases']])
         got = cv.accumulate(np.ones(len(toa), np.int32), toa)
         np.testing.assert_array_equal(got, np.bincount(exp[exp >= 0], minlength=len(e) - 1))
+
+
+def test_rebin_kats_from_the_reference_monitor_tests():
+    """monitor_workflow_test.py:190-216 (sums preserved; 0..10 ns in 10 bins
+    onto linspace(0, 10, 6)) and :518-548 (ten ones -> total 10)."""
+    dst = np.linspace(0, 10, 6)
+    vals = [1.0, 2.0, 3.0, 4.0, 5.0, 4.0, 3.0, 2.0, 1.0, 0.0]
+    got = ora.rebin(np.linspace(0, 10, 11), vals, dst)
+    np.testing.assert_array_equal(got, [3.0, 7.0, 9.0, 5.0, 1.0])
+    assert got.sum() == sum(vals)
+    assert ora.rebin(np.linspace(0, 10, 11), [1.0] * 10, dst).sum() == 10.0
+    # partial overlaps: uniform density, outside the target range dropped
+    got = ora.rebin(np.array([-1.0, 1.0, 3.0]), [2.0, 4.0], np.array([0.0, 2.0, 4.0]))
+    np.testing.assert_array_equal(got, [1.0 + 2.0, 2.0])
