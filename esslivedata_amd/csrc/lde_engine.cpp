@@ -801,6 +801,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         c.n_tiles = h->n_tiles;
         c.rows = a.grid;
         c.groups = tg;
+        c.halves = env_ll("LDE_SORT_HALVES", 1) > 1 ? 2 : 1;  // 2: measured no faster (tools/halves_ab.sh)
         c.cold = h->d_cold;
         c.stride = a.cold_cap + lde::kSplitThreads / 64;
         c.cap = a.cold_cap;

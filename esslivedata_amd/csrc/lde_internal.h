@@ -191,6 +191,7 @@ struct ColdArgs {
     int tile_bits, n_tiles;
     int rows;    // sieve blocks
     int groups;  // wave groups per sieve block (sort blocks per sieve block)
+    int halves = 1;  // sort blocks per (block, group) region: 1 or 2
     const uint32_t *cold;
     long long stride, cap;  // region stride and capacity (keys)
     const uint32_t *cold_cnt, *tcnt;

@@ -521,12 +521,16 @@ size_t cold_sort_smem(int n_tiles) {
     return 4 * ((size_t)kSortPiece + 3 * (size_t)align4(n_tiles) + 32);
 }
 
+// halves == 2: two blocks share a region (two blocks per CU), the first
+// half's pieces fill each tile's slots upward from the region's tile offset,
+// the second half's downward from its end (offset + the region's tile count),
+// so the halves need no count of each other's keys.
 template <int TB>
 __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
     const uint32_t *__restrict__ cold, long long stride, long long cap,
     const uint32_t *__restrict__ cold_cnt, const uint32_t *__restrict__ boff,
-    const uint32_t *__restrict__ tile_base, int n_tiles, int groups,
-    uint16_t *__restrict__ out) {
+    const uint32_t *__restrict__ tcnt, const uint32_t *__restrict__ tile_base, int n_tiles,
+    int groups, int halves, uint16_t *__restrict__ out) {
     constexpr int KPT = kSortPiece / kSortThreads;  // 16 keys per thread
     constexpr uint32_t MASK = (1u << TB) - 1u;
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
@@ -542,7 +546,8 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
     // keys, each filled to a multiple of 4; logical key i lives in the
     // sub-region of the last wave whose prefix is <= i
     constexpr int NW = kSplitThreads / 64;
-    const int b = blockIdx.x / groups, g = blockIdx.x % groups;
+    const int row = blockIdx.x / halves, half = blockIdx.x % halves;
+    const int b = row / groups, g = row % groups;
     const int WPG = NW / groups;
     if (tid == 0) {
         uint32_t acc = 0;
@@ -558,6 +563,9 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
     for (int w = 0; w <= NW; ++w) pre[w] = s_w[w];
     __syncthreads();
     const uint32_t n = pre[NW];
+    const uint32_t npieces = (n + kSortPiece - 1) / kSortPiece;
+    const uint32_t mid = halves > 1 ? min(n, ((npieces + 1) / 2) * (uint32_t)kSortPiece) : n;
+    const uint32_t pb = half ? mid : 0u, pe = half ? n : mid;  // this block's logical keys
     const uint32_t capw = (uint32_t)(cap / NW);
     auto phys = [&](uint32_t i) __attribute__((always_inline)) {
         uint32_t w = 0;
@@ -568,7 +576,8 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
     const uint32_t *src = cold + (size_t)b * (size_t)stride;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, (uint32_t)(cap * 4));
     for (int t = tid; t < n_tiles; t += kSortThreads)
-        s_cur[t] = tile_base[t] + boff[(size_t)blockIdx.x * n_tiles + t];
+        s_cur[t] = tile_base[t] + boff[(size_t)row * n_tiles + t] +
+                   (half ? tcnt[(size_t)row * n_tiles + t] : 0u);
     constexpr int TPT = kMaxTiles / kSortThreads;
     // the next piece's keys are requested before the current piece is sorted
     v4u nk[KPT / 4];
@@ -579,17 +588,17 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
             nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)phys(e0), 0, 0);
         }
     };
-    if (n > 0) fetch(0);
-    for (uint32_t p0 = 0; p0 < n; p0 += kSortPiece) {
+    if (pb < pe) fetch(pb);
+    for (uint32_t p0 = pb; p0 < pe; p0 += kSortPiece) {
         for (int t = tid; t < n_tiles; t += kSortThreads) s_cnt[t] = 0;
         uint32_t key[KPT], rank[KPT];
 #pragma unroll
         for (int j = 0; j < KPT / 4; ++j) {
             const uint32_t e0 = p0 + ((uint32_t)j * kSortThreads + (uint32_t)tid) * 4u;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n ? nk[j][q] : 0xFFFFFFFFu;
+            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < pe ? nk[j][q] : 0xFFFFFFFFu;
         }
-        if (p0 + kSortPiece < n) fetch(p0 + kSortPiece);
+        if (p0 + kSortPiece < pe) fetch(p0 + kSortPiece);
         __syncthreads();
 #pragma unroll
         for (int e = 0; e < KPT; ++e) {
@@ -619,13 +628,24 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(
         for (int e = 0; e < KPT; ++e)
             if (key[e] != 0xFFFFFFFFu) s_sorted[s_start[key[e] >> (TB + 2)] + rank[e]] = key[e];
         __syncthreads();
-        for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
-            const uint32_t k = s_sorted[i];
-            const uint32_t t = k >> (TB + 2);
-            out[s_cur[t] + (i - s_start[t])] = (uint16_t)((k >> 2) & MASK);
+        if (half == 0) {
+            for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
+                const uint32_t k = s_sorted[i];
+                const uint32_t t = k >> (TB + 2);
+                out[s_cur[t] + (i - s_start[t])] = (uint16_t)((k >> 2) & MASK);
+            }
+        } else {
+            for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
+                const uint32_t k = s_sorted[i];
+                const uint32_t t = k >> (TB + 2);
+                out[s_cur[t] - 1u - (i - s_start[t])] = (uint16_t)((k >> 2) & MASK);
+            }
         }
         __syncthreads();
-        for (int t = tid; t < n_tiles; t += kSortThreads) s_cur[t] += s_cnt[t];
+        if (half == 0)
+            for (int t = tid; t < n_tiles; t += kSortThreads) s_cur[t] += s_cnt[t];
+        else
+            for (int t = tid; t < n_tiles; t += kSortThreads) s_cur[t] -= s_cnt[t];
     }
 }
 
@@ -726,9 +746,9 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
     case TB:                                                                                      \
         (void)hipFuncSetAttribute((const void *)k_cold_sort<TB>,                                  \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);           \
-        hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * c.groups), dim3(kSortThreads), sm, st,  \
-                           c.cold, c.stride, c.cap, c.cold_cnt, c.boff, c.tile_base, c.n_tiles,  \
-                           c.groups, c.keys);                                                     \
+        hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * c.groups * c.halves), dim3(kSortThreads), \
+                           sm, st, c.cold, c.stride, c.cap, c.cold_cnt, c.boff, c.tcnt,           \
+                           c.tile_base, c.n_tiles, c.groups, c.halves, c.keys);                   \
         hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, st,\
                               nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist, c.n_bins); \
         break;

@@ -30,6 +30,9 @@ VARIANTS = [
     {'LDE_PIXEL_CACHE_BITS': '6', 'LDE_SPLIT_GRID': '17'},
     {'LDE_PIXEL_CACHE_BITS': '15'},
     # SPLIT with the original event pass instead of the SIEVE pass
+    # k_cold_sort with two blocks per cold region (upward/downward fill)
+    {'LDE_SORT_HALVES': '2'},
+    {'LDE_SORT_HALVES': '2', 'LDE_HOT_ROWS': '8', 'LDE_SPLIT_GRID': '3'},
     {'LDE_SIEVE': '0'},
     {'LDE_SIEVE': '0', 'LDE_PIXEL_CACHE_BITS': '6', 'LDE_SPLIT_GRID': '17'},
 ]
