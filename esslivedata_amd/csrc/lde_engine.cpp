@@ -80,6 +80,9 @@ struct lde_handle {
     long long pin_cap = 0;
     hipEvent_t pin_done = nullptr;
     bool pin_pending = false;
+    // optional second copy stream for host staging (LDE_STAGE_STREAMS=2)
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_s1 = nullptr, ev_s2 = nullptr;
     std::vector<Segment> dev_segments;
 
     // partition workspace
@@ -998,6 +1001,9 @@ void release(lde_handle *h) {
     if (h->h_ppid) (void)hipHostFree(h->h_ppid);
     if (h->h_ptoa) (void)hipHostFree(h->h_ptoa);
     if (h->pin_done) (void)hipEventDestroy(h->pin_done);
+    if (h->ev_s1) (void)hipEventDestroy(h->ev_s1);
+    if (h->ev_s2) (void)hipEventDestroy(h->ev_s2);
+    if (h->stream2) (void)hipStreamDestroy(h->stream2);
     dev_free(h->d_payload);
     dev_free(h->d_starts);
     dev_free(h->d_part);
@@ -1359,6 +1365,18 @@ int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n) 
     const long long n_chunks = (n + chunk - 1) / chunk;
     const int workers = (int)std::min<long long>(
         std::max<long long>(1, env_ll("LDE_STAGE_THREADS", 8)), n_chunks * arrays);
+    // two copy streams: odd chunks go on stream2, which first waits for the
+    // handle's stream (the previous batch's kernels may still read the ring)
+    const bool two = n_chunks * arrays > 1 && env_ll("LDE_STAGE_STREAMS", 1) > 1;
+    if (two) {
+        if (!h->stream2) {
+            HIPCALL(h, hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+            HIPCALL(h, hipEventCreateWithFlags(&h->ev_s1, hipEventDisableTiming));
+            HIPCALL(h, hipEventCreateWithFlags(&h->ev_s2, hipEventDisableTiming));
+        }
+        HIPCALL(h, hipEventRecord(h->ev_s1, h->stream));
+        HIPCALL(h, hipStreamWaitEvent(h->stream2, h->ev_s1, 0));
+    }
     auto copy_chunk = [&](long long item) -> hipError_t {
         const int a = (int)(item % arrays);
         const long long c0 = (item / arrays) * chunk;
@@ -1367,7 +1385,8 @@ int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n) 
         int *dp = (a == 0 ? h->d_stoa : h->d_spid) + off + c0;
         const int32_t *src = (a == 0 ? toa : pid) + c0;
         std::memcpy(hp, src, (size_t)cn * 4);
-        return hipMemcpyAsync(dp, hp, (size_t)cn * 4, hipMemcpyHostToDevice, h->stream);
+        return hipMemcpyAsync(dp, hp, (size_t)cn * 4, hipMemcpyHostToDevice,
+                              (two && ((item / arrays) & 1)) ? h->stream2 : h->stream);
     };
     if (workers <= 1) {
         for (long long it = 0; it < n_chunks * arrays; ++it) HIPCALL(h, copy_chunk(it));
@@ -1387,6 +1406,10 @@ int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n) 
         work();
         for (auto &t : pool) t.join();
         HIPCALL(h, (hipError_t)err.load());
+    }
+    if (two) {
+        HIPCALL(h, hipEventRecord(h->ev_s2, h->stream2));
+        HIPCALL(h, hipStreamWaitEvent(h->stream, h->ev_s2, 0));
     }
     HIPCALL(h, hipEventRecord(h->pin_done, h->stream));
     h->pin_pending = true;
