@@ -63,70 +63,106 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(inst, pixel_screen, seconds: float) -> dict:
-    """Time the CPU restatement of the scipp pipeline on the host cores.
+def cpu_baseline(inst, ps, view, pid_h, toa_h, replica, gpu_hist, seconds: float) -> dict:
+    """Time the CPU restatement of the scipp pipeline on the host cores, on the
+    very batch the GPU binned, and check the GPU's histogram against it.
 
     Main figure: oracle/binning_ref.c (group -> project -> hist -> +=, OpenMP
-    over the host cores, the way scipp's TBB kernels run).  The single-thread
-    NumPy oracle is reported beside it.
+    over the host cores, the way scipp's TBB kernels run) over the whole step
+    batch (1.4e8 events) with this step's replica, repeated until ``seconds``
+    of CPU work.  Its first pass is also the parity check of the GPU's current
+    histogram for that step (bit-exact).  The single-thread NumPy oracle is
+    timed beside it on a 4e6-event slice of the same batch.
     """
-    from esslivedata_amd import synthetic
     from oracle import c_oracle
     from oracle import scipp_semantics as ora
 
-    threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
-    threads = max(1, min(threads, 16))
-    n = 4_000_000
-    gen = (lambda s: synthetic.dream_events(n, inst, seed=s)) if inst.name == 'dream_mantle' else (
-        lambda s: synthetic.uniform_events(n, 1, 802816, seed=s))
-    batches = [gen(s) for s in (1, 2, 3)]
-    c = c_oracle.CDetectorView(inst.detector_number, pixel_screen,
-                               int(np.prod(list(inst.resolution.values()))),
-                               inst.edges.edges_ns(), threads=threads)
+    # threads: the box's CPU share (OMP_NUM_THREADS, set by the harness), else
+    # every core this process may run on
+    visible = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or visible
+    c = c_oracle.CDetectorView(inst.detector_number, ps, view.n_screen, inst.edges.edges_ns(),
+                               threads=threads)
+    n = len(pid_h)
     done, t_total, k = 0, 0.0, 0
-    while t_total < seconds and k < 400:
-        pid, toa = batches[k % 3]
+    bit_exact = None
+    while (t_total < seconds and k < 50) or k == 0:
         t0 = time.perf_counter()
-        c.accumulate(pid, toa, k % pixel_screen.shape[0])
+        c.accumulate(pid_h, toa_h, replica)
         t_total += time.perf_counter() - t0
+        if k == 0:
+            ref = c.hist.reshape(gpu_hist.shape)
+            bit_exact = bool(np.array_equal(ref.astype(np.float64), gpu_hist))
+            ref_total = int(ref.sum())
         done += n
         k += 1
+    m = min(n, 4_000_000)
     o = ora.OracleDetectorView(
-        detector_number=inst.detector_number, pixel_screen=pixel_screen,
-        screen_shape=tuple(inst.resolution.values()), toa_edges_ns=inst.edges.edges_ns())
+        detector_number=inst.detector_number, pixel_screen=ps,
+        screen_shape=tuple(view.screen_shape), toa_edges_ns=inst.edges.edges_ns())
     t0 = time.perf_counter()
-    for j in range(2):
-        o.accumulate(*batches[j])
+    o.batch_histogram(pid_h[:m], toa_h[:m], replica)
     t_np = time.perf_counter() - t0
     return {
         'value': done / t_total,
         'unit': 'events/s',
         'cores': c.threads_used,
+        'cpus_visible': visible,
         'kind': 'port',
-        'sample': f'{k} batches x {n} events of the same workload (3 distinct seeded batches, '
-        f'cycling replicas) through oracle/binning_ref.c with {c.threads_used} OpenMP threads, '
-        f'{t_total:.1f} s; NumPy oracle (1 core): {2 * n / t_np:.3e} events/s',
-        'numpy_1core': 2 * n / t_np,
+        'sample': f'{k} passes over the bench step batch ({n} events, replica {replica}) through '
+        f'oracle/binning_ref.c with {c.threads_used} OpenMP threads, {t_total:.1f} s; NumPy oracle '
+        f'(1 core) on {m} events of it: {m / t_np:.3e} events/s',
+        'numpy_1core': m / t_np,
+        'parity': {'events': n, 'replica': replica, 'bit_exact': bit_exact,
+                   'oracle_total': ref_total, 'gpu_total': int(gpu_hist.sum())},
     }
 
 
-def profiled_traffic(workload: str, kernel: str, events_per_launch: float):
+def _profile_entry(workload: str, kernel: str):
+    path = ROOT / 'profiles' / f'{PROFILE_ROUND}_{workload}_bench.json'
+    try:
+        return json.loads(path.read_text())[KERNEL_SYMBOL[kernel]], str(path.relative_to(ROOT))
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
+def profiled_traffic(workload: str, kernel: str):
     """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC
     summary of this same bench command (2 x FETCH_SIZE + WRITE_SIZE, the gfx950
     correction of MI355X_MICROARCH.md), or None when no profile is committed."""
-    path = ROOT / 'profiles' / f'{PROFILE_ROUND}_{workload}_bench.json'
-    try:
-        prof = json.loads(path.read_text())
-        e = prof[KERNEL_SYMBOL[kernel]]
-        return {
-            'bytes': e['hbm_traffic_bytes'],
-            'read': e['hbm_read_bytes'],
-            'write': e['hbm_write_bytes'],
-            'profiled_avg_ms': e['avg_ms'],
-            'source': str(path.relative_to(ROOT)),
-        }
-    except (OSError, KeyError, ValueError):
+    e, src = _profile_entry(workload, kernel)
+    if e is None or 'hbm_traffic_bytes' not in e:
         return None
+    return {
+        'bytes': e['hbm_traffic_bytes'],
+        'read': e['hbm_read_bytes'],
+        'write': e['hbm_write_bytes'],
+        'profiled_avg_ms': e['avg_ms'],
+        'source': src,
+    }
+
+
+def profiled_lds(workload: str, kernel: str):
+    """LDS counters of ``kernel`` per launch from the committed profile, and the
+    LDS-atomic efficiency north_star asks for: the fraction of LDS-array cycles
+    that are not bank-conflict replays, 1 - SQ_LDS_BANK_CONFLICT /
+    SQ_LDS_IDX_ACTIVE (MI355X_MICROARCH.md 'LDS'); conflict cycles per LDS
+    instruction beside it."""
+    e, src = _profile_entry(workload, kernel)
+    pm = (e or {}).get('pmc_per_dispatch', {})
+    if 'SQ_INSTS_LDS' not in pm or 'SQ_LDS_BANK_CONFLICT' not in pm:
+        return None
+    out = {
+        'SQ_INSTS_LDS': pm['SQ_INSTS_LDS'],
+        'SQ_LDS_BANK_CONFLICT': pm['SQ_LDS_BANK_CONFLICT'],
+        'SQ_LDS_IDX_ACTIVE': pm.get('SQ_LDS_IDX_ACTIVE'),
+        'conflict_cycles_per_lds_inst': pm['SQ_LDS_BANK_CONFLICT'] / max(pm['SQ_INSTS_LDS'], 1.0),
+        'efficiency': None,
+        'source': src,
+    }
+    if pm.get('SQ_LDS_IDX_ACTIVE'):
+        out['efficiency'] = 1.0 - pm['SQ_LDS_BANK_CONFLICT'] / pm['SQ_LDS_IDX_ACTIVE']
+    return out
 
 
 def main():
@@ -279,6 +315,7 @@ def main():
     total_events = n_step * args.steps * world
     value = total_events / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
+    step_gbs = (BYTES_PER_EVENT * n_step + 4 * nbins) * world / (ms_per_step / 1e3) / 1e9
 
     # dominant kernel and its roofline (HIP events of the timed region)
     ms, launches = timed[dom]
@@ -287,7 +324,7 @@ def main():
     alg_bytes = BYTES_PER_EVENT * events_per_launch
     avg_s = (ms / max(launches, 1)) / 1e3
     achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
-    traffic = profiled_traffic(args.workload, dom, events_per_launch)
+    traffic = profiled_traffic(args.workload, dom)
     bin_ms, bin_n = timed['binning']
     pipeline_gbs = BYTES_PER_EVENT * n_step / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0
 
@@ -330,6 +367,11 @@ def main():
             'launches': launches,
             'pipeline_achieved': pipeline_gbs,
             'pipeline_frac': pipeline_gbs / HBM_PEAK_GBS,
+            # whole step (incl. finalize and host gaps): SURVEY 8(d)'s
+            # (8 N + 4 S T) bytes per step over ms_per_step
+            'step_achieved': step_gbs,
+            'step_frac': step_gbs / HBM_PEAK_GBS,
+            'lds': profiled_lds(args.workload, dom),
             'kernel_ms': {k: v[0] / max(v[1], 1) for k, v in stats.items() if v[1]},
             'kernel_ms_note': 'per-kernel breakdown from 3 extra steps after the timed region',
         },
@@ -337,14 +379,21 @@ def main():
     if e2e is not None:
         result['end_to_end'] = e2e
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # CPU baseline + parity leg: one more GPU step with the full current
+        # histogram read back, then the oracle over the same batch
         from oracle import scipp_semantics as ora
 
-        coords = dict(inst.coords)
-        if args.workload == 'loki':
-            coords['x'] = -coords['x']
-        edges_s = {d: ora.screen_edges(coords[d], r) for d, r in inst.resolution.items()}
-        ps = np.stack([ora.geometric_screen_index(coords, edges_s, k) for k in range(view.n_replicas)])
-        result['cpu_baseline'] = cpu_baseline(inst, ps, args.cpu_baseline_seconds)
+        r_chk = (args.warmup + args.steps + 3) % view.n_replicas
+        eng.stage_tensors_batch(messages)
+        eng.accumulate(r_chk)
+        chk = eng.finalize(hists=True)
+        ps = ora.geometric_pixel_screen(inst.coords, inst.resolution, flip_x=args.workload == 'loki')
+        result['cpu_baseline'] = cpu_baseline(inst, ps, view, pid.cpu().numpy(), toa.cpu().numpy(),
+                                              r_chk, chk.current_hist, args.cpu_baseline_seconds)
+        result['check'] = {
+            'current_total': chk.current_total,
+            'bit_exact_vs_oracle': result['cpu_baseline']['parity']['bit_exact'],
+        }
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

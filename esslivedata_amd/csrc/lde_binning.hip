@@ -17,7 +17,8 @@
 //             binary search inside the bucket (any sorted edges).
 //
 // Strategies (bit-identical integer counts):
-//   ATOMIC    : one pass, one agent-scope u32 atomic per event.
+//   ATOMIC    : one pass, agent-scope u32 atomics, equal keys of a wave merged
+//               first (wave_add_aggregated).
 //   PARTITION : pass A partitions events into LDS-sized tiles of the (S, T)
 //               histogram (chunk-major tile-sorted runs, no global atomics);
 //               k_plan splits tiles into balanced work items; pass B
@@ -54,15 +55,14 @@ __global__ __launch_bounds__(256) void k_bin_atomic(const SegDesc seg, const LT 
             const v4i t = ld_stream4(seg.toa + 4 * i);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int k = event_key<LT, FAST>(p[q], t[q], lut, pid_off, L, smem, tp);
-                if (k >= 0) atomicAdd(hist + k, 1u);
+                wave_add_aggregated<4>(hist, event_key<LT, FAST>(p[q], t[q], lut, pid_off, L, smem, tp));
             }
         }
         tail = n4 << 2;
     }
     for (long long i = tail + i0; i < n; i += stride) {
-        const int k = event_key<LT, FAST>(ld_global(seg.pid + i), ld_global(seg.toa + i), lut, pid_off, L, smem, tp);
-        if (k >= 0) atomicAdd(hist + k, 1u);
+        wave_add_aggregated<4>(hist, event_key<LT, FAST>(ld_global(seg.pid + i), ld_global(seg.toa + i),
+                                                         lut, pid_off, L, smem, tp));
     }
 }
 

@@ -91,6 +91,28 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Global u32 += 1 for every active lane with k >= 0, equal keys of the wave
+// merged first (CDNA has no match_any): each of up to ROUNDS rounds takes the
+// lowest remaining lane's key and adds the number of lanes holding it with
+// one atomic; lanes still left add alone.  Zipf-hot bins then cost one
+// memory-side atomic per wave instead of one per event.  Safe under
+// divergence (ballots see active lanes only).
+template <int ROUNDS>
+__device__ __forceinline__ void wave_add_aggregated(uint32_t *hist, int k) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long act = __builtin_amdgcn_ballot_w64(k >= 0);
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        if (!act) return;
+        const int lead = __builtin_ctzll(act);
+        const int kl = __builtin_amdgcn_readlane(k, lead);
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(k == kl) & act;
+        if (lane == lead) atomicAdd(hist + kl, (uint32_t)__popcll(m));
+        act &= ~m;
+    }
+    if ((act >> lane) & 1ull) atomicAdd(hist + k, 1u);
+}
+
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
     const int lane = threadIdx.x & 63;
 #pragma unroll

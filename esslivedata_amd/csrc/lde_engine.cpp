@@ -1824,6 +1824,42 @@ int lde_import_window(lde_handle *h, const void *d_src) {
     return LDE_OK;
 }
 
+int lde_export_window_u64(lde_handle *h, void *d_dst) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!d_dst) return fail(h, LDE_EINVAL, "destination is NULL");
+    if (h->out_dtype == LDE_F32)
+        return fail(h, LDE_EINVAL, "u64 window export needs an integer-exact (float64) view");
+    DeviceGuard guard(h->device);
+    HIPCALL(h, lde::launch_sum3(h->win64_dirty ? h->d_win64 : nullptr, nullptr, h->d_win32,
+                                (unsigned long long *)d_dst, h->nbins, h->stream));
+    return LDE_OK;
+}
+
+int lde_import_window_u64(lde_handle *h, const void *d_src) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!d_src) return fail(h, LDE_EINVAL, "source is NULL");
+    if (h->out_dtype == LDE_F32)
+        return fail(h, LDE_EINVAL, "u64 window import needs an integer-exact (float64) view");
+    DeviceGuard guard(h->device);
+    if (int rc = ensure_win64(h)) return rc;
+    const size_t nb = (size_t)h->nbins;
+    HIPCALL(h, hipMemcpyAsync(h->d_win64, d_src, nb * 8, hipMemcpyDeviceToDevice, h->stream));
+    HIPCALL(h, hipMemsetAsync(h->d_win32, 0, nb * 4, h->stream));
+    // the merged counts live in the u64 part; the u32 part is empty again
+    h->win64_dirty = true;
+    h->win_events = 0;
+    h->window_has_data = true;
+    h->cum_has_data = true;
+    return LDE_OK;
+}
+
+int lde_get_stream(lde_handle *h, void **stream) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!stream) return fail(h, LDE_EINVAL, "stream is NULL");
+    *stream = (void *)h->stream;
+    return LDE_OK;
+}
+
 int lde_synchronize(lde_handle *h) {
     if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
     DeviceGuard guard(h->device);

@@ -10,9 +10,15 @@ binned every event (integer sums are order-independent):
   onto the root -- uint64 partial images (current, cumulative) and totals,
   2*S + 4 words (400 KB for DREAM) instead of the 10 MB window -- with one
   ``torch.distributed.reduce`` (backend ``nccl`` = RCCL over xGMI on ROCm).
-* ``WindowReducer``: sums the uint32 windows onto the root, which then
+* ``WindowReducer``: sums the windows onto the root as uint64 (exact in every
+  window state, also after a rank's u32 window folded into u64), which then
   finalizes as a single GPU would; needed when the full (S, T) histogram is
   published.
+
+Pixel-range (bank) sharding needs no collective: see :func:`assign_banks`.
+
+With the ``gloo`` backend (CPU tests, or ranks sharing one GPU) the device
+buffers travel through host copies, since gloo reduces host tensors.
 """
 
 from __future__ import annotations
@@ -38,57 +44,114 @@ def dist_env() -> tuple[int, int, int]:
     )
 
 
-class OutputReducer:
+def assign_banks(bank_sizes: dict[str, int], world: int) -> dict[str, int]:
+    """Pixel-range sharding (SURVEY 8(e) axis 2): each detector bank is its own
+    job/workflow (e.g. LOKI's 9 banks, config/instruments/loki/streams.py:17-27;
+    DREAM's 5, dream/streams.py:17-23), so banks are placed on devices whole and
+    need no collective.  Greedy longest-processing-time placement by expected
+    load (pixels, or events/s if known): largest bank first onto the least
+    loaded device; ties broken by device index, so the result is deterministic.
+    Returns ``{bank: device}``."""
+    if world < 1:
+        raise ValueError('world must be >= 1')
+    load = [0] * world
+    out: dict[str, int] = {}
+    for name, size in sorted(bank_sizes.items(), key=lambda kv: (-int(kv[1]), kv[0])):
+        if int(size) < 0:
+            raise ValueError(f'bank {name!r} has negative size')
+        d = min(range(world), key=lambda i: (load[i], i))
+        out[name] = d
+        load[d] += int(size)
+    return out
+
+
+class _Reducer:
+    """Reduce of one device buffer onto ``dst`` with stream ordering against
+    the engine: the engine's stream waits for the previous reduce before it
+    rewrites the buffer (RCCL runs the collective asynchronously)."""
+
+    def __init__(self, engine, buf, *, dst: int, group) -> None:
+        import torch.distributed as dist
+
+        self.engine = engine
+        self.buf = buf
+        self.dst = dst
+        self.group = group
+        self._host = buf.is_cuda and dist.get_backend(group) == 'gloo'
+        self._after = None  # event recorded after the last reduce
+
+    def _before_write(self) -> None:
+        if self._after is not None:
+            self.engine.wait_event(self._after)
+            self._after = None
+
+    def _reduce(self) -> bool:
+        import torch.distributed as dist
+
+        self.engine.synchronize()  # the engine may run on its own stream
+        root = dist.get_rank(self.group) == self.dst
+        if self._host:
+            hb = self.buf.cpu()
+            dist.reduce(hb, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group)
+            if root:
+                self.buf.copy_(hb)
+        else:
+            dist.reduce(self.buf, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group)
+        self._mark()
+        return root
+
+    def _mark(self) -> None:
+        """Record the point after torch's last use of the buffer."""
+        if self.buf.is_cuda:
+            import torch
+
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.buf.device))
+            self._after = ev
+
+
+class OutputReducer(_Reducer):
     """Sums every rank's finalize outputs onto the root (see module doc)."""
 
     def __init__(self, engine, device, *, dst: int = 0, group=None) -> None:
         import torch
 
-        self.engine = engine
-        self.dst = dst
-        self.group = group
         self.S = engine.n_screen
-        self.buf = torch.zeros(2 * self.S + 4, dtype=torch.int64, device=device)
+        super().__init__(engine, torch.zeros(2 * self.S + 4, dtype=torch.int64, device=device),
+                         dst=dst, group=group)
 
     def finalize(self):
         """Collective.  On the root: (current image, cumulative image, totals)
         as float64 numpy arrays and a list of 4 ints; elsewhere None."""
-        import torch.distributed as dist
-
+        self._before_write()
         self.engine.finalize_partials(self.buf.data_ptr())
-        self.engine.synchronize()  # the engine may run on its own stream
-        dist.reduce(self.buf, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group)
-        if dist.get_rank(self.group) != self.dst:
+        if not self._reduce():
             return None
         h = self.buf.cpu().numpy()
         S = self.S
         return h[:S].astype('float64'), h[S : 2 * S].astype('float64'), [int(x) for x in h[2 * S :]]
 
 
-class WindowReducer:
-    """Sums every rank's window into the root's window (SUM over uint32)."""
+class WindowReducer(_Reducer):
+    """Sums every rank's window into the root's window (uint64 SUM: exact for
+    any count and after a rank's u32 window has folded into u64)."""
 
     def __init__(self, engine, device, *, dst: int = 0, group=None) -> None:
         import torch
 
-        self.engine = engine
-        self.dst = dst
-        self.group = group
         n = engine.n_screen * engine.n_toa_bins
-        self.buf = torch.zeros(n, dtype=torch.int32, device=device)
+        super().__init__(engine, torch.zeros(n, dtype=torch.int64, device=device), dst=dst,
+                         group=group)
 
     def reduce(self) -> bool:
-        """Collective; returns True on the root (which now holds the merged window)."""
-        import torch.distributed as dist
-
-        self.engine.export_window(self.buf.data_ptr())
-        self.engine.synchronize()  # the engine may run on its own stream
-        dist.reduce(self.buf, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group)
-        root = dist.get_rank(self.group) == self.dst
-        if root:
-            if self.buf.is_cuda:
-                import torch
-
-                torch.cuda.synchronize(self.buf.device)  # reduce result before the engine's stream reads it
-            self.engine.import_window(self.buf.data_ptr())
+        """Collective; returns True on the root, which now holds the merged
+        window; the other ranks' windows are emptied (their counts moved)."""
+        self._before_write()
+        self.engine.export_window_u64(self.buf.data_ptr())
+        root = self._reduce()
+        if not root:
+            self.buf.zero_()  # this rank's counts now live on the root
+            self._mark()
+        self._before_write()  # the reduced buffer before the engine reads it
+        self.engine.import_window_u64(self.buf.data_ptr())
         return root

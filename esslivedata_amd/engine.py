@@ -29,6 +29,16 @@ class FinalizeResult:
     cumulative_in_range: int
 
 
+def _current_raw_stream(device_index: int) -> int:
+    """hipStream_t of torch's current stream (cheap: no Stream object)."""
+    import torch
+
+    try:
+        return int(torch._C._cuda_getCurrentRawStream(device_index))
+    except AttributeError:  # pragma: no cover - older torch
+        return int(torch.cuda.current_stream(device_index).cuda_stream)
+
+
 def _as_i32(a) -> np.ndarray:
     a = np.asarray(a)
     if a.dtype != np.int32:
@@ -98,8 +108,13 @@ class BinningEngine:
         check(rc, None)
         self._h = h
         self._lib = lib
+        self._device = int(device)
         self._keepalive: list = []
         self._n_groups: dict[int, int] = {}
+        sp = ctypes.c_void_p()
+        check(lib.lde_get_stream(h, ctypes.byref(sp)), h)
+        self._stream_ptr = int(sp.value or 0)
+        self._torch_stream = None  # torch view of the engine stream (lazy)
 
     # ------------------------------------------------------------------
     @classmethod
@@ -157,13 +172,61 @@ class BinningEngine:
             self._keepalive.append(keepalive)
         self._call(self._lib.lde_stage_device, pid_ptr, toa_ptr, int(n))
 
+    @property
+    def stream_ptr(self) -> int:
+        """The hipStream_t (as an int) the engine's kernels run on."""
+        return self._stream_ptr
+
+    def _order_after_producer(self, tensors) -> None:
+        """Device staging contract (include/lde.h, lde_stage_device): the
+        engine stream waits for the producing (torch current) stream, and the
+        caching allocator may not reuse the tensors' blocks before the engine
+        stream has passed the kernels the next accumulate enqueues."""
+        import torch
+
+        dev = tensors[0].device
+        cur = torch.cuda.current_stream(dev)
+        if cur.cuda_stream == self._stream_ptr:
+            return  # same stream: in order by construction
+        if dev.index != self._device:
+            raise ValueError(f'event tensors are on {dev}, the engine on device {self._device}')
+        if self._torch_stream is None:
+            self._torch_stream = torch.cuda.ExternalStream(self._stream_ptr, device=dev)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._torch_stream.wait_event(ev)
+        for t in tensors:
+            t.record_stream(self._torch_stream)
+
+    def wait_event(self, event) -> None:
+        """Make the engine stream wait for a ``torch.cuda.Event`` (no-op when
+        the engine runs on torch's current stream, which is ordered anyway)."""
+        import torch
+
+        dev = torch.device('cuda', self._device)
+        if _current_raw_stream(self._device) == self._stream_ptr:
+            return
+        if self._torch_stream is None:
+            self._torch_stream = torch.cuda.ExternalStream(self._stream_ptr, device=dev)
+        self._torch_stream.wait_event(event)
+
+    @staticmethod
+    def _check_event_tensor(t) -> None:
+        import torch
+
+        if t.dtype != torch.int32:
+            raise ValueError(f'device event tensors must be contiguous int32, got {t.dtype}')
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError('device event tensors must be contiguous int32 on the GPU')
+
     def stage_tensors(self, pid, toa) -> None:
         """Stage int32 torch tensors resident on this engine's device."""
         if pid is not None and pid.numel() != toa.numel():
             raise ValueError('pixel_id and time_of_arrival must have the same length')
-        for t in (pid, toa):
-            if t is not None and (t.dtype.itemsize != 4 or not t.is_contiguous()):
-                raise ValueError('device event tensors must be contiguous int32')
+        ts = [t for t in (pid, toa) if t is not None]
+        for t in ts:
+            self._check_event_tensor(t)
+        self._order_after_producer(ts)
         self.stage_device(
             None if pid is None else pid.data_ptr(), toa.data_ptr(), toa.numel(), (pid, toa)
         )
@@ -182,16 +245,18 @@ class BinningEngine:
         rows = []
         for pid, toa in messages:
             nn = toa.numel()
-            if (toa.dtype is not i32 and toa.dtype.itemsize != 4) or not toa.is_contiguous():
-                raise ValueError('device event tensors must be contiguous int32')
+            if toa.dtype is not i32 or not toa.is_contiguous() or not toa.is_cuda:
+                self._check_event_tensor(toa)
             if pid is None:
                 rows.append((0, toa.data_ptr(), nn))
                 continue
-            if (pid.dtype is not i32 and pid.dtype.itemsize != 4) or not pid.is_contiguous():
-                raise ValueError('device event tensors must be contiguous int32')
+            if pid.dtype is not i32 or not pid.is_contiguous() or not pid.is_cuda:
+                self._check_event_tensor(pid)
             if pid.numel() != nn:
                 raise ValueError('pixel_id and time_of_arrival must have the same length')
             rows.append((pid.data_ptr(), toa.data_ptr(), nn))
+        if _current_raw_stream(messages[0][1].device.index) != self._stream_ptr:
+            self._order_after_producer([t for m in messages for t in m if t is not None])
         ptrs = np.array(rows, dtype=np.int64).T.copy()
         self._call(self._lib.lde_stage_device_batch, n, ptrs[0].ctypes.data, ptrs[1].ctypes.data,
                    ptrs[2].ctypes.data)
@@ -249,6 +314,14 @@ class BinningEngine:
 
     def import_window(self, src_ptr: int) -> None:
         self._call(self._lib.lde_import_window, src_ptr)
+
+    def export_window_u64(self, dst_ptr: int) -> None:
+        """Window counts as uint64 [S*T] into device memory (any window state)."""
+        self._call(self._lib.lde_export_window_u64, dst_ptr)
+
+    def import_window_u64(self, src_ptr: int) -> None:
+        """Replace the window with uint64 [S*T] counts from device memory."""
+        self._call(self._lib.lde_import_window_u64, src_ptr)
 
     def synchronize(self) -> None:
         self._call(self._lib.lde_synchronize)

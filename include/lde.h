@@ -161,9 +161,17 @@ int lde_ev44_decode(const uint8_t *buf, int64_t len, lde_ev44_view *out);
 int lde_stage_ev44(lde_handle *h, const uint8_t *buf, int64_t len, int64_t kafka_timestamp_ms,
                    int32_t flags, int64_t *timestamp_ns);
 
-/* Stage events already resident in HBM.  No copy: the device buffers must
- * stay valid until the next lde_accumulate returns. */
+/* Stage events already resident in HBM.  No copy.  The engine orders nothing
+ * against other streams: the caller makes the handle's stream (lde_get_stream)
+ * wait for the work that produces the buffers, and keeps them allocated until
+ * the kernels the next lde_accumulate enqueues on that stream have completed
+ * (e.g. an event recorded on it after lde_accumulate).  The Python host does
+ * both (event wait + allocator stream recording) when the producer's stream
+ * is not the handle's. */
 int lde_stage_device(lde_handle *h, const void *d_pid, const void *d_toa, int64_t n);
+
+/* The hipStream_t the handle runs on (cfg->stream, or the one it created). */
+int lde_get_stream(lde_handle *h, void **stream);
 
 /* Stage a whole batch of device-resident messages in one call (the batch
  * ToNXevent_data.get hands over, to_nxevent_data.py:155-200): message i is
@@ -206,6 +214,13 @@ int lde_export_window(lde_handle *h, void *d_dst);
  * whose per-push rounding is order dependent). */
 int lde_finalize_partials(lde_handle *h, void *d_out);
 int lde_import_window(lde_handle *h, const void *d_src);
+/* Exact window merge in any window state (also after the uint32 window has
+ * folded into its uint64 part): export writes uint64 [S*T] window counts to
+ * caller device memory; import replaces the window with uint64 [S*T] counts
+ * (e.g. the RCCL sum of every rank's export).  Integer (float64) views only:
+ * LDE_EINVAL for f32 views. */
+int lde_export_window_u64(lde_handle *h, void *d_dst);
+int lde_import_window_u64(lde_handle *h, const void *d_src);
 
 /* Screen groupings: per-group TOA spectra summed on the device, replacing the
  * host-side reductions of the finalize outputs

@@ -149,6 +149,20 @@ def geometric_screen_index(
     return flat
 
 
+def geometric_pixel_screen(
+    coords: dict[str, np.ndarray], resolution: dict[str, int], flip_x: bool = False
+) -> np.ndarray:
+    """``(R, P)`` screen index per replica and pixel of a geometric view:
+    ``flip_x`` negates x (projectors.py:341-342), edges over all replicas
+    (:344-350), dims in ``resolution`` order."""
+    c = dict(coords)
+    if flip_x and 'x' in c:
+        c['x'] = -np.asarray(c['x'])
+    edges = {d: screen_edges(c[d], r) for d, r in resolution.items()}
+    n_rep = np.asarray(next(iter(c.values()))).shape[0]
+    return np.stack([geometric_screen_index(c, edges, k) for k in range(n_rep)])
+
+
 def logical_screen_index(
     detector_shape: Sequence[int],
     transform: Callable[[np.ndarray], np.ndarray] | None,

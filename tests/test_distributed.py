@@ -21,18 +21,24 @@ class _HostEngine:
     def __init__(self, n_screen, edges):
         self.n_screen, self.n_toa_bins = n_screen, len(edges) - 1
         self.edges = edges
-        self.window = np.zeros(n_screen * self.n_toa_bins, dtype=np.int32)
+        self.window = np.zeros(n_screen * self.n_toa_bins, dtype=np.int64)
 
     def bin(self, pid, toa):
         pix = ora.pixel_index(pid, np.arange(1, self.n_screen + 1))
         h = ora.detector_histogram(np.arange(self.n_screen), self.n_screen, pix, toa, self.edges)
-        self.window += h.ravel().astype(np.int32)
+        self.window += h.ravel().astype(np.int64)
 
-    def export_window(self, ptr):
-        ctypes.memmove(ptr, self.window.ctypes.data, self.window.nbytes)
+    def export_window_u64(self, ptr):
+        w = self.window.astype(np.int64)
+        ctypes.memmove(ptr, w.ctypes.data, w.nbytes)
 
-    def import_window(self, ptr):
-        ctypes.memmove(self.window.ctypes.data, ptr, self.window.nbytes)
+    def import_window_u64(self, ptr):
+        w = np.zeros(self.window.shape, dtype=np.int64)
+        ctypes.memmove(w.ctypes.data, ptr, w.nbytes)
+        self.window = w
+
+    def wait_event(self, ev):
+        pass
 
     # OutputReducer interface: u64 [S] current image | [S] cumulative | [4] totals
     cum = None
@@ -79,12 +85,17 @@ def _worker(rank, world, port, q):
         eng = _HostEngine(64, edges)
         lo, hi = shard_bounds(n, rank, world)
         eng.bin(pid[lo:hi], toa[lo:hi])
+        # a bin beyond 2^32 on every rank: the int64 reduce stays exact
+        eng.window[5] += 3 * 2**32
         red = WindowReducer(eng, torch.device('cpu'))
         root = red.reduce()
         if root:
             full = _HostEngine(64, edges)
             full.bin(pid, toa)
+            full.window[5] += world * 3 * 2**32
             q.put(bool(np.array_equal(eng.window, full.window)) and int(eng.window.sum()) > 0)
+        else:
+            q.put(not eng.window.any())  # this rank's counts moved to the root
     finally:
         dist.destroy_process_group()
 
@@ -170,4 +181,25 @@ def test_gloo_world2_window_reduce_is_exact():
     for p in procs:
         p.join(120)
     assert all(p.exitcode == 0 for p in procs)
-    assert q.get(timeout=5) is True
+    assert q.get(timeout=5) is True and q.get(timeout=5) is True
+
+
+def test_assign_banks_loki_dream():
+    from esslivedata_amd.distributed import assign_banks
+
+    # LOKI's 9 banks: pixel-id ranges of config/instruments/loki/streams.py:17-27
+    ranges = [(1, 802816), (802817, 1032192), (1032193, 1204224), (1204225, 1433600),
+              (1433601, 1605632), (1605633, 2007040), (2007041, 2465792), (2465793, 2752512),
+              (2752513, 3211264)]
+    loki = {f'loki_detector_{i}': b - a + 1 for i, (a, b) in enumerate(ranges)}
+    for world in (1, 2, 4, 8):
+        a = assign_banks(loki, world)
+        assert set(a) == set(loki) and set(a.values()) <= set(range(world))
+        load = [sum(loki[b] for b, d in a.items() if d == k) for k in range(world)]
+        # LPT bound: no device above max(largest bank, mean + largest bank)
+        assert max(load) <= max(max(loki.values()), sum(loki.values()) / world + max(loki.values()))
+        if world >= len(loki):
+            assert len(set(a.values())) == len(loki)
+    assert assign_banks(loki, 3) == assign_banks(dict(reversed(list(loki.items()))), 3)
+    with pytest.raises(ValueError):
+        assign_banks(loki, 0)

@@ -421,3 +421,72 @@ def test_split_many_device_messages(n_msgs, karg, monkeypatch):
     assert eng.info()['last_strategy'] == 'split'
     np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
     np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
+
+
+def test_side_stream_producer_is_ordered_and_kept_alive():
+    """events produced on another torch stream with a
+    non-blocking copy behind a slow kernel, staged, and dropped right after
+    accumulate while new allocations on that stream reuse their blocks.  The
+    engine (own stream) must wait for the producer and the allocator must not
+    hand the blocks out before the engine's kernels are done."""
+    import torch
+
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.dream_mantle()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    o = ora.OracleDetectorView(detector_number=inst.detector_number,
+                               pixel_screen=_oracle_pixel_screen_geometric(inst),
+                               screen_shape=(80, 320), toa_edges_ns=edges)
+    for strategy in ('split', 'atomic'):
+        eng = _engine(view, edges, strategy)  # engine-owned stream
+        side = torch.cuda.Stream()
+        slow = torch.randn(4096, 4096, device='cuda')
+        for batch in range(3):
+            pid, toa = synthetic.dream_events(2_000_000 if strategy == 'split' else 200_000, inst,
+                                              seed=300 + batch)
+            hp = torch.from_numpy(pid).pin_memory()
+            ht = torch.from_numpy(toa).pin_memory()
+            with torch.cuda.stream(side):
+                for _ in range(8):  # keep the producer stream busy
+                    slow = slow @ slow
+                    slow /= slow.abs().max()
+                dp = hp.to('cuda', non_blocking=True)
+                dt = ht.to('cuda', non_blocking=True)
+                if batch == 2:
+                    eng.stage_tensors_batch([(dp[:777], dt[:777]), (dp[777:], dt[777:])])
+                else:
+                    eng.stage_tensors(dp, dt)
+                del dp, dt
+                eng.accumulate(batch)
+                junk = [torch.full((len(pid),), -5, dtype=torch.int32, device='cuda')
+                        for _ in range(4)]  # may reuse the staged blocks
+                del junk
+            got = eng.finalize(hists=True).current_hist
+            np.testing.assert_array_equal(got, o.batch_histogram(pid, toa, batch))
+        eng.close()
+
+
+def test_device_tensors_must_be_int32():
+    """float32 / uint32 / int64 tensors are refused, not
+    reinterpreted as int32 bits."""
+    import torch
+
+    from esslivedata_amd import projection
+
+    dn = np.arange(1, 65, dtype=np.int32)
+    view = projection.logical_lut(dn)
+    eng = _engine(view, np.linspace(0, 100, 11))
+    ok = torch.arange(10, dtype=torch.int32, device='cuda')
+    for bad in (torch.float32, torch.int64, torch.uint32, torch.int16):
+        b = torch.arange(10, device='cuda').to(bad)
+        with pytest.raises(ValueError):
+            eng.stage_tensors(ok, b)
+        with pytest.raises(ValueError):
+            eng.stage_tensors(b, ok)
+        with pytest.raises(ValueError):
+            eng.stage_tensors_batch([(ok, ok), (b, ok)])
+    with pytest.raises(ValueError):
+        eng.stage_tensors(ok.cpu(), ok.cpu())
+    assert eng.info()['staged'] == 0
