@@ -69,6 +69,7 @@ EXPORTED_SYMBOLS = (
     'lde_export_window_u64',
     'lde_import_window_u64',
     'lde_get_stream',
+    'lde_set_lut',
     'lde_synchronize',
     'lde_timing_enable',
     'lde_timing_select',
@@ -140,6 +141,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_export_window_u64': (ctypes.c_int, [H, P]),
         'lde_import_window_u64': (ctypes.c_int, [H, P]),
         'lde_get_stream': (ctypes.c_int, [H, ctypes.POINTER(ctypes.c_void_p)]),
+        'lde_set_lut': (ctypes.c_int, [H, P]),
         'lde_synchronize': (ctypes.c_int, [H]),
         'lde_set_groups': (ctypes.c_int, [H, i32, i64, P, P]),
         'lde_group_spectra': (ctypes.c_int, [H, i32, i32, P]),

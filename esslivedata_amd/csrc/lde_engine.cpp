@@ -950,6 +950,36 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
     return LDE_OK;
 }
 
+// validate the host LUT and copy it into the device format (allocated once)
+int upload_lut(lde_handle *h, const int32_t *out_lut) {
+    const long long n = (long long)h->R * h->L;
+    std::vector<uint16_t> l16;
+    std::vector<int> l32;
+    if (h->lut16) l16.resize((size_t)n); else l32.resize((size_t)n);
+    for (long long i = 0; i < n; ++i) {
+        const int v = out_lut[i];
+        if (v < -1 || v >= h->S)
+            return fail(h, LDE_EINVAL, "out_lut[%lld] = %d outside [-1, %lld)", i, v, h->S);
+        if (h->lut16) l16[(size_t)i] = v < 0 ? (uint16_t)0xFFFF : (uint16_t)v;
+        else l32[(size_t)i] = v < 0 ? -1 : (int)((long long)v * h->T);
+    }
+    const size_t bytes = (size_t)n * (h->lut16 ? 2 : 4);
+    if (!h->d_lut) {
+        if (h->lut16) {
+            if (int rc = dev_alloc(h, (uint16_t **)&h->d_lut, (size_t)n)) return rc;
+        } else {
+            if (int rc = dev_alloc(h, (int **)&h->d_lut, (size_t)n)) return rc;
+        }
+    }
+    // the previous batch's kernels may still read the old table
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    HIPCALL(h, hipMemcpy(h->d_lut, h->lut16 ? (const void *)l16.data() : (const void *)l32.data(),
+                         bytes, hipMemcpyHostToDevice));
+    // every replica's hot set / SIEVE tables derive from the LUT: rebuild lazily
+    for (auto &u : h->hot_uses) u = -1;
+    return LDE_OK;
+}
+
 int ensure_win64(lde_handle *h) {
     if (h->d_win64) return LDE_OK;
     if (int rc = dev_alloc(h, &h->d_win64, (size_t)h->nbins)) return rc;
@@ -1161,29 +1191,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     // LUT: u16 screen index (0xFFFF = dropped) when S < 65535, else int32
     // screen*T premultiplied (-1 = dropped); validated here
     if (!monitor) {
-        const long long n = (long long)h->R * h->L;
         h->lut16 = h->S < 0xFFFF && env_ll("LDE_LUT32", 0) == 0;
-        std::vector<uint16_t> l16;
-        std::vector<int> l32;
-        if (h->lut16) l16.resize((size_t)n); else l32.resize((size_t)n);
-        for (long long i = 0; i < n; ++i) {
-            const int v = cfg->out_lut[i];
-            if (v < -1 || v >= h->S) {
-                int r = fail(h, LDE_EINVAL, "out_lut[%lld] = %d outside [-1, %lld)", i, v, h->S);
-                g_create_error = h->err;
-                release(h);
-                return r;
-            }
-            if (h->lut16) l16[(size_t)i] = v < 0 ? (uint16_t)0xFFFF : (uint16_t)v;
-            else l32[(size_t)i] = v < 0 ? -1 : (int)((long long)v * h->T);
-        }
-        if (h->lut16) {
-            CREATE_CHECK(dev_alloc(h, (uint16_t **)&h->d_lut, (size_t)n));
-            CREATE_HIP(hipMemcpy(h->d_lut, l16.data(), (size_t)n * 2, hipMemcpyHostToDevice));
-        } else {
-            CREATE_CHECK(dev_alloc(h, (int **)&h->d_lut, (size_t)n));
-            CREATE_HIP(hipMemcpy(h->d_lut, l32.data(), (size_t)n * 4, hipMemcpyHostToDevice));
-        }
+        CREATE_CHECK(upload_lut(h, cfg->out_lut));
     }
     CREATE_CHECK(dev_alloc(h, &h->d_tab, tab.size()));
     CREATE_HIP(hipMemcpy(h->d_tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
@@ -1851,6 +1860,14 @@ int lde_import_window_u64(lde_handle *h, const void *d_src) {
     h->window_has_data = true;
     h->cum_has_data = true;
     return LDE_OK;
+}
+
+int lde_set_lut(lde_handle *h, const int32_t *out_lut) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (h->monitor) return fail(h, LDE_EINVAL, "a monitor handle has no LUT");
+    if (!out_lut) return fail(h, LDE_EINVAL, "out_lut is NULL");
+    DeviceGuard guard(h->device);
+    return upload_lut(h, out_lut);
 }
 
 int lde_get_stream(lde_handle *h, void **stream) {

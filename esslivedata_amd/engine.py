@@ -301,6 +301,17 @@ class BinningEngine:
         self._keepalive.clear()
         self._call(self._lib.lde_clear)
 
+    def set_lut(self, out_lut: np.ndarray) -> None:
+        """Replace the pid -> screen LUT (same shape as at construction)."""
+        lut = np.ascontiguousarray(np.asarray(out_lut, dtype=np.int32))
+        if lut.ndim == 1:
+            lut = lut[None, :]
+        if self._lut is None or lut.shape != self._lut.shape:
+            raise ValueError(f'LUT shape {lut.shape} differs from the engine\'s '
+                             f'{None if self._lut is None else self._lut.shape}')
+        self._call(self._lib.lde_set_lut, lut.ctypes.data)
+        self._lut = lut
+
     def reset_cumulative(self) -> None:
         self._call(self._lib.lde_reset_cumulative)
 

@@ -96,20 +96,29 @@ def _compose(detector_number, pixel_screen: np.ndarray) -> tuple[int, np.ndarray
 def geometric_lut(
     detector_number: np.ndarray,
     coords: dict[str, np.ndarray],
-    resolution: dict[str, int],
+    resolution: dict[str, int] | None = None,
     *,
     flip_x: bool = False,
     unit: str = 'm',
+    edges: dict[str, np.ndarray] | None = None,
 ) -> ViewLUT:
     """LUT for a geometric view from per-replica projected coordinates.
 
     ``coords[dim]`` has shape ``(R, P)`` (replica, detector pixel), as produced
     by essreduce's ``make_xy_plane_coords`` / ``make_cylinder_mantle_coords``
-    on ``CalibratedPositionWithNoisyReplicas``.
+    on ``CalibratedPositionWithNoisyReplicas``.  Screen edges follow scipp's
+    rule for ``resolution`` (make_geometric_projector, projectors.py:344-350),
+    or are given explicitly (``GeometricProjector(coords, edges)``,
+    projectors.py:45-78), dims in dict order.
     """
     coords = {k: np.atleast_2d(np.asarray(v, dtype=np.float64)) for k, v in coords.items()}
     if flip_x and 'x' in coords:
         coords['x'] = -coords['x']
+    if edges is not None:
+        edges = {d: np.asarray(e, dtype=np.float64) for d, e in edges.items()}
+        resolution = {d: len(e) - 1 for d, e in edges.items()}
+    if resolution is None:
+        raise ValueError('geometric_lut needs a resolution or explicit edges')
     dims = tuple(resolution)
     p = int(np.asarray(detector_number).size)
     for d in dims:
@@ -117,7 +126,8 @@ def geometric_lut(
             raise ValueError(f'no projected coordinate for screen dim {d!r}')
         if coords[d].shape[1] != p:
             raise ValueError(f'coordinate {d!r} has {coords[d].shape[1]} pixels, expected {p}')
-    edges = {d: scipp_hist_edges(coords[d], resolution[d]) for d in dims}
+    if edges is None:
+        edges = {d: scipp_hist_edges(coords[d], resolution[d]) for d in dims}
     shape = tuple(int(resolution[d]) for d in dims)
     r = coords[dims[0]].shape[0]
     pixel_screen = np.empty((r, p), dtype=np.int64)

@@ -17,10 +17,10 @@ follow the reference's instrument configs and fakes:
 * BIFROST unified detector: pids 1..13500 folded (arc 5, tube 3, channel 9,
   pixel 100) (bifrost/streams.py:46-48), logical 15 x 900, float32.
 
-Projected per-replica coordinates stand in for essreduce's
-``make_cylinder_mantle_coords`` / ``make_xy_plane_coords`` output; the engine
-takes them as input, exactly like the reference's own projector tests
-(tests/workflows/detector_view/projectors_test.py:19-51).
+Geometric views start from synthetic calibrated pixel positions and go
+through the restated essreduce projections and noise replicas
+(``geometry.GeometricSource``); ``Instrument.coords`` holds the projected
+per-replica coordinates the LUT is built from.
 """
 
 from __future__ import annotations
@@ -40,55 +40,67 @@ class Instrument:
     resolution: dict[str, int] | None
     edges: TOAEdges
     out_dtype: str = 'float64'
+    positions: np.ndarray | None = None  # (P, 3) calibrated pixel positions (m)
+    projection_type: str | None = None
+    pixel_noise: object = None
 
 
 def dream_mantle(n_replicas: int = 5, seed: int = 7) -> Instrument:
-    rng = np.random.default_rng(seed)
+    """DREAM mantle: 1280 x 384 pixels on a cylinder of radius 1.1 m about the
+    beam (z) axis, projected with the restated ``cylinder_mantle_z`` and sigma
+    = 4 mm gaussian noise replicas (dream/factories.py:56-66) through
+    ``geometry.GeometricSource``."""
+    from .geometry import GeometricSource, PixelNoise
+
     first, last = 229377, 720896
-    p = last - first + 1  # 491520
     n_phi, n_z = 1280, 384
     phi = np.linspace(-2.4, 2.4, n_phi)
     zz = np.linspace(-0.8, 0.8, n_z)
     pp, zz2 = np.meshgrid(phi, zz, indexing='ij')
     radius = 1.1
-    x = radius * np.cos(pp).ravel()
-    y = radius * np.sin(pp).ravel()
-    z = zz2.ravel()
-    arcs, zs = [], []
-    for r in range(n_replicas):
-        s = 0.0 if r == 0 else 0.004
-        xn = x + rng.normal(0, s, p) if s else x
-        yn = y + rng.normal(0, s, p) if s else y
-        zn = z + rng.normal(0, s, p) if s else z
-        arcs.append(np.hypot(xn, yn) * np.arctan2(yn, xn))
-        zs.append(zn)
+    pos = np.stack([radius * np.cos(pp).ravel(), radius * np.sin(pp).ravel(), zz2.ravel()], -1)
+    dn = np.arange(first, last + 1, dtype=np.int32)
+    res = {'arc_length': 80, 'z': 320}
+    noise = PixelNoise(sigma=0.004, replicas=n_replicas - 1, seed=seed) if n_replicas > 1 else None
+    src = GeometricSource(dn, pos, projection_type='cylinder_mantle_z', resolution=res,
+                          pixel_noise=noise)
     return Instrument(
         name='dream_mantle',
-        detector_number=np.arange(first, last + 1, dtype=np.int32),
-        coords={'arc_length': np.stack(arcs), 'z': np.stack(zs)},
-        resolution={'arc_length': 80, 'z': 320},
+        detector_number=dn,
+        coords=src.coords(),
+        resolution=res,
         edges=TOAEdges(start=0.5, stop=ESS_PULSE_PERIOD_MS, num_bins=100, scale='log'),
+        positions=pos,
+        projection_type='cylinder_mantle_z',
+        pixel_noise=noise,
     )
 
 
 def loki_bank0(n_replicas: int = 5, seed: int = 42) -> Instrument:
-    rng = np.random.default_rng(seed)
+    """LOKI bank 0: 896 x 896 pixels on a plane 5 m downstream, projected with
+    the restated ``xy_plane`` and cylindrical-pixel noise replicas
+    (loki/factories.py:101-121: straw pixels along x)."""
+    from .geometry import GeometricSource, PixelNoise
+
     p = 802816
     side = 896
     xs = np.linspace(-0.5, 0.5, side)
     xx, yy = np.meshgrid(xs, xs, indexing='ij')
-    x, y = xx.ravel(), yy.ravel()
-    cx, cy = [], []
-    for r in range(n_replicas):
-        s = 0.0 if r == 0 else 0.002
-        cx.append(x + (rng.normal(0, s, p) if s else 0))
-        cy.append(y + (rng.uniform(-s, s, p) if s else 0))
+    pos = np.stack([xx.ravel(), yy.ravel(), np.full(p, 5.0)], -1)
+    dn = np.arange(1, p + 1, dtype=np.int32)
+    res = {'y': 144, 'x': 144}
+    noise = (PixelNoise(cylinder_axis=(1.0 / side, 0.0, 0.0), cylinder_radius=0.5 / side,
+                        replicas=n_replicas - 1, seed=seed) if n_replicas > 1 else None)
+    src = GeometricSource(dn, pos, projection_type='xy_plane', resolution=res, pixel_noise=noise)
     return Instrument(
         name='loki_bank0',
-        detector_number=np.arange(1, p + 1, dtype=np.int32),
-        coords={'x': np.stack(cx), 'y': np.stack(cy)},
-        resolution={'y': 144, 'x': 144},
+        detector_number=dn,
+        coords=src.coords(),
+        resolution=res,
         edges=TOAEdges(),
+        positions=pos,
+        projection_type='xy_plane',
+        pixel_noise=noise,
     )
 
 

@@ -23,7 +23,7 @@ Semantics mirrored:
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Any, Callable, Iterable, Mapping, Sequence
+from typing import TYPE_CHECKING, Any, Callable, Iterable, Mapping, Sequence
 
 import numpy as np
 
@@ -32,6 +32,9 @@ from .edges import TOAEdges, convert_time, label_slice
 from .engine import BinningEngine
 from .preprocessors import DetectorEvents, MonitorEvents, StagedEvents, Timestamp
 from .projection import ViewLUT, geometric_lut, index_groups, logical_lut
+
+if TYPE_CHECKING:
+    from .geometry import GeometricSource
 from . import roi as _roi
 
 DETECTOR_TRANSFORM = 'detector_transform'
@@ -169,8 +172,16 @@ class GpuDetectorViewWorkflow:
         roi_support: bool = False,
         roi_keys: Mapping[str, str] | None = None,
         spectrum_view: SpectrumViewConfig | None = None,
+        geometry: 'GeometricSource | None' = None,
     ) -> None:
         self._source = source_name
+        # geometric views built from positions rebuild their LUT when the
+        # detector transform (the geometry signal) changes
+        self._geometry_src = geometry
+        if view is None:
+            if geometry is None:
+                raise ValueError('a view LUT or a geometry is required')
+            view = geometry.view()
         self._view = view
         self._params = params or DetectorViewParams()
         self._edges_unit = self._params.toa_edges.get_edges()
@@ -236,6 +247,8 @@ class GpuDetectorViewWorkflow:
         if self._start is None:
             self._start = start_time
         self._end = end_time
+        if self._geometry_src is not None and self._geometry.key in data:
+            self._move(data[self._geometry.key])
         if self._geometry.changed(data):
             self._engine.reset_cumulative()
         if self._roi_support:
@@ -249,6 +262,22 @@ class GpuDetectorViewWorkflow:
         replica = self._counter % self._view.n_replicas
         self._counter += 1
         self._engine.accumulate(replica)
+
+    def _move(self, transform) -> None:
+        """A detector-transform value: rebuild the projection and LUT from the
+        moved positions when it differs from the current placement (the
+        reference rebuilds its projector from the re-resolved positions)."""
+        geo = self._geometry_src
+        t = None if transform is None else np.asarray(getattr(transform, 'values', transform))
+        cur = geo.transform
+        if t is None or (cur is not None and np.array_equal(np.asarray(cur), t)):
+            return
+        geo.transform = t
+        view = geo.view()
+        if view.screen_shape != self._view.screen_shape or view.n_replicas != self._view.n_replicas:
+            raise ValueError('a detector move cannot change the view shape')
+        self._engine.set_lut(view.lut)
+        self._view = view
 
     def _update_rois(self, data: Mapping[str, Any]) -> None:
         """New ROI requests -> screen groups on the device (the reference's
@@ -367,14 +396,33 @@ class GpuDetectorViewFactory:
         detector_numbers: Mapping[str, np.ndarray],
         view_config: GeometricViewConfig | LogicalViewConfig | Mapping[str, Any],
         projected_coords: Mapping[str, Mapping[str, np.ndarray]] | None = None,
+        positions: Mapping[str, np.ndarray] | None = None,
+        pixel_shapes: Mapping[str, Mapping[str, Any]] | None = None,
+        transforms: Mapping[str, Any] | None = None,
         out_dtype: str = 'float64',
         device: int = 0,
     ) -> None:
         self._dn = dict(detector_numbers)
         self._cfg = view_config
         self._coords = dict(projected_coords or {})
+        # calibrated pixel positions (offsets in the component frame when a
+        # transform is given) -> projection + noise replicas (geometry.py)
+        self._positions = dict(positions or {})
+        self._pixel_shapes = dict(pixel_shapes or {})
+        self._transforms = dict(transforms or {})
         self._dtype = out_dtype
         self._device = device
+
+    def make_geometry(self, source_name: str) -> 'GeometricSource':
+        from .geometry import GeometricSource
+
+        cfg = self._config(source_name)
+        return GeometricSource(
+            np.asarray(self._dn[source_name]), self._positions[source_name],
+            projection_type=cfg.projection_type, resolution=cfg.resolution,
+            pixel_noise=cfg.pixel_noise, flip_x=cfg.flip_x,
+            pixel_shape=self._pixel_shapes.get(source_name),
+            transform=self._transforms.get(source_name))
 
     def _config(self, source: str):
         if isinstance(self._cfg, Mapping):
@@ -385,8 +433,10 @@ class GpuDetectorViewFactory:
         cfg = self._config(source_name)
         dn = np.asarray(self._dn[source_name])
         if isinstance(cfg, GeometricViewConfig):
+            if source_name in self._positions:
+                return self.make_geometry(source_name).view()
             if source_name not in self._coords:
-                raise ValueError(f'no projected coordinates for {source_name!r}')
+                raise ValueError(f'no positions or projected coordinates for {source_name!r}')
             return geometric_lut(dn, self._coords[source_name], cfg.resolution, flip_x=cfg.flip_x)
         if isinstance(cfg, LogicalViewConfig):
             tf = None if cfg.transform is None else (lambda a: cfg.transform(a, source_name))
@@ -400,10 +450,13 @@ class GpuDetectorViewFactory:
         # geometric views always support ROIs (factory.py:187); logical views per config
         roi_support = isinstance(cfg, GeometricViewConfig) or bool(cfg.roi_support)
         spectrum = cfg.spectrum_view if isinstance(cfg, LogicalViewConfig) else None
+        geometry = None
+        if isinstance(cfg, GeometricViewConfig) and source_name in self._positions:
+            geometry = self.make_geometry(source_name)
         return GpuDetectorViewWorkflow(
-            source_name, self.make_view(source_name), params, out_dtype=self._dtype,
-            device=self._device, roi_support=roi_support, roi_keys=aux_source_names,
-            spectrum_view=spectrum,
+            source_name, None if geometry is not None else self.make_view(source_name), params,
+            out_dtype=self._dtype, device=self._device, roi_support=roi_support,
+            roi_keys=aux_source_names, spectrum_view=spectrum, geometry=geometry,
         )
 
 

@@ -194,6 +194,13 @@ int lde_finalize(lde_handle *h, lde_outputs *out);
 /* Read a full histogram (LDE_CURRENT or LDE_CUMULATIVE) without finalizing. */
 int lde_read_histogram(lde_handle *h, int32_t which, void *host_out);
 
+/* Replace the pid -> screen LUT (same R, lut_len and n_screen as at create),
+ * e.g. rebuilt from moved pixel positions after a detector-transform change
+ * (geometry_signal.py:27-51; the projector is rebuilt with the geometry).
+ * out_lut as in lde_config.  Counts already binned are kept; the workflow
+ * resets them (lde_reset_cumulative) as the reference's accumulators do. */
+int lde_set_lut(lde_handle *h, const int32_t *out_lut);
+
 /* Reset semantics: clear both (workflow.clear / Job.reset) or drop the
  * cumulative and window because the geometry coord changed
  * (NoCopyAccumulator._reset_if_geometry_changed, accumulators.py:116-131). */

@@ -88,6 +88,147 @@ REFERENCE_KATS = [
     },
 ]
 
+
+
+def _fake_nexus_events(y_size: int, x_size: int, n_per_pixel: int) -> dict:
+    """Inputs of tests/workflows/detector_view/utils.py:13-60
+    (make_fake_nexus_detector_data): event ids repeat(arange(1, P + 1), n),
+    event_time_offset = default_rng(42).uniform(0, 71e6) ns.  numpy's
+    generator, so the values are the reference test's own; the engine's wire
+    type is int32 ns, so the TOAs are stored floored (all stay in 0..71 ms)."""
+    rng = np.random.default_rng(42)
+    p = y_size * x_size
+    eto = rng.uniform(0, 71_000_000, p * n_per_pixel)
+    return {'event_id': np.repeat(np.arange(1, p + 1), n_per_pixel).tolist(),
+            'toa': np.floor(eto).astype(np.int64).tolist()}
+
+
+def _screen_coords(n_pixels: int, screen_shape: tuple[int, int]) -> dict:
+    """projectors_test.py:19-54 (make_screen_coords_and_edges): two replicas,
+    x = pixel_x * scale + noise, y = pixel_y * scale + noise with the same
+    default_rng(42).normal(0, 0.1) noise for x and y of a replica."""
+    n_replicas = 2
+    det_side = int(np.sqrt(n_pixels))
+    scale_x = screen_shape[0] / det_side
+    scale_y = screen_shape[1] / det_side
+    pixel_y = np.arange(n_pixels) // det_side
+    pixel_x = np.arange(n_pixels) % det_side
+    rng = np.random.default_rng(42)
+    xs, ys = [], []
+    for _ in range(n_replicas):
+        noise = rng.normal(0, 0.1, n_pixels)
+        xs.append((pixel_x * scale_x + noise).tolist())
+        ys.append((pixel_y * scale_y + noise).tolist())
+    return {'screen_x': xs, 'screen_y': ys}
+
+
+def _windows_multiple_pushes() -> list[int]:
+    """accumulators_test.py:360-389: the number of pushes of each of the 10
+    windows, drawn with the test's own RNG consumption order
+    (default_rng(123): integers(1, 5) per window, random() per push)."""
+    rng = np.random.default_rng(seed=123)
+    out = []
+    for _ in range(10):
+        n = int(rng.integers(1, 5))
+        for _ in range(n):
+            rng.random()
+        out.append(n)
+    return out
+
+
+def reference_kats_r2() -> list[dict]:
+    ev44 = _fake_nexus_events(4, 4, 10)
+    flip_ev = _fake_nexus_events(2, 3, 50)
+    n_push = _windows_multiple_pushes()
+    win_exp, cum = [], [0, 0]
+    for n in n_push:
+        w = [sum(range(n)), sum(range(1, n + 1))]
+        win_exp.append(w)
+        cum = [cum[0] + w[0], cum[1] + w[1]]
+    return [
+        {
+            'name': 'projector_count_conservation',
+            'source': 'tests/workflows/detector_view/projectors_test.py:56-75',
+            'detector_number': list(range(1, 17)),
+            'events': ev44,
+            'coords': _screen_coords(16, (4, 4)),
+            'edges': {'screen_x': np.linspace(-1, 5, 10).tolist(),
+                      'screen_y': np.linspace(-1, 5, 10).tolist()},
+            'replica': 0,
+            'expected_total': 160,
+        },
+        {
+            'name': 'projector_replicas_differ',
+            'source': 'tests/workflows/detector_view/projectors_test.py:107-121',
+            'detector_number': list(range(1, 17)),
+            'events': ev44,
+            'coords': _screen_coords(16, (4, 4)),
+            'edges': {'screen_x': np.linspace(0, 4, 5).tolist(),
+                      'screen_y': np.linspace(0, 4, 5).tolist()},
+            'expected': 'screen counts of replica 0 and replica 1 differ',
+        },
+        {
+            'name': 'projector_flip_x_mirrors',
+            'source': 'tests/workflows/detector_view/projectors_test.py:124-178',
+            'detector_number': list(range(1, 7)),
+            'events': flip_ev,
+            'positions': np.stack([[-0.1, 0.0, 0.1, -0.1, 0.0, 0.1],
+                                   [-0.05, -0.05, -0.05, 0.05, 0.05, 0.05],
+                                   [2.0] * 6], axis=-1).tolist(),
+            'projection_type': 'xy_plane',
+            'resolution': {'x': 3, 'y': 2},
+            'expected': 'flipped[x=i] == normal[x=n-1-i] for every i; y edges identical',
+        },
+        {
+            'name': 'accumulator_window_accumulates',
+            'source': 'tests/preprocessors/accumulators_test.py:260-269',
+            'pushes': [[1, 2], [3, 4]],
+            'expected_window': [4, 6],
+        },
+        {
+            'name': 'accumulator_window_cleared_on_finalize',
+            'source': 'tests/preprocessors/accumulators_test.py:253-258, 271-276',
+            'pushes': [[1, 2]],
+            'expected': 'window empty after on_finalize; reading it raises ValueError',
+        },
+        {
+            'name': 'accumulator_pair_multiple_cycles',
+            'source': 'tests/preprocessors/accumulators_test.py:332-358',
+            'cycles': [[i, i + 1] for i in range(20)],
+            'expected_cumulative': [sum(range(20)), sum(range(1, 21))],
+        },
+        {
+            'name': 'accumulator_pair_multiple_pushes_per_window',
+            'source': 'tests/preprocessors/accumulators_test.py:360-389',
+            'note': 'window w receives pushes [j, j + 1] for j < n_pushes[w]',
+            'n_pushes': n_push,
+            'expected_windows': win_exp,
+            'expected_cumulative': cum,
+        },
+        {
+            'name': 'accumulator_reset_on_coord_change',
+            'source': 'tests/preprocessors/accumulators_test.py:427-463',
+            'cases': [
+                {'pushes': [[[1, 2], 0.0], [[3, 4], 0.0]], 'expected_cumulative': [4, 6]},
+                {'pushes': [[[1, 2], 0.0], [[3, 4], 1.0]], 'expected_cumulative': [3, 4]},
+                {'pushes': [[[1, 2], None], [[3, 4], None]], 'expected_cumulative': [4, 6]},
+                {'pushes': [[[1, 2], 0.0], [[3, 4], 1.0]], 'expected_window': [3, 4]},
+            ],
+        },
+        {
+            'name': 'monitor_full_workflow_cycle',
+            'source': 'tests/workflows/monitor_workflow_test.py:346-391',
+            'note': 'event_time_offset [1.5, 2.5, 3.5, 7.5, 8.5] ns in the test; the ev44 '
+                    'wire carries int32 ns, so floored here (same bins)',
+            'toa_ns': [1, 2, 3, 7, 8],
+            'edges_ns': np.linspace(0, 10, 11).tolist(),
+            'expected': {'cumulative_sum': 5.0, 'current_sum': 5.0, 'counts_total': 5.0,
+                         'counts_in_toa_range': 5.0, 'counts_total_cumulative': 5.0,
+                         'counts_in_toa_range_cumulative': 5.0},
+        },
+    ]
+
+
 # hand-derived: toa -> expected bin (-1 = dropped)
 TIE_KATS = [
     {
@@ -140,7 +281,8 @@ SCREEN_EDGE_KATS = [
 
 
 def main() -> None:
-    (HERE / 'reference_kats.json').write_text(json.dumps(REFERENCE_KATS, indent=1))
+    (HERE / 'reference_kats.json').write_text(
+        json.dumps(REFERENCE_KATS + reference_kats_r2(), indent=1))
     (HERE / 'tie_kats.json').write_text(
         json.dumps({'toa': TIE_KATS, 'screen': SCREEN_EDGE_KATS}, indent=1)
     )

@@ -1,0 +1,218 @@
+"""Reference KATs through the GPU workflow layer.
+
+Each case comes from ``tests/golden/reference_kats.json`` (the reference's own
+test inputs and expectations as data, file:line in each entry) and runs through
+``GpuDetectorViewWorkflow`` / ``GpuMonitorWorkflow`` /
+``GpuDetectorViewFactory`` -- i.e. the HIP engine -- and, where the KAT only
+states a property, also against the CPU oracle.
+"""
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import scipp_semantics as ora
+
+pytestmark = pytest.mark.gpu
+
+REF = {k['name']: k for k in json.loads(
+    (Path(__file__).resolve().parent / 'golden' / 'reference_kats.json').read_text())}
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu(engine_lib):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+
+
+def _t(ns):
+    from esslivedata_amd.preprocessors import Timestamp
+
+    return Timestamp.from_ns(ns)
+
+
+def _events(kat):
+    return (np.array(kat['events']['event_id'], dtype=np.int32),
+            np.array(kat['events']['toa'], dtype=np.int32))
+
+
+def _projector_workflow(kat):
+    from esslivedata_amd import projection
+    from esslivedata_amd.workflows import GpuDetectorViewWorkflow
+
+    coords = {d: np.array(v) for d, v in kat['coords'].items()}
+    edges = {d: np.array(v) for d, v in kat['edges'].items()}
+    view = projection.geometric_lut(np.array(kat['detector_number']), coords, edges=edges)
+    return GpuDetectorViewWorkflow('det', view), coords, edges
+
+
+def test_projector_count_conservation():
+    kat = REF['projector_count_conservation']
+    wf, coords, edges = _projector_workflow(kat)
+    wf.accumulate({'det': _events(kat)}, start_time=_t(0), end_time=_t(1))
+    out = wf.finalize()
+    assert float(out['counts_total'].values) == kat['expected_total']
+    assert float(out['current'].values.sum()) == kat['expected_total']
+
+
+def test_projector_replicas_differ_and_match_oracle():
+    kat = REF['projector_replicas_differ']
+    wf, coords, edges = _projector_workflow(kat)
+    pid, toa = _events(kat)
+    imgs = []
+    for r in range(2):  # the workflow cycles replicas per accumulate
+        wf.accumulate({'det': (pid, toa)}, start_time=_t(r), end_time=_t(r + 1))
+        img = wf.finalize()['current'].values
+        ps = ora.geometric_screen_index(coords, edges, r)
+        exp = ora.detector_histogram(ps, img.size, ora.pixel_index(pid, np.array(kat['detector_number'])),
+                                     toa, np.linspace(0, 71.43, 101) * 1e6).sum(-1)
+        np.testing.assert_array_equal(img.ravel(), exp)
+        imgs.append(img)
+    assert not np.array_equal(imgs[0], imgs[1])
+
+
+def test_flip_x_mirrors_through_factory_positions():
+    """projectors_test.py:140-178 through GpuDetectorViewFactory with calibrated
+    positions (geometry builder -> LUT -> engine)."""
+    from esslivedata_amd.workflows import GeometricViewConfig, GpuDetectorViewFactory
+
+    kat = REF['projector_flip_x_mirrors']
+    pid, toa = _events(kat)
+    imgs, y_edges = {}, {}
+    for flip in (False, True):
+        fac = GpuDetectorViewFactory(
+            detector_numbers={'det': np.array(kat['detector_number'])},
+            view_config=GeometricViewConfig(kat['projection_type'], kat['resolution'],
+                                            flip_x=flip),
+            positions={'det': np.array(kat['positions'])})
+        wf = fac.make_workflow('det')
+        wf.accumulate({'det': (pid, toa)}, start_time=_t(0), end_time=_t(1))
+        imgs[flip] = wf.finalize()['current'].values
+        y_edges[flip] = wf.view.screen_edges['y']
+    n_x = kat['resolution']['x']
+    assert imgs[False].shape == (n_x, kat['resolution']['y'])
+    for i in range(n_x):
+        np.testing.assert_array_equal(imgs[True][i], imgs[False][n_x - 1 - i])
+    np.testing.assert_array_equal(y_edges[False], y_edges[True])
+    assert imgs[False].sum() == 300
+
+
+def _pair_workflow():
+    """Two screens, one TOA bin: a pushed histogram [a, b] is a events of
+    pixel 1 and b events of pixel 2."""
+    from esslivedata_amd import projection
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.workflows import DetectorViewParams, GpuDetectorViewWorkflow
+
+    view = projection.logical_lut(np.array([1, 2], dtype=np.int32))
+    params = DetectorViewParams(toa_edges=TOAEdges(start=0.0, stop=10.0, num_bins=1, unit='ns'))
+    return GpuDetectorViewWorkflow('det', view, params)
+
+
+def _push(wf, vals, coord='absent', k=[0]):
+    k[0] += 1
+    pid = np.repeat(np.array([1, 2], dtype=np.int32), [int(vals[0]), int(vals[1])])
+    data = {'det': (pid, np.full(len(pid), 5, dtype=np.int32))}
+    if coord != 'absent':
+        data['detector_transform'] = coord
+    wf.accumulate(data, start_time=_t(k[0]), end_time=_t(k[0] + 1))
+
+
+def test_accumulator_kats_through_workflow():
+    kat = REF['accumulator_window_accumulates']
+    wf = _pair_workflow()
+    for p in kat['pushes']:
+        _push(wf, p)
+    np.testing.assert_array_equal(wf.finalize()['current'].values, kat['expected_window'])
+
+    wf = _pair_workflow()
+    _push(wf, REF['accumulator_window_cleared_on_finalize']['pushes'][0])
+    wf.finalize()
+    with pytest.raises(ValueError):
+        wf.finalize()  # the window is empty: reading it raises
+
+    kat = REF['accumulator_pair_multiple_cycles']
+    wf = _pair_workflow()
+    for h in kat['cycles']:
+        _push(wf, h)
+        out = wf.finalize()
+        np.testing.assert_array_equal(out['current'].values, h)
+    np.testing.assert_array_equal(out['cumulative'].values, kat['expected_cumulative'])
+
+    kat = REF['accumulator_pair_multiple_pushes_per_window']
+    wf = _pair_workflow()
+    for n, w in zip(kat['n_pushes'], kat['expected_windows']):
+        for j in range(n):
+            _push(wf, [j, j + 1])
+        out = wf.finalize()
+        np.testing.assert_array_equal(out['current'].values, w)
+    np.testing.assert_array_equal(out['cumulative'].values, kat['expected_cumulative'])
+
+    for case in REF['accumulator_reset_on_coord_change']['cases']:
+        wf = _pair_workflow()
+        for vals, coord in case['pushes']:
+            _push(wf, vals, 'absent' if coord is None else np.array(coord))
+        out = wf.finalize()
+        if 'expected_cumulative' in case:
+            np.testing.assert_array_equal(out['cumulative'].values, case['expected_cumulative'])
+        else:
+            np.testing.assert_array_equal(out['current'].values, case['expected_window'])
+
+
+def test_monitor_full_workflow_cycle():
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.workflows import GpuMonitorWorkflow
+
+    kat = REF['monitor_full_workflow_cycle']
+    e = np.array(kat['edges_ns'])
+    wf = GpuMonitorWorkflow('monitor_1', TOAEdges(start=e[0], stop=e[-1], num_bins=len(e) - 1,
+                                                  unit='ns'))
+    wf.build()
+    wf.accumulate({'monitor_1': (None, np.array(kat['toa_ns'], dtype=np.int32))},
+                  start_time=_t(0), end_time=_t(1000))
+    out = wf.finalize()
+    exp = kat['expected']
+    assert float(out['cumulative'].values.sum()) == exp['cumulative_sum']
+    assert float(out['current'].values.sum()) == exp['current_sum']
+    for k in ('counts_total', 'counts_in_toa_range', 'counts_total_cumulative',
+              'counts_in_toa_range_cumulative'):
+        assert float(out[k].values) == exp[k]
+
+
+def test_detector_move_rebuilds_lut_and_resets():
+    """geometry_signal.py:27-51 + accumulators.py:116-131: a new detector
+    transform re-projects the moved pixels (new LUT on the device) and drops
+    the cumulative; outputs match the oracle on the moved geometry."""
+    from esslivedata_amd import geometry, synthetic
+    from esslivedata_amd.workflows import GeometricViewConfig, GpuDetectorViewFactory
+
+    inst = synthetic.loki_bank0(n_replicas=1)
+    off = inst.positions - [0.0, 0.0, 5.0]
+    res = inst.resolution
+    fac = GpuDetectorViewFactory(
+        detector_numbers={'loki': inst.detector_number},
+        view_config=GeometricViewConfig('xy_plane', res, flip_x=True),
+        positions={'loki': off}, transforms={'loki': np.array([0.0, 0.0, 5.0])})
+    wf = fac.make_workflow('loki')
+    pid, toa = synthetic.uniform_events(2_000_000, 1, 802816, seed=9)
+    t0 = np.eye(4)
+    t0[2, 3] = 5.0
+    t1 = t0.copy()  # tilted 0.4 rad about y and shifted: perspective changes the image
+    c, s = np.cos(0.4), np.sin(0.4)
+    t1[:3, :3] = [[c, 0, s], [0, 1, 0], [-s, 0, c]]
+    t1[0, 3] = 0.7
+    for step, tr in enumerate([t0, t0, t1, t1]):
+        wf.accumulate({'loki': (pid, toa), 'detector_transform': tr}, start_time=_t(step),
+                      end_time=_t(step + 1))
+        out = wf.finalize()
+        pos = geometry.apply_transform(tr, off)
+        ps = ora.geometric_pixel_screen(geometry.make_xy_plane_coords(pos), res, flip_x=True)
+        exp = ora.detector_histogram(ps[0], 144 * 144, ora.pixel_index(pid, inst.detector_number),
+                                     toa, inst.edges.edges_ns()).sum(-1).reshape(144, 144)
+        np.testing.assert_array_equal(out['current'].values, exp)
+        n_since_move = 2 if step in (1, 3) else 1
+        np.testing.assert_array_equal(out['cumulative'].values, n_since_move * exp)

@@ -186,3 +186,104 @@ def test_rebin_kats_from_the_reference_monitor_tests():
     # partial overlaps: uniform density, outside the target range dropped
     got = ora.rebin(np.array([-1.0, 1.0, 3.0]), [2.0, 4.0], np.array([0.0, 2.0, 4.0]))
     np.testing.assert_array_equal(got, [1.0 + 2.0, 2.0])
+
+
+# ---------------------------------------------------------------------------
+# round 2: projector, accumulator and monitor-workflow KATs (reference tests
+# transcribed as data, tests/golden/make_golden.py:reference_kats_r2)
+# ---------------------------------------------------------------------------
+DEFAULT_TOA_NS = np.linspace(0, 71.43, 101) * 1e6
+
+
+def _projector_counts(kat, replica):
+    coords = {d: np.array(v) for d, v in kat['coords'].items()}
+    edges = {d: np.array(v) for d, v in kat['edges'].items()}
+    ps = ora.geometric_screen_index(coords, edges, replica)
+    pix = ora.pixel_index(np.array(kat['events']['event_id']), np.array(kat['detector_number']))
+    n = int(np.prod([len(e) - 1 for e in edges.values()]))
+    return ora.detector_histogram(ps, n, pix, np.array(kat['events']['toa']), DEFAULT_TOA_NS)
+
+
+def test_projector_count_conservation_kat():
+    kat = REF['projector_count_conservation']
+    assert _projector_counts(kat, kat['replica']).sum() == kat['expected_total']
+
+
+def test_projector_replicas_differ_kat():
+    kat = REF['projector_replicas_differ']
+    a = _projector_counts(kat, 0).sum(-1)
+    b = _projector_counts(kat, 1).sum(-1)
+    assert not np.array_equal(a, b)
+
+
+def test_projector_flip_x_kat_through_geometry_builder():
+    from esslivedata_amd import geometry
+
+    kat = REF['projector_flip_x_mirrors']
+    coords = geometry.make_xy_plane_coords(np.array(kat['positions']))
+    res = kat['resolution']
+    pix = ora.pixel_index(np.array(kat['events']['event_id']), np.array(kat['detector_number']))
+    imgs = {}
+    for flip in (False, True):
+        ps = ora.geometric_pixel_screen(coords, res, flip_x=flip)
+        h = ora.detector_histogram(ps[0], 6, pix, np.array(kat['events']['toa']), DEFAULT_TOA_NS)
+        imgs[flip] = h.sum(-1).reshape(res['x'], res['y'])
+    n_x = res['x']
+    for i in range(n_x):
+        np.testing.assert_array_equal(imgs[True][i], imgs[False][n_x - 1 - i])
+    assert imgs[False].sum() == 300
+    np.testing.assert_array_equal(ora.screen_edges(coords['y'], 2),
+                                  ora.screen_edges(geometry.make_xy_plane_coords(
+                                      np.array(kat['positions']))['y'], 2))
+
+
+def test_accumulator_pair_kats():
+    kat = REF['accumulator_window_accumulates']
+    acc = ora.AccumulatorPair()
+    for p in kat['pushes']:
+        acc.push(np.array(p, dtype=float))
+    np.testing.assert_array_equal(acc.window, kat['expected_window'])
+
+    acc = ora.AccumulatorPair()
+    acc.push(np.array(REF['accumulator_window_cleared_on_finalize']['pushes'][0], dtype=float))
+    acc.on_finalize()
+    assert acc.window is None
+
+    kat = REF['accumulator_pair_multiple_cycles']
+    acc = ora.AccumulatorPair()
+    for h in kat['cycles']:
+        acc.push(np.array(h, dtype=float))
+        np.testing.assert_array_equal(acc.window, h)
+        acc.on_finalize()
+    np.testing.assert_array_equal(acc.cumulative, kat['expected_cumulative'])
+
+    kat = REF['accumulator_pair_multiple_pushes_per_window']
+    acc = ora.AccumulatorPair()
+    for n, w in zip(kat['n_pushes'], kat['expected_windows']):
+        for j in range(n):
+            acc.push(np.array([j, j + 1], dtype=float))
+        np.testing.assert_array_equal(acc.window, w)
+        acc.on_finalize()
+    np.testing.assert_array_equal(acc.cumulative, kat['expected_cumulative'])
+
+    for case in REF['accumulator_reset_on_coord_change']['cases']:
+        acc = ora.AccumulatorPair()
+        for vals, coord in case['pushes']:
+            acc.push(np.array(vals, dtype=float), coord)
+        if 'expected_cumulative' in case:
+            np.testing.assert_array_equal(acc.cumulative, case['expected_cumulative'])
+        else:
+            np.testing.assert_array_equal(acc.window, case['expected_window'])
+
+
+def test_monitor_full_workflow_cycle_kat():
+    kat = REF['monitor_full_workflow_cycle']
+    o = ora.OracleMonitor(np.array(kat['edges_ns']))
+    o.accumulate(np.array(kat['toa_ns'], dtype=np.int32))
+    out = o.finalize()
+    exp = kat['expected']
+    assert out['cumulative'].sum() == exp['cumulative_sum']
+    assert out['current'].sum() == exp['current_sum']
+    for k in ('counts_total', 'counts_in_toa_range', 'counts_total_cumulative',
+              'counts_in_toa_range_cumulative'):
+        assert out[k] == exp[k]
