@@ -186,7 +186,10 @@ def main():
         inst.detector_number, inst.coords, inst.resolution, flip_x=args.workload == 'loki'
     )
     edges = inst.edges.edges_ns()
-    stream = torch.cuda.current_stream(dev)
+    # one non-default torch stream for the data generation, the engine and
+    # the collectives: everything in order on it, no cross-stream waits
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     eng = BinningEngine(
         toa_edges_ns=edges,
         out_lut=view.lut,

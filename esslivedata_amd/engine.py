@@ -62,7 +62,7 @@ class BinningEngine:
         strategy: str = 'auto',
         toa_range: tuple[int, int] | None = None,
         device: int = 0,
-        stream: int | None = None,
+        stream: int | None = None,  # hipStream_t; None/0: a torch pool stream
     ) -> None:
         lib = _native.lib()
         edges = np.ascontiguousarray(np.asarray(toa_edges_ns, dtype=np.float64))
@@ -78,7 +78,19 @@ class BinningEngine:
         cfg = _native.LdeConfig()
         cfg.abi_version = _native.ABI_VERSION
         cfg.device_id = int(device)
-        cfg.stream = ctypes.c_void_p(stream) if stream else None
+        # The engine runs on a torch stream: the caller's (a raw hipStream_t
+        # whose lifetime the caller guarantees) or, by default, a dedicated
+        # stream from torch's per-device pool.  Pool streams are never
+        # destroyed, so tensors staged from other streams can be recorded on
+        # it for the caching allocator (record_stream) and outlive the engine;
+        # an engine-created stream could not (lde_destroy destroys it).
+        self._torch_stream = None
+        if not stream:
+            import torch
+
+            self._torch_stream = torch.cuda.Stream(device=torch.device('cuda', int(device)))
+            stream = self._torch_stream.cuda_stream
+        cfg.stream = ctypes.c_void_p(stream)
         cfg.pid_offset = int(pid_offset)
         self._lut = None
         if out_lut is None:
@@ -114,7 +126,6 @@ class BinningEngine:
         sp = ctypes.c_void_p()
         check(lib.lde_get_stream(h, ctypes.byref(sp)), h)
         self._stream_ptr = int(sp.value or 0)
-        self._torch_stream = None  # torch view of the engine stream (lazy)
 
     # ------------------------------------------------------------------
     @classmethod

@@ -361,8 +361,8 @@ class GpuDetectorViewWorkflow:
             out['roi_rectangle'] = self._roi_readback('roi_rectangle')
             out['roi_polygon'] = self._roi_readback('roi_polygon')
         if self._start is not None:
-            st = Variable((), self._start.to_ns(), 'ns')
-            tt = Variable((), self._end.to_ns(), 'ns')
+            st = Variable((), np.datetime64(self._start.to_ns(), 'ns'), 'ns')
+            tt = Variable((), np.datetime64(self._end.to_ns(), 'ns'), 'ns')
             names = DETECTOR_WINDOW_OUTPUTS + (ROI_WINDOW_OUTPUTS if self._roi_support else ())
             for name in names:
                 out[name] = out[name].assign_coords(start_time=st, time=tt)
@@ -596,8 +596,8 @@ class GpuMonitorWorkflow:
         if self._hist_mode:
             out = self._finalize_histogram_mode()
             if self._start is not None:
-                st = Variable((), self._start.to_ns(), 'ns')
-                tt = Variable((), self._end.to_ns(), 'ns')
+                st = Variable((), np.datetime64(self._start.to_ns(), 'ns'), 'ns')
+                tt = Variable((), np.datetime64(self._end.to_ns(), 'ns'), 'ns')
                 for name in MONITOR_WINDOW_OUTPUTS:
                     out[name] = out[name].assign_coords(start_time=st, time=tt)
             self._start = self._end = None
@@ -614,8 +614,8 @@ class GpuMonitorWorkflow:
             ),
         }
         if self._start is not None:
-            st = Variable((), self._start.to_ns(), 'ns')
-            tt = Variable((), self._end.to_ns(), 'ns')
+            st = Variable((), np.datetime64(self._start.to_ns(), 'ns'), 'ns')
+            tt = Variable((), np.datetime64(self._end.to_ns(), 'ns'), 'ns')
             for name in MONITOR_WINDOW_OUTPUTS:
                 out[name] = out[name].assign_coords(start_time=st, time=tt)
         self._start = self._end = None

@@ -40,11 +40,18 @@ def _threads() -> int:
 def test_bench_workload_bit_exact(workload):
     import torch
 
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    with torch.cuda.stream(torch.cuda.Stream(dev)):  # as bench.py: one stream for all
+        _run(workload, dev)
+
+
+def _run(workload, dev):
+    import torch
+
     from esslivedata_amd import projection, synthetic
     from esslivedata_amd.engine import BinningEngine
 
-    dev = torch.device('cuda', 0)
-    torch.cuda.set_device(dev)
     dream = workload == 'dream'
     inst = synthetic.dream_mantle() if dream else synthetic.loki_bank0()
     view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution,

@@ -216,3 +216,31 @@ def test_detector_move_rebuilds_lut_and_resets():
         np.testing.assert_array_equal(out['current'].values, exp)
         n_since_move = 2 if step in (1, 3) else 1
         np.testing.assert_array_equal(out['cumulative'].values, n_since_move * exp)
+
+
+def test_finalize_outputs_round_trip_through_da00():
+    """Every output of a GPU detector-view finalize encodes to da00 and
+    decodes back unchanged (values, dims, units, coords incl. time stamps)."""
+    from esslivedata_amd import da00, synthetic
+    from esslivedata_amd.workflows import GeometricViewConfig, GpuDetectorViewFactory
+
+    inst = synthetic.dream_mantle(n_replicas=1)
+    fac = GpuDetectorViewFactory(
+        detector_numbers={'mantle': inst.detector_number},
+        view_config=GeometricViewConfig('cylinder_mantle_z', inst.resolution),
+        positions={'mantle': inst.positions})
+    wf = fac.make_workflow('mantle')
+    pid, toa = synthetic.dream_events(300_000, inst, seed=4)
+    wf.accumulate({'mantle': (pid, toa)}, start_time=_t(10**18), end_time=_t(10**18 + 10**9))
+    out = wf.finalize()
+    assert float(out['counts_total'].values) > 0
+    for name, da in out.items():
+        buf = da00.Da00Serializer().serialize(f'mantle/{name}', 10**18, da)
+        src, ts, variables = da00.deserialise_da00(buf)
+        back = da00.da00_to_dataarray(variables)
+        assert src == f'mantle/{name}' and ts == 10**18
+        np.testing.assert_array_equal(back.values, da.values)
+        assert back.dims == da.dims and back.unit == da.unit
+        assert set(back.coords) == set(da.coords)
+        for k, v in da.coords.items():
+            np.testing.assert_array_equal(back.coords[k].values, v.values)

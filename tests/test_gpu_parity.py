@@ -490,3 +490,30 @@ def test_device_tensors_must_be_int32():
     with pytest.raises(ValueError):
         eng.stage_tensors(ok.cpu(), ok.cpu())
     assert eng.info()['staged'] == 0
+
+
+def test_default_stream_engine_outlives_recorded_tensors():
+    """An engine on its default (torch pool) stream, fed from torch's null
+    stream, then destroyed before the staged tensors are freed: the caching
+    allocator's stream record must point at a live stream (the round-2
+    regression: record_stream on an engine-destroyed stream crashed at free)."""
+    import torch
+
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.dream_mantle(n_replicas=1)
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    pid, toa = synthetic.dream_events(500_000, inst, seed=8)
+    dp = torch.as_tensor(pid, device='cuda')
+    dt = torch.as_tensor(toa, device='cuda')
+    eng = _engine(view, inst.edges.edges_ns())
+    assert eng.stream_ptr != torch.cuda.current_stream().cuda_stream
+    eng.stage_tensors_batch([(dp[:1000], dt[:1000]), (dp[1000:], dt[1000:])])
+    eng.accumulate(0)
+    h = eng.read_histogram()
+    eng.close()
+    del eng, dp, dt
+    torch.cuda.synchronize()
+    x = torch.empty(10**7, dtype=torch.int32, device='cuda')  # allocator reuse after free
+    del x
+    assert h.sum() > 0
