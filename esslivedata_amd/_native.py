@@ -8,10 +8,13 @@ import of :func:`lib` raises -- there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / 'libesslivedata_amd.so'
+if os.environ.get('LDE_LIBRARY'):  # A/B diagnostics: another build of the same ABI
+    LIB_PATH = Path(os.environ['LDE_LIBRARY']).resolve()
 
 ABI_VERSION = 1
 

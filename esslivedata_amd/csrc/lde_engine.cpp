@@ -144,6 +144,9 @@ struct lde_handle {
     uint32_t *d_sieve_tab = nullptr;  // [R][1 << cache_bits] LDS table images
     std::vector<uint32_t> ttab;       // TOA bucket words (host copy)
     uint32_t *d_ttab = nullptr;
+    // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
+    bool lds_ctab = true, karg_segs = true;
+    int sieve_ablate = 0;
     uint32_t ttab_cap = 0;
     int ttab_shift = 0;
     lde::ChunkPtrs *d_chunk_tab = nullptr;
@@ -156,7 +159,7 @@ struct lde_handle {
     size_t cold_keys_cap = 0;
     uint4 *d_cold_items = nullptr;
     size_t cold_items_cap = 0;
-    uint32_t *d_cold_ttot = nullptr, *d_cold_tbase = nullptr;  // [n_tiles]
+    uint32_t *d_cold_ttot = nullptr;  // [n_tiles]
 
     // finalize scratch
     unsigned long long *d_tot4 = nullptr;
@@ -378,15 +381,6 @@ bool build_sieve_toa(const lde::ToaParams &tp, const std::vector<unsigned char> 
     words[(size_t)G] = 0xFFu;
     cap = (G << shift2) > 0xffffffffULL ? 0xffffffffu : (uint32_t)(G << shift2);
     return true;
-}
-
-// SIEVE cold keys are counted per tile for this many wave groups per block
-// (the sort then runs that many blocks per sieve block); <= 8 KB of LDS
-int sieve_groups(int n_tiles) {
-    const long long g = env_ll("LDE_SIEVE_GROUPS", 1);
-    for (int k : {4, 2})
-        if (g >= k && (long long)n_tiles * k * 4 <= 8192) return k;
-    return 1;
 }
 
 // ---- timing ----------------------------------------------------------------
@@ -728,14 +722,12 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.hot_part = h->d_hot_part;
     a.cold = h->d_cold;
     a.cold_cnt = h->d_cold_cnt;
-    const bool sieve = h->sieve_ok && (unsigned long long)a.cold_cap * 4ULL < 0x80000000ULL &&
-                       env_ll("LDE_SIEVE", 1) != 0;
+    const bool sieve = h->sieve_ok && (unsigned long long)a.cold_cap * 4ULL < 0x80000000ULL;
     if (sieve) {
         if (int rc = grow(h, &h->d_chunk_tab, h->chunk_tab_cap, (size_t)chunks + 1)) return rc;
         const size_t nt = (size_t)h->n_tiles;
-        const int tg = sieve_groups(h->n_tiles);
-        if (int rc = grow(h, &h->d_cold_tcnt, h->cold_tcnt_cap, (size_t)a.grid * tg * nt)) return rc;
-        if (int rc = grow(h, &h->d_cold_boff, h->cold_boff_cap, (size_t)a.grid * tg * nt)) return rc;
+        if (int rc = grow(h, &h->d_cold_tcnt, h->cold_tcnt_cap, (size_t)a.grid * lde::kColdGroups * nt)) return rc;
+        if (int rc = grow(h, &h->d_cold_boff, h->cold_boff_cap, (size_t)a.grid * lde::kColdGroups * nt)) return rc;
         // tile-major u16 keys: at most every staged slot, + slack for pass B's 16-byte loads
         if (int rc = grow(h, &h->d_cold_keys, h->cold_keys_cap,
                           (size_t)a.grid * (size_t)a.cold_cap + 64))
@@ -769,9 +761,8 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         sa.cold_cnt = h->d_cold_cnt;
         sa.tile_bits = h->tile_bits;
         sa.n_tiles = h->n_tiles;
-        sa.tgroups = tg;
         sa.cold_tcnt = h->d_cold_tcnt;
-        sa.ablate = (int)env_ll("LDE_SIEVE_ABLATE", 0);
+        sa.ablate = h->sieve_ablate;
         {
             // k_sieve is timed by its own dispatch (start/stop events stamped
             // by hipExtLaunchKernelGGL): no marker packets around it
@@ -784,7 +775,15 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                     ea = nullptr;
                 }
             }
-            if (!uploaded && (long long)sd.size() <= lde::kKargSegs && env_ll("LDE_KARG_SEGS", 1)) {
+            // the sieve builds its chunk table in LDS from descriptors passed
+            // as kernel arguments (no launch in front of it) when they fit
+            const long long per_block = (chunks + a.grid - 1) / a.grid;
+            sa.lds_ctab = (long long)sd.size() <= lde::kKargSegs && per_block + 1 <= lde::kSieveLdsChunks &&
+                          h->lds_ctab;
+            sa.dummy = h->d_sieve_dummy;
+            if (sa.lds_ctab) {
+                for (size_t i = 0; i < sd.size(); ++i) sa.sk.s[i] = sd[i];
+            } else if (!uploaded && (long long)sd.size() <= lde::kKargSegs && h->karg_segs) {
                 HIPCALL(h, lde::launch_chunk_tab_karg(sd.data(), a.n_segs, chunks, h->d_sieve_dummy,
                                                       h->d_chunk_tab, h->d_segs, h->stream));
             } else {
@@ -795,16 +794,15 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
             HIPCALL(h, lde::launch_sieve(sa, a.grid, h->stream, ea, eb));
             if (ea) h->launches.push_back({LDE_K_SPLIT, ea, eb});
         }
-        {
-            Timed tm(h, LDE_K_SPLIT_AUX);
-            HIPCALL(h, lde::launch_hot_reduce(a, h->d_win32, h->stream));
-        }
         lde::ColdArgs c;
+        c.hot_part = h->d_hot_part;
+        c.row_screen = a.row_screen;
+        c.ht = h->hot_rows * h->T;
+        c.ht4 = ht4;
+        c.T = h->T;
         c.tile_bits = h->tile_bits;
         c.n_tiles = h->n_tiles;
         c.rows = a.grid;
-        c.groups = tg;
-        c.halves = env_ll("LDE_SORT_HALVES", 1) > 1 ? 2 : 1;  // 2: measured no faster (tools/halves_ab.sh)
         c.cold = h->d_cold;
         c.stride = a.cold_cap + lde::kSplitThreads / 64;
         c.cap = a.cold_cap;
@@ -812,7 +810,6 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         c.tcnt = h->d_cold_tcnt;
         c.boff = h->d_cold_boff;
         c.tile_total = h->d_cold_ttot;
-        c.tile_base = h->d_cold_tbase;
         c.item_keys = (uint32_t)std::min<long long>(item_keys, 0x7fffffffLL);
         c.max_items = (uint32_t)max_items;
         c.items = h->d_cold_items;
@@ -1069,7 +1066,6 @@ void release(lde_handle *h) {
     dev_free(h->d_cold_keys);
     dev_free(h->d_cold_items);
     dev_free(h->d_cold_ttot);
-    dev_free(h->d_cold_tbase);
     dev_free(h->d_row_screen);
     dev_free(h->d_sel_stats);
     dev_free(h->d_sample_part);
@@ -1279,10 +1275,10 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                     (unsigned long long)h->S * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL &&
                     ((h->L - 1) >> cbits) < 255 && h->L < 0x3fffffffLL) {
                     int Hs = 0;
-                    const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size(), h->n_tiles, sieve_groups(h->n_tiles));
+                    const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size(), h->n_tiles);
                     if (fixed < budget)
                         Hs = (int)std::min<long long>(lde::kHotMaxRows, (long long)((budget - fixed) / (4 * (size_t)h->T)));
-                    while (Hs > 0 && lde::sieve_smem(lde::align4(Hs * h->T), cbits, (int)tt.size(), h->n_tiles, sieve_groups(h->n_tiles)) > budget) --Hs;
+                    while (Hs > 0 && lde::sieve_smem(lde::align4(Hs * h->T), cbits, (int)tt.size(), h->n_tiles) > budget) --Hs;
                     Hs = (int)std::min<long long>(Hs, h->S);
                     if (hmax > 0) Hs = (int)std::min<long long>(Hs, hmax);
                     if (Hs >= 8 && (unsigned long long)Hs * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL) {
@@ -1316,7 +1312,6 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                     std::vector<int> dum((size_t)lde::kChunk, (int)((unsigned)h->pid_off - 1u));
                     CREATE_CHECK(dev_alloc(h, &h->d_sieve_dummy, dum.size()));
                     CREATE_CHECK(dev_alloc(h, &h->d_cold_ttot, (size_t)h->n_tiles));
-                    CREATE_CHECK(dev_alloc(h, &h->d_cold_tbase, (size_t)h->n_tiles));
                     CREATE_HIP(hipMemcpy(h->d_sieve_dummy, dum.data(), dum.size() * 4, hipMemcpyHostToDevice));
                 }
                 CREATE_CHECK(dev_alloc(h, &h->d_row_screen, (size_t)h->R * lde::kHotMaxRows));
@@ -1332,6 +1327,9 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 CREATE_HIP(hipHostMalloc((void **)&h->h_sel_stats, (size_t)h->R * 16, hipHostMallocDefault));
             }
         }
+        h->lds_ctab = env_ll("LDE_LDS_CTAB", 1) != 0;
+        h->karg_segs = env_ll("LDE_KARG_SEGS", 1) != 0;
+        h->sieve_ablate = (int)env_ll("LDE_SIEVE_ABLATE", 0);
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);
         h->auto_partition = (int)env_ll("LDE_AUTO_PARTITION", LDE_STRATEGY_PAGED);

@@ -154,6 +154,18 @@ constexpr int kSieveTagShift = 22;
 constexpr uint32_t kSieveValueMask = (1u << kSieveTagShift) - 1u;
 constexpr uint32_t kSieveEmpty = 0xFFu << kSieveTagShift;  // tag 255, not valid
 constexpr int kSieveMaxT = 254;
+constexpr int kColdGroups = 2;  // SIEVE cold keys: wave groups per block, one sort block each
+
+// Batches of up to kKargSegs messages: the descriptors travel as kernel
+// arguments (no pinned staging + H2D copy before the event pass); the kernel
+// also writes them to segs_out for the kernels that read the device table.
+constexpr int kKargSegs = 24;
+struct SegKarg {
+    SegDesc s[kKargSegs];
+};
+// SIEVE: chunk tables of up to this many entries per block live in LDS,
+// built by the sieve itself from kernel-argument descriptors
+constexpr int kSieveLdsChunks = 128;
 
 struct ChunkPtrs {  // one 8192-event chunk of the staged batch (or the dummy chunk)
     const int *pid;
@@ -165,6 +177,9 @@ struct SieveArgs {
     int n_segs;
     long long n_chunks;
     const ChunkPtrs *chunk_tab;  // [n_chunks + 1]; deferred chunks and entry n_chunks: dummy
+    int lds_ctab;                // 1: build the block's chunk table in LDS from sk (no chunk_tab)
+    SegKarg sk;                  // lds_ctab: the message descriptors (n_segs <= kKargSegs)
+    const int *dummy;            // the all-invalid chunk
     const uint32_t *glut;  // this replica's pixel words, L + 1 entries (entry L = 0)
     uint32_t L;
     int pid_off;
@@ -180,22 +195,24 @@ struct SieveArgs {
     long long cold_cap;  // keys per block region (region stride cold_cap + 16)
     uint32_t *cold_cnt;
     int tile_bits, n_tiles;  // cold keys are counted per tile of 2^tile_bits bins
-    int tgroups;             // ... for each of tgroups groups of waves (1, 2, 4)
-    uint32_t *cold_tcnt;     // [grid][tgroups][n_tiles]
+    uint32_t *cold_tcnt;     // [grid][kColdGroups][n_tiles]
     int ablate;  // benchmark ablation variant (0 = the real pass)
 };
-size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles, int tgroups);
+size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a
 // tile-major u16 array, pass B
 struct ColdArgs {
     int tile_bits, n_tiles;
-    int rows;    // sieve blocks
-    int groups;  // wave groups per sieve block (sort blocks per sieve block)
-    int halves = 1;  // sort blocks per (block, group) region: 1 or 2
+    int rows;    // sieve blocks (one sort block each)
+    // hot rows of the sieve blocks, reduced into hist in the same launch as
+    // the per-tile scan (hot_part == nullptr: none)
+    const uint32_t *hot_part = nullptr;
+    const uint32_t *row_screen = nullptr;
+    int ht = 0, ht4 = 0, T = 1;  // hot bins (rows * T), their row stride
     const uint32_t *cold;
     long long stride, cap;  // region stride and capacity (keys)
     const uint32_t *cold_cnt, *tcnt;
-    uint32_t *boff, *tile_total, *tile_base;
+    uint32_t *boff, *tile_total;
     uint32_t item_keys, max_items;
     uint4 *items;
     uint32_t *item_count;
@@ -215,13 +232,6 @@ hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
 hipError_t launch_chunk_tab(const SegDesc *segs, int n_segs, long long n_chunks, const int *dummy,
                             ChunkPtrs *tab, hipStream_t st,
                             hipEvent_t start = nullptr);
-// Batches of up to kKargSegs messages: the descriptors travel as kernel
-// arguments (no pinned staging + H2D copy before the event pass); the kernel
-// also writes them to segs_out for the kernels that read the device table.
-constexpr int kKargSegs = 24;
-struct SegKarg {
-    SegDesc s[kKargSegs];
-};
 hipError_t launch_chunk_tab_karg(const SegDesc *host_segs, int n_segs, long long n_chunks,
                                  const int *dummy, ChunkPtrs *tab, SegDesc *segs_out,
                                  hipStream_t st);

@@ -176,7 +176,9 @@ __global__ __launch_bounds__(256) void k_chunk_tab_karg(SegKarg sk, int n_segs, 
 // ---------------------------------------------------------------------------
 // ABL (benchmark ablations only, results are wrong when nonzero): 1 no hot
 // LDS atomics, 2 no gathers, 4 no cold stores, 8 no LDS probes, 16 every
-// gather lane out of range, 32 every gather lane on the first two words
+// gather lane out of range, 32 every gather lane on the first two words,
+// 64 cold stores exec-masked to the lanes with keys (results exact), 128
+// cold stores every other half only
 template <int ABL>
 __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // static, so LDS addresses need no runtime base (one block per CU anyway)
@@ -192,6 +194,11 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t o_cur = o_dum + 64u;
     const uint32_t o_stg = o_cur + 4u;
     const uint32_t o_tcnt = o_stg + kSieveStage * (kSplitThreads / 64);
+    // block-local chunk table (kSieveLdsChunks entries of {pid, toa}) and the
+    // message descriptors it is built from (lds_ctab mode)
+    const uint32_t o_ctab = o_tcnt + (uint32_t)(kColdGroups * align4(a.n_tiles));
+    const uint32_t o_seg = o_ctab + 4u * kSieveLdsChunks;
+    SegDesc *s_seg = reinterpret_cast<SegDesc *>(sm + o_seg);
     for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.hot_words; i += kSplitThreads * 4u)
         *reinterpret_cast<uint4 *>(sm + i) = make_uint4(0, 0, 0, 0);
     for (uint32_t i = (uint32_t)tid * 4u; i < C; i += kSplitThreads * 4u)
@@ -202,7 +209,12 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     if (tid == 0) sm[o_cur] = 0;
     for (uint32_t i = (uint32_t)tid; i < kSieveStage * (kSplitThreads / 64); i += kSplitThreads)
         sm[o_stg + i] = 0xFFFFFFFFu;
-    for (int i = tid; i < a.n_tiles * a.tgroups; i += kSplitThreads) sm[o_tcnt + i] = 0;
+    for (int i = tid; i < kColdGroups * align4(a.n_tiles); i += kSplitThreads) sm[o_tcnt + i] = 0;
+    if (a.lds_ctab) {  // descriptors from the kernel arguments (static indices)
+#pragma unroll
+        for (int i = 0; i < kKargSegs; ++i)
+            if (tid == i && i < a.n_segs) s_seg[i] = a.sk.s[i];
+    }
     __syncthreads();
 
     const __amdgpu_buffer_rsrc_t glut = make_rsrc(a.glut, (a.L + 1u) * 4u);
@@ -217,10 +229,11 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t dum_idx = o_dum + (uint32_t)lane;
     const uint32_t dum4 = dum_idx * 4u;
     const uint32_t o_stg_w = o_stg + kSieveStage * (uint32_t)(tid >> 6);
-    // cold keys are counted per tile for each group of 16 / tgroups waves
-    const uint32_t grp = (uint32_t)(tid >> 6) / (uint32_t)((kSplitThreads / 64) / a.tgroups);
+    // cold keys are counted per tile for each of the kColdGroups wave groups
+    // (one sort block per group)
+    const uint32_t grp = (uint32_t)(tid >> 6) / (uint32_t)((kSplitThreads / 64) / kColdGroups);
     const uint32_t o_pc4 = o_pc * 4u, o_tt4 = o_tt * 4u;
-    const uint32_t o_tcnt4 = (o_tcnt + grp * (uint32_t)a.n_tiles) * 4u;
+    const uint32_t o_tcnt4 = (o_tcnt + grp * (uint32_t)align4(a.n_tiles)) * 4u;
     const int tsh = a.tile_bits + 2;
     // this wave's sub-region of the block's cold region (keys), 16-B aligned
     const uint32_t capw = (uint32_t)(a.cold_cap / (kSplitThreads / 64));
@@ -234,7 +247,33 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // vector load (in-order vmcnt) and read back with readlane; chunks outside
     // [cb, ce) and deferred chunks map to the all-invalid dummy chunk
     const uint32_t *ctab = reinterpret_cast<const uint32_t *>(a.chunk_tab);
+    if (a.lds_ctab) {
+        // entry j = chunk cb + j of this block (entry ce - cb: the dummy chunk);
+        // replaces the k_chunk_tab launch in front of the sieve
+        for (long long j = tid; j <= ce - cb; j += kSplitThreads) {
+            const long long c = cb + j;
+            ChunkPtrs r{a.dummy, a.dummy};
+            if (c < ce) {
+                int si = 0;
+                for (int i = 1; i < a.n_segs; ++i)
+                    if (s_seg[i].chunk0 <= c) si = i;
+                const SegDesc sd = s_seg[si];
+                const long long base = (c - sd.chunk0) * kChunk;
+                if (((((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0) && base + kChunk <= sd.n) {
+                    r.pid = sd.pid + base;
+                    r.toa = sd.toa + base;
+                }
+            }
+            *reinterpret_cast<ChunkPtrs *>(sm + o_ctab + 4u * (uint32_t)j) = r;
+        }
+        __syncthreads();
+    }
+    const uint32_t o_ctab4 = o_ctab * 4u;
     auto fetch = [&](long long c) __attribute__((always_inline)) {
+        if (a.lds_ctab) {
+            const uint32_t j = (uint32_t)((c < ce ? c : ce) - cb);
+            return lds_at(sm, o_ctab4 + ((j * 4u + (uint32_t)(lane & 3)) << 2));
+        }
         const long long ci = c < ce ? c : n;
         return ld_global_u32(ctab + (size_t)ci * 4 + (lane & 3));
     };
@@ -339,7 +378,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             }
             const uint32_t res = (tot + 3u) & ~3u;
             // the previous half's keys leave now (their LDS read is long done)
-            if (!(ABL & 4)) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+            if (ABL & 64) {  // diagnostic: only the lanes that hold keys issue the store
+                if (pend_off != kOOB) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+            } else if (ABL & 128) {  // diagnostic: every other half stores (keys lost)
+                if (h == 0) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+            } else if (!(ABL & 4)) {
+                __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+            }
             else sm[o_dum + lane] += pend_kv[0] ^ pend_off;
             __builtin_amdgcn_wave_barrier();
             uint4 *slot = reinterpret_cast<uint4 *>(sm + o_stg_w + 4u * (uint32_t)lane);
@@ -385,18 +430,19 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
 
     // ---- deferred chunks: element-wise loads of a clamped index
     if (cb < ce) {
+        const SegDesc *segs = a.lds_ctab ? s_seg : a.segs;
         int si = 0;
         {
             int lo = 0, hi = a.n_segs - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
-                if (a.segs[mid].chunk0 <= cb) lo = mid; else hi = mid - 1;
+                if (segs[mid].chunk0 <= cb) lo = mid; else hi = mid - 1;
             }
             si = lo;
         }
         for (long long c = cb; c < ce; ++c) {
-            while (si + 1 < a.n_segs && a.segs[si + 1].chunk0 <= c) ++si;
-            const SegDesc sd = a.segs[si];
+            while (si + 1 < a.n_segs && segs[si + 1].chunk0 <= c) ++si;
+            const SegDesc sd = segs[si];
             const long long base = (c - sd.chunk0) * kChunk;
             if (((((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0) && base + kChunk <= sd.n)
                 continue;
@@ -426,44 +472,69 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     uint32_t *dst = a.hot_part + (size_t)blockIdx.x * a.hot_words;
     for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4)
         *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(sm + i);
-    for (int i = tid; i < a.n_tiles * a.tgroups; i += kSplitThreads)
-        a.cold_tcnt[(size_t)blockIdx.x * a.tgroups * a.n_tiles + i] = sm[o_tcnt + i];
+    for (int i = tid; i < kColdGroups * a.n_tiles; i += kSplitThreads) {
+        const int g = i / a.n_tiles, t = i - g * a.n_tiles;
+        a.cold_tcnt[((size_t)blockIdx.x * kColdGroups + g) * a.n_tiles + t] =
+            sm[o_tcnt + g * align4(a.n_tiles) + t];
+    }
 }
 
 // ---------------------------------------------------------------------------
 // cold keys: exact counting sort into a tile-major u16 array, then pass B
 // ---------------------------------------------------------------------------
-// per tile: exclusive scan over sieve blocks of their key counts
-__global__ __launch_bounds__(256) void k_cold_scan(const uint32_t *__restrict__ tcnt, int rows,
-                                                   int n_tiles, uint32_t *__restrict__ boff,
-                                                   uint32_t *__restrict__ tile_total) {
+// One launch, two block roles (saves a dependent launch between the sieve
+// and the sort): blocks [0, hot_blocks) add the sieve blocks' private hot rows
+// into the window (8 row slices per column of 256 hot bins); the other
+// n_tiles blocks scan, per tile, the sieve blocks' cold-key counts into the
+// blocks' offsets inside the tile (boff) and the tile totals.
+__global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blocks) {
     __shared__ uint32_t s_w[32];
-    const int t = blockIdx.x;
+    if ((int)blockIdx.x < hot_blocks) {
+        constexpr int kSlices = 8;
+        const int col = blockIdx.x / kSlices, slice = blockIdx.x % kSlices;
+        const int i = col * 256 + threadIdx.x;
+        if (i >= c.ht) return;
+        const int per = (c.rows + kSlices - 1) / kSlices;
+        const int j0 = slice * per, j1 = min(c.rows, j0 + per);
+        uint32_t sum = 0;
+        for (int j = j0; j < j1; ++j) sum += c.hot_part[(size_t)j * c.ht4 + i];
+        if (sum) {
+            const int row = i / c.T;
+            atomicAdd(c.hist + (size_t)c.row_screen[row] * c.T + (i - row * c.T), sum);
+        }
+        return;
+    }
+    const int t = blockIdx.x - hot_blocks;
+    const int rows = c.rows * kColdGroups;
     uint32_t carry = 0;
     for (int r0 = 0; r0 < rows; r0 += 256) {
         const int r = r0 + threadIdx.x;
-        const uint32_t v = r < rows ? tcnt[(size_t)r * n_tiles + t] : 0u;
+        const uint32_t v = r < rows ? c.tcnt[(size_t)r * c.n_tiles + t] : 0u;
         uint32_t tot;
         const uint32_t ex = block_exclusive_scan(v, s_w, &tot);
-        if (r < rows) boff[(size_t)r * n_tiles + t] = carry + ex;
+        if (r < rows) c.boff[(size_t)r * c.n_tiles + t] = carry + ex;
         carry += tot;
         __syncthreads();
     }
-    if (threadIdx.x == 0) tile_total[t] = carry;
+    if (threadIdx.x == 0) c.tile_total[t] = carry;
 }
 
-// tile bases of the tile-major key array + balanced pass-B items
-// (tile, first key, end key); a tile with n keys gets ceil(n / item_keys) items
-__global__ __launch_bounds__(1024) void k_cold_plan(const uint32_t *__restrict__ tile_total,
-                                                    int n_tiles, uint32_t item_keys,
-                                                    uint32_t *__restrict__ tile_base,
-                                                    uint4 *__restrict__ items,
-                                                    uint32_t *__restrict__ item_count,
-                                                    uint32_t max_items) {
-    __shared__ uint32_t s_w[32];
-    __shared__ uint32_t s_ib[kMaxTiles + 1];
-    __shared__ uint32_t s_kb[kMaxTiles + 1];
-    constexpr int TPT = kMaxTiles / 1024;
+constexpr int kSortThreads = 64 * (kSplitThreads / 64) / kColdGroups;  // one wave per sieve wave
+constexpr int kSortWaves = kSortThreads / 64;
+constexpr int kSortKPT = 16;                           // keys per lane per piece
+constexpr int kSortPiece = kSortThreads * kSortKPT;    // 8192
+// the piece's sorted image (also the scratch of plan_items)
+constexpr int kSortImage = align4(kSortPiece > 2 * (kMaxTiles + 1) ? kSortPiece : 2 * (kMaxTiles + 1));
+
+// Balanced pass-B items (tile, first key, end key, tile has one item) of the
+// tile-major key array: a tile with n keys gets ceil(n / item_keys) items.
+// Run by sort block 0 (kSortThreads threads) before its pieces; s_ib / s_kb are
+// kMaxTiles + 1 words of scratch LDS each.
+__device__ void plan_items(const uint32_t *__restrict__ tile_total, int n_tiles,
+                           uint32_t item_keys, uint4 *__restrict__ items,
+                           uint32_t *__restrict__ item_count, uint32_t max_items, uint32_t *s_w,
+                           uint32_t *s_ib, uint32_t *s_kb) {
+    constexpr int TPT = kMaxTiles / kSortThreads;
     const int tid = threadIdx.x;
     uint32_t nk[TPT], ni[TPT], ksum = 0, isum = 0;
 #pragma unroll
@@ -482,7 +553,6 @@ __global__ __launch_bounds__(1024) void k_cold_plan(const uint32_t *__restrict__
     for (int q = 0; q < TPT; ++q) {
         const int t = tid * TPT + q;
         if (t < n_tiles) {
-            tile_base[t] = kb;
             s_kb[t] = kb;
             s_ib[t] = ib;
         }
@@ -495,7 +565,7 @@ __global__ __launch_bounds__(1024) void k_cold_plan(const uint32_t *__restrict__
     }
     __syncthreads();
     const uint32_t n_items = itot < max_items ? itot : max_items;
-    for (uint32_t i = (uint32_t)tid; i < n_items; i += 1024u) {
+    for (uint32_t i = (uint32_t)tid; i < n_items; i += (uint32_t)kSortThreads) {
         int lo = 0, hi = n_tiles - 1;  // last tile with s_ib[t] <= i
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -505,147 +575,173 @@ __global__ __launch_bounds__(1024) void k_cold_plan(const uint32_t *__restrict__
         const uint32_t k0 = s_kb[lo], kn = s_kb[lo + 1] - k0;
         const uint32_t b0 = k0 + (uint32_t)((unsigned long long)j * kn / nt);
         const uint32_t b1 = k0 + (uint32_t)((unsigned long long)(j + 1) * kn / nt);
-        items[i] = make_uint4((uint32_t)lo, b0, b1, 0u);
+        items[i] = make_uint4((uint32_t)lo, b0, b1, nt == 1u ? 1u : 0u);
     }
     if (tid == 0) *item_count = n_items;
+    __syncthreads();
 }
 
-// One block per sieve block: its cold region (keys scaled by 4, -1 pads; 16
-// wave sub-regions) is sorted by tile in 16K-key
-// pieces in LDS (rank by LDS atomics, scan over tiles, scatter), and each
-// piece's tile runs are written as u16 tile-local keys at the block's exact
-// offsets of the tile-major array.  Pad keys (-1) are skipped.
-constexpr int kSortThreads = 1024;
-constexpr int kSortPiece = 16384;
+// One 1024-thread block per sieve block.  Sort wave w reads sieve wave w's
+// sub-region of the block's cold region (keys scaled by 4, written in
+// multiples of 4 with -1 pads), 1024 keys per wave per piece, so the load
+// address is a plain offset.  Per piece: rank each key among its wave's keys
+// of the same tile (wave-private LDS counters: ~16x less same-address
+// contention than block counters), turn the counters into per-(wave, tile)
+// bases of the piece's tile-sorted LDS image, scatter, and write each tile
+// run as u16 tile-local keys to its exact place in the tile-major array (the
+// sieve's per-tile counts, scanned by k_cold_scan / k_cold_plan).
 size_t cold_sort_smem(int n_tiles) {
-    return 4 * ((size_t)kSortPiece + 3 * (size_t)align4(n_tiles) + 32);
+    const size_t nt4 = (size_t)align4(n_tiles);
+    static_assert(64 % kSortWaves == 0, "tiles per wave in the prefix scan");
+    return 4 * ((size_t)kSortImage + (size_t)kSortWaves * nt4 + 3 * nt4 + 32);
 }
 
-// halves == 2: two blocks share a region (two blocks per CU), the first
-// half's pieces fill each tile's slots upward from the region's tile offset,
-// the second half's downward from its end (offset + the region's tile count),
-// so the halves need no count of each other's keys.
 template <int TB>
-__global__ __launch_bounds__(kSortThreads) void k_cold_sort(
-    const uint32_t *__restrict__ cold, long long stride, long long cap,
-    const uint32_t *__restrict__ cold_cnt, const uint32_t *__restrict__ boff,
-    const uint32_t *__restrict__ tcnt, const uint32_t *__restrict__ tile_base, int n_tiles,
-    int groups, int halves, uint16_t *__restrict__ out) {
-    constexpr int KPT = kSortPiece / kSortThreads;  // 16 keys per thread
+__global__ __launch_bounds__(kSortThreads) void k_cold_sort(ColdArgs c) {
+    const uint32_t *__restrict__ cold = c.cold;
+    const long long stride = c.stride, cap = c.cap;
+    const uint32_t *__restrict__ cold_cnt = c.cold_cnt;
+    const uint32_t *__restrict__ boff = c.boff;
+    const int n_tiles = c.n_tiles;
+    uint16_t *__restrict__ out = c.keys;
     constexpr uint32_t MASK = (1u << TB) - 1u;
+    constexpr int SH = TB + 2;  // keys are scaled by 4
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     const int nt4 = align4(n_tiles);
     uint32_t *s_sorted = sm;
-    uint32_t *s_cnt = sm + kSortPiece;
-    uint32_t *s_start = s_cnt + nt4;
-    uint32_t *s_cur = s_start + nt4;
-    uint32_t *s_w = s_cur + nt4;
+    uint32_t *s_cnt = sm + kSortImage;             // [wave][tile]: count -> base
+    uint32_t *s_pos = s_cnt + kSortWaves * nt4;    // [tile] next global position
+    uint32_t *s_delta = s_pos + nt4;               // [tile] global - LDS position
+    uint32_t *s_tot = s_delta + nt4;               // [tile] piece total -> run base
+    uint32_t *s_w = s_tot + nt4;
     const int tid = threadIdx.x;
-    // block = (sieve block b, wave group g): waves [g * WPG, (g + 1) * WPG) of
-    // the sieve block's cold region, which is 16 wave sub-regions of cap / 16
-    // keys, each filled to a multiple of 4; logical key i lives in the
-    // sub-region of the last wave whose prefix is <= i
-    constexpr int NW = kSplitThreads / 64;
-    const int row = blockIdx.x / halves, half = blockIdx.x % halves;
-    const int b = row / groups, g = row % groups;
-    const int WPG = NW / groups;
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (int w = 0; w < NW; ++w) {
-            s_w[w] = acc;
-            if (w >= g * WPG && w < (g + 1) * WPG) acc += cold_cnt[(size_t)b * NW + w];
-        }
-        s_w[NW] = acc;
-    }
-    __syncthreads();
-    uint32_t pre[NW + 1];
-#pragma unroll
-    for (int w = 0; w <= NW; ++w) pre[w] = s_w[w];
-    __syncthreads();
-    const uint32_t n = pre[NW];
-    const uint32_t npieces = (n + kSortPiece - 1) / kSortPiece;
-    const uint32_t mid = halves > 1 ? min(n, ((npieces + 1) / 2) * (uint32_t)kSortPiece) : n;
-    const uint32_t pb = half ? mid : 0u, pe = half ? n : mid;  // this block's logical keys
+    const int wv = tid >> 6, lane = tid & 63;
+    // block = (sieve block, wave group); boff / tcnt rows are (block, group)
+    const int b = blockIdx.x / kColdGroups, grp = blockIdx.x % kColdGroups;
+    const int row = blockIdx.x;
+    constexpr int NW = kSplitThreads / 64;  // sieve waves per sieve block
     const uint32_t capw = (uint32_t)(cap / NW);
-    auto phys = [&](uint32_t i) __attribute__((always_inline)) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int q = 1; q < NW; ++q) w = i >= pre[q] ? (uint32_t)q : w;
-        return i < n ? (w * capw + (i - pre[w])) * 4u : 0x80000000u;
-    };
-    const uint32_t *src = cold + (size_t)b * (size_t)stride;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, (uint32_t)(cap * 4));
-    for (int t = tid; t < n_tiles; t += kSortThreads)
-        s_cur[t] = tile_base[t] + boff[(size_t)row * n_tiles + t] +
-                   (half ? tcnt[(size_t)row * n_tiles + t] : 0u);
-    constexpr int TPT = kMaxTiles / kSortThreads;
-    // the next piece's keys are requested before the current piece is sorted
-    v4u nk[KPT / 4];
-    auto fetch = [&](uint32_t p0) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < KPT / 4; ++j) {
-            const uint32_t e0 = p0 + ((uint32_t)j * kSortThreads + (uint32_t)tid) * 4u;
-            nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)phys(e0), 0, 0);
-        }
-    };
-    if (pb < pe) fetch(pb);
-    for (uint32_t p0 = pb; p0 < pe; p0 += kSortPiece) {
-        for (int t = tid; t < n_tiles; t += kSortThreads) s_cnt[t] = 0;
-        uint32_t key[KPT], rank[KPT];
-#pragma unroll
-        for (int j = 0; j < KPT / 4; ++j) {
-            const uint32_t e0 = p0 + ((uint32_t)j * kSortThreads + (uint32_t)tid) * 4u;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < pe ? nk[j][q] : 0xFFFFFFFFu;
-        }
-        if (p0 + kSortPiece < pe) fetch(p0 + kSortPiece);
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < KPT; ++e) {
-            rank[e] = 0;
-            if (key[e] != 0xFFFFFFFFu)
-                rank[e] = __hip_atomic_fetch_add(s_cnt + (key[e] >> (TB + 2)), 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        __syncthreads();
-        uint32_t c[TPT], sum = 0;
+    const int sw = grp * kSortWaves + wv;   // my sieve wave
+    const uint32_t n_w = cold_cnt[(size_t)b * NW + sw];  // its keys (incl. pads)
+    // the items of pass B (block 0, in the LDS of the sorted image)
+    if (row == 0)
+        plan_items(c.tile_total, n_tiles, c.item_keys, c.items, c.item_count, c.max_items, s_w,
+                   s_sorted, s_sorted + kMaxTiles + 1);
+    // tile bases of the tile-major array: exclusive scan of the tile totals
+    {
+        constexpr int TPT = (kMaxTiles + kSortThreads - 1) / kSortThreads;
+        uint32_t tt[TPT], sum = 0;
 #pragma unroll
         for (int q = 0; q < TPT; ++q) {
             const int t = tid * TPT + q;
-            c[q] = t < n_tiles ? s_cnt[t] : 0u;
-            sum += c[q];
+            tt[q] = t < n_tiles ? c.tile_total[t] : 0u;
+            sum += tt[q];
         }
         uint32_t total;
         uint32_t run = block_exclusive_scan(sum, s_w, &total);
 #pragma unroll
         for (int q = 0; q < TPT; ++q) {
             const int t = tid * TPT + q;
-            if (t < n_tiles) s_start[t] = run;
-            run += c[q];
+            if (t < n_tiles) s_pos[t] = run + boff[(size_t)row * n_tiles + t];
+            run += tt[q];
+        }
+    }
+    __syncthreads();
+    if (lane == 0) s_w[wv] = (n_w + 64 * kSortKPT - 1) / (64 * kSortKPT);
+    __syncthreads();
+    uint32_t npieces = 0;
+#pragma unroll
+    for (int q = 0; q < kSortWaves; ++q) npieces = max(npieces, s_w[q]);
+    __syncthreads();  // s_w is the scans' scratch below
+    const __amdgpu_buffer_rsrc_t rs =
+        make_rsrc(cold + (size_t)b * (size_t)stride + (size_t)sw * capw, n_w * 4u);
+    uint32_t *my_cnt = s_cnt + wv * nt4;
+    // the next piece's keys are requested before the current piece is sorted
+    v4u nk[kSortKPT / 4];
+    auto fetch = [&](uint32_t p) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < kSortKPT / 4; ++j) {
+            const uint32_t e0 = p * (uint32_t)(64 * kSortKPT) + (uint32_t)j * 256u + (uint32_t)lane * 4u;
+            nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
+        }
+    };
+    if (npieces) fetch(0);
+    for (uint32_t p = 0; p < npieces; ++p) {
+        for (int i = lane; i < nt4; i += 64) my_cnt[i] = 0;
+        uint32_t key[kSortKPT], rank[kSortKPT];
+#pragma unroll
+        for (int j = 0; j < kSortKPT / 4; ++j) {
+            const uint32_t e0 = p * (uint32_t)(64 * kSortKPT) + (uint32_t)j * 256u + (uint32_t)lane * 4u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n_w ? nk[j][q] : 0xFFFFFFFFu;
+        }
+        if (p + 1 < npieces) fetch(p + 1);
+        __builtin_amdgcn_wave_barrier();  // my counters zeroed before the wave ranks
+#pragma unroll
+        for (int e = 0; e < kSortKPT; ++e) {
+            rank[e] = 0;
+            if (key[e] != 0xFFFFFFFFu)
+                rank[e] = __hip_atomic_fetch_add(my_cnt + (key[e] >> SH), 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+        // per tile: wave counts -> wave bases inside the tile's run (a 16-lane
+        // shuffle scan per tile, 4 tiles per wave at a time), tile totals
+        {
+            constexpr int TPW = 64 / kSortWaves;  // tiles per wave and pass
+            const int g = lane / kSortWaves, w2 = lane % kSortWaves;
+            for (int t0 = wv * TPW; t0 < n_tiles; t0 += kSortWaves * TPW) {
+                const int t = t0 + g;
+                const uint32_t v = t < n_tiles ? s_cnt[w2 * nt4 + t] : 0u;
+                uint32_t x = v;
+#pragma unroll
+                for (int d = 1; d < kSortWaves; d <<= 1) {
+                    const uint32_t y = __shfl_up(x, d, kSortWaves);
+                    if (w2 >= d) x += y;
+                }
+                if (t < n_tiles) {
+                    s_cnt[w2 * nt4 + t] = x - v;
+                    if (w2 == kSortWaves - 1) s_tot[t] = x;
+                }
+            }
+        }
+        __syncthreads();
+        // runs of the piece's tile-sorted image: exclusive scan of the totals
+        constexpr int TPT = (kMaxTiles + kSortThreads - 1) / kSortThreads;
+        uint32_t tot[TPT], sum = 0;
+#pragma unroll
+        for (int q = 0; q < TPT; ++q) {
+            const int t = tid * TPT + q;
+            tot[q] = t < n_tiles ? s_tot[t] : 0u;
+            sum += tot[q];
+        }
+        uint32_t total;
+        uint32_t run = block_exclusive_scan(sum, s_w, &total);
+#pragma unroll
+        for (int q = 0; q < TPT; ++q) {
+            const int t = tid * TPT + q;
+            if (t < n_tiles) {
+                s_tot[t] = run;  // now the run's base in the image
+                s_delta[t] = s_pos[t] - run;
+                s_pos[t] += tot[q];
+            }
+            run += tot[q];
+        }
+        __syncthreads();
+        for (int i = tid; i < kSortWaves * nt4; i += kSortThreads) {
+            const int t = i % nt4;
+            if (t < n_tiles) s_cnt[i] += s_tot[t];
         }
         __syncthreads();
 #pragma unroll
-        for (int e = 0; e < KPT; ++e)
-            if (key[e] != 0xFFFFFFFFu) s_sorted[s_start[key[e] >> (TB + 2)] + rank[e]] = key[e];
+        for (int e = 0; e < kSortKPT; ++e)
+            if (key[e] != 0xFFFFFFFFu) s_sorted[my_cnt[key[e] >> SH] + rank[e]] = key[e];
         __syncthreads();
-        if (half == 0) {
-            for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
-                const uint32_t k = s_sorted[i];
-                const uint32_t t = k >> (TB + 2);
-                out[s_cur[t] + (i - s_start[t])] = (uint16_t)((k >> 2) & MASK);
-            }
-        } else {
-            for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
-                const uint32_t k = s_sorted[i];
-                const uint32_t t = k >> (TB + 2);
-                out[s_cur[t] - 1u - (i - s_start[t])] = (uint16_t)((k >> 2) & MASK);
-            }
+        for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
+            const uint32_t k = s_sorted[i];
+            out[s_delta[k >> SH] + i] = (uint16_t)((k >> 2) & MASK);
         }
         __syncthreads();
-        if (half == 0)
-            for (int t = tid; t < n_tiles; t += kSortThreads) s_cur[t] += s_cnt[t];
-        else
-            for (int t = tid; t < n_tiles; t += kSortThreads) s_cur[t] -= s_cnt[t];
     }
 }
 
@@ -684,19 +780,39 @@ __global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
         }
     }
     __syncthreads();
+    // a tile's only item owns its bins (hot rows are other screens, added by
+    // k_hot_reduce before this launch): plain adds; split tiles add atomically
     const long long base = (long long)it.x << TB;
-    for (int i = threadIdx.x; i < NB; i += kTileThreads) {
-        const uint32_t v = s_tile[i];
-        if (v != 0u && base + i < n_bins) atomicAdd(hist + base + i, v);
+    if (it.w && base + NB <= n_bins) {
+        // 16-byte read-modify-write, every load of the thread issued first
+        constexpr int V = NB / 4 / kTileThreads;
+        uint4 *h4 = reinterpret_cast<uint4 *>(hist + base);
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(s_tile);
+        uint4 hv[V];
+#pragma unroll
+        for (int u = 0; u < V; ++u) hv[u] = h4[u * kTileThreads + threadIdx.x];
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            const uint4 a = s4[u * kTileThreads + threadIdx.x];
+            if (a.x | a.y | a.z | a.w)
+                h4[u * kTileThreads + threadIdx.x] =
+                    make_uint4(hv[u].x + a.x, hv[u].y + a.y, hv[u].z + a.z, hv[u].w + a.w);
+        }
+    } else {
+        for (int i = threadIdx.x; i < NB; i += kTileThreads) {
+            const uint32_t v = s_tile[i];
+            if (v != 0u && base + i < n_bins) atomicAdd(hist + base + i, v);
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
-size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles, int tgroups) {
+size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles) {
     return 4 * ((size_t)hot_words + ((size_t)1 << cbits) + (size_t)toa_words4 + 64 + 4 +
-                (size_t)kSieveStage * (kSplitThreads / 64) + (size_t)align4(n_tiles * tgroups));
+                (size_t)kSieveStage * (kSplitThreads / 64) + (size_t)kColdGroups * align4(n_tiles) +
+                4 * (size_t)kSieveLdsChunks + sizeof(SegDesc) / 4 * (size_t)kKargSegs);
 }
 
 hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
@@ -735,10 +851,9 @@ hipError_t launch_chunk_tab_karg(const SegDesc *host_segs, int n_segs, long long
 }
 
 hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t stop) {
-    hipLaunchKernelGGL(k_cold_scan, dim3(c.n_tiles), dim3(256), 0, st, c.tcnt, c.rows * c.groups,
-                       c.n_tiles, c.boff, c.tile_total);
-    hipLaunchKernelGGL(k_cold_plan, dim3(1), dim3(1024), 0, st, c.tile_total, c.n_tiles, c.item_keys,
-                       c.tile_base, c.items, c.item_count, c.max_items);
+    const int hot_blocks = c.hot_part ? ((c.ht + 255) / 256) * 8 : 0;
+    hipLaunchKernelGGL(k_hot_reduce_scan, dim3(hot_blocks + c.n_tiles), dim3(256), 0, st, c,
+                       hot_blocks);
     const size_t sm = cold_sort_smem(c.n_tiles);
     hipError_t e = hipSuccess;
     switch (c.tile_bits) {
@@ -746,9 +861,7 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
     case TB:                                                                                      \
         (void)hipFuncSetAttribute((const void *)k_cold_sort<TB>,                                  \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);           \
-        hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * c.groups * c.halves), dim3(kSortThreads), \
-                           sm, st, c.cold, c.stride, c.cap, c.cold_cnt, c.boff, c.tcnt,           \
-                           c.tile_base, c.n_tiles, c.groups, c.halves, c.keys);                   \
+        hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * kColdGroups), dim3(kSortThreads), sm, st, c); \
         hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, st,\
                               nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist, c.n_bins); \
         break;
@@ -766,7 +879,7 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
 template <int ABL>
 static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                                  hipEvent_t stop) {
-    if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles, a.tgroups) > kSplitSmemMax)
+    if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles) > kSplitSmemMax)
         return hipErrorInvalidValue;
     hipExtLaunchKernelGGL(k_sieve<ABL>, dim3(grid), dim3(kSplitThreads), 0, st, start, stop, 0,
                           a);  // static LDS
@@ -783,6 +896,8 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     case 15: return launch_sieve_t<15>(a, grid, st, start, stop);
     case 16: return launch_sieve_t<16>(a, grid, st, start, stop);
     case 32: return launch_sieve_t<32>(a, grid, st, start, stop);
+    case 64: return launch_sieve_t<64>(a, grid, st, start, stop);
+    case 128: return launch_sieve_t<128>(a, grid, st, start, stop);
     default: return launch_sieve_t<0>(a, grid, st, start, stop);
     }
 }

@@ -249,28 +249,30 @@ class BinningEngine:
         if n == 0:
             return
         # host time here is GPU idle time between batches: one pass over the
-        # messages, identity dtype test first (torch attribute calls dominate)
+        # messages filling a ctypes array (pid pointers | toa pointers |
+        # lengths), identity dtype test first (torch attribute calls dominate)
         import torch
 
         i32 = torch.int32
-        rows = []
-        for pid, toa in messages:
-            nn = toa.numel()
+        arr = (ctypes.c_int64 * (3 * n))()
+        for i, (pid, toa) in enumerate(messages):
             if toa.dtype is not i32 or not toa.is_contiguous() or not toa.is_cuda:
                 self._check_event_tensor(toa)
-            if pid is None:
-                rows.append((0, toa.data_ptr(), nn))
-                continue
-            if pid.dtype is not i32 or not pid.is_contiguous() or not pid.is_cuda:
-                self._check_event_tensor(pid)
-            if pid.numel() != nn:
-                raise ValueError('pixel_id and time_of_arrival must have the same length')
-            rows.append((pid.data_ptr(), toa.data_ptr(), nn))
+            nn = toa.numel()
+            if pid is not None:
+                if pid.dtype is not i32 or not pid.is_contiguous() or not pid.is_cuda:
+                    self._check_event_tensor(pid)
+                if pid.numel() != nn:
+                    raise ValueError('pixel_id and time_of_arrival must have the same length')
+                arr[i] = pid.data_ptr()
+            arr[n + i] = toa.data_ptr()
+            arr[2 * n + i] = nn
         if _current_raw_stream(messages[0][1].device.index) != self._stream_ptr:
             self._order_after_producer([t for m in messages for t in m if t is not None])
-        ptrs = np.array(rows, dtype=np.int64).T.copy()
-        self._call(self._lib.lde_stage_device_batch, n, ptrs[0].ctypes.data, ptrs[1].ctypes.data,
-                   ptrs[2].ctypes.data)
+        base = ctypes.addressof(arr)
+        rc = self._lib.lde_stage_device_batch(self._h, n, base, base + 8 * n, base + 16 * n)
+        if rc:
+            check(rc, self._h)
         self._keepalive.append(messages)
 
     def accumulate(self, replica: int = 0) -> None:

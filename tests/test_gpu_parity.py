@@ -30,11 +30,13 @@ VARIANTS = [
     {'LDE_PIXEL_CACHE_BITS': '6', 'LDE_SPLIT_GRID': '17'},
     {'LDE_PIXEL_CACHE_BITS': '15'},
     # SPLIT with the original event pass instead of the SIEVE pass
-    # k_cold_sort with two blocks per cold region (upward/downward fill)
-    {'LDE_SORT_HALVES': '2'},
-    {'LDE_SORT_HALVES': '2', 'LDE_HOT_ROWS': '8', 'LDE_SPLIT_GRID': '3'},
+    # SIEVE with few hot rows and few blocks: long cold regions, many sort
+    # pieces per wave, tiles split over several accumulate items
+    {'LDE_HOT_ROWS': '8', 'LDE_SPLIT_GRID': '3', 'LDE_ITEM_EVENTS': '40000'},
     {'LDE_SIEVE': '0'},
     {'LDE_SIEVE': '0', 'LDE_PIXEL_CACHE_BITS': '6', 'LDE_SPLIT_GRID': '17'},
+    # one sieve block: its chunk range exceeds the LDS chunk table (global table)
+    {'LDE_SPLIT_GRID': '1'},
 ]
 
 
@@ -393,6 +395,7 @@ def test_split_many_device_messages(n_msgs, karg, monkeypatch):
     import torch
 
     monkeypatch.setenv('LDE_KARG_SEGS', karg)
+    monkeypatch.setenv('LDE_LDS_CTAB', karg)  # '0': the k_chunk_tab paths
     monkeypatch.setenv('LDE_HOT_REFRESH', '2')
     from esslivedata_amd import projection, synthetic
 

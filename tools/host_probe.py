@@ -8,6 +8,7 @@ from esslivedata_amd import projection, synthetic
 from esslivedata_amd.engine import BinningEngine
 
 dev = torch.device('cuda', 0)
+torch.cuda.set_stream(torch.cuda.Stream(dev))  # as bench.py
 inst = synthetic.dream_mantle()
 view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
 eng = BinningEngine(toa_edges_ns=inst.edges.edges_ns(), out_lut=view.lut, pid_offset=view.pid_offset,
@@ -42,10 +43,30 @@ s0 = torch.cuda.Event(enable_timing=True); s1 = torch.cuda.Event(enable_timing=T
 tot = 0.0
 for i in range(20):
     s0.record()
+    torch.cuda._sleep(2_000_000)  # the GPU is busy while the host enqueues the step
     eng.stage_tensors_batch(msgs)
     eng.accumulate(i % view.n_replicas)
     eng.finalize(images=True)
     s1.record()
     s1.synchronize()
     tot += s0.elapsed_time(s1)
-print('gpu span per step (ms)', round(tot / 20, 4))
+tot_sleep = 0.0
+for i in range(20):
+    s0.record()
+    torch.cuda._sleep(2_000_000)
+    s1.record()
+    s1.synchronize()
+    tot_sleep += s0.elapsed_time(s1)
+print('gpu span per step (ms), host enqueue hidden behind a sleep:', round((tot - tot_sleep) / 20, 4))
+
+# host cost of the staging call alone, split
+import numpy as np
+t0 = time.perf_counter()
+for _ in range(200):
+    rows = [(p.data_ptr(), t.data_ptr(), t.numel()) for p, t in msgs]
+t1 = time.perf_counter()
+for _ in range(200):
+    for p, t in msgs:
+        (t.dtype is torch.int32, t.is_contiguous(), t.is_cuda)
+t2 = time.perf_counter()
+print('data_ptr rows us', round((t1 - t0) / 200 * 1e6, 2), 'checks us', round((t2 - t1) / 200 * 1e6, 2))
