@@ -73,6 +73,7 @@ EXPORTED_SYMBOLS = (
     'lde_import_window_u64',
     'lde_get_stream',
     'lde_set_lut',
+    'lde_set_coord_lut',
     'lde_synchronize',
     'lde_timing_enable',
     'lde_timing_select',
@@ -101,6 +102,20 @@ class LdeConfig(ctypes.Structure):
         ('strategy', ctypes.c_int32),
         ('range_lo', ctypes.c_int32),
         ('range_hi', ctypes.c_int32),
+    ]
+
+
+class LdeCoordLut(ctypes.Structure):
+    _fields_ = [
+        ('pixel_distance', ctypes.c_void_p),
+        ('n_pixels', ctypes.c_int64),
+        ('table', ctypes.c_void_p),
+        ('n_dist', ctypes.c_int32),
+        ('n_time', ctypes.c_int32),
+        ('dist0', ctypes.c_double),
+        ('dist_step', ctypes.c_double),
+        ('time0', ctypes.c_double),
+        ('time_step', ctypes.c_double),
     ]
 
 
@@ -145,6 +160,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_import_window_u64': (ctypes.c_int, [H, P]),
         'lde_get_stream': (ctypes.c_int, [H, ctypes.POINTER(ctypes.c_void_p)]),
         'lde_set_lut': (ctypes.c_int, [H, P]),
+        'lde_set_coord_lut': (ctypes.c_int, [H, ctypes.POINTER(LdeCoordLut)]),
         'lde_synchronize': (ctypes.c_int, [H]),
         'lde_set_groups': (ctypes.c_int, [H, i32, i64, P, P]),
         'lde_group_spectra': (ctypes.c_int, [H, i32, i32, P]),

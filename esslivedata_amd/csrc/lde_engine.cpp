@@ -144,6 +144,15 @@ struct lde_handle {
     uint32_t *d_sieve_tab = nullptr;  // [R][1 << cache_bits] LDS table images
     std::vector<uint32_t> ttab;       // TOA bucket words (host copy)
     uint32_t *d_ttab = nullptr;
+    // wavelength mode (lde_set_coord_lut): per-pixel distance rows/fractions,
+    // the lookup table, the coordinate edges, per-event bin scratch
+    bool coord = false;
+    lde::CoordArgs cargs{};
+    int *d_cpi = nullptr;
+    double *d_cpf = nullptr, *d_ctable = nullptr, *d_cedges = nullptr;
+    int *d_cbin = nullptr;
+    size_t cbin_cap = 0;
+    std::vector<double> edges;  // the create-time edges (event unit)
     // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
     bool lds_ctab = true, karg_segs = true;
     int sieve_ablate = 0;
@@ -391,7 +400,10 @@ hipEvent_t pool_event(lde_handle *h) {
         return e;
     }
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    // timing-only events: no system-scope fence (cache write-back and
+    // invalidate) at every stamped dispatch (LDE_EVENT_FLAGS overrides)
+    static const unsigned flags = (unsigned)env_ll("LDE_EVENT_FLAGS", hipEventDisableSystemFence);
+    if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return nullptr;
     return e;
 }
 
@@ -1018,6 +1030,11 @@ void release(lde_handle *h) {
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
     dev_free(h->d_lut);
     dev_free(h->d_tab);
+    dev_free(h->d_cpi);
+    dev_free(h->d_cpf);
+    dev_free(h->d_ctable);
+    dev_free(h->d_cedges);
+    dev_free(h->d_cbin);
     dev_free(h->d_win32);
     dev_free(h->d_win64);
     dev_free(h->d_cum);
@@ -1135,6 +1152,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     DeviceGuard guard(h->device);
     std::vector<unsigned char> tab;
     int rc = build_toa_tables(h, cfg->toa_edges, cfg->n_toa_bins, tab, h->tp);
+    if (!rc) h->edges.assign(cfg->toa_edges, cfg->toa_edges + cfg->n_toa_bins + 1);
     if (rc) {
         g_create_error = h->err;
         release(h);
@@ -1500,6 +1518,17 @@ int lde_accumulate(lde_handle *h, int32_t replica) {
     for (const Segment &s : h->dev_segments) segs.push_back(s);
     long long total = 0;
     for (const Segment &s : segs) total += s.n;
+    if (h->coord && total > 0) {
+        // wavelength mode: every event's coordinate bin replaces its time as
+        // the value binned against the integer edges 0..T
+        if (int rc = grow(h, &h->d_cbin, h->cbin_cap, (size_t)total)) return rc;
+        long long off = 0;
+        for (Segment &s : segs) {
+            HIPCALL(h, lde::launch_event_coord(h->cargs, s.pid, s.toa, s.n, h->d_cbin + off, h->stream));
+            s.toa = h->d_cbin + off;
+            off += s.n;
+        }
+    }
 
     // split into pieces that cannot overflow a u32 window bin
     const long long piece_max = 1LL << 31;
@@ -1857,6 +1886,101 @@ int lde_import_window_u64(lde_handle *h, const void *d_src) {
     h->win_events = 0;
     h->window_has_data = true;
     h->cum_has_data = true;
+    return LDE_OK;
+}
+
+int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!lut) return fail(h, LDE_EINVAL, "lut is NULL");
+    if (h->monitor) return fail(h, LDE_EINVAL, "wavelength mode needs a detector handle");
+    // entering wavelength mode re-bins against integer edges, so it needs an
+    // empty engine; once in it, a new table or new pixel distances (a detector
+    // move) only change the per-event coordinate and keep the accumulated data
+    const bool rebind = h->coord;
+    if (!rebind && (h->window_has_data || h->cum_has_data || h->staged_host > 0 ||
+                    !h->dev_segments.empty()))
+        return fail(h, LDE_ESTATE, "set the coordinate table before the first accumulate (or after clear)");
+    if (lut->n_pixels != h->L) return fail(h, LDE_EINVAL, "n_pixels %lld != lut_len %lld",
+                                           (long long)lut->n_pixels, h->L);
+    if (lut->n_dist < 2 || lut->n_time < 2) return fail(h, LDE_EINVAL, "the grid needs n_dist, n_time >= 2");
+    if (!lut->table || !lut->pixel_distance) return fail(h, LDE_EINVAL, "NULL table");
+    if (!(lut->dist_step > 0) || !(lut->time_step > 0) || !std::isfinite(lut->dist0) ||
+        !std::isfinite(lut->time0))
+        return fail(h, LDE_EINVAL, "grid origin must be finite and steps > 0");
+    if ((long long)lut->n_dist * lut->n_time > (1LL << 28)) return fail(h, LDE_EINVAL, "table too large");
+    if (h->out_dtype == LDE_F32) return fail(h, LDE_EINVAL, "wavelength mode: float64 views only");
+    DeviceGuard guard(h->device);
+    const int T = h->T;
+    // per pixel: distance row and fraction (host, float64, as the oracle)
+    const double inv_dd = 1.0 / lut->dist_step;
+    const double xmax = (double)(lut->n_dist - 1);
+    std::vector<int> pi((size_t)h->L);
+    std::vector<double> pf((size_t)h->L);
+    for (long long k = 0; k < h->L; ++k) {
+        const double x = (lut->pixel_distance[k] - lut->dist0) * inv_dd;
+        if (x >= 0.0 && x <= xmax) {
+            int i = (int)std::floor(x);
+            if (i > lut->n_dist - 2) i = lut->n_dist - 2;
+            pi[(size_t)k] = i;
+            pf[(size_t)k] = x - (double)i;
+        } else {
+            pi[(size_t)k] = -1;
+            pf[(size_t)k] = 0.0;
+        }
+    }
+    HIPCALL(h, hipStreamSynchronize(h->stream));  // in-flight launches may read the old table
+    if (!rebind) {
+    // the binning stage now sees integer bins: edges 0..T
+    std::vector<double> idx((size_t)T + 1);
+    for (int i = 0; i <= T; ++i) idx[(size_t)i] = (double)i;
+    std::vector<unsigned char> tab;
+    lde::ToaParams tp;
+    if (int rc = build_toa_tables(h, idx.data(), T, tab, tp)) return rc;
+    dev_free(h->d_tab);
+    if (int rc = dev_alloc(h, &h->d_tab, tab.size())) return rc;
+    HIPCALL(h, hipMemcpy(h->d_tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
+    h->tp = tp;
+    if (h->sieve_ok) {
+        std::vector<uint32_t> tt;
+        int tsh = 0;
+        uint32_t tcap = 0;
+        if (build_sieve_toa(tp, tab, tt, tsh, tcap) && tt.size() <= h->ttab.size()) {
+            h->ttab = std::move(tt);
+            h->ttab_shift = tsh;
+            h->ttab_cap = tcap;
+            HIPCALL(h, hipMemcpy(h->d_ttab, h->ttab.data(), h->ttab.size() * 4, hipMemcpyHostToDevice));
+        } else {
+            h->sieve_ok = false;
+        }
+    }
+    }
+    dev_free(h->d_cpi);
+    dev_free(h->d_cpf);
+    dev_free(h->d_ctable);
+    dev_free(h->d_cedges);
+    const size_t nt = (size_t)lut->n_dist * (size_t)lut->n_time;
+    if (int rc = dev_alloc(h, &h->d_cpi, (size_t)h->L)) return rc;
+    if (int rc = dev_alloc(h, &h->d_cpf, (size_t)h->L)) return rc;
+    if (int rc = dev_alloc(h, &h->d_ctable, nt)) return rc;
+    if (int rc = dev_alloc(h, &h->d_cedges, (size_t)T + 1)) return rc;
+    HIPCALL(h, hipMemcpy(h->d_cpi, pi.data(), pi.size() * 4, hipMemcpyHostToDevice));
+    HIPCALL(h, hipMemcpy(h->d_cpf, pf.data(), pf.size() * 8, hipMemcpyHostToDevice));
+    HIPCALL(h, hipMemcpy(h->d_ctable, lut->table, nt * 8, hipMemcpyHostToDevice));
+    HIPCALL(h, hipMemcpy(h->d_cedges, h->edges.data(), ((size_t)T + 1) * 8, hipMemcpyHostToDevice));
+    lde::CoordArgs &c = h->cargs;
+    c.pid_off = h->pid_off;
+    c.L = (unsigned)h->L;
+    c.pix_i = h->d_cpi;
+    c.pix_f = h->d_cpf;
+    c.table = h->d_ctable;
+    c.nt = lut->n_time;
+    c.t0 = lut->time0;
+    c.inv_dt = 1.0 / lut->time_step;
+    c.edges = h->d_cedges;
+    c.T = T;
+    h->coord = true;
+    if (!rebind)
+        for (auto &u : h->hot_uses) u = -1;  // hot sets re-select on the new value
     return LDE_OK;
 }
 

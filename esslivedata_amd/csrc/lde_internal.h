@@ -279,6 +279,22 @@ hipError_t launch_group_spectra(int mode, const int4 *items, int n_items, const 
                                 const unsigned long long *cum, const float *fsrc,
                                 unsigned long long *out, hipStream_t st);
 
+// wavelength mode (lde_coord.hip): per-event coordinate bin via a (distance,
+// time) lookup table, written as the int32 "time" of a second binning pass
+struct CoordArgs {
+    int pid_off;
+    unsigned L;
+    const int *pix_i;       // [L] distance row of the pixel id, -1 = no coordinate
+    const double *pix_f;    // [L] fractional distance position
+    const double *table;    // [nd * nt] row-major (distance, time)
+    int nt;
+    double t0, inv_dt;      // time grid: t0 + j / inv_dt (event unit, ns)
+    const double *edges;    // [T + 1] coordinate edges
+    int T;
+};
+hipError_t launch_event_coord(const CoordArgs &a, const int *pid, const int *toa, long long n,
+                              int *out, hipStream_t st);
+
 hipError_t launch_rebin_f64(const double *se, const double *sv, long long ns, const double *de,
                             long long nd, double *out_a, double *out_b, hipStream_t st);
 

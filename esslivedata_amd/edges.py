@@ -52,6 +52,44 @@ class TOAEdges:
         return convert_time(self.get_edges(), self.unit, 'ns')
 
 
+# SRC/parameter_models.py:118-122 (WavelengthUnit); factors to angstrom
+WAVELENGTH_UNIT_TO_ANGSTROM = {'Å': 1.0, 'angstrom': 1.0, 'nm': 10.0}
+
+
+@dataclass(frozen=True)
+class WavelengthEdges:
+    """Wavelength edges (``WavelengthEdges``, SRC/parameter_models.py:201-210;
+    ``EdgesModel`` defaults 1..10, 100 linear bins, :82-105)."""
+
+    start: float = 1.0
+    stop: float = 10.0
+    num_bins: int = 100
+    unit: str = 'Å'
+    scale: str = 'linear'
+
+    def __post_init__(self) -> None:
+        if self.stop <= self.start:
+            raise ValueError('stop must be greater than start')
+        if not 1 <= self.num_bins <= 10000:
+            raise ValueError('num_bins must be in [1, 10000]')
+        if self.scale == 'log' and self.start <= 0:
+            raise ValueError("start must be positive when scale is 'log'")
+        if self.unit not in WAVELENGTH_UNIT_TO_ANGSTROM:
+            raise ValueError(f'unsupported wavelength unit {self.unit!r}')
+        if self.scale not in ('linear', 'log'):
+            raise ValueError(f'unknown scale {self.scale!r}')
+
+    def get_edges(self) -> np.ndarray:
+        op = np.linspace if self.scale == 'linear' else np.geomspace
+        return op(self.start, self.stop, self.num_bins + 1)
+
+    def edges_in(self, unit: str) -> np.ndarray:
+        """Edges converted to ``unit`` (one float64 multiply, as ``bins.to``)."""
+        f = WAVELENGTH_UNIT_TO_ANGSTROM[self.unit] / WAVELENGTH_UNIT_TO_ANGSTROM[unit]
+        e = self.get_edges()
+        return e if f == 1.0 else e * f
+
+
 def convert_time(values: np.ndarray, unit: str, to: str) -> np.ndarray:
     """Unit conversion as one float64 multiply by the conversion factor."""
     values = np.asarray(values, dtype=np.float64)

@@ -325,6 +325,26 @@ class BinningEngine:
         self._call(self._lib.lde_set_lut, lut.ctypes.data)
         self._lut = lut
 
+    def set_coordinate_lut(self, pixel_distance, table, *, dist0: float, dist_step: float,
+                           time0: float, time_step: float) -> None:
+        """Wavelength mode (``lde_set_coord_lut``): events are histogrammed by
+        the coordinate ``table`` (n_dist x n_time, bilinear) at their pixel's
+        distance and their time of arrival (ns); the engine's edges are then
+        in the coordinate's unit.  ``pixel_distance`` is per pixel id of the
+        LUT (pid_offset + k), NaN where the pixel has no coordinate."""
+        d = np.ascontiguousarray(np.asarray(pixel_distance, dtype=np.float64))
+        tab = np.ascontiguousarray(np.asarray(table, dtype=np.float64))
+        if tab.ndim != 2:
+            raise ValueError('table must be 2-D (distance, time)')
+        lut = _native.LdeCoordLut()
+        lut.pixel_distance = d.ctypes.data
+        lut.n_pixels = d.size
+        lut.table = tab.ctypes.data
+        lut.n_dist, lut.n_time = tab.shape
+        lut.dist0, lut.dist_step = float(dist0), float(dist_step)
+        lut.time0, lut.time_step = float(time0), float(time_step)
+        self._call(self._lib.lde_set_coord_lut, ctypes.byref(lut))
+
     def reset_cumulative(self) -> None:
         self._call(self._lib.lde_reset_cumulative)
 

@@ -244,6 +244,11 @@ class GeometricSource:
         r, p, _ = self.local.shape
         return apply_transform(t, self.local.reshape(-1, 3)).reshape(r, p, 3)
 
+    def pixel_positions(self, transform=None) -> np.ndarray:
+        """Noise-free pixel positions (replica 0), ``(P, 3)``."""
+        t = self.transform if transform is None else transform
+        return apply_transform(t, self.local[0])
+
     def coords(self, transform=None) -> dict[str, np.ndarray]:
         return project(self.positions(transform), self.projection_type)
 

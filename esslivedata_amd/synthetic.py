@@ -76,6 +76,18 @@ def dream_mantle(n_replicas: int = 5, seed: int = 7) -> Instrument:
     )
 
 
+DREAM_L1 = 76.55  # m, source -> sample
+
+
+def dream_wavelength_table(distance_min: float = 77.5, distance_max: float = 78.1):
+    """Direct-flight wavelength table covering DREAM mantle flight paths
+    (Ltotal 77.65..77.91 m): 0.05 m x 0.25 ms grid over one pulse period."""
+    from .wavelength import ideal_lookup_table
+
+    n_d = int(round((distance_max - distance_min) / 0.05)) + 1
+    return ideal_lookup_table(distance_min, distance_max, n_d, 71.5e6, 287)
+
+
 def loki_bank0(n_replicas: int = 5, seed: int = 42) -> Instrument:
     """LOKI bank 0: 896 x 896 pixels on a plane 5 m downstream, projected with
     the restated ``xy_plane`` and cylindrical-pixel noise replicas

@@ -28,13 +28,14 @@ from typing import TYPE_CHECKING, Any, Callable, Iterable, Mapping, Sequence
 import numpy as np
 
 from .dataarray import DataArray, Variable
-from .edges import TOAEdges, convert_time, label_slice
+from .edges import TOAEdges, WavelengthEdges, convert_time, label_slice
 from .engine import BinningEngine
 from .preprocessors import DetectorEvents, MonitorEvents, StagedEvents, Timestamp
 from .projection import ViewLUT, geometric_lut, index_groups, logical_lut
 
 if TYPE_CHECKING:
     from .geometry import GeometricSource
+    from .wavelength import WavelengthLookupTable
 from . import roi as _roi
 
 DETECTOR_TRANSFORM = 'detector_transform'
@@ -45,6 +46,7 @@ DETECTOR_WINDOW_OUTPUTS = ('current', 'counts_total', 'counts_in_toa_range')
 # (DetectorViewOutputs.fields_with(Temporality.window), detector_view/factory.py:262-276)
 ROI_WINDOW_OUTPUTS = ('roi_spectra_current',)
 TOA_DIM = 'time_of_arrival'
+WAVELENGTH_DIM = 'wavelength'
 _ROI_SLOT = 0
 _SPECTRUM_SLOT = 1
 MONITOR_WINDOW_OUTPUTS = ('current', 'counts_total', 'counts_in_toa_range')
@@ -55,12 +57,27 @@ MONITOR_WINDOW_OUTPUTS = ('current', 'counts_total', 'counts_in_toa_range')
 # ---------------------------------------------------------------------------
 @dataclass
 class DetectorViewParams:
-    """Subset of ``DetectorViewParams`` (SRC/workflows/detector_view_specs.py:53-124)
-    relevant in TOA mode."""
+    """``DetectorViewParams`` (SRC/workflows/detector_view_specs.py:53-124):
+    ``coordinate_mode`` 'toa' or 'wavelength' selects which edges and range
+    are active (``get_active_edges`` / ``get_active_range``, :106-124)."""
 
     toa_edges: TOAEdges = field(default_factory=TOAEdges)
     toa_range: tuple[float, float] | None = None  # in toa_edges.unit; None = disabled
     pixel_weighting: bool = False
+    coordinate_mode: str = 'toa'
+    wavelength_edges: WavelengthEdges = field(default_factory=WavelengthEdges)
+    wavelength_range: tuple[float, float] | None = None  # in wavelength_edges.unit
+
+    def __post_init__(self) -> None:
+        if self.coordinate_mode not in ('toa', 'wavelength'):
+            raise ValueError(f"coordinate_mode must be 'toa' or 'wavelength', "
+                             f"got {self.coordinate_mode!r}")
+
+    def get_active_edges(self) -> TOAEdges | WavelengthEdges:
+        return self.wavelength_edges if self.coordinate_mode == 'wavelength' else self.toa_edges
+
+    def get_active_range(self) -> tuple[float, float] | None:
+        return self.wavelength_range if self.coordinate_mode == 'wavelength' else self.toa_range
 
 
 @dataclass(frozen=True)
@@ -103,7 +120,7 @@ class SpectrumViewConfig:
     reduction_axes: Sequence[int] = ()
 
 
-def _histogram_slice(edges: TOAEdges, toa_range) -> tuple[int, int] | None:
+def _histogram_slice(edges, toa_range) -> tuple[int, int] | None:
     if toa_range is None:
         return None
     return label_slice(edges.get_edges(), float(toa_range[0]), float(toa_range[1]))
@@ -156,7 +173,7 @@ class _ContextState:
 # detector view
 # ---------------------------------------------------------------------------
 class GpuDetectorViewWorkflow:
-    """Detector view in TOA mode on the MI355X engine."""
+    """Detector view (TOA or wavelength mode) on the MI355X engine."""
 
     def __init__(
         self,
@@ -173,6 +190,9 @@ class GpuDetectorViewWorkflow:
         roi_keys: Mapping[str, str] | None = None,
         spectrum_view: SpectrumViewConfig | None = None,
         geometry: 'GeometricSource | None' = None,
+        lookup_table: 'WavelengthLookupTable | None' = None,
+        source_position=(0.0, 0.0, -76.55),
+        sample_position=(0.0, 0.0, 0.0),
     ) -> None:
         self._source = source_name
         # geometric views built from positions rebuild their LUT when the
@@ -184,10 +204,27 @@ class GpuDetectorViewWorkflow:
             view = geometry.view()
         self._view = view
         self._params = params or DetectorViewParams()
-        self._edges_unit = self._params.toa_edges.get_edges()
-        self._slice = _histogram_slice(self._params.toa_edges, self._params.toa_range)
+        edges = self._params.get_active_edges()
+        self._wavelength = self._params.coordinate_mode == 'wavelength'
+        if self._wavelength:
+            # factory.py:134-142: wavelength mode needs the lookup table and
+            # the geometry (Ltotal per pixel)
+            if lookup_table is None:
+                raise ValueError('wavelength mode requires a lookup table')
+            if geometry is None:
+                raise ValueError('wavelength mode requires geometry for Ltotal computation')
+            engine_edges = edges.edges_in(lookup_table.unit)
+            self._spec_dim = WAVELENGTH_DIM
+        else:
+            engine_edges = edges.edges_ns()
+            self._spec_dim = TOA_DIM
+        self._lookup = lookup_table
+        self._beamline = (source_position, sample_position)
+        self._spec_edges = edges
+        self._edges_unit = edges.get_edges()
+        self._slice = _histogram_slice(edges, self._params.get_active_range())
         self._engine = BinningEngine(
-            toa_edges_ns=self._params.toa_edges.edges_ns(),
+            toa_edges_ns=engine_edges,
             out_lut=view.lut,
             pid_offset=view.pid_offset,
             n_screen=view.n_screen,
@@ -197,6 +234,8 @@ class GpuDetectorViewWorkflow:
             device=device,
             stream=stream,
         )
+        if self._wavelength:
+            self._set_coordinates()
         self._counter = 0
         self._geometry = _ContextState(geometry_key)
         self._context_keys: dict[str, Any] = {}
@@ -278,6 +317,21 @@ class GpuDetectorViewWorkflow:
             raise ValueError('a detector move cannot change the view shape')
         self._engine.set_lut(view.lut)
         self._view = view
+        if self._wavelength:
+            self._set_coordinates()  # Ltotal moved with the detector
+
+    def _set_coordinates(self) -> None:
+        """Per-pixel Ltotal of the current placement + the table -> engine."""
+        from .wavelength import distance_per_pid, pixel_ltotal
+
+        geo, tab = self._geometry_src, self._lookup
+        src, smp = self._beamline
+        lt = pixel_ltotal(geo.pixel_positions(), source_position=src, sample_position=smp)
+        d = distance_per_pid(geo.detector_number, lt, self._view.pid_offset,
+                             self._view.lut.shape[1])
+        self._engine.set_coordinate_lut(d, tab.table, dist0=tab.distance0,
+                                        dist_step=tab.distance_step, time0=tab.time0,
+                                        time_step=tab.time_step)
 
     def _update_rois(self, data: Mapping[str, Any]) -> None:
         """New ROI requests -> screen groups on the device (the reference's
@@ -295,7 +349,8 @@ class GpuDetectorViewWorkflow:
         self._engine.set_groups(_ROI_SLOT, groups)
 
     def _toa_coord(self) -> Variable:
-        return Variable((TOA_DIM,), self._edges_unit, self._params.toa_edges.unit)
+        """The spectral coord: TOA or wavelength edges in the edges' unit."""
+        return Variable((self._spec_dim,), self._edges_unit, self._spec_edges.unit)
 
     def _roi_spectra(self, which: str) -> DataArray:
         """``roi_spectra`` (roi.py:188-266): dims (roi, toa), int32 roi coord."""
@@ -304,9 +359,9 @@ class GpuDetectorViewWorkflow:
             values = self._engine.group_spectra(_ROI_SLOT, which)
         else:
             values = np.zeros((0, self._engine.n_toa_bins), dtype=self._engine.dtype)
-        return DataArray(values, ('roi', TOA_DIM), 'counts', {
+        return DataArray(values, ('roi', self._spec_dim), 'counts', {
             'roi': Variable(('roi',), np.asarray(self._roi_index, dtype=np.int32)),
-            TOA_DIM: self._toa_coord(),
+            self._spec_dim: self._toa_coord(),
         })
 
     def _roi_readback(self, name: str) -> DataArray:
@@ -341,8 +396,8 @@ class GpuDetectorViewWorkflow:
             vals = self._engine.group_spectra(_SPECTRUM_SLOT, 'cumulative')
             extra['spectrum_view'] = DataArray(
                 vals.reshape(*self._spectrum_shape, -1),
-                (*self._spectrum.output_dims, TOA_DIM), 'counts',
-                {TOA_DIM: self._toa_coord()},
+                (*self._spectrum.output_dims, self._spec_dim), 'counts',
+                {self._spec_dim: self._toa_coord()},
             )
         res = self._engine.finalize(images=True)
         dt = self._engine.dtype.type
@@ -371,9 +426,9 @@ class GpuDetectorViewWorkflow:
 
     def read_histogram(self, which: str = 'cumulative') -> DataArray:
         h = self._engine.read_histogram(which)
-        dims = (*self._view.screen_dims, TOA_DIM)
+        dims = (*self._view.screen_dims, self._spec_dim)
         shape = (*self._view.screen_shape, h.shape[-1])
-        return DataArray(h.reshape(shape), dims, 'counts', {TOA_DIM: self._toa_coord()})
+        return DataArray(h.reshape(shape), dims, 'counts', {self._spec_dim: self._toa_coord()})
 
     def clear(self) -> None:
         self._engine.clear()
@@ -399,10 +454,17 @@ class GpuDetectorViewFactory:
         positions: Mapping[str, np.ndarray] | None = None,
         pixel_shapes: Mapping[str, Mapping[str, Any]] | None = None,
         transforms: Mapping[str, Any] | None = None,
+        lookup_table: 'WavelengthLookupTable | None' = None,
+        source_position=(0.0, 0.0, -76.55),
+        sample_position=(0.0, 0.0, 0.0),
         out_dtype: str = 'float64',
         device: int = 0,
     ) -> None:
         self._dn = dict(detector_numbers)
+        # wavelength mode: the (Ltotal, time) table (the reference's
+        # LookupTableFilename) and the beamline for Ltotal
+        self._lookup = lookup_table
+        self._beamline = (source_position, sample_position)
         self._cfg = view_config
         self._coords = dict(projected_coords or {})
         # calibrated pixel positions (offsets in the component frame when a
@@ -457,6 +519,8 @@ class GpuDetectorViewFactory:
             source_name, None if geometry is not None else self.make_view(source_name), params,
             out_dtype=self._dtype, device=self._device, roi_support=roi_support,
             roi_keys=aux_source_names, spectrum_view=spectrum, geometry=geometry,
+            lookup_table=self._lookup, source_position=self._beamline[0],
+            sample_position=self._beamline[1],
         )
 
 

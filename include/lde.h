@@ -201,6 +201,32 @@ int lde_read_histogram(lde_handle *h, int32_t which, void *host_out);
  * resets them (lde_reset_cumulative) as the reference's accumulators do. */
 int lde_set_lut(lde_handle *h, const int32_t *out_lut);
 
+/* Wavelength mode (detector_view/factory.py:134-169 'wavelength',
+ * providers.py:77-95): the histogrammed event coordinate is looked up per event
+ * from its pixel's flight path and its time of arrival, then binned against
+ * the view's float64 edges (cfg->toa_edges, in the coordinate's unit) with
+ * the same half-open rule as TOA.  Bilinear interpolation on the regular grid
+ *   distance dist0 + i * dist_step (i < n_dist), time time0 + j * time_step ns
+ * of table[i * n_time + j]; NaN values, NaN distances and points outside the
+ * grid are dropped.  Arithmetic (restated in oracle/ and lde_coord.hip):
+ *   x = (d - dist0) * (1 / dist_step), i = min(floor x, n_dist - 2), fx = x - i
+ *   y = (t - time0) * (1 / time_step), j = min(floor y, n_time - 2), fy = y - j
+ *   c = a + fx * (b - a), a = v[i][j] + fy * (v[i][j+1] - v[i][j]),
+ *                         b = v[i+1][j] + fy * (v[i+1][j+1] - v[i+1][j])
+ * in float64 without fused multiply-adds.  Detector handles only; the first
+ * call comes before the first lde_accumulate (or after lde_clear), later calls
+ * (new pixel distances after a detector move, a new table) may come at any time
+ * and keep the counts already binned.  n_dist, n_time >= 2. */
+typedef struct lde_coord_lut {
+    const double *pixel_distance; /* [n_pixels] per pixel id (pid_offset + k) */
+    int64_t n_pixels;             /* must equal lut_len */
+    const double *table;          /* [n_dist * n_time] */
+    int32_t n_dist, n_time;
+    double dist0, dist_step;
+    double time0, time_step;      /* event unit (ns) */
+} lde_coord_lut;
+int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut);
+
 /* Reset semantics: clear both (workflow.clear / Job.reset) or drop the
  * cumulative and window because the geometry coord changed
  * (NoCopyAccumulator._reset_if_geometry_changed, accumulators.py:116-131). */

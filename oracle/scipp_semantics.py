@@ -217,6 +217,55 @@ def detector_histogram(
     return counts.reshape(n_screen, t).astype(dtype)
 
 
+def coordinate_lookup(distance: np.ndarray, toa: np.ndarray, table: np.ndarray,
+                      dist0: float, dist_step: float, time0: float,
+                      time_step: float) -> np.ndarray:
+    """Wavelength-mode event coordinate (detector_view/factory.py:134-169,
+    providers.py:77-95): bilinear lookup of ``table`` (n_dist x n_time) at the
+    event's pixel distance and time of arrival; NaN where the distance is NaN
+    or either point lies outside the grid.
+
+    essreduce's ``GenericUnwrapWorkflow`` (the table's producer and
+    interpolator) is not in /root/reference, so this restates the documented
+    engine arithmetic (include/lde.h ``lde_set_coord_lut``) step for step in
+    float64 -- numpy evaluates each ``a + f * (b - a)`` as a rounded product
+    then a rounded sum, the unfused order the kernel is compiled to.  Parity
+    with the reference's own table interpolation is unpinned.
+    """
+    tab = np.asarray(table, dtype=np.float64)
+    nd, nt = tab.shape
+    d = np.asarray(distance, dtype=np.float64)
+    x = (d - dist0) * (1.0 / dist_step)
+    okx = (x >= 0.0) & (x <= nd - 1)
+    i = np.minimum(np.floor(np.where(okx, x, 0.0)), nd - 2).astype(np.int64)
+    fx = x - i
+    y = (np.asarray(toa).astype(np.float64) - time0) * (1.0 / time_step)
+    oky = (y >= 0.0) & (y <= nt - 1)
+    j = np.minimum(np.floor(np.where(oky, y, 0.0)), nt - 2).astype(np.int64)
+    fy = y - j
+    v00 = tab[i, j]
+    v01 = tab[i, j + 1]
+    v10 = tab[i + 1, j]
+    v11 = tab[i + 1, j + 1]
+    a = v00 + fy * (v01 - v00)
+    b = v10 + fy * (v11 - v10)
+    c = a + fx * (b - a)
+    return np.where(okx & oky, c, np.nan)
+
+
+def wavelength_mode(ltotal: np.ndarray, table: np.ndarray, dist0: float, dist_step: float,
+                    time0: float, time_step: float) -> Callable:
+    """``OracleDetectorView.coordinate`` for wavelength mode: each event's
+    pixel ``Ltotal`` (row-major pixel order) and TOA -> ``coordinate_lookup``."""
+    lt = np.asarray(ltotal, dtype=np.float64).ravel()
+
+    def coordinate(pix: np.ndarray, toa: np.ndarray) -> np.ndarray:
+        d = np.where(pix >= 0, lt[np.maximum(pix, 0)], np.nan)
+        return coordinate_lookup(d, toa, table, dist0, dist_step, time0, time_step)
+
+    return coordinate
+
+
 def monitor_histogram(toa: np.ndarray, toa_edges_ns: np.ndarray) -> np.ndarray:
     """``_histogram_monitor`` event mode (monitor_workflow.py:90-100)."""
     tb = hist_bin_index(toa, toa_edges_ns)
@@ -356,6 +405,9 @@ class OracleDetectorView:
     toa_edges_ns: np.ndarray
     toa_slice: tuple[int, int] | None = None  # bin range of HistogramSlice
     dtype: type = np.float64
+    # wavelength mode: (pixel index, toa) -> event coordinate, binned on
+    # ``toa_edges_ns`` (then in the coordinate's unit); see wavelength_mode()
+    coordinate: Callable | None = None
     _counter: int = 0
     _acc: AccumulatorPair = field(default_factory=AccumulatorPair)
 
@@ -365,11 +417,14 @@ class OracleDetectorView:
 
     def batch_histogram(self, pid, toa, replica: int) -> np.ndarray:
         pix = pixel_index(np.asarray(pid), self.detector_number)
+        values = np.asarray(toa)
+        if self.coordinate is not None:
+            values = self.coordinate(pix, values)
         return detector_histogram(
             self.pixel_screen[replica],
             self.n_screen,
             pix,
-            np.asarray(toa),
+            values,
             self.toa_edges_ns,
             self.dtype,
         )

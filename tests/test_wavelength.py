@@ -1,0 +1,131 @@
+"""Wavelength mode on the CPU: the oracle's coordinate lookup, the host-side
+inputs (Ltotal, per-pid distances, edges) and the workflow's mode checks
+(detector_view/factory.py:134-169, detector_view_specs.py:53-124)."""
+
+import numpy as np
+import pytest
+
+from esslivedata_amd import synthetic, wavelength
+from esslivedata_amd.edges import WavelengthEdges
+from esslivedata_amd.workflows import DetectorViewParams, GpuDetectorViewWorkflow
+from oracle import scipp_semantics as ora
+
+
+def _grid():
+    # steps that are exact binary fractions: grid nodes map to integer x, y
+    d0, dd, t0, dt = 10.0, 0.25, 0.0, 1024.0
+    nd, nt = 9, 33
+    rng = np.random.default_rng(3)
+    return rng.uniform(1, 5, (nd, nt)), d0, dd, t0, dt
+
+
+def test_lookup_hits_grid_nodes_exactly():
+    tab, d0, dd, t0, dt = _grid()
+    i, j = np.meshgrid(np.arange(9), np.arange(33), indexing='ij')
+    d = d0 + dd * i.ravel()
+    t = (t0 + dt * j.ravel()).astype(np.int32)
+    c = ora.coordinate_lookup(d, t, tab, d0, dd, t0, dt)
+    np.testing.assert_array_equal(c, tab.ravel())
+
+
+def test_lookup_reproduces_bilinear_functions():
+    d0, dd, t0, dt = 10.0, 0.25, 0.0, 1024.0
+    dg = d0 + dd * np.arange(9)
+    tg = t0 + dt * np.arange(33)
+    f = lambda d, t: 1.5 + 0.25 * d - 3e-5 * t + 2e-6 * d * t  # noqa: E731
+    tab = f(dg[:, None], tg[None, :])
+    rng = np.random.default_rng(0)
+    d = rng.uniform(dg[0], dg[-1], 10000)
+    t = rng.integers(0, int(tg[-1]) + 1, 10000).astype(np.int32)
+    c = ora.coordinate_lookup(d, t, tab, d0, dd, t0, dt)
+    np.testing.assert_allclose(c, f(d, t.astype(np.float64)), rtol=1e-12)
+
+
+def test_lookup_drops_outside_and_nan():
+    tab, d0, dd, t0, dt = _grid()
+    d = np.array([d0 - 1e-9, d0 + 8 * dd + 1e-9, np.nan, d0, d0 + 8 * dd, d0])
+    t = np.array([0, 0, 0, 32 * 1024, 32 * 1024, 32 * 1024 + 1], dtype=np.int32)
+    c = ora.coordinate_lookup(d, t, tab, d0, dd, t0, dt)
+    assert np.isnan(c[[0, 1, 2, 5]]).all()
+    assert c[3] == tab[0, 32] and c[4] == tab[8, 32]
+    tab2 = tab.copy()
+    tab2[2, 3] = np.nan  # NaN table cells poison their neighbourhood only
+    c2 = ora.coordinate_lookup(np.array([d0 + 2.5 * dd, d0 + 5 * dd]),
+                               np.array([3 * 1024 + 10, 10], np.int32), tab2, d0, dd, t0, dt)
+    assert np.isnan(c2[0]) and not np.isnan(c2[1])
+
+
+def test_ideal_table_is_direct_flight():
+    tab = synthetic.dream_wavelength_table()
+    assert tab.table.shape == (13, 287)
+    assert tab.time_step == 250000.0
+    # lambda = h/m_n * t / L: 10 ms over 77.5 m
+    c = ora.coordinate_lookup(np.array([77.5]), np.array([10_000_000], np.int32), tab.table,
+                              tab.distance0, tab.distance_step, tab.time0, tab.time_step)
+    assert c[0] == pytest.approx(wavelength.H_OVER_MN * 0.01 / 77.5, rel=1e-12)
+
+
+def test_ltotal_and_distance_per_pid():
+    inst = synthetic.dream_mantle(n_replicas=1)
+    lt = wavelength.pixel_ltotal(inst.positions, source_position=(0, 0, -synthetic.DREAM_L1))
+    l2 = np.hypot(1.1, inst.positions[:, 2])
+    np.testing.assert_allclose(lt, synthetic.DREAM_L1 + l2, rtol=1e-14)
+    d = wavelength.distance_per_pid(inst.detector_number, lt, 229376, 720896 - 229376 + 2)
+    assert np.isnan(d[0]) and np.isnan(d[-1])
+    np.testing.assert_array_equal(d[1:-1], lt)
+
+
+def test_wavelength_edges_model():
+    e = WavelengthEdges()
+    np.testing.assert_array_equal(e.get_edges(), np.linspace(1.0, 10.0, 101))
+    nm = WavelengthEdges(start=0.1, stop=1.0, num_bins=9, unit='nm')
+    np.testing.assert_array_equal(nm.edges_in('Å'), np.linspace(0.1, 1.0, 10) * 10.0)
+    with pytest.raises(ValueError):
+        WavelengthEdges(start=2.0, stop=1.0)
+    with pytest.raises(ValueError):
+        WavelengthEdges(unit='m/s')
+
+
+def test_params_active_edges_and_mode_checks():
+    p = DetectorViewParams(coordinate_mode='wavelength', wavelength_range=(2.0, 4.0))
+    assert p.get_active_edges() is p.wavelength_edges
+    assert p.get_active_range() == (2.0, 4.0)
+    q = DetectorViewParams()
+    assert q.get_active_edges() is q.toa_edges
+    with pytest.raises(ValueError, match='coordinate_mode'):
+        DetectorViewParams(coordinate_mode='dspacing')
+    inst = synthetic.dream_mantle(n_replicas=1)
+    from esslivedata_amd.projection import geometric_lut
+    view = geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    # factory.py:134-142: no table / no geometry -> refused before any device work
+    with pytest.raises(ValueError, match='lookup table'):
+        GpuDetectorViewWorkflow('dream', view, p)
+    with pytest.raises(ValueError, match='geometry'):
+        GpuDetectorViewWorkflow('dream', view, p, lookup_table=synthetic.dream_wavelength_table())
+
+
+def test_oracle_view_wavelength_mode_counts():
+    """OracleDetectorView in wavelength mode: the looked-up coordinate is the
+    direct-flight wavelength (linear in t, 1/L interpolated over 5 cm: relative
+    error < 2e-7) and the histogram holds every in-range event."""
+    inst = synthetic.dream_mantle(n_replicas=1)
+    tab = synthetic.dream_wavelength_table()
+    lt = wavelength.pixel_ltotal(inst.positions, source_position=(0, 0, -synthetic.DREAM_L1))
+    edges = WavelengthEdges(start=0.2, stop=3.6, num_bins=50).get_edges()
+    screen = np.arange(inst.detector_number.size, dtype=np.int64)[None]
+    coord = ora.wavelength_mode(lt, tab.table, tab.distance0, tab.distance_step, tab.time0,
+                                tab.time_step)
+    o = ora.OracleDetectorView(inst.detector_number, screen, (inst.detector_number.size,), edges,
+                               coordinate=coord)
+    pid, toa = synthetic.dream_events(20000, inst, seed=5)
+    pid[:10] = 1  # unknown ids: no distance, dropped
+    o.accumulate(pid, toa)
+    h = o.finalize()['histogram_current']
+    pix = ora.pixel_index(pid, inst.detector_number)
+    c = coord(pix, toa)
+    assert np.isnan(c[:10]).all()
+    ok = (pix >= 0) & (toa >= 0) & (toa <= 71.5e6)
+    assert np.isnan(c[~ok]).all()
+    lam = wavelength.H_OVER_MN * toa[ok] * 1e-9 / lt[pix[ok]]
+    np.testing.assert_allclose(c[ok], lam, rtol=2e-7)
+    assert h.sum() == ((c >= edges[0]) & (c < edges[-1])).sum()
