@@ -237,7 +237,11 @@ def main():
     # time); the per-kernel breakdown comes from a few extra steps afterwards
     strat = eng.info()['last_strategy']
     dom = {'split': 'split', 'paged': 'paged', 'partition': 'partition', 'atomic': 'atomic'}.get(strat, 'split')
-    eng.timing_select([dom, 'binning'] if not os.environ.get('LDE_BENCH_UNTIMED') else [])
+    # only the dominant kernel is timed in the timed region: its events are
+    # stamped by its own dispatch (no marker packets, no extra host calls in
+    # front of the launch); the binning-sequence span, whose start marker
+    # costs host time before the first launch, comes from the extra steps
+    eng.timing_select([dom] if not os.environ.get('LDE_BENCH_UNTIMED') else [])
     if world > 1:
         dist.barrier()
     eng.timing_enable(True)
@@ -255,7 +259,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    timed = {k: eng.kernel_stats(k) for k in (dom, 'binning')}
+    timed = {dom: eng.kernel_stats(dom)}
 
     names = ('atomic', 'partition', 'tile_accumulate', 'plan', 'paged', 'page_plan',
              'page_accumulate', 'split', 'split_aux', 'binning', 'finalize')
@@ -328,7 +332,7 @@ def main():
     avg_s = (ms / max(launches, 1)) / 1e3
     achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
     traffic = profiled_traffic(args.workload, dom)
-    bin_ms, bin_n = timed['binning']
+    bin_ms, bin_n = stats['binning']  # the extra steps
     pipeline_gbs = BYTES_PER_EVENT * n_step / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0
 
     result = {
@@ -376,7 +380,8 @@ def main():
             'step_frac': step_gbs / HBM_PEAK_GBS,
             'lds': profiled_lds(args.workload, dom),
             'kernel_ms': {k: v[0] / max(v[1], 1) for k, v in stats.items() if v[1]},
-            'kernel_ms_note': 'per-kernel breakdown from 3 extra steps after the timed region',
+            'kernel_ms_note': 'per-kernel breakdown and pipeline_* (the whole binning sequence of '
+                              'one accumulate) from 3 extra steps after the timed region',
         },
     }
     if e2e is not None:

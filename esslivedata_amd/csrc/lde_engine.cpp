@@ -156,6 +156,8 @@ struct lde_handle {
     // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
     bool lds_ctab = true, karg_segs = true;
     int sieve_ablate = 0;
+    bool early_gather = false;  // LDE_EARLY_GATHER
+    bool sieve_pack = false;    // LDE_SIEVE_PACK
     uint32_t ttab_cap = 0;
     int ttab_shift = 0;
     lde::ChunkPtrs *d_chunk_tab = nullptr;
@@ -775,6 +777,8 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         sa.n_tiles = h->n_tiles;
         sa.cold_tcnt = h->d_cold_tcnt;
         sa.ablate = h->sieve_ablate;
+        sa.early_gather = h->early_gather ? 1 : 0;
+        sa.pack = h->sieve_pack ? 1 : 0;
         {
             // k_sieve is timed by its own dispatch (start/stop events stamped
             // by hipExtLaunchKernelGGL): no marker packets around it
@@ -787,14 +791,17 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                     ea = nullptr;
                 }
             }
-            // the sieve builds its chunk table in LDS from descriptors passed
-            // as kernel arguments (no launch in front of it) when they fit
+            // the sieve builds its chunk table in LDS (no launch in front of
+            // it) when the block's chunk range fits, from descriptors passed
+            // as kernel arguments when they fit too, else from d_segs
             const long long per_block = (chunks + a.grid - 1) / a.grid;
-            sa.lds_ctab = (long long)sd.size() <= lde::kKargSegs && per_block + 1 <= lde::kSieveLdsChunks &&
-                          h->lds_ctab;
+            sa.lds_ctab = per_block + 1 <= lde::kSieveLdsChunks && h->lds_ctab;
+            sa.karg = (long long)sd.size() <= lde::kKargSegs;
             sa.dummy = h->d_sieve_dummy;
-            if (sa.lds_ctab) {
+            if (sa.lds_ctab && sa.karg) {
                 for (size_t i = 0; i < sd.size(); ++i) sa.sk.s[i] = sd[i];
+            } else if (sa.lds_ctab) {
+                if (int rc = upload()) return rc;
             } else if (!uploaded && (long long)sd.size() <= lde::kKargSegs && h->karg_segs) {
                 HIPCALL(h, lde::launch_chunk_tab_karg(sd.data(), a.n_segs, chunks, h->d_sieve_dummy,
                                                       h->d_chunk_tab, h->d_segs, h->stream));
@@ -1348,6 +1355,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->lds_ctab = env_ll("LDE_LDS_CTAB", 1) != 0;
         h->karg_segs = env_ll("LDE_KARG_SEGS", 1) != 0;
         h->sieve_ablate = (int)env_ll("LDE_SIEVE_ABLATE", 0);
+        h->early_gather = env_ll("LDE_EARLY_GATHER", 0) != 0;
+        h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);
         h->auto_partition = (int)env_ll("LDE_AUTO_PARTITION", LDE_STRATEGY_PAGED);

@@ -177,7 +177,10 @@ struct SieveArgs {
     int n_segs;
     long long n_chunks;
     const ChunkPtrs *chunk_tab;  // [n_chunks + 1]; deferred chunks and entry n_chunks: dummy
-    int lds_ctab;                // 1: build the block's chunk table in LDS from sk (no chunk_tab)
+    int lds_ctab;                // 1: build the block's chunk table in LDS (no chunk_tab)
+    int karg;                    // lds_ctab: descriptors from sk (else from segs)
+    int early_gather;            // 1: gathers issued one iteration before they are binned
+    int pack;                    // 1: TOA bin packed into the table word at the gather
     SegKarg sk;                  // lds_ctab: the message descriptors (n_segs <= kKargSegs)
     const int *dummy;            // the all-invalid chunk
     const uint32_t *glut;  // this replica's pixel words, L + 1 entries (entry L = 0)

@@ -178,8 +178,18 @@ __global__ __launch_bounds__(256) void k_chunk_tab_karg(SegKarg sk, int n_segs, 
 // LDS atomics, 2 no gathers, 4 no cold stores, 8 no LDS probes, 16 every
 // gather lane out of range, 32 every gather lane on the first two words,
 // 64 cold stores exec-masked to the lanes with keys (results exact), 128
-// cold stores every other half only
-template <int ABL>
+// cold stores every other half only; 256 (exact) the early-gather pipeline;
+// 512 / 1024: 8 extra VALU ops / one extra LDS read per event (load probes);
+// 2048 (exact): cold-key stores deferred behind the next gathers and loads;
+// 4096: loads only (stream skeleton); 8192 (exact): cached instead of
+// nontemporal event loads
+// GCT: the chunk table comes from global memory (k_chunk_tab), for blocks
+// whose chunk range exceeds kSieveLdsChunks.  Otherwise each block builds its
+// own in LDS, and GCT is a template switch rather than a runtime branch so
+// that the loop has one fetch path: with both, the compiler's wait-count
+// insertion merges the paths and waits for every outstanding load (vmcnt(0))
+// once per iteration, which serialized the stream (measured 0.34 -> 0.xx ms).
+template <int ABL, int GCT>
 __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // static, so LDS addresses need no runtime base (one block per CU anyway)
     __shared__ __attribute__((aligned(16))) uint32_t sm[kSplitSmemMax / 4];
@@ -210,7 +220,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     for (uint32_t i = (uint32_t)tid; i < kSieveStage * (kSplitThreads / 64); i += kSplitThreads)
         sm[o_stg + i] = 0xFFFFFFFFu;
     for (int i = tid; i < kColdGroups * align4(a.n_tiles); i += kSplitThreads) sm[o_tcnt + i] = 0;
-    if (a.lds_ctab) {  // descriptors from the kernel arguments (static indices)
+    if (!GCT && a.karg) {  // descriptors from the kernel arguments (static indices)
 #pragma unroll
         for (int i = 0; i < kKargSegs; ++i)
             if (tid == i && i < a.n_segs) s_seg[i] = a.sk.s[i];
@@ -247,17 +257,20 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // vector load (in-order vmcnt) and read back with readlane; chunks outside
     // [cb, ce) and deferred chunks map to the all-invalid dummy chunk
     const uint32_t *ctab = reinterpret_cast<const uint32_t *>(a.chunk_tab);
-    if (a.lds_ctab) {
+    if (!GCT) {
         // entry j = chunk cb + j of this block (entry ce - cb: the dummy chunk);
         // replaces the k_chunk_tab launch in front of the sieve
+        const SegDesc *sg = a.karg ? s_seg : a.segs;
         for (long long j = tid; j <= ce - cb; j += kSplitThreads) {
             const long long c = cb + j;
             ChunkPtrs r{a.dummy, a.dummy};
             if (c < ce) {
-                int si = 0;
-                for (int i = 1; i < a.n_segs; ++i)
-                    if (s_seg[i].chunk0 <= c) si = i;
-                const SegDesc sd = s_seg[si];
+                int lo = 0, hi = a.n_segs - 1;  // last segment with chunk0 <= c
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (sg[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+                }
+                const SegDesc sd = sg[lo];
                 const long long base = (c - sd.chunk0) * kChunk;
                 if (((((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0) && base + kChunk <= sd.n) {
                     r.pid = sd.pid + base;
@@ -270,7 +283,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     }
     const uint32_t o_ctab4 = o_ctab * 4u;
     auto fetch = [&](long long c) __attribute__((always_inline)) {
-        if (a.lds_ctab) {
+        if (!GCT) {
             const uint32_t j = (uint32_t)((c < ce ? c : ce) - cb);
             return lds_at(sm, o_ctab4 + ((j * 4u + (uint32_t)(lane & 3)) << 2));
         }
@@ -291,8 +304,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
 #pragma unroll
         for (int j = 0; j < kEPT / 4; ++j) {
             const int off = (j * kSplitThreads + tid) * 4;
-            const v4i pv = ld_stream4(pp + off);
-            const v4i tv = ld_stream4(tq + off);
+            const v4i pv = (ABL & 8192) ? *(const g_v4i *)(pp + off) : ld_stream4(pp + off);
+            const v4i tv = (ABL & 8192) ? *(const g_v4i *)(tq + off) : ld_stream4(tq + off);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 p[j * 4 + q] = pv[q];
@@ -323,7 +336,11 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // stage 2b: tag check, one gather per event (a table hit or an
     // out-of-range pixel loads out of range: no request, returns 0); w -> the
     // table word of hits (0 otherwise), qs -> the gathered word
-    auto finish = [&](uint32_t (&w)[kEPT], uint32_t (&qs)[kEPT]) __attribute__((always_inline)) {
+    // PACK (ABL & 65536): the TOA bin is computed here and kept in the hit
+    // word's tag bits (free once the tag has been checked; the gathered words
+    // have tag 0), so dc / tw die here and bin() reads one word per event
+    auto finish = [&](uint32_t (&w)[kEPT], uint32_t (&qs)[kEPT], const uint32_t (&dc)[kEPT],
+                      const uint32_t (&tw)[kEPT]) __attribute__((always_inline)) {
 #pragma unroll
         for (int e = 0; e < kEPT; ++e) {
             const unsigned long long hit =
@@ -331,7 +348,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             uint32_t off = vsel(hit, kOOBi, min(qs[e], Lc) << 2);
             if (ABL & 16) off = kOOB | (off & 4u);
             if (ABL & 32) off = off & 4u;
-            w[e] = vsel(hit, w[e], 0u);
+            if (ABL & 65536) {
+                // T <= kSieveMaxT (254): bins >= 255 (past the edges) stay dropped
+                const uint32_t b = min((tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u), 255u);
+                w[e] = vsel(hit, w[e] & ~(0xFFu << kSieveTagShift), 0u) | (b << kSieveTagShift);
+            } else {
+                w[e] = vsel(hit, w[e], 0u);
+            }
             qs[e] = (ABL & 2) ? (off & 0x3u) : __builtin_amdgcn_raw_buffer_load_b32(glut, (int)off, 0, 0);
         }
     };
@@ -345,7 +368,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // to -1, so the <= 3 pad keys of round4(count) are dropped by the sort.
     v4u pend_kv = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     uint32_t pend_off = kOOB;
+    // ABL 2048 (exact): both halves' stores wait for flush(), issued after the
+    // next chunk's gathers and loads, so that waiting for those (vmcnt is in
+    // order and counts stores) never waits for a store's acknowledgement
+    v4u pend_kv1 = pend_kv;
+    uint32_t pend_off1 = kOOB;
     uint32_t wcur = 0;  // this wave's cold keys so far (wave-uniform)
+    uint32_t junk = 0;  // ABL 512/1024 probes: extra VALU / LDS work per event
     auto bin = [&](const uint32_t (&ws)[kEPT], const uint32_t (&g)[kEPT], const uint32_t (&dc)[kEPT],
                    const uint32_t (&tw)[kEPT]) __attribute__((always_inline)) {
 #pragma unroll
@@ -354,7 +383,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
 #pragma unroll
             for (int e = h * kEPT / 2; e < (h + 1) * kEPT / 2; ++e) {
                 const uint32_t v = ws[e] | g[e];
-                const uint32_t b = (tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u);
+                if (ABL & 512) {
+#pragma unroll
+                    for (int x = 0; x < 8; ++x) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(junk) : "v"(v));
+                }
+                if (ABL & 1024) junk += lds_at(sm, dum4 ^ ((v & 1u) << 2));
+                const uint32_t b = (ABL & 65536) ? ((v >> kSieveTagShift) & 0xFFu)
+                                                 : (tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u);
                 const uint32_t fl = v >> 30;
                 // hot rows start at LDS byte 0, so the scaled key is the hot
                 // counter's address; cold keys leave scaled by 4 as well
@@ -378,7 +413,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             }
             const uint32_t res = (tot + 3u) & ~3u;
             // the previous half's keys leave now (their LDS read is long done)
-            if (ABL & 64) {  // diagnostic: only the lanes that hold keys issue the store
+            if (ABL & 2048) {
+            } else if (ABL & 64) {  // diagnostic: only the lanes that hold keys issue the store
                 if (pend_off != kOOB) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
             } else if (ABL & 128) {  // diagnostic: every other half stores (keys lost)
                 if (h == 0) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
@@ -391,46 +427,136 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             const uint4 kv = *slot;
             *slot = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
             __builtin_amdgcn_wave_barrier();
-            pend_kv = v4u{kv.x, kv.y, kv.z, kv.w};
-            pend_off = 4u * (uint32_t)lane < res ? (wave_base + wcur + 4u * (uint32_t)lane) << 2 : kOOB;
+            const uint32_t off = 4u * (uint32_t)lane < res ? (wave_base + wcur + 4u * (uint32_t)lane) << 2 : kOOB;
+            if ((ABL & 2048) && h == 1) {
+                pend_kv1 = v4u{kv.x, kv.y, kv.z, kv.w};
+                pend_off1 = off;
+            } else {
+                pend_kv = v4u{kv.x, kv.y, kv.z, kv.w};
+                pend_off = off;
+            }
             wcur += res;
         }
     };
+    auto flush = [&]() __attribute__((always_inline)) {
+        if (ABL & 2048) {
+            __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(pend_kv1, cold, (int)pend_off1, 0, 0);
+            pend_off = pend_off1 = kOOB;
+        }
+    };
 
-    // ---- pipeline: chunk i is binned while chunk i+1 is probed (before) and
-    // gathered (after), chunks i+2, i+3 stream in and the descriptor of i+4 is
-    // fetched (register sets A/B and X/Y alternate)
+    // ---- pipeline (register sets A/B and X/Y alternate).
+    // ABL 256 (LDE_EARLY_GATHER): iteration i issues chunk i+1's gathers, bins chunk i
+    // (gathered one iteration ago), probes chunk i+2 and streams in chunk i+4,
+    // so a table-miss gather has a whole iteration to return; the probe's LDS
+    // latency is what is left exposed.  Otherwise chunk i is binned while
+    // chunk i+1 is probed (before) and gathered (after).
     int pA[kEPT], tA[kEPT], pB[kEPT], tB[kEPT];
     uint32_t wsX[kEPT], gX[kEPT], dX[kEPT], twX[kEPT];
     uint32_t wsY[kEPT], gY[kEPT], dY[kEPT], twY[kEPT];
-    if (cb < ce) {
+    if ((ABL & 16384) && cb < ce) {
+        // decomposition probe: the main loop with bin() replaced by folding
+        // the chunk's words into junk (+ finish() when ABL & 32768)
+        auto eat = [&](const uint32_t (&ws)[kEPT], const uint32_t (&g)[kEPT], const uint32_t (&dc)[kEPT],
+                       const uint32_t (&tw)[kEPT]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int e = 0; e < kEPT; ++e) junk ^= ws[e] ^ g[e] ^ dc[e] ^ tw[e];
+        };
         uint32_t dA = fetch(cb), dB = fetch(cb + 1);
         load(dA, pA, tA);
         load(dB, pB, tB);
         dA = fetch(cb + 2);
         dB = fetch(cb + 3);
         probe(pA, tA, wsX, gX, dX, twX);
-        finish(wsX, gX);
+        if (ABL & 32768) finish(wsX, gX, dX, twX);
+        load(dA, pA, tA);
+        dA = fetch(cb + 4);
+        for (long long c = cb; c < ce; c += 2) {
+            probe(pB, tB, wsY, gY, dY, twY);
+            eat(wsX, gX, dX, twX);
+            if (ABL & 32768) finish(wsY, gY, dY, twY);
+            load(dB, pB, tB);
+            dB = fetch(c + 5);
+            if (c + 1 >= ce) break;
+            probe(pA, tA, wsX, gX, dX, twX);
+            eat(wsY, gY, dY, twY);
+            if (ABL & 32768) finish(wsX, gX, dX, twX);
+            load(dA, pA, tA);
+            dA = fetch(c + 6);
+        }
+    } else if ((ABL & 4096) && cb < ce) {  // stream skeleton: loads only
+        uint32_t dA = fetch(cb), dB = fetch(cb + 1);
+        load(dA, pA, tA);
+        load(dB, pB, tB);
+        dA = fetch(cb + 2);
+        dB = fetch(cb + 3);
+        for (long long c = cb; c < ce; c += 2) {
+#pragma unroll
+            for (int e = 0; e < kEPT; ++e) junk ^= (uint32_t)(pA[e] ^ tA[e]);
+            load(dA, pA, tA);
+            dA = fetch(c + 4);
+#pragma unroll
+            for (int e = 0; e < kEPT; ++e) junk ^= (uint32_t)(pB[e] ^ tB[e]);
+            load(dB, pB, tB);
+            dB = fetch(c + 5);
+        }
+    } else if ((ABL & 256) && cb < ce) {
+        uint32_t dA = fetch(cb), dB = fetch(cb + 1);
+        load(dA, pA, tA);
+        load(dB, pB, tB);
+        dA = fetch(cb + 2);
+        dB = fetch(cb + 3);
+        probe(pA, tA, wsX, gX, dX, twX);  // chunk cb
+        finish(wsX, gX, dX, twX);
+        load(dA, pA, tA);  // chunk cb + 2
+        dA = fetch(cb + 4);
+        probe(pB, tB, wsY, gY, dY, twY);  // chunk cb + 1
+        load(dB, pB, tB);  // chunk cb + 3
+        dB = fetch(cb + 5);
+        for (long long c = cb; c < ce; c += 2) {
+            finish(wsY, gY, dY, twY);                   // chunk c + 1
+            bin(wsX, gX, dX, twX);             // chunk c
+            probe(pA, tA, wsX, gX, dX, twX);  // chunk c + 2
+            load(dA, pA, tA);                  // chunk c + 4
+            dA = fetch(c + 6);
+            if (c + 1 >= ce) break;
+            finish(wsX, gX, dX, twX);                   // chunk c + 2
+            bin(wsY, gY, dY, twY);             // chunk c + 1
+            probe(pB, tB, wsY, gY, dY, twY);  // chunk c + 3
+            load(dB, pB, tB);                  // chunk c + 5
+            dB = fetch(c + 7);
+        }
+    } else if (cb < ce) {
+        uint32_t dA = fetch(cb), dB = fetch(cb + 1);
+        load(dA, pA, tA);
+        load(dB, pB, tB);
+        dA = fetch(cb + 2);
+        dB = fetch(cb + 3);
+        probe(pA, tA, wsX, gX, dX, twX);
+        finish(wsX, gX, dX, twX);
         load(dA, pA, tA);
         dA = fetch(cb + 4);
         for (long long c = cb; c < ce; c += 2) {
             probe(pB, tB, wsY, gY, dY, twY);  // chunk c + 1
             bin(wsX, gX, dX, twX);             // chunk c
-            finish(wsY, gY);
+            finish(wsY, gY, dY, twY);
             load(dB, pB, tB);  // chunk c + 3
+            flush();           // chunk c's keys
             dB = fetch(c + 5);
             if (c + 1 >= ce) break;
             probe(pA, tA, wsX, gX, dX, twX);  // chunk c + 2
             bin(wsY, gY, dY, twY);             // chunk c + 1
-            finish(wsX, gX);
+            finish(wsX, gX, dX, twX);
             load(dA, pA, tA);  // chunk c + 4
+            flush();           // chunk c + 1's keys
             dA = fetch(c + 6);
         }
     }
 
     // ---- deferred chunks: element-wise loads of a clamped index
     if (cb < ce) {
-        const SegDesc *segs = a.lds_ctab ? s_seg : a.segs;
+        const SegDesc *segs = (!GCT && a.karg) ? s_seg : a.segs;
         int si = 0;
         {
             int lo = 0, hi = a.n_segs - 1;
@@ -461,12 +587,14 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 }
             }
             probe(p, t, wsX, gX, dX, twX);
-            finish(wsX, gX);
+            finish(wsX, gX, dX, twX);
             bin(wsX, gX, dX, twX);
+            flush();
         }
     }
     // the last half's keys
     if (!(ABL & 4)) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+    if (ABL & (512 | 1024 | 4096 | 16384)) sm[o_dum + lane] = junk;
     if (lane == 0) a.cold_cnt[(size_t)blockIdx.x * (kSplitThreads / 64) + (tid >> 6)] = wcur;
     __syncthreads();
     uint32_t *dst = a.hot_part + (size_t)blockIdx.x * a.hot_words;
@@ -881,24 +1009,29 @@ static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, h
                                  hipEvent_t stop) {
     if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles) > kSplitSmemMax)
         return hipErrorInvalidValue;
-    hipExtLaunchKernelGGL(k_sieve<ABL>, dim3(grid), dim3(kSplitThreads), 0, st, start, stop, 0,
-                          a);  // static LDS
+    if (a.lds_ctab)
+        hipExtLaunchKernelGGL(k_sieve<ABL, 0>, dim3(grid), dim3(kSplitThreads), 0, st, start, stop, 0,
+                              a);  // static LDS
+    else
+        hipExtLaunchKernelGGL(k_sieve<ABL, 1>, dim3(grid), dim3(kSplitThreads), 0, st, start, stop, 0,
+                              a);
     return hipGetLastError();
 }
 
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                         hipEvent_t stop) {
-    switch (a.ablate) {
-    case 1: return launch_sieve_t<1>(a, grid, st, start, stop);
-    case 2: return launch_sieve_t<2>(a, grid, st, start, stop);
-    case 4: return launch_sieve_t<4>(a, grid, st, start, stop);
-    case 7: return launch_sieve_t<7>(a, grid, st, start, stop);
-    case 15: return launch_sieve_t<15>(a, grid, st, start, stop);
-    case 16: return launch_sieve_t<16>(a, grid, st, start, stop);
-    case 32: return launch_sieve_t<32>(a, grid, st, start, stop);
-    case 64: return launch_sieve_t<64>(a, grid, st, start, stop);
-    case 128: return launch_sieve_t<128>(a, grid, st, start, stop);
-    default: return launch_sieve_t<0>(a, grid, st, start, stop);
+    const int mode = a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0);
+    switch (mode) {
+#define LDE_SIEVE_MODE(m) \
+    case m: return launch_sieve_t<m>(a, grid, st, start, stop);
+    LDE_SIEVE_MODE(0) LDE_SIEVE_MODE(1) LDE_SIEVE_MODE(2) LDE_SIEVE_MODE(4) LDE_SIEVE_MODE(6)
+    LDE_SIEVE_MODE(8) LDE_SIEVE_MODE(16) LDE_SIEVE_MODE(32) LDE_SIEVE_MODE(64) LDE_SIEVE_MODE(128)
+    LDE_SIEVE_MODE(256) LDE_SIEVE_MODE(512) LDE_SIEVE_MODE(1024) LDE_SIEVE_MODE(2048)
+    LDE_SIEVE_MODE(4096) LDE_SIEVE_MODE(8192) LDE_SIEVE_MODE(12288) LDE_SIEVE_MODE(16384)
+    LDE_SIEVE_MODE(49152) LDE_SIEVE_MODE(65536) LDE_SIEVE_MODE(65536 | 256)
+    LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048)
+#undef LDE_SIEVE_MODE
+    default: return hipErrorInvalidValue;
     }
 }
 

@@ -37,6 +37,11 @@ VARIANTS = [
     {'LDE_SIEVE': '0', 'LDE_PIXEL_CACHE_BITS': '6', 'LDE_SPLIT_GRID': '17'},
     # one sieve block: its chunk range exceeds the LDS chunk table (global table)
     {'LDE_SPLIT_GRID': '1'},
+    # sieve pipeline variants (exact): TOA bin packed into the table word,
+    # gathers issued an iteration early, cold-key stores deferred
+    {'LDE_SIEVE_PACK': '1'},
+    {'LDE_SIEVE_PACK': '1', 'LDE_EARLY_GATHER': '1'},
+    {'LDE_SIEVE_ABLATE': '2048'},
 ]
 
 
