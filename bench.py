@@ -221,14 +221,23 @@ def main():
     messages = [(pid[p * n_pulse : (p + 1) * n_pulse], toa[p * n_pulse : (p + 1) * n_pulse])
                 for p in range(args.pulses)]
 
-    def step(i: int):
-        eng.stage_tensors_batch(messages)
+    # A step bins the batch staged before it, then stages the next batch's
+    # messages and finalizes the window: the next pulses' messages reach the
+    # staging accumulator while the window's outputs are read back, as in the
+    # service, where messages arrive independently of the publish cadence.
+    # Every step stages one batch, so the timed region holds K stagings, K
+    # accumulates and K finalizes; the batch staged by the last step is binned
+    # by the first step after the region.
+    def step(i: int, stage_next: bool = True):
         eng.accumulate(i % view.n_replicas)
+        if stage_next:
+            eng.stage_tensors_batch(messages)
         if reducer is not None:
             reducer.finalize()
         else:
             eng.finalize(images=True)
 
+    eng.stage_tensors_batch(messages)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
@@ -266,7 +275,7 @@ def main():
     eng.timing_select(None)
     eng.timing_enable(True)
     for i in range(3):
-        step(args.warmup + args.steps + i)
+        step(args.warmup + args.steps + i, stage_next=i < 2)  # nothing left staged
     torch.cuda.synchronize(dev)
     stats = {k: eng.kernel_stats(k) for k in names}
     info = eng.info()

@@ -1228,7 +1228,9 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         CREATE_CHECK(ensure_win64(h));
     }
     CREATE_CHECK(dev_alloc(h, &h->d_tot4, 4 + 4 * 8192));  // totals + per-block partials
-    h->pack_bytes = (size_t)h->S * 16 + 48;
+    // [current image S x 8][cumulative image S x 8][totals 32][overflow 16]
+    // [per-block total partials, kHostPartials x 32] (summed on the host)
+    h->pack_bytes = (size_t)h->S * 16 + 48 + 32 * (size_t)lde::kHostPartials;
     CREATE_CHECK(dev_alloc(h, &h->d_pack, h->pack_bytes));
     CREATE_HIP(hipHostMalloc((void **)&h->h_pack, h->pack_bytes, hipHostMallocDefault));
     h->d_img_cur = h->d_pack;
@@ -1647,9 +1649,11 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
             HIPCALL(h, hipMemcpyAsync(out->cumulative_hist, h->d_cumf, nb * 4,
                                       hipMemcpyDeviceToHost, h->stream));
     }
+    int n_parts = 0;
     {
         Timed tm(h, LDE_K_FINALIZE);
-        // totals and the overflow flag land in the pack tail from k_sum_totals
+        // the per-block total partials and the overflow flag land in the
+        // pack (summed here on the host: no k_sum_totals launch and gap)
         unsigned char *d_tail = h->d_pack + (size_t)h->S * 16;
         HIPCALL(h, lde::launch_finalize(
                        f32 ? 1 : 0, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
@@ -1657,12 +1661,13 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
                        h->range_hi, (!f32 && out->current_image) ? h->d_img_cur : nullptr,
                        (!f32 && out->cumulative_image) ? h->d_img_cum : nullptr, h->d_tot4,
                        (unsigned long long *)d_tail, h->d_overflow, (uint32_t *)(d_tail + 32),
-                       h->stream));
+                       h->stream, (unsigned long long *)(d_tail + 48), &n_parts));
     }
     const size_t isz = f32 ? 4 : 8;
-    // images, totals and the overflow flag leave in one pinned D2H copy
+    // images, partials and the overflow flag leave in one pinned D2H copy
     // (separate copies into pageable memory cost ~25 us each)
-    HIPCALL(h, hipMemcpyAsync(h->h_pack, h->d_pack, h->pack_bytes, hipMemcpyDeviceToHost, h->stream));
+    HIPCALL(h, hipMemcpyAsync(h->h_pack, h->d_pack, (size_t)h->S * 16 + 48 + 32 * (size_t)n_parts,
+                              hipMemcpyDeviceToHost, h->stream));
     std::vector<unsigned long long> tmp;
     if (!f32 && (want_cur_hist || want_cum_hist)) tmp.resize(nb);
     if (!f32 && want_cur_hist) {
@@ -1684,8 +1689,10 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
     if (out->current_image) std::memcpy(out->current_image, h->h_pack, (size_t)h->S * isz);
     if (out->cumulative_image)
         std::memcpy(out->cumulative_image, h->h_pack + (size_t)h->S * 8, (size_t)h->S * isz);
-    unsigned long long tot[4];
-    std::memcpy(tot, h_tail, 32);
+    unsigned long long tot[4] = {0, 0, 0, 0};
+    const unsigned long long *parts = reinterpret_cast<const unsigned long long *>(h_tail + 48);
+    for (int b = 0; b < n_parts; ++b)
+        for (int q = 0; q < 4; ++q) tot[q] += parts[4 * b + q];
     for (int q = 0; q < 4; ++q) out->totals[q] = tot[q];
     h->window_has_data = false;
     h->win64_dirty = false;

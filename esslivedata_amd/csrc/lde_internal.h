@@ -154,6 +154,8 @@ constexpr int kSieveTagShift = 22;
 constexpr uint32_t kSieveValueMask = (1u << kSieveTagShift) - 1u;
 constexpr uint32_t kSieveEmpty = 0xFFu << kSieveTagShift;  // tag 255, not valid
 constexpr int kSieveMaxT = 254;
+// finalize: per-block total partials summed on the host (at most this many blocks)
+constexpr int kHostPartials = 1024;
 constexpr int kColdGroups = 2;  // SIEVE cold keys: wave groups per block, one sort block each
 
 // Batches of up to kKargSegs messages: the descriptors travel as kernel
@@ -271,7 +273,8 @@ hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *wi
                            unsigned long long *cum, unsigned long long *snap, long long S, int T,
                            int lo, int hi, void *cur_img, void *cum_img,
                            unsigned long long *totals, unsigned long long *tot_copy,
-                           const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st);
+                           const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st,
+                           unsigned long long *host_parts = nullptr, int *n_parts = nullptr);
 hipError_t launch_rows_f32(const float *h, long long S, int T, int lo, int hi, float *img,
                            hipStream_t st);
 // items: {group, begin, end, group has a single item}; out zeroed unless every

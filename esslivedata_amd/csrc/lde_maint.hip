@@ -64,7 +64,9 @@ __global__ __launch_bounds__(256) void k_finalize(uint32_t *__restrict__ win32,
                                                   long long S, int T, int lo, int hi,
                                                   OUT *__restrict__ cur_img,
                                                   OUT *__restrict__ cum_img,
-                                                  unsigned long long *__restrict__ totals) {
+                                                  unsigned long long *__restrict__ totals,
+                                                  const uint32_t *__restrict__ ovf_src,
+                                                  uint32_t *__restrict__ ovf_dst) {
     __shared__ unsigned long long s_tot[4][4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long acc[4] = {0, 0, 0, 0};
@@ -107,8 +109,10 @@ __global__ __launch_bounds__(256) void k_finalize(uint32_t *__restrict__ win32,
     if (lane == 0)
         for (int q = 0; q < 4; ++q) s_tot[wid][q] = acc[q];
     __syncthreads();
-    // per-block partials (summed by k_sum_totals): thousands of same-word
-    // atomics would serialize at the memory side
+    // per-block partials (summed by k_sum_totals, or by the host from the
+    // finalize pack): thousands of same-word atomics would serialize at the
+    // memory side
+    if (ovf_dst && blockIdx.x == 0 && threadIdx.x == 4) *ovf_dst = ovf_src ? *ovf_src : 0u;
     if (threadIdx.x < 4)
         totals[4 + (size_t)blockIdx.x * 4 + threadIdx.x] =
             s_tot[0][threadIdx.x] + s_tot[1][threadIdx.x] + s_tot[2][threadIdx.x] + s_tot[3][threadIdx.x];
@@ -125,7 +129,9 @@ __global__ __launch_bounds__(256) void k_finalize_v4(uint32_t *__restrict__ win3
                                                      long long S, int T, int lo, int hi,
                                                      OUT *__restrict__ cur_img,
                                                      OUT *__restrict__ cum_img,
-                                                     unsigned long long *__restrict__ totals) {
+                                                     unsigned long long *__restrict__ totals,
+                                                  const uint32_t *__restrict__ ovf_src,
+                                                  uint32_t *__restrict__ ovf_dst) {
     typedef unsigned long long u64;
     __shared__ u64 s_tot[8][4];
     const int gl = threadIdx.x & 31, grp = threadIdx.x >> 5;  // 8 row groups per block
@@ -184,6 +190,7 @@ __global__ __launch_bounds__(256) void k_finalize_v4(uint32_t *__restrict__ win3
     if (gl == 0)
         for (int q = 0; q < 4; ++q) s_tot[grp][q] = acc[q];
     __syncthreads();
+    if (ovf_dst && blockIdx.x == 0 && threadIdx.x == 4) *ovf_dst = ovf_src ? *ovf_src : 0u;
     if (threadIdx.x < 4) {
         u64 v = 0;
         for (int g = 0; g < 8; ++g) v += s_tot[g][threadIdx.x];
@@ -304,29 +311,35 @@ hipError_t launch_sum3(const unsigned long long *a, const unsigned long long *b,
     return hipGetLastError();
 }
 
+// host_parts (non-null): the per-block partials go there (inside the finalize
+// pack) for the host to sum, block 0 copies the overflow flag, and no
+// k_sum_totals launch follows; *n_parts = the number of partial blocks.
 template <typename OUT>
 static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsigned long long *cum,
                               unsigned long long *snap, long long S, int T, int lo, int hi,
                               void *cur_img, void *cum_img, unsigned long long *totals,
                               unsigned long long *tot_copy, const uint32_t *ovf_src,
-                              uint32_t *ovf_dst, hipStream_t st) {
-    if (T % 4 == 0 && T <= 128) {
-        long long b8 = (S + 7) / 8;
-        if (b8 > 8192) b8 = 8192;
-        if (b8 < 1) b8 = 1;
-        hipLaunchKernelGGL(k_finalize_v4<OUT>, dim3((unsigned)b8), dim3(256), 0, st, win32, win64,
-                           cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, totals);
-        hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(1024), 0, st, totals, (int)b8, tot_copy,
-                           ovf_src, ovf_dst);
-        return;
-    }
-    long long blocks = (S + 3) / 4;
-    if (blocks > 2048) blocks = 2048;
+                              uint32_t *ovf_dst, unsigned long long *host_parts, int *n_parts,
+                              hipStream_t st) {
+    const bool v4 = T % 4 == 0 && T <= 128;
+    const long long rows_per_block = v4 ? 8 : 4;
+    long long blocks = (S + rows_per_block - 1) / rows_per_block;
+    const long long cap = host_parts ? kHostPartials : (v4 ? 8192 : 2048);
+    if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_finalize<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
-                       cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, totals);
-    hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(1024), 0, st, totals, (int)blocks, tot_copy,
-                       ovf_src, ovf_dst);
+    unsigned long long *dst = host_parts ? host_parts - 4 : totals;  // partial b at dst[4 + 4 b]
+    const uint32_t *ks = host_parts ? ovf_src : nullptr;
+    uint32_t *kd = host_parts ? ovf_dst : nullptr;
+    if (v4)
+        hipLaunchKernelGGL(k_finalize_v4<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
+                           cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, dst, ks, kd);
+    else
+        hipLaunchKernelGGL(k_finalize<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
+                           cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, dst, ks, kd);
+    if (n_parts) *n_parts = (int)blocks;
+    if (!host_parts)
+        hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(1024), 0, st, totals, (int)blocks, tot_copy,
+                           ovf_src, ovf_dst);
 }
 
 // image element type: 0 f64, 1 f32, 2 u64 (exact partial sums for multi-GPU)
@@ -334,16 +347,18 @@ hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *wi
                            unsigned long long *cum, unsigned long long *snap, long long S, int T,
                            int lo, int hi, void *cur_img, void *cum_img,
                            unsigned long long *totals, unsigned long long *tot_copy,
-                           const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st) {
+                           const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st,
+                           unsigned long long *host_parts, int *n_parts) {
     if (img_kind == 1)
         launch_finalize_t<float>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals,
-                                 tot_copy, ovf_src, ovf_dst, st);
+                                 tot_copy, ovf_src, ovf_dst, host_parts, n_parts, st);
     else if (img_kind == 2)
         launch_finalize_t<unsigned long long>(win32, win64, cum, snap, S, T, lo, hi, cur_img,
-                                              cum_img, totals, tot_copy, ovf_src, ovf_dst, st);
+                                              cum_img, totals, tot_copy, ovf_src, ovf_dst,
+                                              host_parts, n_parts, st);
     else
         launch_finalize_t<double>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals,
-                                  tot_copy, ovf_src, ovf_dst, st);
+                                  tot_copy, ovf_src, ovf_dst, host_parts, n_parts, st);
     return hipGetLastError();
 }
 

@@ -187,8 +187,8 @@ __global__ __launch_bounds__(256) void k_chunk_tab_karg(SegKarg sk, int n_segs, 
 // whose chunk range exceeds kSieveLdsChunks.  Otherwise each block builds its
 // own in LDS, and GCT is a template switch rather than a runtime branch so
 // that the loop has one fetch path: with both, the compiler's wait-count
-// insertion merges the paths and waits for every outstanding load (vmcnt(0))
-// once per iteration, which serialized the stream (measured 0.34 -> 0.xx ms).
+// insertion merged the paths into a vmcnt(0) at the loop head (measured
+// neutral on DREAM, but the single path keeps the waits as written).
 template <int ABL, int GCT>
 __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // static, so LDS addresses need no runtime base (one block per CU anyway)

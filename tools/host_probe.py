@@ -70,3 +70,21 @@ for _ in range(200):
         (t.dtype is torch.int32, t.is_contiguous(), t.is_cuda)
 t2 = time.perf_counter()
 print('data_ptr rows us', round((t1 - t0) / 200 * 1e6, 2), 'checks us', round((t2 - t1) / 200 * 1e6, 2))
+
+# finalize alone with the GPU idle: launch + kernels + D2H + wait + host copies
+tf = []
+for i in range(20):
+    eng.stage_tensors_batch(msgs)
+    eng.accumulate(i % view.n_replicas)
+    eng.synchronize()
+    t0 = time.perf_counter()
+    eng.finalize(images=True)
+    tf.append(time.perf_counter() - t0)
+print('finalize with idle GPU (us): median', round(sorted(tf)[10] * 1e6, 1), 'min', round(min(tf) * 1e6, 1))
+import ctypes
+buf = np.empty(25600 * 2, dtype=np.float64)
+src = np.ones(25600 * 2, dtype=np.float64)
+t0 = time.perf_counter()
+for _ in range(200):
+    np.copyto(buf, src)
+print('host copy of 410 KB (us):', round((time.perf_counter() - t0) / 200 * 1e6, 2))
