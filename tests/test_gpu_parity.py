@@ -525,3 +525,36 @@ def test_default_stream_engine_outlives_recorded_tensors():
     x = torch.empty(10**7, dtype=torch.int32, device='cuda')  # allocator reuse after free
     del x
     assert h.sum() > 0
+
+
+@pytest.mark.parametrize('grid', ['1', '3'])
+def test_sieve_hot_cells_with_millions_of_events(grid, monkeypatch):
+    """One or three sieve blocks (one: its chunk range exceeds the LDS chunk
+    table); two adjacent hot cells take 1.8 M and 0.6 M events per batch,
+    far past any 16-bit count, plus a third hot screen and a uniform rest."""
+    monkeypatch.setenv('LDE_SPLIT_GRID', grid)
+    from esslivedata_amd import projection
+
+    dn = np.arange(1, 4097, dtype=np.int32)
+    view = projection.logical_lut(dn)
+    edges = np.linspace(0.0, 71.43, 101) * 1e6
+    rng = np.random.default_rng(5)
+    n = 3_000_000
+    pid = rng.integers(1, 4097, n).astype(np.int32)
+    toa = rng.uniform(0, 71e6, n).astype(np.int32)
+    mid = lambda b: int((edges[b] + edges[b + 1]) / 2)  # noqa: E731
+    k = rng.random(n)
+    pid[k < 0.8] = 7
+    toa[k < 0.6] = mid(10)
+    toa[(k >= 0.6) & (k < 0.8)] = mid(11)
+    pid[(k >= 0.8) & (k < 0.9)] = 8
+    toa[(k >= 0.8) & (k < 0.9)] = mid(51)
+    eng = _engine(view, edges, 'split')
+    for _ in range(2):
+        eng.stage(pid, toa)
+        eng.accumulate(0)
+    res = eng.finalize(hists=True)
+    assert eng.info()['last_strategy'] == 'split'
+    exp = 2 * ora.detector_histogram(np.arange(4096), 4096, ora.pixel_index(pid, dn), toa, edges)
+    assert exp[6, 10] >= 2 * (k < 0.6).sum() > 3 * 65536
+    np.testing.assert_array_equal(res.current_hist, exp)
