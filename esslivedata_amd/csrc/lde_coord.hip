@@ -49,7 +49,8 @@ __global__ __launch_bounds__(256) void k_event_coord(CoordArgs a, const int *__r
     const double ymax = (double)(a.nt - 1);
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        const unsigned q = (unsigned)ld_global(pid + e) - (unsigned)a.pid_off;
+        // monitors carry no pixel ids: every event is at the one distance
+        const unsigned q = pid ? (unsigned)ld_global(pid + e) - (unsigned)a.pid_off : 0u;
         int bin = -1;
         if (q < a.L) {
             const int pi = a.pix_i[q];

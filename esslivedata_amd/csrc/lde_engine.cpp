@@ -1908,7 +1908,8 @@ int lde_import_window_u64(lde_handle *h, const void *d_src) {
 int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
     if (!lut) return fail(h, LDE_EINVAL, "lut is NULL");
-    if (h->monitor) return fail(h, LDE_EINVAL, "wavelength mode needs a detector handle");
+    // a monitor handle has one flight path (n_pixels = 1) for all its events
+    const long long n_pix = h->monitor ? 1 : h->L;
     // entering wavelength mode re-bins against integer edges, so it needs an
     // empty engine; once in it, a new table or new pixel distances (a detector
     // move) only change the per-event coordinate and keep the accumulated data
@@ -1916,8 +1917,9 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     if (!rebind && (h->window_has_data || h->cum_has_data || h->staged_host > 0 ||
                     !h->dev_segments.empty()))
         return fail(h, LDE_ESTATE, "set the coordinate table before the first accumulate (or after clear)");
-    if (lut->n_pixels != h->L) return fail(h, LDE_EINVAL, "n_pixels %lld != lut_len %lld",
-                                           (long long)lut->n_pixels, h->L);
+    if (lut->n_pixels != n_pix)
+        return fail(h, LDE_EINVAL, "n_pixels %lld != %lld (%s)", (long long)lut->n_pixels, n_pix,
+                    h->monitor ? "one distance for a monitor" : "lut_len");
     if (lut->n_dist < 2 || lut->n_time < 2) return fail(h, LDE_EINVAL, "the grid needs n_dist, n_time >= 2");
     if (!lut->table || !lut->pixel_distance) return fail(h, LDE_EINVAL, "NULL table");
     if (!(lut->dist_step > 0) || !(lut->time_step > 0) || !std::isfinite(lut->dist0) ||
@@ -1930,9 +1932,9 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     // per pixel: distance row and fraction (host, float64, as the oracle)
     const double inv_dd = 1.0 / lut->dist_step;
     const double xmax = (double)(lut->n_dist - 1);
-    std::vector<int> pi((size_t)h->L);
-    std::vector<double> pf((size_t)h->L);
-    for (long long k = 0; k < h->L; ++k) {
+    std::vector<int> pi((size_t)n_pix);
+    std::vector<double> pf((size_t)n_pix);
+    for (long long k = 0; k < n_pix; ++k) {
         const double x = (lut->pixel_distance[k] - lut->dist0) * inv_dd;
         if (x >= 0.0 && x <= xmax) {
             int i = (int)std::floor(x);
@@ -1975,8 +1977,8 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     dev_free(h->d_ctable);
     dev_free(h->d_cedges);
     const size_t nt = (size_t)lut->n_dist * (size_t)lut->n_time;
-    if (int rc = dev_alloc(h, &h->d_cpi, (size_t)h->L)) return rc;
-    if (int rc = dev_alloc(h, &h->d_cpf, (size_t)h->L)) return rc;
+    if (int rc = dev_alloc(h, &h->d_cpi, (size_t)n_pix)) return rc;
+    if (int rc = dev_alloc(h, &h->d_cpf, (size_t)n_pix)) return rc;
     if (int rc = dev_alloc(h, &h->d_ctable, nt)) return rc;
     if (int rc = dev_alloc(h, &h->d_cedges, (size_t)T + 1)) return rc;
     HIPCALL(h, hipMemcpy(h->d_cpi, pi.data(), pi.size() * 4, hipMemcpyHostToDevice));
@@ -1984,8 +1986,8 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     HIPCALL(h, hipMemcpy(h->d_ctable, lut->table, nt * 8, hipMemcpyHostToDevice));
     HIPCALL(h, hipMemcpy(h->d_cedges, h->edges.data(), ((size_t)T + 1) * 8, hipMemcpyHostToDevice));
     lde::CoordArgs &c = h->cargs;
-    c.pid_off = h->pid_off;
-    c.L = (unsigned)h->L;
+    c.pid_off = h->monitor ? 0 : h->pid_off;
+    c.L = (unsigned)n_pix;
     c.pix_i = h->d_cpi;
     c.pix_f = h->d_cpf;
     c.table = h->d_ctable;

@@ -85,10 +85,28 @@ class _Reducer:
             self.engine.wait_event(self._after)
             self._after = None
 
+    def _order_after_engine(self) -> None:
+        """The collective (on torch's current stream) after the engine's
+        writes of the buffer: a stream wait, no host synchronization (when the
+        engine runs on torch's current stream the two are in order already)."""
+        import torch
+
+        if not self.buf.is_cuda:
+            self.engine.synchronize()
+            return
+        cur = torch.cuda.current_stream(self.buf.device)
+        sp = self.engine.stream_ptr
+        if sp == cur.cuda_stream:
+            return
+        es = torch.cuda.ExternalStream(sp, device=self.buf.device)
+        ev = torch.cuda.Event()
+        ev.record(es)
+        cur.wait_event(ev)
+
     def _reduce(self) -> bool:
         import torch.distributed as dist
 
-        self.engine.synchronize()  # the engine may run on its own stream
+        self._order_after_engine()
         root = dist.get_rank(self.group) == self.dst
         if self._host:
             hb = self.buf.cpu()

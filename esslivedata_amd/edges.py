@@ -85,9 +85,14 @@ class WavelengthEdges:
 
     def edges_in(self, unit: str) -> np.ndarray:
         """Edges converted to ``unit`` (one float64 multiply, as ``bins.to``)."""
-        f = WAVELENGTH_UNIT_TO_ANGSTROM[self.unit] / WAVELENGTH_UNIT_TO_ANGSTROM[unit]
-        e = self.get_edges()
-        return e if f == 1.0 else e * f
+        return convert_wavelength(self.get_edges(), self.unit, unit)
+
+
+def convert_wavelength(values: np.ndarray, unit: str, to: str) -> np.ndarray:
+    """Wavelength unit conversion as one float64 multiply."""
+    values = np.asarray(values, dtype=np.float64)
+    f = WAVELENGTH_UNIT_TO_ANGSTROM[unit] / WAVELENGTH_UNIT_TO_ANGSTROM[to]
+    return values if f == 1.0 else values * f
 
 
 def convert_time(values: np.ndarray, unit: str, to: str) -> np.ndarray:

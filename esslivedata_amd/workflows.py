@@ -28,7 +28,7 @@ from typing import TYPE_CHECKING, Any, Callable, Iterable, Mapping, Sequence
 import numpy as np
 
 from .dataarray import DataArray, Variable
-from .edges import TOAEdges, WavelengthEdges, convert_time, label_slice
+from .edges import TOAEdges, WavelengthEdges, convert_time, convert_wavelength, label_slice
 from .engine import BinningEngine
 from .preprocessors import DetectorEvents, MonitorEvents, StagedEvents, Timestamp
 from .projection import ViewLUT, geometric_lut, index_groups, logical_lut
@@ -528,29 +528,54 @@ class GpuDetectorViewFactory:
 # monitor histogram
 # ---------------------------------------------------------------------------
 class GpuMonitorWorkflow:
-    """Monitor TOA histogram (``create_monitor_workflow`` TOA/event mode,
-    monitor_workflow.py:225-331)."""
+    """Monitor histogram (``create_monitor_workflow``, monitor_workflow.py:
+    225-331): TOA mode, or wavelength mode (``histogram_wavelength_monitor``,
+    :126-132) with the monitor's one flight path ``monitor_distance`` (m)
+    through the lookup table."""
 
     def __init__(
         self,
         source_name: str,
-        edges: TOAEdges,
+        edges: TOAEdges | WavelengthEdges,
         *,
         range_filter: tuple[float, float] | None = None,
+        coordinate_mode: str = 'toa',
+        lookup_table: 'WavelengthLookupTable | None' = None,
+        monitor_distance: float | None = None,
         device: int = 0,
         stream: int | None = None,
         geometry_key: str | None = MONITOR_TRANSFORM,
     ) -> None:
         self._source = source_name
         self._edges = edges
+        if coordinate_mode not in ('toa', 'wavelength'):
+            raise ValueError(f'Unsupported coordinate mode: {coordinate_mode}')
+        self._wavelength = coordinate_mode == 'wavelength'
         e_unit = edges.get_edges()
-        e_ns = edges.edges_ns()
-        # output coord: edges converted to ns and back (monitor_workflow.py:100)
-        self._coord = convert_time(e_ns, 'ns', edges.unit)
+        if self._wavelength:
+            if lookup_table is None or monitor_distance is None:
+                raise ValueError('wavelength mode requires a lookup table and the monitor distance')
+            if not isinstance(edges, WavelengthEdges):
+                raise ValueError('wavelength mode needs WavelengthEdges')
+            e_ev = edges.edges_in(lookup_table.unit)
+            # output coord: the edges in the event unit, converted back
+            # (monitor_workflow.py:98-100)
+            self._coord = convert_wavelength(e_ev, lookup_table.unit, edges.unit)
+            self._dim = 'wavelength'
+        else:
+            e_ev = edges.edges_ns()
+            # output coord: edges converted to ns and back (monitor_workflow.py:100)
+            self._coord = convert_time(e_ev, 'ns', edges.unit)
+            self._dim = 'time_of_arrival'
         lo, hi = range_filter if range_filter is not None else (e_unit[0], e_unit[-1])
         self._slice = label_slice(self._coord, float(lo), float(hi))
-        self._engine = BinningEngine.monitor(e_ns, toa_range=self._slice, device=device,
+        self._engine = BinningEngine.monitor(e_ev, toa_range=self._slice, device=device,
                                              stream=stream)
+        if self._wavelength:
+            t = lookup_table
+            self._engine.set_coordinate_lut([float(monitor_distance)], t.table, dist0=t.distance0,
+                                            dist_step=t.distance_step, time0=t.time0,
+                                            time_step=t.time_step)
         self._geometry = _ContextState(geometry_key)
         self._start: Timestamp | None = None
         self._end: Timestamp | None = None
@@ -575,6 +600,8 @@ class GpuMonitorWorkflow:
 
         from ._native import check, lib
 
+        if self._wavelength:
+            raise NotImplementedError('histogram-mode monitors are rebinned in TOA mode only')
         dim = hist.dims[0]
         coord = hist.coords[dim]
         src_edges = convert_time(np.asarray(coord.values, dtype=np.float64), coord.unit,
@@ -625,7 +652,7 @@ class GpuMonitorWorkflow:
         self._engine.accumulate(0)
 
     def _hist(self, values: np.ndarray) -> DataArray:
-        dim = 'time_of_arrival'
+        dim = self._dim
         return DataArray(values.reshape(-1), (dim,), 'counts',
                          {dim: Variable((dim,), self._coord, self._edges.unit)})
 
@@ -694,7 +721,15 @@ class GpuMonitorWorkflow:
         self._start = self._end = None
 
 
-def create_gpu_monitor_workflow(source_name: str, edges: TOAEdges, *,
+def create_gpu_monitor_workflow(source_name: str, edges, *,
                                 range_filter: tuple[float, float] | None = None,
+                                coordinate_mode: str = 'toa',
+                                lookup_table: 'WavelengthLookupTable | None' = None,
+                                monitor_distance: float | None = None,
                                 device: int = 0) -> GpuMonitorWorkflow:
-    return GpuMonitorWorkflow(source_name, edges, range_filter=range_filter, device=device)
+    """``create_monitor_workflow`` (monitor_workflow.py:225-331); the lookup
+    table and the monitor's Ltotal stand for its ``lookup_table_filename`` and
+    ``geometry_filename``."""
+    return GpuMonitorWorkflow(source_name, edges, range_filter=range_filter,
+                              coordinate_mode=coordinate_mode, lookup_table=lookup_table,
+                              monitor_distance=monitor_distance, device=device)

@@ -213,13 +213,14 @@ int lde_set_lut(lde_handle *h, const int32_t *out_lut);
  *   y = (t - time0) * (1 / time_step), j = min(floor y, n_time - 2), fy = y - j
  *   c = a + fx * (b - a), a = v[i][j] + fy * (v[i][j+1] - v[i][j]),
  *                         b = v[i+1][j] + fy * (v[i+1][j+1] - v[i+1][j])
- * in float64 without fused multiply-adds.  Detector handles only; the first
+ * in float64 without fused multiply-adds.  Monitor handles take one distance
+ * (n_pixels = 1) for all their events (monitor_workflow.py:126-132).  The first
  * call comes before the first lde_accumulate (or after lde_clear), later calls
  * (new pixel distances after a detector move, a new table) may come at any time
  * and keep the counts already binned.  n_dist, n_time >= 2. */
 typedef struct lde_coord_lut {
     const double *pixel_distance; /* [n_pixels] per pixel id (pid_offset + k) */
-    int64_t n_pixels;             /* must equal lut_len */
+    int64_t n_pixels;             /* lut_len (detector) or 1 (monitor) */
     const double *table;          /* [n_dist * n_time] */
     int32_t n_dist, n_time;
     double dist0, dist_step;

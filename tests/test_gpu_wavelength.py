@@ -206,3 +206,33 @@ def test_workflow_wavelength_mode_and_move():
         np.testing.assert_array_equal(out['current'].values,
                                       exp[:, lo:hi].sum(-1).reshape(144, 144))
         assert float(out['counts_in_toa_range'].values) == exp[:, lo:hi].sum()
+
+
+@pytest.mark.parametrize('unit', ['Å', 'nm'])
+def test_monitor_wavelength_mode(unit):
+    """``histogram_wavelength_monitor`` (monitor_workflow.py:126-132): every
+    event at the monitor's flight path through the table, binned on the
+    wavelength edges; the coord is the edges in the event unit and back."""
+    from esslivedata_amd import synthetic
+    from esslivedata_amd.edges import WavelengthEdges, convert_wavelength
+    from esslivedata_amd.workflows import create_gpu_monitor_workflow
+
+    tab = synthetic.dream_wavelength_table()
+    wl = (WavelengthEdges(start=0.5, stop=3.5, num_bins=100) if unit == 'Å'
+          else WavelengthEdges(start=0.05, stop=0.35, num_bins=100, unit='nm'))
+    wf = create_gpu_monitor_workflow('monitor_1', wl, range_filter=None,
+                                     coordinate_mode='wavelength', lookup_table=tab,
+                                     monitor_distance=77.85)
+    rng = np.random.default_rng(8)
+    toa = rng.normal(30e6, 12e6, 2_000_000).astype(np.int32)
+    wf.accumulate({'monitor_1': (None, toa)}, start_time=_t(0), end_time=_t(1))
+    out = wf.finalize()
+    e_ev = wl.edges_in('Å')
+    c = ora.coordinate_lookup(np.full(toa.size, 77.85), toa, tab.table, tab.distance0,
+                              tab.distance_step, tab.time0, tab.time_step)
+    exp = ora.monitor_histogram(c, e_ev)
+    np.testing.assert_array_equal(out['current'].values, exp)
+    assert out['current'].dims == ('wavelength',)
+    np.testing.assert_array_equal(out['current'].coords['wavelength'].values,
+                                  convert_wavelength(e_ev, 'Å', unit))
+    assert float(out['counts_total'].values) == exp.sum()

@@ -129,3 +129,17 @@ def test_oracle_view_wavelength_mode_counts():
     lam = wavelength.H_OVER_MN * toa[ok] * 1e-9 / lt[pix[ok]]
     np.testing.assert_allclose(c[ok], lam, rtol=2e-7)
     assert h.sum() == ((c >= edges[0]) & (c < edges[-1])).sum()
+
+
+def test_monitor_wavelength_mode_checks():
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.workflows import GpuMonitorWorkflow
+
+    tab = synthetic.dream_wavelength_table()
+    with pytest.raises(ValueError, match='coordinate mode'):
+        GpuMonitorWorkflow('m', TOAEdges(), coordinate_mode='dspacing')
+    with pytest.raises(ValueError, match='lookup table'):
+        GpuMonitorWorkflow('m', WavelengthEdges(), coordinate_mode='wavelength')
+    with pytest.raises(ValueError, match='WavelengthEdges'):
+        GpuMonitorWorkflow('m', TOAEdges(), coordinate_mode='wavelength', lookup_table=tab,
+                           monitor_distance=77.7)
