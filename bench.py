@@ -53,6 +53,9 @@ def parse():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--workload', default='dream', choices=['dream', 'loki'])
+    ap.add_argument('--coordinate', default='toa', choices=['toa', 'wavelength'],
+                    help='wavelength: DREAM events binned by wavelength through a direct-flight '
+                         'lookup table (diagnostic line, not the headline metric)')
     ap.add_argument('--pulses', type=int, default=14)
     ap.add_argument('--events-per-pulse', type=int, default=10_000_000)
     ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition', 'paged', 'split'])
@@ -186,6 +189,19 @@ def main():
         inst.detector_number, inst.coords, inst.resolution, flip_x=args.workload == 'loki'
     )
     edges = inst.edges.edges_ns()
+    coord = None
+    if args.coordinate == 'wavelength':
+        from esslivedata_amd import wavelength
+        from esslivedata_amd.edges import WavelengthEdges
+
+        tab = synthetic.dream_wavelength_table() if args.workload == 'dream' else \
+            wavelength.ideal_lookup_table(27.5, 29.5, 41, 71.5e6, 287)
+        src = (0.0, 0.0, -synthetic.DREAM_L1 if args.workload == 'dream' else -23.0)
+        lt = wavelength.pixel_ltotal(inst.positions, source_position=src)
+        d = wavelength.distance_per_pid(inst.detector_number, lt, view.pid_offset, view.lut.shape[1])
+        edges = WavelengthEdges(start=0.2, stop=3.6 if args.workload == 'dream' else 10.0,
+                                num_bins=100).get_edges()
+        coord = (d, tab)
     # one non-default torch stream for the data generation, the engine and
     # the collectives: everything in order on it, no cross-stream waits
     stream = torch.cuda.Stream(dev)
@@ -199,6 +215,10 @@ def main():
         device=local,
         stream=stream.cuda_stream,
     )
+    if coord is not None:
+        d, tab = coord
+        eng.set_coordinate_lut(d, tab.table, dist0=tab.distance0, dist_step=tab.distance_step,
+                               time0=tab.time0, time_step=tab.time_step)
     n_pulse = args.events_per_pulse
     n_step = n_pulse * args.pulses
     seed = 7 + 1000 * rank
@@ -271,7 +291,7 @@ def main():
     timed = {dom: eng.kernel_stats(dom)}
 
     names = ('atomic', 'partition', 'tile_accumulate', 'plan', 'paged', 'page_plan',
-             'page_accumulate', 'split', 'split_aux', 'binning', 'finalize')
+             'page_accumulate', 'split', 'split_aux', 'coord', 'binning', 'finalize')
     eng.timing_select(None)
     eng.timing_enable(True)
     for i in range(3):
@@ -359,6 +379,7 @@ def main():
         'data': 'synthetic (seeded ev44-shaped streams generated in HBM; no recorded data offline)',
         'config': {
             'workload': 'dream_mantle_cylinder_mantle_z' if args.workload == 'dream' else 'loki_bank0_xy_plane',
+            'coordinate': args.coordinate,
             'pixels': int(inst.detector_number.size),
             'screen': list(view.screen_shape),
             'replicas': view.n_replicas,
@@ -395,7 +416,7 @@ def main():
     }
     if e2e is not None:
         result['end_to_end'] = e2e
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and coord is None:
         # CPU baseline + parity leg: one more GPU step with the full current
         # histogram read back, then the oracle over the same batch
         from oracle import scipp_semantics as ora

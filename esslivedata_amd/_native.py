@@ -47,6 +47,7 @@ KERNELS = {
     'page_accumulate': 9,
     'split': 10,
     'split_aux': 11,
+    'coord': 12,
 }
 
 # every symbol include/lde.h declares (checked by tests/test_abi.py)

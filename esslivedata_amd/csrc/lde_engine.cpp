@@ -1534,6 +1534,7 @@ int lde_accumulate(lde_handle *h, int32_t replica) {
         // the value binned against the integer edges 0..T
         if (int rc = grow(h, &h->d_cbin, h->cbin_cap, (size_t)total)) return rc;
         long long off = 0;
+        Timed tm(h, LDE_K_COORD);
         for (Segment &s : segs) {
             HIPCALL(h, lde::launch_event_coord(h->cargs, s.pid, s.toa, s.n, h->d_cbin + off, h->stream));
             s.toa = h->d_cbin + off;

@@ -303,7 +303,8 @@ int lde_synchronize(lde_handle *h);
 #define LDE_K_PAGE_ACC 9  /* k_page_accumulate: PAGED pass B                  */
 #define LDE_K_SPLIT 10    /* k_split: SPLIT event pass (hot rows in LDS, cold keys out) */
 #define LDE_K_SPLIT_AUX 11 /* hot-set selection, hot-row reduce, cold segment table */
-#define LDE_K_COUNT 12
+#define LDE_K_COORD 12    /* k_event_coord: wavelength-mode coordinate pass   */
+#define LDE_K_COUNT 13
 int lde_timing_enable(lde_handle *h, int32_t enable);
 /* Record only the kernels whose bit (1 << LDE_K_*) is set in mask (default:
  * all).  Fewer recorded events = less host work per batch. */
