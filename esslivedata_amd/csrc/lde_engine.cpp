@@ -148,8 +148,8 @@ struct lde_handle {
     // the lookup table, the coordinate edges, per-event bin scratch
     bool coord = false;
     lde::CoordArgs cargs{};
-    int *d_cpi = nullptr;
-    double *d_cpf = nullptr, *d_ctable = nullptr, *d_cedges = nullptr;
+    uint16_t *d_cbuck = nullptr;  // coordinate bucket table
+    double *d_cpd = nullptr, *d_ctable = nullptr, *d_cedges = nullptr;
     int *d_cbin = nullptr;
     size_t cbin_cap = 0;
     std::vector<double> edges;  // the create-time edges (event unit)
@@ -723,7 +723,12 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         }
     }
     ++uses;
-    if (!forced && h->hot_cov[replica] < h->split_min_cov) return 1;
+    if (!forced && h->hot_cov[replica] < h->split_min_cov) {
+        if (env_ll("LDE_VERBOSE", 0))
+            fprintf(stderr, "lde split: replica %d hot cover %.3f < %.3f -> paged\n", replica,
+                    h->hot_cov[replica], h->split_min_cov);
+        return 1;
+    }
     const long long per_block = (chunks + a.grid - 1) / a.grid;
     // SIEVE reserves cold slots in multiples of 4 per wave and half chunk
     a.cold_cap = per_block * (lde::kChunk + (h->sieve_ok ? 4 * 2 * (lde::kSplitThreads / 64) : 0));
@@ -1037,8 +1042,8 @@ void release(lde_handle *h) {
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
     dev_free(h->d_lut);
     dev_free(h->d_tab);
-    dev_free(h->d_cpi);
-    dev_free(h->d_cpf);
+    dev_free(h->d_cbuck);
+    dev_free(h->d_cpd);
     dev_free(h->d_ctable);
     dev_free(h->d_cedges);
     dev_free(h->d_cbin);
@@ -1301,6 +1306,9 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 if (cbits > 0 && env_ll("LDE_SIEVE", 1) != 0 && build_sieve_toa(h->tp, tab, tt, tsh, tcap) &&
                     (unsigned long long)h->S * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL &&
                     ((h->L - 1) >> cbits) < 255 && h->L < 0x3fffffffLL) {
+                    // room for the integer-edge table of wavelength mode (edges
+                    // 0..T: T + 1 bucket words), so lde_set_coord_lut keeps the sieve
+                    if (tt.size() < (size_t)lde::align4(h->T + 2)) tt.resize((size_t)lde::align4(h->T + 2), 0u);
                     int Hs = 0;
                     const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size(), h->n_tiles);
                     if (fixed < budget)
@@ -1930,23 +1938,6 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     if (h->out_dtype == LDE_F32) return fail(h, LDE_EINVAL, "wavelength mode: float64 views only");
     DeviceGuard guard(h->device);
     const int T = h->T;
-    // per pixel: distance row and fraction (host, float64, as the oracle)
-    const double inv_dd = 1.0 / lut->dist_step;
-    const double xmax = (double)(lut->n_dist - 1);
-    std::vector<int> pi((size_t)n_pix);
-    std::vector<double> pf((size_t)n_pix);
-    for (long long k = 0; k < n_pix; ++k) {
-        const double x = (lut->pixel_distance[k] - lut->dist0) * inv_dd;
-        if (x >= 0.0 && x <= xmax) {
-            int i = (int)std::floor(x);
-            if (i > lut->n_dist - 2) i = lut->n_dist - 2;
-            pi[(size_t)k] = i;
-            pf[(size_t)k] = x - (double)i;
-        } else {
-            pi[(size_t)k] = -1;
-            pf[(size_t)k] = 0.0;
-        }
-    }
     HIPCALL(h, hipStreamSynchronize(h->stream));  // in-flight launches may read the old table
     if (!rebind) {
     // the binning stage now sees integer bins: edges 0..T
@@ -1970,33 +1961,61 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
             HIPCALL(h, hipMemcpy(h->d_ttab, h->ttab.data(), h->ttab.size() * 4, hipMemcpyHostToDevice));
         } else {
             h->sieve_ok = false;
+            if (env_ll("LDE_VERBOSE", 0))
+                fprintf(stderr, "lde coord: integer bin table does not fit the sieve (%zu > %zu words)\n",
+                        tt.size(), h->ttab.size());
         }
     }
     }
-    dev_free(h->d_cpi);
-    dev_free(h->d_cpf);
+    dev_free(h->d_cbuck);
+    dev_free(h->d_cpd);
     dev_free(h->d_ctable);
     dev_free(h->d_cedges);
+    // bucket table over the edge range: a start candidate per bucket (the
+    // kernel corrects it against the edges, so rounding never matters)
+    const std::vector<double> &ed = h->edges;
+    const double span = ed[(size_t)T] - ed[0];
+    double min_w = span;
+    for (int b = 0; b < T; ++b)
+        if (ed[(size_t)b + 1] > ed[(size_t)b]) min_w = std::min(min_w, ed[(size_t)b + 1] - ed[(size_t)b]);
+    int G = 1;
+    if (span > 0 && std::isfinite(span) && min_w > 0)
+        G = (int)std::max(1.0, std::min(4096.0, std::ceil(2.0 * span / min_w)));
+    std::vector<uint16_t> buck((size_t)G, 0);
+    const double w = span > 0 ? span / G : 1.0;
+    for (int g = 0; g < G; ++g) {
+        const double x = ed[0] + g * w;
+        int b = (int)(std::upper_bound(ed.begin(), ed.end(), x) - ed.begin()) - 1;
+        buck[(size_t)g] = (uint16_t)std::min(std::max(b, 0), std::min(T - 1, 65535));
+    }
     const size_t nt = (size_t)lut->n_dist * (size_t)lut->n_time;
-    if (int rc = dev_alloc(h, &h->d_cpi, (size_t)n_pix)) return rc;
-    if (int rc = dev_alloc(h, &h->d_cpf, (size_t)n_pix)) return rc;
+    if (int rc = dev_alloc(h, &h->d_cpd, (size_t)n_pix)) return rc;
     if (int rc = dev_alloc(h, &h->d_ctable, nt)) return rc;
     if (int rc = dev_alloc(h, &h->d_cedges, (size_t)T + 1)) return rc;
-    HIPCALL(h, hipMemcpy(h->d_cpi, pi.data(), pi.size() * 4, hipMemcpyHostToDevice));
-    HIPCALL(h, hipMemcpy(h->d_cpf, pf.data(), pf.size() * 8, hipMemcpyHostToDevice));
+    if (int rc = dev_alloc(h, &h->d_cbuck, (size_t)G)) return rc;
+    HIPCALL(h, hipMemcpy(h->d_cpd, lut->pixel_distance, (size_t)n_pix * 8, hipMemcpyHostToDevice));
     HIPCALL(h, hipMemcpy(h->d_ctable, lut->table, nt * 8, hipMemcpyHostToDevice));
-    HIPCALL(h, hipMemcpy(h->d_cedges, h->edges.data(), ((size_t)T + 1) * 8, hipMemcpyHostToDevice));
+    HIPCALL(h, hipMemcpy(h->d_cedges, ed.data(), ((size_t)T + 1) * 8, hipMemcpyHostToDevice));
+    HIPCALL(h, hipMemcpy(h->d_cbuck, buck.data(), (size_t)G * 2, hipMemcpyHostToDevice));
     lde::CoordArgs &c = h->cargs;
     c.pid_off = h->monitor ? 0 : h->pid_off;
     c.L = (unsigned)n_pix;
-    c.pix_i = h->d_cpi;
-    c.pix_f = h->d_cpf;
-    c.table = h->d_ctable;
+    c.pix_d = h->d_cpd;
+    c.d0 = lut->dist0;
+    c.inv_dd = 1.0 / lut->dist_step;
+    c.nd = lut->n_dist;
     c.nt = lut->n_time;
+    c.table = h->d_ctable;
     c.t0 = lut->time0;
     c.inv_dt = 1.0 / lut->time_step;
     c.edges = h->d_cedges;
     c.T = T;
+    c.buckets = h->d_cbuck;
+    c.G = G;
+    c.e0 = ed[0];
+    c.inv_w = 1.0 / w;
+    c.edges_lds = 1;
+    if (lde::coord_smem(c, false) > lde::kCoordSmemMax) c.edges_lds = 0;  // huge T: edges from HBM
     h->coord = true;
     if (!rebind)
         for (auto &u : h->hot_uses) u = -1;  // hot sets re-select on the new value

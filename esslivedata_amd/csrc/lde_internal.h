@@ -289,15 +289,21 @@ hipError_t launch_group_spectra(int mode, const int4 *items, int n_items, const 
 // time) lookup table, written as the int32 "time" of a second binning pass
 struct CoordArgs {
     int pid_off;
-    unsigned L;
-    const int *pix_i;       // [L] distance row of the pixel id, -1 = no coordinate
-    const double *pix_f;    // [L] fractional distance position
+    unsigned L;             // pixels with a distance (1 for a monitor)
+    const double *pix_d;    // [L] flight path per pixel id, NaN = no coordinate
+    double d0, inv_dd;      // distance grid: d0 + i / inv_dd
+    int nd, nt;
     const double *table;    // [nd * nt] row-major (distance, time)
-    int nt;
     double t0, inv_dt;      // time grid: t0 + j / inv_dt (event unit, ns)
     const double *edges;    // [T + 1] coordinate edges
     int T;
+    int edges_lds;          // 1: the edges are copied into LDS
+    const uint16_t *buckets;  // [G] first candidate bin per bucket of the edge range
+    int G;
+    double e0, inv_w;       // bucket g = (v - e0) * inv_w
 };
+constexpr size_t kCoordSmemMax = 96 * 1024;
+size_t coord_smem(const CoordArgs &a, bool table_lds);
 hipError_t launch_event_coord(const CoordArgs &a, const int *pid, const int *toa, long long n,
                               int *out, hipStream_t st);
 

@@ -331,7 +331,8 @@ class BinningEngine:
         the coordinate ``table`` (n_dist x n_time, bilinear) at their pixel's
         distance and their time of arrival (ns); the engine's edges are then
         in the coordinate's unit.  ``pixel_distance`` is per pixel id of the
-        LUT (pid_offset + k), NaN where the pixel has no coordinate."""
+        LUT (pid_offset + k), NaN where the pixel has no coordinate; a monitor
+        engine takes one distance (its flight path) for all events."""
         d = np.ascontiguousarray(np.asarray(pixel_distance, dtype=np.float64))
         tab = np.ascontiguousarray(np.asarray(table, dtype=np.float64))
         if tab.ndim != 2:

@@ -236,3 +236,37 @@ def test_monitor_wavelength_mode(unit):
     np.testing.assert_array_equal(out['current'].coords['wavelength'].values,
                                   convert_wavelength(e_ev, 'Å', unit))
     assert float(out['counts_total'].values) == exp.sum()
+
+
+@pytest.mark.parametrize('kind', ['duplicates', 'many_bins'])
+def test_coordinate_bins_for_unusual_edges(kind):
+    """Edges with empty (repeated) bins, and 20000 bins (edges too large for
+    LDS: read from HBM): the bucketed search still gives scipp's bins."""
+    from esslivedata_amd import projection
+    from esslivedata_amd.engine import BinningEngine
+
+    if kind == 'duplicates':
+        edges = np.sort(np.concatenate([np.linspace(1.0, 9.0, 41), [2.0, 2.0, 5.5, 7.25]]))
+    else:
+        edges = np.geomspace(0.5, 9.5, 20001)
+    rng = np.random.default_rng(12)
+    nd, nt, dt = 6, 40, 2048.0
+    tab = rng.uniform(0.4, 9.6, (nd, nt))
+    tab[:, ::7] = edges[rng.integers(0, edges.size, (nd, (nt + 6) // 7))]  # exact edge values
+    dn = np.arange(1, 65, dtype=np.int32)
+    view = projection.logical_lut(dn)
+    ltot = (np.arange(64) % nd) * 0.5 + 3.0
+    eng = BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                        n_screen=view.n_screen, strategy='atomic')
+    eng.set_coordinate_lut(ltot, tab, dist0=3.0, dist_step=0.5, time0=0.0, time_step=dt)
+    n = 300_000
+    pid = rng.integers(1, 65, n).astype(np.int32)
+    toa = rng.integers(-10, int(dt) * nt + 10, n).astype(np.int32)
+    toa[: n // 2] = (toa[: n // 2] // int(dt)) * int(dt)  # on time nodes: exact table values
+    eng.stage(pid, toa)
+    eng.accumulate(0)
+    res = eng.finalize(hists=True)
+    o = ora.OracleDetectorView(dn, np.arange(64)[None], (64,), edges,
+                               coordinate=ora.wavelength_mode(ltot, tab, 3.0, 0.5, 0.0, dt))
+    o.accumulate(pid, toa)
+    np.testing.assert_array_equal(res.current_hist, o.finalize()['histogram_current'])
