@@ -175,11 +175,18 @@ def main():
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    # one GPU per rank; more ranks than GPUs (a gloo rehearsal) share them
+    local = int(os.environ.get('LOCAL_RANK', '0')) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        # RCCL over xGMI; LDE_BENCH_BACKEND=gloo rehearses the multi-rank
+        # path with several ranks on one GPU (host-staged collectives)
+        backend = os.environ.get('LDE_BENCH_BACKEND', 'nccl')
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from esslivedata_amd import projection, synthetic
     from esslivedata_amd.engine import BinningEngine
