@@ -178,6 +178,11 @@ struct lde_handle {
     // finalize outputs leave in one D2H copy: [current image S x 8 B]
     // [cumulative image S x 8 B][totals 32 B][overflow flag 16 B]
     unsigned char *d_pack = nullptr, *h_pack = nullptr;  // h_pack pinned
+    // LDE_FINALIZE_MAPPED (default): h_pack is coherent host memory the
+    // finalize kernel writes directly (hd_pack = its device address), so no
+    // copy command and no cache flush in front of one follows the kernel
+    unsigned char *hd_pack = nullptr;
+    hipEvent_t fin_event = nullptr;  // system-scope release after the kernel
     size_t pack_bytes = 0;
     unsigned long long *d_snap = nullptr;
 
@@ -1111,6 +1116,9 @@ void release(lde_handle *h) {
     dev_free(h->d_pack);
     if (h->h_pack) (void)hipHostFree(h->h_pack);
     h->h_pack = nullptr;
+    h->hd_pack = nullptr;
+    if (h->fin_event) (void)hipEventDestroy(h->fin_event);
+    h->fin_event = nullptr;
     dev_free(h->d_snap);
     for (auto &g : h->groups) {
         dev_free(g.d_items);
@@ -1237,7 +1245,13 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     // [per-block total partials, kHostPartials x 32] (summed on the host)
     h->pack_bytes = (size_t)h->S * 16 + 48 + 32 * (size_t)lde::kHostPartials;
     CREATE_CHECK(dev_alloc(h, &h->d_pack, h->pack_bytes));
-    CREATE_HIP(hipHostMalloc((void **)&h->h_pack, h->pack_bytes, hipHostMallocDefault));
+    if (env_ll("LDE_FINALIZE_MAPPED", 1) != 0) {
+        CREATE_HIP(hipHostMalloc((void **)&h->h_pack, h->pack_bytes, hipHostMallocCoherent));
+        CREATE_HIP(hipHostGetDevicePointer((void **)&h->hd_pack, h->h_pack, 0));
+        CREATE_HIP(hipEventCreateWithFlags(&h->fin_event, hipEventDisableTiming));
+    } else {
+        CREATE_HIP(hipHostMalloc((void **)&h->h_pack, h->pack_bytes, hipHostMallocDefault));
+    }
     h->d_img_cur = h->d_pack;
     h->d_img_cum = h->d_pack + (size_t)h->S * 8;
     CREATE_CHECK(zero_state(h));
@@ -1643,14 +1657,17 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
     const bool want_cum_hist = out->cumulative_hist != nullptr;
     if (want_cur_hist && !f32 && !h->d_snap)
         if (int rc = dev_alloc(h, &h->d_snap, nb)) return rc;
+    // outputs go straight into the host-mapped pack, or into d_pack and one copy
+    unsigned char *pk = h->hd_pack ? h->hd_pack : h->d_pack;
+    void *img_cur = pk, *img_cum = pk + (size_t)h->S * 8;
     if (f32) {
         // images/hists come from the f32 accumulators (mirrors f32 += order)
         if (out->current_image)
             HIPCALL(h, lde::launch_rows_f32(h->d_winf, h->S, h->T, h->range_lo, h->range_hi,
-                                            (float *)h->d_img_cur, h->stream));
+                                            (float *)img_cur, h->stream));
         if (out->cumulative_image)
             HIPCALL(h, lde::launch_rows_f32(h->d_cumf, h->S, h->T, h->range_lo, h->range_hi,
-                                            (float *)h->d_img_cum, h->stream));
+                                            (float *)img_cum, h->stream));
         if (want_cur_hist)
             HIPCALL(h, hipMemcpyAsync(out->current_hist, h->d_winf, nb * 4, hipMemcpyDeviceToHost,
                                       h->stream));
@@ -1663,20 +1680,26 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
         Timed tm(h, LDE_K_FINALIZE);
         // the per-block total partials and the overflow flag land in the
         // pack (summed here on the host: no k_sum_totals launch and gap)
-        unsigned char *d_tail = h->d_pack + (size_t)h->S * 16;
+        unsigned char *d_tail = pk + (size_t)h->S * 16;
         HIPCALL(h, lde::launch_finalize(
                        f32 ? 1 : 0, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
                        (want_cur_hist && !f32) ? h->d_snap : nullptr, h->S, h->T, h->range_lo,
-                       h->range_hi, (!f32 && out->current_image) ? h->d_img_cur : nullptr,
-                       (!f32 && out->cumulative_image) ? h->d_img_cum : nullptr, h->d_tot4,
+                       h->range_hi, (!f32 && out->current_image) ? img_cur : nullptr,
+                       (!f32 && out->cumulative_image) ? img_cum : nullptr, h->d_tot4,
                        (unsigned long long *)d_tail, h->d_overflow, (uint32_t *)(d_tail + 32),
                        h->stream, (unsigned long long *)(d_tail + 48), &n_parts));
     }
     const size_t isz = f32 ? 4 : 8;
-    // images, partials and the overflow flag leave in one pinned D2H copy
-    // (separate copies into pageable memory cost ~25 us each)
-    HIPCALL(h, hipMemcpyAsync(h->h_pack, h->d_pack, (size_t)h->S * 16 + 48 + 32 * (size_t)n_parts,
-                              hipMemcpyDeviceToHost, h->stream));
+    if (h->hd_pack) {
+        // a system-scope release after the kernel: its host writes are visible
+        // once the stream has passed this point
+        HIPCALL(h, hipEventRecord(h->fin_event, h->stream));
+    } else {
+        // images, partials and the overflow flag leave in one pinned D2H copy
+        // (separate copies into pageable memory cost ~25 us each)
+        HIPCALL(h, hipMemcpyAsync(h->h_pack, h->d_pack, (size_t)h->S * 16 + 48 + 32 * (size_t)n_parts,
+                                  hipMemcpyDeviceToHost, h->stream));
+    }
     std::vector<unsigned long long> tmp;
     if (!f32 && (want_cur_hist || want_cum_hist)) tmp.resize(nb);
     if (!f32 && want_cur_hist) {

@@ -134,13 +134,18 @@ __global__ __launch_bounds__(256) void k_finalize_v4(uint32_t *__restrict__ win3
                                                   uint32_t *__restrict__ ovf_dst) {
     typedef unsigned long long u64;
     __shared__ u64 s_tot[8][4];
+    __shared__ OUT s_img[2][8];
     const int gl = threadIdx.x & 31, grp = threadIdx.x >> 5;  // 8 row groups per block
     u64 acc[4] = {0, 0, 0, 0};
     const int i0 = gl * 4;
     const bool act = i0 < T;
-    for (long long s = (long long)blockIdx.x * 8 + grp; s < S; s += (long long)gridDim.x * 8) {
+    // uniform loop over the block's 8-row slices: the slice's image values
+    // leave through LDS as two contiguous 8-element runs (one store
+    // instruction each), which matters when the images are host-mapped
+    for (long long base = (long long)blockIdx.x * 8; base < S; base += (long long)gridDim.x * 8) {
+        const long long s = base + grp;
         u64 rw = 0, rc = 0, tw = 0, tc = 0;
-        if (act) {
+        if (act && s < S) {
             const long long k = s * T + i0;
             const uint4 w4 = *reinterpret_cast<const uint4 *>(win32 + k);
             u64 w[4] = {w4.x, w4.y, w4.z, w4.w};
@@ -179,13 +184,20 @@ __global__ __launch_bounds__(256) void k_finalize_v4(uint32_t *__restrict__ win3
             tc += __shfl_xor(tc, d, 32);
         }
         if (gl == 0) {
-            if (cur_img) cur_img[s] = (OUT)rw;
-            if (cum_img) cum_img[s] = (OUT)rc;
+            s_img[0][grp] = (OUT)rw;
+            s_img[1][grp] = (OUT)rc;
             acc[0] += tw;
             acc[1] += rw;
             acc[2] += tc;
             acc[3] += rc;
         }
+        __syncthreads();
+        if (threadIdx.x < 16) {
+            const int r = threadIdx.x & 7;
+            OUT *img = threadIdx.x < 8 ? cur_img : cum_img;
+            if (img && base + r < S) img[base + r] = s_img[threadIdx.x >> 3][r];
+        }
+        __syncthreads();
     }
     if (gl == 0)
         for (int q = 0; q < 4; ++q) s_tot[grp][q] = acc[q];
