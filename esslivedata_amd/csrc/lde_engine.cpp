@@ -19,6 +19,7 @@
 #include <limits>
 #include <new>
 #include <atomic>
+#include <chrono>
 #include <string>
 #include <thread>
 #include <vector>
@@ -215,6 +216,11 @@ struct lde_handle {
     long long kcount[LDE_K_COUNT] = {};
 
     std::string err;
+    // LDE_HOST_PROBE: host time from lde_accumulate entry to the sieve launch
+    bool probe = false;
+    std::chrono::steady_clock::time_point t_acc0;
+    double probe_us = 0.0, probe_min = 0.0;
+    long long probe_n = 0;
 };
 
 namespace {
@@ -821,6 +827,13 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                                                  h->d_chunk_tab, h->stream));
             }
             HIPCALL(h, lde::launch_sieve(sa, a.grid, h->stream, ea, eb));
+            if (h->probe) {
+                const double us = std::chrono::duration<double, std::micro>(
+                                      std::chrono::steady_clock::now() - h->t_acc0).count();
+                h->probe_us += us;
+                h->probe_min = h->probe_n ? std::min(h->probe_min, us) : us;
+                ++h->probe_n;
+            }
             if (ea) h->launches.push_back({LDE_K_SPLIT, ea, eb});
         }
         lde::ColdArgs c;
@@ -1380,6 +1393,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->karg_segs = env_ll("LDE_KARG_SEGS", 1) != 0;
         h->sieve_ablate = (int)env_ll("LDE_SIEVE_ABLATE", 0);
         h->early_gather = env_ll("LDE_EARLY_GATHER", 0) != 0;
+        h->probe = env_ll("LDE_HOST_PROBE", 0) != 0;
         h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);
@@ -1396,6 +1410,9 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
 
 void lde_destroy(lde_handle *h) {
     if (!h) return;
+    if (h->probe && h->probe_n)
+        fprintf(stderr, "lde probe: accumulate entry -> sieve launched %.2f us mean, %.2f us min (%lld)\n",
+                h->probe_us / h->probe_n, h->probe_min, h->probe_n);
     DeviceGuard guard(h->device);
     release(h);
 }
@@ -1546,6 +1563,7 @@ int lde_accumulate(lde_handle *h, int32_t replica) {
     if (replica < 0 || replica >= h->R)
         return fail(h, LDE_EINVAL, "replica %d out of range [0, %d)", replica, h->R);
     DeviceGuard guard(h->device);
+    if (h->probe) h->t_acc0 = std::chrono::steady_clock::now();
     std::vector<Segment> segs;
     if (h->staged_host > 0) segs.push_back({h->d_spid, h->d_stoa, h->staged_host});
     for (const Segment &s : h->dev_segments) segs.push_back(s);

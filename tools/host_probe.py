@@ -88,3 +88,21 @@ t0 = time.perf_counter()
 for _ in range(200):
     np.copyto(buf, src)
 print('host copy of 410 KB (us):', round((time.perf_counter() - t0) / 200 * 1e6, 2))
+
+# python-side cost of the finalize wrapper around the C call (GPU idle)
+import ctypes
+from esslivedata_amd import _native
+tw = []
+for i in range(20):
+    eng.stage_tensors_batch(msgs)
+    eng.accumulate(i % view.n_replicas)
+    eng.synchronize()
+    out = _native.LdeOutputs()
+    a1 = np.empty(view.n_screen); a2 = np.empty(view.n_screen)
+    out.current_image = a1.ctypes.data; out.cumulative_image = a2.ctypes.data
+    t0 = time.perf_counter()
+    eng._lib.lde_finalize(eng._h, ctypes.byref(out))
+    t1 = time.perf_counter()
+    tw.append(t1 - t0)
+print('raw lde_finalize with idle GPU (us): median', round(sorted(tw)[10] * 1e6, 1))
+del eng
