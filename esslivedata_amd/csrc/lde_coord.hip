@@ -45,22 +45,62 @@ __device__ __forceinline__ int coord_bin(double v, const double *e, const uint16
     return b;
 }
 
-template <bool TLDS>
-__global__ __launch_bounds__(256) void k_event_coord(CoordArgs a, const int *__restrict__ pid,
-                                                     const int *__restrict__ toa, long long n,
-                                                     int *__restrict__ out) {
+// Distance cache image: slot j holds the most-sampled pixel q = j (mod C)
+// with a distance (q, else -1) and that distance.  Built after a hot-set
+// selection from the sampled pixel counts; the coordinate pass keeps it in
+// LDS so the frequent pixels need no gather.
+__global__ __launch_bounds__(256) void k_coord_cache(const uint32_t *__restrict__ cnt,
+                                                     const double *__restrict__ pix_d, long long L,
+                                                     int cbits, uint32_t *__restrict__ cq,
+                                                     double *__restrict__ cd) {
+    const long long C = 1LL << cbits;
+    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (j >= C) return;
+    uint32_t best = 0;
+    long long bq = -1;
+    for (long long q = j; q < L; q += C) {
+        const uint32_t c = cnt[q];
+        if (c > best) {
+            best = c;
+            bq = q;
+        }
+    }
+    cq[j] = bq < 0 ? 0xFFFFFFFFu : (uint32_t)bq;
+    cd[j] = bq < 0 ? 0.0 : pix_d[bq];
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t coord_rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes,
+                                             (int)0x00020000);  // raw buffer, 32-bit format
+}
+
+template <bool TLDS, bool CACHE, bool ELDS>
+__global__ __launch_bounds__(1024) void k_event_coord(CoordArgs a, const int *__restrict__ pid,
+                                                      const int *__restrict__ toa, long long n,
+                                                      int *__restrict__ out) {
     extern __shared__ double sm[];
-    // LDS: edges (T + 1, when they fit) | table (TLDS) | bucket table (u16)
-    const int ne = a.edges_lds ? a.T + 1 : 0;
-    double *s_e = sm;
-    double *s_t = sm + ((ne + 1) & ~1);
+    // LDS: distance cache (CACHE: C doubles + C pixel ids) | edges (T + 1,
+    // when they fit) | table (TLDS) | bucket table (u16)
+    const int C = CACHE ? 1 << a.cache_bits : 0;
+    double *s_cd = sm;
+    uint32_t *s_cq = reinterpret_cast<uint32_t *>(sm + C);
+    double *s_e = sm + C + C / 2;
+    const int ne = ELDS ? a.T + 1 : 0;
+    double *s_t = s_e + ((ne + 1) & ~1);
     const int ntab = TLDS ? a.nd * a.nt : 0;
     uint16_t *s_b = reinterpret_cast<uint16_t *>(s_t + ntab);
+    for (int i = threadIdx.x; i < C; i += blockDim.x) {
+        s_cd[i] = a.cache_d[i];
+        s_cq[i] = a.cache_q[i];
+    }
     for (int i = threadIdx.x; i < ne; i += blockDim.x) s_e[i] = a.edges[i];
     for (int i = threadIdx.x; i < ntab; i += blockDim.x) s_t[i] = a.table[i];
     for (int i = threadIdx.x; i < a.G; i += blockDim.x) s_b[i] = a.buckets[i];
     __syncthreads();
-    const double *e = a.edges_lds ? s_e : a.edges;
+    const __amdgpu_buffer_rsrc_t drs = coord_rsrc(a.pix_d, a.L * 8u);
+    // compile-time LDS or global: a runtime choice makes every edge read a
+    // flat load (counted by both vmcnt and lgkmcnt)
+    const double *e = ELDS ? s_e : a.edges;
     const double *tab = TLDS ? s_t : a.table;
     const double xmax = (double)(a.nd - 1), ymax = (double)(a.nt - 1);
     // one event: its pixel's distance d (NaN: none) and time t -> bin or -1
@@ -87,25 +127,40 @@ __global__ __launch_bounds__(256) void k_event_coord(CoordArgs a, const int *__r
     auto dist = [&](int p) __attribute__((always_inline)) {
         // monitors carry no pixel ids: every event is at the one distance
         const unsigned q = pid ? (unsigned)p - (unsigned)a.pid_off : 0u;
-        return q < a.L ? a.pix_d[q] : __builtin_nan("");
+        if (!CACHE) return q < a.L ? a.pix_d[q] : __builtin_nan("");
+        // cached pixels load out of range (no request, returns 0), the others
+        // gather; ids outside the LUT read the NaN past its end... as -1 below
+        const unsigned slot = q & (unsigned)(C - 1);
+        const bool hit = s_cq[slot] == q;
+        const int off = (hit || q >= a.L) ? (int)0x80000000 : (int)(q * 8u);
+        const double g = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(drs, off, 0, 0));
+        return hit ? s_cd[slot] : (q < a.L ? g : __builtin_nan(""));
     };
     constexpr int V = 8;  // events per thread and iteration: every load issued first
     const bool vec = ((((uintptr_t)pid | (uintptr_t)toa | (uintptr_t)out) & 15u) == 0) && pid;
     const long long stride = (long long)gridDim.x * blockDim.x * V;
     long long k0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * V;
     if (vec) {
-        for (; k0 + V <= n; k0 += stride) {
-            int p[V], t[V];
+        // the next group's events are requested before this group's gathers
+        // and arithmetic (one group of loads always in flight)
+        int p[V], t[V];
+        auto load = [&](long long k, int (&pp)[V], int (&tt)[V]) __attribute__((always_inline)) {
 #pragma unroll
             for (int h = 0; h < V / 4; ++h) {
-                const v4i pv = ld_stream4(pid + k0 + 4 * h);
-                const v4i tv = ld_stream4(toa + k0 + 4 * h);
+                const v4i pv = ld_stream4(pid + k + 4 * h);
+                const v4i tv = ld_stream4(toa + k + 4 * h);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    p[4 * h + q] = pv[q];
-                    t[4 * h + q] = tv[q];
+                    pp[4 * h + q] = pv[q];
+                    tt[4 * h + q] = tv[q];
                 }
             }
+        };
+        if (k0 + V <= n) load(k0, p, t);
+        for (; k0 + V <= n; k0 += stride) {
+            int np[V], nt[V];
+            const bool more = k0 + stride + V <= n;
+            if (more) load(k0 + stride, np, nt);
             double d[V];
 #pragma unroll
             for (int q = 0; q < V; ++q) d[q] = dist(p[q]);
@@ -116,6 +171,13 @@ __global__ __launch_bounds__(256) void k_event_coord(CoordArgs a, const int *__r
             for (int h = 0; h < V / 4; ++h)
                 *reinterpret_cast<int4 *>(out + k0 + 4 * h) =
                     make_int4(b[4 * h], b[4 * h + 1], b[4 * h + 2], b[4 * h + 3]);
+            if (more) {
+#pragma unroll
+                for (int q = 0; q < V; ++q) {
+                    p[q] = np[q];
+                    t[q] = nt[q];
+                }
+            }
         }
     }
     // the vectorized loop's last, partial group; or every group of a segment
@@ -127,30 +189,56 @@ __global__ __launch_bounds__(256) void k_event_coord(CoordArgs a, const int *__r
     }
 }
 
-size_t coord_smem(const CoordArgs &a, bool table_lds) {
+size_t coord_smem(const CoordArgs &a, bool table_lds, bool cache) {
     const int ne = a.edges_lds ? a.T + 1 : 0;
-    return 8 * (size_t)((ne + 1) & ~1) + (table_lds ? 8 * (size_t)a.nd * a.nt : 0) +
+    const size_t C = cache ? (size_t)1 << a.cache_bits : 0;
+    return 12 * C + 8 * (size_t)((ne + 1) & ~1) + (table_lds ? 8 * (size_t)a.nd * a.nt : 0) +
            2 * (size_t)a.G;
+}
+
+hipError_t launch_coord_cache(const uint32_t *pix_cnt, const double *pix_d, long long L, int cbits,
+                              uint32_t *cq, double *cd, hipStream_t st) {
+    hipLaunchKernelGGL(k_coord_cache, dim3((unsigned)(((1LL << cbits) + 255) / 256)), dim3(256), 0, st,
+                       pix_cnt, pix_d, L, cbits, cq, cd);
+    return hipGetLastError();
+}
+
+template <bool TLDS, bool CACHE, bool ELDS>
+static void launch_coord_t(const CoordArgs &a, const int *pid, const int *toa, long long n, int *out,
+                           size_t sm, int threads, long long g, hipStream_t st) {
+    (void)hipFuncSetAttribute((const void *)k_event_coord<TLDS, CACHE, ELDS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    hipLaunchKernelGGL((k_event_coord<TLDS, CACHE, ELDS>), dim3((unsigned)g), dim3(threads), sm, st, a,
+                       pid, toa, n, out);
+}
+
+template <bool TLDS, bool CACHE>
+static void launch_coord_e(const CoordArgs &a, const int *pid, const int *toa, long long n, int *out,
+                           size_t sm, int threads, long long g, hipStream_t st) {
+    if (a.edges_lds) launch_coord_t<TLDS, CACHE, true>(a, pid, toa, n, out, sm, threads, g, st);
+    else launch_coord_t<TLDS, CACHE, false>(a, pid, toa, n, out, sm, threads, g, st);
 }
 
 hipError_t launch_event_coord(const CoordArgs &a, const int *pid, const int *toa, long long n,
                               int *out, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    long long g = (n + 256 * 8 - 1) / (256 * 8);
-    if (g > 4096) g = 4096;
-    const bool tl = coord_smem(a, true) <= kCoordSmemMax;
-    const size_t sm = coord_smem(a, tl);
+    // with the distance cache: one 1024-thread block per CU (the cache fills
+    // most of the LDS); without: 256-thread blocks, several per CU
+    const bool cache = a.cache_bits > 0 && a.cache_q && pid &&
+                       coord_smem(a, false, true) <= kCoordSmemMax;
+    const bool tl = coord_smem(a, true, cache) <= kCoordSmemMax;
+    const size_t sm = coord_smem(a, tl, cache);
     if (sm > kCoordSmemMax) return hipErrorInvalidValue;
-    if (tl) {
-        (void)hipFuncSetAttribute((const void *)k_event_coord<true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL(k_event_coord<true>, dim3((unsigned)g), dim3(256), sm, st, a, pid, toa,
-                           n, out);
+    const int threads = cache ? 1024 : 256;
+    long long g = (n + (long long)threads * 8 - 1) / ((long long)threads * 8);
+    const long long gmax = cache ? a.cus : 4096;
+    if (g > gmax) g = gmax;
+    if (cache) {
+        if (tl) launch_coord_e<true, true>(a, pid, toa, n, out, sm, threads, g, st);
+        else launch_coord_e<false, true>(a, pid, toa, n, out, sm, threads, g, st);
     } else {
-        (void)hipFuncSetAttribute((const void *)k_event_coord<false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL(k_event_coord<false>, dim3((unsigned)g), dim3(256), sm, st, a, pid, toa,
-                           n, out);
+        if (tl) launch_coord_e<true, false>(a, pid, toa, n, out, sm, threads, g, st);
+        else launch_coord_e<false, false>(a, pid, toa, n, out, sm, threads, g, st);
     }
     return hipGetLastError();
 }

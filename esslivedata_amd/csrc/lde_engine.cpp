@@ -150,6 +150,9 @@ struct lde_handle {
     bool coord = false;
     lde::CoordArgs cargs{};
     uint16_t *d_cbuck = nullptr;  // coordinate bucket table
+    uint32_t *d_ccq = nullptr;    // coordinate distance cache: pixel per slot
+    double *d_ccd = nullptr;      // ... and its distance
+    bool coord_cache_built = false;
     double *d_cpd = nullptr, *d_ctable = nullptr, *d_cedges = nullptr;
     int *d_cbin = nullptr;
     size_t cbin_cap = 0;
@@ -719,6 +722,19 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                                h->d_glut + (size_t)(h->L + 1) * r,
                                h->d_sieve_tab + ((size_t)r << h->cache_bits), h->stream));
         }
+        if (h->coord && h->d_pix_cnt) {
+            // wavelength mode: the sampled hottest pixels' distances in LDS
+            if (!h->d_ccq) {
+                if (int rc = dev_alloc(h, &h->d_ccq, (size_t)1 << lde::kCoordCacheBits)) return rc;
+                if (int rc = dev_alloc(h, &h->d_ccd, (size_t)1 << lde::kCoordCacheBits)) return rc;
+            }
+            HIPCALL(h, lde::launch_coord_cache(h->d_pix_cnt, h->d_cpd, h->L, lde::kCoordCacheBits,
+                                               h->d_ccq, h->d_ccd, h->stream));
+            h->cargs.cache_q = h->d_ccq;
+            h->cargs.cache_d = h->d_ccd;
+            h->cargs.cache_bits = lde::kCoordCacheBits;
+            h->coord_cache_built = true;
+        }
         HIPCALL(h, hipMemcpyAsync(h->h_sel_stats, h->d_sel_stats, (size_t)h->R * 16,
                                   hipMemcpyDeviceToHost, h->stream));
         HIPCALL(h, hipStreamSynchronize(h->stream));
@@ -1064,6 +1080,8 @@ void release(lde_handle *h) {
     dev_free(h->d_cpd);
     dev_free(h->d_ctable);
     dev_free(h->d_cedges);
+    dev_free(h->d_ccq);
+    dev_free(h->d_ccd);
     dev_free(h->d_cbin);
     dev_free(h->d_win32);
     dev_free(h->d_win64);
@@ -2056,7 +2074,18 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     c.e0 = ed[0];
     c.inv_w = 1.0 / w;
     c.edges_lds = 1;
-    if (lde::coord_smem(c, false) > lde::kCoordSmemMax) c.edges_lds = 0;  // huge T: edges from HBM
+    if (lde::coord_smem(c, false, false) > lde::kCoordSmemMax) c.edges_lds = 0;  // huge T: edges from HBM
+    c.cus = h->cus;
+    // the distance cache follows the pixel distances: rebuilt from the last
+    // sampled pixel counts, else off until the next hot-set selection
+    c.cache_bits = 0;
+    if (h->coord_cache_built) {
+        HIPCALL(h, lde::launch_coord_cache(h->d_pix_cnt, h->d_cpd, h->L, lde::kCoordCacheBits,
+                                           h->d_ccq, h->d_ccd, h->stream));
+        c.cache_q = h->d_ccq;
+        c.cache_d = h->d_ccd;
+        c.cache_bits = lde::kCoordCacheBits;
+    }
     h->coord = true;
     if (!rebind)
         for (auto &u : h->hot_uses) u = -1;  // hot sets re-select on the new value

@@ -301,9 +301,16 @@ struct CoordArgs {
     const uint16_t *buckets;  // [G] first candidate bin per bucket of the edge range
     int G;
     double e0, inv_w;       // bucket g = (v - e0) * inv_w
+    const uint32_t *cache_q = nullptr;  // [1 << cache_bits] cached pixel per slot (-1: none)
+    const double *cache_d = nullptr;    // its distance
+    int cache_bits = 0;                 // 0: no distance cache
+    int cus = 256;                      // grid of the cached variant (one block per CU)
 };
-constexpr size_t kCoordSmemMax = 96 * 1024;
-size_t coord_smem(const CoordArgs &a, bool table_lds);
+constexpr size_t kCoordSmemMax = 160 * 1024;
+constexpr int kCoordCacheBits = 13;  // 8192-slot distance cache (96 KB of LDS)
+size_t coord_smem(const CoordArgs &a, bool table_lds, bool cache);
+hipError_t launch_coord_cache(const uint32_t *pix_cnt, const double *pix_d, long long L, int cbits,
+                              uint32_t *cq, double *cd, hipStream_t st);
 hipError_t launch_event_coord(const CoordArgs &a, const int *pid, const int *toa, long long n,
                               int *out, hipStream_t st);
 
