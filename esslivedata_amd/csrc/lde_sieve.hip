@@ -348,6 +348,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             uint32_t off = vsel(hit, kOOBi, min(qs[e], Lc) << 2);
             if (ABL & 16) off = kOOB | (off & 4u);
             if (ABL & 32) off = off & 4u;
+            if (ABL & 131072) off = (off & 0x80000000u) | (off & 0xFFFCu);  // gathers confined to 64 KB
             if (ABL & 65536) {
                 // T <= kSieveMaxT (254): bins >= 255 (past the edges) stay dropped
                 const uint32_t b = min((tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u), 255u);
@@ -1029,7 +1030,7 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     LDE_SIEVE_MODE(256) LDE_SIEVE_MODE(512) LDE_SIEVE_MODE(1024) LDE_SIEVE_MODE(2048)
     LDE_SIEVE_MODE(4096) LDE_SIEVE_MODE(8192) LDE_SIEVE_MODE(12288) LDE_SIEVE_MODE(16384)
     LDE_SIEVE_MODE(49152) LDE_SIEVE_MODE(65536) LDE_SIEVE_MODE(65536 | 256)
-    LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048)
+    LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048) LDE_SIEVE_MODE(131072)
 #undef LDE_SIEVE_MODE
     default: return hipErrorInvalidValue;
     }
