@@ -162,6 +162,9 @@ struct lde_handle {
     int sieve_ablate = 0;
     bool early_gather = false;  // LDE_EARLY_GATHER
     bool sieve_pack = false;    // LDE_SIEVE_PACK
+    int cold_sort_mode = 2;     // LDE_COLD_SORT: 0 block, 1 wave-independent, 2 16-byte groups
+    int cold_sort_kpt = 32;     // LDE_COLD_SORT_KPT: keys per thread per piece of mode 2
+    int cold_sort_ablate = 0;   // LDE_COLD_SORT_ABLATE (diagnostic, wrong results)
     uint32_t ttab_cap = 0;
     int ttab_shift = 0;
     lde::ChunkPtrs *d_chunk_tab = nullptr;
@@ -774,9 +777,14 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         const size_t nt = (size_t)h->n_tiles;
         if (int rc = grow(h, &h->d_cold_tcnt, h->cold_tcnt_cap, (size_t)a.grid * lde::kColdGroups * nt)) return rc;
         if (int rc = grow(h, &h->d_cold_boff, h->cold_boff_cap, (size_t)a.grid * lde::kColdGroups * nt)) return rc;
-        // tile-major u16 keys: at most every staged slot, + slack for pass B's 16-byte loads
+        // tile-major u16 keys: at most every staged slot, + the 8-key padding
+        // of every (row, tile) range (k_cold_sort_a), + slack for pass B's
+        // 16-byte loads
+        const bool pad8 = h->cold_sort_mode == 2 && h->n_tiles <= lde::kSortThreadsHost &&
+                          lde::cold_sort_a_smem(h->n_tiles, h->cold_sort_kpt) <= 80 * 1024;
         if (int rc = grow(h, &h->d_cold_keys, h->cold_keys_cap,
-                          (size_t)a.grid * (size_t)a.cold_cap + 64))
+                          (size_t)a.grid * (size_t)a.cold_cap +
+                              (pad8 ? (size_t)a.grid * lde::kColdGroups * nt * 8 : 0) + 64))
             return rc;
         const double cold_est = std::min(1.0, std::max(0.05, 1.0 - h->hot_cov[replica])) * (double)total;
         const long long item_keys = h->item_events_override > 0
@@ -875,6 +883,10 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         c.keys = h->d_cold_keys;
         c.hist = h->d_win32;
         c.n_bins = h->nbins;
+        c.wave_sort = h->cold_sort_mode == 1 ? 1 : 0;
+        c.pad8 = pad8 ? 1 : 0;
+        c.sort_kpt = h->cold_sort_kpt;
+        c.ablate = h->cold_sort_ablate;
         Timed tm(h, LDE_K_PAGED);
         HIPCALL(h, lde::launch_cold_pipeline(c, h->stream, h->bin_stop_ext));
         if (h->bin_stop_ext) h->bin_stop_used = true;
@@ -1413,6 +1425,9 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->early_gather = env_ll("LDE_EARLY_GATHER", 0) != 0;
         h->probe = env_ll("LDE_HOST_PROBE", 0) != 0;
         h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
+        h->cold_sort_mode = (int)env_ll("LDE_COLD_SORT", 2);
+        h->cold_sort_kpt = env_ll("LDE_COLD_SORT_KPT", 32) == 16 ? 16 : 32;
+        h->cold_sort_ablate = (int)env_ll("LDE_COLD_SORT_ABLATE", 0);
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);
         h->auto_partition = (int)env_ll("LDE_AUTO_PARTITION", LDE_STRATEGY_PAGED);

@@ -224,8 +224,15 @@ struct ColdArgs {
     uint16_t *keys;  // tile-major, 16-byte aligned, >= total + 8 entries
     uint32_t *hist;
     long long n_bins;
+    int wave_sort = 0;  // 1: k_cold_sort_w (wave-independent) when its LDS fits
+    int pad8 = 0;       // 1: k_cold_sort_a (16-byte groups; ranges padded to 8 keys)
+    int sort_kpt = 32;  // k_cold_sort_a keys per thread per piece (16 or 32)
+    int ablate = 0;     // cold-sort diagnostics (wrong results): 1 no writes, 2 no loads
 };
 size_t cold_sort_smem(int n_tiles);
+size_t cold_sort_w_smem(int n_tiles);
+size_t cold_sort_a_smem(int n_tiles, int kpt);
+constexpr int kSortThreadsHost = 64 * (kSplitThreads / 64) / kColdGroups;  // cold-sort block
 // start/stop: optional HIP events stamped by the kernel dispatch itself
 // (hipExtLaunchKernelGGL), so timing adds no marker packets between kernels
 hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t stop = nullptr);

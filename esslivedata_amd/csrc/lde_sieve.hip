@@ -35,6 +35,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "lde_device.h"
 #include "lde_internal.h"
 
@@ -638,7 +640,8 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
     uint32_t carry = 0;
     for (int r0 = 0; r0 < rows; r0 += 256) {
         const int r = r0 + threadIdx.x;
-        const uint32_t v = r < rows ? c.tcnt[(size_t)r * c.n_tiles + t] : 0u;
+        uint32_t v = r < rows ? c.tcnt[(size_t)r * c.n_tiles + t] : 0u;
+        if (c.pad8) v = (v + 7u) & ~7u;  // k_cold_sort_a: 16-byte aligned (row, tile) ranges
         uint32_t tot;
         const uint32_t ex = block_exclusive_scan(v, s_w, &tot);
         if (r < rows) c.boff[(size_t)r * c.n_tiles + t] = carry + ex;
@@ -648,7 +651,7 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
     if (threadIdx.x == 0) c.tile_total[t] = carry;
 }
 
-constexpr int kSortThreads = 64 * (kSplitThreads / 64) / kColdGroups;  // one wave per sieve wave
+constexpr int kSortThreads = kSortThreadsHost;  // one wave per sieve wave
 constexpr int kSortWaves = kSortThreads / 64;
 constexpr int kSortKPT = 16;                           // keys per lane per piece
 constexpr int kSortPiece = kSortThreads * kSortKPT;    // 8192
@@ -868,9 +871,338 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(ColdArgs c) {
         __syncthreads();
         for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
             const uint32_t k = s_sorted[i];
-            out[s_delta[k >> SH] + i] = (uint16_t)((k >> 2) & MASK);
+            if (!(c.ablate & 1)) out[s_delta[k >> SH] + i] = (uint16_t)((k >> 2) & MASK);
         }
         __syncthreads();
+    }
+}
+
+// Wave-independent variant of k_cold_sort: same block <-> region mapping and
+// the same tile-major output, but every sort wave sorts its own pieces of
+// kWsPiece keys in wave-private LDS with no block barrier after the set-up.
+// A wave's run of tile t is placed by one LDS atomicAdd on the block's tile
+// cursor s_pos[t] (pass B counts keys per tile, so the order of the runs
+// inside a (block, tile) range does not matter).  Per key: one LDS count
+// atomic, one returning LDS atomic for its slot, the scatter into the wave's
+// image, one sequential read back and one read of the run's offset -- about
+// half the LDS instructions of the block-cooperative sort, no barrier stalls.
+constexpr int kWsKPT = 32;                 // keys per lane per wave piece
+constexpr int kWsPiece = 64 * kWsKPT;      // 2048 keys
+size_t cold_sort_w_smem(int n_tiles) {
+    const size_t nt4 = (size_t)align4(n_tiles);
+    return 4 * (nt4 + 32 + (size_t)kSortWaves * ((size_t)kWsPiece + 2 * nt4));
+}
+
+template <int TB>
+__global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_cold_sort_w(ColdArgs c) {
+    const int n_tiles = c.n_tiles;
+    uint16_t *__restrict__ out = c.keys;
+    constexpr uint32_t MASK = (1u << TB) - 1u;
+    constexpr int SH = TB + 2;  // keys are scaled by 4
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    const int nt4 = align4(n_tiles);
+    const int tid = threadIdx.x;
+    const int wv = tid >> 6, lane = tid & 63;
+    uint32_t *s_pos = sm;         // [tile] the block's next global position
+    uint32_t *s_w = sm + nt4;     // scan scratch
+    uint32_t *s_wave = s_w + 32;  // per wave: image | base | delta
+    uint32_t *img = s_wave + wv * (kWsPiece + 2 * nt4);
+    uint32_t *base = img + kWsPiece;
+    uint32_t *dlt = base + nt4;
+    const int b = blockIdx.x / kColdGroups, grp = blockIdx.x % kColdGroups;
+    const int row = blockIdx.x;
+    constexpr int NW = kSplitThreads / 64;
+    const uint32_t capw = (uint32_t)(c.cap / NW);
+    const int sw = grp * kSortWaves + wv;
+    const uint32_t n_w = c.cold_cnt[(size_t)b * NW + sw];
+    // the items of pass B (block 0; the wave images are its scratch)
+    if (row == 0)
+        plan_items(c.tile_total, n_tiles, c.item_keys, c.items, c.item_count, c.max_items, s_w,
+                   s_wave, s_wave + kMaxTiles + 1);
+    {
+        constexpr int TPT = (kMaxTiles + kSortThreads - 1) / kSortThreads;
+        uint32_t tt[TPT], sum = 0;
+#pragma unroll
+        for (int q = 0; q < TPT; ++q) {
+            const int t = tid * TPT + q;
+            tt[q] = t < n_tiles ? c.tile_total[t] : 0u;
+            sum += tt[q];
+        }
+        uint32_t total;
+        uint32_t run = block_exclusive_scan(sum, s_w, &total);
+#pragma unroll
+        for (int q = 0; q < TPT; ++q) {
+            const int t = tid * TPT + q;
+            if (t < n_tiles) s_pos[t] = run + c.boff[(size_t)row * n_tiles + t];
+            run += tt[q];
+        }
+    }
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rs =
+        make_rsrc(c.cold + (size_t)b * (size_t)c.stride + (size_t)sw * capw, n_w * 4u);
+    const uint32_t npieces = (n_w + kWsPiece - 1) / kWsPiece;
+    const int tpl = (n_tiles + 63) / 64;  // tiles per lane in the wave scan
+    const int t0 = lane * tpl;
+    v4u nk[kWsKPT / 4];
+    auto fetch = [&](uint32_t p) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < kWsKPT / 4; ++j) {
+            const uint32_t e0 = p * (uint32_t)kWsPiece + (uint32_t)j * 256u + (uint32_t)lane * 4u;
+            nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
+        }
+    };
+    if (npieces && !(c.ablate & 2)) fetch(0);
+    for (uint32_t p = 0; p < npieces; ++p) {
+        for (int i = lane; i < nt4; i += 64) base[i] = 0;
+        uint32_t key[kWsKPT];
+#pragma unroll
+        for (int j = 0; j < kWsKPT / 4; ++j) {
+            const uint32_t e0 = p * (uint32_t)kWsPiece + (uint32_t)j * 256u + (uint32_t)lane * 4u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n_w ? nk[j][q] : 0xFFFFFFFFu;
+        }
+        if (c.ablate & 2) {  // diagnostic: keys synthesized, not loaded
+#pragma unroll
+            for (int e = 0; e < kWsKPT; ++e)
+                key[e] = ((((uint32_t)(lane * kWsKPT + e) + p * 977u) * 2654435761u) %
+                          ((uint32_t)n_tiles << TB)) << 2;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int e = 0; e < kWsKPT; ++e)
+            if (key[e] != 0xFFFFFFFFu)
+                __hip_atomic_fetch_add(base + (key[e] >> SH), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_wave_barrier();
+        // counts -> run bases in the image (wave scan, tpl tiles per lane);
+        // each non-empty run reserves its place in the block's tile range
+        uint32_t lsum = 0;
+        for (int j = 0; j < tpl; ++j) {
+            const int t = t0 + j;
+            if (t < n_tiles) lsum += base[t];
+        }
+        const uint32_t inc = wave_inclusive_scan(lsum);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        uint32_t run = inc - lsum;
+        for (int j = 0; j < tpl; ++j) {
+            const int t = t0 + j;
+            if (t < n_tiles) {
+                const uint32_t n = base[t];
+                base[t] = run;
+                if (n)
+                    dlt[t] = __hip_atomic_fetch_add(s_pos + t, n, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP) - run;
+                run += n;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // scatter: each key takes the next slot of its run (order inside a
+        // run is irrelevant), so no per-key rank is kept in registers
+#pragma unroll
+        for (int e = 0; e < kWsKPT; ++e) {
+            // the tile index is recomputed (opaque to CSE), so the count
+            // pass's LDS addresses do not stay live in registers
+            uint32_t k = key[e];
+            asm volatile("" : "+v"(k));
+            if (k != 0xFFFFFFFFu)
+                img[__hip_atomic_fetch_add(base + (k >> SH), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP)] = k;
+        }
+        // the next piece's keys are requested once this piece's are dead (the
+        // register budget of two blocks per CU), ahead of the write-out
+        if (p + 1 < npieces && !(c.ablate & 2)) fetch(p + 1);
+        __builtin_amdgcn_wave_barrier();
+        // runs leave as u16 tile-local keys, four image words per lane in flight
+        for (uint32_t i0 = (uint32_t)lane; i0 < total; i0 += 256u) {
+            uint32_t k[4], d[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t i = i0 + 64u * (uint32_t)u;
+                k[u] = i < total ? img[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) d[u] = dlt[k[u] >> SH];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t i = i0 + 64u * (uint32_t)u;
+                if (i < total && !(c.ablate & 1)) out[d[u] + i] = (uint16_t)((k[u] >> 2) & MASK);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Block-cooperative sort with whole 16-byte output groups (n_tiles <=
+// kSortThreads: thread t owns tile t).  The scan gives every (row, tile)
+// range a length rounded up to 8 keys, so each range starts 16-byte aligned.
+// A piece's run of a tile is placed in the tile-sorted image behind the <= 7
+// keys the tile carried over from earlier pieces; the full 8-key groups leave
+// as one 16-byte store each and the rest is carried again; the last carry of
+// each tile leaves padded with 0xFFFF (skipped by pass B).  The image holds
+// u16 tile-local keys.  Compared with k_cold_sort's per-key u16 stores into
+// short unaligned runs this issues 8x fewer store lanes and no partial lines.
+size_t cold_sort_a_smem(int n_tiles, int kpt) {
+    const size_t nt4 = (size_t)align4(n_tiles);
+    const size_t img_words = ((size_t)kSortThreads * kpt + 16 * nt4) / 2;
+    const size_t scratch = std::max(img_words, (size_t)2 * (kMaxTiles + 1));
+    // scratch | s_cnt [waves][nt4] | tot, pos, B, full, cn | carry [nt4][4] | s_w
+    return 4 * ((size_t)align4((int)scratch) + (size_t)kSortWaves * nt4 + 5 * nt4 + 4 * nt4 + 32);
+}
+
+template <int TB, int KPT>
+__global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_cold_sort_a(ColdArgs c) {
+    constexpr int PIECE = kSortThreads * KPT;
+    const int n_tiles = c.n_tiles;
+    uint16_t *__restrict__ out = c.keys;
+    constexpr uint32_t MASK = (1u << TB) - 1u;
+    constexpr int SH = TB + 2;  // keys are scaled by 4
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    const int nt4 = align4(n_tiles);
+    const int img_words = (PIECE + 16 * nt4) / 2;
+    const int scratch = align4(max(img_words, 2 * (kMaxTiles + 1)));
+    uint16_t *img = reinterpret_cast<uint16_t *>(sm);   // tile segments, 16-byte aligned
+    uint32_t *s_cnt = sm + scratch;                      // [wave][tile]
+    uint32_t *s_tot = s_cnt + kSortWaves * nt4;          // [tile] keys of this piece
+    uint32_t *s_pos = s_tot + nt4;                       // [tile] next global position (8-aligned)
+    uint32_t *s_B = s_pos + nt4;                         // [tile] segment base in the image (u16)
+    uint32_t *s_full = s_B + nt4;                        // [tile] full groups of this piece
+    uint32_t *s_cn = s_full + nt4;                       // [tile] carried keys (0..7)
+    uint4 *s_carry = reinterpret_cast<uint4 *>(s_cn + nt4);  // [tile] 8 carried u16
+    uint32_t *s_w = reinterpret_cast<uint32_t *>(s_carry + nt4);
+    const int tid = threadIdx.x;
+    const int wv = tid >> 6, lane = tid & 63;
+    const int b = blockIdx.x / kColdGroups, grp = blockIdx.x % kColdGroups;
+    const int row = blockIdx.x;
+    constexpr int NW = kSplitThreads / 64;
+    const uint32_t capw = (uint32_t)(c.cap / NW);
+    const int sw = grp * kSortWaves + wv;
+    const uint32_t n_w = c.cold_cnt[(size_t)b * NW + sw];
+    const bool own = tid < n_tiles;  // thread tid owns tile tid
+    if (row == 0)
+        plan_items(c.tile_total, n_tiles, c.item_keys, c.items, c.item_count, c.max_items, s_w,
+                   sm, sm + kMaxTiles + 1);
+    {
+        const uint32_t tt = own ? c.tile_total[tid] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan(tt, s_w, &total);
+        if (own) {
+            s_pos[tid] = ex + c.boff[(size_t)row * n_tiles + tid];
+            s_cn[tid] = 0;
+        }
+    }
+    if (lane == 0) s_w[20 + wv] = (n_w + 64 * KPT - 1) / (64 * KPT);
+    __syncthreads();
+    uint32_t npieces = 0;
+#pragma unroll
+    for (int q = 0; q < kSortWaves; ++q) npieces = max(npieces, s_w[20 + q]);
+    const __amdgpu_buffer_rsrc_t rs =
+        make_rsrc(c.cold + (size_t)b * (size_t)c.stride + (size_t)sw * capw, n_w * 4u);
+    uint32_t *my_cnt = s_cnt + wv * nt4;
+    v4u nk[KPT / 4];
+    auto fetch = [&](uint32_t p) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < KPT / 4; ++j) {
+            const uint32_t e0 = p * (uint32_t)(64 * KPT) + (uint32_t)j * 256u + (uint32_t)lane * 4u;
+            nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
+        }
+    };
+    if (npieces) fetch(0);
+    uint32_t cn = 0;  // own tile: carried keys
+    for (uint32_t p = 0; p < npieces; ++p) {
+        for (int i = lane; i < nt4; i += 64) my_cnt[i] = 0;
+        uint32_t key[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT / 4; ++j) {
+            const uint32_t e0 = p * (uint32_t)(64 * KPT) + (uint32_t)j * 256u + (uint32_t)lane * 4u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n_w ? nk[j][q] : 0xFFFFFFFFu;
+        }
+        if (KPT <= 16 && p + 1 < npieces) fetch(p + 1);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int e = 0; e < KPT; ++e)
+            if (key[e] != 0xFFFFFFFFu)
+                __hip_atomic_fetch_add(my_cnt + (key[e] >> SH), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+        __syncthreads();
+        // own tile: wave counts -> wave offsets inside the run (serial over
+        // the 8 waves), run length, segment [carry | run] rounded up to 8
+        uint32_t n = 0;
+        if (own) {
+#pragma unroll
+            for (int w = 0; w < kSortWaves; ++w) {
+                const uint32_t v = s_cnt[w * nt4 + tid];
+                s_cnt[w * nt4 + tid] = n + cn;  // offset inside the segment
+                n += v;
+            }
+            n += cn;
+        }
+        uint32_t gtotal;
+        const uint32_t B = block_exclusive_scan((n + 7u) & ~7u, s_w, &gtotal);
+        if (own) {
+            s_B[tid] = B;
+            s_full[tid] = n >> 3;
+            if (cn) {  // the carried keys head the segment
+                const uint4 cv = s_carry[tid];
+                const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+                for (uint32_t i = 0; i < 7; ++i)
+                    if (i < cn) img[B + i] = (uint16_t)(cw[i >> 1] >> ((i & 1) * 16));
+            }
+        }
+        __syncthreads();
+        // scatter: each key takes the next slot of its wave's part of the run
+        // (the order inside a run is irrelevant: pass B only counts)
+#pragma unroll
+        for (int e = 0; e < KPT; ++e) {
+            uint32_t k = key[e];
+            asm volatile("" : "+v"(k));  // keeps the count pass's addresses dead
+            if (k != 0xFFFFFFFFu) {
+                const uint32_t t = k >> SH;
+                img[s_B[t] + __hip_atomic_fetch_add(my_cnt + t, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP)] =
+                    (uint16_t)((k >> 2) & MASK);
+            }
+        }
+        // wide pieces: the next keys are requested once this piece's are dead
+        if (KPT > 16 && p + 1 < npieces) fetch(p + 1);
+        __syncthreads();
+        // one thread per 8-key group: full groups leave as 16-byte stores,
+        // a segment's partial last group becomes the tile's new carry
+        const uint32_t G = gtotal >> 3;
+        for (uint32_t gi = (uint32_t)tid; gi < G; gi += kSortThreads) {
+            const uint32_t pos = gi * 8u;
+            int lo = 0, hi = n_tiles - 1;  // last tile whose segment starts at or before pos
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_B[mid] <= pos) lo = mid; else hi = mid - 1;
+            }
+            const uint32_t k = (pos - s_B[lo]) >> 3;
+            const uint4 v = *reinterpret_cast<const uint4 *>(img + pos);
+            if (k < s_full[lo]) {
+                if (!(c.ablate & 1))
+                    *reinterpret_cast<uint4 *>(out + s_pos[lo] + 8u * k) = v;
+            } else {
+                s_carry[lo] = v;
+            }
+        }
+        __syncthreads();
+        if (own) {
+            s_pos[tid] += 8u * (n >> 3);
+            cn = n & 7u;
+        }
+        // (the next piece's first barrier orders these before their readers)
+    }
+    // the last carry of the own tile, padded with 0xFFFF
+    if (own && cn) {
+        const uint4 cv = s_carry[tid];
+        uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i)
+            if (i >= cn) cw[i >> 1] |= 0xFFFFu << ((i & 1) * 16);
+        if (!(c.ablate & 1))
+            *reinterpret_cast<uint4 *>(out + s_pos[tid]) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
     }
 }
 
@@ -902,9 +1234,11 @@ __global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const uint32_t idx = i + (uint32_t)q;
-                if (idx >= it.y && idx < it.z)
-                    __hip_atomic_fetch_add(s_tile + ((w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu), 1u,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint32_t key = (w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu;
+                // 0xFFFF: pad of an aligned range (never a key: tile_bits <= 15)
+                if (idx >= it.y && idx < it.z && key != 0xFFFFu)
+                    __hip_atomic_fetch_add(s_tile + key, 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
     }
@@ -984,13 +1318,37 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
     hipLaunchKernelGGL(k_hot_reduce_scan, dim3(hot_blocks + c.n_tiles), dim3(256), 0, st, c,
                        hot_blocks);
     const size_t sm = cold_sort_smem(c.n_tiles);
+    // the wave-independent sort when its LDS (2 blocks per CU) fits
+    const size_t smw = cold_sort_w_smem(c.n_tiles);
+    const bool wave = c.wave_sort == 1 && smw <= 80 * 1024;
+    const size_t sma = cold_sort_a_smem(c.n_tiles, c.sort_kpt);
+    const bool aligned = c.pad8 != 0;
     hipError_t e = hipSuccess;
     switch (c.tile_bits) {
 #define LDE_COLD(TB)                                                                              \
     case TB:                                                                                      \
-        (void)hipFuncSetAttribute((const void *)k_cold_sort<TB>,                                  \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);           \
-        hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * kColdGroups), dim3(kSortThreads), sm, st, c); \
+        if (aligned && c.sort_kpt == 32) {                                                        \
+            (void)hipFuncSetAttribute((const void *)k_cold_sort_a<TB, 32>,                        \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);      \
+            hipLaunchKernelGGL((k_cold_sort_a<TB, 32>), dim3(c.rows * kColdGroups),               \
+                               dim3(kSortThreads), sma, st, c);                                   \
+        } else if (aligned) {                                                                     \
+            (void)hipFuncSetAttribute((const void *)k_cold_sort_a<TB, 16>,                        \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);      \
+            hipLaunchKernelGGL((k_cold_sort_a<TB, 16>), dim3(c.rows * kColdGroups),               \
+                               dim3(kSortThreads), sma, st, c);                                   \
+        } else if (wave) {                                                                        \
+            (void)hipFuncSetAttribute((const void *)k_cold_sort_w<TB>,                            \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smw);      \
+            hipLaunchKernelGGL(k_cold_sort_w<TB>, dim3(c.rows * kColdGroups), dim3(kSortThreads), \
+                               smw, st, c);                                                       \
+        } else {                                                                                  \
+            (void)hipFuncSetAttribute((const void *)k_cold_sort<TB>,                              \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);       \
+            hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * kColdGroups), dim3(kSortThreads),   \
+                               sm, st, c);                                                        \
+        }                                                                                         \
+        if (!c.ablate) /* diagnostics: the keys are not valid */                                 \
         hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, st,\
                               nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist, c.n_bins); \
         break;
