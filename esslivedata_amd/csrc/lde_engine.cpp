@@ -580,7 +580,11 @@ int paged_core(lde_handle *h, const lde::SegDesc *segs, int n_segs, long long ch
     // pass-B work items: ~2 per CU for a full batch; the (smaller) cold-key
     // stream of SPLIT gets ~1 per 2 CUs, since every item pays a flush of its
     // whole tile (measured: 64K -> 256K events per item, pass B -23 %)
-    const long long per_items = n_chunks_dev ? std::max(1, h->cus / 2) : 2LL * h->cus;
+    // (full batch: as many items as fit resident, as for the SIEVE cold keys)
+    const long long resident =
+        (long long)h->cus * std::max<long long>(1, (160LL * 1024) / (4LL << h->tile_bits));
+    const long long per_items = n_chunks_dev ? std::max(1, h->cus / 2)
+                                             : std::max<long long>(h->cus, resident - h->n_tiles);
     long long item_events = h->item_events_override > 0
                                 ? h->item_events_override
                                 : std::max<long long>(32768, (events + per_items - 1) / per_items);
@@ -787,9 +791,20 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                               (pad8 ? (size_t)a.grid * lde::kColdGroups * nt * 8 : 0) + 64))
             return rc;
         const double cold_est = std::min(1.0, std::max(0.05, 1.0 - h->hot_cov[replica])) * (double)total;
-        const long long item_keys = h->item_events_override > 0
-                                        ? h->item_events_override
-                                        : std::max<long long>(32768, (long long)(cold_est / std::max(1, h->cus / 2)));
+        // pass B items: as many as fit resident at once (LDS: one 2^tile_bits
+        // u32 tile per block), so no second round of blocks; a tile with n keys
+        // gets ceil(n / item_keys) <= n / item_keys + 1 items, hence the
+        // n_tiles subtracted (DREAM: 2 x 256 slots, 157 tiles -> ~96K keys per
+        // item, 3 items per tile; one item per tile measured 12 us slower)
+        const long long resident =
+            (long long)h->cus * std::max<long long>(1, (160LL * 1024) / (4LL << h->tile_bits));
+        const long long slots = resident - h->n_tiles;
+        const long long item_keys =
+            h->item_events_override > 0
+                ? h->item_events_override
+                : std::max<long long>(32768, (long long)(cold_est / (double)(slots >= h->cus / 2
+                                                                              ? slots
+                                                                              : std::max(1, h->cus / 2))));
         const long long max_items = ((long long)a.grid * a.cold_cap) / item_keys + h->n_tiles + 1;
         if (int rc = grow(h, &h->d_cold_items, h->cold_items_cap, (size_t)max_items)) return rc;
         lde::SieveArgs sa;
