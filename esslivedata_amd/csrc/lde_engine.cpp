@@ -164,6 +164,7 @@ struct lde_handle {
     bool sieve_pack = false;    // LDE_SIEVE_PACK
     int cold_sort_mode = 2;     // LDE_COLD_SORT: 0 block, 1 wave-independent, 2 16-byte groups
     int cold_sort_kpt = 32;     // LDE_COLD_SORT_KPT: keys per thread per piece of mode 2
+    bool key24 = true;          // LDE_KEY24: 24-bit cold keys when S * T < 2^24 - 1
     int cold_sort_ablate = 0;   // LDE_COLD_SORT_ABLATE (diagnostic, wrong results)
     uint32_t ttab_cap = 0;
     int ttab_shift = 0;
@@ -834,6 +835,9 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         sa.ablate = h->sieve_ablate;
         sa.early_gather = h->early_gather ? 1 : 0;
         sa.pack = h->sieve_pack ? 1 : 0;
+        // 24-bit cold keys need the 16-byte-group sort (the only reader)
+        const bool key24 = pad8 && h->key24 && h->nbins < 0xFFFFFFLL;
+        sa.key24 = key24 ? 1 : 0;
         {
             // k_sieve is timed by its own dispatch (start/stop events stamped
             // by hipExtLaunchKernelGGL): no marker packets around it
@@ -901,6 +905,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         c.wave_sort = h->cold_sort_mode == 1 ? 1 : 0;
         c.pad8 = pad8 ? 1 : 0;
         c.sort_kpt = h->cold_sort_kpt;
+        c.key24 = key24 ? 1 : 0;
         c.ablate = h->cold_sort_ablate;
         Timed tm(h, LDE_K_PAGED);
         HIPCALL(h, lde::launch_cold_pipeline(c, h->stream, h->bin_stop_ext));
@@ -1442,6 +1447,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
         h->cold_sort_mode = (int)env_ll("LDE_COLD_SORT", 2);
         h->cold_sort_kpt = env_ll("LDE_COLD_SORT_KPT", 32) == 16 ? 16 : 32;
+        h->key24 = env_ll("LDE_KEY24", 1) != 0;
         h->cold_sort_ablate = (int)env_ll("LDE_COLD_SORT_ABLATE", 0);
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);

@@ -202,6 +202,7 @@ struct SieveArgs {
     int tile_bits, n_tiles;  // cold keys are counted per tile of 2^tile_bits bins
     uint32_t *cold_tcnt;     // [grid][kColdGroups][n_tiles]
     int ablate;  // benchmark ablation variant (0 = the real pass)
+    int key24 = 0;  // cold keys leave as 24-bit keys (3 bytes; S * T < 2^24 - 1)
 };
 size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a
@@ -227,6 +228,7 @@ struct ColdArgs {
     int wave_sort = 0;  // 1: k_cold_sort_w (wave-independent) when its LDS fits
     int pad8 = 0;       // 1: k_cold_sort_a (16-byte groups; ranges padded to 8 keys)
     int sort_kpt = 32;  // k_cold_sort_a keys per thread per piece (16 or 32)
+    int key24 = 0;      // the sieve wrote 24-bit keys (k_cold_sort_a only)
     int ablate = 0;     // cold-sort diagnostics (wrong results): 1 no writes, 2 no loads
 };
 size_t cold_sort_smem(int n_tiles);

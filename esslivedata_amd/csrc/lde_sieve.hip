@@ -50,6 +50,7 @@ constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data fo
 constexpr int kEPT = kSplitEPT;               // 8 events per thread per chunk
 constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (half a chunk)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes,
@@ -76,6 +77,22 @@ __device__ __forceinline__ uint32_t vsel(unsigned long long m, uint32_t t, uint3
 // LDS word at a byte offset (the sieve keeps its LDS indices pre-scaled)
 __device__ __forceinline__ uint32_t &lds_at(uint32_t *sm, uint32_t byte_off) {
     return *reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(sm) + byte_off);
+}
+
+// Four cold keys (scaled by 4; pads all ones) as 24-bit keys in 12 bytes:
+// the key stream of the sieve when S * T < 2^24 - 1 (key24 mode), 25 % fewer
+// bytes written by the sieve and read by the sort.  The pad is 0xFFFFFF.
+__device__ __forceinline__ v3u pack_keys24(v4u k4) {
+    const uint32_t k0 = (k4[0] >> 2) & 0xFFFFFFu, k1 = (k4[1] >> 2) & 0xFFFFFFu;
+    const uint32_t k2 = (k4[2] >> 2) & 0xFFFFFFu, k3 = (k4[3] >> 2) & 0xFFFFFFu;
+    return v3u{k0 | (k1 << 24), (k1 >> 8) | (k2 << 16), (k2 >> 16) | (k3 << 8)};
+}
+// back to scaled keys, the pad to 0xFFFFFFFF
+__device__ __forceinline__ void unpack_keys24(v3u w, uint32_t *k) {
+    const uint32_t r[4] = {w[0] & 0xFFFFFFu, (w[0] >> 24) | ((w[1] & 0xFFFFu) << 8),
+                           (w[1] >> 16) | ((w[2] & 0xFFu) << 16), w[2] >> 8};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) k[q] = r[q] == 0xFFFFFFu ? 0xFFFFFFFFu : r[q] << 2;
 }
 
 }  // namespace
@@ -230,8 +247,19 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     __syncthreads();
 
     const __amdgpu_buffer_rsrc_t glut = make_rsrc(a.glut, (a.L + 1u) * 4u);
-    uint32_t *my_cold = a.cold + (size_t)blockIdx.x * (size_t)(a.cold_cap + kSplitThreads / 64);
-    const __amdgpu_buffer_rsrc_t cold = make_rsrc(my_cold, (uint32_t)a.cold_cap * 4u);  // 16-B aligned
+    // this block's cold region: cold_cap keys of 4 bytes, or of 3 (key24)
+    const uint32_t kbytes = a.key24 ? 3u : 4u;
+    unsigned char *my_cold = reinterpret_cast<unsigned char *>(a.cold) +
+                             (size_t)blockIdx.x * (size_t)(a.cold_cap + kSplitThreads / 64) * kbytes;
+    const __amdgpu_buffer_rsrc_t cold = make_rsrc(my_cold, (uint32_t)a.cold_cap * kbytes);
+    // one lane's four keys: offset = key index * 4 (kOOB: discarded)
+    auto store_keys = [&](v4u kv, uint32_t off) __attribute__((always_inline)) {
+        if (a.key24)
+            __builtin_amdgcn_raw_buffer_store_b96(pack_keys24(kv), cold,
+                                                  (int)(off == kOOB ? kOOB : (off >> 2) * 3u), 0, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b128(kv, cold, (int)off, 0, 0);
+    };
     const uint32_t cmask = C - 1u;
     const uint32_t pid_off = (uint32_t)a.pid_off;
     const uint32_t Lc = a.L;
@@ -418,11 +446,11 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             // the previous half's keys leave now (their LDS read is long done)
             if (ABL & 2048) {
             } else if (ABL & 64) {  // diagnostic: only the lanes that hold keys issue the store
-                if (pend_off != kOOB) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+                if (pend_off != kOOB) store_keys(pend_kv, pend_off);
             } else if (ABL & 128) {  // diagnostic: every other half stores (keys lost)
-                if (h == 0) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+                if (h == 0) store_keys(pend_kv, pend_off);
             } else if (!(ABL & 4)) {
-                __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+                store_keys(pend_kv, pend_off);
             }
             else sm[o_dum + lane] += pend_kv[0] ^ pend_off;
             __builtin_amdgcn_wave_barrier();
@@ -443,8 +471,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     };
     auto flush = [&]() __attribute__((always_inline)) {
         if (ABL & 2048) {
-            __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(pend_kv1, cold, (int)pend_off1, 0, 0);
+            store_keys(pend_kv, pend_off);
+            store_keys(pend_kv1, pend_off1);
             pend_off = pend_off1 = kOOB;
         }
     };
@@ -596,7 +624,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         }
     }
     // the last half's keys
-    if (!(ABL & 4)) __builtin_amdgcn_raw_buffer_store_b128(pend_kv, cold, (int)pend_off, 0, 0);
+    if (!(ABL & 4)) store_keys(pend_kv, pend_off);
     if (ABL & (512 | 1024 | 4096 | 16384)) sm[o_dum + lane] = junk;
     if (lane == 0) a.cold_cnt[(size_t)blockIdx.x * (kSplitThreads / 64) + (tid >> 6)] = wcur;
     __syncthreads();
@@ -1049,7 +1077,7 @@ size_t cold_sort_a_smem(int n_tiles, int kpt) {
     return 4 * ((size_t)align4((int)scratch) + (size_t)kSortWaves * nt4 + 5 * nt4 + 4 * nt4 + 32);
 }
 
-template <int TB, int KPT>
+template <int TB, int KPT, bool KEY24>
 __global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void k_cold_sort_a(ColdArgs c) {
     constexpr int PIECE = kSortThreads * KPT;
@@ -1096,15 +1124,23 @@ void k_cold_sort_a(ColdArgs c) {
     uint32_t npieces = 0;
 #pragma unroll
     for (int q = 0; q < kSortWaves; ++q) npieces = max(npieces, s_w[20 + q]);
+    constexpr uint32_t KB = KEY24 ? 3u : 4u;  // bytes per key in the sieve's regions
     const __amdgpu_buffer_rsrc_t rs =
-        make_rsrc(c.cold + (size_t)b * (size_t)c.stride + (size_t)sw * capw, n_w * 4u);
+        make_rsrc(reinterpret_cast<const unsigned char *>(c.cold) +
+                      ((size_t)b * (size_t)c.stride + (size_t)sw * capw) * KB,
+                  n_w * KB);
     uint32_t *my_cnt = s_cnt + wv * nt4;
     v4u nk[KPT / 4];
     auto fetch = [&](uint32_t p) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < KPT / 4; ++j) {
             const uint32_t e0 = p * (uint32_t)(64 * KPT) + (uint32_t)j * 256u + (uint32_t)lane * 4u;
-            nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
+            if (KEY24) {
+                const v3u w = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(e0 * 3u), 0, 0);
+                nk[j] = v4u{w[0], w[1], w[2], 0u};
+            } else {
+                nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
+            }
         }
     };
     if (npieces) fetch(0);
@@ -1115,8 +1151,13 @@ void k_cold_sort_a(ColdArgs c) {
 #pragma unroll
         for (int j = 0; j < KPT / 4; ++j) {
             const uint32_t e0 = p * (uint32_t)(64 * KPT) + (uint32_t)j * 256u + (uint32_t)lane * 4u;
+            uint32_t kk[4];
+            if (KEY24)
+                unpack_keys24(v3u{nk[j][0], nk[j][1], nk[j][2]}, kk);
+            else
+                for (int q = 0; q < 4; ++q) kk[q] = nk[j][q];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n_w ? nk[j][q] : 0xFFFFFFFFu;
+            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n_w ? kk[q] : 0xFFFFFFFFu;
         }
         if (KPT <= 16 && p + 1 < npieces) fetch(p + 1);
         __builtin_amdgcn_wave_barrier();
@@ -1327,16 +1368,25 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
     switch (c.tile_bits) {
 #define LDE_COLD(TB)                                                                              \
     case TB:                                                                                      \
-        if (aligned && c.sort_kpt == 32) {                                                        \
-            (void)hipFuncSetAttribute((const void *)k_cold_sort_a<TB, 32>,                        \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);      \
-            hipLaunchKernelGGL((k_cold_sort_a<TB, 32>), dim3(c.rows * kColdGroups),               \
-                               dim3(kSortThreads), sma, st, c);                                   \
-        } else if (aligned) {                                                                     \
-            (void)hipFuncSetAttribute((const void *)k_cold_sort_a<TB, 16>,                        \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);      \
-            hipLaunchKernelGGL((k_cold_sort_a<TB, 16>), dim3(c.rows * kColdGroups),               \
-                               dim3(kSortThreads), sma, st, c);                                   \
+        if (aligned) {                                                                            \
+            const void *f = c.sort_kpt == 32                                                      \
+                                ? (c.key24 ? (const void *)k_cold_sort_a<TB, 32, true>            \
+                                           : (const void *)k_cold_sort_a<TB, 32, false>)          \
+                                : (c.key24 ? (const void *)k_cold_sort_a<TB, 16, true>            \
+                                           : (const void *)k_cold_sort_a<TB, 16, false>);         \
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);   \
+            if (c.sort_kpt == 32 && c.key24)                                                      \
+                hipLaunchKernelGGL((k_cold_sort_a<TB, 32, true>), dim3(c.rows * kColdGroups),     \
+                                   dim3(kSortThreads), sma, st, c);                               \
+            else if (c.sort_kpt == 32)                                                            \
+                hipLaunchKernelGGL((k_cold_sort_a<TB, 32, false>), dim3(c.rows * kColdGroups),    \
+                                   dim3(kSortThreads), sma, st, c);                               \
+            else if (c.key24)                                                                     \
+                hipLaunchKernelGGL((k_cold_sort_a<TB, 16, true>), dim3(c.rows * kColdGroups),     \
+                                   dim3(kSortThreads), sma, st, c);                               \
+            else                                                                                  \
+                hipLaunchKernelGGL((k_cold_sort_a<TB, 16, false>), dim3(c.rows * kColdGroups),    \
+                                   dim3(kSortThreads), sma, st, c);                               \
         } else if (wave) {                                                                        \
             (void)hipFuncSetAttribute((const void *)k_cold_sort_w<TB>,                            \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smw);      \

@@ -47,6 +47,8 @@ VARIANTS = [
     {'LDE_COLD_SORT': '0'},
     {'LDE_COLD_SORT': '1'},
     {'LDE_COLD_SORT_KPT': '16'},
+    # cold keys as 32-bit words instead of packed 24-bit keys
+    {'LDE_KEY24': '0'},
 ]
 
 
