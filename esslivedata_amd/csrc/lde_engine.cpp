@@ -136,6 +136,7 @@ struct lde_handle {
     uint32_t *d_cold = nullptr;
     size_t cold_total_cap = 0;
     uint32_t *d_cold_cnt = nullptr;
+    uint32_t *d_hot_fmt = nullptr;  // SIEVE: per block, hot rows flushed as u16 (LDE_HOT16)
     lde::SegDesc *d_cold_segs = nullptr;
     long long *d_cold_chunks = nullptr;
     int *d_dummy = nullptr;  // 64 zero bytes
@@ -838,6 +839,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         // 24-bit cold keys need the 16-byte-group sort (the only reader)
         const bool key24 = pad8 && h->key24 && h->nbins < 0xFFFFFFLL;
         sa.key24 = key24 ? 1 : 0;
+        sa.hot_fmt = h->d_hot_fmt;
         {
             // k_sieve is timed by its own dispatch (start/stop events stamped
             // by hipExtLaunchKernelGGL): no marker packets around it
@@ -906,6 +908,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         c.pad8 = pad8 ? 1 : 0;
         c.sort_kpt = h->cold_sort_kpt;
         c.key24 = key24 ? 1 : 0;
+        c.hot_fmt = h->d_hot_fmt;
         c.ablate = h->cold_sort_ablate;
         Timed tm(h, LDE_K_PAGED);
         HIPCALL(h, lde::launch_cold_pipeline(c, h->stream, h->bin_stop_ext));
@@ -1172,6 +1175,7 @@ void release(lde_handle *h) {
     dev_free(h->d_hot_part);
     dev_free(h->d_cold);
     dev_free(h->d_cold_cnt);
+    dev_free(h->d_hot_fmt);
     dev_free(h->d_cold_segs);
     dev_free(h->d_cold_chunks);
     dev_free(h->d_dummy);
@@ -1432,6 +1436,9 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 CREATE_CHECK(dev_alloc(h, &h->d_screen_cnt, (size_t)h->S));
                 CREATE_CHECK(dev_alloc(h, &h->d_screen_row, (size_t)h->S));
                 CREATE_CHECK(dev_alloc(h, &h->d_cold_cnt, (size_t)h->split_grid * (lde::kSplitThreads / 64)));  // SIEVE: per wave
+                if (env_ll("LDE_HOT16", 1) != 0) {
+                    CREATE_CHECK(dev_alloc(h, &h->d_hot_fmt, (size_t)h->split_grid));
+                }
                 CREATE_CHECK(dev_alloc(h, &h->d_cold_segs, (size_t)h->split_grid));
                 CREATE_CHECK(dev_alloc(h, &h->d_cold_chunks, 1));
                 CREATE_CHECK(dev_alloc(h, &h->d_dummy, 16));

@@ -203,6 +203,7 @@ struct SieveArgs {
     uint32_t *cold_tcnt;     // [grid][kColdGroups][n_tiles]
     int ablate;  // benchmark ablation variant (0 = the real pass)
     int key24 = 0;  // cold keys leave as 24-bit keys (3 bytes; S * T < 2^24 - 1)
+    uint32_t *hot_fmt = nullptr;  // [grid] 1: the block's hot rows left as u16 (null: u32)
 };
 size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a
@@ -229,6 +230,7 @@ struct ColdArgs {
     int pad8 = 0;       // 1: k_cold_sort_a (16-byte groups; ranges padded to 8 keys)
     int sort_kpt = 32;  // k_cold_sort_a keys per thread per piece (16 or 32)
     int key24 = 0;      // the sieve wrote 24-bit keys (k_cold_sort_a only)
+    const uint32_t *hot_fmt = nullptr;  // per sieve block: hot rows as u16 (1) or u32 (0)
     int ablate = 0;     // cold-sort diagnostics (wrong results): 1 no writes, 2 no loads
 };
 size_t cold_sort_smem(int n_tiles);

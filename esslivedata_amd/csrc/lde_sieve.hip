@@ -235,7 +235,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.toa_words4; i += kSplitThreads * 4u)
         *reinterpret_cast<uint4 *>(sm + o_tt + i) = *reinterpret_cast<const uint4 *>(a.ttab + i);
     if (tid < 64) sm[o_dum + tid] = 0;
-    if (tid == 0) sm[o_cur] = 0;
+    if (tid == 0) sm[o_cur] = sm[o_cur + 1] = 0;  // cursor, hot-count overflow vote
     for (uint32_t i = (uint32_t)tid; i < kSieveStage * (kSplitThreads / 64); i += kSplitThreads)
         sm[o_stg + i] = 0xFFFFFFFFu;
     for (int i = tid; i < kColdGroups * align4(a.n_tiles); i += kSplitThreads) sm[o_tcnt + i] = 0;
@@ -628,9 +628,33 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     if (ABL & (512 | 1024 | 4096 | 16384)) sm[o_dum + lane] = junk;
     if (lane == 0) a.cold_cnt[(size_t)blockIdx.x * (kSplitThreads / 64) + (tid >> 6)] = wcur;
     __syncthreads();
+    // hot rows leave as u16 counts (half the bytes written here and read by
+    // k_hot_reduce_scan) unless a count of this block exceeds 0xFFFF
     uint32_t *dst = a.hot_part + (size_t)blockIdx.x * a.hot_words;
-    for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4)
-        *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(sm + i);
+    bool packed = false;
+    if (a.hot_fmt && (a.hot_words & 7) == 0) {
+        uint32_t big = 0;
+        for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(sm + i);
+            big |= (v.x | v.y | v.z | v.w) >> 16;
+        }
+        if (big) sm[o_cur + 1] = 1u;  // benign race: every writer stores 1
+        __syncthreads();
+        packed = sm[o_cur + 1] == 0u;
+    }
+    if (packed) {
+        uint4 *d16 = reinterpret_cast<uint4 *>(dst);  // 8 counts per 16 bytes
+        for (int i = tid * 8; i < a.hot_words; i += kSplitThreads * 8) {
+            const uint4 v0 = *reinterpret_cast<const uint4 *>(sm + i);
+            const uint4 v1 = *reinterpret_cast<const uint4 *>(sm + i + 4);
+            d16[i >> 3] = make_uint4(v0.x | (v0.y << 16), v0.z | (v0.w << 16), v1.x | (v1.y << 16),
+                                     v1.z | (v1.w << 16));
+        }
+    } else {
+        for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4)
+            *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(sm + i);
+    }
+    if (a.hot_fmt && tid == 0) a.hot_fmt[blockIdx.x] = packed ? 1u : 0u;
     for (int i = tid; i < kColdGroups * a.n_tiles; i += kSplitThreads) {
         const int g = i / a.n_tiles, t = i - g * a.n_tiles;
         a.cold_tcnt[((size_t)blockIdx.x * kColdGroups + g) * a.n_tiles + t] =
@@ -656,7 +680,11 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
         const int per = (c.rows + kSlices - 1) / kSlices;
         const int j0 = slice * per, j1 = min(c.rows, j0 + per);
         uint32_t sum = 0;
-        for (int j = j0; j < j1; ++j) sum += c.hot_part[(size_t)j * c.ht4 + i];
+        for (int j = j0; j < j1; ++j) {
+            const uint32_t *row = c.hot_part + (size_t)j * c.ht4;
+            sum += (c.hot_fmt && c.hot_fmt[j]) ? (uint32_t)reinterpret_cast<const uint16_t *>(row)[i]
+                                               : row[i];
+        }
         if (sum) {
             const int row = i / c.T;
             atomicAdd(c.hist + (size_t)c.row_screen[row] * c.T + (i - row * c.T), sum);

@@ -49,6 +49,8 @@ VARIANTS = [
     {'LDE_COLD_SORT_KPT': '16'},
     # cold keys as 32-bit words instead of packed 24-bit keys
     {'LDE_KEY24': '0'},
+    # hot rows flushed as u32 instead of u16
+    {'LDE_HOT16': '0'},
 ]
 
 
@@ -564,4 +566,36 @@ def test_sieve_hot_cells_with_millions_of_events(grid, monkeypatch):
     assert eng.info()['last_strategy'] == 'split'
     exp = 2 * ora.detector_histogram(np.arange(4096), 4096, ora.pixel_index(pid, dn), toa, edges)
     assert exp[6, 10] >= 2 * (k < 0.6).sum() > 3 * 65536
+    np.testing.assert_array_equal(res.current_hist, exp)
+
+
+def test_sieve_hot_rows_mixed_u16_and_u32_blocks(monkeypatch):
+    """Eight sieve blocks over one batch whose first half piles millions of
+    events into two hot cells: the first blocks' hot rows overflow 16 bits
+    (flushed as u32), the last blocks' do not (flushed as u16); the reduce
+    mixes both formats."""
+    monkeypatch.setenv('LDE_SPLIT_GRID', '8')
+    from esslivedata_amd import projection
+
+    dn = np.arange(1, 4097, dtype=np.int32)
+    view = projection.logical_lut(dn)
+    edges = np.linspace(0.0, 71.43, 101) * 1e6
+    rng = np.random.default_rng(11)
+    n = 4_000_000
+    pid = rng.integers(1, 4097, n).astype(np.int32)
+    toa = rng.uniform(0, 71e6, n).astype(np.int32)
+    mid = lambda b: int((edges[b] + edges[b + 1]) / 2)  # noqa: E731
+    head = np.arange(n) < n // 2
+    k = rng.random(n)
+    pid[head & (k < 0.7)] = 7
+    toa[head & (k < 0.5)] = mid(10)
+    toa[head & (k >= 0.5) & (k < 0.7)] = mid(11)
+    pid[~head & (k < 0.3)] = 7  # still hot, but < 2^16 per block
+    eng = _engine(view, edges, 'split')
+    eng.stage(pid, toa)
+    eng.accumulate(0)
+    res = eng.finalize(hists=True)
+    assert eng.info()['last_strategy'] == 'split'
+    exp = ora.detector_histogram(np.arange(4096), 4096, ora.pixel_index(pid, dn), toa, edges)
+    assert exp[6, 10] > 4 * 65536
     np.testing.assert_array_equal(res.current_hist, exp)
