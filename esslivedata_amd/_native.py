@@ -82,6 +82,8 @@ EXPORTED_SYMBOLS = (
     'lde_info',
     'lde_set_groups',
     'lde_group_spectra',
+    'lde_host_alloc',
+    'lde_host_free',
 )
 
 MAX_GROUP_SETS = 4
@@ -165,6 +167,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_synchronize': (ctypes.c_int, [H]),
         'lde_set_groups': (ctypes.c_int, [H, i32, i64, P, P]),
         'lde_group_spectra': (ctypes.c_int, [H, i32, i32, P]),
+        'lde_host_alloc': (ctypes.c_int, [i64, ctypes.POINTER(ctypes.c_void_p)]),
+        'lde_host_free': (ctypes.c_int, [P]),
         'lde_timing_enable': (ctypes.c_int, [H, i32]),
         'lde_timing_select': (ctypes.c_int, [H, ctypes.c_uint32]),
         'lde_kernel_stats': (

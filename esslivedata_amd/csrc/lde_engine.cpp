@@ -20,6 +20,8 @@
 #include <new>
 #include <atomic>
 #include <chrono>
+#include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -229,6 +231,8 @@ struct lde_handle {
     std::chrono::steady_clock::time_point t_acc0;
     double probe_us = 0.0, probe_min = 0.0;
     long long probe_n = 0;
+    double probe_fin_post_us = 0.0;  // finalize: from the stream wait's return to the return
+    long long probe_fin_n = 0;
 };
 
 namespace {
@@ -1205,6 +1209,67 @@ extern "C" {
 
 int lde_abi_version(void) { return LDE_ABI_VERSION; }
 
+// lde_host_alloc blocks: host base -> (bytes, device address)
+namespace {
+struct HostBlock {
+    size_t bytes;
+    unsigned char *dev;
+};
+std::mutex g_host_mu;
+std::map<uintptr_t, HostBlock> g_host_blocks;
+
+// device address of host pointer p inside an lde_host_alloc block with n
+// bytes from p on, else nullptr
+void *mapped_device_ptr(const void *p, size_t n) {
+    if (!p) return nullptr;
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    if (g_host_blocks.empty()) return nullptr;
+    auto it = g_host_blocks.upper_bound(a);
+    if (it == g_host_blocks.begin()) return nullptr;
+    --it;
+    if (a + n > it->first + it->second.bytes) return nullptr;
+    return it->second.dev + (a - it->first);
+}
+}  // namespace
+
+int lde_host_alloc(int64_t bytes, void **out) {
+    if (!out) return fail(nullptr, LDE_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (bytes <= 0) return fail(nullptr, LDE_EINVAL, "bytes must be positive");
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, (size_t)bytes, hipHostMallocCoherent | hipHostMallocPortable);
+    if (e != hipSuccess)
+        return fail(nullptr, LDE_ENOMEM, "hipHostMalloc(%lld bytes) failed: %s", (long long)bytes,
+                    hipGetErrorString(e));
+    void *d = nullptr;
+    e = hipHostGetDevicePointer(&d, p, 0);
+    if (e != hipSuccess) {
+        (void)hipHostFree(p);
+        return fail(nullptr, LDE_EHIP, "hipHostGetDevicePointer failed: %s", hipGetErrorString(e));
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        g_host_blocks[(uintptr_t)p] = HostBlock{(size_t)bytes, (unsigned char *)d};
+    }
+    *out = p;
+    return LDE_OK;
+}
+
+int lde_host_free(void *p) {
+    if (!p) return LDE_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        auto it = g_host_blocks.find((uintptr_t)p);
+        if (it == g_host_blocks.end())
+            return fail(nullptr, LDE_EINVAL, "pointer was not returned by lde_host_alloc");
+        g_host_blocks.erase(it);
+    }
+    hipError_t e = hipHostFree(p);
+    if (e != hipSuccess) return fail(nullptr, LDE_EHIP, "hipHostFree failed: %s", hipGetErrorString(e));
+    return LDE_OK;
+}
+
 const char *lde_last_error(const lde_handle *h) {
     return h ? h->err.c_str() : g_create_error.c_str();
 }
@@ -1474,6 +1539,9 @@ void lde_destroy(lde_handle *h) {
     if (h->probe && h->probe_n)
         fprintf(stderr, "lde probe: accumulate entry -> sieve launched %.2f us mean, %.2f us min (%lld)\n",
                 h->probe_us / h->probe_n, h->probe_min, h->probe_n);
+    if (h->probe && h->probe_fin_n)
+        fprintf(stderr, "lde probe: finalize after the stream wait (copies, totals) %.2f us mean (%lld)\n",
+                h->probe_fin_post_us / h->probe_fin_n, h->probe_fin_n);
     DeviceGuard guard(h->device);
     release(h);
 }
@@ -1739,6 +1807,12 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
     // outputs go straight into the host-mapped pack, or into d_pack and one copy
     unsigned char *pk = h->hd_pack ? h->hd_pack : h->d_pack;
     void *img_cur = pk, *img_cum = pk + (size_t)h->S * 8;
+    // images into lde_host_alloc memory are written by the kernel in place
+    const size_t img_bytes = (size_t)h->S * (f32 ? 4 : 8);
+    void *const map_cur = mapped_device_ptr(out->current_image, img_bytes);
+    void *const map_cum = mapped_device_ptr(out->cumulative_image, img_bytes);
+    if (map_cur) img_cur = map_cur;
+    if (map_cum) img_cum = map_cum;
     if (f32) {
         // images/hists come from the f32 accumulators (mirrors f32 += order)
         if (out->current_image)
@@ -1793,12 +1867,23 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
     }
     if (f32) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
     HIPCALL(h, wait_stream(h));
+    const auto t_waited = h->probe ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+    struct PostProbe {
+        lde_handle *h;
+        std::chrono::steady_clock::time_point t0;
+        ~PostProbe() {
+            if (!h->probe) return;
+            h->probe_fin_post_us += std::chrono::duration<double, std::micro>(
+                                        std::chrono::steady_clock::now() - t0).count();
+            ++h->probe_fin_n;
+        }
+    } post_probe{h, t_waited};
     const unsigned char *h_tail = h->h_pack + (size_t)h->S * 16;
     uint32_t ovf = 0;
     std::memcpy(&ovf, h_tail + 32, 4);
     if (ovf) return fail(h, LDE_ESTATE, "page pool overflow (internal error)");
-    if (out->current_image) std::memcpy(out->current_image, h->h_pack, (size_t)h->S * isz);
-    if (out->cumulative_image)
+    if (out->current_image && !map_cur) std::memcpy(out->current_image, h->h_pack, (size_t)h->S * isz);
+    if (out->cumulative_image && !map_cum)
         std::memcpy(out->cumulative_image, h->h_pack + (size_t)h->S * 8, (size_t)h->S * isz);
     unsigned long long tot[4] = {0, 0, 0, 0};
     const unsigned long long *parts = reinterpret_cast<const unsigned long long *>(h_tail + 48);

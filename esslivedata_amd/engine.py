@@ -39,6 +39,52 @@ def _current_raw_stream(device_index: int) -> int:
         return int(torch.cuda.current_stream(device_index).cuda_stream)
 
 
+class _HostBlock:
+    """One ``lde_host_alloc`` block (page-locked, device-mapped host memory),
+    exposed to numpy; freed when the last array viewing it is gone."""
+
+    def __init__(self, nbytes: int, dtype: np.dtype, count: int) -> None:
+        self._lib = _native.lib()
+        p = ctypes.c_void_p()
+        check(self._lib.lde_host_alloc(int(nbytes), ctypes.byref(p)))
+        self.ptr = int(p.value)
+        self.__array_interface__ = {
+            'shape': (count,), 'typestr': np.dtype(dtype).str, 'data': (self.ptr, False),
+            'version': 3,
+        }
+
+    def __del__(self) -> None:
+        try:
+            self._lib.lde_host_free(self.ptr)
+        except Exception:
+            pass
+
+
+class _OutputPool:
+    """Finalize images the kernel writes in place (no host copy after the
+    wait): arrays over ``lde_host_alloc`` blocks, handed out again only once
+    nothing but the pool references them (a caller that keeps a result keeps
+    its memory; a view of it counts as a reference).  At most ``cap`` blocks,
+    beyond that finalize falls back to ordinary arrays and a copy."""
+
+    def __init__(self, count: int, dtype: np.dtype, cap: int = 8) -> None:
+        self._count, self._dtype, self._cap = count, np.dtype(dtype), cap
+        self._arrays: list[np.ndarray] = []
+
+    def take(self) -> np.ndarray:
+        import sys
+
+        for a in self._arrays:
+            # references: the pool's list, this loop variable, getrefcount's argument
+            if sys.getrefcount(a) <= 3:
+                return a
+        if len(self._arrays) >= self._cap:
+            return np.empty(self._count, dtype=self._dtype)
+        a = np.asarray(_HostBlock(self._count * self._dtype.itemsize, self._dtype, self._count))
+        self._arrays.append(a)
+        return a
+
+
 def _as_i32(a) -> np.ndarray:
     a = np.asarray(a)
     if a.dtype != np.int32:
@@ -123,6 +169,7 @@ class BinningEngine:
         self._device = int(device)
         self._keepalive: list = []
         self._n_groups: dict[int, int] = {}
+        self._img_pool = _OutputPool(self._S, self._dtype)
         sp = ctypes.c_void_p()
         check(lib.lde_get_stream(h, ctypes.byref(sp)), h)
         self._stream_ptr = int(sp.value or 0)
@@ -283,8 +330,9 @@ class BinningEngine:
         out = _native.LdeOutputs()
         arrs = {}
         if images:
-            arrs['current_image'] = np.empty(self._S, dtype=self._dtype)
-            arrs['cumulative_image'] = np.empty(self._S, dtype=self._dtype)
+            # written in place by the finalize kernel (page-locked pool)
+            arrs['current_image'] = self._img_pool.take()
+            arrs['cumulative_image'] = self._img_pool.take()
         if hists:
             arrs['current_hist'] = np.empty(self._S * self._T, dtype=self._dtype)
             arrs['cumulative_hist'] = np.empty(self._S * self._T, dtype=self._dtype)

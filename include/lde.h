@@ -191,6 +191,16 @@ int lde_accumulate(lde_handle *h, int32_t replica);
  * accumulator raises ValueError). */
 int lde_finalize(lde_handle *h, lde_outputs *out);
 
+/* Page-locked, device-mapped host memory for finalize outputs.  An image
+ * pointer of lde_outputs that lies inside such a block is written by the
+ * finalize kernel directly (no staging buffer, no host copy after the wait):
+ * the caller's numpy arrays can be views of these blocks.  Blocks are not tied
+ * to a handle; free them with lde_host_free once nothing reads them.  (Host
+ * side of the reference's finalize -> da00 hand-off, job.py:435-467: the
+ * outputs are read once, serialized, and dropped.) */
+int lde_host_alloc(int64_t bytes, void **out);
+int lde_host_free(void *p);
+
 /* Read a full histogram (LDE_CURRENT or LDE_CUMULATIVE) without finalizing. */
 int lde_read_histogram(lde_handle *h, int32_t which, void *host_out);
 

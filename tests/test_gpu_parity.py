@@ -599,3 +599,34 @@ def test_sieve_hot_rows_mixed_u16_and_u32_blocks(monkeypatch):
     exp = ora.detector_histogram(np.arange(4096), 4096, ora.pixel_index(pid, dn), toa, edges)
     assert exp[6, 10] > 4 * 65536
     np.testing.assert_array_equal(res.current_hist, exp)
+
+
+def test_finalize_images_written_in_place_are_never_reused_while_held():
+    """Finalize images live in page-locked blocks the kernel writes directly;
+    a block is handed out again only once the caller dropped every array (and
+    view) of it, and past the pool cap finalize falls back to plain arrays."""
+    from esslivedata_amd import projection
+
+    dn = np.arange(1, 1025, dtype=np.int32)
+    view = projection.logical_lut(dn)
+    edges = np.linspace(0.0, 71.43, 11) * 1e6
+    rng = np.random.default_rng(3)
+    eng = _engine(view, edges, 'atomic')
+    held, copies = [], []
+    for k in range(12):
+        pid = rng.integers(1, 1025, 5000 + 100 * k).astype(np.int32)
+        toa = rng.uniform(0, 71e6, pid.size).astype(np.int32)
+        eng.stage(pid, toa)
+        eng.accumulate(0)
+        res = eng.finalize(images=True)
+        exp = ora.detector_histogram(np.arange(1024), 1024, ora.pixel_index(pid, dn), toa,
+                                     edges).sum(axis=1)
+        np.testing.assert_array_equal(res.current_image, exp)
+        if k % 2 == 0:
+            held.append(res.current_image[:])  # a view keeps its block
+            copies.append(res.current_image.copy())
+    for a, c in zip(held, copies):
+        np.testing.assert_array_equal(a, c)
+    ptrs = {a.__array_interface__['data'][0] for a in held}
+    assert len(ptrs) == len(held)
+    eng.close()
