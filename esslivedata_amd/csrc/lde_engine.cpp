@@ -139,6 +139,8 @@ struct lde_handle {
     size_t cold_total_cap = 0;
     uint32_t *d_cold_cnt = nullptr;
     uint32_t *d_hot_fmt = nullptr;  // SIEVE: per block, hot rows flushed as u16 (LDE_HOT16)
+    unsigned long long *d_trace = nullptr;  // LDE_SIEVE_TRACE: per-block sieve timeline
+    std::vector<double> trace_stats;        // per launch: start spread, end spread, mean span (us)
     lde::SegDesc *d_cold_segs = nullptr;
     long long *d_cold_chunks = nullptr;
     int *d_dummy = nullptr;  // 64 zero bytes
@@ -844,6 +846,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         const bool key24 = pad8 && h->key24 && h->nbins < 0xFFFFFFLL;
         sa.key24 = key24 ? 1 : 0;
         sa.hot_fmt = h->d_hot_fmt;
+        sa.trace = h->d_trace;
         {
             // k_sieve is timed by its own dispatch (start/stop events stamped
             // by hipExtLaunchKernelGGL): no marker packets around it
@@ -876,6 +879,28 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                                                  h->d_chunk_tab, h->stream));
             }
             HIPCALL(h, lde::launch_sieve(sa, a.grid, h->stream, ea, eb));
+            if (h->d_trace) {  // diagnostic only: a host sync per batch
+                std::vector<unsigned long long> tr((size_t)a.grid * 3);
+                HIPCALL(h, hipMemcpyAsync(tr.data(), h->d_trace, tr.size() * 8, hipMemcpyDeviceToHost,
+                                          h->stream));
+                HIPCALL(h, hipStreamSynchronize(h->stream));
+                unsigned long long s0 = ~0ull, s1 = 0, m0 = ~0ull, m1 = 0, e0 = ~0ull, e1 = 0;
+                for (int b = 0; b < a.grid; ++b) {
+                    s0 = std::min(s0, tr[3 * b]); s1 = std::max(s1, tr[3 * b]);
+                    m0 = std::min(m0, tr[3 * b + 1]); m1 = std::max(m1, tr[3 * b + 1]);
+                    e0 = std::min(e0, tr[3 * b + 2]); e1 = std::max(e1, tr[3 * b + 2]);
+                }
+                const double us = 1e6 / 100e6;  // s_memrealtime: 100 MHz
+                h->trace_stats.push_back((s1 - s0) * us);
+                h->trace_stats.push_back((m1 - m0) * us);
+                h->trace_stats.push_back((e1 - e0) * us);
+                h->trace_stats.push_back((e1 - s0) * us);
+                if (env_ll("LDE_SIEVE_TRACE", 0) > 1) {  // per block: stream end after the first start
+                    fprintf(stderr, "lde sieve trace blocks:");
+                    for (int b = 0; b < a.grid; ++b) fprintf(stderr, " %.1f", (tr[3 * b + 1] - s0) * us);
+                    fprintf(stderr, "\n");
+                }
+            }
             if (h->probe) {
                 const double us = std::chrono::duration<double, std::micro>(
                                       std::chrono::steady_clock::now() - h->t_acc0).count();
@@ -1180,6 +1205,17 @@ void release(lde_handle *h) {
     dev_free(h->d_cold);
     dev_free(h->d_cold_cnt);
     dev_free(h->d_hot_fmt);
+    if (h->d_trace && !h->trace_stats.empty()) {
+        const size_t n = h->trace_stats.size() / 4;
+        double a[4] = {0, 0, 0, 0};
+        for (size_t i = 0; i < n; ++i)
+            for (int q = 0; q < 4; ++q) a[q] += h->trace_stats[4 * i + q];
+        fprintf(stderr,
+                "lde sieve trace (%zu launches, us): block start spread %.2f, stream-end spread %.2f, "
+                "end spread %.2f, first start -> last end %.2f\n",
+                n, a[0] / n, a[1] / n, a[2] / n, a[3] / n);
+    }
+    dev_free(h->d_trace);
     dev_free(h->d_cold_segs);
     dev_free(h->d_cold_chunks);
     dev_free(h->d_dummy);
@@ -1501,6 +1537,9 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 CREATE_CHECK(dev_alloc(h, &h->d_screen_cnt, (size_t)h->S));
                 CREATE_CHECK(dev_alloc(h, &h->d_screen_row, (size_t)h->S));
                 CREATE_CHECK(dev_alloc(h, &h->d_cold_cnt, (size_t)h->split_grid * (lde::kSplitThreads / 64)));  // SIEVE: per wave
+                if (env_ll("LDE_SIEVE_TRACE", 0) != 0) {
+                    CREATE_CHECK(dev_alloc(h, &h->d_trace, (size_t)h->split_grid * 3));
+                }
                 if (env_ll("LDE_HOT16", 1) != 0) {
                     CREATE_CHECK(dev_alloc(h, &h->d_hot_fmt, (size_t)h->split_grid));
                 }

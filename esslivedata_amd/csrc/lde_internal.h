@@ -204,6 +204,7 @@ struct SieveArgs {
     int ablate;  // benchmark ablation variant (0 = the real pass)
     int key24 = 0;  // cold keys leave as 24-bit keys (3 bytes; S * T < 2^24 - 1)
     uint32_t *hot_fmt = nullptr;  // [grid] 1: the block's hot rows left as u16 (null: u32)
+    unsigned long long *trace = nullptr;  // diagnostic [grid][3]: start, stream end, end (realtime)
 };
 size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a

@@ -215,6 +215,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const uint32_t C = 1u << a.cbits;
+    const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     // LDS carve (words): hot rows | pixel table | TOA buckets | 64 dummies |
     // cursor (4) | cold staging (256 per wave) | cold keys per tile
     const uint32_t o_pc = (uint32_t)a.hot_words;
@@ -628,6 +629,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     if (ABL & (512 | 1024 | 4096 | 16384)) sm[o_dum + lane] = junk;
     if (lane == 0) a.cold_cnt[(size_t)blockIdx.x * (kSplitThreads / 64) + (tid >> 6)] = wcur;
     __syncthreads();
+    const unsigned long long t_stream = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     // hot rows leave as u16 counts (half the bytes written here and read by
     // k_hot_reduce_scan) unless a count of this block exceeds 0xFFFF
     uint32_t *dst = a.hot_part + (size_t)blockIdx.x * a.hot_words;
@@ -655,6 +657,12 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(sm + i);
     }
     if (a.hot_fmt && tid == 0) a.hot_fmt[blockIdx.x] = packed ? 1u : 0u;
+    if (a.trace) {  // diagnostic: per-block timeline (LDE_SIEVE_TRACE)
+        __syncthreads();
+        if (tid < 3)
+            a.trace[(size_t)blockIdx.x * 3 + tid] =
+                tid == 0 ? t_start : tid == 1 ? t_stream : __builtin_amdgcn_s_memrealtime();
+    }
     for (int i = tid; i < kColdGroups * a.n_tiles; i += kSplitThreads) {
         const int g = i / a.n_tiles, t = i - g * a.n_tiles;
         a.cold_tcnt[((size_t)blockIdx.x * kColdGroups + g) * a.n_tiles + t] =
