@@ -1938,17 +1938,19 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
 int lde_finalize_partials(lde_handle *h, void *d_out) {
     if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
     if (!d_out) return fail(h, LDE_EINVAL, "output buffer is NULL");
-    if (h->out_dtype == LDE_F32)
-        return fail(h, LDE_EINVAL, "partial outputs need an integer-exact (float64) view");
     DeviceGuard guard(h->device);
     unsigned long long *o = (unsigned long long *)d_out;
     {
+        // float32 views keep exact integer window (win64) and cumulative
+        // counts beside their f32 accumulators: the partials come from those
         Timed tm(h, LDE_K_FINALIZE);
         HIPCALL(h, lde::launch_finalize(2, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr,
                                         h->d_cum, nullptr, h->S, h->T, h->range_lo, h->range_hi,
                                         o, o + h->S, h->d_tot4, o + 2 * h->S, nullptr, nullptr,
                                         h->stream));
     }
+    if (h->out_dtype == LDE_F32)  // the window's f32 accumulator restarts too
+        HIPCALL(h, hipMemsetAsync(h->d_winf, 0, (size_t)h->nbins * 4, h->stream));
     h->window_has_data = false;
     h->win64_dirty = false;
     h->win_events = 0;

@@ -140,14 +140,17 @@ class OutputReducer(_Reducer):
 
     def finalize(self):
         """Collective.  On the root: (current image, cumulative image, totals)
-        as float64 numpy arrays and a list of 4 ints; elsewhere None."""
+        as numpy arrays of the engine's output dtype (float64, or float32 for
+        BIFROST-like views: the exact merged counts rounded once) and a list
+        of 4 ints; elsewhere None."""
         self._before_write()
         self.engine.finalize_partials(self.buf.data_ptr())
         if not self._reduce():
             return None
         h = self.buf.cpu().numpy()
         S = self.S
-        return h[:S].astype('float64'), h[S : 2 * S].astype('float64'), [int(x) for x in h[2 * S :]]
+        dt = self.engine.dtype
+        return h[:S].astype(dt), h[S : 2 * S].astype(dt), [int(x) for x in h[2 * S :]]
 
 
 class WindowReducer(_Reducer):

@@ -254,8 +254,12 @@ int lde_export_window(lde_handle *h, void *d_dst);
  * image | [4] totals (lde_outputs.totals order), asynchronously on the
  * handle's stream.  Summed over ranks (RCCL reduce) they equal the outputs of
  * one handle that binned every rank's events.  An empty window is allowed
- * (zeros for the current outputs).  float64 views only (LDE_EINVAL for f32,
- * whose per-push rounding is order dependent). */
+ * (zeros for the current outputs).  float32 views (BIFROST) export their exact
+ * integer counts too (kept beside the f32 accumulators): rounded once to f32
+ * by the caller, the merged images equal one handle's f32 images whenever
+ * every per-push f32 bin value is an exact integer (< 2^24 counts per bin);
+ * beyond that they are the exact counts rounded once, where the reference's
+ * per-push f32 sums drift by at most one f32 rounding per push. */
 int lde_finalize_partials(lde_handle *h, void *d_out);
 int lde_import_window(lde_handle *h, const void *d_src);
 /* Exact window merge in any window state (also after the uint32 window has

@@ -18,6 +18,8 @@ from oracle import scipp_semantics as ora
 class _HostEngine:
     """Oracle-backed stand-in with BinningEngine's export/import interface."""
 
+    dtype = np.dtype('float64')  # output dtype (float32 for BIFROST-like views)
+
     def __init__(self, n_screen, edges):
         self.n_screen, self.n_toa_bins = n_screen, len(edges) - 1
         self.edges = edges

@@ -99,6 +99,60 @@ def _outputs_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _bifrost_worker(rank, world, port, q):
+    """float32 view (BIFROST unified detector, 45 bank streams): every rank
+    bins its share of the bank messages; the merged f32 images equal one
+    engine that binned every message."""
+    import torch
+    import torch.distributed as dist
+
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.distributed import OutputReducer
+    from esslivedata_amd.engine import BinningEngine
+
+    _init(rank, world, port)
+    try:
+        inst = synthetic.bifrost_unified()
+        view = projection.logical_lut(inst.detector_number, transform=synthetic.bifrost_transform)
+        edges = inst.edges.edges_ns()
+
+        def make():
+            return BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                                 n_screen=view.n_screen, device=0, out_dtype='float32',
+                                 toa_range=(5, 95))
+
+        eng = make()
+        full = make() if rank == 0 else None
+        red = OutputReducer(eng, torch.device('cuda', 0))
+        ok = True
+        for window in range(3):
+            for bank in range(45):  # bifrost/streams.py:22-43: one message per bank
+                pid, toa = synthetic.fake_detector_events(1000, 1 + 300 * bank, 300 * (bank + 1),
+                                                          seed=1000 * window + bank)
+                if bank % world == rank:
+                    eng.stage(pid, toa)
+                if rank == 0:
+                    full.stage(pid, toa)
+            eng.accumulate(0)
+            if rank == 0:
+                full.accumulate(0)
+            res = red.finalize()
+            if rank == 0:
+                ref = full.finalize(images=True)
+                cur, cum, tot = res
+                ok &= cur.dtype == np.float32 and bool(np.array_equal(cur, ref.current_image))
+                ok &= bool(np.array_equal(cum, ref.cumulative_image))
+                ok &= tot == [ref.current_total, ref.current_in_range, ref.cumulative_total,
+                              ref.cumulative_in_range] and tot[0] > 0
+            else:
+                ok &= res is None
+        q.put((rank, bool(ok)))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
 FIREHOSE = 100_000_000
 FIRE_MSGS = 44  # 4.4e9 events per rank: the u32 window folds into u64
 
@@ -183,3 +237,7 @@ def test_output_reducer_two_ranks_real_engines():
 
 def test_window_reducer_after_u64_fold_two_ranks():
     _run(_window_worker)
+
+
+def test_output_reducer_float32_view_two_ranks():
+    _run(_bifrost_worker)

@@ -249,6 +249,46 @@ def test_bifrost_float32_accumulation():
             np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
 
 
+def test_bifrost_float32_partials_match_finalize():
+    """float32 views export their exact integer counts as partial outputs;
+    rounded once to f32 they equal the handle's own f32 finalize images (every
+    per-push f32 bin value is an exact integer here), over several windows."""
+    import torch
+
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.bifrost_unified()
+    view = projection.logical_lut(inst.detector_number, transform=synthetic.bifrost_transform)
+    edges = inst.edges.edges_ns()
+    a = _engine(view, edges, 'auto', out_dtype='float32', toa_range=(10, 90))
+    b = _engine(view, edges, 'auto', out_dtype='float32', toa_range=(10, 90))
+    S = view.n_screen
+    buf = torch.zeros(2 * S + 4, dtype=torch.int64, device='cuda')
+    for batch in range(12):
+        pid, toa = synthetic.fake_detector_events(45_000, 1, 13500, seed=100 + batch)
+        for e in (a, b):
+            e.stage(pid, toa)
+            e.accumulate(0)
+        if batch % 4 == 3:
+            ref = a.finalize(images=True)
+            b.finalize_partials(buf.data_ptr())
+            b.synchronize()
+            h = buf.cpu().numpy()
+            assert ref.current_image.dtype == np.float32
+            np.testing.assert_array_equal(h[:S].astype(np.float32), ref.current_image)
+            np.testing.assert_array_equal(h[S:2 * S].astype(np.float32), ref.cumulative_image)
+            assert [int(x) for x in h[2 * S:]] == [ref.current_total, ref.current_in_range,
+                                                   ref.cumulative_total, ref.cumulative_in_range]
+    # the f32 window restarted after the partials: b's next finalize = a's
+    pid, toa = synthetic.fake_detector_events(45_000, 1, 13500, seed=999)
+    for e in (a, b):
+        e.stage(pid, toa)
+        e.accumulate(0)
+    ra, rb = a.finalize(hists=True), b.finalize(hists=True)
+    np.testing.assert_array_equal(ra.current_hist, rb.current_hist)
+    np.testing.assert_array_equal(ra.cumulative_hist, rb.cumulative_hist)
+
+
 def test_empty_and_all_dropped_batches():
     from esslivedata_amd import projection
 
