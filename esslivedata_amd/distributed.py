@@ -129,6 +129,22 @@ class _Reducer:
 
 
 class OutputReducer(_Reducer):
+    _hbuf = None  # page-locked host copy of the reduced outputs (root)
+
+    def _to_host(self):
+        """The reduced buffer on the host: one async copy into a reused
+        page-locked tensor on the collective's stream, then a stream sync
+        (``Tensor.cpu()`` would allocate pageable memory every finalize)."""
+        import torch
+
+        if not self.buf.is_cuda:
+            return self.buf.numpy()
+        if self._hbuf is None:
+            self._hbuf = torch.empty(self.buf.shape, dtype=self.buf.dtype, pin_memory=True)
+        self._hbuf.copy_(self.buf, non_blocking=True)
+        torch.cuda.current_stream(self.buf.device).synchronize()
+        return self._hbuf.numpy()
+
     """Sums every rank's finalize outputs onto the root (see module doc)."""
 
     def __init__(self, engine, device, *, dst: int = 0, group=None) -> None:
@@ -147,7 +163,7 @@ class OutputReducer(_Reducer):
         self.engine.finalize_partials(self.buf.data_ptr())
         if not self._reduce():
             return None
-        h = self.buf.cpu().numpy()
+        h = self._to_host()
         S = self.S
         dt = self.engine.dtype
         return h[:S].astype(dt), h[S : 2 * S].astype(dt), [int(x) for x in h[2 * S :]]
