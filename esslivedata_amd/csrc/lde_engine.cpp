@@ -170,6 +170,8 @@ struct lde_handle {
     int cold_sort_mode = 2;     // LDE_COLD_SORT: 0 block, 1 wave-independent, 2 16-byte groups
     int cold_sort_kpt = 32;     // LDE_COLD_SORT_KPT: keys per thread per piece of mode 2
     bool key24 = true;          // LDE_KEY24: 24-bit cold keys when S * T < 2^24 - 1
+    int tail_release = 1;       // LDE_TAIL_RELEASE: per-block L2 writeback at the end of
+                                // 1 the sieve, 2 the cold sort, 4 pass B
     int cold_sort_ablate = 0;   // LDE_COLD_SORT_ABLATE (diagnostic, wrong results)
     uint32_t ttab_cap = 0;
     int ttab_shift = 0;
@@ -846,6 +848,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         const bool key24 = pad8 && h->key24 && h->nbins < 0xFFFFFFLL;
         sa.key24 = key24 ? 1 : 0;
         sa.hot_fmt = h->d_hot_fmt;
+        sa.tail_release = h->tail_release;
         sa.trace = h->d_trace;
         {
             // k_sieve is timed by its own dispatch (start/stop events stamped
@@ -938,6 +941,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         c.sort_kpt = h->cold_sort_kpt;
         c.key24 = key24 ? 1 : 0;
         c.hot_fmt = h->d_hot_fmt;
+        c.tail_release = h->tail_release;
         c.ablate = h->cold_sort_ablate;
         Timed tm(h, LDE_K_PAGED);
         HIPCALL(h, lde::launch_cold_pipeline(c, h->stream, h->bin_stop_ext));
@@ -1559,6 +1563,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->cold_sort_mode = (int)env_ll("LDE_COLD_SORT", 2);
         h->cold_sort_kpt = env_ll("LDE_COLD_SORT_KPT", 32) == 16 ? 16 : 32;
         h->key24 = env_ll("LDE_KEY24", 1) != 0;
+        h->tail_release = (int)env_ll("LDE_TAIL_RELEASE", 1);
         h->cold_sort_ablate = (int)env_ll("LDE_COLD_SORT_ABLATE", 0);
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);

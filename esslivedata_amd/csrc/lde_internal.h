@@ -205,6 +205,7 @@ struct SieveArgs {
     int key24 = 0;  // cold keys leave as 24-bit keys (3 bytes; S * T < 2^24 - 1)
     uint32_t *hot_fmt = nullptr;  // [grid] 1: the block's hot rows left as u16 (null: u32)
     unsigned long long *trace = nullptr;  // diagnostic [grid][3]: start, stream end, end (realtime)
+    int tail_release = 0;  // each block ends with an agent-scope release (L2 writeback of its stores)
 };
 size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a
@@ -232,6 +233,7 @@ struct ColdArgs {
     int sort_kpt = 32;  // k_cold_sort_a keys per thread per piece (16 or 32)
     int key24 = 0;      // the sieve wrote 24-bit keys (k_cold_sort_a only)
     const uint32_t *hot_fmt = nullptr;  // per sieve block: hot rows as u16 (1) or u32 (0)
+    int tail_release = 0;  // bit 1: sort blocks, bit 2: pass-B blocks end with an agent release
     int ablate = 0;     // cold-sort diagnostics (wrong results): 1 no writes, 2 no loads
 };
 size_t cold_sort_smem(int n_tiles);

@@ -668,6 +668,12 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         a.cold_tcnt[((size_t)blockIdx.x * kColdGroups + g) * a.n_tiles + t] =
             sm[o_tcnt + g * align4(a.n_tiles) + t];
     }
+    if (a.tail_release & 1) {
+        // write this XCD's dirty lines back while other blocks still stream,
+        // instead of all at the end-of-kernel release (LDE_SIEVE_TAIL_RELEASE)
+        __syncthreads();
+        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1281,13 +1287,18 @@ void k_cold_sort_a(ColdArgs c) {
         if (!(c.ablate & 1))
             *reinterpret_cast<uint4 *>(out + s_pos[tid]) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
     }
+    if (c.tail_release & 2) {  // this block's keys written back before the kernel ends
+        __syncthreads();
+        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
 }
 
 // pass B: one item = a contiguous key range of one tile
 template <int TB>
 __global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
     const uint16_t *__restrict__ keys, const uint4 *__restrict__ items,
-    const uint32_t *__restrict__ item_count, uint32_t *__restrict__ hist, long long n_bins) {
+    const uint32_t *__restrict__ item_count, uint32_t *__restrict__ hist, long long n_bins,
+    int tail_release) {
     constexpr int NB = 1 << TB;
     __shared__ __attribute__((aligned(16))) uint32_t s_tile[NB];
     if (blockIdx.x >= *item_count) return;
@@ -1343,6 +1354,10 @@ __global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
             const uint32_t v = s_tile[i];
             if (v != 0u && base + i < n_bins) atomicAdd(hist + base + i, v);
         }
+    }
+    if (tail_release) {  // this block's window lines written back before the kernel ends
+        __syncthreads();
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
 }
 
@@ -1436,7 +1451,8 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
         }                                                                                         \
         if (!c.ablate) /* diagnostics: the keys are not valid */                                 \
         hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, st,\
-                              nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist, c.n_bins); \
+                              nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist, c.n_bins,  \
+                              (c.tail_release & 4) ? 1 : 0);                                      \
         break;
         LDE_COLD(13)
         LDE_COLD(14)

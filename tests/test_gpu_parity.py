@@ -51,6 +51,9 @@ VARIANTS = [
     {'LDE_KEY24': '0'},
     # hot rows flushed as u32 instead of u16
     {'LDE_HOT16': '0'},
+    # per-block release fences: none / also at the end of the sort and pass B
+    {'LDE_TAIL_RELEASE': '0'},
+    {'LDE_TAIL_RELEASE': '7'},
 ]
 
 
