@@ -171,7 +171,7 @@ struct lde_handle {
     int cold_sort_kpt = 32;     // LDE_COLD_SORT_KPT: keys per thread per piece of mode 2
     bool key24 = true;          // LDE_KEY24: 24-bit cold keys when S * T < 2^24 - 1
     int tail_release = 1;       // LDE_TAIL_RELEASE: per-block L2 writeback at the end of
-                                // 1 the sieve, 2 the cold sort, 4 pass B
+                                // 1 the sieve, 2 the cold sort, 4 pass B, 8 PAGED pass A
     int cold_sort_ablate = 0;   // LDE_COLD_SORT_ABLATE (diagnostic, wrong results)
     uint32_t ttab_cap = 0;
     int ttab_shift = 0;
@@ -647,6 +647,7 @@ int paged_core(lde_handle *h, const lde::SegDesc *segs, int n_segs, long long ch
     a.cap = cap;
     a.overflow = h->d_overflow;
     a.grid = grid;
+    a.tail_release = (h->tail_release & 8) ? 1 : 0;
     {
         Timed tm(h, LDE_K_PAGED);
         if (n_chunks_dev) HIPCALL(h, lde::launch_paged_keys(a, n_chunks_dev, h->stream));

@@ -111,6 +111,7 @@ struct PagedArgs {
     int cap;  // pages per block pool
     uint32_t *overflow;
     int grid;
+    int tail_release = 0;  // pass-A blocks end with an agent-scope release
 };
 
 size_t paged_smem(int n_tiles, int subc, const ToaParams &tp);

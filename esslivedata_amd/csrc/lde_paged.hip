@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_part
     const long long *__restrict__ n_chunks_dev, const LT *__restrict__ lut,
     int pid_off, unsigned L, const unsigned char *__restrict__ g_tab, ToaParams tp, int n_tiles,
     uint16_t *__restrict__ pages, uint32_t *__restrict__ page_tile, uint32_t *__restrict__ page_cnt,
-    uint32_t *__restrict__ pool_used, int cap, uint32_t *__restrict__ overflow) {
+    uint32_t *__restrict__ pool_used, int cap, uint32_t *__restrict__ overflow, int tail_release) {
     constexpr int EPT = kPartEventsPerThread;
     constexpr uint32_t MASK = (1u << TILE_BITS) - 1u;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -334,7 +334,12 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_paged_part
         page_cnt[cur] = fill;
     }
     __syncthreads();
-    if (threadIdx.x == 0) pool_used[blockIdx.x] = min(s_pool[0], (uint32_t)cap);
+    if (threadIdx.x == 0) {
+        pool_used[blockIdx.x] = min(s_pool[0], (uint32_t)cap);
+        // this XCD's dirty page lines written back while other blocks still
+        // run, not all in the end-of-kernel release (LDE_TAIL_RELEASE & 8)
+        if (tail_release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
 }
 
 // per (block, tile): number of non-empty pages and events
@@ -555,7 +560,7 @@ static hipError_t launch_paged_t(const PagedArgs &a, const LT *lut, hipStream_t 
     hipLaunchKernelGGL((k_paged_partition<TB, LT, FAST, SUBC, KEYS>), dim3(a.grid),
                        dim3(kPartThreads), sm, st, a.segs, a.n_segs, a.n_chunks, n_chunks_dev, lut,
                        a.pid_off, a.L, a.tab, a.tp, a.n_tiles, a.pages, a.page_tile, a.page_cnt,
-                       a.pool_used, a.cap, a.overflow);
+                       a.pool_used, a.cap, a.overflow, a.tail_release);
     return hipGetLastError();
 }
 
