@@ -694,10 +694,28 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
         const int per = (c.rows + kSlices - 1) / kSlices;
         const int j0 = slice * per, j1 = min(c.rows, j0 + per);
         uint32_t sum = 0;
-        for (int j = j0; j < j1; ++j) {
-            const uint32_t *row = c.hot_part + (size_t)j * c.ht4;
-            sum += (c.hot_fmt && c.hot_fmt[j]) ? (uint32_t)reinterpret_cast<const uint16_t *>(row)[i]
-                                               : row[i];
+        bool all16 = c.hot_fmt != nullptr;  // block-uniform: every row of the slice packed
+        if (all16)
+            for (int j = j0; j < j1; ++j) all16 &= c.hot_fmt[j] != 0u;
+        if (all16) {
+            // the common case: independent u16 loads, eight rows in flight
+            const uint16_t *col = reinterpret_cast<const uint16_t *>(c.hot_part) + i;
+            const size_t rs = (size_t)c.ht4 * 2;  // row stride in u16
+            int j = j0;
+            for (; j + 8 <= j1; j += 8) {
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = col[(size_t)(j + u) * rs];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) sum += v[u];
+            }
+            for (; j < j1; ++j) sum += col[(size_t)j * rs];
+        } else {
+            for (int j = j0; j < j1; ++j) {
+                const uint32_t *row = c.hot_part + (size_t)j * c.ht4;
+                sum += (c.hot_fmt && c.hot_fmt[j]) ? (uint32_t)reinterpret_cast<const uint16_t *>(row)[i]
+                                                   : row[i];
+            }
         }
         if (sum) {
             const int row = i / c.T;

@@ -170,6 +170,8 @@ class BinningEngine:
         self._keepalive: list = []
         self._n_groups: dict[int, int] = {}
         self._img_pool = _OutputPool(self._S, self._dtype)
+        self._out = _native.LdeOutputs()  # reused by finalize (every field set per call)
+        self._out_ref = ctypes.byref(self._out)
         sp = ctypes.c_void_p()
         check(lib.lde_get_stream(h, ctypes.byref(sp)), h)
         self._stream_ptr = int(sp.value or 0)
@@ -323,33 +325,39 @@ class BinningEngine:
         self._keepalive.append(messages)
 
     def accumulate(self, replica: int = 0) -> None:
-        self._call(self._lib.lde_accumulate, int(replica))
+        rc = self._lib.lde_accumulate(self._h, int(replica))
+        if rc:
+            check(rc, self._h)
         self._keepalive.clear()
 
     def finalize(self, *, images: bool = True, hists: bool = False) -> FinalizeResult:
-        out = _native.LdeOutputs()
-        arrs = {}
+        out = self._out
+        ci = mi = ch = mh = None
         if images:
             # written in place by the finalize kernel (page-locked pool)
-            arrs['current_image'] = self._img_pool.take()
-            arrs['cumulative_image'] = self._img_pool.take()
+            ci = self._img_pool.take()
+            mi = self._img_pool.take()
         if hists:
-            arrs['current_hist'] = np.empty(self._S * self._T, dtype=self._dtype)
-            arrs['cumulative_hist'] = np.empty(self._S * self._T, dtype=self._dtype)
-        for k, a in arrs.items():
-            setattr(out, k, a.ctypes.data)
-        self._call(self._lib.lde_finalize, ctypes.byref(out))
-        tot = list(out.totals)
+            ch = np.empty(self._S * self._T, dtype=self._dtype)
+            mh = np.empty(self._S * self._T, dtype=self._dtype)
+        out.current_image = ci.ctypes.data if ci is not None else None
+        out.cumulative_image = mi.ctypes.data if mi is not None else None
+        out.current_hist = ch.ctypes.data if ch is not None else None
+        out.cumulative_hist = mh.ctypes.data if mh is not None else None
+        rc = self._lib.lde_finalize(self._h, self._out_ref)
+        if rc:
+            check(rc, self._h)
+        t0, t1, t2, t3 = out.totals
         shape = (self._S, self._T)
         return FinalizeResult(
-            current_image=arrs.get('current_image'),
-            cumulative_image=arrs.get('cumulative_image'),
-            current_hist=arrs['current_hist'].reshape(shape) if hists else None,
-            cumulative_hist=arrs['cumulative_hist'].reshape(shape) if hists else None,
-            current_total=int(tot[0]),
-            current_in_range=int(tot[1]),
-            cumulative_total=int(tot[2]),
-            cumulative_in_range=int(tot[3]),
+            current_image=ci,
+            cumulative_image=mi,
+            current_hist=ch.reshape(shape) if hists else None,
+            cumulative_hist=mh.reshape(shape) if hists else None,
+            current_total=t0,
+            current_in_range=t1,
+            cumulative_total=t2,
+            cumulative_in_range=t3,
         )
 
     def read_histogram(self, which: str = 'current') -> np.ndarray:
