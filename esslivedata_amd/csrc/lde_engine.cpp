@@ -168,7 +168,7 @@ struct lde_handle {
     bool early_gather = false;  // LDE_EARLY_GATHER
     bool sieve_pack = false;    // LDE_SIEVE_PACK
     int cold_sort_mode = 2;     // LDE_COLD_SORT: 0 block, 1 wave-independent, 2 16-byte groups
-    int cold_sort_kpt = 32;     // LDE_COLD_SORT_KPT: keys per thread per piece of mode 2
+    int cold_sort_kpt = 48;     // LDE_COLD_SORT_KPT: keys per thread per piece of mode 2 (16, 32, 48)
     bool key24 = true;          // LDE_KEY24: 24-bit cold keys when S * T < 2^24 - 1
     int tail_release = 1;       // LDE_TAIL_RELEASE: per-block L2 writeback at the end of
                                 // 1 the sieve, 2 the cold sort, 4 pass B, 8 PAGED pass A
@@ -1562,7 +1562,10 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->probe = env_ll("LDE_HOST_PROBE", 0) != 0;
         h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
         h->cold_sort_mode = (int)env_ll("LDE_COLD_SORT", 2);
-        h->cold_sort_kpt = env_ll("LDE_COLD_SORT_KPT", 32) == 16 ? 16 : 32;
+        {
+            const long long k = env_ll("LDE_COLD_SORT_KPT", 48);
+            h->cold_sort_kpt = k == 16 ? 16 : k == 32 ? 32 : 48;
+        }
         h->key24 = env_ll("LDE_KEY24", 1) != 0;
         h->tail_release = (int)env_ll("LDE_TAIL_RELEASE", 1);
         h->cold_sort_ablate = (int)env_ll("LDE_COLD_SORT_ABLATE", 0);

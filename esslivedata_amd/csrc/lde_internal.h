@@ -231,7 +231,7 @@ struct ColdArgs {
     long long n_bins;
     int wave_sort = 0;  // 1: k_cold_sort_w (wave-independent) when its LDS fits
     int pad8 = 0;       // 1: k_cold_sort_a (16-byte groups; ranges padded to 8 keys)
-    int sort_kpt = 32;  // k_cold_sort_a keys per thread per piece (16 or 32)
+    int sort_kpt = 48;  // k_cold_sort_a keys per thread per piece (16, 32 or 48)
     int key24 = 0;      // the sieve wrote 24-bit keys (k_cold_sort_a only)
     const uint32_t *hot_fmt = nullptr;  // per sieve block: hot rows as u16 (1) or u32 (0)
     int tail_release = 0;  // bit 1: sort blocks, bit 2: pass-B blocks end with an agent release

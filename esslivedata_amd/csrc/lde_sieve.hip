@@ -1423,6 +1423,26 @@ hipError_t launch_chunk_tab_karg(const SegDesc *host_segs, int n_segs, long long
     return hipGetLastError();
 }
 
+template <int TB, int KPT, bool K24>
+static void launch_sort_a(const ColdArgs &c, size_t sma, hipStream_t st) {
+    (void)hipFuncSetAttribute((const void *)k_cold_sort_a<TB, KPT, K24>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);
+    hipLaunchKernelGGL((k_cold_sort_a<TB, KPT, K24>), dim3(c.rows * kColdGroups), dim3(kSortThreads),
+                       sma, st, c);
+}
+
+template <int TB>
+static void launch_sort_a_tb(const ColdArgs &c, size_t sma, hipStream_t st) {
+    switch (c.sort_kpt) {
+    case 48:
+        return c.key24 ? launch_sort_a<TB, 48, true>(c, sma, st) : launch_sort_a<TB, 48, false>(c, sma, st);
+    case 32:
+        return c.key24 ? launch_sort_a<TB, 32, true>(c, sma, st) : launch_sort_a<TB, 32, false>(c, sma, st);
+    default:
+        return c.key24 ? launch_sort_a<TB, 16, true>(c, sma, st) : launch_sort_a<TB, 16, false>(c, sma, st);
+    }
+}
+
 hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t stop) {
     const int hot_blocks = c.hot_part ? ((c.ht + 255) / 256) * 8 : 0;
     hipLaunchKernelGGL(k_hot_reduce_scan, dim3(hot_blocks + c.n_tiles), dim3(256), 0, st, c,
@@ -1438,24 +1458,7 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
 #define LDE_COLD(TB)                                                                              \
     case TB:                                                                                      \
         if (aligned) {                                                                            \
-            const void *f = c.sort_kpt == 32                                                      \
-                                ? (c.key24 ? (const void *)k_cold_sort_a<TB, 32, true>            \
-                                           : (const void *)k_cold_sort_a<TB, 32, false>)          \
-                                : (c.key24 ? (const void *)k_cold_sort_a<TB, 16, true>            \
-                                           : (const void *)k_cold_sort_a<TB, 16, false>);         \
-            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);   \
-            if (c.sort_kpt == 32 && c.key24)                                                      \
-                hipLaunchKernelGGL((k_cold_sort_a<TB, 32, true>), dim3(c.rows * kColdGroups),     \
-                                   dim3(kSortThreads), sma, st, c);                               \
-            else if (c.sort_kpt == 32)                                                            \
-                hipLaunchKernelGGL((k_cold_sort_a<TB, 32, false>), dim3(c.rows * kColdGroups),    \
-                                   dim3(kSortThreads), sma, st, c);                               \
-            else if (c.key24)                                                                     \
-                hipLaunchKernelGGL((k_cold_sort_a<TB, 16, true>), dim3(c.rows * kColdGroups),     \
-                                   dim3(kSortThreads), sma, st, c);                               \
-            else                                                                                  \
-                hipLaunchKernelGGL((k_cold_sort_a<TB, 16, false>), dim3(c.rows * kColdGroups),    \
-                                   dim3(kSortThreads), sma, st, c);                               \
+            launch_sort_a_tb<TB>(c, sma, st);                                                     \
         } else if (wave) {                                                                        \
             (void)hipFuncSetAttribute((const void *)k_cold_sort_w<TB>,                            \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smw);      \

@@ -43,10 +43,11 @@ VARIANTS = [
     {'LDE_SIEVE_PACK': '1', 'LDE_EARLY_GATHER': '1'},
     {'LDE_SIEVE_ABLATE': '2048'},
     # cold-key sorts: block-cooperative per-key stores, wave-independent,
-    # 16-byte groups with 16 keys per thread (default: 16-byte groups, 32)
+    # 16-byte groups with 16 / 32 keys per thread (default: 16-byte groups, 48)
     {'LDE_COLD_SORT': '0'},
     {'LDE_COLD_SORT': '1'},
     {'LDE_COLD_SORT_KPT': '16'},
+    {'LDE_COLD_SORT_KPT': '32'},
     # cold keys as 32-bit words instead of packed 24-bit keys
     {'LDE_KEY24': '0'},
     # hot rows flushed as u32 instead of u16
