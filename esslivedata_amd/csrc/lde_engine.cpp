@@ -795,8 +795,11 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         // tile-major u16 keys: at most every staged slot, + the 8-key padding
         // of every (row, tile) range (k_cold_sort_a), + slack for pass B's
         // 16-byte loads
+        // the widest sort piece whose LDS still fits two blocks per CU
+        int sort_kpt = h->cold_sort_kpt;
+        while (sort_kpt > 16 && lde::cold_sort_a_smem(h->n_tiles, sort_kpt) > 80 * 1024) sort_kpt -= 16;
         const bool pad8 = h->cold_sort_mode == 2 && h->n_tiles <= lde::kSortThreadsHost &&
-                          lde::cold_sort_a_smem(h->n_tiles, h->cold_sort_kpt) <= 80 * 1024;
+                          lde::cold_sort_a_smem(h->n_tiles, sort_kpt) <= 80 * 1024;
         if (int rc = grow(h, &h->d_cold_keys, h->cold_keys_cap,
                           (size_t)a.grid * (size_t)a.cold_cap +
                               (pad8 ? (size_t)a.grid * lde::kColdGroups * nt * 8 : 0) + 64))
@@ -939,7 +942,7 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         c.n_bins = h->nbins;
         c.wave_sort = h->cold_sort_mode == 1 ? 1 : 0;
         c.pad8 = pad8 ? 1 : 0;
-        c.sort_kpt = h->cold_sort_kpt;
+        c.sort_kpt = sort_kpt;
         c.key24 = key24 ? 1 : 0;
         c.hot_fmt = h->d_hot_fmt;
         c.tail_release = h->tail_release;
