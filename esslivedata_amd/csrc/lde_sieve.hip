@@ -432,15 +432,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 const unsigned long long hm = inb & __builtin_amdgcn_ballot_w64(fl == 3u);
                 const uint32_t pos4 = (lanes_below(bal) + o_stg_w + tot) << 2;
                 tot += (uint32_t)__popcll(bal);
-                const uint32_t hidx4 = vsel(hm, k4, dum4);
-                if (!(ABL & 1))
-                    __hip_atomic_fetch_add(&lds_at(sm, hidx4), 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                else
-                    tot += hidx4 & 1u;
                 lds_at(sm, vsel(bal, pos4, dum4)) = k4;
+                // hot and cold lanes are disjoint: one LDS atomic adds 1 to the
+                // hot counter (hot lanes), the tile's cold-key count (cold
+                // lanes) or the lane's dummy word (the rest)
                 const uint32_t tidx4 = vsel(bal, ((k4 >> tsh) << 2) + o_tcnt4, dum4);
-                __hip_atomic_fetch_add(&lds_at(sm, tidx4), 1u, __ATOMIC_RELAXED,
+                const uint32_t aidx4 = (ABL & 1) ? tidx4 : vsel(hm, k4, tidx4);
+                __hip_atomic_fetch_add(&lds_at(sm, aidx4), 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             const uint32_t res = (tot + 3u) & ~3u;
