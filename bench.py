@@ -396,7 +396,9 @@ def main():
             'pulses_per_step': args.pulses,
             'strategy': info['last_strategy'],
             'tile_bits': info['tile_bits'],
-            'parallelism': f'event-batch sharding x{world} + RCCL reduce of partial outputs' if world > 1 else 'single GPU',
+            'parallelism': (f'event-batch sharding x{world} + '
+                            f'{"RCCL" if dist.get_backend() == "nccl" else dist.get_backend()} '
+                            'reduce of partial outputs') if world > 1 else 'single GPU',
         },
         'roofline': {
             'bound': 'hbm',
