@@ -1,0 +1,101 @@
+"""bench.py's output contract.
+
+CPU: the committed bench lines under profiles/ carry every field the driver
+and the roofline accounting need, and their numbers are consistent with each
+other and with the committed rocprofv3 summary they cite.
+GPU: a short bench run prints exactly one JSON line with the same fields.
+"""
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import bench  # noqa: E402  (no torch at import time)
+
+TOP_KEYS = ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step',
+            'higher_is_better', 'scaling', 'vs_baseline', 'dtype', 'data', 'config', 'roofline')
+ROOFLINE_KEYS = ('bound', 'achieved', 'peak', 'unit', 'frac', 'traffic')
+
+
+def _check_line(d: dict, n_gpus: int = 1):
+    for k in TOP_KEYS:
+        assert k in d, k
+    for k in ROOFLINE_KEYS:
+        assert k in d['roofline'], k
+    assert d['unit'] == 'events/s' and d['higher_is_better'] is True
+    assert d['n_gpus'] == n_gpus and d['scaling'] == 'weak'
+    cfg = d['config']
+    assert 'workload' in cfg and 'model' not in cfg
+    # value = all events of the timed steps over the timed wall time
+    per_step = cfg['events_per_step'] * d['n_gpus']
+    assert d['value'] == pytest.approx(per_step / (d['ms_per_step'] / 1e3), rel=1e-9)
+    r = d['roofline']
+    assert r['bound'] == 'hbm' and r['unit'] == 'GB/s' and r['peak'] == bench.HBM_PEAK_GBS
+    assert r['frac'] == pytest.approx(r['achieved'] / r['peak'], rel=1e-12)
+    # achieved = 8 algorithmic bytes per event of one launch / its average time
+    events_per_launch = cfg['events_per_step'] * d['steps'] / r['launches']
+    assert r['achieved'] == pytest.approx(
+        bench.BYTES_PER_EVENT * events_per_launch / (r['avg_launch_ms'] / 1e3) / 1e9, rel=1e-9)
+    assert 0.0 < r['frac'] < 1.0
+    assert 0.0 < r['step_frac'] <= r['pipeline_frac'] * 1.2
+
+
+@pytest.mark.parametrize('name', ['r2_bench_line.json', 'r2_loki_bench_line.json'])
+def test_committed_bench_line_contract(name):
+    d = json.loads((ROOT / 'profiles' / name).read_text())
+    _check_line(d)
+    r = d['roofline']
+    # the PMC traffic and the rocprofv3 average come from the committed summary
+    t = r['traffic_detail']
+    assert t is not None and (ROOT / t['source']).exists()
+    assert r['traffic'] == t['bytes'] == pytest.approx(t['read'] + t['write'])
+    prof = json.loads((ROOT / t['source']).read_text())[bench.KERNEL_SYMBOL[r['kernel']]]
+    assert prof['hbm_traffic_bytes'] == t['bytes']
+    # live HIP-event average and the traced rocprofv3 average of the same
+    # command agree within the tracing overhead
+    assert r['avg_launch_ms'] == pytest.approx(t['profiled_avg_ms'], rel=0.06)
+    # the kernel reads at least its algorithmic bytes
+    events_per_launch = d['config']['events_per_step'] * d['steps'] / r['launches']
+    assert t['read'] >= 0.95 * bench.BYTES_PER_EVENT * events_per_launch
+
+
+def test_committed_headline_line_has_baseline_and_check():
+    d = json.loads((ROOT / 'profiles' / 'r2_bench_line.json').read_text())
+    assert d['config']['workload'] == 'dream_mantle_cylinder_mantle_z'
+    assert d['config']['events_per_step'] == 140_000_000
+    cb = d['cpu_baseline']
+    for k in ('value', 'unit', 'cores', 'kind', 'sample'):
+        assert k in cb, k
+    assert cb['kind'] in ('port', 'reference') and cb['cores'] >= 1
+    assert d['check']['bit_exact_vs_oracle'] is True
+    assert cb['parity']['oracle_total'] == cb['parity']['gpu_total'] == d['check']['current_total']
+    lds = d['roofline']['lds']
+    assert 0.0 < lds['efficiency'] < 1.0
+    assert lds['efficiency'] == pytest.approx(1 - lds['SQ_LDS_BANK_CONFLICT'] / lds['SQ_LDS_IDX_ACTIVE'])
+
+
+def test_profile_readers_match_committed_summary():
+    t = bench.profiled_traffic('dream', 'split')
+    lds = bench.profiled_lds('dream', 'split')
+    assert t is not None and lds is not None
+    assert t['source'] == lds['source'] == 'profiles/r2_dream_bench.json'
+    assert bench.profiled_traffic('dream', 'atomic') is None  # no such kernel in the profile
+
+
+@pytest.mark.gpu
+def test_bench_prints_one_contract_line():
+    env = dict(os.environ)
+    cmd = [sys.executable, str(ROOT / 'bench.py'), '--steps', '2', '--warmup', '1',
+           '--pulses', '2', '--events-per-pulse', '1000000', '--no-cpu-baseline', '--e2e-steps', '0']
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, p.stdout[-2000:]
+    _check_line(json.loads(lines[0]))
