@@ -13,8 +13,14 @@ import threading
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / 'libesslivedata_amd.so'
+# the diagnostics build (python -m esslivedata_amd.build --diagnostics)
+DIAG_LIB_PATH = Path(__file__).resolve().parent / 'libesslivedata_amd_diag.so'
 if os.environ.get('LDE_LIBRARY'):  # A/B diagnostics: another build of the same ABI
     LIB_PATH = Path(os.environ['LDE_LIBRARY']).resolve()
+    import sys
+
+    print(f'esslivedata_amd: LDE_LIBRARY set, loading {LIB_PATH} instead of the product '
+          f'library', file=sys.stderr)
 
 ABI_VERSION = 1
 

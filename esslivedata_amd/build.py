@@ -16,6 +16,9 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / 'csrc'
 LIB = PKG / 'libesslivedata_amd.so'
+# -DLDE_DIAGNOSTICS: adds the timing ablations (wrong results by design) the
+# product library refuses; loaded only through LDE_LIBRARY by the A/B tools
+DIAG_LIB = PKG / 'libesslivedata_amd_diag.so'
 ARCH = os.environ.get('LDE_OFFLOAD_ARCH', 'gfx950')
 
 
@@ -30,10 +33,10 @@ def sources() -> list[Path]:
     return sorted(CSRC.glob('*.hip')) + sorted(CSRC.glob('*.cpp'))
 
 
-def needs_build() -> bool:
-    if not LIB.exists():
+def needs_build(lib: Path = LIB) -> bool:
+    if not lib.exists():
         return True
-    mtime = LIB.stat().st_mtime
+    mtime = lib.stat().st_mtime
     deps = sources() + sorted(CSRC.glob('*.h')) + [ROOT / 'include' / 'lde.h']
     return any(p.stat().st_mtime > mtime for p in deps)
 
@@ -48,10 +51,12 @@ def _run(cmd: list[str], verbose: bool) -> None:
         print(res.stderr, file=sys.stderr)
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile every source to an object in parallel, then link the library."""
-    if not force and not needs_build():
-        return LIB
+def build(force: bool = False, verbose: bool = False, diagnostics: bool = False) -> Path:
+    """Compile every source to an object in parallel, then link the library
+    (the product library; ``diagnostics=True`` the separate diagnostics one)."""
+    lib = DIAG_LIB if diagnostics else LIB
+    if not force and not needs_build(lib):
+        return lib
     from concurrent.futures import ThreadPoolExecutor
 
     flags = [
@@ -64,7 +69,9 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         '-Wno-unused-result',
         f'-I{ROOT / "include"}',
     ]
-    objdir = PKG / 'build'
+    if diagnostics:
+        flags.append('-DLDE_DIAGNOSTICS')
+    objdir = PKG / ('build_diag' if diagnostics else 'build')
     objdir.mkdir(exist_ok=True)
     srcs = sources()
     objs = [objdir / (s.name + '.o') for s in srcs]
@@ -74,13 +81,14 @@ def build(force: bool = False, verbose: bool = False) -> Path:
                 for s, o in zip(srcs, objs)]
         for f in futs:
             f.result()
-    tmp = LIB.with_suffix('.so.tmp')
+    tmp = lib.with_suffix('.so.tmp')
     _run([_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-Wl,--no-undefined',
           *[str(o) for o in objs], '-o',
           str(tmp)], verbose)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == '__main__':
-    print(build(force='--force' in sys.argv, verbose=True))
+    print(build(force='--force' in sys.argv, verbose=True,
+                diagnostics='--diagnostics' in sys.argv))

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_partition(
     for (long long c = c_begin + blockIdx.x; c < n_chunks; c += gridDim.x) {
         int key[EPT];
         uint32_t rank[EPT];
-        if (tp.pad == 0) {
+        if (LDE_DIAG(tp.pad) == 0) {
 #pragma unroll
             for (int e = 0; e < EPT; ++e)
                 key[e] = event_key<LT, FAST>(nxt.p[e], nxt.t[e], lut, pid_off, L, s_tab, tp);
@@ -115,9 +115,9 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_partition(
 #pragma unroll
             for (int e = 0; e < EPT; ++e) {
                 const unsigned p = (unsigned)nxt.p[e] - (unsigned)pid_off;
-                const int base = (tp.pad & 1) ? (int)((p & 16383u) * (unsigned)tp.T)
+                const int base = (LDE_DIAG(tp.pad) & 1) ? (int)((p & 16383u) * (unsigned)tp.T)
                                               : (p < L ? lut_base(lut, p, tp.T) : -1);
-                const int b = (tp.pad & 2) ? (int)((unsigned)nxt.t[e] & 63u) : toa_bin<FAST>(nxt.t[e], s_tab, tp);
+                const int b = (LDE_DIAG(tp.pad) & 2) ? (int)((unsigned)nxt.t[e] & 63u) : toa_bin<FAST>(nxt.t[e], s_tab, tp);
                 key[e] = (p >= L || base < 0 || b < 0) ? -1 : base + b;
             }
         }
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_partition(
         for (int e = 0; e < EPT; ++e) {
             const int tile = key[e] >= 0 ? (key[e] >> TILE_BITS) : -1;
             rank[e] = 0;
-            if (tp.pad & 4) {
+            if (LDE_DIAG(tp.pad) & 4) {
                 rank[e] = (uint32_t)(e * 64 + lane) & 255u;
             } else if (PEEL) {
                 const int lead = __builtin_amdgcn_readlane(tile, (e * 5) & 63);
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_partition(
         if (tid == 0) g_starts[n_tiles] = total;
         __syncthreads();
         // ---- scatter into LDS staging (tile-sorted)
-        if (!(tp.pad & 8)) {
+        if (!(LDE_DIAG(tp.pad) & 8)) {
 #pragma unroll
             for (int e = 0; e < EPT; ++e)
                 if (key[e] >= 0) s_stg[s_cnt[key[e] >> TILE_BITS] + rank[e]] = (uint16_t)(key[e] & MASK);
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_partition(
         __syncthreads();
         // ---- coalesced write-out of the valid prefix (16 B per lane)
         uint16_t *g_out = payload + c * (long long)CH;
-        if (!(tp.pad & 8))
+        if (!(LDE_DIAG(tp.pad) & 8))
             for (int i = tid * 8; i < (int)total; i += kPartThreads * 8)
                 *reinterpret_cast<uint4 *>(g_out + i) = *reinterpret_cast<const uint4 *>(s_stg + i);
         for (int i = tid; i <= n_tiles; i += blockDim.x) s_cnt[i] = 0;

@@ -26,6 +26,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "../../include/lde.h"
 #include "lde_internal.h"
 
@@ -172,7 +174,7 @@ struct lde_handle {
     bool key24 = true;          // LDE_KEY24: 24-bit cold keys when S * T < 2^24 - 1
     int tail_release = 1;       // LDE_TAIL_RELEASE: per-block L2 writeback at the end of
                                 // 1 the sieve, 2 the cold sort, 4 pass B, 8 PAGED pass A
-    int cold_sort_ablate = 0;   // LDE_COLD_SORT_ABLATE (diagnostic, wrong results)
+    int cold_sort_ablate = 0;   // LDE_COLD_SORT_ABLATE (LDE_DIAGNOSTICS build only)
     uint32_t ttab_cap = 0;
     int ttab_shift = 0;
     lde::ChunkPtrs *d_chunk_tab = nullptr;
@@ -275,6 +277,36 @@ long long env_ll(const char *name, long long dflt) {
     const char *v = std::getenv(name);
     if (!v || !*v) return dflt;
     return std::atoll(v);
+}
+
+// Diagnostic ablations produce wrong counts by design; the product library
+// has none compiled in and refuses the variables that would select them.
+// Any other LDE_* variable only changes how the engine computes (every knob
+// is exact); they are named once on stderr so a stray one is visible.
+int check_knobs() {
+#ifndef LDE_DIAGNOSTICS
+    static const char *const diag[] = {"LDE_ABLATE", "LDE_SIEVE_ABLATE", "LDE_COLD_SORT_ABLATE"};
+    for (const char *n : diag)
+        if (env_ll(n, 0) != 0)
+            return fail(nullptr, LDE_EINVAL,
+                        "%s selects a diagnostic ablation (wrong results by design), which only "
+                        "the LDE_DIAGNOSTICS build has",
+                        n);
+#endif
+    static std::once_flag once;
+    std::call_once(once, [] {
+        std::string names;
+        for (char **e = environ; e && *e; ++e)
+            if (std::strncmp(*e, "LDE_", 4) == 0) {
+                names += ' ';
+                names.append(*e, std::strcspn(*e, "="));
+            }
+#ifdef LDE_DIAGNOSTICS
+        names += " [diagnostics build]";
+#endif
+        if (!names.empty()) fprintf(stderr, "lde: non-default engine settings:%s\n", names.c_str());
+    });
+    return LDE_OK;
 }
 
 // Wait for the handle's stream.  Finalize returns results the caller waits
@@ -1052,7 +1084,11 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
         pa.L = (unsigned)h->L;
         pa.tab = h->d_tab;
         pa.tp = h->tp;
+#ifdef LDE_DIAGNOSTICS
         pa.tp.pad = (int)env_ll("LDE_ABLATE", 0);
+#else
+        pa.tp.pad = 0;
+#endif
         pa.n_tiles = h->n_tiles;
         pa.payload = h->d_payload;
         pa.starts = h->d_starts;
@@ -1324,6 +1360,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     if (!cfg) return fail(nullptr, LDE_EINVAL, "config is NULL");
     if (cfg->abi_version != LDE_ABI_VERSION)
         return fail(nullptr, LDE_EINVAL, "abi_version %d != %d", cfg->abi_version, LDE_ABI_VERSION);
+    if (int rc = check_knobs()) return rc;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(nullptr, LDE_EHIP, "no HIP device available");
@@ -1560,7 +1597,12 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         }
         h->lds_ctab = env_ll("LDE_LDS_CTAB", 1) != 0;
         h->karg_segs = env_ll("LDE_KARG_SEGS", 1) != 0;
+#ifdef LDE_DIAGNOSTICS
         h->sieve_ablate = (int)env_ll("LDE_SIEVE_ABLATE", 0);
+        h->cold_sort_ablate = (int)env_ll("LDE_COLD_SORT_ABLATE", 0);
+#endif
+        // exact variant: cold-key stores deferred behind the next gathers
+        if (env_ll("LDE_DEFER_STORES", 0) != 0) h->sieve_ablate |= 2048;
         h->early_gather = env_ll("LDE_EARLY_GATHER", 0) != 0;
         h->probe = env_ll("LDE_HOST_PROBE", 0) != 0;
         h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
@@ -1571,7 +1613,6 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         }
         h->key24 = env_ll("LDE_KEY24", 1) != 0;
         h->tail_release = (int)env_ll("LDE_TAIL_RELEASE", 1);
-        h->cold_sort_ablate = (int)env_ll("LDE_COLD_SORT_ABLATE", 0);
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);
         h->auto_partition = (int)env_ll("LDE_AUTO_PARTITION", LDE_STRATEGY_PAGED);

@@ -8,6 +8,17 @@
 
 struct lde_ev44_view;  // include/lde.h
 
+// Diagnostic ablations (timing probes whose results are wrong by design:
+// LDE_ABLATE, LDE_SIEVE_ABLATE, LDE_COLD_SORT_ABLATE) exist only in a
+// -DLDE_DIAGNOSTICS build (python -m esslivedata_amd.build --diagnostics);
+// in the product library LDE_DIAG(x) is the constant 0, so their branches and
+// kernel variants are not compiled, and lde_create refuses those variables.
+#ifdef LDE_DIAGNOSTICS
+#define LDE_DIAG(x) (x)
+#else
+#define LDE_DIAG(x) 0
+#endif
+
 namespace lde {
 
 constexpr int kPartThreads = 512;                  // pass A block

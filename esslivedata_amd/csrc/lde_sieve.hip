@@ -957,7 +957,7 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(ColdArgs c) {
         __syncthreads();
         for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
             const uint32_t k = s_sorted[i];
-            if (!(c.ablate & 1)) out[s_delta[k >> SH] + i] = (uint16_t)((k >> 2) & MASK);
+            if (!(LDE_DIAG(c.ablate) & 1)) out[s_delta[k >> SH] + i] = (uint16_t)((k >> 2) & MASK);
         }
         __syncthreads();
     }
@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4,
             nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
         }
     };
-    if (npieces && !(c.ablate & 2)) fetch(0);
+    if (npieces && !(LDE_DIAG(c.ablate) & 2)) fetch(0);
     for (uint32_t p = 0; p < npieces; ++p) {
         for (int i = lane; i < nt4; i += 64) base[i] = 0;
         uint32_t key[kWsKPT];
@@ -1047,7 +1047,7 @@ __global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4,
 #pragma unroll
             for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n_w ? nk[j][q] : 0xFFFFFFFFu;
         }
-        if (c.ablate & 2) {  // diagnostic: keys synthesized, not loaded
+        if (LDE_DIAG(c.ablate) & 2) {  // diagnostic: keys synthesized, not loaded
 #pragma unroll
             for (int e = 0; e < kWsKPT; ++e)
                 key[e] = ((((uint32_t)(lane * kWsKPT + e) + p * 977u) * 2654435761u) %
@@ -1096,7 +1096,7 @@ __global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4,
         }
         // the next piece's keys are requested once this piece's are dead (the
         // register budget of two blocks per CU), ahead of the write-out
-        if (p + 1 < npieces && !(c.ablate & 2)) fetch(p + 1);
+        if (p + 1 < npieces && !(LDE_DIAG(c.ablate) & 2)) fetch(p + 1);
         __builtin_amdgcn_wave_barrier();
         // runs leave as u16 tile-local keys, four image words per lane in flight
         for (uint32_t i0 = (uint32_t)lane; i0 < total; i0 += 256u) {
@@ -1111,7 +1111,7 @@ __global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4,
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const uint32_t i = i0 + 64u * (uint32_t)u;
-                if (i < total && !(c.ablate & 1)) out[d[u] + i] = (uint16_t)((k[u] >> 2) & MASK);
+                if (i < total && !(LDE_DIAG(c.ablate) & 1)) out[d[u] + i] = (uint16_t)((k[u] >> 2) & MASK);
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1280,7 +1280,7 @@ void k_cold_sort_a(ColdArgs c) {
             const uint32_t k = (pos - s_B[lo]) >> 3;
             const uint4 v = *reinterpret_cast<const uint4 *>(img + pos);
             if (k < s_full[lo]) {
-                if (!(c.ablate & 1))
+                if (!(LDE_DIAG(c.ablate) & 1))
                     *reinterpret_cast<uint4 *>(out + s_pos[lo] + 8u * k) = v;
             } else {
                 s_carry[lo] = v;
@@ -1300,7 +1300,7 @@ void k_cold_sort_a(ColdArgs c) {
 #pragma unroll
         for (uint32_t i = 0; i < 8; ++i)
             if (i >= cn) cw[i >> 1] |= 0xFFFFu << ((i & 1) * 16);
-        if (!(c.ablate & 1))
+        if (!(LDE_DIAG(c.ablate) & 1))
             *reinterpret_cast<uint4 *>(out + s_pos[tid]) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
     }
     if (c.tail_release & 2) {  // this block's keys written back before the kernel ends
@@ -1468,7 +1468,7 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
             hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * kColdGroups), dim3(kSortThreads),   \
                                sm, st, c);                                                        \
         }                                                                                         \
-        if (!c.ablate) /* diagnostics: the keys are not valid */                                 \
+        if (!LDE_DIAG(c.ablate)) /* diagnostics: the keys are not valid */                                 \
         hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, st,\
                               nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist, c.n_bins,  \
                               (c.tail_release & 4) ? 1 : 0);                                      \
@@ -1504,12 +1504,17 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     switch (mode) {
 #define LDE_SIEVE_MODE(m) \
     case m: return launch_sieve_t<m>(a, grid, st, start, stop);
-    LDE_SIEVE_MODE(0) LDE_SIEVE_MODE(1) LDE_SIEVE_MODE(2) LDE_SIEVE_MODE(4) LDE_SIEVE_MODE(6)
+    // exact variants: the pass, early gathers (256), deferred stores (2048),
+    // the packed table word (65536)
+    LDE_SIEVE_MODE(0) LDE_SIEVE_MODE(256) LDE_SIEVE_MODE(2048) LDE_SIEVE_MODE(65536)
+    LDE_SIEVE_MODE(65536 | 256) LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048)
+#ifdef LDE_DIAGNOSTICS
+    // timing probes (wrong results), diagnostics build only
+    LDE_SIEVE_MODE(1) LDE_SIEVE_MODE(2) LDE_SIEVE_MODE(4) LDE_SIEVE_MODE(6)
     LDE_SIEVE_MODE(8) LDE_SIEVE_MODE(16) LDE_SIEVE_MODE(32) LDE_SIEVE_MODE(64) LDE_SIEVE_MODE(128)
-    LDE_SIEVE_MODE(256) LDE_SIEVE_MODE(512) LDE_SIEVE_MODE(1024) LDE_SIEVE_MODE(2048)
-    LDE_SIEVE_MODE(4096) LDE_SIEVE_MODE(8192) LDE_SIEVE_MODE(12288) LDE_SIEVE_MODE(16384)
-    LDE_SIEVE_MODE(49152) LDE_SIEVE_MODE(65536) LDE_SIEVE_MODE(65536 | 256)
-    LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048) LDE_SIEVE_MODE(131072)
+    LDE_SIEVE_MODE(512) LDE_SIEVE_MODE(1024) LDE_SIEVE_MODE(4096) LDE_SIEVE_MODE(8192)
+    LDE_SIEVE_MODE(12288) LDE_SIEVE_MODE(16384) LDE_SIEVE_MODE(49152) LDE_SIEVE_MODE(131072)
+#endif
 #undef LDE_SIEVE_MODE
     default: return hipErrorInvalidValue;
     }

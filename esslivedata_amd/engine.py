@@ -85,13 +85,33 @@ class _OutputPool:
         return a
 
 
-def _as_i32(a) -> np.ndarray:
+_I32_MIN, _I32_MAX = -(2**31), 2**31 - 1
+
+
+def _as_i32(a, what: str, unknown_id: int | None = None) -> np.ndarray:
+    """Contiguous int32 event array.  Wider integer arrays are converted
+    only where their values fit: out-of-range pixel ids become
+    ``unknown_id`` (an id outside the detector, so the event is dropped like
+    any unknown id, group_by_pixel.py:46-54) instead of wrapping onto a valid
+    pixel; out-of-range TOA values (the ev44 field is int32) are refused."""
     a = np.asarray(a)
-    if a.dtype != np.int32:
-        if a.dtype.kind not in 'iu':
-            raise TypeError(f'event arrays must be integer, got {a.dtype}')
-        a = a.astype(np.int32)
-    return np.ascontiguousarray(a)
+    if a.dtype == np.int32:
+        return np.ascontiguousarray(a)
+    if a.dtype.kind not in 'iu':
+        raise TypeError(f'event arrays must be integer, got {a.dtype}')
+    if a.size == 0:
+        return np.zeros(0, dtype=np.int32)
+    if a.dtype.kind == 'u':
+        bad = a > _I32_MAX
+    else:
+        bad = (a < _I32_MIN) | (a > _I32_MAX)
+    if not bad.any():
+        return np.ascontiguousarray(a, dtype=np.int32)
+    if unknown_id is None:
+        raise ValueError(f'{what} values must fit in int32')
+    out = np.where(bad, 0, a).astype(np.int32)
+    out[bad] = unknown_id
+    return out
 
 
 class BinningEngine:
@@ -161,6 +181,9 @@ class BinningEngine:
         else:
             cfg.range_lo, cfg.range_hi = int(toa_range[0]), int(toa_range[1])
         self._n_replicas = cfg.n_replicas
+        # a pixel id no LUT entry covers: stands in for ids beyond int32
+        lo, hi = int(pid_offset), int(pid_offset) + int(cfg.lut_len)
+        self._unknown_id = lo - 1 if lo > _I32_MIN else (hi if hi <= _I32_MAX else None)
         h = ctypes.c_void_p()
         rc = lib.lde_create(ctypes.byref(cfg), ctypes.byref(h))
         check(rc, None)
@@ -203,11 +226,11 @@ class BinningEngine:
     # ------------------------------------------------------------------
     def stage(self, pid, toa) -> None:
         """Stage one message of host events (ToNXevent_data.add equivalent)."""
-        t = _as_i32(toa)
+        t = _as_i32(toa, 'time_of_arrival')
         if pid is None:
             self._call(self._lib.lde_stage, None, t.ctypes.data, len(t))
             return
-        p = _as_i32(pid)
+        p = _as_i32(pid, 'pixel_id', self._unknown_id)
         if len(p) != len(t):
             raise ValueError(
                 f'pixel_id and time_of_arrival must have the same length, '

@@ -116,12 +116,18 @@ class StagedEvents:
 
 
 def _int32_view(a) -> np.ndarray:
+    """The message array as contiguous int32 (zero-copy when it already is).
+    Wider integer arrays whose values do not all fit are kept as they are:
+    the engine's ``stage`` converts them with range checks (an id beyond int32
+    is an unknown id and dropped, as ``group_event_data`` drops it; it must
+    not wrap onto a valid pixel)."""
     arr = np.asarray(a)
-    if arr.dtype == np.int32 and arr.flags.c_contiguous:
-        return arr
     if arr.dtype.kind not in 'iu':
         raise TypeError(f'event arrays must be integer, got {arr.dtype}')
-    return np.ascontiguousarray(arr, dtype=np.int32)
+    if arr.dtype == np.int32 or arr.size == 0 or (
+            int(arr.min()) >= -(2**31) and int(arr.max()) < 2**31):
+        return np.ascontiguousarray(arr, dtype=np.int32)
+    return np.ascontiguousarray(arr)
 
 
 class EventStaging:

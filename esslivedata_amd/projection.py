@@ -25,6 +25,8 @@ from typing import Callable, Sequence
 
 import numpy as np
 
+from .logical import LogicalIndex, detector_index, reduction_dims
+
 MAX_LUT_LEN = 1 << 28
 
 
@@ -162,6 +164,27 @@ def geometric_lut(
     )
 
 
+def _reduce_axes(t, reduction_axes: Sequence[int],
+                 reduction_dim: str | Sequence[str] | None) -> tuple[np.ndarray, list[int], tuple]:
+    """Transformed index array, the kept axes and their names (None when
+    the transform returned a plain array)."""
+    names = t.dims if isinstance(t, LogicalIndex) else None
+    arr = np.asarray(t.values if isinstance(t, LogicalIndex) else t)
+    red = set(int(a) % arr.ndim for a in reduction_axes) if arr.ndim else set()
+    rdims = reduction_dims(reduction_dim)
+    if rdims:
+        if names is None:
+            raise ValueError('reduction_dim needs a transform that keeps dim names '
+                             '(fold/flatten on the LogicalIndex it receives)')
+        for d in rdims:
+            if d not in names:
+                raise ValueError(f'reduction dim {d!r} not in the transformed dims {names}')
+            red.add(names.index(d))
+    kept = [a for a in range(arr.ndim) if a not in red]
+    kept_names = None if names is None else tuple(names[a] for a in kept)
+    return arr, kept, kept_names
+
+
 def logical_lut(
     detector_number: np.ndarray,
     *,
@@ -169,33 +192,44 @@ def logical_lut(
     transform: Callable[[np.ndarray], np.ndarray] | None = None,
     output_dims: Sequence[str] | None = None,
     reduction_axes: Sequence[int] = (),
+    reduction_dim: str | Sequence[str] | None = None,
 ) -> ViewLUT:
     """LUT for a logical view (identity, fold/flatten/slice, reduction).
 
-    ``transform`` receives an index array shaped like ``detector_number`` and
-    returns the reshaped/sliced array; pixels it drops map to -1; axes listed
-    in ``reduction_axes`` (of the transformed array) are merged.
+    ``transform`` receives a :class:`LogicalIndex` (pixel indices shaped like
+    ``detector_number``, dims ``dims`` or ``('detector_number',)`` for 1-D) and
+    returns the folded / transposed / sliced / flattened result, as the
+    reference's transforms do to the detector data
+    (LogicalProjector.project_events, projectors.py:243-270); pixels it drops
+    map to -1.  The named ``reduction_dim`` (projectors.py:186-207), or the
+    positional ``reduction_axes`` of a transform returning a plain array, are
+    merged (``bins.concat``).  Output dims are the kept names.
     """
     dn = np.asarray(detector_number)
     p = dn.size
-    idx = np.arange(p, dtype=np.int64).reshape(dn.shape)
-    t = np.asarray(idx if transform is None else transform(idx))
-    red = set(int(a) % t.ndim for a in reduction_axes) if t.ndim else set()
-    kept = [a for a in range(t.ndim) if a not in red]
-    out_shape = tuple(t.shape[a] for a in kept)
-    moved = np.moveaxis(t, kept, list(range(len(kept)))) if t.ndim else t
+    idx = detector_index(dn, dims)
+    t = idx if transform is None else transform(idx)
+    arr, kept, kept_names = _reduce_axes(t, reduction_axes, reduction_dim)
+    out_shape = tuple(arr.shape[a] for a in kept)
+    moved = np.moveaxis(arr, kept, list(range(len(kept)))) if arr.ndim else arr
     n_out = int(np.prod(out_shape)) if out_shape else 1
     moved = moved.reshape(n_out, -1)
+    if moved.size and (moved.min() < 0 or moved.max() >= p):
+        raise ValueError('the transform produced indices outside the detector')
+    if moved.size != len(np.unique(moved)):
+        raise ValueError('the transform duplicated detector pixels')
     pix_out = np.full(p, -1, dtype=np.int64)
     out_ids = np.repeat(np.arange(n_out, dtype=np.int64), moved.shape[1])
     pix_out[moved.ravel()] = out_ids
     off, lut = _compose(dn, pix_out[None, :])
     weights = np.bincount(pix_out[pix_out >= 0], minlength=n_out).astype(np.float32)
     if output_dims is None:
-        if dims is not None and transform is None and not red:
-            output_dims = tuple(dims)
+        if kept_names is not None:
+            output_dims = kept_names
         else:
             output_dims = tuple(f'dim_{i}' for i in range(len(out_shape)))
+    if len(tuple(output_dims)) != len(out_shape):
+        raise ValueError(f'output_dims {tuple(output_dims)} do not match the view shape {out_shape}')
     return ViewLUT(
         pid_offset=off,
         lut=lut,

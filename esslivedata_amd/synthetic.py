@@ -144,6 +144,102 @@ def bifrost_transform(idx: np.ndarray) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------
+# logical views over folded banks (DREAM, MAGIC)
+# ---------------------------------------------------------------------------
+# Logical voxel structure of the DREAM banks, ``ess.dream.workflows.
+# DETECTOR_BANK_SIZES`` (essreduce-side package, not in /root/reference;
+# the mantle's dim order is the one dream/views.py:47-48 states: after the
+# fold the dims are (wire, module, segment, strip, counter)).  The mantle's
+# product is its 491,520 pixels (dream/streams.py:19).
+DREAM_BANK_SIZES: dict[str, dict[str, int]] = {
+    'mantle_detector': {'wire': 32, 'module': 5, 'segment': 6, 'strip': 256, 'counter': 2},
+}
+
+# MAGIC banks, as the reference defines them (magic/views.py:32-35).
+MAGIC_BANK_SIZES: dict[str, dict[str, int]] = {
+    'magic_detector_a': {'wire': 32, 'strip': 128, 'segment': 120},
+    'magic_detector_b': {'wire': 32, 'strip': 16, 'segment': 256},
+}
+
+
+def dream_mantle_front_layer(da, source_name: str):
+    """``get_mantle_front_layer`` (dream/views.py:13-21): wire 0 only,
+    (mod/seg/cntr, strip)."""
+    return (
+        da.fold(dim=da.dim, sizes=DREAM_BANK_SIZES[source_name])
+        .transpose(('wire', 'module', 'segment', 'counter', 'strip'))['wire', 0]
+        .flatten(('module', 'segment', 'counter'), to='mod/seg/cntr')
+    )
+
+
+def dream_wire_view(da, source_name: str):
+    """``get_wire_view`` (dream/views.py:24-53): (strip, wire, mod/seg/cntr);
+    the view reduces ``strip``."""
+    return (
+        da.fold(dim=da.dim, sizes=DREAM_BANK_SIZES[source_name])
+        .transpose(('strip', 'wire', 'module', 'segment', 'counter'))
+        .flatten(('module', 'segment', 'counter'), to='mod/seg/cntr')
+    )
+
+
+def dream_strip_view(da, source_name: str):
+    """``get_strip_view`` (dream/views.py:56-85): (other, strip); the view
+    reduces ``other``."""
+    folded = da.fold(dim=da.dim, sizes=DREAM_BANK_SIZES[source_name])
+    rest = tuple(d for d in folded.dims if d != 'strip')
+    if len(rest) > 1:
+        folded = folded.transpose((*rest, 'strip')).flatten(rest, to='other')
+    return folded
+
+
+def magic_wire_view(da, source_name: str):
+    """``get_wire_view`` (magic/views.py:38-58): (wire, strip, segment); the
+    view reduces ``strip``."""
+    return da.fold(dim=da.dim, sizes=MAGIC_BANK_SIZES[source_name])
+
+
+def magic_strip_view(da, source_name: str):
+    """``get_strip_view`` (magic/views.py:61-85): (wire/segment, strip); the
+    view reduces ``wire/segment``."""
+    folded = da.fold(dim=da.dim, sizes=MAGIC_BANK_SIZES[source_name])
+    return folded.transpose(('wire', 'segment', 'strip')).flatten(('wire', 'segment'),
+                                                                   to='wire/segment')
+
+
+def dream_logical_views() -> dict:
+    """The DREAM logical views registered for the mantle (dream/specs.py:
+    151-180): name -> ``LogicalViewConfig``."""
+    from .workflows import LogicalViewConfig
+
+    return {
+        'mantle_front_layer': LogicalViewConfig(transform=dream_mantle_front_layer),
+        'wire_view': LogicalViewConfig(transform=dream_wire_view, roi_support=False,
+                                       reduction_dim='strip'),
+        'strip_view': LogicalViewConfig(transform=dream_strip_view, roi_support=False,
+                                        reduction_dim='other'),
+    }
+
+
+def magic_logical_views() -> dict:
+    """MAGIC's wire and strip views (magic/specs.py:93-111)."""
+    from .workflows import LogicalViewConfig
+
+    return {
+        'wire_view': LogicalViewConfig(transform=magic_wire_view, roi_support=False,
+                                       reduction_dim='strip'),
+        'strip_view': LogicalViewConfig(transform=magic_strip_view, roi_support=False,
+                                        reduction_dim='wire/segment'),
+    }
+
+
+def magic_bank(name: str = 'magic_detector_a', first: int = 1) -> Instrument:
+    """A MAGIC bank: contiguous detector numbers over its voxels."""
+    n = int(np.prod(list(MAGIC_BANK_SIZES[name].values())))
+    return Instrument(name=name, detector_number=np.arange(first, first + n, dtype=np.int32),
+                      coords=None, resolution=None, edges=TOAEdges())
+
+
+# ---------------------------------------------------------------------------
 # event streams (numpy, for tests and the CPU baseline)
 # ---------------------------------------------------------------------------
 def zipf_pixel_weights(p: int, s: float = 1.2, seed: int = 7) -> np.ndarray:

@@ -92,11 +92,18 @@ class GeometricViewConfig:
 
 @dataclass(frozen=True)
 class LogicalViewConfig:
-    """``LogicalViewConfig`` (types.py:134-162); ``transform`` maps an
-    index-valued array shaped like ``detector_number`` (and the source name) to
-    the reshaped/sliced view; ``reduction_axes`` are merged."""
+    """``LogicalViewConfig`` (SRC/workflows/detector_view/types.py:100-126).
 
-    transform: Callable[[np.ndarray, str], np.ndarray] | None = None
+    ``transform(da, source_name)`` receives a :class:`logical.LogicalIndex`
+    (the pixel indices with the detector's dims) and folds / transposes /
+    slices / flattens it with the scipp calls the reference's transforms use;
+    ``reduction_dim`` (a dim name or a list of names) is merged as
+    ``bins.concat`` does (projectors.py:243-270).  A transform that returns a
+    plain array instead names its merged axes by position in
+    ``reduction_axes``."""
+
+    transform: Callable[[Any, str], Any] | None = None
+    reduction_dim: str | Sequence[str] | None = None
     reduction_axes: Sequence[int] = ()
     output_dims: tuple[str, ...] | None = None
     roi_support: bool = True
@@ -459,8 +466,11 @@ class GpuDetectorViewFactory:
         sample_position=(0.0, 0.0, 0.0),
         out_dtype: str = 'float64',
         device: int = 0,
+        detector_dims: Mapping[str, Sequence[str]] | None = None,
+        strategy: str = 'auto',
     ) -> None:
         self._dn = dict(detector_numbers)
+        self._strategy = strategy
         # wavelength mode: the (Ltotal, time) table (the reference's
         # LookupTableFilename) and the beamline for Ltotal
         self._lookup = lookup_table
@@ -474,6 +484,8 @@ class GpuDetectorViewFactory:
         self._transforms = dict(transforms or {})
         self._dtype = out_dtype
         self._device = device
+        # dim names of each detector_number (1-D: 'detector_number')
+        self._dims = dict(detector_dims or {})
 
     def make_geometry(self, source_name: str) -> 'GeometricSource':
         from .geometry import GeometricSource
@@ -503,7 +515,8 @@ class GpuDetectorViewFactory:
         if isinstance(cfg, LogicalViewConfig):
             tf = None if cfg.transform is None else (lambda a: cfg.transform(a, source_name))
             return logical_lut(dn, transform=tf, reduction_axes=cfg.reduction_axes,
-                               output_dims=cfg.output_dims)
+                               reduction_dim=cfg.reduction_dim, output_dims=cfg.output_dims,
+                               dims=self._dims.get(source_name))
         raise TypeError(f'unknown view config {type(cfg).__name__}')
 
     def make_workflow(self, source_name: str, params: DetectorViewParams | None = None,
@@ -517,7 +530,8 @@ class GpuDetectorViewFactory:
             geometry = self.make_geometry(source_name)
         return GpuDetectorViewWorkflow(
             source_name, None if geometry is not None else self.make_view(source_name), params,
-            out_dtype=self._dtype, device=self._device, roi_support=roi_support,
+            out_dtype=self._dtype, device=self._device, strategy=self._strategy,
+            roi_support=roi_support,
             roi_keys=aux_source_names, spectrum_view=spectrum, geometry=geometry,
             lookup_table=self._lookup, source_position=self._beamline[0],
             sample_position=self._beamline[1],

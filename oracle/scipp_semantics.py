@@ -189,6 +189,47 @@ def logical_screen_index(
     return lut, out_shape
 
 
+def folded_view_index(
+    sizes: dict[str, int],
+    out_axes: Sequence[Sequence[str]],
+    fixed: dict[str, int] | None = None,
+) -> tuple[np.ndarray, tuple[int, ...]]:
+    """Closed-form output index per pixel of a fold / transpose / slice /
+    flatten / ``bins.concat`` logical view (projectors.py:243-270), derived
+    without applying any transform: pixel ``p`` has mixed-radix coordinates
+    over ``sizes`` (row-major ``fold``, dict order slowest first); it is kept
+    when every ``fixed`` dim equals its value (``['wire', 0]``); its output
+    index is the mixed-radix number over ``out_axes`` (each a group of dims
+    flattened in the given order, e.g. ``('module', 'segment', 'counter')``);
+    dims in neither are merged.  Used for the DREAM views
+    (config/instruments/dream/views.py:13-85) and MAGIC views
+    (config/instruments/magic/views.py:38-85)."""
+    fixed = dict(fixed or {})
+    names = list(sizes)
+    radix = [int(sizes[d]) for d in names]
+    p = int(np.prod(radix))
+    coord = {}
+    rem = np.arange(p, dtype=np.int64)
+    for d, n in zip(reversed(names), reversed(radix)):
+        coord[d] = rem % n
+        rem = rem // n
+    keep = np.ones(p, dtype=bool)
+    for d, v in fixed.items():
+        keep &= coord[d] == int(v)
+    out = np.zeros(p, dtype=np.int64)
+    shape = []
+    for group in out_axes:
+        n_group = 1
+        g = np.zeros(p, dtype=np.int64)
+        for d in group:
+            g = g * sizes[d] + coord[d]
+            n_group *= sizes[d]
+        out = out * n_group + g
+        shape.append(n_group)
+    out[~keep] = -1
+    return out, tuple(shape)
+
+
 # --------------------------------------------------------------------------
 # Histograms
 # --------------------------------------------------------------------------

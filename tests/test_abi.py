@@ -65,3 +65,40 @@ def test_library_is_gfx950_code_object():
     assert '.hip_fatbin' in out
     blob = lib.read_bytes()
     assert b'gfx950' in blob
+
+
+@pytest.mark.parametrize('knob', ['LDE_SIEVE_ABLATE', 'LDE_ABLATE', 'LDE_COLD_SORT_ABLATE'])
+def test_product_library_refuses_diagnostic_ablations(knob):
+    """Result-corrupting timing ablations exist only in the LDE_DIAGNOSTICS
+    build: the product library's lde_create refuses them (before any device
+    call, so this runs without a GPU)."""
+    import os
+    import subprocess
+    import sys
+
+    code = (
+        'import ctypes\n'
+        'from esslivedata_amd import _native\n'
+        'lib = _native.lib()\n'
+        'cfg = _native.LdeConfig(); cfg.abi_version = _native.ABI_VERSION\n'
+        'h = ctypes.c_void_p()\n'
+        'rc = lib.lde_create(ctypes.byref(cfg), ctypes.byref(h))\n'
+        'print(rc, lib.lde_last_error(None).decode())\n'
+    )
+    env = dict(os.environ, **{knob: '1'})
+    env.pop('LDE_LIBRARY', None)
+    res = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True,
+                         cwd=ROOT, timeout=120)
+    assert res.returncode == 0, res.stderr
+    rc, msg = res.stdout.strip().split(' ', 1)
+    assert int(rc) == -1 and knob in msg and 'DIAGNOSTICS' in msg
+
+
+def test_product_library_has_only_exact_sieve_variants():
+    import subprocess
+
+    lib = ROOT / 'esslivedata_amd' / 'libesslivedata_amd.so'
+    out = subprocess.run(['nm', '-C', str(lib)], capture_output=True, text=True).stdout
+    modes = {int(m) for m in re.findall(r'lde::k_sieve<(\d+), \d>\(', out)}
+    assert 0 in modes
+    assert modes <= {0, 256, 2048, 65536, 65536 | 256, 65536 | 2048, 65536 | 256 | 2048}, modes

@@ -41,7 +41,7 @@ VARIANTS = [
     # gathers issued an iteration early, cold-key stores deferred
     {'LDE_SIEVE_PACK': '1'},
     {'LDE_SIEVE_PACK': '1', 'LDE_EARLY_GATHER': '1'},
-    {'LDE_SIEVE_ABLATE': '2048'},
+    {'LDE_DEFER_STORES': '1'},
     # cold-key sorts: block-cooperative per-key stores, wave-independent,
     # 16-byte groups with 16 / 32 keys per thread (default: 16-byte groups, 48)
     {'LDE_COLD_SORT': '0'},

@@ -154,3 +154,28 @@ def test_product_package_never_imports_oracle():
     for f in pkg.rglob('*.py'):
         text = f.read_text()
         assert 'import oracle' not in text and 'from oracle' not in text, f
+
+
+def test_wide_pixel_ids_are_dropped_not_wrapped():
+    """An int64 id of 2**32 + 5 is an unknown id (dropped, group_by_pixel.py:
+    46-54), not pixel 5; a TOA beyond int32 is refused (the ev44 field is
+    int32).  Conversion only; nothing runs on a device."""
+    from esslivedata_amd.engine import _as_i32
+
+    pid = np.array([5, 2**32 + 5, -(2**31) - 1, 7], dtype=np.int64)
+    out = _as_i32(pid, 'pixel_id', unknown_id=0)
+    np.testing.assert_array_equal(out, [5, 0, 0, 7])
+    assert out.dtype == np.int32
+    np.testing.assert_array_equal(_as_i32(np.array([3, 2**40], dtype=np.uint64), 'pixel_id', -1), [3, -1])
+    np.testing.assert_array_equal(_as_i32(np.array([1, 2], dtype=np.int64), 'toa'), [1, 2])
+    with pytest.raises(ValueError):
+        _as_i32(np.array([2**31], dtype=np.int64), 'time_of_arrival')
+    with pytest.raises(TypeError):
+        _as_i32(np.array([1.0]), 'pixel_id', 0)
+    # the staging accumulator keeps wide arrays unconverted for the engine
+    from esslivedata_amd.preprocessors import DetectorEvents, EventStaging, Timestamp
+
+    st = EventStaging()
+    st.add(Timestamp.from_ns(0), DetectorEvents(pixel_id=pid, time_of_arrival=np.arange(4),
+                                                unit='ns'))
+    assert st.get().pixel_id[0].dtype == np.int64
