@@ -38,6 +38,8 @@ KERNEL_SYMBOL = {
     'paged': 'k_paged_partition',
     'page_accumulate': 'k_page_accumulate',
     'split': 'k_sieve',  # SPLIT's event pass (k_split when LDE_SIEVE=0)
+    'coord': 'k_event_coord',  # wavelength-mode coordinate pass
+    'finalize': 'k_finalize_v4',
 }
 # engine timing buckets (include/lde.h LDE_K_*) as they are used by the SPLIT
 # strategy's SIEVE pass: 'split' = k_chunk_tab + k_sieve, 'split_aux' = hot-set
@@ -211,7 +213,7 @@ def main():
         d = wavelength.distance_per_pid(inst.detector_number, lt, view.pid_offset, view.lut.shape[1])
         edges = WavelengthEdges(start=0.2, stop=3.6 if args.workload == 'dream' else 10.0,
                                 num_bins=100).get_edges()
-        coord = (d, tab)
+        coord = (d, tab, lt)
     # one non-default torch stream for the data generation, the engine and
     # the collectives: everything in order on it, no cross-stream waits
     stream = torch.cuda.Stream(dev)
@@ -226,7 +228,7 @@ def main():
         stream=stream.cuda_stream,
     )
     if coord is not None:
-        d, tab = coord
+        d, tab, _ = coord
         eng.set_coordinate_lut(d, tab.table, dist0=tab.distance0, dist_step=tab.distance_step,
                                time0=tab.time0, time_step=tab.time_step)
     n_pulse = args.events_per_pulse
@@ -271,22 +273,34 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
-    # inside the timed region only the dominant kernel and the whole binning
-    # sequence are bracketed with HIP events (every recorded pair costs host
-    # time); the per-kernel breakdown comes from a few extra steps afterwards
-    strat = eng.info()['last_strategy']
-    dom = {'split': 'split', 'paged': 'paged', 'partition': 'partition', 'atomic': 'atomic'}.get(strat, 'split')
-    # only the dominant kernel is timed in the timed region: its events are
-    # stamped by its own dispatch (no marker packets, no extra host calls in
-    # front of the launch); the binning-sequence span, whose start marker
-    # costs host time before the first launch, comes from the extra steps.
-    # A stamped dispatch still costs step time (hipExtLaunchKernelGGL with
+    # per-kernel breakdown (every kernel bracketed with HIP events) from 3
+    # extra steps before the timed region; the dominant kernel is the one
+    # with the largest time per step among them (a kernel, not a strategy:
+    # in wavelength mode the coordinate pass dominates the sieve)
+    names = ('atomic', 'partition', 'tile_accumulate', 'plan', 'paged', 'page_plan',
+             'page_accumulate', 'split', 'split_aux', 'coord', 'binning', 'finalize')
+    eng.timing_select(None)
+    eng.timing_enable(True)
+    n_prof = 3
+    for i in range(n_prof):
+        step(args.warmup + i)
+    torch.cuda.synchronize(dev)
+    stats = {k: eng.kernel_stats(k) for k in names}
+    info = eng.info()
+    eng.timing_enable(False)
+    per_step = {k: v[0] / n_prof for k, v in stats.items()
+                if v[1] and k in KERNEL_SYMBOL and k != 'binning'}
+    dom = max(per_step, key=per_step.get) if per_step else 'split'
+    # The timed region stamps only the dominant kernel, by its own dispatch
+    # (no marker packets, no extra host calls in front of the launch).  A
+    # stamped dispatch still costs step time (hipExtLaunchKernelGGL with
     # events: ~5 us before the next kernel starts plus host time, ~16 us per
-    # step on DREAM), so the kernel is stamped on every `timing_stride`-th
-    # step of the region, spread over it, and its average is taken over those
+    # step on DREAM), so the kernel is stamped on every `timing_stride`-th step
+    # of the region, spread over it, and its average is taken over those
     stride = max(1, args.timing_stride)
     untimed = os.environ.get('LDE_BENCH_UNTIMED', '0') not in ('', '0')
     sampled = set() if untimed else set(range(0, args.steps, stride))
+    first = args.warmup + n_prof
     eng.timing_select([])
     if world > 1:
         dist.barrier()
@@ -298,10 +312,10 @@ def main():
     for i in range(args.steps):
         if i in sampled:
             eng.timing_select([dom])
-            step(args.warmup + i)
+            step(first + i)
             eng.timing_select([])
         else:
-            step(args.warmup + i)
+            step(first + i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -311,17 +325,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     timed = {dom: eng.kernel_stats(dom)}
-
-    names = ('atomic', 'partition', 'tile_accumulate', 'plan', 'paged', 'page_plan',
-             'page_accumulate', 'split', 'split_aux', 'coord', 'binning', 'finalize')
-    eng.timing_select(None)
-    eng.timing_enable(True)
-    for i in range(3):
-        step(args.warmup + args.steps + i, stage_next=i < 2)  # nothing left staged
-    torch.cuda.synchronize(dev)
-    stats = {k: eng.kernel_stats(k) for k in names}
-    info = eng.info()
     eng.timing_enable(False)
+    step(first + args.steps, stage_next=False)  # bins the batch the last timed step staged
 
     # end-to-end (PCIe-inclusive) leg, reported beside `value`: the same
     # messages as host arrays, staged through lde_stage (copy into the pinned
@@ -458,6 +463,37 @@ def main():
         result['check'] = {
             'current_total': chk.current_total,
             'bit_exact_vs_oracle': result['cpu_baseline']['parity']['bit_exact'],
+        }
+    elif rank == 0 and world == 1 and coord is not None:
+        # wavelength parity leg: a step over the first `check_msgs` messages
+        # of the batch, its full current histogram against the NumPy oracle
+        # (pixel Ltotal -> bilinear table lookup -> hist on the wavelength
+        # edges, oracle.scipp_semantics.wavelength_mode) on the same events
+        from oracle import scipp_semantics as ora
+
+        d, tab, lt = coord
+        check_msgs = max(1, min(args.pulses, -(-20_000_000 // n_pulse)))
+        r_chk = (args.warmup + args.steps + 3) % view.n_replicas
+        eng.stage_tensors_batch(messages[:check_msgs])
+        eng.accumulate(r_chk)
+        chk = eng.finalize(hists=True)
+        n_chk = check_msgs * n_pulse
+        ps = ora.geometric_pixel_screen(inst.coords, inst.resolution, flip_x=args.workload == 'loki')
+        o = ora.OracleDetectorView(
+            detector_number=inst.detector_number, pixel_screen=ps,
+            screen_shape=tuple(view.screen_shape), toa_edges_ns=edges,
+            coordinate=ora.wavelength_mode(lt, tab.table, tab.distance0, tab.distance_step,
+                                           tab.time0, tab.time_step))
+        t_c = time.perf_counter()
+        ref = o.batch_histogram(pid[:n_chk].cpu().numpy(), toa[:n_chk].cpu().numpy(), r_chk)
+        t_c = time.perf_counter() - t_c
+        result['check'] = {
+            'events': n_chk,
+            'current_total': chk.current_total,
+            'oracle_total': int(ref.sum()),
+            'bit_exact_vs_oracle': bool(np.array_equal(ref, chk.current_hist)),
+            'oracle': 'oracle.scipp_semantics.wavelength_mode (NumPy, 1 core)',
+            'oracle_events_per_s': n_chk / t_c,
         }
     if rank == 0:
         print(json.dumps(result), flush=True)

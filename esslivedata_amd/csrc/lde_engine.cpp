@@ -2220,38 +2220,48 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     DeviceGuard guard(h->device);
     const int T = h->T;
     HIPCALL(h, hipStreamSynchronize(h->stream));  // in-flight launches may read the old table
+    // Everything new is built and uploaded into temporaries first; the handle
+    // is changed only once every allocation and copy succeeded, so a failure
+    // leaves it binning exactly as before (no half-switched tables, no freed
+    // buffers still referenced by cargs).
+    struct Staged {
+        unsigned char *tab = nullptr;
+        uint32_t *ttab = nullptr;
+        double *cpd = nullptr, *ctable = nullptr, *cedges = nullptr;
+        uint16_t *cbuck = nullptr;
+        ~Staged() {  // whatever was not committed
+            dev_free(tab);
+            dev_free(ttab);
+            dev_free(cpd);
+            dev_free(ctable);
+            dev_free(cedges);
+            dev_free(cbuck);
+        }
+    } st;
+    lde::ToaParams tp = h->tp;
+    std::vector<uint32_t> tt;
+    int tsh = 0;
+    uint32_t tcap = 0;
+    bool sieve_fits = h->sieve_ok;
     if (!rebind) {
-    // the binning stage now sees integer bins: edges 0..T
-    std::vector<double> idx((size_t)T + 1);
-    for (int i = 0; i <= T; ++i) idx[(size_t)i] = (double)i;
-    std::vector<unsigned char> tab;
-    lde::ToaParams tp;
-    if (int rc = build_toa_tables(h, idx.data(), T, tab, tp)) return rc;
-    dev_free(h->d_tab);
-    if (int rc = dev_alloc(h, &h->d_tab, tab.size())) return rc;
-    HIPCALL(h, hipMemcpy(h->d_tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
-    h->tp = tp;
-    if (h->sieve_ok) {
-        std::vector<uint32_t> tt;
-        int tsh = 0;
-        uint32_t tcap = 0;
-        if (build_sieve_toa(tp, tab, tt, tsh, tcap) && tt.size() <= h->ttab.size()) {
-            h->ttab = std::move(tt);
-            h->ttab_shift = tsh;
-            h->ttab_cap = tcap;
-            HIPCALL(h, hipMemcpy(h->d_ttab, h->ttab.data(), h->ttab.size() * 4, hipMemcpyHostToDevice));
-        } else {
-            h->sieve_ok = false;
-            if (env_ll("LDE_VERBOSE", 0))
+        // the binning stage now sees integer bins: edges 0..T
+        std::vector<double> idx((size_t)T + 1);
+        for (int i = 0; i <= T; ++i) idx[(size_t)i] = (double)i;
+        std::vector<unsigned char> tab;
+        if (int rc = build_toa_tables(h, idx.data(), T, tab, tp)) return rc;
+        if (int rc = dev_alloc(h, &st.tab, tab.size())) return rc;
+        HIPCALL(h, hipMemcpy(st.tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
+        if (h->sieve_ok) {
+            sieve_fits = build_sieve_toa(tp, tab, tt, tsh, tcap) && tt.size() <= h->ttab.size();
+            if (sieve_fits) {
+                if (int rc = dev_alloc(h, &st.ttab, h->ttab.size())) return rc;
+                HIPCALL(h, hipMemcpy(st.ttab, tt.data(), tt.size() * 4, hipMemcpyHostToDevice));
+            } else if (env_ll("LDE_VERBOSE", 0)) {
                 fprintf(stderr, "lde coord: integer bin table does not fit the sieve (%zu > %zu words)\n",
                         tt.size(), h->ttab.size());
+            }
         }
     }
-    }
-    dev_free(h->d_cbuck);
-    dev_free(h->d_cpd);
-    dev_free(h->d_ctable);
-    dev_free(h->d_cedges);
     // bucket table over the edge range: a start candidate per bucket (the
     // kernel corrects it against the edges, so rounding never matters)
     const std::vector<double> &ed = h->edges;
@@ -2270,14 +2280,37 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
         buck[(size_t)g] = (uint16_t)std::min(std::max(b, 0), std::min(T - 1, 65535));
     }
     const size_t nt = (size_t)lut->n_dist * (size_t)lut->n_time;
-    if (int rc = dev_alloc(h, &h->d_cpd, (size_t)n_pix)) return rc;
-    if (int rc = dev_alloc(h, &h->d_ctable, nt)) return rc;
-    if (int rc = dev_alloc(h, &h->d_cedges, (size_t)T + 1)) return rc;
-    if (int rc = dev_alloc(h, &h->d_cbuck, (size_t)G)) return rc;
-    HIPCALL(h, hipMemcpy(h->d_cpd, lut->pixel_distance, (size_t)n_pix * 8, hipMemcpyHostToDevice));
-    HIPCALL(h, hipMemcpy(h->d_ctable, lut->table, nt * 8, hipMemcpyHostToDevice));
-    HIPCALL(h, hipMemcpy(h->d_cedges, ed.data(), ((size_t)T + 1) * 8, hipMemcpyHostToDevice));
-    HIPCALL(h, hipMemcpy(h->d_cbuck, buck.data(), (size_t)G * 2, hipMemcpyHostToDevice));
+    if (int rc = dev_alloc(h, &st.cpd, (size_t)n_pix)) return rc;
+    if (int rc = dev_alloc(h, &st.ctable, nt)) return rc;
+    if (int rc = dev_alloc(h, &st.cedges, (size_t)T + 1)) return rc;
+    if (int rc = dev_alloc(h, &st.cbuck, (size_t)G)) return rc;
+    HIPCALL(h, hipMemcpy(st.cpd, lut->pixel_distance, (size_t)n_pix * 8, hipMemcpyHostToDevice));
+    HIPCALL(h, hipMemcpy(st.ctable, lut->table, nt * 8, hipMemcpyHostToDevice));
+    HIPCALL(h, hipMemcpy(st.cedges, ed.data(), ((size_t)T + 1) * 8, hipMemcpyHostToDevice));
+    HIPCALL(h, hipMemcpy(st.cbuck, buck.data(), (size_t)G * 2, hipMemcpyHostToDevice));
+    // the distance cache follows the pixel distances: rebuilt from the last
+    // sampled pixel counts (into the existing cache buffers, from the new
+    // distances), else off until the next hot-set selection
+    if (h->coord_cache_built)
+        HIPCALL(h, lde::launch_coord_cache(h->d_pix_cnt, st.cpd, h->L, lde::kCoordCacheBits,
+                                           h->d_ccq, h->d_ccd, h->stream));
+    // ---- commit (no failure past this point)
+    if (!rebind) {
+        std::swap(h->d_tab, st.tab);
+        h->tp = tp;
+        if (h->sieve_ok && sieve_fits) {
+            std::swap(h->d_ttab, st.ttab);
+            h->ttab = std::move(tt);
+            h->ttab_shift = tsh;
+            h->ttab_cap = tcap;
+        } else {
+            h->sieve_ok = false;
+        }
+    }
+    std::swap(h->d_cpd, st.cpd);
+    std::swap(h->d_ctable, st.ctable);
+    std::swap(h->d_cedges, st.cedges);
+    std::swap(h->d_cbuck, st.cbuck);
     lde::CoordArgs &c = h->cargs;
     c.pid_off = h->monitor ? 0 : h->pid_off;
     c.L = (unsigned)n_pix;
@@ -2298,12 +2331,8 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     c.edges_lds = 1;
     if (lde::coord_smem(c, false, false) > lde::kCoordSmemMax) c.edges_lds = 0;  // huge T: edges from HBM
     c.cus = h->cus;
-    // the distance cache follows the pixel distances: rebuilt from the last
-    // sampled pixel counts, else off until the next hot-set selection
     c.cache_bits = 0;
     if (h->coord_cache_built) {
-        HIPCALL(h, lde::launch_coord_cache(h->d_pix_cnt, h->d_cpd, h->L, lde::kCoordCacheBits,
-                                           h->d_ccq, h->d_ccd, h->stream));
         c.cache_q = h->d_ccq;
         c.cache_d = h->d_ccd;
         c.cache_bits = lde::kCoordCacheBits;

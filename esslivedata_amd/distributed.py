@@ -151,22 +151,29 @@ class OutputReducer(_Reducer):
         import torch
 
         self.S = engine.n_screen
-        super().__init__(engine, torch.zeros(2 * self.S + 4, dtype=torch.int64, device=device),
+        # [S] current image | [S] cumulative image | [4] totals | [1] windows
+        # that held data (summed: the merged window is empty only if all were)
+        super().__init__(engine, torch.zeros(2 * self.S + 5, dtype=torch.int64, device=device),
                          dst=dst, group=group)
+        self.had_data = True  # root: any rank's window held data at the last finalize
 
-    def finalize(self):
+    def finalize(self, had_data: bool = True):
         """Collective.  On the root: (current image, cumulative image, totals)
         as numpy arrays of the engine's output dtype (float64, or float32 for
         BIFROST-like views: the exact merged counts rounded once) and a list
-        of 4 ints; elsewhere None."""
+        of 4 ints; elsewhere None.  ``had_data``: this rank accumulated since
+        its last finalize (merged into ``self.had_data`` on the root)."""
         self._before_write()
         self.engine.finalize_partials(self.buf.data_ptr())
+        self._order_after_engine()
+        self.buf[2 * self.S + 4].fill_(1 if had_data else 0)
         if not self._reduce():
             return None
         h = self._to_host()
         S = self.S
         dt = self.engine.dtype
-        return h[:S].astype(dt), h[S : 2 * S].astype(dt), [int(x) for x in h[2 * S :]]
+        self.had_data = bool(h[2 * S + 4])
+        return h[:S].astype(dt), h[S : 2 * S].astype(dt), [int(x) for x in h[2 * S : 2 * S + 4]]
 
 
 class WindowReducer(_Reducer):

@@ -65,15 +65,28 @@ class _OutputPool:
     wait): arrays over ``lde_host_alloc`` blocks, handed out again only once
     nothing but the pool references them (a caller that keeps a result keeps
     its memory; a view of it counts as a reference).  At most ``cap`` blocks,
-    beyond that finalize falls back to ordinary arrays and a copy."""
+    beyond that finalize falls back to ordinary arrays and a copy.
 
-    def __init__(self, count: int, dtype: np.dtype, cap: int = 8) -> None:
+    Ownership protocol: a caller keeps an image by keeping a Python reference
+    to it (or to a numpy view of it).  A raw address alone (``a.ctypes.data``,
+    ``__array_interface__`` consumers that keep no reference) does not keep
+    the block, and the next finalize may overwrite it.  The reference count
+    test is CPython's; on other interpreters, or with
+    ``BinningEngine(reuse_output_buffers=False)``, every finalize returns fresh
+    arrays (one host copy)."""
+
+    def __init__(self, count: int, dtype: np.dtype, cap: int = 8, reuse: bool = True) -> None:
+        import sys
+
         self._count, self._dtype, self._cap = count, np.dtype(dtype), cap
         self._arrays: list[np.ndarray] = []
+        self._reuse = bool(reuse) and sys.implementation.name == 'cpython'
 
     def take(self) -> np.ndarray:
         import sys
 
+        if not self._reuse:
+            return np.empty(self._count, dtype=self._dtype)
         for a in self._arrays:
             # references: the pool's list, this loop variable, getrefcount's argument
             if sys.getrefcount(a) <= 3:
@@ -129,6 +142,7 @@ class BinningEngine:
         toa_range: tuple[int, int] | None = None,
         device: int = 0,
         stream: int | None = None,  # hipStream_t; None/0: a torch pool stream
+        reuse_output_buffers: bool = True,
     ) -> None:
         lib = _native.lib()
         edges = np.ascontiguousarray(np.asarray(toa_edges_ns, dtype=np.float64))
@@ -192,7 +206,7 @@ class BinningEngine:
         self._device = int(device)
         self._keepalive: list = []
         self._n_groups: dict[int, int] = {}
-        self._img_pool = _OutputPool(self._S, self._dtype)
+        self._img_pool = _OutputPool(self._S, self._dtype, reuse=reuse_output_buffers)
         self._out = _native.LdeOutputs()  # reused by finalize (every field set per call)
         self._out_ref = ctypes.byref(self._out)
         sp = ctypes.c_void_p()
@@ -510,6 +524,7 @@ class BinningEngine:
             'n_tiles': nt.value,
             'events_binned': eb.value,
             'last_strategy': {0: 'monitor', 1: 'atomic', 2: 'partition', 3: 'paged', 4: 'split'}.get(ls.value, '?'),
+            'device': self._device,
         }
 
     def close(self) -> None:

@@ -1,0 +1,119 @@
+"""A detector view sharded over ranks, behind the reference's ``Workflow``
+protocol (SRC/workflows/workflow_factory.py:22-34).
+
+Event-batch sharding (SURVEY 8(e) axis 1): every rank runs its own
+``GpuDetectorViewWorkflow`` (its own engine, LUT, window and cumulative) on
+its share of the event messages.  The ranks call ``accumulate`` / ``finalize``
+/ ``clear`` in the same sequence (SPMD, one process per GPU); what must agree
+across ranks is kept in agreement by the wrapper:
+
+* **Context** (the geometry signal ``detector_transform``, ROI requests and any
+  other non-event keys) is taken from the root's ``accumulate`` call and
+  broadcast, so every rank applies a detector move -- new LUT, cumulative
+  reset (SRC/preprocessors/accumulators.py:116-131,
+  SRC/workflows/geometry_signal.py:27-51) -- before binning the same batch.
+  A rank's own context keys are ignored: with sharding the root is the one
+  context consumer.
+* **clear()** is collective: every rank drops its window and cumulative.
+* **finalize()** merges exactly: ``merge='outputs'`` RCCL-reduces every rank's
+  uint64 partial images and totals onto the root (``OutputReducer``,
+  2*S + 5 words); ``merge='window'`` reduces the windows (``WindowReducer``)
+  so the root finalizes every output a single GPU would, including ROI
+  spectra and spectrum views, which read the full histogram.  The root
+  returns the reference's output dict; other ranks return ``None``.
+
+Integer sums are order-independent, so the root's outputs are bit-identical
+to one workflow that binned every rank's events.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Iterable, Mapping
+
+from .distributed import OutputReducer, WindowReducer
+from .preprocessors import Timestamp
+from .workflows import GpuDetectorViewWorkflow
+
+
+class ShardedDetectorViewWorkflow:
+    """``Workflow`` over the ranks of ``group`` (see the module doc)."""
+
+    def __init__(self, workflow: GpuDetectorViewWorkflow, device, *, merge: str = 'outputs',
+                 root: int = 0, group=None) -> None:
+        import torch.distributed as dist
+
+        if merge not in ('outputs', 'window'):
+            raise ValueError(f"merge must be 'outputs' or 'window', got {merge!r}")
+        if merge == 'outputs' and workflow.has_grouped_outputs:
+            raise ValueError("ROI spectra and spectrum views read the full histogram: use merge='window'")
+        self._wf = workflow
+        self._group = group
+        self._root = root
+        self._rank = dist.get_rank(group)
+        self._is_root = self._rank == root
+        self._merge = merge
+        eng = workflow.engine
+        self._reducer = (OutputReducer(eng, device, dst=root, group=group) if merge == 'outputs'
+                         else WindowReducer(eng, device, dst=root, group=group))
+        self._had_data = False  # this rank accumulated events since its last finalize
+
+    @property
+    def workflow(self) -> GpuDetectorViewWorkflow:
+        return self._wf
+
+    @property
+    def is_root(self) -> bool:
+        return self._is_root
+
+    def build(self, *, context_keys: Mapping[str, Any] | None = None,
+              chain_patch_bindings: Iterable = ()) -> None:
+        self._wf.build(context_keys=context_keys, chain_patch_bindings=chain_patch_bindings)
+
+    def _broadcast_context(self, context: dict[str, Any]) -> dict[str, Any]:
+        import torch.distributed as dist
+
+        box = [context if self._is_root else None]
+        dist.broadcast_object_list(box, src=self._root, group=self._group)
+        return box[0] or {}
+
+    def accumulate(self, data: dict[str, Any], *, start_time: Timestamp,
+                   end_time: Timestamp) -> None:
+        """Collective.  ``data[source]`` holds this rank's event shard (may be
+        absent); context keys come from the root."""
+        source = self._wf.source_name
+        context = self._broadcast_context({k: v for k, v in data.items() if k != source})
+        local = dict(context)
+        if source in data:
+            local[source] = data[source]
+            self._had_data = True
+        self._wf.accumulate(local, start_time=start_time, end_time=end_time)
+
+    def finalize(self) -> dict[str, Any] | None:
+        """Collective.  The merged outputs on the root, ``None`` elsewhere."""
+        had, self._had_data = self._had_data, False
+        if self._merge == 'window':
+            root = self._reducer.reduce()
+            if not root:
+                # the window's counts moved to the root; this rank's cumulative
+                # is never published, so it is dropped with the window
+                self._wf.clear()
+                self._wf._end_window()
+                return None
+            return self._wf.finalize()
+        merged = self._reducer.finalize(had_data=had)
+        if merged is None:
+            self._wf._end_window()
+            return None
+        if not self._reducer.had_data:
+            self._wf._end_window()
+            raise ValueError('No data has been added')
+        cur, cum, totals = merged
+        return self._wf._outputs(cur, cum, totals)
+
+    def clear(self) -> None:
+        """Collective: every rank drops its window and cumulative."""
+        import torch.distributed as dist
+
+        dist.barrier(group=self._group)
+        self._wf.clear()
+        self._had_data = False

@@ -318,14 +318,20 @@ class GpuDetectorViewWorkflow:
         cur = geo.transform
         if t is None or (cur is not None and np.array_equal(np.asarray(cur), t)):
             return
-        geo.transform = t
-        view = geo.view()
+        # build and validate the moved view before anything is committed, so a
+        # rejected move leaves geometry, LUT and coordinates at the old placement
+        view = geo.view(t)
         if view.screen_shape != self._view.screen_shape or view.n_replicas != self._view.n_replicas:
             raise ValueError('a detector move cannot change the view shape')
         self._engine.set_lut(view.lut)
+        geo.transform = t
         self._view = view
         if self._wavelength:
             self._set_coordinates()  # Ltotal moved with the detector
+        if self._roi_support and any(r is not None for r in self._roi_requests.values()):
+            # the ROI masks are screen metadata of the moved projection
+            # (precompute_roi_rectangle_bounds / _polygon_masks, roi.py:31-125)
+            self._set_roi_groups()
 
     def _set_coordinates(self) -> None:
         """Per-pixel Ltotal of the current placement + the table -> engine."""
@@ -348,8 +354,10 @@ class GpuDetectorViewWorkflow:
             if wire in data:
                 self._roi_requests[name] = data[wire]
                 changed = True
-        if not changed:
-            return
+        if changed:
+            self._set_roi_groups()
+
+    def _set_roi_groups(self) -> None:
         rects = _roi.from_concatenated(self._roi_requests['roi_rectangle'])
         polys = _roi.from_concatenated(self._roi_requests['roi_polygon'])
         self._roi_index, groups = _roi.roi_groups(self._view, rects, polys)
@@ -407,18 +415,26 @@ class GpuDetectorViewWorkflow:
                 {self._spec_dim: self._toa_coord()},
             )
         res = self._engine.finalize(images=True)
+        totals = (res.current_total, res.current_in_range, res.cumulative_total,
+                  res.cumulative_in_range)
+        return self._outputs(res.current_image, res.cumulative_image, totals, extra)
+
+    def _outputs(self, current_image, cumulative_image, totals, extra=None) -> dict[str, Any]:
+        """The published outputs from the window's and the cumulative's images
+        and the four totals (current, current in range, cumulative,
+        cumulative in range); also used by the sharded workflow on the merged
+        partial outputs."""
         dt = self._engine.dtype.type
+        cur_t, cur_r, cum_t, cum_r = totals
         out = {
-            'cumulative': self._image(res.cumulative_image),
-            'current': self._image(res.current_image),
-            'counts_total': DataArray(np.asarray(dt(res.current_total)), (), 'counts'),
-            'counts_in_toa_range': DataArray(np.asarray(dt(res.current_in_range)), (), 'counts'),
-            'counts_total_cumulative': DataArray(np.asarray(dt(res.cumulative_total)), (), 'counts'),
-            'counts_in_toa_range_cumulative': DataArray(
-                np.asarray(dt(res.cumulative_in_range)), (), 'counts'
-            ),
+            'cumulative': self._image(cumulative_image),
+            'current': self._image(current_image),
+            'counts_total': DataArray(np.asarray(dt(cur_t)), (), 'counts'),
+            'counts_in_toa_range': DataArray(np.asarray(dt(cur_r)), (), 'counts'),
+            'counts_total_cumulative': DataArray(np.asarray(dt(cum_t)), (), 'counts'),
+            'counts_in_toa_range_cumulative': DataArray(np.asarray(dt(cum_r)), (), 'counts'),
         }
-        out.update(extra)
+        out.update(extra or {})
         if self._roi_support:
             out['roi_rectangle'] = self._roi_readback('roi_rectangle')
             out['roi_polygon'] = self._roi_readback('roi_polygon')
@@ -427,9 +443,23 @@ class GpuDetectorViewWorkflow:
             tt = Variable((), np.datetime64(self._end.to_ns(), 'ns'), 'ns')
             names = DETECTOR_WINDOW_OUTPUTS + (ROI_WINDOW_OUTPUTS if self._roi_support else ())
             for name in names:
-                out[name] = out[name].assign_coords(start_time=st, time=tt)
+                if name in out:
+                    out[name] = out[name].assign_coords(start_time=st, time=tt)
         self._start = self._end = None
         return out
+
+    @property
+    def source_name(self) -> str:
+        return self._source
+
+    @property
+    def has_grouped_outputs(self) -> bool:
+        """ROI spectra or a spectrum view (read from the full histograms)."""
+        return self._roi_support or self._spectrum is not None
+
+    def _end_window(self) -> None:
+        """Window bookkeeping of a finalize whose outputs are produced elsewhere."""
+        self._start = self._end = None
 
     def read_histogram(self, which: str = 'cumulative') -> DataArray:
         h = self._engine.read_histogram(which)

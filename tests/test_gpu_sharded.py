@@ -1,0 +1,246 @@
+"""The sharded detector-view workflow on real engines.
+
+Two spawned ranks share cuda:0 and talk gloo (the reducers stage device
+buffers through host copies), each running ``ShardedDetectorViewWorkflow``
+over its own ``GpuDetectorViewWorkflow`` on its shard of every batch.  Only
+rank 0 is handed the context (detector transform, ROI requests); the wrapper
+broadcasts it, so a detector move mid-run re-projects and resets the
+cumulative on both ranks in the same batch.  The root's outputs are compared
+bit-exactly with one workflow that saw every event and every context value
+(reference semantics: accumulators.py:116-131, geometry_signal.py:27-51).
+Also: a collective ``clear()``, a batch in which one rank has no events, the
+window merge with ROI spectra, and bank placement through
+``GpuDetectorViewFactory(device=...)`` driven by ``assign_banks``.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _t(ns):
+    from esslivedata_amd.preprocessors import Timestamp
+
+    return Timestamp.from_ns(ns)
+
+
+def _loki_factory(roi: bool):
+    from esslivedata_amd import synthetic
+    from esslivedata_amd.workflows import GeometricViewConfig, GpuDetectorViewFactory
+
+    inst = synthetic.loki_bank0(n_replicas=3)
+    off = inst.positions - [0.0, 0.0, 5.0]
+    fac = GpuDetectorViewFactory(
+        detector_numbers={'loki': inst.detector_number},
+        view_config=GeometricViewConfig('xy_plane', inst.resolution, pixel_noise=inst.pixel_noise),
+        positions={'loki': off}, transforms={'loki': np.array([0.0, 0.0, 5.0])})
+    return inst, fac
+
+
+def _transforms():
+    t0 = np.eye(4)
+    t0[2, 3] = 5.0
+    t1 = t0.copy()
+    c, s = np.cos(0.3), np.sin(0.3)
+    t1[:3, :3] = [[c, 0, s], [0, 1, 0], [-s, 0, c]]
+    t1[0, 3] = 0.4
+    return t0, t1
+
+
+def _rois():
+    from esslivedata_amd import roi
+
+    rects = {0: roi.RectangleROI(x=roi.Interval(-0.3, 0.2, 'm'), y=roi.Interval(-0.4, 0.3, 'm'))}
+    polys = {2: roi.PolygonROI(x=[-0.5, 0.4, 0.0], y=[-0.5, -0.3, 0.45], x_unit='m', y_unit='m')}
+    return roi.to_concatenated(rects, 'rectangle'), roi.to_concatenated(polys, 'polygon')
+
+
+def _same(a, b) -> bool:
+    if set(a) != set(b):
+        return False
+    for k in a:
+        va, vb = a[k], b[k]
+        if k in ('roi_rectangle', 'roi_polygon'):
+            continue  # request readbacks: compared by content elsewhere
+        if not np.array_equal(np.asarray(va.values), np.asarray(vb.values)):
+            return False
+        if va.dims != vb.dims or set(va.coords) != set(vb.coords):
+            return False
+    return True
+
+
+def _sharded_worker(rank, world, port, q, merge):
+    import torch
+    import torch.distributed as dist
+
+    from esslivedata_amd import synthetic
+    from esslivedata_amd.distributed import shard_bounds
+    from esslivedata_amd.sharded import ShardedDetectorViewWorkflow
+
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        roi_on = merge == 'window'
+        inst, fac = _loki_factory(roi_on)
+        aux = {'roi_rectangle': 'j/roi_rectangle', 'roi_polygon': 'j/roi_polygon'}
+        local = fac.make_workflow('loki', None, aux)
+        if not roi_on:
+            local._roi_support = False  # outputs merge: images and totals only
+        sw = ShardedDetectorViewWorkflow(local, torch.device('cuda', 0), merge=merge)
+        full = None
+        if rank == 0:
+            full = fac.make_workflow('loki', None, aux)
+            if not roi_on:
+                full._roi_support = False
+        t0, t1 = _transforms()
+        rect, poly = _rois()
+        # (transform, rank 1 gets events, clear before) per batch
+        plan = [(t0, True, False), (t0, False, False), (t1, True, False), (t1, True, True),
+                (t1, True, False)]
+        ok = True
+        for b, (tr, r1_events, clear) in enumerate(plan):
+            if clear:
+                sw.clear()
+                if full is not None:
+                    full.clear()
+            n = 400_003 + b
+            pid, toa = synthetic.uniform_events(n, 1, 802816, seed=70 + b)
+            lo, hi = shard_bounds(n, rank, world) if r1_events else ((0, n) if rank == 0 else (0, 0))
+            data = {}
+            if hi > lo:
+                data['loki'] = (pid[lo:hi], toa[lo:hi])
+            context = {'detector_transform': tr}
+            if b == 0 and roi_on:
+                context.update({aux['roi_rectangle']: rect, aux['roi_polygon']: poly})
+            if rank == 0:
+                data.update(context)
+            sw.accumulate(data, start_time=_t(b), end_time=_t(b + 1))
+            out = sw.finalize()
+            if rank == 0:
+                full.accumulate({'loki': (pid, toa), **context}, start_time=_t(b), end_time=_t(b + 1))
+                ref = full.finalize()
+                ok &= _same(out, ref)
+                ok &= float(ref['counts_total'].values) > 0
+                if roi_on:
+                    ok &= out['roi_spectra_current'].values.sum() > 0
+                # the move (batch 2) and the clear (batch 3) restart the
+                # cumulative: it equals the current image there
+                if b in (0, 2, 3):
+                    ok &= bool(np.array_equal(out['cumulative'].values, out['current'].values))
+                else:
+                    ok &= not np.array_equal(out['cumulative'].values, out['current'].values)
+            else:
+                ok &= out is None
+        q.put((rank, bool(ok)))
+    except Exception as e:  # pragma: no cover - reported through the queue
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _outputs_merge(rank, world, port, q):
+    _sharded_worker(rank, world, port, q, 'outputs')
+
+
+def _window_merge(rank, world, port, q):
+    _sharded_worker(rank, world, port, q, 'window')
+
+
+def _run(target, world=2, timeout=240):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        results = dict(q.get(timeout=timeout) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert results == {r: True for r in range(world)}, results
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu(engine_lib):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+
+
+def test_sharded_workflow_outputs_merge_with_move_and_clear():
+    _run(_outputs_merge)
+
+
+def test_sharded_workflow_window_merge_with_roi_spectra():
+    _run(_window_merge)
+
+
+def test_outputs_merge_refuses_grouped_outputs():
+    import torch
+    import torch.distributed as dist
+
+    from esslivedata_amd.sharded import ShardedDetectorViewWorkflow
+
+    inst, fac = _loki_factory(True)
+    wf = fac.make_workflow('loki')  # geometric views support ROIs
+    if not dist.is_initialized():
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()))
+        dist.init_process_group('gloo', rank=0, world_size=1)
+    try:
+        with pytest.raises(ValueError, match='window'):
+            ShardedDetectorViewWorkflow(wf, torch.device('cuda', 0), merge='outputs')
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bank_placement_through_factory_devices():
+    """SURVEY 8(e) axis 2: LOKI-like banks placed whole on devices by
+    ``assign_banks`` (no collective), each bank's workflow created on its
+    device through ``GpuDetectorViewFactory(device=...)``; every bank's image
+    matches the oracle."""
+    import torch
+
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.distributed import assign_banks
+    from esslivedata_amd.workflows import GpuDetectorViewFactory, LogicalViewConfig
+    from oracle import scipp_semantics as ora
+
+    n_dev = torch.cuda.device_count()
+    sizes = {f'loki_detector_{i}': (9 - i) * 4096 for i in range(9)}
+    placement = assign_banks(sizes, n_dev)
+    first = 1
+    for bank, size in sizes.items():
+        dn = np.arange(first, first + size, dtype=np.int32).reshape(-1, 64)
+        first += size
+        fac = GpuDetectorViewFactory(detector_numbers={bank: dn}, view_config=LogicalViewConfig(),
+                                     device=placement[bank])
+        wf = fac.make_workflow(bank)
+        assert wf.engine.info()['device'] == placement[bank]
+        pid, toa = synthetic.uniform_events(50_000, int(dn.min()) - 10, int(dn.max()) + 10, seed=size)
+        wf.accumulate({bank: (pid, toa)}, start_time=_t(0), end_time=_t(1))
+        out = wf.finalize()
+        v = projection.logical_lut(dn)
+        exp = ora.detector_histogram(v.lut[0], v.n_screen, ora.pixel_index(pid, dn), toa,
+                                     synthetic.TOAEdges().edges_ns()).sum(-1).reshape(dn.shape)
+        np.testing.assert_array_equal(out['current'].values, exp)

@@ -360,3 +360,85 @@ def test_monitor_workflow_histogram_mode_rebin():
         out = wf.finalize()
         np.testing.assert_allclose(out['current'].values, exp, rtol=1e-12, atol=1e-9)
     np.testing.assert_allclose(out['cumulative'].values, cum, rtol=1e-12, atol=1e-9)
+
+
+def test_roi_spectra_follow_a_detector_move():
+    """after a detector move the ROI masks are recomputed on the
+    moved projection (the reference's roi.py:31-125 providers depend on the
+    rebuilt ScreenMetadata), so physical-unit rectangles and polygons select
+    the moved screen cells."""
+    from esslivedata_amd import geometry, roi, synthetic
+    from esslivedata_amd.workflows import GeometricViewConfig, GpuDetectorViewFactory
+
+    inst = synthetic.loki_bank0(n_replicas=1)
+    off = inst.positions - [0.0, 0.0, 5.0]
+    res = inst.resolution
+    fac = GpuDetectorViewFactory(
+        detector_numbers={'loki': inst.detector_number},
+        view_config=GeometricViewConfig('xy_plane', res),
+        positions={'loki': off}, transforms={'loki': np.array([0.0, 0.0, 5.0])})
+    aux = {'roi_rectangle': 'j/roi_rectangle', 'roi_polygon': 'j/roi_polygon'}
+    wf = fac.make_workflow('loki', None, aux)
+    rects = {0: roi.RectangleROI(x=roi.Interval(-0.2, 0.3, 'm'), y=roi.Interval(-0.4, 0.1, 'm')),
+             3: roi.RectangleROI(x=roi.Interval(-0.6, -0.1, 'm'), y=roi.Interval(0.0, 0.5, 'm'))}
+    polys = {1: roi.PolygonROI(x=[-0.5, 0.4, 0.0], y=[-0.5, -0.3, 0.45], x_unit='m', y_unit='m')}
+    t0 = np.eye(4)
+    t0[2, 3] = 5.0
+    t1 = t0.copy()
+    t1[0, 3] = 0.35  # shifted in x: the screen edges and the ROI cells move
+    t1[1, 3] = -0.1
+    edges = inst.edges.edges_ns()
+    pid, toa = synthetic.uniform_events(1_000_000, 1, 802816, seed=21)
+    for step, tr in enumerate([t0, t1, t1]):
+        data = {'loki': (pid, toa), 'detector_transform': tr}
+        if step == 0:
+            data[aux['roi_rectangle']] = roi.to_concatenated(rects, 'rectangle')
+            data[aux['roi_polygon']] = roi.to_concatenated(polys, 'polygon')
+        wf.accumulate(data, start_time=_ts(step), end_time=_ts(step + 1))
+        out = wf.finalize()
+        pos = geometry.apply_transform(tr, off)
+        coords = geometry.make_xy_plane_coords(pos)
+        oedges = {d: ora.screen_edges(coords[d], r) for d, r in res.items()}
+        ps = ora.geometric_screen_index(coords, oedges, 0)
+        h = ora.detector_histogram(ps, 144 * 144, ora.pixel_index(pid, inst.detector_number),
+                                   toa, edges).reshape(144, 144, -1)
+        yc = 0.5 * (oedges['y'][1:] + oedges['y'][:-1])
+        xc = 0.5 * (oedges['x'][1:] + oedges['x'][:-1])
+        o_r = [((r.y.min, r.y.max, r.y.unit), (r.x.min, r.x.max, r.x.unit)) for r in rects.values()]
+        o_p = [ora.polygon_inside(p.x, p.y, xc, yc) for p in polys.values()]
+        exp = ora.roi_spectra(h, o_r, o_p, oedges['y'], oedges['x'])
+        np.testing.assert_array_equal(out['roi_spectra_current'].values, exp)
+        assert exp[0].sum() > 0 and exp[2].sum() > 0
+    # a rejected move (shape change cannot happen here; an invalid transform
+    # raising inside the projection) leaves the placement untouched
+    assert np.array_equal(wf._geometry_src.transform, t1)
+
+
+def test_output_buffers_fresh_without_reuse():
+    """``reuse_output_buffers=False`` hands out fresh images each
+    finalize (no reliance on reference counts); with reuse, a held image keeps
+    its block.  Both exact."""
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.engine import BinningEngine
+
+    inst = synthetic.dummy_panel()
+    view = projection.logical_lut(inst.detector_number)
+    edges = inst.edges.edges_ns()
+    for reuse in (True, False):
+        eng = BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                            n_screen=view.n_screen, reuse_output_buffers=reuse)
+        held = []
+        for k in range(4):
+            pid, toa = synthetic.fake_detector_events(50_000, 1, 16384, seed=k)
+            eng.stage(pid, toa)
+            eng.accumulate(0)
+            res = eng.finalize(images=True)
+            exp = ora.detector_histogram(view.lut[0], view.n_screen,
+                                         ora.pixel_index(pid, inst.detector_number), toa, edges).sum(-1)
+            np.testing.assert_array_equal(res.current_image, exp)
+            held.append((res.current_image, exp.copy()))
+        for img, exp in held:  # earlier results were not overwritten
+            np.testing.assert_array_equal(img, exp)
+        if not reuse:
+            assert len({id(i) for i, _ in held}) == 4
+        eng.close()
