@@ -189,6 +189,185 @@ __global__ __launch_bounds__(1024) void k_event_coord(CoordArgs a, const int *__
     }
 }
 
+// ---------------------------------------------------------------------------
+// keyed pass: coordinate bin + pixel word -> the sieve's final word per event
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_key_dist(const uint32_t *__restrict__ tab, int cbits,
+                                                  const double *__restrict__ pix_d, unsigned L,
+                                                  double *__restrict__ tab_d) {
+    const unsigned j = blockIdx.x * 256u + threadIdx.x;
+    if (j >= (1u << cbits)) return;
+    const uint32_t w = tab[j];
+    double d = __builtin_nan("");
+    if (w & kSieveValid) {
+        const unsigned q = (((w >> kSieveTagShift) & 0xFFu) << cbits) | j;
+        if (q < L) d = pix_d[q];
+    }
+    tab_d[j] = d;
+}
+
+// LDS: pixel table (C words) | slot distances (C doubles) | edges | table | buckets
+size_t key_smem(const KeyArgs &a, bool table_lds) {
+    const size_t C = (size_t)1 << a.cbits;
+    const int ne = a.c.edges_lds ? a.c.T + 1 : 0;
+    return 12 * C + 8 * (size_t)((ne + 1) & ~1) + (table_lds ? 8 * (size_t)a.c.nd * a.c.nt : 0) +
+           2 * (size_t)a.c.G;
+}
+
+// One block per CU walks a contiguous range of the batch's global chunks;
+// thread t handles events (j * 1024 + t) * 4 + q (j < 2, q < 4) of a chunk,
+// the sieve's layout.  Per event: the pixel's table slot in LDS (a hit gives
+// its word and distance), else two gathers (word, distance; none for ids
+// outside the LUT); the coordinate bin as in k_event_coord; the word
+// (tag bits cleared) plus the bin, or 0 when the pixel or the bin is invalid.
+template <bool TLDS, bool ELDS>
+__global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
+    extern __shared__ double sm[];
+    const CoordArgs &a = k.c;
+    const uint32_t C = 1u << k.cbits;
+    uint32_t *s_w = reinterpret_cast<uint32_t *>(sm);
+    double *s_d = sm + C / 2;
+    double *s_e = s_d + C;
+    const int ne = ELDS ? a.T + 1 : 0;
+    double *s_t = s_e + ((ne + 1) & ~1);
+    const int ntab = TLDS ? a.nd * a.nt : 0;
+    uint16_t *s_b = reinterpret_cast<uint16_t *>(s_t + ntab);
+    for (uint32_t i = threadIdx.x; i < C; i += blockDim.x) {
+        s_w[i] = k.pix_tab[i];
+        s_d[i] = k.tab_d[i];
+    }
+    for (int i = threadIdx.x; i < ne; i += blockDim.x) s_e[i] = a.edges[i];
+    for (int i = threadIdx.x; i < ntab; i += blockDim.x) s_t[i] = a.table[i];
+    for (int i = threadIdx.x; i < a.G; i += blockDim.x) s_b[i] = a.buckets[i];
+    __syncthreads();
+    const double *e = ELDS ? s_e : a.edges;
+    const double *tab = TLDS ? s_t : a.table;
+    const double xmax = (double)(a.nd - 1), ymax = (double)(a.nt - 1);
+    const __amdgpu_buffer_rsrc_t drs = coord_rsrc(a.pix_d, a.L * 8u);
+    const __amdgpu_buffer_rsrc_t grs = coord_rsrc(k.glut, (a.L + 1u) * 4u);
+    const uint32_t cmask = C - 1u;
+    const uint32_t pid_off = (uint32_t)a.pid_off;
+    const uint32_t Lc = a.L;
+    auto coord = [&](double d, int t) __attribute__((always_inline)) {
+        const double x = (d - a.d0) * a.inv_dd;
+        const double y = ((double)t - a.t0) * a.inv_dt;
+        int bin = -1;
+        if (x >= 0.0 && x <= xmax && y >= 0.0 && y <= ymax) {
+            int i = (int)floor(x);
+            if (i > a.nd - 2) i = a.nd - 2;
+            int j = (int)floor(y);
+            if (j > a.nt - 2) j = a.nt - 2;
+            const double fx = x - (double)i;
+            const double fy = y - (double)j;
+            const double *r0 = tab + (size_t)i * a.nt + j;
+            const double *r1 = r0 + a.nt;
+            const double v00 = r0[0], v01 = r0[1], v10 = r1[0], v11 = r1[1];
+            const double ra = v00 + fy * (v01 - v00);
+            const double rb = v10 + fy * (v11 - v10);
+            bin = coord_bin(ra + fx * (rb - ra), e, s_b, a.T, a.e0, a.inv_w, a.G);
+        }
+        return bin;
+    };
+    const long long n = k.n_chunks;
+    const long long cb = (long long)blockIdx.x * n / gridDim.x;
+    const long long ce = ((long long)blockIdx.x + 1) * n / gridDim.x;
+    const int tid = threadIdx.x;
+    int si = 0;
+    for (long long c = cb; c < ce; ++c) {
+        if (c == cb) {
+            int lo = 0, hi = k.n_segs - 1;  // last segment with chunk0 <= c
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (k.segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+            }
+            si = lo;
+        }
+        while (si + 1 < k.n_segs && k.segs[si + 1].chunk0 <= c) ++si;
+        const SegDesc sd = k.segs[si];
+        const long long base = (c - sd.chunk0) * kChunk;
+        const bool full = ((((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0) && base + kChunk <= sd.n;
+        int p[8], t[8];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const long long e0 = base + ((long long)j * 1024 + tid) * 4;
+            if (full) {
+                const v4i pv = ld_stream4(sd.pid + e0);
+                const v4i tv = ld_stream4(sd.toa + e0);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    p[j * 4 + q] = pv[q];
+                    t[j * 4 + q] = tv[q];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool ok = e0 + q < sd.n;
+                    p[j * 4 + q] = ok ? ld_global(sd.pid + e0 + q) : a.pid_off - 1;  // dropped
+                    t[j * 4 + q] = ok ? ld_global(sd.toa + e0 + q) : 0;
+                }
+            }
+        }
+        uint32_t w[8], g[8];
+        double d[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t pq = (uint32_t)p[q] - pid_off;
+            const uint32_t slot = pq & cmask;
+            const uint32_t tw = s_w[slot];
+            const bool hit = ((tw >> kSieveTagShift) & 0xFFu) == (pq >> k.cbits);
+            // hits and ids outside the LUT load out of range (no request, 0);
+            // the word of an id outside the LUT is 0 (dropped)
+            const int goff = (hit || pq >= Lc) ? (int)0x80000000 : (int)(pq * 4u);
+            const int doff = (hit || pq >= Lc) ? (int)0x80000000 : (int)(pq * 8u);
+            g[q] = __builtin_amdgcn_raw_buffer_load_b32(grs, goff, 0, 0);
+            d[q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(drs, doff, 0, 0));
+            w[q] = hit ? (tw & (kSieveValid | kSieveHot | kSieveValueMask)) : 0u;
+            if (hit) d[q] = s_d[slot];
+        }
+        int out[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t word = w[q] | g[q];
+            const int b = (word & kSieveValid) ? coord(d[q], t[q]) : -1;
+            out[q] = b >= 0 ? (int)(word + (uint32_t)b) : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            *reinterpret_cast<int4 *>(k.keys + c * kChunk + ((long long)j * 1024 + tid) * 4) =
+                make_int4(out[j * 4], out[j * 4 + 1], out[j * 4 + 2], out[j * 4 + 3]);
+    }
+}
+
+hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix_d, unsigned L,
+                           double *tab_d, hipStream_t st) {
+    hipLaunchKernelGGL(k_key_dist, dim3(((1u << cbits) + 255) / 256), dim3(256), 0, st, pix_tab, cbits,
+                       pix_d, L, tab_d);
+    return hipGetLastError();
+}
+
+template <bool TLDS, bool ELDS>
+static void launch_key_t(const KeyArgs &a, size_t sm, int grid, hipStream_t st) {
+    (void)hipFuncSetAttribute((const void *)k_event_key<TLDS, ELDS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    hipLaunchKernelGGL((k_event_key<TLDS, ELDS>), dim3((unsigned)grid), dim3(1024), sm, st, a);
+}
+
+hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st) {
+    if (a.n_chunks <= 0) return hipSuccess;
+    const bool tl = key_smem(a, true) <= kCoordSmemMax;
+    const size_t sm = key_smem(a, tl);
+    if (sm > kCoordSmemMax) return hipErrorInvalidValue;
+    if (grid > a.n_chunks) grid = (int)a.n_chunks;
+    if (tl) {
+        if (a.c.edges_lds) launch_key_t<true, true>(a, sm, grid, st);
+        else launch_key_t<true, false>(a, sm, grid, st);
+    } else {
+        if (a.c.edges_lds) launch_key_t<false, true>(a, sm, grid, st);
+        else launch_key_t<false, false>(a, sm, grid, st);
+    }
+    return hipGetLastError();
+}
+
 size_t coord_smem(const CoordArgs &a, bool table_lds, bool cache) {
     const int ne = a.edges_lds ? a.T + 1 : 0;
     const size_t C = cache ? (size_t)1 << a.cache_bits : 0;

@@ -163,6 +163,10 @@ struct lde_handle {
     double *d_cpd = nullptr, *d_ctable = nullptr, *d_cedges = nullptr;
     int *d_cbin = nullptr;
     size_t cbin_cap = 0;
+    // keyed wavelength pass (SIEVE path): one k_event_key launch emits the
+    // sieve's finished words (LDE_COORD_KEYED, default 1)
+    bool coord_keyed = true;
+    double *d_key_dist = nullptr;  // [1 << cache_bits] distance of each pixel-table slot
     std::vector<double> edges;  // the create-time edges (event unit)
     // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
     bool lds_ctab = true, karg_segs = true;
@@ -707,10 +711,56 @@ int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     return paged_core(h, h->d_segs, (int)sd.size(), chunks, total, total, lut, nullptr);
 }
 
+// Wavelength mode, bin stream: every event's coordinate bin (k_event_coord)
+// replaces its time, contiguously in d_cbin, for the non-keyed strategies.
+int coord_prepass(lde_handle *h, std::vector<Segment> &segs) {
+    long long total = 0;
+    for (const Segment &s : segs) total += s.n;
+    if (total == 0) return LDE_OK;
+    if (int rc = grow(h, &h->d_cbin, h->cbin_cap, (size_t)total)) return rc;
+    long long off = 0;
+    Timed tm(h, LDE_K_COORD);
+    for (Segment &s : segs) {
+        HIPCALL(h, lde::launch_event_coord(h->cargs, s.pid, s.toa, s.n, h->d_cbin + off, h->stream));
+        s.toa = h->d_cbin + off;
+        off += s.n;
+    }
+    return LDE_OK;
+}
+
+int coord_prepass(lde_handle *h, std::vector<lde::SegDesc> &sd) {
+    std::vector<Segment> segs;
+    for (const lde::SegDesc &d : sd) segs.push_back({d.pid, d.toa, d.n});
+    if (int rc = coord_prepass(h, segs)) return rc;
+    for (size_t i = 0; i < sd.size(); ++i) sd[i].toa = segs[i].toa;
+    return LDE_OK;
+}
+
+int auto_strategy(const lde_handle *h, long long total) {
+    if (h->strategy != LDE_STRATEGY_AUTO) return h->strategy;
+    const long long thr = h->atomic_threshold >= 0 ? h->atomic_threshold
+                                                   : std::max<long long>(1 << 20, h->nbins / 2);
+    return (h->n_tiles > 0 && total >= thr) ? h->auto_partition : LDE_STRATEGY_ATOMIC;
+}
+
+// Wavelength mode: the coordinate pass can be deferred into the SIEVE path
+// (keyed pass) when the batch may take it; bin_segments runs the plain
+// pass for whatever does not.
+bool coord_keyed_candidate(const lde_handle *h, long long total) {
+    if (!h->coord || !h->coord_keyed || h->monitor || !h->sieve_ok || !h->split_ok || h->n_tiles == 0)
+        return false;
+    const int strat = auto_strategy(h, total);
+    return strat == LDE_STRATEGY_SPLIT ||
+           (h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED);
+}
+
 // SPLIT: hot rows of this replica in LDS, cold keys through paged_core.
 // Returns 1 (nothing launched) when AUTO should fall back to PAGED.
-int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks,
-              long long total, int replica, bool forced) {
+// coord_deferred (wavelength mode): `sd` still holds times; the sieve path
+// runs the keyed coordinate pass, the k_split path the plain one (and `sd`
+// is updated to the bin stream).
+int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
+              long long total, int replica, bool forced, bool coord_deferred) {
     // the descriptor table is uploaded lazily: the SIEVE pass of a batch of
     // at most kKargSegs messages passes it as kernel arguments instead
     if (int rc = ensure_segs_cap(h, (long long)sd.size())) return rc;  // d_segs fixed from here
@@ -853,9 +903,36 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                                                                               : std::max(1, h->cus / 2))));
         const long long max_items = ((long long)a.grid * a.cold_cap) / item_keys + h->n_tiles + 1;
         if (int rc = grow(h, &h->d_cold_items, h->cold_items_cap, (size_t)max_items)) return rc;
+        // wavelength mode: the keyed pass turns (pid, toa) into the sieve's
+        // finished words, one chunk-aligned stream (ssd) the sieve reads
+        std::vector<lde::SegDesc> ksd;
+        if (coord_deferred) {
+            if (int rc = upload()) return rc;  // k_event_key reads the messages from d_segs
+            if (int rc = grow(h, &h->d_cbin, h->cbin_cap, (size_t)chunks * lde::kChunk)) return rc;
+            if (!h->d_key_dist)
+                if (int rc = dev_alloc(h, &h->d_key_dist, (size_t)1 << h->cache_bits)) return rc;
+            const uint32_t *tab_r = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
+            Timed tm(h, LDE_K_COORD);
+            HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->d_key_dist,
+                                            h->stream));
+            lde::KeyArgs ka;
+            ka.c = h->cargs;
+            ka.segs = h->d_segs;
+            ka.n_segs = (int)sd.size();
+            ka.n_chunks = chunks;
+            ka.glut = h->d_glut + (size_t)(h->L + 1) * replica;
+            ka.pix_tab = tab_r;
+            ka.tab_d = h->d_key_dist;
+            ka.cbits = h->cache_bits;
+            ka.keys = h->d_cbin;
+            HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream));
+            ksd.push_back({h->d_cbin, h->d_cbin, chunks * lde::kChunk, 0});
+        }
+        const std::vector<lde::SegDesc> &ssd = coord_deferred ? ksd : sd;
         lde::SieveArgs sa;
+        sa.keyed = coord_deferred ? 1 : 0;
         sa.segs = h->d_segs;
-        sa.n_segs = a.n_segs;
+        sa.n_segs = (int)ssd.size();
         sa.n_chunks = chunks;
         sa.chunk_tab = h->d_chunk_tab;
         sa.glut = h->d_glut + (size_t)(h->L + 1) * replica;
@@ -903,14 +980,17 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
             // as kernel arguments when they fit too, else from d_segs
             const long long per_block = (chunks + a.grid - 1) / a.grid;
             sa.lds_ctab = per_block + 1 <= lde::kSieveLdsChunks && h->lds_ctab;
-            sa.karg = (long long)sd.size() <= lde::kKargSegs;
+            sa.karg = (long long)ssd.size() <= lde::kKargSegs;
             sa.dummy = h->d_sieve_dummy;
             if (sa.lds_ctab && sa.karg) {
-                for (size_t i = 0; i < sd.size(); ++i) sa.sk.s[i] = sd[i];
+                for (size_t i = 0; i < ssd.size(); ++i) sa.sk.s[i] = ssd[i];
             } else if (sa.lds_ctab) {
                 if (int rc = upload()) return rc;
-            } else if (!uploaded && (long long)sd.size() <= lde::kKargSegs && h->karg_segs) {
-                HIPCALL(h, lde::launch_chunk_tab_karg(sd.data(), a.n_segs, chunks, h->d_sieve_dummy,
+            } else if ((!uploaded || coord_deferred) && (long long)ssd.size() <= lde::kKargSegs &&
+                       (h->karg_segs || coord_deferred)) {
+                // (keyed: also rewrites d_segs to the key stream's descriptor,
+                // which the sieve's deferred-chunk pass reads)
+                HIPCALL(h, lde::launch_chunk_tab_karg(ssd.data(), sa.n_segs, chunks, h->d_sieve_dummy,
                                                       h->d_chunk_tab, h->d_segs, h->stream));
             } else {
                 if (int rc = upload()) return rc;
@@ -984,6 +1064,10 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         if (h->bin_stop_ext) h->bin_stop_used = true;
         return LDE_OK;
     } else {
+        if (coord_deferred) {
+            if (int rc = coord_prepass(h, sd)) return rc;
+            uploaded = false;
+        }
         if (int rc = upload()) return rc;
         Timed tm(h, LDE_K_SPLIT);
         HIPCALL(h, lde::launch_split(a, h->stream));
@@ -997,7 +1081,8 @@ int bin_split(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                       nullptr, h->d_cold_chunks);
 }
 
-int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long total, int replica) {
+int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int replica,
+                 bool coord_deferred) {
     const size_t lut_es = h->lut16 ? 2 : 4;
     const void *lut = h->monitor ? nullptr
                                  : (const void *)((const unsigned char *)h->d_lut +
@@ -1014,17 +1099,16 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
         }
         return LDE_OK;
     }
-    int strat = h->strategy;
-    if (strat == LDE_STRATEGY_AUTO) {
-        const long long thr = h->atomic_threshold >= 0
-                                  ? h->atomic_threshold
-                                  : std::max<long long>(1 << 20, h->nbins / 2);
-        strat = (h->n_tiles > 0 && total >= thr) ? h->auto_partition : LDE_STRATEGY_ATOMIC;
-    }
+    int strat = auto_strategy(h, total);
     const bool auto_split = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && h->split_ok;
     if (strat == LDE_STRATEGY_SPLIT && !h->split_ok) strat = LDE_STRATEGY_PAGED;
     if ((strat == LDE_STRATEGY_PARTITION || strat == LDE_STRATEGY_PAGED) && h->n_tiles == 0)
         strat = LDE_STRATEGY_ATOMIC;
+    if (coord_deferred && !coord_keyed_candidate(h, total)) {
+        // this piece does not take the keyed path: the plain coordinate pass
+        if (int rc = coord_prepass(h, segs)) return rc;
+        coord_deferred = false;
+    }
     h->last_strategy = strat;
     if (strat == LDE_STRATEGY_ATOMIC) {
         for (const Segment &s : segs) {
@@ -1048,10 +1132,15 @@ int bin_segments(lde_handle *h, const std::vector<Segment> &segs, long long tota
     }
     if (chunks == 0) return LDE_OK;
     if (strat == LDE_STRATEGY_SPLIT || auto_split) {
-        const int rc = bin_split(h, sd, chunks, total, replica, strat == LDE_STRATEGY_SPLIT);
+        const int rc = bin_split(h, sd, chunks, total, replica, strat == LDE_STRATEGY_SPLIT,
+                                 coord_deferred);
         if (rc != 1) {
             if (rc == LDE_OK) h->last_strategy = LDE_STRATEGY_SPLIT;
             return rc;
+        }
+        if (coord_deferred) {  // AUTO fell back to PAGED: the plain coordinate pass
+            if (int rc2 = coord_prepass(h, sd)) return rc2;
+            if (int rc2 = upload_segments(h, sd)) return rc2;
         }
         return paged_core(h, h->d_segs, (int)sd.size(), chunks, total, total, lut, nullptr);
     }
@@ -1191,6 +1280,7 @@ void release(lde_handle *h) {
     dev_free(h->d_ccq);
     dev_free(h->d_ccd);
     dev_free(h->d_cbin);
+    dev_free(h->d_key_dist);
     dev_free(h->d_win32);
     dev_free(h->d_win64);
     dev_free(h->d_cum);
@@ -1603,6 +1693,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
 #endif
         // exact variant: cold-key stores deferred behind the next gathers
         if (env_ll("LDE_DEFER_STORES", 0) != 0) h->sieve_ablate |= 2048;
+        h->coord_keyed = env_ll("LDE_COORD_KEYED", 1) != 0;
         h->early_gather = env_ll("LDE_EARLY_GATHER", 0) != 0;
         h->probe = env_ll("LDE_HOST_PROBE", 0) != 0;
         h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
@@ -1790,18 +1881,12 @@ int lde_accumulate(lde_handle *h, int32_t replica) {
     for (const Segment &s : h->dev_segments) segs.push_back(s);
     long long total = 0;
     for (const Segment &s : segs) total += s.n;
-    if (h->coord && total > 0) {
-        // wavelength mode: every event's coordinate bin replaces its time as
-        // the value binned against the integer edges 0..T
-        if (int rc = grow(h, &h->d_cbin, h->cbin_cap, (size_t)total)) return rc;
-        long long off = 0;
-        Timed tm(h, LDE_K_COORD);
-        for (Segment &s : segs) {
-            HIPCALL(h, lde::launch_event_coord(h->cargs, s.pid, s.toa, s.n, h->d_cbin + off, h->stream));
-            s.toa = h->d_cbin + off;
-            off += s.n;
-        }
-    }
+    // wavelength mode: every event's coordinate bin replaces its time as the
+    // value binned against the integer edges 0..T -- computed here, or inside
+    // the SIEVE path by the keyed pass (coord_deferred)
+    const bool coord_deferred = h->coord && total > 0 && coord_keyed_candidate(h, total);
+    if (h->coord && total > 0 && !coord_deferred)
+        if (int rc = coord_prepass(h, segs)) return rc;
 
     // split into pieces that cannot overflow a u32 window bin
     const long long piece_max = 1LL << 31;
@@ -1863,7 +1948,7 @@ int lde_accumulate(lde_handle *h, int32_t replica) {
                 h->win64_dirty = true;
                 h->win_events = 0;
             }
-            if (int rc = bin_segments(h, p, n, replica)) return rc;
+            if (int rc = bin_segments(h, p, n, replica, coord_deferred)) return rc;
             h->win_events += (unsigned long long)n;
         }
     }

@@ -218,6 +218,7 @@ struct SieveArgs {
     uint32_t *hot_fmt = nullptr;  // [grid] 1: the block's hot rows left as u16 (null: u32)
     unsigned long long *trace = nullptr;  // diagnostic [grid][3]: start, stream end, end (realtime)
     int tail_release = 0;  // each block ends with an agent-scope release (L2 writeback of its stores)
+    int keyed = 0;  // the 'toa' stream holds finished pixel words (k_event_key): no probe/gather/TOA
 };
 size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a
@@ -339,6 +340,29 @@ hipError_t launch_coord_cache(const uint32_t *pix_cnt, const double *pix_d, long
                               uint32_t *cq, double *cd, hipStream_t st);
 hipError_t launch_event_coord(const CoordArgs &a, const int *pid, const int *toa, long long n,
                               int *out, hipStream_t st);
+
+// Wavelength mode on the SIEVE path: one pass over the batch that computes
+// each event's coordinate bin AND looks up its pixel word, emitting the
+// sieve's final word (valid | hot | row*T + bin or screen*T + bin; 0 =
+// dropped) per event, chunk-aligned (entry c * kChunk + i of global chunk c,
+// unused tail entries 0).  The keyed sieve (launch_sieve with keyed = 1) then
+// reads 4 bytes per event and does no table probe, gather or TOA lookup.
+struct KeyArgs {
+    CoordArgs c;              // coordinate arithmetic (its cache fields unused)
+    const SegDesc *segs;      // the batch's messages (device table)
+    int n_segs;
+    long long n_chunks;
+    const uint32_t *glut;     // this replica's pixel words, L + 1 entries (entry L = 0)
+    const uint32_t *pix_tab;  // this replica's LDS pixel-table image (1 << cbits words)
+    const double *tab_d;      // distance of each table slot's pixel (1 << cbits)
+    int cbits;
+    int *keys;                // [n_chunks * kChunk]
+};
+size_t key_smem(const KeyArgs &a, bool table_lds);
+hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st);
+// distance of every pixel-table slot's pixel (NaN for empty slots)
+hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix_d, unsigned L,
+                           double *tab_d, hipStream_t st);
 
 hipError_t launch_rebin_f64(const double *se, const double *sv, long long ns, const double *de,
                             long long nd, double *out_a, double *out_b, hipStream_t st);

@@ -49,6 +49,7 @@ constexpr uint32_t kOOBi = 0xFFFFFFF0u;       // same, as an inline constant (-1
 constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data format
 constexpr int kEPT = kSplitEPT;               // 8 events per thread per chunk
 constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (half a chunk)
+constexpr int kSieveKeyed = 262144;           // mode bit: the stream holds finished words
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
@@ -335,6 +336,15 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
 #pragma unroll
         for (int j = 0; j < kEPT / 4; ++j) {
             const int off = (j * kSplitThreads + tid) * 4;
+            if (ABL & kSieveKeyed) {  // finished words only (k_event_key)
+                const v4i tv = ld_stream4(tq + off);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    p[j * 4 + q] = 0;
+                    t[j * 4 + q] = tv[q];
+                }
+                continue;
+            }
             const v4i pv = (ABL & 8192) ? *(const g_v4i *)(pp + off) : ld_stream4(pp + off);
             const v4i tv = (ABL & 8192) ? *(const g_v4i *)(tq + off) : ld_stream4(tq + off);
 #pragma unroll
@@ -351,6 +361,11 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                      __attribute__((always_inline)) {
 #pragma unroll
         for (int e = 0; e < kEPT; ++e) {
+            if (ABL & kSieveKeyed) {  // the word is the event: nothing to look up
+                qs[e] = (uint32_t)t[e];
+                w[e] = dc[e] = tw[e] = 0u;
+                continue;
+            }
             const uint32_t q = (uint32_t)p[e] - pid_off;
             qs[e] = q;
             const uint32_t d = min((uint32_t)t[e] - toa_lo, toa_cap);
@@ -372,6 +387,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // have tag 0), so dc / tw die here and bin() reads one word per event
     auto finish = [&](uint32_t (&w)[kEPT], uint32_t (&qs)[kEPT], const uint32_t (&dc)[kEPT],
                       const uint32_t (&tw)[kEPT]) __attribute__((always_inline)) {
+        if (ABL & kSieveKeyed) return;
 #pragma unroll
         for (int e = 0; e < kEPT; ++e) {
             const unsigned long long hit =
@@ -420,8 +436,9 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                     for (int x = 0; x < 8; ++x) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(junk) : "v"(v));
                 }
                 if (ABL & 1024) junk += lds_at(sm, dum4 ^ ((v & 1u) << 2));
-                const uint32_t b = (ABL & 65536) ? ((v >> kSieveTagShift) & 0xFFu)
-                                                 : (tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u);
+                const uint32_t b = (ABL & kSieveKeyed) ? 0u
+                                   : (ABL & 65536) ? ((v >> kSieveTagShift) & 0xFFu)
+                                                   : (tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u);
                 const uint32_t fl = v >> 30;
                 // hot rows start at LDS byte 0, so the scaled key is the hot
                 // counter's address; cold keys leave scaled by 4 as well
@@ -1500,7 +1517,8 @@ static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, h
 
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                         hipEvent_t stop) {
-    const int mode = a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0);
+    const int mode = a.keyed ? kSieveKeyed
+                             : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0);
     switch (mode) {
 #define LDE_SIEVE_MODE(m) \
     case m: return launch_sieve_t<m>(a, grid, st, start, stop);
@@ -1508,6 +1526,7 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     // the packed table word (65536)
     LDE_SIEVE_MODE(0) LDE_SIEVE_MODE(256) LDE_SIEVE_MODE(2048) LDE_SIEVE_MODE(65536)
     LDE_SIEVE_MODE(65536 | 256) LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048)
+    LDE_SIEVE_MODE(kSieveKeyed)
 #ifdef LDE_DIAGNOSTICS
     // timing probes (wrong results), diagnostics build only
     LDE_SIEVE_MODE(1) LDE_SIEVE_MODE(2) LDE_SIEVE_MODE(4) LDE_SIEVE_MODE(6)

@@ -101,4 +101,5 @@ def test_product_library_has_only_exact_sieve_variants():
     out = subprocess.run(['nm', '-C', str(lib)], capture_output=True, text=True).stdout
     modes = {int(m) for m in re.findall(r'lde::k_sieve<(\d+), \d>\(', out)}
     assert 0 in modes
-    assert modes <= {0, 256, 2048, 65536, 65536 | 256, 65536 | 2048, 65536 | 256 | 2048}, modes
+    # the exact variants, and the keyed wavelength pass (262144)
+    assert modes <= {0, 256, 2048, 65536, 65536 | 256, 65536 | 2048, 65536 | 256 | 2048, 262144}, modes
