@@ -9,11 +9,14 @@ across ranks is kept in agreement by the wrapper:
 
 * **Context** (the geometry signal ``detector_transform``, ROI requests and any
   other non-event keys) is taken from the root's ``accumulate`` call and
-  broadcast, so every rank applies a detector move -- new LUT, cumulative
-  reset (SRC/preprocessors/accumulators.py:116-131,
-  SRC/workflows/geometry_signal.py:27-51) -- before binning the same batch.
-  A rank's own context keys are ignored: with sharding the root is the one
-  context consumer.
+  shared in one small collective per batch, so every rank applies a detector
+  move -- new LUT, cumulative reset (SRC/preprocessors/accumulators.py:
+  116-131, SRC/workflows/geometry_signal.py:27-51) -- before binning the same
+  batch.  A rank's own context keys are ignored: with sharding the root is
+  the one context consumer.  The same collective tells every rank whether
+  any rank has events in the batch, so the noise-replica cycle (one replica
+  per batch, projectors.py:105-113) stays aligned when a rank's shard is
+  empty.
 * **clear()** is collective: every rank drops its window and cumulative.
 * **finalize()** merges exactly: ``merge='outputs'`` RCCL-reduces every rank's
   uint64 partial images and totals onto the root (``OutputReducer``,
@@ -69,24 +72,32 @@ class ShardedDetectorViewWorkflow:
               chain_patch_bindings: Iterable = ()) -> None:
         self._wf.build(context_keys=context_keys, chain_patch_bindings=chain_patch_bindings)
 
-    def _broadcast_context(self, context: dict[str, Any]) -> dict[str, Any]:
+    def _exchange(self, context: dict[str, Any], has_events: bool) -> tuple[dict[str, Any], bool]:
+        """One collective: the root's context and whether any rank has
+        events in this batch (the replica cycle advances once per batch with
+        events, projectors.py:105-113, on every rank alike)."""
         import torch.distributed as dist
 
-        box = [context if self._is_root else None]
-        dist.broadcast_object_list(box, src=self._root, group=self._group)
-        return box[0] or {}
+        world = dist.get_world_size(self._group)
+        box: list = [None] * world
+        dist.all_gather_object(box, (context if self._is_root else None, bool(has_events)),
+                               group=self._group)
+        root_index = dist.get_group_rank(self._group, self._root) if self._group is not None \
+            else self._root
+        return box[root_index][0] or {}, any(h for _, h in box)
 
     def accumulate(self, data: dict[str, Any], *, start_time: Timestamp,
                    end_time: Timestamp) -> None:
         """Collective.  ``data[source]`` holds this rank's event shard (may be
         absent); context keys come from the root."""
         source = self._wf.source_name
-        context = self._broadcast_context({k: v for k, v in data.items() if k != source})
+        context, any_events = self._exchange({k: v for k, v in data.items() if k != source},
+                                             source in data)
         local = dict(context)
         if source in data:
             local[source] = data[source]
             self._had_data = True
-        self._wf.accumulate(local, start_time=start_time, end_time=end_time)
+        self._wf._accumulate(local, start_time, end_time, batch_has_events=any_events)
 
     def finalize(self) -> dict[str, Any] | None:
         """Collective.  The merged outputs on the root, ``None`` elsewhere."""

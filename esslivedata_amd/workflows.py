@@ -290,6 +290,12 @@ class GpuDetectorViewWorkflow:
 
     def accumulate(self, data: dict[str, Any], *, start_time: Timestamp,
                    end_time: Timestamp) -> None:
+        self._accumulate(data, start_time, end_time)
+
+    def _accumulate(self, data: Mapping[str, Any], start_time: Timestamp, end_time: Timestamp,
+                    batch_has_events: bool = False) -> None:
+        """``batch_has_events``: another rank binned events of this batch (the
+        sharded workflow), so the replica cycle advances here too."""
         if self._start is None:
             self._start = start_time
         self._end = end_time
@@ -300,6 +306,8 @@ class GpuDetectorViewWorkflow:
         if self._roi_support:
             self._update_rois(data)
         if self._source not in data:
+            if batch_has_events:
+                self._counter += 1  # one replica per batch (projectors.py:105-113)
             return
         toas, pids = _events_of(data[self._source])
         if pids is None:

@@ -132,19 +132,27 @@ def _sharded_worker(rank, world, port, q, merge):
             if rank == 0:
                 full.accumulate({'loki': (pid, toa), **context}, start_time=_t(b), end_time=_t(b + 1))
                 ref = full.finalize()
-                ok &= _same(out, ref)
-                ok &= float(ref['counts_total'].values) > 0
-                if roi_on:
-                    ok &= out['roi_spectra_current'].values.sum() > 0
+                why = []
+                if not _same(out, ref):
+                    why.append('outputs differ from one workflow: ' + ', '.join(
+                        k for k in ref if k in out and not np.array_equal(
+                            np.asarray(out[k].values), np.asarray(ref[k].values))))
+                if not float(ref['counts_total'].values) > 0:
+                    why.append('no counts')
+                if roi_on and not out['roi_spectra_current'].values.sum() > 0:
+                    why.append('empty ROI spectra')
                 # the move (batch 2) and the clear (batch 3) restart the
                 # cumulative: it equals the current image there
-                if b in (0, 2, 3):
-                    ok &= bool(np.array_equal(out['cumulative'].values, out['current'].values))
-                else:
-                    ok &= not np.array_equal(out['cumulative'].values, out['current'].values)
-            else:
-                ok &= out is None
-        q.put((rank, bool(ok)))
+                same_cc = bool(np.array_equal(out['cumulative'].values, out['current'].values))
+                if same_cc != (b in (0, 2, 3)):
+                    why.append('cumulative restart')
+                if why:
+                    ok = f'batch {b}: ' + '; '.join(why)
+                    break
+            elif out is not None:
+                ok = 'non-root returned outputs'
+                break
+        q.put((rank, ok))
     except Exception as e:  # pragma: no cover - reported through the queue
         import traceback
 
