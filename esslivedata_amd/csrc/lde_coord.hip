@@ -273,20 +273,21 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     const long long ce = ((long long)blockIdx.x + 1) * n / gridDim.x;
     const int tid = threadIdx.x;
     int si = 0;
-    for (long long c = cb; c < ce; ++c) {
-        if (c == cb) {
-            int lo = 0, hi = k.n_segs - 1;  // last segment with chunk0 <= c
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (k.segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
-            }
-            si = lo;
+    if (cb < ce) {
+        int lo = 0, hi = k.n_segs - 1;  // last segment with chunk0 <= cb
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (k.segs[mid].chunk0 <= cb) lo = mid; else hi = mid - 1;
         }
+        si = lo;
+    }
+    // chunk c's events (8 per lane, the sieve's layout); events past a
+    // message's end read as a dropped id
+    auto fetch = [&](long long c, int (&p)[8], int (&t)[8]) __attribute__((always_inline)) {
         while (si + 1 < k.n_segs && k.segs[si + 1].chunk0 <= c) ++si;
         const SegDesc sd = k.segs[si];
         const long long base = (c - sd.chunk0) * kChunk;
         const bool full = ((((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0) && base + kChunk <= sd.n;
-        int p[8], t[8];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const long long e0 = base + ((long long)j * 1024 + tid) * 4;
@@ -307,28 +308,40 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
                 }
             }
         }
-        uint32_t w[8], g[8];
+    };
+    // Per chunk: probe the LDS table, issue the misses' gathers, then the
+    // next chunk's loads, then the arithmetic -- vmcnt is in order, so the
+    // wait for the gathers leaves the next chunk's loads in flight.
+    int p[8], t[8];
+    if (cb < ce) fetch(cb, p, t);
+    for (long long c = cb; c < ce; ++c) {
+        uint32_t w[8], g[8], slot[8];
         double d[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const uint32_t pq = (uint32_t)p[q] - pid_off;
-            const uint32_t slot = pq & cmask;
-            const uint32_t tw = s_w[slot];
+            slot[q] = pq & cmask;
+            const uint32_t tw = s_w[slot[q]];
             const bool hit = ((tw >> kSieveTagShift) & 0xFFu) == (pq >> k.cbits);
             // hits and ids outside the LUT load out of range (no request, 0);
             // the word of an id outside the LUT is 0 (dropped)
-            const int goff = (hit || pq >= Lc) ? (int)0x80000000 : (int)(pq * 4u);
-            const int doff = (hit || pq >= Lc) ? (int)0x80000000 : (int)(pq * 8u);
-            g[q] = __builtin_amdgcn_raw_buffer_load_b32(grs, goff, 0, 0);
-            d[q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(drs, doff, 0, 0));
+            const bool skip = hit || pq >= Lc;
+            g[q] = __builtin_amdgcn_raw_buffer_load_b32(grs, skip ? (int)0x80000000 : (int)(pq * 4u), 0, 0);
+            d[q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                  drs, skip ? (int)0x80000000 : (int)(pq * 8u), 0, 0));
             w[q] = hit ? (tw & (kSieveValid | kSieveHot | kSieveValueMask)) : 0u;
-            if (hit) d[q] = s_d[slot];
+            slot[q] = hit ? slot[q] : 0xFFFFFFFFu;
         }
+        int tc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tc[q] = t[q];
+        if (c + 1 < ce) fetch(c + 1, p, t);
         int out[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
+            const double dq = slot[q] != 0xFFFFFFFFu ? s_d[slot[q]] : d[q];
             const uint32_t word = w[q] | g[q];
-            const int b = (word & kSieveValid) ? coord(d[q], t[q]) : -1;
+            const int b = (word & kSieveValid) ? coord(dq, tc[q]) : -1;
             out[q] = b >= 0 ? (int)(word + (uint32_t)b) : 0;
         }
 #pragma unroll

@@ -7,7 +7,7 @@ out=gpurun_out/knob_sweep.log
 while read -r line; do
   [ -z "$line" ] && continue
   echo "== $line" >> $out
-  env $line timeout -k 10 120 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --e2e-steps 0 > gpurun_out/ks_one.log 2>&1
+  env $line timeout -k 10 120 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --e2e-steps 0 ${BENCH_ARGS} > gpurun_out/ks_one.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "rc=$rc" >> $out; tail -5 gpurun_out/ks_one.log >> $out; exit $rc; fi
   python - gpurun_out/ks_one.log >> $out <<'PY'
