@@ -47,6 +47,8 @@ KERNEL_SYMBOL = {
 # k_cold_plan, k_cold_sort, k_cold_accumulate)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_EVENT = 8  # int32 pixel_id + int32 time_of_flight
+# the wavelength-mode coordinate pass also writes its 4-byte per-event word
+KERNEL_BYTES_PER_EVENT = {'coord': 12}
 
 
 def parse():
@@ -61,6 +63,10 @@ def parse():
     ap.add_argument('--pulses', type=int, default=14)
     ap.add_argument('--events-per-pulse', type=int, default=10_000_000)
     ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition', 'paged', 'split'])
+    ap.add_argument('--view', default='geometric',
+                    choices=['geometric', 'mantle_front_layer', 'wire_view', 'strip_view'],
+                    help='DREAM logical views (dream/specs.py:151-180) instead of the '
+                         'cylinder_mantle_z projection (diagnostic lines, not the headline)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--timing-stride', type=int, default=5,
@@ -197,9 +203,17 @@ def main():
     from esslivedata_amd.engine import BinningEngine
 
     inst = synthetic.dream_mantle() if args.workload == 'dream' else synthetic.loki_bank0()
-    view = projection.geometric_lut(
-        inst.detector_number, inst.coords, inst.resolution, flip_x=args.workload == 'loki'
-    )
+    if args.view != 'geometric':
+        if args.workload != 'dream' or args.coordinate != 'toa':
+            raise SystemExit('--view: DREAM mantle logical views, TOA mode')
+        cfg = synthetic.dream_logical_views()[args.view]
+        view = projection.logical_lut(inst.detector_number,
+                                      transform=lambda a: cfg.transform(a, 'mantle_detector'),
+                                      reduction_dim=cfg.reduction_dim)
+    else:
+        view = projection.geometric_lut(
+            inst.detector_number, inst.coords, inst.resolution, flip_x=args.workload == 'loki'
+        )
     edges = inst.edges.edges_ns()
     coord = None
     if args.coordinate == 'wavelength':
@@ -384,7 +398,7 @@ def main():
     ms, launches = timed[dom]
     # every binning kernel processes all events of the timed steps across its launches
     events_per_launch = n_step * len(sampled) / max(launches, 1)
-    alg_bytes = BYTES_PER_EVENT * events_per_launch
+    alg_bytes = KERNEL_BYTES_PER_EVENT.get(dom, BYTES_PER_EVENT) * events_per_launch
     avg_s = (ms / max(launches, 1)) / 1e3
     achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
     traffic = profiled_traffic(args.workload, dom)
@@ -405,7 +419,9 @@ def main():
         'dtype': 'int32',
         'data': 'synthetic (seeded ev44-shaped streams generated in HBM; no recorded data offline)',
         'config': {
-            'workload': 'dream_mantle_cylinder_mantle_z' if args.workload == 'dream' else 'loki_bank0_xy_plane',
+            'workload': ('dream_mantle_cylinder_mantle_z' if args.workload == 'dream'
+                         else 'loki_bank0_xy_plane') if args.view == 'geometric'
+                        else f'dream_mantle_{args.view}',
             'coordinate': args.coordinate,
             'pixels': int(inst.detector_number.size),
             'screen': list(view.screen_shape),
@@ -457,7 +473,14 @@ def main():
         eng.stage_tensors_batch(messages)
         eng.accumulate(r_chk)
         chk = eng.finalize(hists=True)
-        ps = ora.geometric_pixel_screen(inst.coords, inst.resolution, flip_x=args.workload == 'loki')
+        if args.view == 'geometric':
+            ps = ora.geometric_pixel_screen(inst.coords, inst.resolution,
+                                            flip_x=args.workload == 'loki')
+        else:  # the oracle's closed-form view index (no transform applied)
+            spec = {'mantle_front_layer': ([('module', 'segment', 'counter'), ('strip',)], {'wire': 0}),
+                    'wire_view': ([('wire',), ('module', 'segment', 'counter')], {}),
+                    'strip_view': ([('strip',)], {})}[args.view]
+            ps = ora.folded_view_index(synthetic.DREAM_BANK_SIZES['mantle_detector'], *spec)[0][None]
         result['cpu_baseline'] = cpu_baseline(inst, ps, view, pid.cpu().numpy(), toa.cpu().numpy(),
                                               r_chk, chk.current_hist, args.cpu_baseline_seconds)
         result['check'] = {

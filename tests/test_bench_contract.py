@@ -39,10 +39,12 @@ def _check_line(d: dict, n_gpus: int = 1):
     r = d['roofline']
     assert r['bound'] == 'hbm' and r['unit'] == 'GB/s' and r['peak'] == bench.HBM_PEAK_GBS
     assert r['frac'] == pytest.approx(r['achieved'] / r['peak'], rel=1e-12)
-    # achieved = 8 algorithmic bytes per event of one launch / its average time
+    # achieved = algorithmic bytes per event (8; 12 for the coordinate pass,
+    # which also writes its word) of one launch / its average time
     events_per_launch = cfg['events_per_step'] * r.get('timed_steps', d['steps']) / r['launches']
+    bpe = bench.KERNEL_BYTES_PER_EVENT.get(r['kernel'], bench.BYTES_PER_EVENT)
     assert r['achieved'] == pytest.approx(
-        bench.BYTES_PER_EVENT * events_per_launch / (r['avg_launch_ms'] / 1e3) / 1e9, rel=1e-9)
+        bpe * events_per_launch / (r['avg_launch_ms'] / 1e3) / 1e9, rel=1e-9)
     assert 0.0 < r['frac'] < 1.0
     assert 0.0 < r['step_frac'] <= r['pipeline_frac'] * 1.2
 
