@@ -29,7 +29,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-PROFILE_ROUND = 'r2'  # profiles/<round>_<workload>_bench.json (tools/prof_round.sh)
+PROFILE_ROUND = 'r3'  # profiles/<round>_<workload>_bench.json (tools/prof_round.sh)
 # bench kernel name -> device symbol in the rocprofv3 summary
 KERNEL_SYMBOL = {
     'atomic': 'k_bin_atomic',
@@ -401,7 +401,9 @@ def main():
     alg_bytes = KERNEL_BYTES_PER_EVENT.get(dom, BYTES_PER_EVENT) * events_per_launch
     avg_s = (ms / max(launches, 1)) / 1e3
     achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
-    traffic = profiled_traffic(args.workload, dom)
+    prof_name = ('wavelength' if args.coordinate == 'wavelength' else
+                 args.workload if args.view == 'geometric' else args.view)
+    traffic = profiled_traffic(prof_name, dom)
     bin_ms, bin_n = stats['binning']  # the extra steps
     pipeline_gbs = BYTES_PER_EVENT * n_step / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0
 
@@ -456,7 +458,7 @@ def main():
             # (8 N + 4 S T) bytes per step over ms_per_step
             'step_achieved': step_gbs,
             'step_frac': step_gbs / HBM_PEAK_GBS,
-            'lds': profiled_lds(args.workload, dom),
+            'lds': profiled_lds(prof_name, dom),
             'kernel_ms': {k: v[0] / max(v[1], 1) for k, v in stats.items() if v[1]},
             'kernel_ms_note': 'per-kernel breakdown and pipeline_* (the whole binning sequence of '
                               'one accumulate) from 3 extra steps after the timed region',

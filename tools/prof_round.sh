@@ -5,8 +5,9 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 WL=${WL:-dream}
-TAG=${TAG:-r2}
-OUT=gpurun_out/prof_${TAG}_${WL}
+TAG=${TAG:-r3}
+NAME=${NAME:-$WL}  # profile name (e.g. wavelength with BENCH_ARGS="--coordinate wavelength")
+OUT=gpurun_out/prof_${TAG}_${NAME}
 ARGS="bench.py --workload $WL --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline --e2e-steps 0 ${BENCH_ARGS}"
 rm -rf $OUT
 mkdir -p $OUT
@@ -21,5 +22,5 @@ for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_I
   echo "pmc $pmc rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/pmc_$name.log; exit $rc; fi
 done
-python3 tools/prof_summary.py $OUT $OUT/${TAG}_${WL}_bench > $OUT/summary.log 2>&1 || { cat $OUT/summary.log; exit 1; }
+python3 tools/prof_summary.py $OUT $OUT/${TAG}_${NAME}_bench > $OUT/summary.log 2>&1 || { cat $OUT/summary.log; exit 1; }
 echo done
