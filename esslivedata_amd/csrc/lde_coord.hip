@@ -69,6 +69,8 @@ __global__ __launch_bounds__(256) void k_coord_cache(const uint32_t *__restrict_
     cd[j] = bq < 0 ? 0.0 : pix_d[bq];
 }
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t coord_rsrc(const void *p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes,
                                              (int)0x00020000);  // raw buffer, 32-bit format
@@ -243,8 +245,7 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     const double *e = ELDS ? s_e : a.edges;
     const double *tab = TLDS ? s_t : a.table;
     const double xmax = (double)(a.nd - 1), ymax = (double)(a.nt - 1);
-    const __amdgpu_buffer_rsrc_t drs = coord_rsrc(a.pix_d, a.L * 8u);
-    const __amdgpu_buffer_rsrc_t grs = coord_rsrc(k.glut, (a.L + 1u) * 4u);
+    const __amdgpu_buffer_rsrc_t rrs = coord_rsrc(k.rec, (a.L + 1u) * 16u);
     const uint32_t cmask = C - 1u;
     const uint32_t pid_off = (uint32_t)a.pid_off;
     const uint32_t Lc = a.L;
@@ -326,9 +327,10 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
             // hits and ids outside the LUT load out of range (no request, 0);
             // the word of an id outside the LUT is 0 (dropped)
             const bool skip = hit || pq >= Lc;
-            g[q] = __builtin_amdgcn_raw_buffer_load_b32(grs, skip ? (int)0x80000000 : (int)(pq * 4u), 0, 0);
-            d[q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                                                  drs, skip ? (int)0x80000000 : (int)(pq * 8u), 0, 0));
+            const v4u r = __builtin_amdgcn_raw_buffer_load_b128(rrs, skip ? (int)0x80000000 : (int)(pq * 16u),
+                                                                 0, 0);
+            g[q] = r[0];
+            d[q] = __builtin_bit_cast(double, ((unsigned long long)r[3] << 32) | r[2]);
             w[q] = hit ? (tw & (kSieveValid | kSieveHot | kSieveValueMask)) : 0u;
             slot[q] = hit ? slot[q] : 0xFFFFFFFFu;
         }
@@ -349,6 +351,24 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
             *reinterpret_cast<int4 *>(k.keys + c * kChunk + ((long long)j * 1024 + tid) * 4) =
                 make_int4(out[j * 4], out[j * 4 + 1], out[j * 4 + 2], out[j * 4 + 3]);
     }
+}
+
+// per pixel {word, 0, distance}: a table miss gathers one 16-byte record
+// instead of a word and a distance from two tables (entry L: word 0)
+__global__ __launch_bounds__(256) void k_key_records(const uint32_t *__restrict__ glut,
+                                                     const double *__restrict__ pix_d, unsigned L,
+                                                     uint4 *__restrict__ rec) {
+    const unsigned q = blockIdx.x * 256u + threadIdx.x;
+    if (q > L) return;
+    const double d = q < L ? pix_d[q] : __builtin_nan("");
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, d);
+    rec[q] = make_uint4(q < L ? glut[q] : 0u, 0u, (uint32_t)b, (uint32_t)(b >> 32));
+}
+
+hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, uint4 *rec,
+                              hipStream_t st) {
+    hipLaunchKernelGGL(k_key_records, dim3((L + 1u + 255u) / 256u), dim3(256), 0, st, glut, pix_d, L, rec);
+    return hipGetLastError();
 }
 
 hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix_d, unsigned L,

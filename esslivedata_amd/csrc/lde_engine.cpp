@@ -167,6 +167,7 @@ struct lde_handle {
     // sieve's finished words (LDE_COORD_KEYED, default 1)
     bool coord_keyed = true;
     double *d_key_dist = nullptr;  // [1 << cache_bits] distance of each pixel-table slot
+    uint4 *d_key_rec = nullptr;    // [L + 1] {word, 0, distance} of the batch's replica
     std::vector<double> edges;  // the create-time edges (event unit)
     // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
     bool lds_ctab = true, karg_segs = true;
@@ -915,6 +916,10 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             Timed tm(h, LDE_K_COORD);
             HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->d_key_dist,
                                             h->stream));
+            if (!h->d_key_rec)
+                if (int rc = dev_alloc(h, &h->d_key_rec, (size_t)h->L + 1)) return rc;
+            HIPCALL(h, lde::launch_key_records(h->d_glut + (size_t)(h->L + 1) * replica, h->d_cpd,
+                                               (unsigned)h->L, h->d_key_rec, h->stream));
             lde::KeyArgs ka;
             ka.c = h->cargs;
             ka.segs = h->d_segs;
@@ -923,6 +928,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             ka.glut = h->d_glut + (size_t)(h->L + 1) * replica;
             ka.pix_tab = tab_r;
             ka.tab_d = h->d_key_dist;
+            ka.rec = h->d_key_rec;
             ka.cbits = h->cache_bits;
             ka.keys = h->d_cbin;
             HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream));
@@ -1281,6 +1287,7 @@ void release(lde_handle *h) {
     dev_free(h->d_ccd);
     dev_free(h->d_cbin);
     dev_free(h->d_key_dist);
+    dev_free(h->d_key_rec);
     dev_free(h->d_win32);
     dev_free(h->d_win64);
     dev_free(h->d_cum);

@@ -355,6 +355,7 @@ struct KeyArgs {
     const uint32_t *glut;     // this replica's pixel words, L + 1 entries (entry L = 0)
     const uint32_t *pix_tab;  // this replica's LDS pixel-table image (1 << cbits words)
     const double *tab_d;      // distance of each table slot's pixel (1 << cbits)
+    const uint4 *rec;         // per pixel {word, 0, distance lo, hi}, L + 1 entries (k_key_records)
     int cbits;
     int *keys;                // [n_chunks * kChunk]
 };
@@ -363,6 +364,8 @@ hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st);
 // distance of every pixel-table slot's pixel (NaN for empty slots)
 hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix_d, unsigned L,
                            double *tab_d, hipStream_t st);
+hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, uint4 *rec,
+                              hipStream_t st);
 
 hipError_t launch_rebin_f64(const double *se, const double *sv, long long ns, const double *de,
                             long long nd, double *out_a, double *out_b, hipStream_t st);

@@ -119,7 +119,8 @@ __global__ __launch_bounds__(256) void k_sieve_glut(const LT *__restrict__ lut, 
     glut[q] = w;
 }
 
-// slot j of the LDS pixel table: the most-sampled valid pixel q = j (mod C)
+// slot j of the LDS pixel table: the most-sampled pixel q = j (mod C), with
+// the pixel's word (0 for a dropped pixel: valid bit clear) and its tag
 __global__ __launch_bounds__(256) void k_sieve_table(const uint32_t *__restrict__ cnt,
                                                      const uint32_t *__restrict__ glut, long long L,
                                                      int cbits, uint32_t *__restrict__ tab) {
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(256) void k_sieve_table(const uint32_t *__restrict_
     long long bq = -1;
     for (long long q = j; q < L; q += C) {
         const uint32_t c = cnt[q];
-        if (c > best && glut[q] != 0u) {
+        if (c > best) {  // dropped pixels too: their word is 0 (a hit drops the event)
             best = c;
             bq = q;
         }

@@ -139,9 +139,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_sample_screens(
     for (int e = 0; e < kSplitEPT; ++e) {
         const unsigned q = (unsigned)p[e] - (unsigned)pid_off;
         const int s = q < L ? screen_of(lut, q, T) : -1;
-        if (s >= 0) {
-            atomicAdd(&s_cnt[s], 1u);
-            if (pix_cnt) {
+        if (s >= 0) atomicAdd(&s_cnt[s], 1u);
+        // pixel counts of every id inside the LUT, dropped pixels included: the
+        // SIEVE table then holds frequent dropped pixels too, so their events
+        // need no gather (a view that drops most of the detector, e.g.
+        // mantle_front_layer, would otherwise gather nearly every event)
+        if (q < L && pix_cnt) {
+            {
                 bool done = false;
                 if (H) {
                     uint32_t h = (q * 2654435761u) >> (32 - hbits);
