@@ -35,7 +35,7 @@ LDE_ENOTSUP = -6
 LDE_F64 = 0
 LDE_F32 = 1
 
-STRATEGIES = {'auto': 0, 'atomic': 1, 'partition': 2, 'paged': 3, 'split': 4}
+STRATEGIES = {'auto': 0, 'atomic': 1, 'partition': 2, 'paged': 3, 'split': 4, 'pixel': 5}
 
 LDE_CURRENT = 0
 LDE_CUMULATIVE = 1
@@ -54,6 +54,7 @@ KERNELS = {
     'split': 10,
     'split_aux': 11,
     'coord': 12,
+    'pixel': 13,
 }
 
 # every symbol include/lde.h declares (checked by tests/test_abi.py)

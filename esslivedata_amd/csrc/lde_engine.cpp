@@ -168,6 +168,17 @@ struct lde_handle {
     bool coord_keyed = true;
     double *d_key_dist = nullptr;  // [1 << cache_bits] distance of each pixel-table slot
     uint4 *d_key_rec = nullptr;    // [L + 1] {word, 0, distance} of the batch's replica
+    // PIXEL strategy (lde_pixel.hip): pixel-range footprints built from the LUT
+    bool pixel_ok = false;
+    lde::PixSetup pix{};
+    uint16_t *d_ploc = nullptr;
+    uint32_t *d_pfp_off = nullptr, *d_pfp_scr = nullptr;
+    uint32_t *d_pcounts = nullptr, *d_prstart = nullptr, *d_ppayload = nullptr;
+    size_t ppayload_cap = 0;
+    uint4 *d_pitems = nullptr;
+    size_t pitems_cap = 0;
+    uint32_t *d_pitem_count = nullptr;
+    int pix_grid = 0;
     std::vector<double> edges;  // the create-time edges (event unit)
     // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
     bool lds_ctab = true, karg_segs = true;
@@ -1087,6 +1098,42 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
                       nullptr, h->d_cold_chunks);
 }
 
+int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks, long long total,
+              int replica) {
+    if (int rc = upload_segments(h, sd)) return rc;
+    if (int rc = grow(h, &h->d_ppayload, h->ppayload_cap, (size_t)total + 4)) return rc;
+    // pass-B items: a few per CU (LDS: one block per CU), and a range's
+    // footprint flush per item, so not many more
+    const long long per = std::max<long long>(65536, (total + 2LL * h->cus - 1) / (2LL * h->cus));
+    const long long max_items = total / per + h->pix.nr + 1;
+    if (int rc = grow(h, &h->d_pitems, h->pitems_cap, (size_t)max_items)) return rc;
+    lde::PixArgs a;
+    a.segs = h->d_segs;
+    a.n_segs = (int)sd.size();
+    a.n_chunks = chunks;
+    a.pid_off = h->pid_off;
+    a.L = (unsigned)h->L;
+    a.rb = h->pix.rb;
+    a.nr = h->pix.nr;
+    a.tab = h->d_tab;
+    a.tp = h->tp;
+    a.counts = h->d_pcounts;
+    a.rstart = h->d_prstart;
+    a.payload = h->d_ppayload;
+    a.grid = (int)std::min<long long>(chunks, (long long)h->pix_grid);
+    {
+        Timed tm(h, LDE_K_PIXEL);
+        HIPCALL(h, lde::launch_pixel(a, h->pix, replica, (uint32_t)per, (int)max_items, h->d_pitems,
+                                     h->d_pitem_count, h->d_win32, h->stream, 0));
+    }
+    {
+        Timed tm(h, LDE_K_PAGE_ACC);
+        HIPCALL(h, lde::launch_pixel(a, h->pix, replica, (uint32_t)per, (int)max_items, h->d_pitems,
+                                     h->d_pitem_count, h->d_win32, h->stream, 1));
+    }
+    return LDE_OK;
+}
+
 int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int replica,
                  bool coord_deferred) {
     const size_t lut_es = h->lut16 ? 2 : 4;
@@ -1108,6 +1155,10 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
     int strat = auto_strategy(h, total);
     const bool auto_split = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && h->split_ok;
     if (strat == LDE_STRATEGY_SPLIT && !h->split_ok) strat = LDE_STRATEGY_PAGED;
+    if (strat == LDE_STRATEGY_PIXEL && !h->pixel_ok) strat = LDE_STRATEGY_PAGED;
+    // AUTO without skew: PIXEL (no LUT gather) where the footprints fit
+    const bool auto_pixel = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && h->pixel_ok;
+    if (auto_pixel && !auto_split) strat = LDE_STRATEGY_PIXEL;
     if ((strat == LDE_STRATEGY_PARTITION || strat == LDE_STRATEGY_PAGED) && h->n_tiles == 0)
         strat = LDE_STRATEGY_ATOMIC;
     if (coord_deferred && !coord_keyed_candidate(h, total)) {
@@ -1148,8 +1199,13 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             if (int rc2 = coord_prepass(h, sd)) return rc2;
             if (int rc2 = upload_segments(h, sd)) return rc2;
         }
+        if (auto_pixel) {
+            h->last_strategy = LDE_STRATEGY_PIXEL;
+            return bin_pixel(h, sd, chunks, total, replica);
+        }
         return paged_core(h, h->d_segs, (int)sd.size(), chunks, total, total, lut, nullptr);
     }
+    if (strat == LDE_STRATEGY_PIXEL) return bin_pixel(h, sd, chunks, total, replica);
     if (strat == LDE_STRATEGY_PAGED) return bin_paged(h, sd, chunks, total, lut);
     long long item_events = h->item_events_override > 0
                                 ? h->item_events_override
@@ -1238,6 +1294,79 @@ int upload_lut(lde_handle *h, const int32_t *out_lut) {
     return LDE_OK;
 }
 
+// PIXEL setup: ranges of 2^rb consecutive pixels, each range's screen
+// footprint over every replica (sorted screen list) and every pixel's index
+// in its range's footprint.  Available when the ranges fit kPixMaxRanges and
+// the largest footprint's counters fit LDS (pix_acc_smem).
+int build_pixel(lde_handle *h, const int32_t *lut) {
+    h->pixel_ok = false;
+    if (h->monitor || h->n_tiles == 0 || env_ll("LDE_PIXEL", 1) == 0) return LDE_OK;
+    const long long L = h->L, R = h->R, S = h->S;
+    const int T = h->T;
+    int rb = 8;
+    while (rb < 20 && ((L + (1LL << rb) - 1) >> rb) > lde::kPixMaxRanges) ++rb;
+    int tbits = 0;
+    while ((1 << tbits) < T) ++tbits;
+    if (rb + tbits > 24) return LDE_OK;  // payload: local pixel | bin << rb in 24 bits
+    const int nr = (int)((L + (1LL << rb) - 1) >> rb);
+    std::vector<int> stamp((size_t)S, -1), pos((size_t)S, 0);
+    std::vector<uint32_t> fp_off((size_t)nr + 1, 0), fp;
+    std::vector<uint16_t> loc((size_t)(R * L), 0xFFFF);
+    int fmax = 0;
+    for (int r = 0; r < nr; ++r) {
+        const long long q0 = (long long)r << rb, q1 = std::min(L, q0 + (1LL << rb));
+        const size_t first = fp.size();
+        for (long long rep = 0; rep < R; ++rep)
+            for (long long q = q0; q < q1; ++q) {
+                const int sc = lut[rep * L + q];
+                if (sc >= 0 && stamp[(size_t)sc] != r) {
+                    stamp[(size_t)sc] = r;
+                    fp.push_back((uint32_t)sc);
+                }
+            }
+        std::sort(fp.begin() + (long)first, fp.end());
+        const int nf = (int)(fp.size() - first);
+        if (nf > 0xFFFE) return LDE_OK;
+        fmax = std::max(fmax, nf);
+        if (lde::pix_acc_smem(rb, fmax, T) > 150 * 1024) return LDE_OK;  // footprint too wide
+        for (int i = 0; i < nf; ++i) pos[fp[first + (size_t)i]] = i;
+        for (long long rep = 0; rep < R; ++rep)
+            for (long long q = q0; q < q1; ++q) {
+                const int sc = lut[rep * L + q];
+                if (sc >= 0) loc[(size_t)(rep * L + q)] = (uint16_t)pos[(size_t)sc];
+            }
+        fp_off[(size_t)r + 1] = (uint32_t)fp.size();
+    }
+    // (re)upload; the previous batch's kernels may still read the old tables
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    dev_free(h->d_ploc);
+    dev_free(h->d_pfp_off);
+    dev_free(h->d_pfp_scr);
+    if (int rc = dev_alloc(h, &h->d_ploc, loc.size())) return rc;
+    if (int rc = dev_alloc(h, &h->d_pfp_off, fp_off.size())) return rc;
+    if (int rc = dev_alloc(h, &h->d_pfp_scr, std::max<size_t>(1, fp.size()))) return rc;
+    HIPCALL(h, hipMemcpy(h->d_ploc, loc.data(), loc.size() * 2, hipMemcpyHostToDevice));
+    HIPCALL(h, hipMemcpy(h->d_pfp_off, fp_off.data(), fp_off.size() * 4, hipMemcpyHostToDevice));
+    if (!fp.empty()) HIPCALL(h, hipMemcpy(h->d_pfp_scr, fp.data(), fp.size() * 4, hipMemcpyHostToDevice));
+    h->pix_grid = h->cus;
+    if (!h->d_pcounts) {
+        if (int rc = dev_alloc(h, &h->d_pcounts, (size_t)h->pix_grid * lde::kPixMaxRanges)) return rc;
+        if (int rc = dev_alloc(h, &h->d_prstart, (size_t)lde::kPixMaxRanges + 1)) return rc;
+        if (int rc = dev_alloc(h, &h->d_pitem_count, 1)) return rc;
+    }
+    h->pix.rb = rb;
+    h->pix.nr = nr;
+    h->pix.fmax = fmax;
+    h->pix.loc = h->d_ploc;
+    h->pix.fp_off = h->d_pfp_off;
+    h->pix.fp_scr = h->d_pfp_scr;
+    h->pixel_ok = true;
+    if (env_ll("LDE_VERBOSE", 0))
+        fprintf(stderr, "lde pixel: %d ranges of 2^%d pixels, widest footprint %d screens (%zu B LDS)\n",
+                nr, rb, fmax, lde::pix_acc_smem(rb, fmax, T));
+    return LDE_OK;
+}
+
 int ensure_win64(lde_handle *h) {
     if (h->d_win64) return LDE_OK;
     if (int rc = dev_alloc(h, &h->d_win64, (size_t)h->nbins)) return rc;
@@ -1288,6 +1417,14 @@ void release(lde_handle *h) {
     dev_free(h->d_cbin);
     dev_free(h->d_key_dist);
     dev_free(h->d_key_rec);
+    dev_free(h->d_ploc);
+    dev_free(h->d_pfp_off);
+    dev_free(h->d_pfp_scr);
+    dev_free(h->d_pcounts);
+    dev_free(h->d_prstart);
+    dev_free(h->d_ppayload);
+    dev_free(h->d_pitems);
+    dev_free(h->d_pitem_count);
     dev_free(h->d_win32);
     dev_free(h->d_win64);
     dev_free(h->d_cum);
@@ -1537,6 +1674,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     if (!monitor) {
         h->lut16 = h->S < 0xFFFF && env_ll("LDE_LUT32", 0) == 0;
         CREATE_CHECK(upload_lut(h, cfg->out_lut));
+        if (cfg->strategy < LDE_STRATEGY_AUTO || cfg->strategy > LDE_STRATEGY_PIXEL)
+            CREATE_CHECK(fail(h, LDE_EINVAL, "unknown strategy %d", cfg->strategy));
     }
     CREATE_CHECK(dev_alloc(h, &h->d_tab, tab.size()));
     CREATE_HIP(hipMemcpy(h->d_tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
@@ -1715,6 +1854,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);
         h->auto_partition = (int)env_ll("LDE_AUTO_PARTITION", LDE_STRATEGY_PAGED);
     }
+    if (!monitor) CREATE_CHECK(build_pixel(h, cfg->out_lut));
     CREATE_HIP(hipEventCreateWithFlags(&h->pin_done, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&h->segs_done, hipEventDisableTiming));
     CREATE_HIP(hipStreamSynchronize(h->stream));
@@ -2440,7 +2580,8 @@ int lde_set_lut(lde_handle *h, const int32_t *out_lut) {
     if (h->monitor) return fail(h, LDE_EINVAL, "a monitor handle has no LUT");
     if (!out_lut) return fail(h, LDE_EINVAL, "out_lut is NULL");
     DeviceGuard guard(h->device);
-    return upload_lut(h, out_lut);
+    if (int rc = upload_lut(h, out_lut)) return rc;
+    return build_pixel(h, out_lut);
 }
 
 int lde_get_stream(lde_handle *h, void **stream) {

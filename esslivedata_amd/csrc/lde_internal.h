@@ -367,6 +367,37 @@ hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix
 hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, uint4 *rec,
                               hipStream_t st);
 
+// PIXEL strategy (lde_pixel.hip): events partitioned by pixel range, the
+// LUT lookup done in pass B from the range's LDS slice
+constexpr int kPixMaxRanges = 256;
+struct PixArgs {
+    const SegDesc *segs;
+    int n_segs;
+    long long n_chunks;
+    int pid_off;
+    unsigned L;
+    int rb;                      // range of pixel q: q >> rb
+    int nr;                      // ranges (<= kPixMaxRanges)
+    const unsigned char *tab;    // TOA lookup image
+    ToaParams tp;
+    uint32_t *counts;            // [grid][nr] events, then payload offsets
+    uint32_t *rstart;            // [nr + 1]
+    uint32_t *payload;           // local pixel | bin << rb per event, range-major
+    int grid;
+};
+struct PixSetup {                // setup-time tables (lde_create / lde_set_lut)
+    int rb = 0, nr = 0, fmax = 0;
+    const uint16_t *loc = nullptr;     // [R][L] footprint-local screen of every pixel (0xFFFF: dropped)
+    const uint32_t *fp_off = nullptr;  // [nr + 1] footprint list offsets
+    const uint32_t *fp_scr = nullptr;  // footprint screens, range after range
+};
+size_t pix_scatter_smem(const ToaParams &tp);
+size_t pix_acc_smem(int rb, int fmax, int T);
+// phase 0: count + scan + scatter; phase 1: accumulate
+hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32_t item_events,
+                        int max_items, uint4 *items, uint32_t *item_count, uint32_t *hist,
+                        hipStream_t st, int phase);
+
 hipError_t launch_rebin_f64(const double *se, const double *sv, long long ns, const double *de,
                             long long nd, double *out_a, double *out_b, hipStream_t st);
 

@@ -523,7 +523,7 @@ class BinningEngine:
             'tile_bits': tb.value,
             'n_tiles': nt.value,
             'events_binned': eb.value,
-            'last_strategy': {0: 'monitor', 1: 'atomic', 2: 'partition', 3: 'paged', 4: 'split'}.get(ls.value, '?'),
+            'last_strategy': {0: 'monitor', 1: 'atomic', 2: 'partition', 3: 'paged', 4: 'split', 5: 'pixel'}.get(ls.value, '?'),
             'device': self._device,
         }
 

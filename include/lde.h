@@ -54,6 +54,8 @@ extern "C" {
 #define LDE_STRATEGY_PARTITION 2   /* tile partition (chunk-major runs) + LDS sub-histograms */
 #define LDE_STRATEGY_PAGED 3       /* tile partition into per-block page chains + LDS sub-histograms */
 #define LDE_STRATEGY_SPLIT 4       /* hot screen rows in LDS + cold remainder through PAGED (skewed streams) */
+#define LDE_STRATEGY_PIXEL 5       /* partition by pixel range (no LUT gather) + the range's LUT slice and
+                                      screen footprint in LDS; needs footprints that fit (else PAGED) */
 
 /* histogram selectors for lde_read_histogram */
 #define LDE_CURRENT 0    /* window since the last finalize  (accumulators.py:138-163) */
@@ -317,8 +319,9 @@ int lde_synchronize(lde_handle *h);
 #define LDE_K_PAGE_ACC 9  /* k_page_accumulate: PAGED pass B                  */
 #define LDE_K_SPLIT 10    /* k_split: SPLIT event pass (hot rows in LDS, cold keys out) */
 #define LDE_K_SPLIT_AUX 11 /* hot-set selection, hot-row reduce, cold segment table */
-#define LDE_K_COORD 12    /* k_event_coord: wavelength-mode coordinate pass   */
-#define LDE_K_COUNT 13
+#define LDE_K_COORD 12    /* k_event_coord / k_event_key: wavelength-mode coordinate pass */
+#define LDE_K_PIXEL 13    /* k_pix_count + k_pix_scan + k_pix_scatter: PIXEL pass A */
+#define LDE_K_COUNT 14
 int lde_timing_enable(lde_handle *h, int32_t enable);
 /* Record only the kernels whose bit (1 << LDE_K_*) is set in mask (default:
  * all).  Fewer recorded events = less host work per batch. */

@@ -37,7 +37,7 @@ DREAM_SPEC = {
     'wire_view': ([('wire',), ('module', 'segment', 'counter')], {}),
     'strip_view': ([('strip',)], {}),
 }
-STRATEGIES = ['auto', 'atomic', 'partition', 'paged', 'split']
+STRATEGIES = ['auto', 'atomic', 'partition', 'paged', 'split', 'pixel']
 
 
 @pytest.fixture(scope='module', autouse=True)

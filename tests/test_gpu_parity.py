@@ -11,7 +11,7 @@ from oracle import scipp_semantics as ora
 
 pytestmark = pytest.mark.gpu
 
-STRATEGIES = ['atomic', 'partition', 'paged', 'split']
+STRATEGIES = ['atomic', 'partition', 'paged', 'split', 'pixel']
 
 # internal kernel variants that must all be bit-identical
 VARIANTS = [
@@ -185,7 +185,9 @@ def test_dream_mantle_geometric_skewed(strategy, variant, monkeypatch):
         o.accumulate(pid, toa)
     res = eng.finalize(hists=True)
     exp = o.finalize()
-    assert eng.info()['last_strategy'] == strategy
+    # PIXEL needs footprints that fit LDS: the mantle's 2048-pixel ranges span
+    # two arc columns of 320 screens, so it falls back to PAGED here
+    assert eng.info()['last_strategy'] == (strategy if strategy != 'pixel' else 'paged')
     np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
     np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
     np.testing.assert_array_equal(res.current_image.reshape(80, 320), exp['current'])
@@ -674,3 +676,46 @@ def test_finalize_images_written_in_place_are_never_reused_while_held():
     ptrs = {a.__array_interface__['data'][0] for a in held}
     assert len(ptrs) == len(held)
     eng.close()
+
+
+@pytest.mark.parametrize('strategy', ['pixel', 'paged'])
+def test_loki_pixel_ranges_multi_replica_and_move(strategy):
+    """PIXEL (pixel-range partition, LUT slice in LDS) on LOKI bank 0 with
+    five replicas, unknown ids, TOAs outside the edges, misaligned and empty
+    messages, and a LUT replaced mid-run (a detector move rebuilds the
+    footprints): bit-exact against the oracle, like PAGED."""
+    from esslivedata_amd import geometry, projection, synthetic
+
+    inst = synthetic.loki_bank0()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution, flip_x=True)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, strategy, toa_range=(5, 95))
+    ps = ora.geometric_pixel_screen(inst.coords, inst.resolution, flip_x=True)
+    o = ora.OracleDetectorView(detector_number=inst.detector_number, pixel_screen=ps,
+                               screen_shape=(144, 144), toa_edges_ns=edges, toa_slice=(5, 95))
+    for batch in range(4):
+        if batch == 2:  # moved: new coordinates, new LUT, new footprints
+            src = geometry.GeometricSource(inst.detector_number, inst.positions,
+                                           projection_type='xy_plane', resolution=inst.resolution,
+                                           pixel_noise=inst.pixel_noise, flip_x=True)
+            t = np.eye(4)
+            t[0, 3], t[1, 3] = 0.21, -0.13
+            moved = src.view(t)
+            eng.set_lut(moved.lut)
+            o.pixel_screen = ora.geometric_pixel_screen(src.coords(t), inst.resolution, flip_x=True)
+        pid, toa = synthetic.uniform_events(3_000_001 + batch, 1, 802816, seed=300 + batch)
+        pid[:500] = 0  # unknown ids on both sides of the LUT
+        pid[500:1000] = 802817
+        toa[1000:1200] = -7  # before the first edge
+        toa[1200:1400] = 2_000_000_000  # past the last edge
+        eng.stage(pid[:1_000_001], toa[:1_000_001])
+        eng.stage(pid[1_000_001:1_000_001], toa[1_000_001:1_000_001])
+        eng.stage(pid[1_000_001:], toa[1_000_001:])
+        eng.accumulate(batch % view.n_replicas)
+        o.accumulate(pid, toa)
+        res = eng.finalize(hists=True)
+        exp = o.finalize()
+        assert eng.info()['last_strategy'] == strategy
+        np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
+        np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
+        assert res.current_in_range == exp['counts_in_toa_range']

@@ -15,7 +15,7 @@ from oracle import scipp_semantics as ora
 
 pytestmark = pytest.mark.gpu
 
-STRATEGIES = ['atomic', 'partition', 'paged', 'split']
+STRATEGIES = ['atomic', 'partition', 'paged', 'split', 'pixel']
 
 
 @pytest.fixture(scope='module', autouse=True)
