@@ -87,7 +87,7 @@ def test_profile_readers_match_committed_summary():
     t = bench.profiled_traffic('dream', 'split')
     lds = bench.profiled_lds('dream', 'split')
     assert t is not None and lds is not None
-    assert t['source'] == lds['source'] == 'profiles/r2_dream_bench.json'
+    assert t['source'] == lds['source'] == f'profiles/{bench.PROFILE_ROUND}_dream_bench.json'
     assert bench.profiled_traffic('dream', 'atomic') is None  # no such kernel in the profile
 
 
