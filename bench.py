@@ -38,7 +38,9 @@ KERNEL_SYMBOL = {
     'paged': 'k_paged_partition',
     'page_accumulate': 'k_page_accumulate',
     'split': 'k_sieve',  # SPLIT's event pass (k_split when LDE_SIEVE=0)
-    'coord': 'k_event_coord',  # wavelength-mode coordinate pass
+    'coord': 'k_event_key',  # wavelength-mode coordinate pass (keyed; k_event_coord otherwise)
+    'pixel': 'k_pix_scatter',  # PIXEL pass A (with k_pix_count + k_pix_scan in the bucket)
+    'page_accumulate': 'k_page_accumulate',
     'finalize': 'k_finalize_v4',
 }
 # engine timing buckets (include/lde.h LDE_K_*) as they are used by the SPLIT
@@ -292,7 +294,7 @@ def main():
     # with the largest time per step among them (a kernel, not a strategy:
     # in wavelength mode the coordinate pass dominates the sieve)
     names = ('atomic', 'partition', 'tile_accumulate', 'plan', 'paged', 'page_plan',
-             'page_accumulate', 'split', 'split_aux', 'coord', 'binning', 'finalize')
+             'page_accumulate', 'split', 'split_aux', 'coord', 'pixel', 'binning', 'finalize')
     eng.timing_select(None)
     eng.timing_enable(True)
     n_prof = 3

@@ -1104,7 +1104,7 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     if (int rc = grow(h, &h->d_ppayload, h->ppayload_cap, (size_t)total + 4)) return rc;
     // pass-B items: a few per CU (LDS: one block per CU), and a range's
     // footprint flush per item, so not many more
-    const long long per = std::max<long long>(65536, (total + 2LL * h->cus - 1) / (2LL * h->cus));
+    const long long per = std::max<long long>(65536, (total + h->cus - 1) / h->cus);
     const long long max_items = total / per + h->pix.nr + 1;
     if (int rc = grow(h, &h->d_pitems, h->pitems_cap, (size_t)max_items)) return rc;
     lde::PixArgs a;
@@ -1348,10 +1348,10 @@ int build_pixel(lde_handle *h, const int32_t *lut) {
     HIPCALL(h, hipMemcpy(h->d_ploc, loc.data(), loc.size() * 2, hipMemcpyHostToDevice));
     HIPCALL(h, hipMemcpy(h->d_pfp_off, fp_off.data(), fp_off.size() * 4, hipMemcpyHostToDevice));
     if (!fp.empty()) HIPCALL(h, hipMemcpy(h->d_pfp_scr, fp.data(), fp.size() * 4, hipMemcpyHostToDevice));
-    h->pix_grid = h->cus;
+    h->pix_grid = 4 * h->cus;  // several partition blocks per CU (LDS ~36 KB each)
     if (!h->d_pcounts) {
         if (int rc = dev_alloc(h, &h->d_pcounts, (size_t)h->pix_grid * lde::kPixMaxRanges)) return rc;
-        if (int rc = dev_alloc(h, &h->d_prstart, (size_t)lde::kPixMaxRanges + 1)) return rc;
+        if (int rc = dev_alloc(h, &h->d_prstart, 2 * (size_t)lde::kPixMaxRanges + 1)) return rc;
         if (int rc = dev_alloc(h, &h->d_pitem_count, 1)) return rc;
     }
     h->pix.rb = rb;

@@ -381,7 +381,7 @@ struct PixArgs {
     const unsigned char *tab;    // TOA lookup image
     ToaParams tp;
     uint32_t *counts;            // [grid][nr] events, then payload offsets
-    uint32_t *rstart;            // [nr + 1]
+    uint32_t *rstart;            // [nr + 1] range starts, then [nr] range totals (scratch)
     uint32_t *payload;           // local pixel | bin << rb per event, range-major
     int grid;
 };

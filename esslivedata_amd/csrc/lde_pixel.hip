@@ -101,31 +101,42 @@ __global__ __launch_bounds__(kPixThreads) void k_pix_count(PixArgs a) {
     for (int r = threadIdx.x; r < a.nr; r += kPixThreads) a.counts[(size_t)blockIdx.x * a.nr + r] = s_cnt[r];
 }
 
-// One block of 1024 threads: thread r owns range r.  counts[b][r] become the
-// payload offsets of (block b, range r); rstart[r] the start of range r;
-// items split every range into pieces of at most item_events.
-__global__ __launch_bounds__(1024) void k_pix_scan(PixArgs a, int grid, uint32_t item_events,
-                                                   uint4 *__restrict__ items,
+// One block per range r: its total over the blocks and the exclusive prefix
+// over blocks (counts[b][r] becomes the offset of (block b, range r) inside
+// range r).
+__global__ __launch_bounds__(1024) void k_pix_scan_blocks(PixArgs a, int grid,
+                                                          uint32_t *__restrict__ rtot) {
+    __shared__ uint32_t s_w[32];
+    const int r = blockIdx.x;
+    uint32_t carry = 0;
+    for (int b0 = 0; b0 < grid; b0 += 1024) {
+        const int b = b0 + (int)threadIdx.x;
+        const size_t i = (size_t)b * a.nr + r;
+        const uint32_t v = b < grid ? a.counts[i] : 0u;
+        uint32_t tot;
+        const uint32_t x = block_exclusive_scan(v, s_w, &tot);
+        if (b < grid) a.counts[i] = carry + x;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) rtot[r] = carry;
+}
+
+// One block of 1024 threads, thread r = range r: range starts (rstart) and
+// work items, every range split into pieces of at most item_events.
+__global__ __launch_bounds__(1024) void k_pix_scan(PixArgs a, const uint32_t *__restrict__ rtot,
+                                                   uint32_t item_events, uint4 *__restrict__ items,
                                                    uint32_t *__restrict__ item_count, int max_items) {
     __shared__ uint32_t s_w[32];
     const int r = threadIdx.x;
-    uint32_t tot = 0;
-    if (r < a.nr)
-        for (int b = 0; b < grid; ++b) tot += a.counts[(size_t)b * a.nr + r];
+    const uint32_t tot = r < a.nr ? rtot[r] : 0u;
     uint32_t all;
-    const uint32_t start = block_exclusive_scan(r < a.nr ? tot : 0u, s_w, &all);
-    const uint32_t k = (r < a.nr && tot > 0) ? (tot + item_events - 1) / item_events : 0u;
+    const uint32_t start = block_exclusive_scan(tot, s_w, &all);
+    const uint32_t k = tot > 0 ? (tot + item_events - 1) / item_events : 0u;
     uint32_t n_items;
     const uint32_t ifirst = block_exclusive_scan(k, s_w, &n_items);
     if (r < a.nr) {
         a.rstart[r] = start;
-        uint32_t run = start;
-        for (int b = 0; b < grid; ++b) {
-            const size_t i = (size_t)b * a.nr + r;
-            const uint32_t n = a.counts[i];
-            a.counts[i] = run;
-            run += n;
-        }
         for (uint32_t j = 0; j < k && ifirst + j < (uint32_t)max_items; ++j) {
             const uint32_t b0 = start + j * item_events;
             const uint32_t b1 = b0 + item_events < start + tot ? b0 + item_events : start + tot;
@@ -157,7 +168,7 @@ __global__ __launch_bounds__(kPixThreads) void k_pix_scatter(PixArgs a) {
     const int tid = threadIdx.x;
     for (int r = tid; r < a.nr; r += kPixThreads) {
         s_cnt[r] = 0;
-        s_cur[r] = a.counts[(size_t)blockIdx.x * a.nr + r];  // this block's slot of range r
+        s_cur[r] = a.rstart[r] + a.counts[(size_t)blockIdx.x * a.nr + r];  // this block's slot of range r
     }
     __syncthreads();
     const uint32_t mask = (1u << a.rb) - 1u;
@@ -263,8 +274,9 @@ hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32
     if (a.nr > kPixMaxRanges || a.nr > 1024) return hipErrorInvalidValue;
     if (phase == 0) {
         hipLaunchKernelGGL(k_pix_count, dim3(a.grid), dim3(kPixThreads), 0, st, a);
-        hipLaunchKernelGGL(k_pix_scan, dim3(1), dim3(1024), 0, st, a, a.grid, item_events, items,
-                           item_count, max_items);
+        hipLaunchKernelGGL(k_pix_scan_blocks, dim3(a.nr), dim3(1024), 0, st, a, a.grid, a.rstart + a.nr + 1);
+        hipLaunchKernelGGL(k_pix_scan, dim3(1), dim3(1024), 0, st, a, a.rstart + a.nr + 1, item_events,
+                           items, item_count, max_items);
         const size_t sm = pix_scatter_smem(a.tp);
         if (a.tp.fast) {
             (void)hipFuncSetAttribute((const void *)k_pix_scatter<true>,
