@@ -1101,10 +1101,13 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
 int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks, long long total,
               int replica) {
     if (int rc = upload_segments(h, sd)) return rc;
-    if (int rc = grow(h, &h->d_ppayload, h->ppayload_cap, (size_t)total + 4)) return rc;
+    // runs padded to 4 payloads: at most 3 pads per (chunk, range)
+    if (int rc = grow(h, &h->d_ppayload, h->ppayload_cap,
+                      (size_t)total + 3 * (size_t)chunks * (size_t)h->pix.nr + 4))
+        return rc;
     // pass-B items: a few per CU (LDS: one block per CU), and a range's
     // footprint flush per item, so not many more
-    const long long per = std::max<long long>(65536, (total + h->cus - 1) / h->cus);
+    const long long per = std::max<long long>(65536, (total + 2LL * h->cus - 1) / (2LL * h->cus));
     const long long max_items = total / per + h->pix.nr + 1;
     if (int rc = grow(h, &h->d_pitems, h->pitems_cap, (size_t)max_items)) return rc;
     lde::PixArgs a;

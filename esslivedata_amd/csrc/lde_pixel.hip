@@ -82,9 +82,12 @@ __device__ __forceinline__ void block_chunks(long long n, long long &cb, long lo
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// Every chunk's run of a range is padded to a multiple of 4 payloads (the
+// pads are dropped payloads), so the scatter writes whole 16-byte groups;
+// the count sums those padded run lengths per (block, range).
 __global__ __launch_bounds__(kPixThreads) void k_pix_count(PixArgs a) {
-    __shared__ uint32_t s_cnt[kPixMaxRanges];
-    for (int r = threadIdx.x; r < a.nr; r += kPixThreads) s_cnt[r] = 0;
+    __shared__ uint32_t s_cnt[kPixMaxRanges], s_tot[kPixMaxRanges];
+    for (int r = threadIdx.x; r < a.nr; r += kPixThreads) s_cnt[r] = s_tot[r] = 0;
     __syncthreads();
     long long cb, ce;
     block_chunks(a.n_chunks, cb, ce);
@@ -96,9 +99,14 @@ __global__ __launch_bounds__(kPixThreads) void k_pix_count(PixArgs a) {
             const uint32_t q = (uint32_t)p[e] - (uint32_t)a.pid_off;
             if (q < a.L) atomicAdd(&s_cnt[q >> a.rb], 1u);
         }
+        __syncthreads();
+        for (int r = threadIdx.x; r < a.nr; r += kPixThreads) {
+            s_tot[r] += (s_cnt[r] + 3u) & ~3u;
+            s_cnt[r] = 0;
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    for (int r = threadIdx.x; r < a.nr; r += kPixThreads) a.counts[(size_t)blockIdx.x * a.nr + r] = s_cnt[r];
+    for (int r = threadIdx.x; r < a.nr; r += kPixThreads) a.counts[(size_t)blockIdx.x * a.nr + r] = s_tot[r];
 }
 
 // One block per range r: its total over the blocks and the exclusive prefix
@@ -152,14 +160,15 @@ __global__ __launch_bounds__(1024) void k_pix_scan(PixArgs a, const uint32_t *__
 // LDS: staging (kChunk u32) | counts, chunk offsets, cursors (nr each) |
 // scan scratch (32) | TOA image
 size_t pix_scatter_smem(const ToaParams &tp) {
-    return 4 * ((size_t)kChunk + 3 * (size_t)kPixMaxRanges + 32) + toa_lds_bytes(tp);
+    return 4 * ((size_t)kChunk + 4 * (size_t)kPixMaxRanges + 3 * (size_t)kPixMaxRanges + 32) +
+           toa_lds_bytes(tp);
 }
 
 template <bool FAST>
 __global__ __launch_bounds__(kPixThreads) void k_pix_scatter(PixArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *s_stg = reinterpret_cast<uint32_t *>(smem);
-    uint32_t *s_cnt = s_stg + kChunk;
+    uint32_t *s_cnt = s_stg + kChunk + 4 * kPixMaxRanges;  // staging holds the pads too
     uint32_t *s_off = s_cnt + kPixMaxRanges;
     uint32_t *s_cur = s_off + kPixMaxRanges;
     uint32_t *s_w = s_cur + kPixMaxRanges;
@@ -190,24 +199,30 @@ __global__ __launch_bounds__(kPixThreads) void k_pix_scatter(PixArgs a) {
         // the next chunk's events load while this one is partitioned
         if (c + 1 < ce) pix_load<true>(a.segs, a.n_segs, c + 1, a.pid_off, p, t);
         __syncthreads();
+        // runs padded to 4: staging offsets, slot cursors and the pads are
+        // 16-byte aligned groups
         uint32_t v = 0, total;
-        if (tid < a.nr) v = s_cnt[tid];  // nr <= kPixMaxRanges <= kPixThreads
-        const uint32_t off = block_exclusive_scan(tid < a.nr ? v : 0u, s_w, &total);
-        if (tid < a.nr) s_off[tid] = off;
+        if (tid < a.nr) v = (s_cnt[tid] + 3u) & ~3u;  // nr <= kPixMaxRanges <= kPixThreads
+        const uint32_t off = block_exclusive_scan(v, s_w, &total);
+        if (tid < a.nr) {
+            s_off[tid] = off;
+            for (uint32_t j = s_cnt[tid]; j < v; ++j) s_stg[off + j] = ((uint32_t)tid << 24) | kPixDropped;
+        }
         __syncthreads();
 #pragma unroll
         for (int e = 0; e < kPixEPT; ++e)
             if (rank[e] != 0xFFFFFFFFu) s_stg[s_off[word[e] >> 24] + rank[e]] = word[e];
         __syncthreads();
-        // runs of one range are contiguous in staging and in the range's slot
-        for (uint32_t i = (uint32_t)tid; i < total; i += kPixThreads) {
-            const uint32_t w = s_stg[i];
-            const uint32_t r = w >> 24;
-            a.payload[s_cur[r] + (i - s_off[r])] = w & 0xFFFFFFu;
+        // a 4-group never straddles two runs; its slot position is 4-aligned
+        for (uint32_t g = (uint32_t)tid * 4u; g < total; g += kPixThreads * 4u) {
+            const uint4 w = *reinterpret_cast<const uint4 *>(s_stg + g);
+            const uint32_t r = w.x >> 24;
+            *reinterpret_cast<uint4 *>(a.payload + s_cur[r] + (g - s_off[r])) =
+                make_uint4(w.x & 0xFFFFFFu, w.y & 0xFFFFFFu, w.z & 0xFFFFFFu, w.w & 0xFFFFFFu);
         }
         __syncthreads();
         for (int r = tid; r < a.nr; r += kPixThreads) {
-            s_cur[r] += s_cnt[r];
+            s_cur[r] += (s_cnt[r] + 3u) & ~3u;
             s_cnt[r] = 0;
         }
         __syncthreads();
@@ -250,10 +265,30 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
     const uint32_t h = e0 + ((4u - (e0 & 3u)) & 3u) < e1 ? e0 + ((4u - (e0 & 3u)) & 3u) : e1;
     if (threadIdx.x < h - e0) add(a.payload[e0 + threadIdx.x]);
     const uint32_t n4 = (e1 - h) >> 2;
-    for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) {
-        const v4i w = ld_stream4(reinterpret_cast<const int *>(a.payload) + h + 4 * i);
+    // U groups of 4 per lane and iteration, the next iteration's loads issued
+    // before this one's LDS work (the loop is otherwise load-latency bound)
+    constexpr int U = 4;
+    const int *pl = reinterpret_cast<const int *>(a.payload) + h;
+    const uint32_t step = blockDim.x * U;
+    v4i cur[U], nxt[U];
+    uint32_t i0 = threadIdx.x;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) add((uint32_t)w[q]);
+    for (int u = 0; u < U; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        cur[u] = i < n4 ? ld_stream4(pl + 4 * i) : v4i{-1, -1, -1, -1};
+    }
+    for (; i0 < n4; i0 += step) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = i0 + step + u * blockDim.x;
+            nxt[u] = i < n4 ? ld_stream4(pl + 4 * i) : v4i{-1, -1, -1, -1};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) add((uint32_t)cur[u][q] & 0xFFFFFFu);
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
     }
     const uint32_t tail = h + 4 * n4;
     if (tail + threadIdx.x < e1) add(a.payload[tail + threadIdx.x]);
