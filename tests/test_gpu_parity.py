@@ -383,8 +383,9 @@ def test_device_staging_matches_host_staging(strategy):
         c.stage_tensors_batch([(dp[:5], dt[:4])])
 
 
-def test_auto_picks_split_for_skewed_and_paged_for_uniform():
-    """AUTO: the sampled hot-row coverage decides (performance only; counts exact)."""
+def test_auto_picks_split_for_skewed_and_pixel_for_uniform():
+    """AUTO: the sampled hot-row coverage decides SPLIT; an unskewed stream whose
+    pixel-range footprints fit in LDS takes PIXEL (performance only; counts exact)."""
     from esslivedata_amd import projection, synthetic
 
     inst = synthetic.dream_mantle()
@@ -409,7 +410,14 @@ def test_auto_picks_split_for_skewed_and_paged_for_uniform():
     pid, toa = synthetic.uniform_events(3_000_000, 1, 802816, seed=5)
     eng.stage(pid, toa)
     eng.accumulate(0)
-    assert eng.info()['last_strategy'] == 'paged'
+    assert eng.info()['last_strategy'] == 'pixel'
+    exp = ora.OracleDetectorView(
+        detector_number=inst.detector_number,
+        pixel_screen=_oracle_pixel_screen_geometric(inst),
+        screen_shape=view.screen_shape,
+        toa_edges_ns=inst.edges.edges_ns(),
+    ).batch_histogram(pid, toa, 0)
+    np.testing.assert_array_equal(eng.read_histogram(), exp)
 
 
 def test_finalize_partials_match_finalize():

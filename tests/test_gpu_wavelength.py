@@ -81,7 +81,8 @@ def test_dream_wavelength_matches_oracle(strategy, scale, table_min):
         o.accumulate(pid, toa)
     res = eng.finalize(hists=True)
     exp = o.finalize()
-    assert eng.info()['last_strategy'] == strategy
+    # PIXEL needs footprints that fit LDS; the mantle's do not (PAGED runs)
+    assert eng.info()['last_strategy'] == (strategy if strategy != 'pixel' else 'paged')
     assert exp['histogram_cumulative'].sum() > 1_000_000  # most events binned
     np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
     np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
