@@ -177,8 +177,11 @@ struct lde_handle {
     size_t ppayload_cap = 0;
     uint4 *d_pitems = nullptr;
     size_t pitems_cap = 0;
+    lde::PixChunk *d_pctab = nullptr;
+    size_t pctab_cap = 0;
     uint32_t *d_pitem_count = nullptr;
-    int pix_grid = 0;
+    int pix_grid = 0, pix_unit = 2, pix_ept = 16;
+    bool pix24 = true;
     std::vector<double> edges;  // the create-time edges (event unit)
     // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
     bool lds_ctab = true, karg_segs = true;
@@ -1101,16 +1104,22 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
 int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks, long long total,
               int replica) {
     if (int rc = upload_segments(h, sd)) return rc;
-    // runs padded to 4 payloads: at most 3 pads per (chunk, range)
-    if (int rc = grow(h, &h->d_ppayload, h->ppayload_cap,
-                      (size_t)total + 3 * (size_t)chunks * (size_t)h->pix.nr + 4))
+    // runs padded to 4 payloads: at most 3 pads per (unit, range); 24-bit
+    // payloads take 3 bytes each
+    const long long units = (chunks + h->pix_unit - 1) / h->pix_unit;
+    const size_t n_pay = (size_t)total + 3 * (size_t)units * (size_t)h->pix.nr + 4;
+    if (int rc = grow(h, &h->d_ppayload, h->ppayload_cap, h->pix24 ? (n_pay * 3 + 3) / 4 + 4 : n_pay))
         return rc;
     // pass-B items: a few per CU (LDS: one block per CU), and a range's
-    // footprint flush per item, so not many more
-    const long long per = std::max<long long>(65536, (total + 2LL * h->cus - 1) / (2LL * h->cus));
+    // footprint flush per item, so not many more; whole groups of 4 payloads
+    const long long per =
+        (std::max<long long>(65536, (total + 2LL * h->cus - 1) / (2LL * h->cus)) + 3) & ~3LL;
     const long long max_items = total / per + h->pix.nr + 1;
     if (int rc = grow(h, &h->d_pitems, h->pitems_cap, (size_t)max_items)) return rc;
+    if (int rc = grow(h, &h->d_pctab, h->pctab_cap, (size_t)chunks)) return rc;
     lde::PixArgs a;
+    a.ctab = h->d_pctab;
+    a.ept = h->pix_ept;
     a.segs = h->d_segs;
     a.n_segs = (int)sd.size();
     a.n_chunks = chunks;
@@ -1123,7 +1132,9 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.counts = h->d_pcounts;
     a.rstart = h->d_prstart;
     a.payload = h->d_ppayload;
-    a.grid = (int)std::min<long long>(chunks, (long long)h->pix_grid);
+    a.unit = h->pix_unit;
+    a.p24 = h->pix24 ? 1 : 0;
+    a.grid = (int)std::min<long long>(units, (long long)h->pix_grid);
     {
         Timed tm(h, LDE_K_PIXEL);
         HIPCALL(h, lde::launch_pixel(a, h->pix, replica, (uint32_t)per, (int)max_items, h->d_pitems,
@@ -1351,7 +1362,15 @@ int build_pixel(lde_handle *h, const int32_t *lut) {
     HIPCALL(h, hipMemcpy(h->d_ploc, loc.data(), loc.size() * 2, hipMemcpyHostToDevice));
     HIPCALL(h, hipMemcpy(h->d_pfp_off, fp_off.data(), fp_off.size() * 4, hipMemcpyHostToDevice));
     if (!fp.empty()) HIPCALL(h, hipMemcpy(h->d_pfp_scr, fp.data(), fp.size() * 4, hipMemcpyHostToDevice));
-    h->pix_grid = 4 * h->cus;  // several partition blocks per CU (LDS ~36 KB each)
+    // partition blocks: 4 x 512 or 2 x 1024 threads per CU (LDS ~36 / ~70 KB each)
+    h->pix_unit = (int)std::max<long long>(1, std::min<long long>(2, env_ll("LDE_PIX_UNIT", 2)));
+    h->pix_ept = h->pix_unit == 2 || env_ll("LDE_PIX_EPT", 8) == 16 ? 16 : 8;
+    h->pix24 = env_ll("LDE_PIX24", 1) != 0;
+    // blocks of unit * kChunk / ept threads: 4 x 512 or 2 x 1024 per CU
+    h->pix_grid = (int)std::max<long long>(
+        1, env_ll("LDE_PIX_GRID", (h->pix_ept == 16 && h->pix_unit == 1 ? 4 : 2) * (long long)h->cus));
+    while (h->pix_unit > 1 && lde::pix_scatter_smem(h->tp, h->pix_unit) > 80 * 1024) --h->pix_unit;
+    if (lde::pix_scatter_smem(h->tp, h->pix_unit) > 160 * 1024) return LDE_OK;
     if (!h->d_pcounts) {
         if (int rc = dev_alloc(h, &h->d_pcounts, (size_t)h->pix_grid * lde::kPixMaxRanges)) return rc;
         if (int rc = dev_alloc(h, &h->d_prstart, 2 * (size_t)lde::kPixMaxRanges + 1)) return rc;
@@ -1426,6 +1445,7 @@ void release(lde_handle *h) {
     dev_free(h->d_pcounts);
     dev_free(h->d_prstart);
     dev_free(h->d_ppayload);
+    dev_free(h->d_pctab);
     dev_free(h->d_pitems);
     dev_free(h->d_pitem_count);
     dev_free(h->d_win32);

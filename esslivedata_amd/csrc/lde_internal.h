@@ -370,7 +370,14 @@ hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigne
 // PIXEL strategy (lde_pixel.hip): events partitioned by pixel range, the
 // LUT lookup done in pass B from the range's LDS slice
 constexpr int kPixMaxRanges = 256;
+struct PixChunk {                // one chunk of the batch (k_pix_chunks)
+    const int *pid;
+    const int *toa;
+    int n;                       // valid events; kChunk: full and aligned, -kChunk: full, misaligned
+    int pad;
+};
 struct PixArgs {
+    const PixChunk *ctab;        // [n_chunks]
     const SegDesc *segs;
     int n_segs;
     long long n_chunks;
@@ -383,7 +390,11 @@ struct PixArgs {
     uint32_t *counts;            // [grid][nr] events, then payload offsets
     uint32_t *rstart;            // [nr + 1] range starts, then [nr] range totals (scratch)
     uint32_t *payload;           // local pixel | bin << rb per event, range-major
+                                 // (24-bit payloads packed 4 per 12 bytes when p24)
     int grid;
+    int unit = 1;                // chunks per partition step (runs padded per unit)
+    int ept = 8;                 // events per thread and load: unit * kChunk / ept threads
+    int p24 = 1;                 // 3-byte payloads
 };
 struct PixSetup {                // setup-time tables (lde_create / lde_set_lut)
     int rb = 0, nr = 0, fmax = 0;
@@ -391,7 +402,7 @@ struct PixSetup {                // setup-time tables (lde_create / lde_set_lut)
     const uint32_t *fp_off = nullptr;  // [nr + 1] footprint list offsets
     const uint32_t *fp_scr = nullptr;  // footprint screens, range after range
 };
-size_t pix_scatter_smem(const ToaParams &tp);
+size_t pix_scatter_smem(const ToaParams &tp, int unit);
 size_t pix_acc_smem(int rb, int fmax, int T);
 // phase 0: count + scan + scatter; phase 1: accumulate
 hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32_t item_events,

@@ -32,81 +32,166 @@ namespace lde {
 
 namespace {
 
-constexpr int kPixThreads = kPartThreads;          // 512
-constexpr int kPixEPT = kPartEventsPerThread;      // 16 events per thread and chunk
 constexpr uint32_t kPixDropped = 0xFFFFFFu;
+constexpr int kPixLdsChunks = 128;                 // chunk-table entries a block keeps in LDS
+typedef unsigned int v3u __attribute__((ext_vector_type(3)));
+typedef __attribute__((address_space(1))) v3u g_v3u;
 
-// chunk c of the staged batch: pid (and toa) of every event this thread owns;
-// events past a message's end read as pid_off - 1 (outside the LUT)
-template <bool TOA>
-__device__ __forceinline__ void pix_load(const SegDesc *__restrict__ segs, int n_segs, long long c,
-                                         int pid_off, int (&p)[kPixEPT], int (&t)[kPixEPT]) {
-    int lo = 0, hi = n_segs - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
-    }
-    const SegDesc sd = segs[lo];
-    const long long base = (c - sd.chunk0) * kChunk;
-    const uintptr_t al = TOA ? ((uintptr_t)sd.pid | (uintptr_t)sd.toa) : (uintptr_t)sd.pid;
-    const bool vec = (al & 15u) == 0;
+// Four 24-bit payloads in 12 bytes (P24) or 16 (u32 payloads)
+__device__ __forceinline__ v3u pack24(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3) {
+    return v3u{p0 | (p1 << 24), (p1 >> 8) | (p2 << 16), (p2 >> 16) | (p3 << 8)};
+}
+__device__ __forceinline__ void unpack24(v3u w, uint32_t (&p)[4]) {
+    p[0] = w[0] & 0xFFFFFFu;
+    p[1] = (w[0] >> 24) | ((w[1] & 0xFFFFu) << 8);
+    p[2] = (w[1] >> 16) | ((w[2] & 0xFFu) << 16);
+    p[3] = w[2] >> 8;
+}
+
+// unit u = chunks [u * U, u * U + U), loaded by U * kChunk / E threads
+// (thread tid takes chunk u * U + tid / (kChunk / E), wave-uniform, as thread
+// tid % (kChunk / E) of that chunk): pid (and toa) of the E events it owns.
+// The chunk's pointers come from the block's copy of its chunk table in LDS
+// (s_ct, chunks from c0 on), so no wait on the vector-memory counter (which
+// also counts the previous unit's payload stores) precedes the event loads;
+// blocks with more than kPixLdsChunks chunks read the global table.  Full, aligned
+// chunks take vector loads; events past a message's end, and chunks past the
+// batch (the odd half of the last unit), read as pid_off - 1 (outside the LUT).
+template <int U, int E, bool TOA>
+__device__ __forceinline__ void unit_load(const PixArgs &a, const PixChunk *s_ct, long long c0,
+                                          long long u, int (&p)[E], int (&t)[E]) {
+    constexpr int CT = kChunk / E;
     const int tid = threadIdx.x;
+    const long long c = u * U + __builtin_amdgcn_readfirstlane(tid / CT);
+    const int tl = tid % CT;
+    if (c >= a.n_chunks) {
 #pragma unroll
-    for (int j = 0; j < kPixEPT / 4; ++j) {
-        const long long e0 = base + ((long long)j * kPixThreads + tid) * 4;
-        if (vec && e0 + 3 < sd.n) {
-            const v4i pv = ld_stream4(sd.pid + e0);
+        for (int e = 0; e < E; ++e) {
+            p[e] = a.pid_off - 1;
+            t[e] = 0;
+        }
+        return;
+    }
+    const PixChunk ch = s_ct ? s_ct[c - c0] : a.ctab[c];
+    if (ch.n == kChunk) {  // full and 16-byte aligned
+#pragma unroll
+        for (int j = 0; j < E / 4; ++j) {
+            const int off = (j * CT + tl) * 4;
+            const v4i pv = ld_stream4(ch.pid + off);
 #pragma unroll
             for (int q = 0; q < 4; ++q) p[j * 4 + q] = pv[q];
             if (TOA) {
-                const v4i tv = ld_stream4(sd.toa + e0);
+                const v4i tv = ld_stream4(ch.toa + off);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) t[j * 4 + q] = tv[q];
             }
-        } else {
+        }
+        return;
+    }
+    const int rem = ch.n < 0 ? -ch.n : ch.n;  // < 0: full but misaligned
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const bool ok = e0 + q < sd.n;
-                p[j * 4 + q] = ok ? ld_global(sd.pid + e0 + q) : pid_off - 1;
-                if (TOA) t[j * 4 + q] = ok ? ld_global(sd.toa + e0 + q) : 0;
-            }
+    for (int j = 0; j < E / 4; ++j) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int off = (j * CT + tl) * 4 + q;
+            const bool ok = off < rem;
+            p[j * 4 + q] = ok ? ld_global(ch.pid + off) : a.pid_off - 1;
+            if (TOA) t[j * 4 + q] = ok ? ld_global(ch.toa + off) : 0;
         }
     }
 }
 
-__device__ __forceinline__ void block_chunks(long long n, long long &cb, long long &ce) {
+// TOA bin without a branch (fast layout): out-of-range times look up a
+// clamped bucket and are dropped by the final select, so the two LDS reads of
+// every event can be in flight together
+__device__ __forceinline__ int toa_bin_nb(int t, const unsigned char *s_tab, const ToaParams &tp) {
+    const unsigned d = (unsigned)t - (unsigned)tp.lo;
+    const unsigned dc = d < tp.span ? d : tp.span - 1u;
+    const uint32_t *rthr = reinterpret_cast<const uint32_t *>(s_tab);
+    const uint16_t *bst = reinterpret_cast<const uint16_t *>(s_tab + align16((size_t)(tp.T + 1) * 4));
+    const int b = bst[dc >> tp.shift];
+    const int r = b + (dc >= rthr[b + 1] ? 1 : 0);
+    return d < tp.span ? r : -1;
+}
+template <bool FAST>
+__device__ __forceinline__ int pix_toa_bin(int t, const unsigned char *s_tab, const ToaParams &tp) {
+    return FAST ? toa_bin_nb(t, s_tab, tp) : toa_bin<false>(t, s_tab, tp);
+}
+
+__device__ __forceinline__ void block_units(long long n, long long &cb, long long &ce) {
     cb = (long long)blockIdx.x * n / gridDim.x;
     ce = ((long long)blockIdx.x + 1) * n / gridDim.x;
+}
+
+// the block's chunks [cb * U, ce * U) of the global chunk table into LDS;
+// nullptr (global reads) when they do not fit.  Ends with a barrier.
+template <int U>
+__device__ __forceinline__ const PixChunk *block_chunk_table(const PixArgs &a, PixChunk *s_ct, long long cb,
+                                                             long long ce) {
+    const long long c0 = cb * U;
+    const long long c1 = ce * U < a.n_chunks ? ce * U : a.n_chunks;
+    const bool fit = c1 - c0 <= kPixLdsChunks;
+    if (fit)
+        for (long long i = threadIdx.x; i < c1 - c0; i += blockDim.x) s_ct[i] = a.ctab[c0 + i];
+    __syncthreads();
+    return fit ? s_ct : nullptr;
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Every chunk's run of a range is padded to a multiple of 4 payloads (the
-// pads are dropped payloads), so the scatter writes whole 16-byte groups;
-// the count sums those padded run lengths per (block, range).
-__global__ __launch_bounds__(kPixThreads) void k_pix_count(PixArgs a) {
+// the batch's chunk table: pointers and valid events of every chunk (n =
+// kChunk: full and 16-byte aligned; -kChunk: full, misaligned)
+__global__ __launch_bounds__(256) void k_pix_chunks(PixArgs a, PixChunk *__restrict__ ctab) {
+    const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (c >= a.n_chunks) return;
+    int lo = 0, hi = a.n_segs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+    }
+    const SegDesc sd = a.segs[lo];
+    const long long base = (c - sd.chunk0) * kChunk;
+    const long long left = sd.n - base;
+    PixChunk ch;
+    ch.pid = sd.pid + base;
+    ch.toa = sd.toa + base;
+    ch.n = (int)(left < kChunk ? left : kChunk);
+    if (ch.n == kChunk && (((uintptr_t)ch.pid | (uintptr_t)ch.toa) & 15u) != 0) ch.n = -kChunk;
+    ch.pad = 0;
+    ctab[c] = ch;
+}
+
+// ---------------------------------------------------------------------------
+// Every unit's run of a range is padded to a multiple of 4 payloads (the
+// pads are dropped payloads), so the scatter writes whole groups of four
+// (16 bytes, or 12 with 24-bit payloads); the count sums those padded run
+// lengths per (block, range).
+template <int U, int E>
+__global__ __launch_bounds__(U * kChunk / E) void k_pix_count(PixArgs a) {
+    constexpr int NT = U * kChunk / E;
     __shared__ uint32_t s_cnt[kPixMaxRanges], s_tot[kPixMaxRanges];
-    for (int r = threadIdx.x; r < a.nr; r += kPixThreads) s_cnt[r] = s_tot[r] = 0;
-    __syncthreads();
+    __shared__ PixChunk s_ctab[kPixLdsChunks];
+    for (int r = threadIdx.x; r < a.nr; r += NT) s_cnt[r] = s_tot[r] = 0;
     long long cb, ce;
-    block_chunks(a.n_chunks, cb, ce);
-    int p[kPixEPT], t[kPixEPT];
+    block_units((a.n_chunks + U - 1) / U, cb, ce);
+    const PixChunk *s_ct = block_chunk_table<U>(a, s_ctab, cb, ce);
+    int p[E], t[E];
     for (long long c = cb; c < ce; ++c) {
-        pix_load<false>(a.segs, a.n_segs, c, a.pid_off, p, t);
+        unit_load<U, E, false>(a, s_ct, cb * U, c, p, t);
 #pragma unroll
-        for (int e = 0; e < kPixEPT; ++e) {
+        for (int e = 0; e < E; ++e) {
             const uint32_t q = (uint32_t)p[e] - (uint32_t)a.pid_off;
             if (q < a.L) atomicAdd(&s_cnt[q >> a.rb], 1u);
         }
         __syncthreads();
-        for (int r = threadIdx.x; r < a.nr; r += kPixThreads) {
+        for (int r = threadIdx.x; r < a.nr; r += NT) {
             s_tot[r] += (s_cnt[r] + 3u) & ~3u;
             s_cnt[r] = 0;
         }
         __syncthreads();
     }
-    for (int r = threadIdx.x; r < a.nr; r += kPixThreads) a.counts[(size_t)blockIdx.x * a.nr + r] = s_tot[r];
+    for (int r = threadIdx.x; r < a.nr; r += NT) a.counts[(size_t)blockIdx.x * a.nr + r] = s_tot[r];
 }
 
 // One block per range r: its total over the blocks and the exclusive prefix
@@ -131,7 +216,8 @@ __global__ __launch_bounds__(1024) void k_pix_scan_blocks(PixArgs a, int grid,
 }
 
 // One block of 1024 threads, thread r = range r: range starts (rstart) and
-// work items, every range split into pieces of at most item_events.
+// work items, every range split into pieces of at most item_events (a
+// multiple of 4, so items hold whole groups).
 __global__ __launch_bounds__(1024) void k_pix_scan(PixArgs a, const uint32_t *__restrict__ rtot,
                                                    uint32_t item_events, uint4 *__restrict__ items,
                                                    uint32_t *__restrict__ item_count, int max_items) {
@@ -157,71 +243,87 @@ __global__ __launch_bounds__(1024) void k_pix_scan(PixArgs a, const uint32_t *__
     }
 }
 
-// LDS: staging (kChunk u32) | counts, chunk offsets, cursors (nr each) |
-// scan scratch (32) | TOA image
-size_t pix_scatter_smem(const ToaParams &tp) {
-    return 4 * ((size_t)kChunk + 4 * (size_t)kPixMaxRanges + 3 * (size_t)kPixMaxRanges + 32) +
-           toa_lds_bytes(tp);
+// LDS: staging (unit events + pads, u32) | counts, unit offsets, cursors,
+// staging positions (nr each) | scan scratch (32) | chunk table | TOA image
+size_t pix_scatter_smem(const ToaParams &tp, int unit) {
+    return 4 * ((size_t)unit * kChunk + 4 * (size_t)kPixMaxRanges + 4 * (size_t)kPixMaxRanges + 32) +
+           sizeof(PixChunk) * kPixLdsChunks + toa_lds_bytes(tp);
 }
 
-template <bool FAST>
-__global__ __launch_bounds__(kPixThreads) void k_pix_scatter(PixArgs a) {
+template <int U, int E, bool P24, bool FAST>
+__global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
+    constexpr int NT = U * kChunk / E;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *s_stg = reinterpret_cast<uint32_t *>(smem);
-    uint32_t *s_cnt = s_stg + kChunk + 4 * kPixMaxRanges;  // staging holds the pads too
+    uint32_t *s_cnt = s_stg + U * kChunk + 4 * kPixMaxRanges;  // staging holds the pads too
     uint32_t *s_off = s_cnt + kPixMaxRanges;
     uint32_t *s_cur = s_off + kPixMaxRanges;
-    uint32_t *s_w = s_cur + kPixMaxRanges;
-    unsigned char *s_tab = reinterpret_cast<unsigned char *>(s_w + 32);
+    uint32_t *s_pos = s_cur + kPixMaxRanges;
+    uint32_t *s_w = s_pos + kPixMaxRanges;
+    PixChunk *s_ctab = reinterpret_cast<PixChunk *>(s_w + 32);
+    unsigned char *s_tab = reinterpret_cast<unsigned char *>(s_ctab + kPixLdsChunks);
     load_toa_tables(s_tab, a.tab, a.tp);
     const int tid = threadIdx.x;
-    for (int r = tid; r < a.nr; r += kPixThreads) {
+    for (int r = tid; r < a.nr; r += NT) {
         s_cnt[r] = 0;
         s_cur[r] = a.rstart[r] + a.counts[(size_t)blockIdx.x * a.nr + r];  // this block's slot of range r
     }
-    __syncthreads();
     const uint32_t mask = (1u << a.rb) - 1u;
     long long cb, ce;
-    block_chunks(a.n_chunks, cb, ce);
-    int p[kPixEPT], t[kPixEPT];
-    if (cb < ce) pix_load<true>(a.segs, a.n_segs, cb, a.pid_off, p, t);
+    block_units((a.n_chunks + U - 1) / U, cb, ce);
+    const PixChunk *s_ct = block_chunk_table<U>(a, s_ctab, cb, ce);  // (+ the barrier for s_cnt, s_cur)
+    int p[E], t[E];
+    if (cb < ce) unit_load<U, E, true>(a, s_ct, cb * U, cb, p, t);
     for (long long c = cb; c < ce; ++c) {
-        uint32_t word[kPixEPT], rank[kPixEPT];
+        // pass 1: the events' words and their ranges' counts; only the words
+        // stay live across the scan (registers: the next unit's loads are in
+        // flight at the same time), pass 2 takes the slots
+        uint32_t word[E];
 #pragma unroll
-        for (int e = 0; e < kPixEPT; ++e) {
+        for (int e = 0; e < E; ++e) {
             const uint32_t q = (uint32_t)p[e] - (uint32_t)a.pid_off;
-            const int b = toa_bin<FAST>(t[e], s_tab, a.tp);
+            const int b = pix_toa_bin<FAST>(t[e], s_tab, a.tp);
             const uint32_t r = q >> a.rb;
             word[e] = q < a.L ? ((r << 24) | (b < 0 ? kPixDropped : ((q & mask) | ((uint32_t)b << a.rb))))
-                              : 0xFFFFFFFFu;
-            rank[e] = q < a.L ? atomicAdd(&s_cnt[r], 1u) : 0xFFFFFFFFu;  // unknown id: no slot
+                              : 0xFFFFFFFFu;  // unknown id: no slot
+            if (q < a.L) atomicAdd(&s_cnt[r], 1u);
+            asm volatile("" : "+v"(word[e]));  // materialized here, not recomputed after the scan
         }
-        // the next chunk's events load while this one is partitioned
-        if (c + 1 < ce) pix_load<true>(a.segs, a.n_segs, c + 1, a.pid_off, p, t);
+        // the next unit's events load while this one is partitioned (not
+        // hoisted above the words: both sets live would double the registers)
+        __builtin_amdgcn_sched_barrier(0);
+        if (c + 1 < ce) unit_load<U, E, true>(a, s_ct, cb * U, c + 1, p, t);
         __syncthreads();
         // runs padded to 4: staging offsets, slot cursors and the pads are
-        // 16-byte aligned groups
+        // whole groups
         uint32_t v = 0, total;
-        if (tid < a.nr) v = (s_cnt[tid] + 3u) & ~3u;  // nr <= kPixMaxRanges <= kPixThreads
+        if (tid < a.nr) v = (s_cnt[tid] + 3u) & ~3u;  // nr <= kPixMaxRanges <= NT
         const uint32_t off = block_exclusive_scan(v, s_w, &total);
         if (tid < a.nr) {
             s_off[tid] = off;
+            s_pos[tid] = off;
             for (uint32_t j = s_cnt[tid]; j < v; ++j) s_stg[off + j] = ((uint32_t)tid << 24) | kPixDropped;
         }
         __syncthreads();
 #pragma unroll
-        for (int e = 0; e < kPixEPT; ++e)
-            if (rank[e] != 0xFFFFFFFFu) s_stg[s_off[word[e] >> 24] + rank[e]] = word[e];
+        for (int e = 0; e < E; ++e)
+            if (word[e] != 0xFFFFFFFFu) s_stg[atomicAdd(&s_pos[word[e] >> 24], 1u)] = word[e];
         __syncthreads();
-        // a 4-group never straddles two runs; its slot position is 4-aligned
-        for (uint32_t g = (uint32_t)tid * 4u; g < total; g += kPixThreads * 4u) {
+        // a group never straddles two runs; its slot position is 4-aligned
+        for (uint32_t g = (uint32_t)tid * 4u; g < total; g += NT * 4u) {
             const uint4 w = *reinterpret_cast<const uint4 *>(s_stg + g);
             const uint32_t r = w.x >> 24;
-            *reinterpret_cast<uint4 *>(a.payload + s_cur[r] + (g - s_off[r])) =
-                make_uint4(w.x & 0xFFFFFFu, w.y & 0xFFFFFFu, w.z & 0xFFFFFFu, w.w & 0xFFFFFFu);
+            const uint32_t dst = s_cur[r] + (g - s_off[r]);
+            if (P24) {
+                *(g_v3u *)(reinterpret_cast<unsigned char *>(a.payload) + (size_t)dst * 3u) =
+                    pack24(w.x & 0xFFFFFFu, w.y & 0xFFFFFFu, w.z & 0xFFFFFFu, w.w & 0xFFFFFFu);
+            } else {
+                *reinterpret_cast<uint4 *>(a.payload + dst) =
+                    make_uint4(w.x & 0xFFFFFFu, w.y & 0xFFFFFFu, w.z & 0xFFFFFFu, w.w & 0xFFFFFFu);
+            }
         }
         __syncthreads();
-        for (int r = tid; r < a.nr; r += kPixThreads) {
+        for (int r = tid; r < a.nr; r += NT) {
             s_cur[r] += (s_cnt[r] + 3u) & ~3u;
             s_cnt[r] = 0;
         }
@@ -229,11 +331,12 @@ __global__ __launch_bounds__(kPixThreads) void k_pix_scatter(PixArgs a) {
     }
 }
 
-// LDS: LUT slice (2^rb u16) | footprint counters (F x T u32)
+// LDS: LUT slice (2^rb u16) | footprint counters (F x T u32) | 64 dummies
 size_t pix_acc_smem(int rb, int fmax, int T) {
-    return align16(((size_t)2 << rb)) + 4 * (size_t)fmax * (size_t)T;
+    return align16(((size_t)2 << rb)) + 4 * (size_t)fmax * (size_t)T + 4 * 64;
 }
 
+template <bool P24>
 __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16_t *__restrict__ loc,
                                                          const uint32_t *__restrict__ fp_off,
                                                          const uint32_t *__restrict__ fp_scr,
@@ -253,45 +356,63 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
     for (uint32_t j = threadIdx.x; j < span; j += blockDim.x)
         s_loc[j] = q0 + j < a.L ? loc[q0 + j] : (uint16_t)0xFFFFu;
     for (uint32_t j = threadIdx.x; j < nbin; j += blockDim.x) s_cnt[j] = 0;
-    __syncthreads();
     const uint32_t mask = span - 1u;
-    const uint32_t e0 = it.y, e1 = it.z;
-    auto add = [&](uint32_t w) __attribute__((always_inline)) {
-        if (w == kPixDropped) return;
-        const uint32_t f = s_loc[w & mask];
-        if (f != 0xFFFFu) atomicAdd(&s_cnt[f * (uint32_t)T + (w >> a.rb)], 1u);
-    };
-    // head to a 16-byte boundary, then four payloads per lane
-    const uint32_t h = e0 + ((4u - (e0 & 3u)) & 3u) < e1 ? e0 + ((4u - (e0 & 3u)) & 3u) : e1;
-    if (threadIdx.x < h - e0) add(a.payload[e0 + threadIdx.x]);
-    const uint32_t n4 = (e1 - h) >> 2;
-    // U groups of 4 per lane and iteration, the next iteration's loads issued
-    // before this one's LDS work (the loop is otherwise load-latency bound)
+    // events the view drops and pads count into a lane-private dummy word
+    // past the footprint, so no lane branches around its LDS atomic
+    const uint32_t dummy = nbin + (threadIdx.x & 63u);
+    for (uint32_t j = threadIdx.x; j < 64; j += blockDim.x) s_cnt[nbin + j] = 0;
+    // items hold whole groups of four payloads (run lengths, range starts and
+    // item sizes are multiples of 4); U groups per lane and iteration, the
+    // next iteration's loads issued before this one's LDS work.  Loads are
+    // unconditional (index clamped, the surplus marked dropped afterwards), so
+    // the compiler does not wait for each inside its own branch.
+    const uint32_t g0 = it.y >> 2, n4 = (it.z - it.y) >> 2;  // n4 >= 1 (items of non-empty ranges)
     constexpr int U = 4;
-    const int *pl = reinterpret_cast<const int *>(a.payload) + h;
     const uint32_t step = blockDim.x * U;
-    v4i cur[U], nxt[U];
-    uint32_t i0 = threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t i = i0 + u * blockDim.x;
-        cur[u] = i < n4 ? ld_stream4(pl + 4 * i) : v4i{-1, -1, -1, -1};
-    }
-    for (; i0 < n4; i0 += step) {
+    // raw groups (4 words; 3 used with 24-bit payloads), unpacked at use
+    auto ld = [&](uint32_t i) __attribute__((always_inline)) -> v4i {
+        const uint32_t ic = i < n4 ? i : n4 - 1u;
+        if (P24) {
+            const v3u w = __builtin_nontemporal_load(
+                (const g_v3u *)(reinterpret_cast<const unsigned char *>(a.payload) + (size_t)(g0 + ic) * 12u));
+            return v4i{(int)w[0], (int)w[1], (int)w[2], 0};
+        }
+        return ld_stream4(reinterpret_cast<const int *>(a.payload) + (size_t)(g0 + ic) * 4u);
+    };
+    auto add4 = [&](const v4i (&raw)[U], uint32_t ib) __attribute__((always_inline)) {
+        uint32_t w[U][4], f[U][4];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t i = i0 + step + u * blockDim.x;
-            nxt[u] = i < n4 ? ld_stream4(pl + 4 * i) : v4i{-1, -1, -1, -1};
+            if (P24) {
+                unpack24(v3u{(uint32_t)raw[u][0], (uint32_t)raw[u][1], (uint32_t)raw[u][2]}, w[u]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) w[u][q] = (uint32_t)raw[u][q] & 0xFFFFFFu;
+            }
+            if (ib + u * blockDim.x >= n4) w[u][0] = w[u][1] = w[u][2] = w[u][3] = kPixDropped;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) f[u][q] = s_loc[w[u][q] & mask];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) add((uint32_t)cur[u][q] & 0xFFFFFFu);
+            for (int q = 0; q < 4; ++q) {
+                const bool ok = w[u][q] != kPixDropped && f[u][q] != 0xFFFFu;
+                atomicAdd(&s_cnt[ok ? f[u][q] * (uint32_t)T + (w[u][q] >> a.rb) : dummy], 1u);
+            }
+    };
+    __syncthreads();
+    v4i cur[U], nxt[U];
+    uint32_t i0 = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = ld(i0 + u * blockDim.x);
+    for (; i0 < n4; i0 += step) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) nxt[u] = ld(i0 + step + u * blockDim.x);
+        add4(cur, i0);
 #pragma unroll
         for (int u = 0; u < U; ++u) cur[u] = nxt[u];
     }
-    const uint32_t tail = h + 4 * n4;
-    if (tail + threadIdx.x < e1) add(a.payload[tail + threadIdx.x]);
     __syncthreads();
     // flush: consecutive counters of one screen row are consecutive bins
     for (uint32_t j = threadIdx.x; j < nbin; j += blockDim.x) {
@@ -303,32 +424,58 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
     }
 }
 
+namespace {
+template <int U, int E, bool P24>
+void launch_pass_a(const PixArgs &a, uint32_t item_events, int max_items, uint4 *items,
+                   uint32_t *item_count, hipStream_t st) {
+    constexpr int NT = U * kChunk / E;
+    hipLaunchKernelGGL(k_pix_chunks, dim3((unsigned)((a.n_chunks + 255) / 256)), dim3(256), 0, st, a,
+                       const_cast<PixChunk *>(a.ctab));
+    hipLaunchKernelGGL((k_pix_count<U, E>), dim3(a.grid), dim3(NT), 0, st, a);
+    hipLaunchKernelGGL(k_pix_scan_blocks, dim3(a.nr), dim3(1024), 0, st, a, a.grid, a.rstart + a.nr + 1);
+    hipLaunchKernelGGL(k_pix_scan, dim3(1), dim3(1024), 0, st, a, a.rstart + a.nr + 1, item_events,
+                       items, item_count, max_items);
+    const size_t sm = pix_scatter_smem(a.tp, U);
+    if (a.tp.fast) {
+        (void)hipFuncSetAttribute((const void *)k_pix_scatter<U, E, P24, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL((k_pix_scatter<U, E, P24, true>), dim3(a.grid), dim3(NT), sm, st, a);
+    } else {
+        (void)hipFuncSetAttribute((const void *)k_pix_scatter<U, E, P24, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL((k_pix_scatter<U, E, P24, false>), dim3(a.grid), dim3(NT), sm, st, a);
+    }
+}
+template <bool P24>
+void launch_pass_a_shape(const PixArgs &a, uint32_t item_events, int max_items, uint4 *items,
+                         uint32_t *item_count, hipStream_t st) {
+    if (a.unit == 2) launch_pass_a<2, 16, P24>(a, item_events, max_items, items, item_count, st);
+    else if (a.ept == 8) launch_pass_a<1, 8, P24>(a, item_events, max_items, items, item_count, st);
+    else launch_pass_a<1, 16, P24>(a, item_events, max_items, items, item_count, st);
+}
+}  // namespace
+
 hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32_t item_events,
                         int max_items, uint4 *items, uint32_t *item_count, uint32_t *hist,
                         hipStream_t st, int phase) {
-    if (a.nr > kPixMaxRanges || a.nr > 1024) return hipErrorInvalidValue;
+    if (a.nr > kPixMaxRanges || a.nr > 1024 || (item_events & 3u) || (a.unit != 1 && a.unit != 2) ||
+        (a.ept != 8 && a.ept != 16) || (a.unit == 2 && a.ept != 16))
+        return hipErrorInvalidValue;
     if (phase == 0) {
-        hipLaunchKernelGGL(k_pix_count, dim3(a.grid), dim3(kPixThreads), 0, st, a);
-        hipLaunchKernelGGL(k_pix_scan_blocks, dim3(a.nr), dim3(1024), 0, st, a, a.grid, a.rstart + a.nr + 1);
-        hipLaunchKernelGGL(k_pix_scan, dim3(1), dim3(1024), 0, st, a, a.rstart + a.nr + 1, item_events,
-                           items, item_count, max_items);
-        const size_t sm = pix_scatter_smem(a.tp);
-        if (a.tp.fast) {
-            (void)hipFuncSetAttribute((const void *)k_pix_scatter<true>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-            hipLaunchKernelGGL(k_pix_scatter<true>, dim3(a.grid), dim3(kPixThreads), sm, st, a);
-        } else {
-            (void)hipFuncSetAttribute((const void *)k_pix_scatter<false>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-            hipLaunchKernelGGL(k_pix_scatter<false>, dim3(a.grid), dim3(kPixThreads), sm, st, a);
-        }
+        if (a.p24) launch_pass_a_shape<true>(a, item_events, max_items, items, item_count, st);
+        else launch_pass_a_shape<false>(a, item_events, max_items, items, item_count, st);
     } else {
         const size_t sm = pix_acc_smem(s.rb, s.fmax, a.tp.T);
-        (void)hipFuncSetAttribute((const void *)k_pix_accumulate,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL(k_pix_accumulate, dim3((unsigned)max_items), dim3(1024), sm, st, a,
-                           s.loc + (size_t)replica * a.L, s.fp_off, s.fp_scr, items, item_count,
-                           a.tp.T, hist);
+        const void *k = a.p24 ? (const void *)k_pix_accumulate<true> : (const void *)k_pix_accumulate<false>;
+        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        if (a.p24)
+            hipLaunchKernelGGL(k_pix_accumulate<true>, dim3((unsigned)max_items), dim3(1024), sm, st, a,
+                               s.loc + (size_t)replica * a.L, s.fp_off, s.fp_scr, items, item_count,
+                               a.tp.T, hist);
+        else
+            hipLaunchKernelGGL(k_pix_accumulate<false>, dim3((unsigned)max_items), dim3(1024), sm, st, a,
+                               s.loc + (size_t)replica * a.L, s.fp_off, s.fp_scr, items, item_count,
+                               a.tp.T, hist);
     }
     return hipGetLastError();
 }
