@@ -180,7 +180,7 @@ struct lde_handle {
     lde::PixChunk *d_pctab = nullptr;
     size_t pctab_cap = 0;
     uint32_t *d_pitem_count = nullptr;
-    int pix_grid = 0, pix_unit = 2, pix_ept = 16;
+    int pix_grid = 0, pix_unit = 2, pix_ept = 16, pix_bu = 4, pix_items_per_cu = 2;
     bool pix24 = true;
     std::vector<double> edges;  // the create-time edges (event unit)
     // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
@@ -1112,8 +1112,9 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         return rc;
     // pass-B items: a few per CU (LDS: one block per CU), and a range's
     // footprint flush per item, so not many more; whole groups of 4 payloads
+    const long long ipc = h->pix_items_per_cu;
     const long long per =
-        (std::max<long long>(65536, (total + 2LL * h->cus - 1) / (2LL * h->cus)) + 3) & ~3LL;
+        (std::max<long long>(65536, (total + ipc * h->cus - 1) / (ipc * h->cus)) + 3) & ~3LL;
     const long long max_items = total / per + h->pix.nr + 1;
     if (int rc = grow(h, &h->d_pitems, h->pitems_cap, (size_t)max_items)) return rc;
     if (int rc = grow(h, &h->d_pctab, h->pctab_cap, (size_t)chunks)) return rc;
@@ -1127,6 +1128,7 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.L = (unsigned)h->L;
     a.rb = h->pix.rb;
     a.nr = h->pix.nr;
+    a.rs = h->pix.rs;
     a.tab = h->d_tab;
     a.tp = h->tp;
     a.counts = h->d_pcounts;
@@ -1134,6 +1136,7 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.payload = h->d_ppayload;
     a.unit = h->pix_unit;
     a.p24 = h->pix24 ? 1 : 0;
+    a.bu = h->pix_bu;
     a.grid = (int)std::min<long long>(units, (long long)h->pix_grid);
     {
         Timed tm(h, LDE_K_PIXEL);
@@ -1317,12 +1320,25 @@ int build_pixel(lde_handle *h, const int32_t *lut) {
     if (h->monitor || h->n_tiles == 0 || env_ll("LDE_PIXEL", 1) == 0) return LDE_OK;
     const long long L = h->L, R = h->R, S = h->S;
     const int T = h->T;
+    // ranges of 2^rb pixels: the smallest rb with at most 256 ranges
+    // (LDE_PIX_MAX_RANGES, up to kPixMaxRanges; LOKI bank 0: 196 ranges of 4096
+    // pixels; 392 of 2048 keep the same 288-screen widest footprint, so pass B
+    // gains nothing and pass A's runs get shorter)
+    const long long max_nr = std::max<long long>(
+        1, std::min<long long>(lde::kPixMaxRanges, env_ll("LDE_PIX_MAX_RANGES", 256)));
     int rb = 8;
-    while (rb < 20 && ((L + (1LL << rb) - 1) >> rb) > lde::kPixMaxRanges) ++rb;
+    while (rb < 20 && ((L + (1LL << rb) - 1) >> rb) > max_nr) ++rb;
     int tbits = 0;
     while ((1 << tbits) < T) ++tbits;
-    if (rb + tbits > 24) return LDE_OK;  // payload: local pixel | bin << rb in 24 bits
     const int nr = (int)((L + (1LL << rb) - 1) >> rb);
+    // scatter staging word: range (rbits, the all-ones range never used) above
+    // an rs-bit payload whose all-ones value is the dropped marker; stored
+    // payloads are 24-bit (0xFFFFFF dropped), so local pixel | bin << rb
+    // must stay below both
+    int rbits = 0;
+    while ((1 << rbits) < nr + 1) ++rbits;
+    const int rs = 32 - rbits;
+    if (rb + tbits > std::min(23, rs - 1)) return LDE_OK;
     std::vector<int> stamp((size_t)S, -1), pos((size_t)S, 0);
     std::vector<uint32_t> fp_off((size_t)nr + 1, 0), fp;
     std::vector<uint16_t> loc((size_t)(R * L), 0xFFFF);
@@ -1366,10 +1382,12 @@ int build_pixel(lde_handle *h, const int32_t *lut) {
     h->pix_unit = (int)std::max<long long>(1, std::min<long long>(2, env_ll("LDE_PIX_UNIT", 2)));
     h->pix_ept = h->pix_unit == 2 || env_ll("LDE_PIX_EPT", 8) == 16 ? 16 : 8;
     h->pix24 = env_ll("LDE_PIX24", 1) != 0;
+    h->pix_bu = env_ll("LDE_PIX_BU", 4) == 8 ? 8 : 4;
+    h->pix_items_per_cu = (int)std::max<long long>(1, std::min<long long>(16, env_ll("LDE_PIX_ITEMS", 2)));
     // blocks of unit * kChunk / ept threads: 4 x 512 or 2 x 1024 per CU
     h->pix_grid = (int)std::max<long long>(
         1, env_ll("LDE_PIX_GRID", (h->pix_ept == 16 && h->pix_unit == 1 ? 4 : 2) * (long long)h->cus));
-    while (h->pix_unit > 1 && lde::pix_scatter_smem(h->tp, h->pix_unit) > 80 * 1024) --h->pix_unit;
+    while (h->pix_unit > 1 && lde::pix_scatter_smem(h->tp, h->pix_unit) > 150 * 1024) --h->pix_unit;
     if (lde::pix_scatter_smem(h->tp, h->pix_unit) > 160 * 1024) return LDE_OK;
     if (!h->d_pcounts) {
         if (int rc = dev_alloc(h, &h->d_pcounts, (size_t)h->pix_grid * lde::kPixMaxRanges)) return rc;
@@ -1378,6 +1396,7 @@ int build_pixel(lde_handle *h, const int32_t *lut) {
     }
     h->pix.rb = rb;
     h->pix.nr = nr;
+    h->pix.rs = rs;
     h->pix.fmax = fmax;
     h->pix.loc = h->d_ploc;
     h->pix.fp_off = h->d_pfp_off;

@@ -369,7 +369,7 @@ hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigne
 
 // PIXEL strategy (lde_pixel.hip): events partitioned by pixel range, the
 // LUT lookup done in pass B from the range's LDS slice
-constexpr int kPixMaxRanges = 256;
+constexpr int kPixMaxRanges = 512;
 struct PixChunk {                // one chunk of the batch (k_pix_chunks)
     const int *pid;
     const int *toa;
@@ -385,6 +385,7 @@ struct PixArgs {
     unsigned L;
     int rb;                      // range of pixel q: q >> rb
     int nr;                      // ranges (<= kPixMaxRanges)
+    int rs;                      // scatter staging word: range << rs | payload (rs bits)
     const unsigned char *tab;    // TOA lookup image
     ToaParams tp;
     uint32_t *counts;            // [grid][nr] events, then payload offsets
@@ -395,9 +396,10 @@ struct PixArgs {
     int unit = 1;                // chunks per partition step (runs padded per unit)
     int ept = 8;                 // events per thread and load: unit * kChunk / ept threads
     int p24 = 1;                 // 3-byte payloads
+    int bu = 4;                  // pass B: groups per lane in flight (4 or 8)
 };
 struct PixSetup {                // setup-time tables (lde_create / lde_set_lut)
-    int rb = 0, nr = 0, fmax = 0;
+    int rb = 0, nr = 0, fmax = 0, rs = 24;
     const uint16_t *loc = nullptr;     // [R][L] footprint-local screen of every pixel (0xFFFF: dropped)
     const uint32_t *fp_off = nullptr;  // [nr + 1] footprint list offsets
     const uint32_t *fp_scr = nullptr;  // footprint screens, range after range

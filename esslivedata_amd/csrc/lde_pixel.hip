@@ -269,6 +269,9 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
         s_cur[r] = a.rstart[r] + a.counts[(size_t)blockIdx.x * a.nr + r];  // this block's slot of range r
     }
     const uint32_t mask = (1u << a.rb) - 1u;
+    // staging word: range << rs | payload (rs bits, all ones = dropped); the
+    // stored payloads are 24-bit with 0xFFFFFF = dropped
+    const uint32_t dmask = (1u << a.rs) - 1u;
     long long cb, ce;
     block_units((a.n_chunks + U - 1) / U, cb, ce);
     const PixChunk *s_ct = block_chunk_table<U>(a, s_ctab, cb, ce);  // (+ the barrier for s_cnt, s_cur)
@@ -284,7 +287,7 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
             const uint32_t q = (uint32_t)p[e] - (uint32_t)a.pid_off;
             const int b = pix_toa_bin<FAST>(t[e], s_tab, a.tp);
             const uint32_t r = q >> a.rb;
-            word[e] = q < a.L ? ((r << 24) | (b < 0 ? kPixDropped : ((q & mask) | ((uint32_t)b << a.rb))))
+            word[e] = q < a.L ? ((r << a.rs) | (b < 0 ? dmask : ((q & mask) | ((uint32_t)b << a.rb))))
                               : 0xFFFFFFFFu;  // unknown id: no slot
             if (q < a.L) atomicAdd(&s_cnt[r], 1u);
             asm volatile("" : "+v"(word[e]));  // materialized here, not recomputed after the scan
@@ -302,24 +305,28 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
         if (tid < a.nr) {
             s_off[tid] = off;
             s_pos[tid] = off;
-            for (uint32_t j = s_cnt[tid]; j < v; ++j) s_stg[off + j] = ((uint32_t)tid << 24) | kPixDropped;
+            for (uint32_t j = s_cnt[tid]; j < v; ++j) s_stg[off + j] = ((uint32_t)tid << a.rs) | dmask;
         }
         __syncthreads();
 #pragma unroll
         for (int e = 0; e < E; ++e)
-            if (word[e] != 0xFFFFFFFFu) s_stg[atomicAdd(&s_pos[word[e] >> 24], 1u)] = word[e];
+            if (word[e] != 0xFFFFFFFFu) s_stg[atomicAdd(&s_pos[word[e] >> a.rs], 1u)] = word[e];
         __syncthreads();
         // a group never straddles two runs; its slot position is 4-aligned
         for (uint32_t g = (uint32_t)tid * 4u; g < total; g += NT * 4u) {
             const uint4 w = *reinterpret_cast<const uint4 *>(s_stg + g);
-            const uint32_t r = w.x >> 24;
+            const uint32_t r = w.x >> a.rs;
+            auto pl = [&](uint32_t x) __attribute__((always_inline)) {
+                const uint32_t v = x & dmask;
+                return v == dmask ? kPixDropped : v;
+            };
             const uint32_t dst = s_cur[r] + (g - s_off[r]);
             if (P24) {
                 *(g_v3u *)(reinterpret_cast<unsigned char *>(a.payload) + (size_t)dst * 3u) =
-                    pack24(w.x & 0xFFFFFFu, w.y & 0xFFFFFFu, w.z & 0xFFFFFFu, w.w & 0xFFFFFFu);
+                    pack24(pl(w.x), pl(w.y), pl(w.z), pl(w.w));
             } else {
                 *reinterpret_cast<uint4 *>(a.payload + dst) =
-                    make_uint4(w.x & 0xFFFFFFu, w.y & 0xFFFFFFu, w.z & 0xFFFFFFu, w.w & 0xFFFFFFu);
+                    make_uint4(pl(w.x), pl(w.y), pl(w.z), pl(w.w));
             }
         }
         __syncthreads();
@@ -336,7 +343,7 @@ size_t pix_acc_smem(int rb, int fmax, int T) {
     return align16(((size_t)2 << rb)) + 4 * (size_t)fmax * (size_t)T + 4 * 64;
 }
 
-template <bool P24>
+template <bool P24, int U>
 __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16_t *__restrict__ loc,
                                                          const uint32_t *__restrict__ fp_off,
                                                          const uint32_t *__restrict__ fp_scr,
@@ -367,7 +374,6 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
     // unconditional (index clamped, the surplus marked dropped afterwards), so
     // the compiler does not wait for each inside its own branch.
     const uint32_t g0 = it.y >> 2, n4 = (it.z - it.y) >> 2;  // n4 >= 1 (items of non-empty ranges)
-    constexpr int U = 4;
     const uint32_t step = blockDim.x * U;
     // raw groups (4 words; 3 used with 24-bit payloads), unpacked at use
     auto ld = [&](uint32_t i) __attribute__((always_inline)) -> v4i {
@@ -466,16 +472,17 @@ hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32
         else launch_pass_a_shape<false>(a, item_events, max_items, items, item_count, st);
     } else {
         const size_t sm = pix_acc_smem(s.rb, s.fmax, a.tp.T);
-        const void *k = a.p24 ? (const void *)k_pix_accumulate<true> : (const void *)k_pix_accumulate<false>;
-        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        if (a.p24)
-            hipLaunchKernelGGL(k_pix_accumulate<true>, dim3((unsigned)max_items), dim3(1024), sm, st, a,
+        auto go = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+            hipLaunchKernelGGL(kern, dim3((unsigned)max_items), dim3(1024), sm, st, a,
                                s.loc + (size_t)replica * a.L, s.fp_off, s.fp_scr, items, item_count,
                                a.tp.T, hist);
-        else
-            hipLaunchKernelGGL(k_pix_accumulate<false>, dim3((unsigned)max_items), dim3(1024), sm, st, a,
-                               s.loc + (size_t)replica * a.L, s.fp_off, s.fp_scr, items, item_count,
-                               a.tp.T, hist);
+        };
+        if (a.p24) {
+            if (a.bu == 8) go(k_pix_accumulate<true, 8>); else go(k_pix_accumulate<true, 4>);
+        } else {
+            if (a.bu == 8) go(k_pix_accumulate<false, 8>); else go(k_pix_accumulate<false, 4>);
+        }
     }
     return hipGetLastError();
 }
