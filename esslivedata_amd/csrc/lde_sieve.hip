@@ -851,7 +851,7 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(ColdArgs c) {
     uint32_t *s_tot = s_delta + nt4;               // [tile] piece total -> run base
     uint32_t *s_w = s_tot + nt4;
     const int tid = threadIdx.x;
-    const int wv = tid >> 6, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave-uniform: SGPR buffer descriptors
     // block = (sieve block, wave group); boff / tcnt rows are (block, group)
     const int b = blockIdx.x / kColdGroups, grp = blockIdx.x % kColdGroups;
     const int row = blockIdx.x;
@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4,
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     const int nt4 = align4(n_tiles);
     const int tid = threadIdx.x;
-    const int wv = tid >> 6, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave-uniform: SGPR buffer descriptors
     uint32_t *s_pos = sm;         // [tile] the block's next global position
     uint32_t *s_w = sm + nt4;     // scan scratch
     uint32_t *s_wave = s_w + 32;  // per wave: image | base | delta
@@ -1175,7 +1175,7 @@ void k_cold_sort_a(ColdArgs c) {
     uint4 *s_carry = reinterpret_cast<uint4 *>(s_cn + nt4);  // [tile] 8 carried u16
     uint32_t *s_w = reinterpret_cast<uint32_t *>(s_carry + nt4);
     const int tid = threadIdx.x;
-    const int wv = tid >> 6, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave-uniform: SGPR buffer descriptors
     const int b = blockIdx.x / kColdGroups, grp = blockIdx.x % kColdGroups;
     const int row = blockIdx.x;
     constexpr int NW = kSplitThreads / 64;
@@ -1334,35 +1334,48 @@ __global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
     const uint32_t *__restrict__ item_count, uint32_t *__restrict__ hist, long long n_bins,
     int tail_release) {
     constexpr int NB = 1 << TB;
-    __shared__ __attribute__((aligned(16))) uint32_t s_tile[NB];
+    // + 64 lane-private dummy counters: pads and keys outside the item count
+    // there, so no lane branches around its LDS atomic
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[NB + 64];
     if (blockIdx.x >= *item_count) return;
     const uint4 it = items[blockIdx.x];
-    for (int i = threadIdx.x * 4; i < NB; i += kTileThreads * 4)
+    for (int i = threadIdx.x * 4; i < NB + 64; i += kTileThreads * 4)
         *reinterpret_cast<uint4 *>(s_tile + i) = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    // four 16-byte loads (32 keys) per thread in flight per iteration
+    const uint32_t dummy = NB + (threadIdx.x & 63u);
+    // 16-byte groups of 8 keys; four per thread per iteration, the next
+    // iteration's four issued before this one's atomics (indices clamped so
+    // every load is unconditional; keys outside [it.y, it.z) count into the
+    // dummy)
+    constexpr uint32_t STEP = kTileThreads * 32u;
     const uint32_t k0 = it.y & ~7u;
-    for (uint32_t i0 = k0 + (uint32_t)threadIdx.x * 8u; i0 < it.z; i0 += kTileThreads * 32u) {
-        uint4 v[4];
+    const uint32_t last = (it.z - 1u) & ~7u;  // the item's last group (it.z > it.y)
+    auto ld = [&](uint32_t i) __attribute__((always_inline)) {
+        return *reinterpret_cast<const uint4 *>(keys + (i <= last ? i : last));
+    };
+    uint4 cur[4], nxt[4];
+    uint32_t i0 = k0 + (uint32_t)threadIdx.x * 8u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = ld(i0 + (uint32_t)u * kTileThreads * 8u);
+    for (; i0 < it.z; i0 += STEP) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) nxt[u] = ld(i0 + STEP + (uint32_t)u * kTileThreads * 8u);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t i = i0 + (uint32_t)u * kTileThreads * 8u;
-            v[u] = i < it.z ? *reinterpret_cast<const uint4 *>(keys + i) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t i = i0 + (uint32_t)u * kTileThreads * 8u;
-            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            const uint32_t w[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const uint32_t idx = i + (uint32_t)q;
                 const uint32_t key = (w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu;
                 // 0xFFFF: pad of an aligned range (never a key: tile_bits <= 15)
-                if (idx >= it.y && idx < it.z && key != 0xFFFFu)
-                    __hip_atomic_fetch_add(s_tile + key, 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                const bool ok = idx >= it.y && idx < it.z && key != 0xFFFFu;
+                __hip_atomic_fetch_add(s_tile + (ok ? key : dummy), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
     }
     __syncthreads();
     // a tile's only item owns its bins (hot rows are other screens, added by
