@@ -39,7 +39,7 @@ KERNEL_SYMBOL = {
     'page_accumulate': 'k_page_accumulate',
     'split': 'k_sieve',  # SPLIT's event pass (k_split when LDE_SIEVE=0)
     'coord': 'k_event_key',  # wavelength-mode coordinate pass (keyed; k_event_coord otherwise)
-    'pixel': 'k_pix_scatter',  # PIXEL pass A (with k_pix_count + k_pix_scan in the bucket)
+    'pixel': 'pix_pass_a',  # PIXEL pass A: k_pix_chunks + k_pix_count + scans + k_pix_scatter
     'page_accumulate': 'k_page_accumulate',
     'finalize': 'k_finalize_v4',
 }
@@ -64,7 +64,7 @@ def parse():
                          'lookup table (diagnostic line, not the headline metric)')
     ap.add_argument('--pulses', type=int, default=14)
     ap.add_argument('--events-per-pulse', type=int, default=10_000_000)
-    ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition', 'paged', 'split'])
+    ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition', 'paged', 'split', 'pixel'])
     ap.add_argument('--view', default='geometric',
                     choices=['geometric', 'mantle_front_layer', 'wire_view', 'strip_view'],
                     help='DREAM logical views (dream/specs.py:151-180) instead of the '

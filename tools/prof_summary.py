@@ -24,6 +24,12 @@ from collections import defaultdict
 from pathlib import Path
 
 
+# PIXEL pass A (the engine's 'pixel' timing bucket)
+COMPOSITES = {
+    'pix_pass_a': ['k_pix_chunks', 'k_pix_count', 'k_pix_scan_blocks', 'k_pix_scan', 'k_pix_scatter'],
+}
+
+
 def short(name: str) -> str:
     m = re.search(r'lde::(k_\w+)', name)
     return m.group(1) if m else name.split('(')[0][:80]
@@ -63,6 +69,20 @@ def main(prof: Path, stem: Path) -> None:
             e['hbm_traffic_bytes'] = e['hbm_read_bytes'] + e['hbm_write_bytes']
             e['hbm_GBs_at_avg'] = e['hbm_traffic_bytes'] / (d['avg_ms'] * 1e-3) / 1e9
         out[k] = e
+    # composite entries for engine timing buckets that span several launches
+    # (each launched once per batch): the bucket's time is the sum of the
+    # members' averages, its traffic the sum of their traffic per dispatch
+    for name, members in COMPOSITES.items():
+        ms = [out[m] for m in members if m in out]
+        if not ms:
+            continue
+        e = {'members': [m for m in members if m in out], 'calls': min(m['calls'] for m in ms),
+             'avg_ms': sum(m['avg_ms'] for m in ms)}
+        if all('hbm_traffic_bytes' in m for m in ms):
+            for key in ('hbm_read_bytes', 'hbm_write_bytes', 'hbm_traffic_bytes'):
+                e[key] = sum(m[key] for m in ms)
+            e['hbm_GBs_at_avg'] = e['hbm_traffic_bytes'] / (e['avg_ms'] * 1e-3) / 1e9
+        out[name] = e
     stem.parent.mkdir(parents=True, exist_ok=True)
     Path(str(stem) + '.json').write_text(json.dumps(out, indent=1, sort_keys=True) + '\n')
     rows = sorted(stats, key=lambda r: -float(r['TotalDurationNs']))
