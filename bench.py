@@ -38,7 +38,7 @@ KERNEL_SYMBOL = {
     'paged': 'k_paged_partition',
     'page_accumulate': 'k_page_accumulate',
     'split': 'k_sieve',  # SPLIT's event pass (k_split when LDE_SIEVE=0)
-    'coord': 'k_event_key',  # wavelength-mode coordinate pass (keyed; k_event_coord otherwise)
+    'coord': 'coord_keyed',  # wavelength-mode coordinate pass: k_key_dist + k_key_records + k_event_key
     'pixel': 'pix_pass_a',  # PIXEL pass A: k_pix_chunks + k_pix_count + scans + k_pix_scatter
     'page_accumulate': 'k_page_accumulate',
     'finalize': 'k_finalize_v4',

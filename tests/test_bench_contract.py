@@ -49,7 +49,8 @@ def _check_line(d: dict, n_gpus: int = 1):
     assert 0.0 < r['step_frac'] <= r['pipeline_frac'] * 1.2
 
 
-@pytest.mark.parametrize('name', ['r2_bench_line.json', 'r2_loki_bench_line.json'])
+@pytest.mark.parametrize('name', ['r3_bench_line.json', 'r3_loki_bench_line.json',
+                                  'r3_wavelength_bench_line.json'])
 def test_committed_bench_line_contract(name):
     d = json.loads((ROOT / 'profiles' / name).read_text())
     _check_line(d)
@@ -61,15 +62,18 @@ def test_committed_bench_line_contract(name):
     prof = json.loads((ROOT / t['source']).read_text())[bench.KERNEL_SYMBOL[r['kernel']]]
     assert prof['hbm_traffic_bytes'] == t['bytes']
     # live HIP-event average and the traced rocprofv3 average of the same
-    # command agree within the tracing overhead
-    assert r['avg_launch_ms'] == pytest.approx(t['profiled_avg_ms'], rel=0.06)
+    # command agree within the tracing overhead (per-dispatch tracing slows
+    # the sieve by 4-8 % depending on the box: every one of the 11 traced
+    # dispatches of profiles/r3_dream_bench.json's run is 0.330-0.339 ms, the
+    # bench's untraced stamps 0.312 ms on the same box)
+    assert r['avg_launch_ms'] == pytest.approx(t['profiled_avg_ms'], rel=0.08)
     # the kernel reads at least its algorithmic bytes
     events_per_launch = d['config']['events_per_step'] * r.get('timed_steps', d['steps']) / r['launches']
     assert t['read'] >= 0.95 * bench.BYTES_PER_EVENT * events_per_launch
 
 
 def test_committed_headline_line_has_baseline_and_check():
-    d = json.loads((ROOT / 'profiles' / 'r2_bench_line.json').read_text())
+    d = json.loads((ROOT / 'profiles' / 'r3_bench_line.json').read_text())
     assert d['config']['workload'] == 'dream_mantle_cylinder_mantle_z'
     assert d['config']['events_per_step'] == 140_000_000
     cb = d['cpu_baseline']

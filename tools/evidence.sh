@@ -22,4 +22,11 @@ timeout -k 10 300 python bench.py --coordinate wavelength --no-cpu-baseline --e2
 for v in strip_view wire_view mantle_front_layer; do
   timeout -k 10 300 python bench.py --view $v --e2e-steps 0 --cpu-baseline-seconds 3 > gpurun_out/bench_$v.log 2>&1 || { tail -20 gpurun_out/bench_$v.log; exit 1; }
 done
+# the bench lines beside the profiles they cite
+grep -h '^{' gpurun_out/bench_dream.log | tail -1 > gpurun_out/profiles/${TAG}_bench_line.json
+grep -h '^{' gpurun_out/bench_loki.log | tail -1 > gpurun_out/profiles/${TAG}_loki_bench_line.json
+grep -h '^{' gpurun_out/bench_wl.log | tail -1 > gpurun_out/profiles/${TAG}_wavelength_bench_line.json
+for v in strip_view wire_view mantle_front_layer; do
+  grep -h '^{' gpurun_out/bench_$v.log | tail -1 > gpurun_out/profiles/${TAG}_${v}_bench_line.json
+done
 grep -h '^{' gpurun_out/bench_*.log | cut -c1-300

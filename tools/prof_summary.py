@@ -24,9 +24,11 @@ from collections import defaultdict
 from pathlib import Path
 
 
-# PIXEL pass A (the engine's 'pixel' timing bucket)
+# PIXEL pass A (the engine's 'pixel' timing bucket); the keyed wavelength
+# coordinate pass ('coord' bucket on the sieve path)
 COMPOSITES = {
     'pix_pass_a': ['k_pix_chunks', 'k_pix_count', 'k_pix_scan_blocks', 'k_pix_scan', 'k_pix_scatter'],
+    'coord_keyed': ['k_key_dist', 'k_key_records', 'k_event_key'],
 }
 
 
