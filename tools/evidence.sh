@@ -17,7 +17,7 @@ if [ -z "$SKIP_PROF" ]; then
 fi
 [ -n "$SKIP_BENCH" ] && exit 0
 timeout -k 10 400 python bench.py > gpurun_out/bench_dream.log 2>&1 || { tail -20 gpurun_out/bench_dream.log; exit 1; }
-timeout -k 10 300 python bench.py --workload loki --no-cpu-baseline > gpurun_out/bench_loki.log 2>&1 || { tail -20 gpurun_out/bench_loki.log; exit 1; }
+timeout -k 10 300 python bench.py --workload loki --e2e-steps 0 --cpu-baseline-seconds 3 > gpurun_out/bench_loki.log 2>&1 || { tail -20 gpurun_out/bench_loki.log; exit 1; }
 timeout -k 10 300 python bench.py --coordinate wavelength --no-cpu-baseline --e2e-steps 0 > gpurun_out/bench_wl.log 2>&1 || { tail -20 gpurun_out/bench_wl.log; exit 1; }
 for v in strip_view wire_view mantle_front_layer; do
   timeout -k 10 300 python bench.py --view $v --e2e-steps 0 --cpu-baseline-seconds 3 > gpurun_out/bench_$v.log 2>&1 || { tail -20 gpurun_out/bench_$v.log; exit 1; }
