@@ -180,7 +180,7 @@ struct lde_handle {
     lde::PixChunk *d_pctab = nullptr;
     size_t pctab_cap = 0;
     uint32_t *d_pitem_count = nullptr;
-    int pix_grid = 0, pix_unit = 2, pix_ept = 16, pix_bu = 4, pix_items_per_cu = 2;
+    int pix_grid = 0, pix_unit = 2, pix_ept = 16, pix_bu = 4, pix_items_per_cu = 0;
     bool pix24 = true;
     std::vector<double> edges;  // the create-time edges (event unit)
     // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
@@ -1110,11 +1110,15 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     const size_t n_pay = (size_t)total + 3 * (size_t)units * (size_t)h->pix.nr + 4;
     if (int rc = grow(h, &h->d_ppayload, h->ppayload_cap, h->pix24 ? (n_pay * 3 + 3) / 4 + 4 : n_pay))
         return rc;
-    // pass-B items: a few per CU (LDS: one block per CU), and a range's
-    // footprint flush per item, so not many more; whole groups of 4 payloads
+    // pass-B items: each flushes its range's whole footprint (F x T
+    // atomics), so as few as keep the CUs busy: one per range up to twice the
+    // mean range total, larger ranges (skewed streams) split (LOKI: 196
+    // items, pass B 0.157 -> 0.120 ms against ~600 items of total / 2 CUs);
+    // LDE_PIX_ITEMS=k: total / (k x CUs) events per item instead
     const long long ipc = h->pix_items_per_cu;
     const long long per =
-        (std::max<long long>(65536, (total + ipc * h->cus - 1) / (ipc * h->cus)) + 3) & ~3LL;
+        (std::max<long long>(65536, ipc == 0 ? (2 * total + h->pix.nr - 1) / h->pix.nr
+                                              : (total + ipc * h->cus - 1) / (ipc * h->cus)) + 3) & ~3LL;
     const long long max_items = total / per + h->pix.nr + 1;
     if (int rc = grow(h, &h->d_pitems, h->pitems_cap, (size_t)max_items)) return rc;
     if (int rc = grow(h, &h->d_pctab, h->pctab_cap, (size_t)chunks)) return rc;
@@ -1172,9 +1176,13 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
     int strat = auto_strategy(h, total);
     const bool auto_split = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && h->split_ok;
     if (strat == LDE_STRATEGY_SPLIT && !h->split_ok) strat = LDE_STRATEGY_PAGED;
-    if (strat == LDE_STRATEGY_PIXEL && !h->pixel_ok) strat = LDE_STRATEGY_PAGED;
+    // PIXEL's payload offsets are u32: batches whose payload (events + pads)
+    // could reach 2^31 take PAGED
+    const long long max_chunks = total / lde::kChunk + (long long)segs.size() + 1;
+    const bool pixel_ok = h->pixel_ok && total + 3LL * (max_chunks / h->pix_unit + 1) * h->pix.nr < 0x7FFFFFF0LL;
+    if (strat == LDE_STRATEGY_PIXEL && !pixel_ok) strat = LDE_STRATEGY_PAGED;
     // AUTO without skew: PIXEL (no LUT gather) where the footprints fit
-    const bool auto_pixel = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && h->pixel_ok;
+    const bool auto_pixel = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && pixel_ok;
     if (auto_pixel && !auto_split) strat = LDE_STRATEGY_PIXEL;
     if ((strat == LDE_STRATEGY_PARTITION || strat == LDE_STRATEGY_PAGED) && h->n_tiles == 0)
         strat = LDE_STRATEGY_ATOMIC;
@@ -1383,7 +1391,7 @@ int build_pixel(lde_handle *h, const int32_t *lut) {
     h->pix_ept = h->pix_unit == 2 || env_ll("LDE_PIX_EPT", 8) == 16 ? 16 : 8;
     h->pix24 = env_ll("LDE_PIX24", 1) != 0;
     h->pix_bu = env_ll("LDE_PIX_BU", 4) == 8 ? 8 : 4;
-    h->pix_items_per_cu = (int)std::max<long long>(1, std::min<long long>(16, env_ll("LDE_PIX_ITEMS", 2)));
+    h->pix_items_per_cu = (int)std::max<long long>(0, std::min<long long>(16, env_ll("LDE_PIX_ITEMS", 0)));
     // blocks of unit * kChunk / ept threads: 4 x 512 or 2 x 1024 per CU
     h->pix_grid = (int)std::max<long long>(
         1, env_ll("LDE_PIX_GRID", (h->pix_ept == 16 && h->pix_unit == 1 ? 4 : 2) * (long long)h->cus));
