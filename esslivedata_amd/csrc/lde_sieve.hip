@@ -1149,8 +1149,10 @@ size_t cold_sort_a_smem(int n_tiles, int kpt) {
     const size_t nt4 = (size_t)align4(n_tiles);
     const size_t img_words = ((size_t)kSortThreads * kpt + 16 * nt4) / 2;
     const size_t scratch = std::max(img_words, (size_t)2 * (kMaxTiles + 1));
-    // scratch | s_cnt [waves][nt4] | tot, pos, B, full, cn | carry [nt4][4] | s_w
-    return 4 * ((size_t)align4((int)scratch) + (size_t)kSortWaves * nt4 + 5 * nt4 + 4 * nt4 + 32);
+    // scratch | s_cnt [waves][nt4] | tot, pos, B, full, ng | carry [nt4][4] | s_w |
+    // group -> tile (u16, one per 8-key group of a piece)
+    const size_t gt_words = ((size_t)kSortThreads * kpt / 8 + nt4 + 1) / 2;
+    return 4 * ((size_t)align4((int)scratch) + (size_t)kSortWaves * nt4 + 5 * nt4 + 4 * nt4 + 32 + gt_words);
 }
 
 template <int TB, int KPT, bool KEY24>
@@ -1171,9 +1173,10 @@ void k_cold_sort_a(ColdArgs c) {
     uint32_t *s_pos = s_tot + nt4;                       // [tile] next global position (8-aligned)
     uint32_t *s_B = s_pos + nt4;                         // [tile] segment base in the image (u16)
     uint32_t *s_full = s_B + nt4;                        // [tile] full groups of this piece
-    uint32_t *s_cn = s_full + nt4;                       // [tile] carried keys (0..7)
-    uint4 *s_carry = reinterpret_cast<uint4 *>(s_cn + nt4);  // [tile] 8 carried u16
+    uint32_t *s_ng = s_full + nt4;                       // [tile] 8-key groups of its segment
+    uint4 *s_carry = reinterpret_cast<uint4 *>(s_ng + nt4);  // [tile] 8 carried u16
     uint32_t *s_w = reinterpret_cast<uint32_t *>(s_carry + nt4);
+    uint16_t *s_gt = reinterpret_cast<uint16_t *>(s_w + 32);  // [group] its tile
     const int tid = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave-uniform: SGPR buffer descriptors
     const int b = blockIdx.x / kColdGroups, grp = blockIdx.x % kColdGroups;
@@ -1192,7 +1195,6 @@ void k_cold_sort_a(ColdArgs c) {
         const uint32_t ex = block_exclusive_scan(tt, s_w, &total);
         if (own) {
             s_pos[tid] = ex + c.boff[(size_t)row * n_tiles + tid];
-            s_cn[tid] = 0;
         }
     }
     if (lane == 0) s_w[20 + wv] = (n_w + 64 * KPT - 1) / (64 * KPT);
@@ -1260,6 +1262,7 @@ void k_cold_sort_a(ColdArgs c) {
         if (own) {
             s_B[tid] = B;
             s_full[tid] = n >> 3;
+            s_ng[tid] = (n + 7u) >> 3;
             if (cn) {  // the carried keys head the segment
                 const uint4 cv = s_carry[tid];
                 const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w};
@@ -1282,6 +1285,12 @@ void k_cold_sort_a(ColdArgs c) {
                     (uint16_t)((k >> 2) & MASK);
             }
         }
+        // every group's tile, a wave per tile (its lanes over the tile's
+        // groups), so the write-out below reads it instead of searching s_B
+        for (int t = wv; t < n_tiles; t += kSortWaves) {
+            const uint32_t g0 = s_B[t] >> 3, ng = s_ng[t];
+            for (uint32_t j = (uint32_t)lane; j < ng; j += 64u) s_gt[g0 + j] = (uint16_t)t;
+        }
         // wide pieces: the next keys are requested once this piece's are dead
         if (KPT > 16 && p + 1 < npieces) fetch(p + 1);
         __syncthreads();
@@ -1290,11 +1299,7 @@ void k_cold_sort_a(ColdArgs c) {
         const uint32_t G = gtotal >> 3;
         for (uint32_t gi = (uint32_t)tid; gi < G; gi += kSortThreads) {
             const uint32_t pos = gi * 8u;
-            int lo = 0, hi = n_tiles - 1;  // last tile whose segment starts at or before pos
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (s_B[mid] <= pos) lo = mid; else hi = mid - 1;
-            }
+            const int lo = s_gt[gi];
             const uint32_t k = (pos - s_B[lo]) >> 3;
             const uint4 v = *reinterpret_cast<const uint4 *>(img + pos);
             if (k < s_full[lo]) {
@@ -1499,10 +1504,12 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
             hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * kColdGroups), dim3(kSortThreads),   \
                                sm, st, c);                                                        \
         }                                                                                         \
-        if (!LDE_DIAG(c.ablate)) /* diagnostics: the keys are not valid */                                 \
-        hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, st,\
-                              nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist, c.n_bins,  \
-                              (c.tail_release & 4) ? 1 : 0);                                      \
+        if (!LDE_DIAG(c.ablate)) /* diagnostics: the keys are not valid */                       \
+            hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, \
+                                  st, nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist,   \
+                                  c.n_bins, (c.tail_release & 4) ? 1 : 0);                       \
+        else if (stop) /* the binning's end marker is still recorded */                          \
+            (void)hipEventRecord(stop, st);                                                      \
         break;
         LDE_COLD(13)
         LDE_COLD(14)
