@@ -204,6 +204,52 @@ def _window_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _rccl_worker(rank, world, port, q):
+    """The RCCL path itself (backend 'nccl' with device_id, device-buffer
+    reduces, as bench.py --gpus N runs it), on one rank: the box has one GPU
+    and RCCL refuses two ranks on one device.  OutputReducer and WindowReducer
+    through RCCL must return exactly what the engine alone finalizes."""
+    import torch
+    import torch.distributed as dist
+
+    from esslivedata_amd import synthetic
+    from esslivedata_amd.distributed import OutputReducer, WindowReducer
+
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=rank, world_size=world, device_id=dev)
+    try:
+        ok = dist.get_backend() == 'nccl'
+        inst, view = _dream()
+        edges = inst.edges.edges_ns()
+        eng = _engine(view, edges)
+        ref = _engine(view, edges)
+        red = OutputReducer(eng, dev)
+        for batch in range(2):
+            pid, toa = synthetic.torch_dream_events(3_000_000, inst, 70 + batch, dev)
+            for e in (eng, ref):
+                e.stage_tensors_batch([(pid, toa)])
+                e.accumulate(batch)
+            cur, cum, tot = red.finalize()
+            exp = ref.finalize(images=True)
+            ok &= bool(np.array_equal(cur, exp.current_image))
+            ok &= bool(np.array_equal(cum, exp.cumulative_image))
+            ok &= tot == [exp.current_total, exp.current_in_range, exp.cumulative_total,
+                          exp.cumulative_in_range] and tot[0] > 0
+        pid, toa = synthetic.torch_dream_events(3_000_000, inst, 80, dev)
+        for e in (eng, ref):
+            e.stage_tensors_batch([(pid, toa)])
+            e.accumulate(2)
+        ok &= WindowReducer(eng, dev).reduce() is True
+        ok &= bool(np.array_equal(eng.read_histogram('current'), ref.read_histogram('current')))
+        q.put((rank, bool(ok)))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
 def _run(target, world=2, timeout=240):
     import torch.multiprocessing as mp
 
@@ -241,3 +287,7 @@ def test_window_reducer_after_u64_fold_two_ranks():
 
 def test_output_reducer_float32_view_two_ranks():
     _run(_bifrost_worker)
+
+
+def test_rccl_reducers_single_rank():
+    _run(_rccl_worker, world=1)
