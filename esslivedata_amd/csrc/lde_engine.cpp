@@ -135,6 +135,7 @@ struct lde_handle {
     uint32_t *h_sel_stats = nullptr;   // pinned
     std::vector<int> hot_uses;         // per replica: -1 = not selected yet
     std::vector<double> hot_cov;
+    std::vector<char> all_hot;         // per replica: every screen has a hot row
     uint32_t *d_hot_part = nullptr;
     size_t hot_part_cap = 0;
     uint32_t *d_cold = nullptr;
@@ -857,6 +858,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             const uint32_t *st = h->h_sel_stats + 4 * r;
             const double sampled = (double)st[0];
             h->hot_cov[(size_t)r] = sampled > 0 ? (double)st[1] / sampled : 0.0;
+            h->all_hot[(size_t)r] = st[2] == (uint32_t)h->S ? 1 : 0;
             h->hot_uses[(size_t)r] = 0;
             if (env_ll("LDE_VERBOSE", 0))
                 fprintf(stderr, "lde split: replica %d sampled %u, hot rows %u cover %.3f, pixel table covers %.3f\n",
@@ -1079,6 +1081,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         c.hot_fmt = h->d_hot_fmt;
         c.tail_release = h->tail_release;
         c.ablate = h->cold_sort_ablate;
+        c.all_hot = h->all_hot[replica];
         Timed tm(h, LDE_K_PAGED);
         HIPCALL(h, lde::launch_cold_pipeline(c, h->stream, h->bin_stop_ext));
         if (h->bin_stop_ext) h->bin_stop_used = true;
@@ -1801,6 +1804,28 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
             };
             // the cache never takes the room of the last 64 hot rows
             while (cbits > 8 && rows_for(cbits) < std::min<long long>(64, h->S)) --cbits;
+            // views with few screens (DREAM strip_view: 256): a smaller pixel
+            // table (down to 2^10 slots) when it makes room for a hot row per
+            // screen, so that no event is cold and the cold-key pipeline never
+            // runs (the table's misses cost a gather; a cold key a sort and a
+            // second pass)
+            {
+                std::vector<uint32_t> tt0;
+                int tsh0 = 0;
+                uint32_t tcap0 = 0;
+                if (h->S <= lde::kHotMaxRows && build_sieve_toa(h->tp, tab, tt0, tsh0, tcap0)) {
+                    if (tt0.size() < (size_t)lde::align4(h->T + 2)) tt0.resize((size_t)lde::align4(h->T + 2), 0u);
+                    auto sieve_fits_all = [&](int cb) {
+                        return lde::sieve_smem(lde::align4((int)h->S * h->T), cb, (int)tt0.size(), h->n_tiles) <= budget;
+                    };
+                    if (cbits > 0 && !sieve_fits_all(cbits) && env_ll("LDE_ALL_HOT", 1) != 0)
+                        for (int cb = cbits - 1; cb >= 10; --cb)
+                            if (sieve_fits_all(cb)) {
+                                cbits = cb;
+                                break;
+                            }
+                }
+            }
             int H = rows_for(cbits);
             H = (int)std::min<long long>(H, h->S);
             const long long hmax = env_ll("LDE_HOT_ROWS", 0);
@@ -1847,6 +1872,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 h->split_min_cov = (double)env_ll("LDE_SPLIT_MIN_COV_PCT", 30) / 100.0;
                 h->hot_uses.assign((size_t)h->R, -1);
                 h->hot_cov.assign((size_t)h->R, 0.0);
+                h->all_hot.assign((size_t)h->R, 0);
                 CREATE_CHECK(dev_alloc(h, &h->d_hlut, (size_t)h->R * h->L));
                 if (cbits > 0) {
                     CREATE_CHECK(dev_alloc(h, &h->d_pix_cnt, (size_t)h->L));

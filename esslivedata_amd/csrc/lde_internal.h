@@ -248,6 +248,7 @@ struct ColdArgs {
     const uint32_t *hot_fmt = nullptr;  // per sieve block: hot rows as u16 (1) or u32 (0)
     int tail_release = 0;  // bit 1: sort blocks, bit 2: pass-B blocks end with an agent release
     int ablate = 0;     // cold-sort diagnostics (wrong results): 1 no writes, 2 no loads
+    int all_hot = 0;    // every screen has a hot row (no cold keys): hot-row reduce only
 };
 size_t cold_sort_smem(int n_tiles);
 size_t cold_sort_w_smem(int n_tiles);

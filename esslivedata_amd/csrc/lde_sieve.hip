@@ -1479,6 +1479,13 @@ static void launch_sort_a_tb(const ColdArgs &c, size_t sma, hipStream_t st) {
 
 hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t stop) {
     const int hot_blocks = c.hot_part ? ((c.ht + 255) / 256) * 8 : 0;
+    if (c.all_hot && hot_blocks > 0) {
+        // every screen has a hot row: the sieve wrote no cold key, only the
+        // hot rows go into the window
+        hipLaunchKernelGGL(k_hot_reduce_scan, dim3(hot_blocks), dim3(256), 0, st, c, hot_blocks);
+        if (stop) (void)hipEventRecord(stop, st);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_hot_reduce_scan, dim3(hot_blocks + c.n_tiles), dim3(256), 0, st, c,
                        hot_blocks);
     const size_t sm = cold_sort_smem(c.n_tiles);

@@ -191,6 +191,22 @@ __global__ __launch_bounds__(1024) void k_select_hot(const uint32_t *__restrict_
     __shared__ uint32_t s_w[32];
     __shared__ uint32_t s_sel[4];
     const int tid = threadIdx.x;
+    if (H >= S) {  // a row for every screen, sampled or not: no event is cold
+        uint32_t tot = 0;
+        for (int s = tid; s < S; s += 1024) {
+            tot += cnt[s];
+            screen_row[s] = (uint16_t)(s + 1);
+            row_screen[s] = (uint32_t)s;
+        }
+        uint32_t tt;
+        (void)block_exclusive_scan(tot, s_w, &tt);
+        if (tid == 0) {
+            stats[0] = stats[1] = tt;
+            stats[2] = (uint32_t)S;
+            stats[3] = 0;
+        }
+        return;
+    }
     if (tid < 33) s_cls[tid] = 0;
     __syncthreads();
     const int per = (S + 1023) / 1024;
