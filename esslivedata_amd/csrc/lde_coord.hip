@@ -213,7 +213,7 @@ size_t key_smem(const KeyArgs &a, bool table_lds) {
     const size_t C = (size_t)1 << a.cbits;
     const int ne = a.c.edges_lds ? a.c.T + 1 : 0;
     return 12 * C + 8 * (size_t)((ne + 1) & ~1) + (table_lds ? 8 * (size_t)a.c.nd * a.c.nt : 0) +
-           2 * (size_t)a.c.G;
+           2 * (size_t)((a.c.G + 7) & ~7) + 16 * (size_t)kKeyLdsChunks;
 }
 
 // One block per CU walks a contiguous range of the batch's global chunks;
@@ -273,49 +273,44 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     const long long cb = (long long)blockIdx.x * n / gridDim.x;
     const long long ce = ((long long)blockIdx.x + 1) * n / gridDim.x;
     const int tid = threadIdx.x;
-    int si = 0;
-    if (cb < ce) {
-        int lo = 0, hi = k.n_segs - 1;  // last segment with chunk0 <= cb
+    // The block's chunks in windows of kKeyLdsChunks: each window's {pid, toa}
+    // pointers go to LDS first (one segment search per chunk, by its own
+    // thread), with chunks that are not full and 16-byte aligned mapped to the
+    // all-invalid dummy chunk and redone element-wise after the window.  The
+    // main loop then has one load path and reads its pointers from LDS, so
+    // the in-order vmcnt waits for exactly the gathers it needs while the
+    // next chunk's loads stay in flight.
+    const int **s_cp = reinterpret_cast<const int **>(s_b + ((a.G + 7) & ~7));  // [window][2]
+    auto chunk_ptrs = [&](long long c, const int *&pp, const int *&tp) -> bool {
+        int lo = 0, hi = k.n_segs - 1;  // last segment with chunk0 <= c
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (k.segs[mid].chunk0 <= cb) lo = mid; else hi = mid - 1;
+            if (k.segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
         }
-        si = lo;
-    }
-    // chunk c's events (8 per lane, the sieve's layout); events past a
-    // message's end read as a dropped id
-    auto fetch = [&](long long c, int (&p)[8], int (&t)[8]) __attribute__((always_inline)) {
-        while (si + 1 < k.n_segs && k.segs[si + 1].chunk0 <= c) ++si;
-        const SegDesc sd = k.segs[si];
+        const SegDesc sd = k.segs[lo];
         const long long base = (c - sd.chunk0) * kChunk;
-        const bool full = ((((uintptr_t)sd.pid | (uintptr_t)sd.toa) & 15u) == 0) && base + kChunk <= sd.n;
+        pp = sd.pid + base;
+        tp = sd.toa + base;
+        return ((((uintptr_t)pp | (uintptr_t)tp) & 15u) == 0) && base + kChunk <= sd.n;
+    };
+    auto fetch = [&](long long w0, long long c, int (&p)[8], int (&t)[8]) __attribute__((always_inline)) {
+        const int *pp = s_cp[2 * (c - w0)], *tp = s_cp[2 * (c - w0) + 1];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const long long e0 = base + ((long long)j * 1024 + tid) * 4;
-            if (full) {
-                const v4i pv = ld_stream4(sd.pid + e0);
-                const v4i tv = ld_stream4(sd.toa + e0);
+            const int e0 = (j * 1024 + tid) * 4;
+            const v4i pv = ld_stream4(pp + e0);
+            const v4i tv = ld_stream4(tp + e0);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    p[j * 4 + q] = pv[q];
-                    t[j * 4 + q] = tv[q];
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const bool ok = e0 + q < sd.n;
-                    p[j * 4 + q] = ok ? ld_global(sd.pid + e0 + q) : a.pid_off - 1;  // dropped
-                    t[j * 4 + q] = ok ? ld_global(sd.toa + e0 + q) : 0;
-                }
+            for (int q = 0; q < 4; ++q) {
+                p[j * 4 + q] = pv[q];
+                t[j * 4 + q] = tv[q];
             }
         }
     };
-    // Per chunk: probe the LDS table, issue the misses' gathers, then the
-    // next chunk's loads, then the arithmetic -- vmcnt is in order, so the
-    // wait for the gathers leaves the next chunk's loads in flight.
-    int p[8], t[8];
-    if (cb < ce) fetch(cb, p, t);
-    for (long long c = cb; c < ce; ++c) {
+    // one chunk's words: table probe, the misses' gathers, then `next` (the
+    // next chunk's loads, issued after the gathers), then the arithmetic
+    auto words = [&](const int (&p)[8], const int (&t)[8], int (&out)[8], auto &&next)
+        __attribute__((always_inline)) {
         uint32_t w[8], g[8], slot[8];
         double d[8];
 #pragma unroll
@@ -337,8 +332,10 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
         int tc[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) tc[q] = t[q];
-        if (c + 1 < ce) fetch(c + 1, p, t);
-        int out[8];
+        // issue order fixed: every gather, then the next chunk's loads
+        __builtin_amdgcn_sched_barrier(0);
+        next();
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const double dq = slot[q] != 0xFFFFFFFFu ? s_d[slot[q]] : d[q];
@@ -346,10 +343,61 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
             const int b = (word & kSieveValid) ? coord(dq, tc[q]) : -1;
             out[q] = b >= 0 ? (int)(word + (uint32_t)b) : 0;
         }
+    };
+    auto store = [&](long long c, const int (&out)[8]) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
             *reinterpret_cast<int4 *>(k.keys + c * kChunk + ((long long)j * 1024 + tid) * 4) =
                 make_int4(out[j * 4], out[j * 4 + 1], out[j * 4 + 2], out[j * 4 + 3]);
+    };
+    for (long long w0 = cb; w0 < ce; w0 += kKeyLdsChunks) {
+        const long long w1 = w0 + kKeyLdsChunks < ce ? w0 + kKeyLdsChunks : ce;
+        __syncthreads();  // the previous window's pointers are dead
+        for (long long c = w0 + tid; c < w1; c += blockDim.x) {
+            const int *pp, *tp;
+            const bool full = chunk_ptrs(c, pp, tp);
+            s_cp[2 * (c - w0)] = full ? pp : k.dummy;
+            s_cp[2 * (c - w0) + 1] = full ? tp : k.dummy;
+        }
+        __syncthreads();
+        int p[8], t[8];
+        fetch(w0, w0, p, t);
+        for (long long c = w0; c < w1; ++c) {
+            int out[8];
+            // the window's last chunk reloads itself: the loads stay
+            // unconditional (a branch around them makes the compiler wait for
+            // every outstanding load after it, the next chunk's included)
+            const long long cn = c + 1 < w1 ? c + 1 : c;
+            words(p, t, out, [&]() __attribute__((always_inline)) { fetch(w0, cn, p, t); });
+            store(c, out);
+        }
+        // the window's chunks that are not full and aligned: element loads
+        for (long long c = w0; c < w1; ++c) {
+            if (s_cp[2 * (c - w0)] != k.dummy) continue;  // block-uniform
+            const int *pp, *tp;
+            (void)chunk_ptrs(c, pp, tp);
+            long long left;
+            {
+                int lo = 0, hi = k.n_segs - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (k.segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+                }
+                left = k.segs[lo].n - (c - k.segs[lo].chunk0) * kChunk;
+            }
+            int pe[8], te[8], out[8];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const long long e = ((long long)j * 1024 + tid) * 4 + q;
+                    const bool ok = e < left;
+                    pe[j * 4 + q] = ok ? ld_global(pp + e) : a.pid_off - 1;  // dropped
+                    te[j * 4 + q] = ok ? ld_global(tp + e) : 0;
+                }
+            words(pe, te, out, []() {});
+            store(c, out);
+        }
     }
 }
 

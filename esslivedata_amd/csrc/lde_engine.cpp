@@ -947,6 +947,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             ka.rec = h->d_key_rec;
             ka.cbits = h->cache_bits;
             ka.keys = h->d_cbin;
+            ka.dummy = h->d_sieve_dummy;
             HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream));
             ksd.push_back({h->d_cbin, h->d_cbin, chunks * lde::kChunk, 0});
         }

@@ -359,7 +359,9 @@ struct KeyArgs {
     const uint4 *rec;         // per pixel {word, 0, distance lo, hi}, L + 1 entries (k_key_records)
     int cbits;
     int *keys;                // [n_chunks * kChunk]
+    const int *dummy;         // kChunk x (pid_off - 1): the all-invalid chunk
 };
+constexpr int kKeyLdsChunks = 128;  // k_event_key: chunk pointers per LDS window
 size_t key_smem(const KeyArgs &a, bool table_lds);
 hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st);
 // distance of every pixel-table slot's pixel (NaN for empty slots)
