@@ -727,3 +727,36 @@ def test_loki_pixel_ranges_multi_replica_and_move(strategy):
         np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
         np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
         assert res.current_in_range == exp['counts_in_toa_range']
+
+
+def test_loki_pixel_forced_on_skewed_stream_splits_hot_ranges():
+    """Forced PIXEL on a stream AUTO would not give it: 70 % of the events in
+    the first 4,096 pixels (one pixel range) and a batch that is one pixel and
+    one TOA value only.  A range holding many times the mean range total is
+    split over several pass-B items whose footprint flushes add into the same
+    bins; counts stay bit-exact."""
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.loki_bank0(n_replicas=1)
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, 'pixel')
+    ps = _oracle_pixel_screen_geometric(inst)
+    rng = np.random.default_rng(17)
+    for batch in range(2):
+        n = 8_000_003
+        if batch == 0:
+            pid, toa = synthetic.uniform_events(n, 1, 802816, seed=41)
+            hot = rng.random(n) < 0.7
+            pid[hot] = rng.integers(1, 4097, int(hot.sum())).astype(np.int32)
+        else:
+            pid = np.full(n, 123_457, dtype=np.int32)
+            toa = np.full(n, 35_000_000, dtype=np.int32)
+        eng.stage(pid, toa)
+        eng.accumulate(0)
+        res = eng.finalize(hists=True)
+        assert eng.info()['last_strategy'] == 'pixel'
+        exp = ora.detector_histogram(ps[0], view.n_screen, ora.pixel_index(pid, inst.detector_number),
+                                     toa, edges)
+        np.testing.assert_array_equal(res.current_hist, exp)
+        assert res.current_total == int(exp.sum())
