@@ -197,6 +197,7 @@ struct lde_handle {
     int cold_sort_ablate = 0;   // LDE_COLD_SORT_ABLATE (LDE_DIAGNOSTICS build only)
     uint32_t ttab_cap = 0;
     int ttab_shift = 0;
+    bool ttab_log = false;   // log-linear TOA buckets (ttab_shift = M)
     lde::ChunkPtrs *d_chunk_tab = nullptr;
     size_t chunk_tab_cap = 0;
     int *d_sieve_dummy = nullptr;     // kChunk x (pid_off - 1): the all-invalid chunk
@@ -446,27 +447,78 @@ int build_toa_tables(lde_handle *h, const double *edges, int T, std::vector<unsi
     return LDE_OK;
 }
 
-// SIEVE TOA image: one u32 per 2^shift2-wide bucket of the fast layout,
-// (offset of the next threshold inside the bucket, capped at 2^shift2) << 8 |
-// bin of the bucket start, then a sentinel bucket (bin 255 -> 256, dropped).
-// Buckets inherit the one-step property of the fast layout (at most one
-// threshold inside), so bin = (w & 0xFF) + ((d & (2^shift2 - 1)) >= (w >> 8)).
+// SIEVE TOA image: one u32 per bucket, (offset of the next threshold inside
+// the bucket, capped at the bucket width) << 8 | bin of the bucket start.
+// Buckets hold at most one threshold, so bin = (w & 0xFF) + (offset of d in
+// its bucket >= (w >> 8)); d >= span (and TOAs before the first edge, which
+// wrap) clamp to `cap` and land on a word whose bin comes out as T (dropped).
+// Linear buckets (2^shift2 wide, the fast layout's) or, with LDE_SIEVE_TOA_LOG=1
+// and a table at least twice smaller, log-linear ones (geometric edges: DREAM's log edges
+// need 4,330 linear buckets for a 25 us narrowest bin, 705 log-linear ones):
+// for d with floor(log2 d) = e, s = max(0, e - M), bucket (s << M) + (d >> s)
+// of width 2^s, i.e. 2^M buckets per octave (*is_log, shift2 = M).
 bool build_sieve_toa(const lde::ToaParams &tp, const std::vector<unsigned char> &img,
-                     std::vector<uint32_t> &words, int &shift2, uint32_t &cap) {
+                     std::vector<uint32_t> &words, int &shift2, uint32_t &cap, bool *is_log) {
+    if (is_log) *is_log = false;
     if (!tp.fast || tp.T > lde::kSieveMaxT || tp.span == 0) return false;
     const uint32_t *rthr = reinterpret_cast<const uint32_t *>(img.data());
+    const int T = tp.T;
     shift2 = std::min(tp.shift, 23);
     const unsigned long long span = tp.span;
     const unsigned long long G = ((span - 1) >> shift2) + 1;
     if (G > (unsigned long long)lde::kMaxFastBuckets) return false;
+    // bucket [start, start + width) -> its word, or false when a second
+    // threshold falls inside it
+    auto word = [&](unsigned long long start, unsigned long long width, int &b, uint32_t &w) {
+        while (b + 1 < T && rthr[b + 1] <= start) ++b;
+        if (b + 2 <= T && (unsigned long long)rthr[b + 2] < start + width && start < span) return false;
+        const unsigned long long nxt = rthr[b + 1] > start ? rthr[b + 1] - start : 0;
+        w = (uint32_t)(std::min<unsigned long long>(nxt, width) << 8) | (uint32_t)b;
+        return true;
+    };
+    // (off by default: the log-linear index costs the sieve a few VALU ops per
+    // event and, in its default pipeline, register spills; with the packed
+    // table word it measured +2 us sieve / -2.4 us cold path, net zero, for
+    // 36 more hot rows on DREAM)
+    if (is_log && span < (1ULL << 31) && env_ll("LDE_SIEVE_TOA_LOG", 0) != 0) {
+        const int e_max = 63 - __builtin_clzll(span | 1ULL);  // d <= span
+        for (int M = 0; M <= 12; ++M) {
+            const int s_max = std::max(0, e_max - M);
+            if (s_max > 23) continue;  // offsets stay below 2^24
+            const unsigned long long Gl = ((unsigned long long)s_max << M) + (span >> s_max) + 1;
+            if (2 * Gl > G + 1) break;  // not worth it: finer M only grows the table
+            std::vector<uint32_t> lw((size_t)lde::align4((int)Gl), 0xFFu);
+            int b = 0;
+            bool ok = true;
+            for (unsigned long long g = 0; g < Gl && ok; ++g) {
+                unsigned long long start, width;
+                if (g < (2ULL << M)) {
+                    start = g;
+                    width = 1;
+                } else {
+                    const int sg = (int)(g >> M) - 1;
+                    start = (g - ((unsigned long long)sg << M)) << sg;
+                    width = 1ULL << sg;
+                }
+                uint32_t w = 0;
+                ok = word(start, width, b, w);
+                lw[(size_t)g] = w;
+            }
+            if (!ok) continue;
+            words = std::move(lw);
+            shift2 = M;
+            cap = (uint32_t)span;
+            *is_log = true;
+            return true;
+        }
+    }
     const unsigned long long W = 1ULL << shift2;
     words.assign((size_t)lde::align4((int)G + 1), 0u);
     int b = 0;
     for (unsigned long long g = 0; g < G; ++g) {
-        const unsigned long long start = g << shift2;
-        while (b + 1 < tp.T && rthr[b + 1] <= start) ++b;
-        const unsigned long long off = std::min<unsigned long long>(rthr[b + 1] - start, W);
-        words[(size_t)g] = (uint32_t)(off << 8) | (uint32_t)b;
+        uint32_t w = 0;
+        (void)word(g << shift2, W, b, w);  // the fast layout guarantees one threshold at most
+        words[(size_t)g] = w;
     }
     words[(size_t)G] = 0xFFu;
     cap = (G << shift2) > 0xffffffffULL ? 0xffffffffu : (uint32_t)(G << shift2);
@@ -965,6 +1017,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         sa.toa_lo = (uint32_t)h->tp.lo;
         sa.toa_cap = h->ttab_cap;
         sa.toa_shift = h->ttab_shift;
+        sa.toa_log = h->ttab_log ? 1 : 0;
         sa.toa_words4 = (int)h->ttab.size();
         sa.T = h->T;
         sa.pix_tab = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
@@ -1814,7 +1867,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 std::vector<uint32_t> tt0;
                 int tsh0 = 0;
                 uint32_t tcap0 = 0;
-                if (h->S <= lde::kHotMaxRows && build_sieve_toa(h->tp, tab, tt0, tsh0, tcap0)) {
+                bool log0 = false;
+                if (h->S <= lde::kHotMaxRows && build_sieve_toa(h->tp, tab, tt0, tsh0, tcap0, &log0)) {
                     if (tt0.size() < (size_t)lde::align4(h->T + 2)) tt0.resize((size_t)lde::align4(h->T + 2), 0u);
                     auto sieve_fits_all = [&](int cb) {
                         return lde::sieve_smem(lde::align4((int)h->S * h->T), cb, (int)tt0.size(), h->n_tiles) <= budget;
@@ -1842,7 +1896,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 std::vector<uint32_t> tt;
                 int tsh = 0;
                 uint32_t tcap = 0;
-                if (cbits > 0 && env_ll("LDE_SIEVE", 1) != 0 && build_sieve_toa(h->tp, tab, tt, tsh, tcap) &&
+                bool tlog = false;
+                if (cbits > 0 && env_ll("LDE_SIEVE", 1) != 0 && build_sieve_toa(h->tp, tab, tt, tsh, tcap, &tlog) &&
                     (unsigned long long)h->S * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL &&
                     ((h->L - 1) >> cbits) < 255 && h->L < 0x3fffffffLL) {
                     // room for the integer-edge table of wavelength mode (edges
@@ -1861,6 +1916,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                         h->ttab = std::move(tt);
                         h->ttab_shift = tsh;
                         h->ttab_cap = tcap;
+                        h->ttab_log = tlog;
                     }
                 }
             }
@@ -2551,6 +2607,7 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     std::vector<uint32_t> tt;
     int tsh = 0;
     uint32_t tcap = 0;
+    bool tlog = false;
     bool sieve_fits = h->sieve_ok;
     if (!rebind) {
         // the binning stage now sees integer bins: edges 0..T
@@ -2561,7 +2618,7 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
         if (int rc = dev_alloc(h, &st.tab, tab.size())) return rc;
         HIPCALL(h, hipMemcpy(st.tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
         if (h->sieve_ok) {
-            sieve_fits = build_sieve_toa(tp, tab, tt, tsh, tcap) && tt.size() <= h->ttab.size();
+            sieve_fits = build_sieve_toa(tp, tab, tt, tsh, tcap, &tlog) && tt.size() <= h->ttab.size();
             if (sieve_fits) {
                 if (int rc = dev_alloc(h, &st.ttab, h->ttab.size())) return rc;
                 HIPCALL(h, hipMemcpy(st.ttab, tt.data(), tt.size() * 4, hipMemcpyHostToDevice));
@@ -2612,6 +2669,7 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
             h->ttab = std::move(tt);
             h->ttab_shift = tsh;
             h->ttab_cap = tcap;
+            h->ttab_log = tlog;
         } else {
             h->sieve_ok = false;
         }

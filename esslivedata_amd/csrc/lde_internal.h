@@ -202,7 +202,8 @@ struct SieveArgs {
     int pid_off;
     const uint32_t *ttab;  // TOA bucket words (+ sentinel), padded to toa_words4
     uint32_t toa_lo, toa_cap;
-    int toa_shift, toa_words4;
+    int toa_shift, toa_words4;  // toa_log: toa_shift = M (2^M log-linear buckets per octave)
+    int toa_log = 0;
     int T;
     const uint32_t *pix_tab;  // this replica's LDS table image (1 << cbits words)
     int cbits;

@@ -50,6 +50,7 @@ constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data fo
 constexpr int kEPT = kSplitEPT;               // 8 events per thread per chunk
 constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (half a chunk)
 constexpr int kSieveKeyed = 262144;           // mode bit: the stream holds finished words
+constexpr int kSieveToaLog = 1 << 20;         // mode bit: log-linear TOA buckets
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
@@ -267,7 +268,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t pid_off = (uint32_t)a.pid_off;
     const uint32_t Lc = a.L;
     const uint32_t toa_lo = a.toa_lo, toa_cap = a.toa_cap;
-    const uint32_t wmask = (1u << a.toa_shift) - 1u;
+    // log-linear TOA buckets (ABL & kSieveToaLog): the offset inside the
+    // bucket is already masked in probe(), so bin() masks nothing
+    const uint32_t wmask = (ABL & kSieveToaLog) ? 0xFFFFFFFFu : (1u << a.toa_shift) - 1u;
+    const int toa_m = a.toa_shift;  // log-linear: 2^M buckets per octave
     const uint32_t T = (uint32_t)a.T;
     const uint32_t dum_idx = o_dum + (uint32_t)lane;
     const uint32_t dum4 = dum_idx * 4u;
@@ -370,13 +374,23 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             const uint32_t q = (uint32_t)p[e] - pid_off;
             qs[e] = q;
             const uint32_t d = min((uint32_t)t[e] - toa_lo, toa_cap);
-            dc[e] = d;
+            // bucket of d: linear (d >> shift), or log-linear: s = max(0,
+            // floor(log2 d) - M), bucket (s << M) + (d >> s), width 2^s
+            uint32_t bk;
+            if (ABL & kSieveToaLog) {
+                const int sh = max(0, 31 - (int)__builtin_clz(d | 1u) - toa_m);
+                bk = ((uint32_t)sh << toa_m) + (d >> sh);
+                dc[e] = d & ((1u << sh) - 1u);
+            } else {
+                bk = d >> a.toa_shift;
+                dc[e] = d;
+            }
             if (ABL & 8) {
                 w[e] = q ^ d;
                 tw[e] = d & 0xFFFu;
             } else {
                 w[e] = lds_at(sm, o_pc4 + ((q & cmask) << 2));
-                tw[e] = lds_at(sm, o_tt4 + ((d >> a.toa_shift) << 2));
+                tw[e] = lds_at(sm, o_tt4 + (bk << 2));
             }
         }
     };
@@ -1546,7 +1560,8 @@ static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, h
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                         hipEvent_t stop) {
     const int mode = a.keyed ? kSieveKeyed
-                             : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0);
+                             : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0) |
+                                   (a.toa_log ? kSieveToaLog : 0);
     switch (mode) {
 #define LDE_SIEVE_MODE(m) \
     case m: return launch_sieve_t<m>(a, grid, st, start, stop);
@@ -1555,6 +1570,10 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     LDE_SIEVE_MODE(0) LDE_SIEVE_MODE(256) LDE_SIEVE_MODE(2048) LDE_SIEVE_MODE(65536)
     LDE_SIEVE_MODE(65536 | 256) LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048)
     LDE_SIEVE_MODE(kSieveKeyed)
+    // the same with log-linear TOA buckets (tables of geometric edges)
+    LDE_SIEVE_MODE(kSieveToaLog) LDE_SIEVE_MODE(kSieveToaLog | 256) LDE_SIEVE_MODE(kSieveToaLog | 2048)
+    LDE_SIEVE_MODE(kSieveToaLog | 65536) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256)
+    LDE_SIEVE_MODE(kSieveToaLog | 65536 | 2048) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256 | 2048)
 #ifdef LDE_DIAGNOSTICS
     // timing probes (wrong results), diagnostics build only
     LDE_SIEVE_MODE(1) LDE_SIEVE_MODE(2) LDE_SIEVE_MODE(4) LDE_SIEVE_MODE(6)

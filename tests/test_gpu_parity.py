@@ -41,6 +41,10 @@ VARIANTS = [
     # gathers issued an iteration early, cold-key stores deferred
     {'LDE_SIEVE_PACK': '1'},
     {'LDE_SIEVE_PACK': '1', 'LDE_EARLY_GATHER': '1'},
+    # log-linear TOA buckets (2^M per octave) instead of linear ones, alone
+    # and with the packed table word
+    {'LDE_SIEVE_TOA_LOG': '1'},
+    {'LDE_SIEVE_TOA_LOG': '1', 'LDE_SIEVE_PACK': '1'},
     {'LDE_DEFER_STORES': '1'},
     # cold-key sorts: block-cooperative per-key stores, wave-independent,
     # 16-byte groups with 16 / 32 keys per thread (default: 16-byte groups, 48)
