@@ -41,6 +41,7 @@ KERNEL_SYMBOL = {
     'coord': 'coord_keyed',  # wavelength-mode coordinate pass: k_key_dist + k_key_records + k_event_key
     'pixel': 'pix_pass_a',  # PIXEL pass A: k_pix_chunks + k_pix_count + scans + k_pix_scatter
     'page_accumulate': 'k_page_accumulate',
+    'monitor': 'k_monitor',  # monitor TOA histogram (--workload monitor)
     'finalize': 'k_finalize_v4',
 }
 # engine timing buckets (include/lde.h LDE_K_*) as they are used by the SPLIT
@@ -50,7 +51,8 @@ KERNEL_SYMBOL = {
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_EVENT = 8  # int32 pixel_id + int32 time_of_flight
 # the wavelength-mode coordinate pass also writes its 4-byte per-event word
-KERNEL_BYTES_PER_EVENT = {'coord': 12}
+KERNEL_BYTES_PER_EVENT = {'coord': 12, 'monitor': 4}
+MONITOR_BYTES_PER_EVENT = 4  # int32 time_of_arrival only
 
 
 def parse():
@@ -58,7 +60,9 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--workload', default='dream', choices=['dream', 'loki'])
+    ap.add_argument('--workload', default='dream', choices=['dream', 'loki', 'monitor'],
+                    help='monitor: the beam-monitor TOA histogram (A13), 1e7 events per pulse '
+                         'into 100 bins (diagnostic line, not the headline metric)')
     ap.add_argument('--coordinate', default='toa', choices=['toa', 'wavelength'],
                     help='wavelength: DREAM events binned by wavelength through a direct-flight '
                          'lookup table (diagnostic line, not the headline metric)')
@@ -204,8 +208,16 @@ def main():
     from esslivedata_amd import projection, synthetic
     from esslivedata_amd.engine import BinningEngine
 
-    inst = synthetic.dream_mantle() if args.workload == 'dream' else synthetic.loki_bank0()
-    if args.view != 'geometric':
+    monitor = args.workload == 'monitor'
+    if monitor and (args.view != 'geometric' or args.coordinate != 'toa'):
+        raise SystemExit('--workload monitor: TOA mode, no detector view')
+    inst = (synthetic.dream_mantle() if args.workload == 'dream' else
+            synthetic.loki_bank0() if args.workload == 'loki' else None)
+    if monitor:
+        from esslivedata_amd.edges import TOAEdges
+
+        view = None  # the monitor histogram: every event, one TOA axis
+    elif args.view != 'geometric':
         if args.workload != 'dream' or args.coordinate != 'toa':
             raise SystemExit('--view: DREAM mantle logical views, TOA mode')
         cfg = synthetic.dream_logical_views()[args.view]
@@ -216,7 +228,7 @@ def main():
         view = projection.geometric_lut(
             inst.detector_number, inst.coords, inst.resolution, flip_x=args.workload == 'loki'
         )
-    edges = inst.edges.edges_ns()
+    edges = TOAEdges().edges_ns() if monitor else inst.edges.edges_ns()
     coord = None
     if args.coordinate == 'wavelength':
         from esslivedata_amd import wavelength
@@ -234,15 +246,19 @@ def main():
     # the collectives: everything in order on it, no cross-stream waits
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    eng = BinningEngine(
-        toa_edges_ns=edges,
-        out_lut=view.lut,
-        pid_offset=view.pid_offset,
-        n_screen=view.n_screen,
-        strategy=args.strategy,
-        device=local,
-        stream=stream.cuda_stream,
-    )
+    if monitor:
+        eng = BinningEngine.monitor(edges, device=local, stream=stream.cuda_stream)
+    else:
+        eng = BinningEngine(
+            toa_edges_ns=edges,
+            out_lut=view.lut,
+            pid_offset=view.pid_offset,
+            n_screen=view.n_screen,
+            strategy=args.strategy,
+            device=local,
+            stream=stream.cuda_stream,
+        )
+    n_rep = 1 if monitor else view.n_replicas
     if coord is not None:
         d, tab, _ = coord
         eng.set_coordinate_lut(d, tab.table, dist0=tab.distance0, dist_step=tab.distance_step,
@@ -252,10 +268,17 @@ def main():
     seed = 7 + 1000 * rank
     if args.workload == 'dream':
         pid, toa = synthetic.torch_dream_events(n_step, inst, seed, dev)
-    else:
+    elif args.workload == 'loki':
         pid, toa = synthetic.torch_uniform_events(n_step, 1, 802816, seed, dev)
+    else:  # fake_monitors.py: TOA normal(30 ms, 10 ms)
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        toa = (torch.randn(n_step, generator=g, device=dev, dtype=torch.float32) * 10e6 + 30e6).to(
+            torch.int32)
+        pid = None
     torch.cuda.synchronize(dev)
-    nbins = view.n_screen * eng.n_toa_bins
+    nbins = (1 if monitor else view.n_screen) * eng.n_toa_bins
+    bpe_step = MONITOR_BYTES_PER_EVENT if monitor else BYTES_PER_EVENT
     from esslivedata_amd.distributed import OutputReducer
 
     # N > 1: every rank keeps its own histograms; per finalize only the
@@ -266,8 +289,8 @@ def main():
     # one device buffer view per ev44 message, made once: in the service each
     # message arrives as its own buffer, slicing here is only how the
     # synthetic stream is laid out
-    messages = [(pid[p * n_pulse : (p + 1) * n_pulse], toa[p * n_pulse : (p + 1) * n_pulse])
-                for p in range(args.pulses)]
+    messages = [(None if pid is None else pid[p * n_pulse : (p + 1) * n_pulse],
+                 toa[p * n_pulse : (p + 1) * n_pulse]) for p in range(args.pulses)]
 
     # A step bins the batch staged before it, then stages the next batch's
     # messages and finalizes the window: the next pulses' messages reach the
@@ -277,7 +300,7 @@ def main():
     # accumulates and K finalizes; the batch staged by the last step is binned
     # by the first step after the region.
     def step(i: int, stage_next: bool = True):
-        eng.accumulate(i % view.n_replicas)
+        eng.accumulate(i % n_rep)
         if stage_next:
             eng.stage_tensors_batch(messages)
         if reducer is not None:
@@ -294,7 +317,8 @@ def main():
     # with the largest time per step among them (a kernel, not a strategy:
     # in wavelength mode the coordinate pass dominates the sieve)
     names = ('atomic', 'partition', 'tile_accumulate', 'plan', 'paged', 'page_plan',
-             'page_accumulate', 'split', 'split_aux', 'coord', 'pixel', 'binning', 'finalize')
+             'page_accumulate', 'split', 'split_aux', 'coord', 'pixel', 'monitor', 'binning',
+             'finalize')
     eng.timing_select(None)
     eng.timing_enable(True)
     n_prof = 3
@@ -348,7 +372,7 @@ def main():
     # messages as host arrays, staged through lde_stage (copy into the pinned
     # ring + async H2D on the engine stream), binned and finalized
     e2e = None
-    if args.e2e_steps > 0:
+    if args.e2e_steps > 0 and not monitor:
         from esslivedata_amd.ev44 import serialise_ev44
 
         t_pulse = 1_767_225_600 * 10**9
@@ -394,7 +418,7 @@ def main():
     total_events = n_step * args.steps * world
     value = total_events / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
-    step_gbs = (BYTES_PER_EVENT * n_step + 4 * nbins) * world / (ms_per_step / 1e3) / 1e9
+    step_gbs = (bpe_step * n_step + 4 * nbins) * world / (ms_per_step / 1e3) / 1e9
 
     # dominant kernel and its roofline (HIP events of the timed region)
     ms, launches = timed[dom]
@@ -407,7 +431,7 @@ def main():
                  args.workload if args.view == 'geometric' else args.view)
     traffic = profiled_traffic(prof_name, dom)
     bin_ms, bin_n = stats['binning']  # the extra steps
-    pipeline_gbs = BYTES_PER_EVENT * n_step / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0
+    pipeline_gbs = bpe_step * n_step / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0
 
     result = {
         'metric': 'binned events/sec (whole node), DREAM-scale detector view; % HBM roofline',
@@ -423,15 +447,16 @@ def main():
         'dtype': 'int32',
         'data': 'synthetic (seeded ev44-shaped streams generated in HBM; no recorded data offline)',
         'config': {
-            'workload': ('dream_mantle_cylinder_mantle_z' if args.workload == 'dream'
+            'workload': ('monitor_toa_histogram' if monitor else
+                         'dream_mantle_cylinder_mantle_z' if args.workload == 'dream'
                          else 'loki_bank0_xy_plane') if args.view == 'geometric'
                         else f'dream_mantle_{args.view}',
             'coordinate': args.coordinate,
-            'pixels': int(inst.detector_number.size),
-            'screen': list(view.screen_shape),
-            'replicas': view.n_replicas,
+            'pixels': 0 if monitor else int(inst.detector_number.size),
+            'screen': [1] if monitor else list(view.screen_shape),
+            'replicas': n_rep,
             'toa_bins': eng.n_toa_bins,
-            'toa_edges': inst.edges.scale,
+            'toa_edges': 'linear' if monitor else inst.edges.scale,
             'events_per_step': n_step,
             'pulses_per_step': args.pulses,
             'strategy': info['last_strategy'],
@@ -457,7 +482,7 @@ def main():
             'pipeline_achieved': pipeline_gbs,
             'pipeline_frac': pipeline_gbs / HBM_PEAK_GBS,
             # whole step (incl. finalize and host gaps): SURVEY 8(d)'s
-            # (8 N + 4 S T) bytes per step over ms_per_step
+            # (8 N + 4 S T) bytes per step (4 N + 4 T for a monitor) over ms_per_step
             'step_achieved': step_gbs,
             'step_frac': step_gbs / HBM_PEAK_GBS,
             'lds': profiled_lds(prof_name, dom),
@@ -468,7 +493,32 @@ def main():
     }
     if e2e is not None:
         result['end_to_end'] = e2e
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and coord is None:
+    if rank == 0 and world == 1 and monitor:
+        # parity leg: one more step's histogram against the NumPy oracle
+        # (monitor_workflow.py:90-100 event mode) on the whole batch; the CPU
+        # baseline is that oracle timed on a 2e7-event slice (1 core)
+        from oracle import scipp_semantics as ora
+
+        eng.stage_tensors_batch(messages)
+        eng.accumulate(0)
+        chk = eng.finalize(hists=True)
+        toa_h = toa.cpu().numpy()
+        ref = ora.monitor_histogram(toa_h, edges)
+        m = min(len(toa_h), 20_000_000)
+        t_c = time.perf_counter()
+        ora.monitor_histogram(toa_h[:m], edges)
+        t_c = time.perf_counter() - t_c
+        result['check'] = {
+            'current_total': chk.current_total,
+            'bit_exact_vs_oracle': bool(np.array_equal(np.asarray(chk.current_hist).ravel(), ref)),
+        }
+        if not args.no_cpu_baseline:
+            result['cpu_baseline'] = {
+                'value': m / t_c, 'unit': 'events/s', 'cores': 1, 'kind': 'port',
+                'sample': f'oracle.scipp_semantics.monitor_histogram (NumPy, 1 core) on {m} events '
+                          f'of the bench batch, {t_c:.2f} s',
+            }
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and coord is None:
         # CPU baseline + parity leg: one more GPU step with the full current
         # histogram read back, then the oracle over the same batch
         from oracle import scipp_semantics as ora

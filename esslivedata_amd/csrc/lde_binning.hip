@@ -352,37 +352,55 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_accumulate(
 // each half-wave always hit 32 distinct banks (conflict-free for any skew).
 // ---------------------------------------------------------------------------
 template <bool FAST, bool COLUMNS>
-__global__ __launch_bounds__(256) void k_monitor(const SegDesc seg,
+__global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
                                                  const unsigned char *__restrict__ g_tab,
                                                  ToaParams tp, uint32_t *__restrict__ hist) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *s_h = reinterpret_cast<uint32_t *>(smem);
     const int HB = COLUMNS ? tp.T * 32 : tp.T;
-    unsigned char *s_tab = smem + align16((size_t)HB * 4);
+    unsigned char *s_tab = smem + align16((size_t)(HB + 64) * 4);
     load_toa_tables(s_tab, g_tab, tp);
-    for (int i = threadIdx.x; i < HB; i += blockDim.x) s_h[i] = 0;
+    for (int i = threadIdx.x; i < HB + 64; i += blockDim.x) s_h[i] = 0;
     __syncthreads();
     const int col = threadIdx.x & 31;
-    const long long n = seg.n;
+    const uint32_t dummy = (uint32_t)HB + (threadIdx.x & 63u);  // dropped events count here
     const long long stride = (long long)gridDim.x * blockDim.x;
     const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    auto add = [&](int t) {
-        const int b = toa_bin<FAST>(t, s_tab, tp);
-        if (b >= 0) atomicAdd(&s_h[COLUMNS ? b * 32 + col : b], 1u);
+    // branch-free: every event adds 1 to its bin's counter or to the lane's
+    // dummy word, so no lane waits inside a branch around its LDS atomic
+    auto add = [&](int t, bool valid) __attribute__((always_inline)) {
+        const int b = FAST ? toa_bin_nb(t, s_tab, tp) : toa_bin<false>(t, s_tab, tp);
+        const uint32_t k = (valid && b >= 0) ? (COLUMNS ? (uint32_t)b * 32u + (uint32_t)col : (uint32_t)b) : dummy;
+        atomicAdd(&s_h[k], 1u);
     };
-    long long tail = 0;
-    if (((uintptr_t)seg.toa & 15u) == 0) {
-        const long long n4 = n >> 2;
-        for (long long i = i0; i < n4; i += stride) {
-            const v4i t = ld_stream4(seg.toa + 4 * i);
-            add(t[0]);
-            add(t[1]);
-            add(t[2]);
-            add(t[3]);
+    // up to kKargSegs messages per launch, their descriptors passed as kernel
+    // arguments (no descriptor upload in front); per lane U groups of four
+    // events in flight (indices clamped, so the loads are unconditional)
+    constexpr int U = 4;
+    for (int si = 0; si < n_segs; ++si) {
+        const SegDesc seg = segs.s[si];
+        const long long n = seg.n;
+        long long tail = 0;
+        if (((uintptr_t)seg.toa & 15u) == 0 && n >= 4) {
+            const long long n4 = n >> 2;
+            for (long long i = i0; i < n4; i += stride * U) {
+                v4i t[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const long long k = i + u * stride;
+                    t[u] = ld_stream4(seg.toa + 4 * (k < n4 ? k : n4 - 1));
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const bool ok = i + u * stride < n4;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) add(t[u][q], ok);
+                }
+            }
+            tail = n4 << 2;
         }
-        tail = n4 << 2;
+        for (long long i = tail + i0; i < n; i += stride) add(ld_global(seg.toa + i), true);
     }
-    for (long long i = tail + i0; i < n; i += stride) add(ld_global(seg.toa + i));
     __syncthreads();
     for (int b = threadIdx.x; b < tp.T; b += blockDim.x) {
         uint32_t v = 0;
@@ -497,16 +515,18 @@ hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const 
     return hipGetLastError();
 }
 
-hipError_t launch_monitor(const SegDesc &seg, const unsigned char *tab, const ToaParams &tp,
-                          uint32_t *hist, int grid, hipStream_t st) {
+hipError_t launch_monitor(const SegKarg &segs, int n_segs, const unsigned char *tab,
+                          const ToaParams &tp, uint32_t *hist, int grid, hipStream_t st) {
+    if (n_segs < 1 || n_segs > kKargSegs) return hipErrorInvalidValue;
     const bool columns = tp.T <= kMonitorColumnsMaxT;
-    const size_t hb = align16((size_t)(columns ? tp.T * 32 : tp.T) * 4);
+    const size_t hb = align16((size_t)((columns ? tp.T * 32 : tp.T) + 64) * 4);
     const size_t sm = hb + toa_lds_bytes(tp);
 #define LDE_MON(F, C)                                                                          \
     do {                                                                                       \
         (void)hipFuncSetAttribute((const void *)k_monitor<F, C>,                               \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);        \
-        hipLaunchKernelGGL((k_monitor<F, C>), dim3(grid), dim3(256), sm, st, seg, tab, tp, hist); \
+        hipLaunchKernelGGL((k_monitor<F, C>), dim3(grid), dim3(256), sm, st, segs, n_segs, tab, tp, \
+                           hist);                                                              \
     } while (0)
     if (tp.fast && columns) LDE_MON(true, true);
     else if (tp.fast) LDE_MON(true, false);

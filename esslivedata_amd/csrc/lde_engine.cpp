@@ -1219,16 +1219,29 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
                                  : (const void *)((const unsigned char *)h->d_lut +
                                                   (size_t)replica * h->L * lut_es);
     if (h->monitor) {
+        // one launch per kKargSegs messages (a batch of 14 pulses: one)
         h->last_strategy = LDE_STRATEGY_AUTO;
-        for (const Segment &s : segs) {
-            if (s.n == 0) continue;
-            long long g = (s.n / 4 + 255) / 256;
+        lde::SegKarg ka{};
+        int k = 0;
+        long long n = 0;
+        auto flush = [&]() -> int {
+            if (k == 0) return LDE_OK;
+            long long g = (n / 16 + 255) / 256;  // 16 events per lane and iteration
             g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 4));
             Timed tm(h, LDE_K_MONITOR);
-            HIPCALL(h, lde::launch_monitor({nullptr, s.toa, s.n, 0}, h->d_tab, h->tp, h->d_win32,
-                                           (int)g, h->stream));
+            HIPCALL(h, lde::launch_monitor(ka, k, h->d_tab, h->tp, h->d_win32, (int)g, h->stream));
+            k = 0;
+            n = 0;
+            return LDE_OK;
+        };
+        for (const Segment &s : segs) {
+            if (s.n == 0) continue;
+            ka.s[k++] = {nullptr, s.toa, s.n, 0};
+            n += s.n;
+            if (k == lde::kKargSegs)
+                if (int rc = flush()) return rc;
         }
-        return LDE_OK;
+        return flush();
     }
     int strat = auto_strategy(h, total);
     const bool auto_split = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && h->split_ok;

@@ -290,8 +290,8 @@ hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const 
                                   int n_tiles, long long n_chunks, const uint2 *items,
                                   const uint32_t *item_count, const uint32_t *tile_items,
                                   uint32_t *hist, long long n_bins, int grid, hipStream_t st);
-hipError_t launch_monitor(const SegDesc &seg, const unsigned char *tab, const ToaParams &tp,
-                          uint32_t *hist, int grid, hipStream_t st);
+hipError_t launch_monitor(const SegKarg &segs, int n_segs, const unsigned char *tab,
+                          const ToaParams &tp, uint32_t *hist, int grid, hipStream_t st);
 hipError_t launch_fold_window(uint32_t *win32, unsigned long long *win64, long long n,
                               hipStream_t st);
 hipError_t launch_merge_f32(uint32_t *batch, unsigned long long *win64, float *winf, float *cumf,

@@ -101,18 +101,6 @@ __device__ __forceinline__ void unit_load(const PixArgs &a, const PixChunk *s_ct
     }
 }
 
-// TOA bin without a branch (fast layout): out-of-range times look up a
-// clamped bucket and are dropped by the final select, so the two LDS reads of
-// every event can be in flight together
-__device__ __forceinline__ int toa_bin_nb(int t, const unsigned char *s_tab, const ToaParams &tp) {
-    const unsigned d = (unsigned)t - (unsigned)tp.lo;
-    const unsigned dc = d < tp.span ? d : tp.span - 1u;
-    const uint32_t *rthr = reinterpret_cast<const uint32_t *>(s_tab);
-    const uint16_t *bst = reinterpret_cast<const uint16_t *>(s_tab + align16((size_t)(tp.T + 1) * 4));
-    const int b = bst[dc >> tp.shift];
-    const int r = b + (dc >= rthr[b + 1] ? 1 : 0);
-    return d < tp.span ? r : -1;
-}
 template <bool FAST>
 __device__ __forceinline__ int pix_toa_bin(int t, const unsigned char *s_tab, const ToaParams &tp) {
     return FAST ? toa_bin_nb(t, s_tab, tp) : toa_bin<false>(t, s_tab, tp);
