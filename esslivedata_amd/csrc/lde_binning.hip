@@ -37,16 +37,21 @@ namespace lde {
 // ATOMIC strategy: one pass, global u32 atomics (agent scope)
 // ---------------------------------------------------------------------------
 template <typename LT, bool FAST>
-__global__ __launch_bounds__(256) void k_bin_atomic(const SegDesc seg, const LT *__restrict__ lut,
-                                                    int pid_off, unsigned L,
+__global__ __launch_bounds__(256) void k_bin_atomic(const SegKarg segs, int n_segs,
+                                                    const LT *__restrict__ lut, int pid_off,
+                                                    unsigned L,
                                                     const unsigned char *__restrict__ g_tab,
                                                     ToaParams tp, uint32_t *__restrict__ hist) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     load_toa_tables(smem, g_tab, tp);
     __syncthreads();
-    const long long n = seg.n;
     const long long stride = (long long)gridDim.x * blockDim.x;
     const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    // up to kKargSegs messages per launch (small batches: BIFROST's 45 bank
+    // messages of 1,000 events take two launches instead of 45)
+    for (int si = 0; si < n_segs; ++si) {
+    const SegDesc seg = segs.s[si];
+    const long long n = seg.n;
     long long tail = 0;
     if ((((uintptr_t)seg.pid | (uintptr_t)seg.toa) & 15u) == 0) {
         const long long n4 = n >> 2;
@@ -63,6 +68,7 @@ __global__ __launch_bounds__(256) void k_bin_atomic(const SegDesc seg, const LT 
     for (long long i = tail + i0; i < n; i += stride) {
         wave_add_aggregated<4>(hist, event_key<LT, FAST>(ld_global(seg.pid + i), ld_global(seg.toa + i),
                                                          lut, pid_off, L, smem, tp));
+    }
     }
 }
 
@@ -422,29 +428,30 @@ size_t partition_smem(int n_tiles, const ToaParams &tp) {
 }
 
 template <typename LT>
-static hipError_t launch_bin_atomic_t(const SegDesc &seg, const LT *lut, int pid_off, unsigned L,
-                                      const unsigned char *tab, const ToaParams &tp,
+static hipError_t launch_bin_atomic_t(const SegKarg &seg, int n_segs, const LT *lut, int pid_off,
+                                      unsigned L, const unsigned char *tab, const ToaParams &tp,
                                       uint32_t *hist, int grid, hipStream_t st) {
     const size_t sm = toa_lds_bytes(tp);
     if (tp.fast) {
         (void)hipFuncSetAttribute((const void *)k_bin_atomic<LT, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL((k_bin_atomic<LT, true>), dim3(grid), dim3(256), sm, st, seg, lut,
+        hipLaunchKernelGGL((k_bin_atomic<LT, true>), dim3(grid), dim3(256), sm, st, seg, n_segs, lut,
                            pid_off, L, tab, tp, hist);
     } else {
         (void)hipFuncSetAttribute((const void *)k_bin_atomic<LT, false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL((k_bin_atomic<LT, false>), dim3(grid), dim3(256), sm, st, seg, lut,
+        hipLaunchKernelGGL((k_bin_atomic<LT, false>), dim3(grid), dim3(256), sm, st, seg, n_segs, lut,
                            pid_off, L, tab, tp, hist);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_bin_atomic(const SegDesc &seg, const void *lut, bool lut16, int pid_off,
+hipError_t launch_bin_atomic(const SegKarg &seg, int n_segs, const void *lut, bool lut16, int pid_off,
                              unsigned L, const unsigned char *tab, const ToaParams &tp,
                              uint32_t *hist, int grid, hipStream_t st) {
-    return lut16 ? launch_bin_atomic_t(seg, (const uint16_t *)lut, pid_off, L, tab, tp, hist, grid, st)
-                 : launch_bin_atomic_t(seg, (const int *)lut, pid_off, L, tab, tp, hist, grid, st);
+    if (n_segs < 1 || n_segs > kKargSegs) return hipErrorInvalidValue;
+    return lut16 ? launch_bin_atomic_t(seg, n_segs, (const uint16_t *)lut, pid_off, L, tab, tp, hist, grid, st)
+                 : launch_bin_atomic_t(seg, n_segs, (const int *)lut, pid_off, L, tab, tp, hist, grid, st);
 }
 
 template <int TB, typename LT, bool FAST, bool PEEL>

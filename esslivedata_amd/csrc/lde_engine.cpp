@@ -1263,16 +1263,29 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
     }
     h->last_strategy = strat;
     if (strat == LDE_STRATEGY_ATOMIC) {
-        for (const Segment &s : segs) {
-            if (s.n == 0) continue;
-            long long g = (s.n / 4 + 255) / 256;
+        // one launch per kKargSegs messages, descriptors as kernel arguments
+        lde::SegKarg ka{};
+        int k = 0;
+        long long n = 0;
+        auto flush = [&]() -> int {
+            if (k == 0) return LDE_OK;
+            long long g = (n / 4 + 255) / 256;
             g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 8));
             Timed tm(h, LDE_K_ATOMIC);
-            HIPCALL(h, lde::launch_bin_atomic({s.pid, s.toa, s.n, 0}, lut, h->lut16, h->pid_off,
-                                              (unsigned)h->L, h->d_tab, h->tp, h->d_win32, (int)g,
-                                              h->stream));
+            HIPCALL(h, lde::launch_bin_atomic(ka, k, lut, h->lut16, h->pid_off, (unsigned)h->L, h->d_tab,
+                                              h->tp, h->d_win32, (int)g, h->stream));
+            k = 0;
+            n = 0;
+            return LDE_OK;
+        };
+        for (const Segment &s : segs) {
+            if (s.n == 0) continue;
+            ka.s[k++] = {s.pid, s.toa, s.n, 0};
+            n += s.n;
+            if (k == lde::kKargSegs)
+                if (int rc = flush()) return rc;
         }
-        return LDE_OK;
+        return flush();
     }
     // PARTITION / PAGED
     long long chunks = 0;

@@ -51,6 +51,14 @@ struct SegDesc {  // one staged ev44 message (device pointers)
     long long chunk0;  // first global chunk of this segment
 };
 
+// Batches of up to kKargSegs messages: the descriptors travel as kernel
+// arguments (no pinned staging + H2D copy before the event pass): the sieve's
+// chunk-table path, the monitor and the atomic strategy.
+constexpr int kKargSegs = 24;
+struct SegKarg {
+    SegDesc s[kKargSegs];
+};
+
 struct ToaParams {
     long long lo;   // ceil(edge[0])  (clamped to [INT32_MIN, INT32_MAX + 1])
     long long hi;   // ceil(edge[T])
@@ -98,7 +106,7 @@ inline unsigned grid_for(long long n) {
 
 size_t partition_smem(int n_tiles, const ToaParams &tp);
 
-hipError_t launch_bin_atomic(const SegDesc &seg, const void *lut, bool lut16, int pid_off,
+hipError_t launch_bin_atomic(const SegKarg &seg, int n_segs, const void *lut, bool lut16, int pid_off,
                              unsigned L, const unsigned char *tab, const ToaParams &tp,
                              uint32_t *hist, int grid, hipStream_t st);
 hipError_t launch_partition(const PartitionArgs &a, hipStream_t st);
@@ -170,13 +178,6 @@ constexpr int kSieveMaxT = 254;
 constexpr int kHostPartials = 1024;
 constexpr int kColdGroups = 2;  // SIEVE cold keys: wave groups per block, one sort block each
 
-// Batches of up to kKargSegs messages: the descriptors travel as kernel
-// arguments (no pinned staging + H2D copy before the event pass); the kernel
-// also writes them to segs_out for the kernels that read the device table.
-constexpr int kKargSegs = 24;
-struct SegKarg {
-    SegDesc s[kKargSegs];
-};
 // SIEVE: chunk tables of up to this many entries per block live in LDS,
 // built by the sieve itself from kernel-argument descriptors
 constexpr int kSieveLdsChunks = 128;
