@@ -60,9 +60,11 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--workload', default='dream', choices=['dream', 'loki', 'monitor'],
+    ap.add_argument('--workload', default='dream', choices=['dream', 'loki', 'monitor', 'bifrost'],
                     help='monitor: the beam-monitor TOA histogram (A13), 1e7 events per pulse '
-                         'into 100 bins (diagnostic line, not the headline metric)')
+                         'into 100 bins; bifrost: 45 bank messages of 1,000 events per pulse into '
+                         'the float32 15 x 900 unified view, one accumulate (f32 push) per pulse, '
+                         'one finalize per step (diagnostic lines, not the headline metric)')
     ap.add_argument('--coordinate', default='toa', choices=['toa', 'wavelength'],
                     help='wavelength: DREAM events binned by wavelength through a direct-flight '
                          'lookup table (diagnostic line, not the headline metric)')
@@ -209,14 +211,18 @@ def main():
     from esslivedata_amd.engine import BinningEngine
 
     monitor = args.workload == 'monitor'
-    if monitor and (args.view != 'geometric' or args.coordinate != 'toa'):
-        raise SystemExit('--workload monitor: TOA mode, no detector view')
+    bifrost = args.workload == 'bifrost'
+    if (monitor or bifrost) and (args.view != 'geometric' or args.coordinate != 'toa'):
+        raise SystemExit(f'--workload {args.workload}: TOA mode, its own view')
     inst = (synthetic.dream_mantle() if args.workload == 'dream' else
-            synthetic.loki_bank0() if args.workload == 'loki' else None)
-    if monitor:
-        from esslivedata_amd.edges import TOAEdges
+            synthetic.loki_bank0() if args.workload == 'loki' else
+            synthetic.bifrost_unified() if bifrost else None)
+    from esslivedata_amd.edges import TOAEdges
 
+    if monitor:
         view = None  # the monitor histogram: every event, one TOA axis
+    elif bifrost:  # bifrost/specs.py:285-299: (arc, tube) x (channel, pixel), float32
+        view = projection.logical_lut(inst.detector_number, transform=synthetic.bifrost_transform)
     elif args.view != 'geometric':
         if args.workload != 'dream' or args.coordinate != 'toa':
             raise SystemExit('--view: DREAM mantle logical views, TOA mode')
@@ -257,19 +263,26 @@ def main():
             strategy=args.strategy,
             device=local,
             stream=stream.cuda_stream,
+            **({'out_dtype': 'float32'} if bifrost else {}),
         )
     n_rep = 1 if monitor else view.n_replicas
     if coord is not None:
         d, tab, _ = coord
         eng.set_coordinate_lut(d, tab.table, dist0=tab.distance0, dist_step=tab.distance_step,
                                time0=tab.time0, time_step=tab.time_step)
-    n_pulse = args.events_per_pulse
+    n_pulse = 45 * 1000 if bifrost else args.events_per_pulse  # bifrost/streams.py:22-43
     n_step = n_pulse * args.pulses
     seed = 7 + 1000 * rank
     if args.workload == 'dream':
         pid, toa = synthetic.torch_dream_events(n_step, inst, seed, dev)
     elif args.workload == 'loki':
         pid, toa = synthetic.torch_uniform_events(n_step, 1, 802816, seed, dev)
+    elif bifrost:  # fake_detectors.py: uniform ids, TOA normal(30 ms, 10 ms)
+        pid, _ = synthetic.torch_uniform_events(n_step, 1, 13500, seed, dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + 1)
+        toa = (torch.randn(n_step, generator=g, device=dev, dtype=torch.float32) * 10e6 + 30e6).to(
+            torch.int32)
     else:  # fake_monitors.py: TOA normal(30 ms, 10 ms)
         g = torch.Generator(device=dev)
         g.manual_seed(seed)
@@ -291,6 +304,10 @@ def main():
     # synthetic stream is laid out
     messages = [(None if pid is None else pid[p * n_pulse : (p + 1) * n_pulse],
                  toa[p * n_pulse : (p + 1) * n_pulse]) for p in range(args.pulses)]
+    if bifrost:  # per pulse one message per bank (300 pixels each), 1,000 events each
+        pushes = [[(pid[p * n_pulse + b * 1000 : p * n_pulse + (b + 1) * 1000],
+                    toa[p * n_pulse + b * 1000 : p * n_pulse + (b + 1) * 1000]) for b in range(45)]
+                  for p in range(args.pulses)]
 
     # A step bins the batch staged before it, then stages the next batch's
     # messages and finalizes the window: the next pulses' messages reach the
@@ -300,6 +317,12 @@ def main():
     # accumulates and K finalizes; the batch staged by the last step is binned
     # by the first step after the region.
     def step(i: int, stage_next: bool = True):
+        if bifrost:  # every pulse is one accumulate (a float32 push, reference order)
+            for push in pushes:
+                eng.stage_tensors_batch(push)
+                eng.accumulate(0)
+            eng.finalize(images=True)
+            return
         eng.accumulate(i % n_rep)
         if stage_next:
             eng.stage_tensors_batch(messages)
@@ -308,7 +331,8 @@ def main():
         else:
             eng.finalize(images=True)
 
-    eng.stage_tensors_batch(messages)
+    if not bifrost:
+        eng.stage_tensors_batch(messages)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
@@ -372,7 +396,7 @@ def main():
     # messages as host arrays, staged through lde_stage (copy into the pinned
     # ring + async H2D on the engine stream), binned and finalized
     e2e = None
-    if args.e2e_steps > 0 and not monitor:
+    if args.e2e_steps > 0 and not (monitor or bifrost):
         from esslivedata_amd.ev44 import serialise_ev44
 
         t_pulse = 1_767_225_600 * 10**9
@@ -431,7 +455,8 @@ def main():
                  args.workload if args.view == 'geometric' else args.view)
     traffic = profiled_traffic(prof_name, dom)
     bin_ms, bin_n = stats['binning']  # the extra steps
-    pipeline_gbs = bpe_step * n_step / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0
+    n_acc = n_pulse if bifrost else n_step  # events one accumulate bins
+    pipeline_gbs = bpe_step * n_acc / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0
 
     result = {
         'metric': 'binned events/sec (whole node), DREAM-scale detector view; % HBM roofline',
@@ -447,7 +472,7 @@ def main():
         'dtype': 'int32',
         'data': 'synthetic (seeded ev44-shaped streams generated in HBM; no recorded data offline)',
         'config': {
-            'workload': ('monitor_toa_histogram' if monitor else
+            'workload': ('monitor_toa_histogram' if monitor else 'bifrost_unified_f32' if bifrost else
                          'dream_mantle_cylinder_mantle_z' if args.workload == 'dream'
                          else 'loki_bank0_xy_plane') if args.view == 'geometric'
                         else f'dream_mantle_{args.view}',
@@ -517,6 +542,41 @@ def main():
                 'value': m / t_c, 'unit': 'events/s', 'cores': 1, 'kind': 'port',
                 'sample': f'oracle.scipp_semantics.monitor_histogram (NumPy, 1 core) on {m} events '
                           f'of the bench batch, {t_c:.2f} s',
+            }
+    elif rank == 0 and world == 1 and bifrost:
+        # parity leg: one more step (14 f32 pushes) from zeroed accumulators
+        # against the oracle's float32 per-push sums (accumulators.py:86-163)
+        from oracle import scipp_semantics as ora
+
+        eng.clear()
+        for push in pushes:
+            eng.stage_tensors_batch(push)
+            eng.accumulate(0)
+        chk = eng.finalize(hists=True)
+        pid_h, toa_h = pid.cpu().numpy(), toa.cpu().numpy()
+        o = ora.OracleDetectorView(
+            detector_number=inst.detector_number,
+            pixel_screen=ora.logical_screen_index(inst.detector_number.shape,
+                                                  synthetic.bifrost_transform)[0][None],
+            screen_shape=(15, 900), toa_edges_ns=edges, dtype=np.float32)
+        t_c = time.perf_counter()
+        for p in range(args.pulses):
+            o.accumulate(pid_h[p * n_pulse : (p + 1) * n_pulse], toa_h[p * n_pulse : (p + 1) * n_pulse])
+        exp = o.finalize()
+        t_c = time.perf_counter() - t_c
+        result['check'] = {
+            'current_total': float(exp['histogram_current'].sum()),
+            'bit_exact_vs_oracle': bool(
+                chk.current_hist.dtype == np.float32
+                and np.array_equal(chk.current_hist, exp['histogram_current'])
+                and np.array_equal(chk.cumulative_hist, exp['histogram_cumulative'])),
+        }
+        if not args.no_cpu_baseline:
+            result['cpu_baseline'] = {
+                'value': n_step / t_c, 'unit': 'events/s', 'cores': 1, 'kind': 'port',
+                'sample': f'oracle.scipp_semantics.OracleDetectorView (NumPy, 1 core, float32 '
+                          f'per-push sums) on one step ({args.pulses} pushes, {n_step} events), '
+                          f'{t_c:.2f} s',
             }
     elif rank == 0 and world == 1 and not args.no_cpu_baseline and coord is None:
         # CPU baseline + parity leg: one more GPU step with the full current

@@ -15,12 +15,14 @@ if [ -z "$SKIP_PROF" ]; then
   prof loki loki ""
   prof wavelength dream "--coordinate wavelength"
   prof monitor monitor ""
+  prof bifrost bifrost ""
 fi
 [ -n "$SKIP_BENCH" ] && exit 0
 timeout -k 10 400 python bench.py > gpurun_out/bench_dream.log 2>&1 || { tail -20 gpurun_out/bench_dream.log; exit 1; }
 timeout -k 10 300 python bench.py --workload loki --e2e-steps 0 --cpu-baseline-seconds 3 > gpurun_out/bench_loki.log 2>&1 || { tail -20 gpurun_out/bench_loki.log; exit 1; }
 timeout -k 10 300 python bench.py --coordinate wavelength --no-cpu-baseline --e2e-steps 0 > gpurun_out/bench_wl.log 2>&1 || { tail -20 gpurun_out/bench_wl.log; exit 1; }
 timeout -k 10 300 python bench.py --workload monitor --cpu-baseline-seconds 3 > gpurun_out/bench_monitor.log 2>&1 || { tail -20 gpurun_out/bench_monitor.log; exit 1; }
+timeout -k 10 300 python bench.py --workload bifrost > gpurun_out/bench_bifrost.log 2>&1 || { tail -20 gpurun_out/bench_bifrost.log; exit 1; }
 for v in strip_view wire_view mantle_front_layer; do
   timeout -k 10 300 python bench.py --view $v --e2e-steps 0 --cpu-baseline-seconds 3 > gpurun_out/bench_$v.log 2>&1 || { tail -20 gpurun_out/bench_$v.log; exit 1; }
 done
@@ -29,6 +31,7 @@ grep -h '^{' gpurun_out/bench_dream.log | tail -1 > gpurun_out/profiles/${TAG}_b
 grep -h '^{' gpurun_out/bench_loki.log | tail -1 > gpurun_out/profiles/${TAG}_loki_bench_line.json
 grep -h '^{' gpurun_out/bench_wl.log | tail -1 > gpurun_out/profiles/${TAG}_wavelength_bench_line.json
 grep -h '^{' gpurun_out/bench_monitor.log | tail -1 > gpurun_out/profiles/${TAG}_monitor_bench_line.json
+grep -h '^{' gpurun_out/bench_bifrost.log | tail -1 > gpurun_out/profiles/${TAG}_bifrost_bench_line.json
 for v in strip_view wire_view mantle_front_layer; do
   grep -h '^{' gpurun_out/bench_$v.log | tail -1 > gpurun_out/profiles/${TAG}_${v}_bench_line.json
 done
