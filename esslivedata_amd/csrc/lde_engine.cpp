@@ -183,6 +183,14 @@ struct lde_handle {
     uint32_t *d_pitem_count = nullptr;
     int pix_grid = 0, pix_unit = 2, pix_ept = 16, pix_bu = 4, pix_items_per_cu = 0;
     bool pix24 = true;
+    // predicted slots (LDE_PIX_PRED, default on): the last scatter's run
+    // totals (d_pprev) size this batch's slots, no count pass
+    bool pix_pred = true;
+    uint32_t *d_pprev = nullptr, *d_povf = nullptr;
+    uint4 *d_povf_grp = nullptr;
+    size_t povf_cap = 0;
+    long long pix_prev_n = 0, pix_prev_units = 0;
+    int pix_prev_grid = 0;
     std::vector<double> edges;  // the create-time edges (event unit)
     // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
     bool lds_ctab = true, karg_segs = true;
@@ -1164,7 +1172,22 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     // runs padded to 4 payloads: at most 3 pads per (unit, range); 24-bit
     // payloads take 3 bytes each
     const long long units = (chunks + h->pix_unit - 1) / h->pix_unit;
-    const size_t n_pay = (size_t)total + 3 * (size_t)units * (size_t)h->pix.nr + 4;
+    const int grid = (int)std::min<long long>(units, (long long)h->pix_grid);
+    size_t n_pay = (size_t)total + 3 * (size_t)units * (size_t)h->pix.nr + 4;
+    // predicted slots: the previous batch had the same blocks and a similar
+    // size, and slots average >= 256 events (margins <= 22 %).  Slot sum
+    // bound: caps <= 1.25 x pred + 20 per slot, run totals <= events + pads
+    const long long slots = (long long)grid * h->pix.nr;
+    const double ratio = h->pix_prev_n > 0 ? (double)total / (double)h->pix_prev_n : 0.0;
+    const double pred_pay = 1.25 * ratio * (double)(h->pix_prev_n + 3 * h->pix_prev_units * h->pix.nr) +
+                            20.0 * (double)slots + 4.0;
+    const bool pred = h->pix_pred && h->pix_prev_grid == grid && ratio >= 0.5 && ratio <= 2.0 &&
+                      total >= 256 * slots && pred_pay < 0x7FFFFFF0;
+    const size_t ovf_groups = n_pay / 4 + 1;  // every group of the batch, at most
+    if (pred) {
+        n_pay = std::max(n_pay, (size_t)pred_pay);
+        if (int rc = grow(h, &h->d_povf_grp, h->povf_cap, ovf_groups)) return rc;
+    }
     if (int rc = grow(h, &h->d_ppayload, h->ppayload_cap, h->pix24 ? (n_pay * 3 + 3) / 4 + 4 : n_pay))
         return rc;
     // pass-B items: each flushes its range's whole footprint (F x T
@@ -1176,7 +1199,7 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     const long long per =
         (std::max<long long>(65536, ipc == 0 ? (2 * total + h->pix.nr - 1) / h->pix.nr
                                               : (total + ipc * h->cus - 1) / (ipc * h->cus)) + 3) & ~3LL;
-    const long long max_items = total / per + h->pix.nr + 1;
+    const long long max_items = (long long)(n_pay / (size_t)per) + h->pix.nr + 1;
     if (int rc = grow(h, &h->d_pitems, h->pitems_cap, (size_t)max_items)) return rc;
     if (int rc = grow(h, &h->d_pctab, h->pctab_cap, (size_t)chunks)) return rc;
     lde::PixArgs a;
@@ -1198,7 +1221,17 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.unit = h->pix_unit;
     a.p24 = h->pix24 ? 1 : 0;
     a.bu = h->pix_bu;
-    a.grid = (int)std::min<long long>(units, (long long)h->pix_grid);
+    a.grid = grid;
+    a.prev = h->d_pprev;
+    a.ovf = h->d_povf;
+    if (pred) {
+        a.pred = (float)ratio;
+        a.ovf_grp = h->d_povf_grp;
+        a.ovf_cap = (uint32_t)ovf_groups;
+    }
+    h->pix_prev_n = total;  // the scatter records this batch's run totals
+    h->pix_prev_units = units;
+    h->pix_prev_grid = grid;
     {
         Timed tm(h, LDE_K_PIXEL);
         HIPCALL(h, lde::launch_pixel(a, h->pix, replica, (uint32_t)per, (int)max_items, h->d_pitems,
@@ -1475,16 +1508,23 @@ int build_pixel(lde_handle *h, const int32_t *lut) {
     h->pix24 = env_ll("LDE_PIX24", 1) != 0;
     h->pix_bu = env_ll("LDE_PIX_BU", 4) == 8 ? 8 : 4;
     h->pix_items_per_cu = (int)std::max<long long>(0, std::min<long long>(16, env_ll("LDE_PIX_ITEMS", 0)));
-    // blocks of unit * kChunk / ept threads: 4 x 512 or 2 x 1024 per CU
+    // blocks of unit * kChunk / ept threads: 4 x 512 or 2 x 1024 per CU; one
+    // 1024-thread block per CU with predicted slots (half the slots, so
+    // relatively smaller margins: LOKI step 0.529 -> 0.520 ms)
+    h->pix_pred = env_ll("LDE_PIX_PRED", 1) != 0;
     h->pix_grid = (int)std::max<long long>(
-        1, env_ll("LDE_PIX_GRID", (h->pix_ept == 16 && h->pix_unit == 1 ? 4 : 2) * (long long)h->cus));
+        1, env_ll("LDE_PIX_GRID", (h->pix_ept == 16 && h->pix_unit == 1 ? 4 : h->pix_pred ? 1 : 2) *
+                                      (long long)h->cus));
     while (h->pix_unit > 1 && lde::pix_scatter_smem(h->tp, h->pix_unit) > 150 * 1024) --h->pix_unit;
     if (lde::pix_scatter_smem(h->tp, h->pix_unit) > 160 * 1024) return LDE_OK;
     if (!h->d_pcounts) {
         if (int rc = dev_alloc(h, &h->d_pcounts, (size_t)h->pix_grid * lde::kPixMaxRanges)) return rc;
+        if (int rc = dev_alloc(h, &h->d_pprev, (size_t)h->pix_grid * lde::kPixMaxRanges)) return rc;
+        if (int rc = dev_alloc(h, &h->d_povf, 1)) return rc;
         if (int rc = dev_alloc(h, &h->d_prstart, 2 * (size_t)lde::kPixMaxRanges + 1)) return rc;
         if (int rc = dev_alloc(h, &h->d_pitem_count, 1)) return rc;
     }
+    h->pix_prev_n = 0;  // ranges may have changed: the next batch counts
     h->pix.rb = rb;
     h->pix.nr = nr;
     h->pix.rs = rs;
@@ -1558,6 +1598,9 @@ void release(lde_handle *h) {
     dev_free(h->d_pctab);
     dev_free(h->d_pitems);
     dev_free(h->d_pitem_count);
+    dev_free(h->d_pprev);
+    dev_free(h->d_povf);
+    dev_free(h->d_povf_grp);
     dev_free(h->d_win32);
     dev_free(h->d_win64);
     dev_free(h->d_cum);

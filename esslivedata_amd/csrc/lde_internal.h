@@ -402,6 +402,15 @@ struct PixArgs {
     int ept = 8;                 // events per thread and load: unit * kChunk / ept threads
     int p24 = 1;                 // 3-byte payloads
     int bu = 4;                  // pass B: groups per lane in flight (4 or 8)
+    // predicted slots (no count pass): every (block, range) slot is sized
+    // from the previous batch's run totals (prev) scaled by pred; a run past
+    // its slot goes to the overflow groups, added at the end of pass B.  pred = 0:
+    // exact slots from k_pix_count.  The scatter always records prev.
+    float pred = 0.f;
+    uint32_t *prev = nullptr;    // [grid][nr] padded run totals of the last scatter
+    uint32_t *ovf = nullptr;     // [1] overflow groups written (reset by k_pix_chunks)
+    uint4 *ovf_grp = nullptr;    // [ovf_cap] staging words (range << rs | payload) x 4
+    uint32_t ovf_cap = 0;
 };
 struct PixSetup {                // setup-time tables (lde_create / lde_set_lut)
     int rb = 0, nr = 0, fmax = 0, rs = 24;
@@ -411,7 +420,8 @@ struct PixSetup {                // setup-time tables (lde_create / lde_set_lut)
 };
 size_t pix_scatter_smem(const ToaParams &tp, int unit);
 size_t pix_acc_smem(int rb, int fmax, int T);
-// phase 0: count + scan + scatter; phase 1: accumulate
+// phase 0: count (exact slots) + scan + scatter; phase 1: accumulate (+ the
+// overflow groups with predicted slots)
 hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32_t item_events,
                         int max_items, uint4 *items, uint32_t *item_count, uint32_t *hist,
                         hipStream_t st, int phase);

@@ -10,6 +10,7 @@
 // the range's slice of the LUT sits in LDS:
 //
 //   k_pix_count      events per (block, range), pid stream only
+//                    (predicted slots skip it: see below)
 //   k_pix_scan       range-major exclusive offsets, range starts, work items
 //   k_pix_scatter    per 8,192-event chunk: rank by range (LDS atomics), scan,
 //                    range-sorted LDS staging, coalesced runs to each range's
@@ -22,6 +23,18 @@
 // Unknown ids (pid outside the LUT) are dropped in the count and the
 // scatter alike; pixels the view drops map to 0xFFFF in the slice.  Counts
 // are bit-identical to every other strategy.
+//
+// Predicted slots (PixArgs::pred > 0): the count pass reads the pid stream
+// only to size every (block, range) slot.  A stream's per-slot totals change
+// little from batch to batch (each slot holds thousands of events), so the
+// slots can be sized from the previous batch's totals instead (the scatter
+// records them in prev), scaled to this batch's size, plus a margin of
+// 2 sqrt(n) + 4.  The scatter fills each slot's unused tail with dropped
+// payloads; a run that does not fit goes, as raw staging words, to the
+// overflow groups, which pass B's blocks add with global atomics after their
+// items (pix_overflow).  Every
+// event is still counted exactly once: a prediction only decides where its
+// payload is stored.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -132,6 +145,7 @@ __device__ __forceinline__ const PixChunk *block_chunk_table(const PixArgs &a, P
 // kChunk: full and 16-byte aligned; -kChunk: full, misaligned)
 __global__ __launch_bounds__(256) void k_pix_chunks(PixArgs a, PixChunk *__restrict__ ctab) {
     const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (c == 0 && a.ovf) *a.ovf = 0u;  // before this batch's scatter
     if (c >= a.n_chunks) return;
     int lo = 0, hi = a.n_segs - 1;
     while (lo < hi) {
@@ -182,9 +196,17 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_count(PixArgs a) {
     for (int r = threadIdx.x; r < a.nr; r += NT) a.counts[(size_t)blockIdx.x * a.nr + r] = s_tot[r];
 }
 
+// predicted slot of a (block, range) whose run total was x in the last
+// batch: y = x * pred, y + 2 sqrt(y) + 4 rounded up to 4 (<= 1.25 y + 12);
+// Poisson noise past two sigma (about 0.4 % of a slot's events) overflows
+__device__ __forceinline__ uint32_t pix_cap(uint32_t x, float pred) {
+    const float y = (float)x * pred;
+    return ((uint32_t)(y + 2.f * __builtin_sqrtf(y) + 4.f) + 3u) & ~3u;
+}
+
 // One block per range r: its total over the blocks and the exclusive prefix
 // over blocks (counts[b][r] becomes the offset of (block b, range r) inside
-// range r).
+// range r).  Slot sizes: the counts, or predicted from prev.
 __global__ __launch_bounds__(1024) void k_pix_scan_blocks(PixArgs a, int grid,
                                                           uint32_t *__restrict__ rtot) {
     __shared__ uint32_t s_w[32];
@@ -193,7 +215,7 @@ __global__ __launch_bounds__(1024) void k_pix_scan_blocks(PixArgs a, int grid,
     for (int b0 = 0; b0 < grid; b0 += 1024) {
         const int b = b0 + (int)threadIdx.x;
         const size_t i = (size_t)b * a.nr + r;
-        const uint32_t v = b < grid ? a.counts[i] : 0u;
+        const uint32_t v = b >= grid ? 0u : a.pred > 0.f ? pix_cap(a.prev[i], a.pred) : a.counts[i];
         uint32_t tot;
         const uint32_t x = block_exclusive_scan(v, s_w, &tot);
         if (b < grid) a.counts[i] = carry + x;
@@ -232,9 +254,10 @@ __global__ __launch_bounds__(1024) void k_pix_scan(PixArgs a, const uint32_t *__
 }
 
 // LDS: staging (unit events + pads, u32) | counts, unit offsets, cursors,
-// staging positions (nr each) | scan scratch (32) | chunk table | TOA image
+// staging positions, slot ends (nr each) | scan scratch (32) | chunk table |
+// TOA image
 size_t pix_scatter_smem(const ToaParams &tp, int unit) {
-    return 4 * ((size_t)unit * kChunk + 4 * (size_t)kPixMaxRanges + 4 * (size_t)kPixMaxRanges + 32) +
+    return 4 * ((size_t)unit * kChunk + 4 * (size_t)kPixMaxRanges + 5 * (size_t)kPixMaxRanges + 32) +
            sizeof(PixChunk) * kPixLdsChunks + toa_lds_bytes(tp);
 }
 
@@ -247,14 +270,18 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     uint32_t *s_off = s_cnt + kPixMaxRanges;
     uint32_t *s_cur = s_off + kPixMaxRanges;
     uint32_t *s_pos = s_cur + kPixMaxRanges;
-    uint32_t *s_w = s_pos + kPixMaxRanges;
+    uint32_t *s_end = s_pos + kPixMaxRanges;
+    uint32_t *s_w = s_end + kPixMaxRanges;
     PixChunk *s_ctab = reinterpret_cast<PixChunk *>(s_w + 32);
     unsigned char *s_tab = reinterpret_cast<unsigned char *>(s_ctab + kPixLdsChunks);
     load_toa_tables(s_tab, a.tab, a.tp);
     const int tid = threadIdx.x;
+    const uint32_t *rtot = a.rstart + a.nr + 1;  // k_pix_scan_blocks' range totals
     for (int r = tid; r < a.nr; r += NT) {
         s_cnt[r] = 0;
         s_cur[r] = a.rstart[r] + a.counts[(size_t)blockIdx.x * a.nr + r];  // this block's slot of range r
+        s_end[r] = a.rstart[r] + ((int)blockIdx.x + 1 < a.grid ? a.counts[(size_t)(blockIdx.x + 1) * a.nr + r]
+                                                               : rtot[r]);
     }
     const uint32_t mask = (1u << a.rb) - 1u;
     // staging word: range << rs | payload (rs bits, all ones = dropped); the
@@ -309,12 +336,28 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
                 return v == dmask ? kPixDropped : v;
             };
             const uint32_t dst = s_cur[r] + (g - s_off[r]);
-            if (P24) {
-                *(g_v3u *)(reinterpret_cast<unsigned char *>(a.payload) + (size_t)dst * 3u) =
-                    pack24(pl(w.x), pl(w.y), pl(w.z), pl(w.w));
-            } else {
-                *reinterpret_cast<uint4 *>(a.payload + dst) =
-                    make_uint4(pl(w.x), pl(w.y), pl(w.z), pl(w.w));
+            const bool fits = dst < s_end[r];  // always, with exact slots
+            if (fits) {
+                if (P24) {
+                    *(g_v3u *)(reinterpret_cast<unsigned char *>(a.payload) + (size_t)dst * 3u) =
+                        pack24(pl(w.x), pl(w.y), pl(w.z), pl(w.w));
+                } else {
+                    *reinterpret_cast<uint4 *>(a.payload + dst) =
+                        make_uint4(pl(w.x), pl(w.y), pl(w.z), pl(w.w));
+                }
+            }
+            // predicted slot too small: the raw group to the overflow list,
+            // one counter atomic per wave
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(!fits);
+            if (m) {
+                const int lead = __builtin_ctzll(m);
+                uint32_t base = 0;
+                if ((tid & 63) == lead) base = atomicAdd(a.ovf, (uint32_t)__popcll(m));
+                base = __builtin_amdgcn_readlane(base, lead);
+                if (!fits) {
+                    const uint32_t k = base + lanes_below(m);
+                    if (k < a.ovf_cap) a.ovf_grp[k] = w;
+                }
             }
         }
         __syncthreads();
@@ -323,6 +366,47 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
             s_cnt[r] = 0;
         }
         __syncthreads();
+    }
+    // this batch's run totals (the next batch's prediction), then each slot's
+    // unused tail as dropped groups, one wave per range
+    for (int r = tid; r < a.nr; r += NT) {
+        const size_t i = (size_t)blockIdx.x * a.nr + r;
+        a.prev[i] = s_cur[r] - (a.rstart[r] + a.counts[i]);
+    }
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int r = wv; r < a.nr; r += NT / 64)
+        for (uint32_t d = s_cur[r] + (uint32_t)(tid & 63) * 4u; d < s_end[r]; d += 256u) {
+            if (P24) {
+                *(g_v3u *)(reinterpret_cast<unsigned char *>(a.payload) + (size_t)d * 3u) =
+                    v3u{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            } else {
+                *reinterpret_cast<uint4 *>(a.payload + d) =
+                    make_uint4(kPixDropped, kPixDropped, kPixDropped, kPixDropped);
+            }
+        }
+}
+
+
+// The overflow groups of a batch with predicted slots (normally none or a
+// few hundred), spread over pass B's blocks after their items: each event's
+// LUT entry and one global atomic.
+__device__ __forceinline__ void pix_overflow(const PixArgs &a, const uint16_t *__restrict__ loc,
+                                             const uint32_t *__restrict__ fp_off,
+                                             const uint32_t *__restrict__ fp_scr, int T,
+                                             uint32_t *__restrict__ hist) {
+    const uint32_t n0 = *a.ovf;
+    const uint32_t n = n0 < a.ovf_cap ? n0 : a.ovf_cap;
+    const uint32_t dmask = (1u << a.rs) - 1u, mask = (1u << a.rb) - 1u;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint4 w = a.ovf_grp[i];
+        const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = x[q] >> a.rs, v = x[q] & dmask;
+            if (v == dmask) continue;  // pad or TOA outside the edges
+            const uint32_t f = loc[(r << a.rb) | (v & mask)];
+            if (f != 0xFFFFu) atomicAdd(&hist[(size_t)fp_scr[fp_off[r] + f] * T + (v >> a.rb)], 1u);
+        }
     }
 }
 
@@ -338,7 +422,10 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
                                                          const uint4 *__restrict__ items,
                                                          const uint32_t *__restrict__ item_count,
                                                          int T, uint32_t *__restrict__ hist) {
-    if (blockIdx.x >= *item_count) return;
+    if (blockIdx.x >= *item_count) {
+        if (a.pred > 0.f) pix_overflow(a, loc, fp_off, fp_scr, T, hist);
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint4 it = items[blockIdx.x];
     const uint32_t r = it.x;
@@ -416,6 +503,7 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
             atomicAdd(&hist[(size_t)fp_scr[f0 + f] * T + (j - f * (uint32_t)T)], n);
         }
     }
+    if (a.pred > 0.f) pix_overflow(a, loc, fp_off, fp_scr, T, hist);
 }
 
 namespace {
@@ -425,7 +513,7 @@ void launch_pass_a(const PixArgs &a, uint32_t item_events, int max_items, uint4 
     constexpr int NT = U * kChunk / E;
     hipLaunchKernelGGL(k_pix_chunks, dim3((unsigned)((a.n_chunks + 255) / 256)), dim3(256), 0, st, a,
                        const_cast<PixChunk *>(a.ctab));
-    hipLaunchKernelGGL((k_pix_count<U, E>), dim3(a.grid), dim3(NT), 0, st, a);
+    if (a.pred <= 0.f) hipLaunchKernelGGL((k_pix_count<U, E>), dim3(a.grid), dim3(NT), 0, st, a);
     hipLaunchKernelGGL(k_pix_scan_blocks, dim3(a.nr), dim3(1024), 0, st, a, a.grid, a.rstart + a.nr + 1);
     hipLaunchKernelGGL(k_pix_scan, dim3(1), dim3(1024), 0, st, a, a.rstart + a.nr + 1, item_events,
                        items, item_count, max_items);
@@ -471,6 +559,7 @@ hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32
         } else {
             if (a.bu == 8) go(k_pix_accumulate<false, 8>); else go(k_pix_accumulate<false, 4>);
         }
+
     }
     return hipGetLastError();
 }

@@ -764,3 +764,42 @@ def test_loki_pixel_forced_on_skewed_stream_splits_hot_ranges():
                                      toa, edges)
         np.testing.assert_array_equal(res.current_hist, exp)
         assert res.current_total == int(exp.sum())
+
+
+def test_loki_pixel_predicted_slots_exact_under_shifts(monkeypatch):
+    """PIXEL with predicted slots (no count pass: each (block, range) slot is
+    sized from the previous batch's run totals).  Four partition blocks make
+    the 784 slots hold >= 256 events each at 1e6 events per batch, so every
+    batch after the first is predicted; the stream then shifts under the
+    prediction: a new seed (a few runs past their slot), 70 % of the events
+    in one pixel range, a 1.6x larger batch, one pixel only, and back.  Runs
+    that miss their slot go through the overflow groups (global atomics);
+    both replicas; counts stay bit-exact."""
+    from esslivedata_amd import projection, synthetic
+
+    monkeypatch.setenv('LDE_PIX_GRID', '4')
+    inst = synthetic.loki_bank0(n_replicas=2)
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, 'pixel')
+    ps = _oracle_pixel_screen_geometric(inst)
+    rng = np.random.default_rng(23)
+    cum = np.zeros((view.n_screen, len(edges) - 1), dtype=np.int64)
+    for batch in range(7):
+        n = 1_600_000 if batch == 4 else 1_000_000
+        pid, toa = synthetic.uniform_events(n, 1, 802816, seed=100 + batch)
+        if batch == 3:
+            hot = rng.random(n) < 0.7
+            pid[hot] = rng.integers(40_000, 44_096, int(hot.sum())).astype(np.int32)
+        elif batch == 5:
+            pid[:] = 654_321
+        eng.stage(pid, toa)
+        eng.accumulate(batch % 2)
+        res = eng.finalize(hists=True)
+        assert eng.info()['last_strategy'] == 'pixel'
+        exp = ora.detector_histogram(ps[batch % 2], view.n_screen,
+                                     ora.pixel_index(pid, inst.detector_number), toa, edges)
+        cum += exp.astype(np.int64)
+        np.testing.assert_array_equal(res.current_hist, exp)
+        np.testing.assert_array_equal(res.cumulative_hist, cum)
+        assert res.current_total == int(exp.sum())
