@@ -33,6 +33,18 @@
 
 namespace lde {
 
+// Kernel-argument message lists: this block's place in message si when the
+// message starts at block `rot`, and the next message's start (after the
+// blocks this one fills with one group of four events per thread; a message
+// that fills the whole grid leaves it where it was).
+__device__ __forceinline__ int seg_block(int rot) {
+    return (int)((blockIdx.x + gridDim.x - (unsigned)rot) % gridDim.x);
+}
+__device__ __forceinline__ int next_rot(int rot, long long n) {
+    const long long used = ((n >> 2) + blockDim.x - 1) / blockDim.x;
+    return used >= gridDim.x ? rot : (int)((rot + used) % gridDim.x);  // large ones fill the grid
+}
+
 // ---------------------------------------------------------------------------
 // ATOMIC strategy: one pass, global u32 atomics (agent scope)
 // ---------------------------------------------------------------------------
@@ -46,12 +58,16 @@ __global__ __launch_bounds__(256) void k_bin_atomic(const SegKarg segs, int n_se
     load_toa_tables(smem, g_tab, tp);
     __syncthreads();
     const long long stride = (long long)gridDim.x * blockDim.x;
-    const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     // up to kKargSegs messages per launch (small batches: BIFROST's 45 bank
-    // messages of 1,000 events take two launches instead of 45)
+    // messages of 1,000 events take two launches instead of 45); each message
+    // starts on the block after the last one the previous message used, so
+    // messages smaller than the grid run on different blocks side by side
+    int rot = 0;
     for (int si = 0; si < n_segs; ++si) {
     const SegDesc seg = segs.s[si];
     const long long n = seg.n;
+    const long long i0 = (long long)seg_block(rot) * blockDim.x + threadIdx.x;
+    rot = next_rot(rot, n);
     long long tail = 0;
     if ((((uintptr_t)seg.pid | (uintptr_t)seg.toa) & 15u) == 0) {
         const long long n4 = n >> 2;
@@ -371,7 +387,6 @@ __global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
     const int col = threadIdx.x & 31;
     const uint32_t dummy = (uint32_t)HB + (threadIdx.x & 63u);  // dropped events count here
     const long long stride = (long long)gridDim.x * blockDim.x;
-    const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     // branch-free: every event adds 1 to its bin's counter or to the lane's
     // dummy word, so no lane waits inside a branch around its LDS atomic
     auto add = [&](int t, bool valid) __attribute__((always_inline)) {
@@ -383,9 +398,12 @@ __global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
     // arguments (no descriptor upload in front); per lane U groups of four
     // events in flight (indices clamped, so the loads are unconditional)
     constexpr int U = 4;
+    int rot = 0;  // as in k_bin_atomic: small messages side by side
     for (int si = 0; si < n_segs; ++si) {
         const SegDesc seg = segs.s[si];
         const long long n = seg.n;
+        const long long i0 = (long long)seg_block(rot) * blockDim.x + threadIdx.x;
+        rot = next_rot(rot, n);
         long long tail = 0;
         if (((uintptr_t)seg.toa & 15u) == 0 && n >= 4) {
             const long long n4 = n >> 2;

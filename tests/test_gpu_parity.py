@@ -803,3 +803,42 @@ def test_loki_pixel_predicted_slots_exact_under_shifts(monkeypatch):
         np.testing.assert_array_equal(res.current_hist, exp)
         np.testing.assert_array_equal(res.cumulative_hist, cum)
         assert res.current_total == int(exp.sum())
+
+
+PIXEL_VARIANTS = [
+    {},
+    {'LDE_PIX_PRED': '0'},
+    {'LDE_PIX24': '0'},
+    {'LDE_PIX_UNIT': '1', 'LDE_PIX_EPT': '8'},
+    {'LDE_PIX_UNIT': '1', 'LDE_PIX_EPT': '16'},
+    {'LDE_PIX_BU': '8'},
+    {'LDE_PIX_ITEMS': '3'},
+    {'LDE_PIX_MAX_RANGES': '512'},
+]
+
+
+@pytest.mark.parametrize('knobs', PIXEL_VARIANTS, ids=lambda k: ','.join(f'{a}={b}' for a, b in k.items()) or 'default')
+def test_loki_pixel_variants(monkeypatch, knobs):
+    """Every PIXEL shape knob, counted (first batch) and predicted (second
+    and third: six partition blocks, so 1.2e6-event batches fill the slots),
+    bit-exact against the oracle over two replicas."""
+    from esslivedata_amd import projection, synthetic
+
+    monkeypatch.setenv('LDE_PIX_GRID', '6')
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    inst = synthetic.loki_bank0(n_replicas=2)
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, 'pixel')
+    ps = _oracle_pixel_screen_geometric(inst)
+    for batch in range(3):
+        pid, toa = synthetic.uniform_events(1_200_001 + 3 * batch, 1, 802816, seed=300 + batch)
+        eng.stage(pid[: 500_000], toa[: 500_000])
+        eng.stage(pid[500_000:], toa[500_000:])
+        eng.accumulate(batch % 2)
+        res = eng.finalize(hists=True)
+        assert eng.info()['last_strategy'] == 'pixel'
+        exp = ora.detector_histogram(ps[batch % 2], view.n_screen,
+                                     ora.pixel_index(pid, inst.detector_number), toa, edges)
+        np.testing.assert_array_equal(res.current_hist, exp)
