@@ -38,11 +38,14 @@ namespace lde {
 // blocks this one fills with one group of four events per thread; a message
 // that fills the whole grid leaves it where it was).
 __device__ __forceinline__ int seg_block(int rot) {
-    return (int)((blockIdx.x + gridDim.x - (unsigned)rot) % gridDim.x);
+    const int b = (int)blockIdx.x - rot;  // no division: 0 <= rot < gridDim.x
+    return b < 0 ? b + (int)gridDim.x : b;
 }
 __device__ __forceinline__ int next_rot(int rot, long long n) {
-    const long long used = ((n >> 2) + blockDim.x - 1) / blockDim.x;
-    return used >= gridDim.x ? rot : (int)((rot + used) % gridDim.x);  // large ones fill the grid
+    const long long n4 = n >> 2;
+    if (n4 >= (long long)gridDim.x * blockDim.x) return rot;  // large ones fill the grid
+    const int r = rot + (int)(((unsigned)n4 + blockDim.x - 1u) / blockDim.x);
+    return r >= (int)gridDim.x ? r - (int)gridDim.x : r;
 }
 
 // ---------------------------------------------------------------------------

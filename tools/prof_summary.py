@@ -71,18 +71,24 @@ def main(prof: Path, stem: Path) -> None:
             e['hbm_traffic_bytes'] = e['hbm_read_bytes'] + e['hbm_write_bytes']
             e['hbm_GBs_at_avg'] = e['hbm_traffic_bytes'] / (d['avg_ms'] * 1e-3) / 1e9
         out[k] = e
-    # composite entries for engine timing buckets that span several launches
-    # (each launched once per batch): the bucket's time is the sum of the
-    # members' averages, its traffic the sum of their traffic per dispatch
+    # composite entries for engine timing buckets that span several launches:
+    # per launch of the last member (launched once per batch), the members'
+    # time and traffic per dispatch weighted by their launches per batch (a
+    # PIXEL batch with predicted slots has no k_pix_count: only the counted
+    # first batch does)
     for name, members in COMPOSITES.items():
-        ms = [out[m] for m in members if m in out]
-        if not ms:
+        names = [m for m in members if m in out]
+        ms = [out[m] for m in names]
+        if not ms or members[-1] not in out:
             continue
-        e = {'members': [m for m in members if m in out], 'calls': min(m['calls'] for m in ms),
-             'avg_ms': sum(m['avg_ms'] for m in ms)}
+        n = out[members[-1]]['calls']
+        w = [m['calls'] / n for m in ms]
+        e = {'members': names, 'calls': n,
+             'launches_per_call': {m: round(x, 4) for m, x in zip(names, w)},
+             'avg_ms': sum(x * m['avg_ms'] for x, m in zip(w, ms))}
         if all('hbm_traffic_bytes' in m for m in ms):
             for key in ('hbm_read_bytes', 'hbm_write_bytes', 'hbm_traffic_bytes'):
-                e[key] = sum(m[key] for m in ms)
+                e[key] = sum(x * m[key] for x, m in zip(w, ms))
             e['hbm_GBs_at_avg'] = e['hbm_traffic_bytes'] / (e['avg_ms'] * 1e-3) / 1e9
         out[name] = e
     stem.parent.mkdir(parents=True, exist_ok=True)
