@@ -82,7 +82,40 @@ def parse():
                          '(a stamped dispatch costs ~16 us of step time on the sieve path)')
     ap.add_argument('--e2e-steps', type=int, default=3,
                     help='steps of the PCIe-inclusive host-staged leg (0 = skip)')
+    ap.add_argument('--batches', type=int, default=3,
+                    help='distinct pre-generated batches rotated through the steps (a stream '
+                         'never repeats the previous batch, so per-batch predictions are tested)')
     return ap.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """``--gpus N`` (N > 1) without a torchrun environment: start N rank
+    processes as children (``torch.distributed.run``, one rank per GPU,
+    rendezvous on 127.0.0.1) and return their exit code.  This process never
+    initialises HIP (``torch.cuda.device_count`` does not), so no process that
+    touched the GPU is replaced; the ranks' stdout (rank 0's JSON line) passes
+    through.  ``LDE_BENCH_BACKEND=gloo`` rehearses N ranks on fewer GPUs."""
+    import socket
+    import subprocess
+
+    backend = os.environ.get('LDE_BENCH_BACKEND', 'nccl')
+    if backend == 'nccl':
+        import torch
+
+        visible = torch.cuda.device_count()
+        if args.gpus > visible:
+            print(f'bench.py: --gpus {args.gpus} but {visible} GPU(s) visible '
+                  '(LDE_BENCH_BACKEND=gloo rehearses ranks sharing a GPU)', file=sys.stderr)
+            return 2
+    with socket.socket() as s:  # a free rendezvous port on the loopback
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           f'--nproc-per-node={args.gpus}', '--master-addr=127.0.0.1', f'--master-port={port}',
+           str(ROOT / 'bench.py'), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault('OMP_NUM_THREADS', str(max(1, min(16, len(os.sched_getaffinity(0)) // args.gpus))))
+    return subprocess.run(cmd, env=env).returncode
 
 
 def cpu_baseline(inst, ps, view, pid_h, toa_h, replica, gpu_hist, seconds: float) -> dict:
@@ -140,6 +173,20 @@ def cpu_baseline(inst, ps, view, pid_h, toa_h, replica, gpu_hist, seconds: float
     }
 
 
+def oracle_pixel_screen(args, inst):
+    """The oracle's pixel -> screen index of the bench view (test infrastructure)."""
+    from esslivedata_amd import synthetic
+    from oracle import scipp_semantics as ora
+
+    if args.view == 'geometric':
+        return ora.geometric_pixel_screen(inst.coords, inst.resolution, flip_x=args.workload == 'loki')
+    # the oracle's closed-form view index (no transform applied)
+    spec = {'mantle_front_layer': ([('module', 'segment', 'counter'), ('strip',)], {'wire': 0}),
+            'wire_view': ([('wire',), ('module', 'segment', 'counter')], {}),
+            'strip_view': ([('strip',)], {})}[args.view]
+    return ora.folded_view_index(synthetic.DREAM_BANK_SIZES['mantle_detector'], *spec)[0][None]
+
+
 def _profile_entry(workload: str, kernel: str):
     path = ROOT / 'profiles' / f'{PROFILE_ROUND}_{workload}_bench.json'
     try:
@@ -189,10 +236,14 @@ def profiled_lds(workload: str, kernel: str):
 
 def main():
     args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(args))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world != args.gpus:
+        raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}')
     rank = int(os.environ.get('RANK', '0'))
     # one GPU per rank; more ranks than GPUs (a gloo rehearsal) share them
     local = int(os.environ.get('LOCAL_RANK', '0')) % max(1, torch.cuda.device_count())
@@ -272,23 +323,25 @@ def main():
                                time0=tab.time0, time_step=tab.time_step)
     n_pulse = 45 * 1000 if bifrost else args.events_per_pulse  # bifrost/streams.py:22-43
     n_step = n_pulse * args.pulses
-    seed = 7 + 1000 * rank
-    if args.workload == 'dream':
-        pid, toa = synthetic.torch_dream_events(n_step, inst, seed, dev)
-    elif args.workload == 'loki':
-        pid, toa = synthetic.torch_uniform_events(n_step, 1, 802816, seed, dev)
-    elif bifrost:  # fake_detectors.py: uniform ids, TOA normal(30 ms, 10 ms)
-        pid, _ = synthetic.torch_uniform_events(n_step, 1, 13500, seed, dev)
+    n_batches = max(1, args.batches)
+
+    def gen(b: int, r: int = rank):
+        """Batch ``b`` of rank ``r`` (seeded; any rank can regenerate another's)."""
+        seed = 7 + 1000 * r + 17 * b
+        if args.workload == 'dream':
+            return synthetic.torch_dream_events(n_step, inst, seed, dev)
+        if args.workload == 'loki':
+            return synthetic.torch_uniform_events(n_step, 1, 802816, seed, dev)
         g = torch.Generator(device=dev)
         g.manual_seed(seed + 1)
-        toa = (torch.randn(n_step, generator=g, device=dev, dtype=torch.float32) * 10e6 + 30e6).to(
+        # fake_monitors.py / fake_detectors.py: TOA normal(30 ms, 10 ms)
+        t = (torch.randn(n_step, generator=g, device=dev, dtype=torch.float32) * 10e6 + 30e6).to(
             torch.int32)
-    else:  # fake_monitors.py: TOA normal(30 ms, 10 ms)
-        g = torch.Generator(device=dev)
-        g.manual_seed(seed)
-        toa = (torch.randn(n_step, generator=g, device=dev, dtype=torch.float32) * 10e6 + 30e6).to(
-            torch.int32)
-        pid = None
+        if bifrost:  # uniform ids over the 13,500 pixels
+            return synthetic.torch_uniform_events(n_step, 1, 13500, seed, dev)[0], t
+        return None, t
+
+    batches = [gen(b) for b in range(n_batches)]
     torch.cuda.synchronize(dev)
     nbins = (1 if monitor else view.n_screen) * eng.n_toa_bins
     bpe_step = MONITOR_BYTES_PER_EVENT if monitor else BYTES_PER_EVENT
@@ -302,12 +355,15 @@ def main():
     # one device buffer view per ev44 message, made once: in the service each
     # message arrives as its own buffer, slicing here is only how the
     # synthetic stream is laid out
-    messages = [(None if pid is None else pid[p * n_pulse : (p + 1) * n_pulse],
+    def split(pid, toa):
+        return [(None if pid is None else pid[p * n_pulse : (p + 1) * n_pulse],
                  toa[p * n_pulse : (p + 1) * n_pulse]) for p in range(args.pulses)]
+
+    batch_msgs = [split(*bt) for bt in batches]
     if bifrost:  # per pulse one message per bank (300 pixels each), 1,000 events each
-        pushes = [[(pid[p * n_pulse + b * 1000 : p * n_pulse + (b + 1) * 1000],
-                    toa[p * n_pulse + b * 1000 : p * n_pulse + (b + 1) * 1000]) for b in range(45)]
-                  for p in range(args.pulses)]
+        batch_pushes = [[[(pid[p * n_pulse + b * 1000 : p * n_pulse + (b + 1) * 1000],
+                           toa[p * n_pulse + b * 1000 : p * n_pulse + (b + 1) * 1000])
+                          for b in range(45)] for p in range(args.pulses)] for pid, toa in batches]
 
     # A step bins the batch staged before it, then stages the next batch's
     # messages and finalizes the window: the next pulses' messages reach the
@@ -316,23 +372,26 @@ def main():
     # Every step stages one batch, so the timed region holds K stagings, K
     # accumulates and K finalizes; the batch staged by the last step is binned
     # by the first step after the region.
+    # Step i bins batch i % n_batches: consecutive steps never see the same
+    # events (a stream's batches differ; per-batch predictions such as PIXEL's
+    # slot sizes are exercised as in the service).
     def step(i: int, stage_next: bool = True):
         if bifrost:  # every pulse is one accumulate (a float32 push, reference order)
-            for push in pushes:
+            for push in batch_pushes[i % n_batches]:
                 eng.stage_tensors_batch(push)
                 eng.accumulate(0)
             eng.finalize(images=True)
             return
         eng.accumulate(i % n_rep)
         if stage_next:
-            eng.stage_tensors_batch(messages)
+            eng.stage_tensors_batch(batch_msgs[(i + 1) % n_batches])
         if reducer is not None:
             reducer.finalize()
         else:
             eng.finalize(images=True)
 
     if not bifrost:
-        eng.stage_tensors_batch(messages)
+        eng.stage_tensors_batch(batch_msgs[0])
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
@@ -373,6 +432,7 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    cpu0 = time.process_time()
     for i in range(args.steps):
         if i in sampled:
             eng.timing_select([dom])
@@ -384,6 +444,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    host_cpu_s = time.process_time() - cpu0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -391,6 +452,11 @@ def main():
     timed = {dom: eng.kernel_stats(dom)}
     eng.timing_enable(False)
     step(first + args.steps, stage_next=False)  # bins the batch the last timed step staged
+    # the parity legs bin the batch after the last one binned (never a repeat)
+    b_chk = (first + args.steps + 1) % n_batches
+    pid, toa = batches[b_chk]
+    messages = batch_msgs[b_chk]
+    pushes = batch_pushes[b_chk] if bifrost else None
 
     # end-to-end (PCIe-inclusive) leg, reported beside `value`: the same
     # messages as host arrays, staged through lde_stage (copy into the pinned
@@ -516,6 +582,9 @@ def main():
                               'one accumulate) from 3 extra steps after the timed region',
         },
     }
+    # host CPU time (all threads of this process) per timed step: the finalize
+    # wait sleeps through most of the GPU work instead of spinning a core
+    result['host_cpu_ms_per_step'] = 1e3 * host_cpu_s / args.steps
     if e2e is not None:
         result['end_to_end'] = e2e
     if rank == 0 and world == 1 and monitor:
@@ -587,14 +656,7 @@ def main():
         eng.stage_tensors_batch(messages)
         eng.accumulate(r_chk)
         chk = eng.finalize(hists=True)
-        if args.view == 'geometric':
-            ps = ora.geometric_pixel_screen(inst.coords, inst.resolution,
-                                            flip_x=args.workload == 'loki')
-        else:  # the oracle's closed-form view index (no transform applied)
-            spec = {'mantle_front_layer': ([('module', 'segment', 'counter'), ('strip',)], {'wire': 0}),
-                    'wire_view': ([('wire',), ('module', 'segment', 'counter')], {}),
-                    'strip_view': ([('strip',)], {})}[args.view]
-            ps = ora.folded_view_index(synthetic.DREAM_BANK_SIZES['mantle_detector'], *spec)[0][None]
+        ps = oracle_pixel_screen(args, inst)
         result['cpu_baseline'] = cpu_baseline(inst, ps, view, pid.cpu().numpy(), toa.cpu().numpy(),
                                               r_chk, chk.current_hist, args.cpu_baseline_seconds)
         result['check'] = {
@@ -632,6 +694,44 @@ def main():
             'oracle': 'oracle.scipp_semantics.wavelength_mode (NumPy, 1 core)',
             'oracle_events_per_s': n_chk / t_c,
         }
+        result['cpu_baseline'] = {
+            'value': n_chk / t_c, 'unit': 'events/s', 'cores': 1, 'kind': 'port',
+            'sample': f'oracle.scipp_semantics wavelength mode (NumPy, 1 core: Ltotal lookup, '
+                      f'bilinear table interpolation, hist) on the {n_chk}-event check slice of '
+                      f'the bench batch, {t_c:.2f} s',
+        }
+    elif world > 1 and not (monitor or bifrost) and coord is None:
+        # parity leg of the sharded path: every rank bins batch b_chk of its own
+        # stream, the reducer merges the ranks' outputs onto the root (RCCL),
+        # and the root checks the merged current image and totals against
+        # oracle/binning_ref.c run over every rank's batch
+        r_chk = (args.warmup + args.steps + 3) % view.n_replicas
+        eng.stage_tensors_batch(messages)
+        eng.accumulate(r_chk)
+        merged = reducer.finalize()
+        if rank == 0:
+            from oracle import c_oracle
+
+            threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
+            c = c_oracle.CDetectorView(inst.detector_number, oracle_pixel_screen(args, inst),
+                                       view.n_screen, inst.edges.edges_ns(), threads=threads)
+            for r in range(world):  # regenerate rank r's batch b_chk on this device
+                p_r, t_r = gen(b_chk, r)
+                c.accumulate(p_r.cpu().numpy(), t_r.cpu().numpy(), r_chk)
+                del p_r, t_r
+            ref = c.hist.reshape(view.n_screen, eng.n_toa_bins)
+            cur, _, totals = merged
+            result['check'] = {
+                'events': n_step * world,
+                'ranks': world,
+                'current_total': totals[0],
+                'oracle_total': int(ref.sum()),
+                'bit_exact_vs_oracle': bool(np.array_equal(ref.sum(axis=1).astype(np.float64), cur)
+                                            and totals[0] == int(ref.sum())),
+                'compared': 'merged current image and current total (RCCL reduce of every '
+                            "rank's partial outputs) vs oracle/binning_ref.c over all ranks' batches",
+            }
+        dist.barrier()
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -76,6 +76,8 @@ EXPORTED_SYMBOLS = (
     'lde_reset_cumulative',
     'lde_export_window',
     'lde_finalize_partials',
+    'lde_accumulate_push',
+    'lde_push_u64',
     'lde_import_window',
     'lde_export_window_u64',
     'lde_import_window_u64',
@@ -165,6 +167,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_reset_cumulative': (ctypes.c_int, [H]),
         'lde_export_window': (ctypes.c_int, [H, P]),
         'lde_finalize_partials': (ctypes.c_int, [H, P]),
+        'lde_accumulate_push': (ctypes.c_int, [H, i32, P]),
+        'lde_push_u64': (ctypes.c_int, [H, P]),
         'lde_import_window': (ctypes.c_int, [H, P]),
         'lde_export_window_u64': (ctypes.c_int, [H, P]),
         'lde_import_window_u64': (ctypes.c_int, [H, P]),

@@ -229,6 +229,9 @@ struct lde_handle {
     // copy command and no cache flush in front of one follows the kernel
     unsigned char *hd_pack = nullptr;
     hipEvent_t fin_event = nullptr;  // system-scope release after the kernel
+    hipEvent_t block_event = nullptr;  // blocking-sync event: waits past the spin budget
+    double wait_pred_us = 0.0;         // predicted stream wait of a finalize (EMA)
+    long long waits_blocked = 0, waits_total = 0;
     size_t pack_bytes = 0;
     unsigned long long *d_snap = nullptr;
 
@@ -339,15 +342,58 @@ int check_knobs() {
 }
 
 // Wait for the handle's stream.  Finalize returns results the caller waits
-// for, so the wake-up latency is GPU idle time before the next batch:
-// it polls hipStreamQuery instead of blocking (measured -8 us per DREAM step;
-// LDE_SYNC_POLL=0 blocks).
+// for, so the wake-up latency is GPU idle time before the next batch, but a
+// thread spinning through the whole wait burns a host core per job (the
+// reference service runs job_threads=5 jobs, service_factory.py:65).  So:
+//   * sleep through the predicted part of the wait (EMA of this handle's past
+//     waits) minus a wake-up margin, then
+//   * spin on hipStreamQuery for the last stretch, at most kSpinCapUs, then
+//   * block on an interrupt-driven (hipEventBlockingSync) event.
+// A steady stream of batches spins ~kWakeUs per finalize; a wait with no
+// history, or longer than predicted, spins kSpinCapUs and then sleeps.
 hipError_t wait_stream(lde_handle *h) {
-    static const bool poll = env_ll("LDE_SYNC_POLL", 1) != 0;
-    if (!poll) return hipStreamSynchronize(h->stream);
-    hipError_t e;
-    while ((e = hipStreamQuery(h->stream)) == hipErrorNotReady) {
+    using clk = std::chrono::steady_clock;
+    constexpr double kWakeUs = 100.0;    // wake this long before the predicted end
+    constexpr double kSpinCapUs = 150.0; // spin budget before the blocking wait
+    hipError_t e = hipStreamQuery(h->stream);
+    if (e != hipErrorNotReady) return e;
+    ++h->waits_total;
+    const auto t0 = clk::now();
+    auto since = [](clk::time_point t) {
+        return std::chrono::duration<double, std::micro>(clk::now() - t).count();
+    };
+    const double pred = h->wait_pred_us;
+    if (pred > 2.0 * kWakeUs) {
+        std::this_thread::sleep_for(std::chrono::microseconds((long long)(pred - kWakeUs)));
+        e = hipStreamQuery(h->stream);
+        if (e != hipErrorNotReady) {
+            // done before the wake-up: the end is unknown, move the prediction earlier
+            h->wait_pred_us = 0.8 * pred + 0.2 * std::min(pred, 0.8 * since(t0));
+            return e;
+        }
     }
+    const auto ts = clk::now();
+    bool blocked = false;
+    while ((e = hipStreamQuery(h->stream)) == hipErrorNotReady) {
+        if (since(ts) > kSpinCapUs) {
+            blocked = true;
+            ++h->waits_blocked;
+            if (!h->block_event) {
+                e = hipEventCreateWithFlags(&h->block_event,
+                                            hipEventBlockingSync | hipEventDisableTiming);
+                if (e != hipSuccess) {
+                    h->block_event = nullptr;
+                    return hipStreamSynchronize(h->stream);
+                }
+            }
+            e = hipEventRecord(h->block_event, h->stream);
+            if (e == hipSuccess) e = hipEventSynchronize(h->block_event);
+            break;
+        }
+    }
+    const double took = since(t0);
+    // a blocked wait ends late by the wake-up latency: learn from it too
+    h->wait_pred_us = pred <= 0.0 ? took : 0.7 * pred + 0.3 * (blocked ? 0.9 * took : took);
     return e;
 }
 
@@ -1680,6 +1726,8 @@ void release(lde_handle *h) {
     h->hd_pack = nullptr;
     if (h->fin_event) (void)hipEventDestroy(h->fin_event);
     h->fin_event = nullptr;
+    if (h->block_event) (void)hipEventDestroy(h->block_event);
+    h->block_event = nullptr;
     dev_free(h->d_snap);
     for (auto &g : h->groups) {
         dev_free(g.d_items);
@@ -2219,7 +2267,42 @@ int lde_stage_device_batch(lde_handle *h, int64_t count, const void *const *d_pi
     return LDE_OK;
 }
 
-int lde_accumulate(lde_handle *h, int32_t replica) {
+namespace {
+int accumulate_impl(lde_handle *h, int32_t replica, unsigned long long *d_push);
+}
+
+int lde_accumulate(lde_handle *h, int32_t replica) { return accumulate_impl(h, replica, nullptr); }
+
+int lde_accumulate_push(lde_handle *h, int32_t replica, void *d_counts) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!d_counts) return fail(h, LDE_EINVAL, "push buffer is NULL");
+    if (h->out_dtype != LDE_F32)
+        return fail(h, LDE_EINVAL, "push export is for float32 views (integer views merge exactly "
+                                   "at finalize)");
+    return accumulate_impl(h, replica, (unsigned long long *)d_counts);
+}
+
+int lde_push_u64(lde_handle *h, const void *d_counts) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!d_counts) return fail(h, LDE_EINVAL, "push buffer is NULL");
+    if (h->out_dtype != LDE_F32) return fail(h, LDE_EINVAL, "lde_push_u64 is for float32 views");
+    DeviceGuard guard(h->device);
+    if (int rc = ensure_win64(h)) return rc;
+    {
+        Timed tm(h, LDE_K_FINALIZE);
+        HIPCALL(h, lde::launch_merge_f32_u64((const unsigned long long *)d_counts, h->d_win64,
+                                             h->d_winf, h->d_cumf, h->nbins,
+                                             h->window_has_data ? 0 : 1, h->cum_has_data ? 0 : 1,
+                                             h->stream));
+    }
+    h->win64_dirty = true;
+    h->window_has_data = true;
+    h->cum_has_data = true;
+    return LDE_OK;
+}
+
+namespace {
+int accumulate_impl(lde_handle *h, int32_t replica, unsigned long long *d_push) {
     if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
     if (replica < 0 || replica >= h->R)
         return fail(h, LDE_EINVAL, "replica %d out of range [0, %d)", replica, h->R);
@@ -2301,6 +2384,16 @@ int lde_accumulate(lde_handle *h, int32_t replica) {
             h->win_events += (unsigned long long)n;
         }
     }
+    if (d_push) {
+        // the push's exact counts leave for the merge (lde_push_u64 on the
+        // root); this handle's accumulators are untouched
+        HIPCALL(h, lde::launch_push_export(h->d_win32, d_push, h->nbins, h->stream));
+        h->win_events = 0;
+        h->events_binned += total;
+        h->staged_host = 0;
+        h->dev_segments.clear();
+        return LDE_OK;
+    }
     if (f32) {
         Timed tm(h, LDE_K_FINALIZE);
         HIPCALL(h, lde::launch_merge_f32(h->d_win32, h->d_win64, h->d_winf, h->d_cumf, h->nbins,
@@ -2316,6 +2409,7 @@ int lde_accumulate(lde_handle *h, int32_t replica) {
     h->dev_segments.clear();
     return LDE_OK;
 }
+}  // namespace
 
 int lde_finalize(lde_handle *h, lde_outputs *out) {
     if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");

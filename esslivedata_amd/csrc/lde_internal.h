@@ -297,6 +297,10 @@ hipError_t launch_fold_window(uint32_t *win32, unsigned long long *win64, long l
                               hipStream_t st);
 hipError_t launch_merge_f32(uint32_t *batch, unsigned long long *win64, float *winf, float *cumf,
                             long long n, int first_win, int first_cum, hipStream_t st);
+hipError_t launch_merge_f32_u64(const unsigned long long *src, unsigned long long *win64, float *winf,
+                                float *cumf, long long n, int first_win, int first_cum,
+                                hipStream_t st);
+hipError_t launch_push_export(uint32_t *batch, unsigned long long *out, long long n, hipStream_t st);
 hipError_t launch_sum3(const unsigned long long *a, const unsigned long long *b, const uint32_t *c,
                        unsigned long long *out, long long n, hipStream_t st);
 hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *win64,

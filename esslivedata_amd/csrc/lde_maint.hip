@@ -41,6 +41,34 @@ __global__ void k_merge_f32(uint32_t *__restrict__ batch, unsigned long long *__
     }
 }
 
+// one push of exact counts (the RCCL sum of every rank's push, u64) into a
+// float32 view's accumulators in the reference order: f32 += float32(count)
+// (accumulators.py:129-135, the cast of bifrost/specs.py:295), exact u64
+// window += count; the source is left as it is
+__global__ void k_merge_f32_u64(const unsigned long long *__restrict__ src,
+                                unsigned long long *__restrict__ win64, float *__restrict__ winf,
+                                float *__restrict__ cumf, long long n, int first_win, int first_cum) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const unsigned long long b = src[i];
+        const float fb = (float)b;  // one rounding, as float32(float64(count))
+        winf[i] = first_win ? fb : winf[i] + fb;
+        cumf[i] = first_cum ? fb : cumf[i] + fb;
+        win64[i] += b;
+    }
+}
+
+// a push's batch counts out as u64 (the push buffer of a sharded float32
+// view), the batch emptied for the next push
+__global__ void k_push_export(uint32_t *__restrict__ batch, unsigned long long *__restrict__ out,
+                              long long n) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        out[i] = batch[i];
+        batch[i] = 0;
+    }
+}
+
 // snapshot: out = a (+ b) (+ c) as u64, for reads that must not finalize
 __global__ void k_sum3(const unsigned long long *__restrict__ a, const unsigned long long *__restrict__ b,
                        const uint32_t *__restrict__ c, unsigned long long *__restrict__ out,
@@ -314,6 +342,19 @@ hipError_t launch_merge_f32(uint32_t *batch, unsigned long long *win64, float *w
                             long long n, int first_win, int first_cum, hipStream_t st) {
     hipLaunchKernelGGL(k_merge_f32, dim3(grid_for(n)), dim3(256), 0, st, batch, win64, winf, cumf,
                        n, first_win, first_cum);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_f32_u64(const unsigned long long *src, unsigned long long *win64, float *winf,
+                                float *cumf, long long n, int first_win, int first_cum,
+                                hipStream_t st) {
+    hipLaunchKernelGGL(k_merge_f32_u64, dim3(grid_for(n)), dim3(256), 0, st, src, win64, winf, cumf,
+                       n, first_win, first_cum);
+    return hipGetLastError();
+}
+
+hipError_t launch_push_export(uint32_t *batch, unsigned long long *out, long long n, hipStream_t st) {
+    hipLaunchKernelGGL(k_push_export, dim3(grid_for(n)), dim3(256), 0, st, batch, out, n);
     return hipGetLastError();
 }
 

@@ -14,6 +14,16 @@ binned every event (integer sums are order-independent):
   window state, also after a rank's u32 window folded into u64), which then
   finalizes as a single GPU would; needed when the full (S, T) histogram is
   published.
+* ``PushReducer`` (float32 views, BIFROST): the reference adds every push to
+  float32 accumulators (SRC/preprocessors/accumulators.py:129-135, the cast of
+  config/instruments/bifrost/specs.py:295), which rounds once per push beyond
+  2^24 counts per bin; merging at finalize would round once in total.  So the
+  ranks' exact counts of each push are summed onto the root before that
+  push's f32 add: one reduce of S*T uint64 per push.  The two reducers above
+  refuse float32 engines.
+
+``dst``/``root`` is always a global rank (``torch.distributed`` collectives
+take global ranks for ``dst`` in any group).
 
 Pixel-range (bank) sharding needs no collective: see :func:`assign_banks`.
 
@@ -107,7 +117,7 @@ class _Reducer:
         import torch.distributed as dist
 
         self._order_after_engine()
-        root = dist.get_rank(self.group) == self.dst
+        root = dist.get_rank() == self.dst  # dst is a global rank
         if self._host:
             hb = self.buf.cpu()
             dist.reduce(hb, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group)
@@ -150,6 +160,7 @@ class OutputReducer(_Reducer):
     def __init__(self, engine, device, *, dst: int = 0, group=None) -> None:
         import torch
 
+        _refuse_f32(engine, 'OutputReducer')
         self.S = engine.n_screen
         # [S] current image | [S] cumulative image | [4] totals | [1] windows
         # that held data (summed: the merged window is empty only if all were)
@@ -159,9 +170,7 @@ class OutputReducer(_Reducer):
 
     def finalize(self, had_data: bool = True):
         """Collective.  On the root: (current image, cumulative image, totals)
-        as numpy arrays of the engine's output dtype (float64, or float32 for
-        BIFROST-like views: the exact merged counts rounded once) and a list
-        of 4 ints; elsewhere None.  ``had_data``: this rank accumulated since
+        as float64 numpy arrays and a list of 4 ints; elsewhere None.  ``had_data``: this rank accumulated since
         its last finalize (merged into ``self.had_data`` on the root)."""
         self._before_write()
         self.engine.finalize_partials(self.buf.data_ptr())
@@ -183,19 +192,76 @@ class WindowReducer(_Reducer):
     def __init__(self, engine, device, *, dst: int = 0, group=None) -> None:
         import torch
 
-        n = engine.n_screen * engine.n_toa_bins
-        super().__init__(engine, torch.zeros(n, dtype=torch.int64, device=device), dst=dst,
-                         group=group)
+        _refuse_f32(engine, 'WindowReducer')
+        self.n = engine.n_screen * engine.n_toa_bins
+        # [S*T] window | [1] ranks whose window held data
+        super().__init__(engine, torch.zeros(self.n + 1, dtype=torch.int64, device=device),
+                         dst=dst, group=group)
+        self.had_data = True  # root: any rank's window held data at the last reduce
 
-    def reduce(self) -> bool:
+    def reduce(self, had_data: bool = True) -> bool:
         """Collective; returns True on the root, which now holds the merged
-        window; the other ranks' windows are emptied (their counts moved)."""
+        window; the other ranks' windows are emptied (their counts moved).
+        ``had_data``: this rank accumulated since its last finalize.  When no
+        rank had data the root's window is left empty (``self.had_data`` is
+        False), so its finalize raises 'No data has been added' as a single
+        workflow's would."""
         self._before_write()
         self.engine.export_window_u64(self.buf.data_ptr())
+        self._order_after_engine()
+        self.buf[self.n].fill_(1 if had_data else 0)
         root = self._reduce()
         if not root:
             self.buf.zero_()  # this rank's counts now live on the root
             self._mark()
+        else:
+            self.had_data = bool(int(self.buf[self.n].item()))
+            if not self.had_data:
+                return True  # nothing to import: the window stays empty
         self._before_write()  # the reduced buffer before the engine reads it
         self.engine.import_window_u64(self.buf.data_ptr())
         return root
+
+
+class PushReducer(_Reducer):
+    """Per-push exact merge of a float32 view (see the module doc): every
+    rank bins its share of a push with ``accumulate_push`` (exact counts into
+    the reduce buffer, its own accumulators untouched), the counts are summed
+    onto the root, and the root adds the sum as ONE push (``push_counts``:
+    f32 += float32(count)).  Only the root's accumulators hold data; it
+    finalizes as a single GPU that binned every push would."""
+
+    def __init__(self, engine, device, *, dst: int = 0, group=None) -> None:
+        import torch
+
+        if engine.dtype != 'float32':
+            raise ValueError('PushReducer is for float32 views; integer views merge exactly at '
+                             'finalize (OutputReducer / WindowReducer)')
+        self.n = engine.n_screen * engine.n_toa_bins
+        super().__init__(engine, torch.zeros(self.n, dtype=torch.int64, device=device), dst=dst,
+                         group=group)
+
+    def push(self, replica: int, has_events: bool = True) -> bool:
+        """Collective.  Bins this rank's staged events of the push (zeros when
+        ``has_events`` is False and nothing is staged) and merges the push
+        onto the root; returns True on the root."""
+        self._before_write()
+        if has_events:
+            self.engine.accumulate_push(int(replica), self.buf.data_ptr())
+        else:
+            self._order_after_engine()
+            self.buf.zero_()
+        root = self._reduce()
+        if root:
+            self._before_write()
+            # the next push's export runs behind this add on the engine stream;
+            # a push without events zeroes the buffer after waiting for it
+            self.engine.push_counts(self.buf.data_ptr())
+        return root
+
+
+def _refuse_f32(engine, what: str) -> None:
+    if engine.dtype == 'float32':
+        raise ValueError(f'{what} merges integer counts at finalize, which is not the '
+                         "reference's per-push float32 sum beyond 2^24 counts per bin: "
+                         'float32 views merge per push (PushReducer)')

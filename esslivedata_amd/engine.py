@@ -447,6 +447,20 @@ class BinningEngine:
         cumulative image, [4] totals (this rank's exact share, for a reduce)."""
         self._call(self._lib.lde_finalize_partials, dst_ptr)
 
+    def accumulate_push(self, replica: int, dst_ptr: int) -> None:
+        """Bin the staged events and write this push's exact counts (uint64
+        [S*T]) to device memory instead of adding them (float32 views: the
+        sharded per-push merge, ``lde_accumulate_push``)."""
+        rc = self._lib.lde_accumulate_push(self._h, int(replica), dst_ptr)
+        if rc:
+            check(rc, self._h)
+        self._keepalive.clear()
+
+    def push_counts(self, src_ptr: int) -> None:
+        """Add one push of exact uint64 [S*T] counts to the float32 window and
+        cumulative in the reference order (``lde_push_u64``)."""
+        self._call(self._lib.lde_push_u64, src_ptr)
+
     def export_window(self, dst_ptr: int) -> None:
         self._call(self._lib.lde_export_window, dst_ptr)
 

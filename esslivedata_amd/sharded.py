@@ -24,16 +24,23 @@ across ranks is kept in agreement by the wrapper:
   so the root finalizes every output a single GPU would, including ROI
   spectra and spectrum views, which read the full histogram.  The root
   returns the reference's output dict; other ranks return ``None``.
+* **float32 views** (BIFROST) merge per push (``merge='push'``, the default
+  for them): the reference rounds its float32 accumulators once per push
+  (SRC/preprocessors/accumulators.py:129-135, config/instruments/bifrost/
+  specs.py:295), so the ranks' exact counts of every push are reduced onto
+  the root (``PushReducer``) before the root adds them as one push; only the
+  root's accumulators hold data and its finalize is a single workflow's.
 
 Integer sums are order-independent, so the root's outputs are bit-identical
-to one workflow that binned every rank's events.
+to one workflow that binned every rank's events.  ``root`` is a global rank,
+also when ``group`` is a subgroup.
 """
 
 from __future__ import annotations
 
 from typing import Any, Iterable, Mapping
 
-from .distributed import OutputReducer, WindowReducer
+from .distributed import OutputReducer, PushReducer, WindowReducer
 from .preprocessors import Timestamp
 from .workflows import GpuDetectorViewWorkflow
 
@@ -41,23 +48,29 @@ from .workflows import GpuDetectorViewWorkflow
 class ShardedDetectorViewWorkflow:
     """``Workflow`` over the ranks of ``group`` (see the module doc)."""
 
-    def __init__(self, workflow: GpuDetectorViewWorkflow, device, *, merge: str = 'outputs',
+    def __init__(self, workflow: GpuDetectorViewWorkflow, device, *, merge: str | None = None,
                  root: int = 0, group=None) -> None:
         import torch.distributed as dist
 
-        if merge not in ('outputs', 'window'):
-            raise ValueError(f"merge must be 'outputs' or 'window', got {merge!r}")
+        eng = workflow.engine
+        f32 = eng.dtype == 'float32'
+        if merge is None:
+            merge = 'push' if f32 else 'outputs'
+        if merge not in ('outputs', 'window', 'push'):
+            raise ValueError(f"merge must be 'outputs', 'window' or 'push', got {merge!r}")
+        if f32 != (merge == 'push'):
+            raise ValueError("float32 views merge per push (merge='push'), integer views at "
+                             "finalize ('outputs' or 'window')")
         if merge == 'outputs' and workflow.has_grouped_outputs:
             raise ValueError("ROI spectra and spectrum views read the full histogram: use merge='window'")
         self._wf = workflow
         self._group = group
-        self._root = root
-        self._rank = dist.get_rank(group)
+        self._root = root  # a global rank
+        self._rank = dist.get_rank()
         self._is_root = self._rank == root
         self._merge = merge
-        eng = workflow.engine
-        self._reducer = (OutputReducer(eng, device, dst=root, group=group) if merge == 'outputs'
-                         else WindowReducer(eng, device, dst=root, group=group))
+        cls = {'outputs': OutputReducer, 'window': WindowReducer, 'push': PushReducer}[merge]
+        self._reducer = cls(eng, device, dst=root, group=group)
         self._had_data = False  # this rank accumulated events since its last finalize
 
     @property
@@ -97,13 +110,30 @@ class ShardedDetectorViewWorkflow:
         if source in data:
             local[source] = data[source]
             self._had_data = True
-        self._wf._accumulate(local, start_time, end_time, batch_has_events=any_events)
+        if self._merge != 'push':
+            self._wf._accumulate(local, start_time, end_time, batch_has_events=any_events)
+            return
+        pushed = []
+
+        def push(replica: int) -> None:
+            self._reducer.push(replica)
+            pushed.append(replica)
+
+        self._wf._accumulate(local, start_time, end_time, batch_has_events=any_events, bin_fn=push)
+        if any_events and not pushed:  # this rank has no share of the push
+            self._reducer.push(0, has_events=False)
 
     def finalize(self) -> dict[str, Any] | None:
         """Collective.  The merged outputs on the root, ``None`` elsewhere."""
         had, self._had_data = self._had_data, False
+        if self._merge == 'push':
+            # every push was merged onto the root as it came
+            if self._is_root:
+                return self._wf.finalize()
+            self._wf._end_window()
+            return None
         if self._merge == 'window':
-            root = self._reducer.reduce()
+            root = self._reducer.reduce(had_data=had)
             if not root:
                 # the window's counts moved to the root; this rank's cumulative
                 # is never published, so it is dropped with the window

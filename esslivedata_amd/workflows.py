@@ -293,9 +293,11 @@ class GpuDetectorViewWorkflow:
         self._accumulate(data, start_time, end_time)
 
     def _accumulate(self, data: Mapping[str, Any], start_time: Timestamp, end_time: Timestamp,
-                    batch_has_events: bool = False) -> None:
+                    batch_has_events: bool = False, bin_fn=None) -> None:
         """``batch_has_events``: another rank binned events of this batch (the
-        sharded workflow), so the replica cycle advances here too."""
+        sharded workflow), so the replica cycle advances here too.
+        ``bin_fn(replica)`` bins the staged events instead of
+        ``engine.accumulate`` (the sharded per-push merge)."""
         if self._start is None:
             self._start = start_time
         self._end = end_time
@@ -315,7 +317,7 @@ class GpuDetectorViewWorkflow:
         _stage(self._engine, toas, pids)
         replica = self._counter % self._view.n_replicas
         self._counter += 1
-        self._engine.accumulate(replica)
+        (bin_fn or self._engine.accumulate)(replica)
 
     def _move(self, transform) -> None:
         """A detector-transform value: rebuild the projection and LUT from the

@@ -257,11 +257,10 @@ int lde_export_window(lde_handle *h, void *d_dst);
  * handle's stream.  Summed over ranks (RCCL reduce) they equal the outputs of
  * one handle that binned every rank's events.  An empty window is allowed
  * (zeros for the current outputs).  float32 views (BIFROST) export their exact
- * integer counts too (kept beside the f32 accumulators): rounded once to f32
- * by the caller, the merged images equal one handle's f32 images whenever
- * every per-push f32 bin value is an exact integer (< 2^24 counts per bin);
- * beyond that they are the exact counts rounded once, where the reference's
- * per-push f32 sums drift by at most one f32 rounding per push. */
+ * integer counts too (kept beside the f32 accumulators); their merge is NOT
+ * the reference's float32 result beyond 2^24 counts per bin (the reference
+ * rounds once per push), so sharded float32 views merge per push instead
+ * (lde_accumulate_push / lde_push_u64 below). */
 int lde_finalize_partials(lde_handle *h, void *d_out);
 int lde_import_window(lde_handle *h, const void *d_src);
 /* Exact window merge in any window state (also after the uint32 window has
@@ -271,6 +270,21 @@ int lde_import_window(lde_handle *h, const void *d_src);
  * LDE_EINVAL for f32 views. */
 int lde_export_window_u64(lde_handle *h, void *d_dst);
 int lde_import_window_u64(lde_handle *h, const void *d_src);
+
+/* Exact sharded float32 views (BIFROST), one collective per push.  The
+ * reference adds every push to its float32 window and cumulative
+ * (accumulators.py:129-135; the cast is bifrost/specs.py:295), so a sharded
+ * view must merge the ranks' counts of a push BEFORE that push's f32 add:
+ *   lde_accumulate_push: bins the staged events like lde_accumulate but
+ *     writes the push's exact counts, uint64 [S*T], to caller device memory
+ *     instead of adding them (this handle's accumulators are untouched);
+ *   lde_push_u64: adds one push of exact counts (e.g. the RCCL sum of every
+ *     rank's lde_accumulate_push) in the reference order: window and
+ *     cumulative f32 += float32(count), the exact integer window += count.
+ * Float32 views only (LDE_EINVAL otherwise: integer views merge exactly at
+ * finalize, lde_finalize_partials / lde_export_window_u64). */
+int lde_accumulate_push(lde_handle *h, int32_t replica, void *d_counts);
+int lde_push_u64(lde_handle *h, const void *d_counts);
 
 /* Screen groupings: per-group TOA spectra summed on the device, replacing the
  * host-side reductions of the finalize outputs

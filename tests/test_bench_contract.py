@@ -105,3 +105,30 @@ def test_bench_prints_one_contract_line():
     lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
     assert len(lines) == 1, p.stdout[-2000:]
     _check_line(json.loads(lines[0]))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize('workload', ['dream', 'loki'])
+def test_bench_gpus2_launches_ranks_and_checks_merge(workload):
+    """``bench.py --gpus 2`` without a torchrun environment starts two rank
+    processes itself; here they share cuda:0 over gloo.
+    Rank 0's one line reports n_gpus == 2 and the merged (reduced) current
+    image and total bit-exact against the oracle over both ranks' batches."""
+    env = dict(os.environ)
+    env['LDE_BENCH_BACKEND'] = 'gloo'
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    cmd = [sys.executable, str(ROOT / 'bench.py'), '--gpus', '2', '--workload', workload,
+           '--steps', '3', '--warmup', '1', '--pulses', '3', '--events-per-pulse', '2000000',
+           '--no-cpu-baseline', '--e2e-steps', '0']
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=380)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    _check_line(d, n_gpus=2)
+    assert 'x2' in d['config']['parallelism']
+    assert d['check']['ranks'] == 2
+    assert d['check']['bit_exact_vs_oracle'] is True, d['check']
+    assert d['check']['current_total'] == d['check']['oracle_total'] > 0

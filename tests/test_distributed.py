@@ -205,3 +205,90 @@ def test_assign_banks_loki_dream():
     assert assign_banks(loki, 3) == assign_banks(dict(reversed(list(loki.items()))), 3)
     with pytest.raises(ValueError):
         assign_banks(loki, 0)
+
+
+def _worker_subgroup(rank, world, port, q):
+    """Ranks 1 and 2 form a subgroup whose root is global rank 2:
+    the reducers treat ``dst`` as a global rank; rank 0 stays out."""
+    import torch
+    import torch.distributed as dist
+
+    from esslivedata_amd.distributed import OutputReducer, WindowReducer
+
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        grp = dist.new_group([1, 2])
+        if rank == 0:
+            q.put((rank, True))
+            return
+        edges = np.linspace(0, 100, 11)
+        rng = np.random.default_rng(3)
+        n = 40_000
+        pid = rng.integers(0, 70, n).astype(np.int32)
+        toa = rng.integers(-10, 110, n).astype(np.int32)
+        half = n // 2
+        eng = _HostEngine(64, edges)
+        sl = slice(0, half) if rank == 1 else slice(half, n)
+        eng.bin(pid[sl], toa[sl])
+        full = _HostEngine(64, edges)
+        full.bin(pid, toa)
+        ok = True
+        # outputs: the root (global rank 2) gets the merged outputs
+        red = OutputReducer(eng, torch.device('cpu'), dst=2, group=grp)
+        res = red.finalize()
+        buf = np.zeros(2 * 64 + 4, dtype=np.int64)
+        full.finalize_partials(buf.ctypes.data)
+        if rank == 2:
+            cur, cum, tot = res
+            ok &= np.array_equal(cur, buf[:64].astype(np.float64))
+            ok &= tot == [int(x) for x in buf[128:]] and tot[0] > 0
+        else:
+            ok &= res is None
+        # window: the next window merged onto global rank 2
+        eng.bin(pid[sl], toa[sl])
+        wr = WindowReducer(eng, torch.device('cpu'), dst=2, group=grp)
+        root = wr.reduce()
+        ok &= root == (rank == 2)
+        if rank == 2:
+            w2 = _HostEngine(64, edges)
+            w2.bin(pid, toa)
+            ok &= np.array_equal(eng.window, w2.window) and wr.had_data
+            eng.window[:] = 0  # the root's finalize empties its window
+        # a window no rank filled: the root's window stays empty, had_data False
+        root = wr.reduce(had_data=False)
+        if rank == 2:
+            ok &= wr.had_data is False and not eng.window.any()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reducers_subgroup_root_is_global_rank():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_subgroup, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert results == {0: True, 1: True, 2: True}
+
+
+def test_reducers_refuse_float32_engines():
+    """Integer merges at finalize are not the reference's per-push float32
+    sums beyond 2^24 counts per bin: float32 engines need PushReducer."""
+    from esslivedata_amd.distributed import OutputReducer, PushReducer, WindowReducer
+
+    eng = _HostEngine(4, np.linspace(0, 1, 3))
+    eng.dtype = np.dtype('float32')
+    for cls in (OutputReducer, WindowReducer):
+        with pytest.raises(ValueError, match='per push'):
+            cls(eng, 'cpu')
+    eng.dtype = np.dtype('float64')
+    with pytest.raises(ValueError, match='float32 views'):
+        PushReducer(eng, 'cpu')

@@ -101,13 +101,19 @@ def _outputs_worker(rank, world, port, q):
 
 def _bifrost_worker(rank, world, port, q):
     """float32 view (BIFROST unified detector, 45 bank streams): every rank
-    bins its share of the bank messages; the merged f32 images equal one
-    engine that binned every message."""
+    bins its share of each push's bank messages; ``PushReducer`` sums the
+    push's exact counts onto the root before the root's float32 add, so the
+    root's images equal one engine that binned every message, push by push.
+    Then one bin is driven past 2^24 counts: a first push of 2^24 events
+    (split over the ranks), then pushes of one event each.  The reference's
+    per-push float32 sum stays at 2^24 (16777216 + 1 rounds to even); the
+    root's cumulative must equal that, not the exact count rounded once
+    (accumulators.py:129-135, bifrost/specs.py:295)."""
     import torch
     import torch.distributed as dist
 
     from esslivedata_amd import projection, synthetic
-    from esslivedata_amd.distributed import OutputReducer
+    from esslivedata_amd.distributed import PushReducer
     from esslivedata_amd.engine import BinningEngine
 
     _init(rank, world, port)
@@ -123,32 +129,55 @@ def _bifrost_worker(rank, world, port, q):
 
         eng = make()
         full = make() if rank == 0 else None
-        red = OutputReducer(eng, torch.device('cuda', 0))
+        red = PushReducer(eng, torch.device('cuda', 0))
         ok = True
         for window in range(3):
-            for bank in range(45):  # bifrost/streams.py:22-43: one message per bank
-                pid, toa = synthetic.fake_detector_events(1000, 1 + 300 * bank, 300 * (bank + 1),
-                                                          seed=1000 * window + bank)
-                if bank % world == rank:
-                    eng.stage(pid, toa)
+            for push in range(2):
+                for bank in range(45):  # bifrost/streams.py:22-43: one message per bank
+                    pid, toa = synthetic.fake_detector_events(
+                        1000, 1 + 300 * bank, 300 * (bank + 1), seed=1000 * window + 100 * push + bank)
+                    if bank % world == rank:
+                        eng.stage(pid, toa)
+                    if rank == 0:
+                        full.stage(pid, toa)
+                red.push(0)
                 if rank == 0:
-                    full.stage(pid, toa)
-            eng.accumulate(0)
-            if rank == 0:
-                full.accumulate(0)
-            res = red.finalize()
+                    full.accumulate(0)
             if rank == 0:
                 ref = full.finalize(images=True)
-                cur, cum, tot = res
-                ok &= cur.dtype == np.float32 and bool(np.array_equal(cur, ref.current_image))
-                ok &= bool(np.array_equal(cum, ref.cumulative_image))
-                ok &= tot == [ref.current_total, ref.current_in_range, ref.cumulative_total,
-                              ref.cumulative_in_range] and tot[0] > 0
-            else:
-                ok &= res is None
+                res = eng.finalize(images=True)
+                ok &= res.current_image.dtype == np.float32
+                ok &= bool(np.array_equal(res.current_image, ref.current_image))
+                ok &= bool(np.array_equal(res.cumulative_image, ref.cumulative_image))
+                ok &= [res.current_total, res.cumulative_total] == [ref.current_total,
+                                                                    ref.cumulative_total]
+                ok &= ref.current_total > 0
+        # one bin past 2^24: pid 1, a TOA inside bin 50
+        if rank == 0:
+            eng.clear()
+        t50 = int((edges[50] + edges[51]) / 2)
+        dev = torch.device('cuda', 0)
+        big = 1 << 24
+        share = big // world + (1 if rank < big % world else 0)
+        pushes = [share] + [1 if rank == world - 1 else 0 for _ in range(4)]
+        exp = np.float32(0)
+        for k, n in enumerate(pushes):
+            if n:
+                eng.stage_tensors(torch.full((n,), 1, dtype=torch.int32, device=dev),
+                                  torch.full((n,), t50, dtype=torch.int32, device=dev))
+            red.push(0, has_events=n > 0)
+            exp = np.float32(exp + np.float32(big if k == 0 else 1))
+        if rank == 0:
+            res = eng.finalize(hists=True)
+            s0 = int(view.lut[0][0])  # pixel 1's screen
+            got = res.cumulative_hist[s0, 50]
+            ok &= got == exp == np.float32(big)  # per-push rounding, not 2^24 + 4
+            ok &= res.cumulative_total == big + 4  # exact integer totals
         q.put((rank, bool(ok)))
     except Exception as e:  # pragma: no cover
-        q.put((rank, repr(e)))
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()))
     finally:
         dist.destroy_process_group()
 
@@ -285,7 +314,7 @@ def test_window_reducer_after_u64_fold_two_ranks():
     _run(_window_worker)
 
 
-def test_output_reducer_float32_view_two_ranks():
+def test_push_reducer_float32_view_two_ranks_past_2_24():
     _run(_bifrost_worker)
 
 

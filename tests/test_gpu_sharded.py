@@ -161,6 +161,63 @@ def _sharded_worker(rank, world, port, q, merge):
         dist.destroy_process_group()
 
 
+def _subgroup_worker(rank, world, port, q):
+    """Three ranks; the view is sharded over the subgroup {1, 2} whose root is
+    global rank 2: the root's context (a detector move) reaches
+    rank 1, and rank 2 publishes outputs equal to one workflow's."""
+    import torch
+    import torch.distributed as dist
+
+    from esslivedata_amd import synthetic
+    from esslivedata_amd.distributed import shard_bounds
+    from esslivedata_amd.sharded import ShardedDetectorViewWorkflow
+
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        grp = dist.new_group([1, 2])
+        if rank == 0:
+            q.put((rank, True))
+            return
+        inst, fac = _loki_factory(False)
+        local = fac.make_workflow('loki')
+        local._roi_support = False
+        sw = ShardedDetectorViewWorkflow(local, torch.device('cuda', 0), root=2, group=grp)
+        full = None
+        if rank == 2:
+            full = fac.make_workflow('loki')
+            full._roi_support = False
+        t0, t1 = _transforms()
+        ok = True
+        for b, tr in enumerate([t0, t1, t1]):
+            n = 300_001 + b
+            pid, toa = synthetic.uniform_events(n, 1, 802816, seed=170 + b)
+            lo, hi = shard_bounds(n, rank - 1, 2)
+            data = {'loki': (pid[lo:hi], toa[lo:hi])}
+            if rank == 2:
+                data['detector_transform'] = tr
+            sw.accumulate(data, start_time=_t(b), end_time=_t(b + 1))
+            out = sw.finalize()
+            if rank == 2:
+                full.accumulate({'loki': (pid, toa), 'detector_transform': tr},
+                                start_time=_t(b), end_time=_t(b + 1))
+                ref = full.finalize()
+                if out is None or not _same(out, ref) or not float(ref['counts_total'].values) > 0:
+                    ok = f'batch {b}: root outputs differ'
+                    break
+            elif out is not None:
+                ok = 'non-root returned outputs'
+                break
+        q.put((rank, ok))
+    except Exception as e:  # pragma: no cover - reported through the queue
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
 def _outputs_merge(rank, world, port, q):
     _sharded_worker(rank, world, port, q, 'outputs')
 
@@ -202,6 +259,10 @@ def test_sharded_workflow_outputs_merge_with_move_and_clear():
 
 def test_sharded_workflow_window_merge_with_roi_spectra():
     _run(_window_merge)
+
+
+def test_sharded_workflow_subgroup_root_is_global_rank():
+    _run(_subgroup_worker, world=3)
 
 
 def test_outputs_merge_refuses_grouped_outputs():

@@ -179,3 +179,48 @@ def test_wide_pixel_ids_are_dropped_not_wrapped():
     st.add(Timestamp.from_ns(0), DetectorEvents(pixel_id=pid, time_of_arrival=np.arange(4),
                                                 unit='ns'))
     assert st.get().pixel_id[0].dtype == np.int64
+
+
+def test_bench_launcher_refuses_more_ranks_than_gpus(monkeypatch):
+    """``bench.py --gpus N`` over RCCL refuses N beyond the visible GPUs
+    (without initialising HIP in the launching process)."""
+    import subprocess
+
+    import bench
+
+    class A:
+        gpus = 4
+
+    monkeypatch.setenv('LDE_BENCH_BACKEND', 'nccl')
+    monkeypatch.setattr(subprocess, 'run', lambda *a, **k: pytest.fail('must not launch'))
+    assert bench.launch_ranks(A()) == 2
+
+
+def test_bench_launcher_command(monkeypatch):
+    """The launcher starts torch.distributed.run with N ranks on 127.0.0.1 and
+    passes its own arguments through."""
+    import subprocess
+    import sys
+
+    import bench
+
+    seen = {}
+
+    class R:
+        returncode = 0
+
+    def fake_run(cmd, env=None, **k):
+        seen['cmd'], seen['env'] = cmd, env
+        return R()
+
+    class A:
+        gpus = 3
+
+    monkeypatch.setenv('LDE_BENCH_BACKEND', 'gloo')
+    monkeypatch.setattr(subprocess, 'run', fake_run)
+    monkeypatch.setattr(sys, 'argv', ['bench.py', '--gpus', '3', '--steps', '2'])
+    assert bench.launch_ranks(A()) == 0
+    cmd = seen['cmd']
+    assert cmd[1:3] == ['-m', 'torch.distributed.run']
+    assert '--nproc-per-node=3' in cmd and '--master-addr=127.0.0.1' in cmd
+    assert cmd[-4:] == ['--gpus', '3', '--steps', '2']
