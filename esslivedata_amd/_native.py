@@ -7,6 +7,7 @@ import of :func:`lib` raises -- there is no CPU fallback.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -142,7 +143,10 @@ class LdeOutputs(ctypes.Structure):
 
 
 _lock = threading.Lock()
-_lib: ctypes.CDLL | None = None
+_libs: dict[bool, ctypes.CDLL] = {}
+# engines created while this is set load the diagnostics build (tests only:
+# the parity matrix over the engine's tuning variants, diagnostics_library())
+_use_diag = False
 
 
 def _declare(lib: ctypes.CDLL) -> None:
@@ -206,39 +210,58 @@ def _declare(lib: ctypes.CDLL) -> None:
         fn.argtypes = args
 
 
-def lib() -> ctypes.CDLL:
-    """Load the engine library (once).  Raises if it is missing."""
-    global _lib
+def lib(diagnostics: bool | None = None) -> ctypes.CDLL:
+    """Load the engine library (once).  Raises if it is missing.
+    ``diagnostics`` (default: inside :func:`diagnostics_library`) loads the
+    diagnostics build instead, whose tuning knobs (``LDE_*`` variables) select
+    the engine's internal kernel variants; the product library fixes them."""
+    diag = _use_diag if diagnostics is None else bool(diagnostics)
     with _lock:
-        if _lib is not None:
-            return _lib
-        if not LIB_PATH.exists():
+        if diag in _libs:
+            return _libs[diag]
+        path = DIAG_LIB_PATH if diag else LIB_PATH
+        if not path.exists():
             raise RuntimeError(
-                f'HIP engine library {LIB_PATH} is missing; build it with '
-                '`python -m esslivedata_amd.build` (no CPU fallback exists)'
+                f'HIP engine library {path} is missing; build it with '
+                f'`python -m esslivedata_amd.build{" --diagnostics" if diag else ""}` '
+                '(no CPU fallback exists)'
             )
         try:  # share torch's HIP runtime (same SONAME) when torch is present
             import torch  # noqa: F401
         except Exception:  # pragma: no cover - torch is part of the image
             pass
-        cdll = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        # both builds may be loaded side by side (-Bsymbolic: each binds its
+        # own symbols); only the product library goes into the global scope
+        cdll = ctypes.CDLL(str(path), mode=ctypes.RTLD_LOCAL if diag else ctypes.RTLD_GLOBAL)
         _declare(cdll)
         if cdll.lde_abi_version() != ABI_VERSION:
             raise RuntimeError('libesslivedata_amd ABI version mismatch')
-        _lib = cdll
+        _libs[diag] = cdll
         return cdll
 
 
-def last_error(handle) -> str:
-    msg = lib().lde_last_error(handle)
+@contextlib.contextmanager
+def diagnostics_library():
+    """Engines created inside use the diagnostics build (test infrastructure)."""
+    global _use_diag
+    prev, _use_diag = _use_diag, True
+    try:
+        yield lib(True)
+    finally:
+        _use_diag = prev
+
+
+def last_error(handle, library: ctypes.CDLL | None = None) -> str:
+    msg = (library or lib()).lde_last_error(handle)
     return msg.decode() if msg else ''
 
 
-def check(rc: int, handle=None) -> None:
-    """Map engine error codes onto the reference's exception conventions."""
+def check(rc: int, handle=None, library: ctypes.CDLL | None = None) -> None:
+    """Map engine error codes onto the reference's exception conventions
+    (``library``: the build the handle belongs to)."""
     if rc == LDE_OK:
         return
-    msg = last_error(handle)
+    msg = last_error(handle, library)
     if rc in (LDE_EINVAL, LDE_ENODATA):
         raise ValueError(msg)
     if rc == LDE_ENOTSUP:

@@ -82,7 +82,7 @@ def build(force: bool = False, verbose: bool = False, diagnostics: bool = False)
         for f in futs:
             f.result()
     tmp = lib.with_suffix('.so.tmp')
-    _run([_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-Wl,--no-undefined',
+    _run([_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-Wl,--no-undefined', '-Wl,-Bsymbolic',
           *[str(o) for o in objs], '-o',
           str(tmp)], verbose)
     os.replace(tmp, lib)

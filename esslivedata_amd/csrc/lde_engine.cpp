@@ -305,7 +305,25 @@ struct DeviceGuard {
     }
 };
 
+// Runtime settings.  The product library reads only the documented
+// deployment settings below; every tuning knob of the engine (strategy
+// internals, kernel variants, probes) is fixed at its measured default and
+// selectable only in the diagnostics build (-DLDE_DIAGNOSTICS,
+// libesslivedata_amd_diag.so), which the parity tests load to run every
+// exact variant (tests/test_gpu_parity.py VARIANTS).
+//   LDE_VERBOSE        setup and strategy lines on stderr
+//   LDE_STAGE_THREADS  host threads copying ev44 payloads into the pinned ring
+bool runtime_setting(const char *name) {
+#ifdef LDE_DIAGNOSTICS
+    (void)name;
+    return true;
+#else
+    return std::strcmp(name, "LDE_VERBOSE") == 0 || std::strcmp(name, "LDE_STAGE_THREADS") == 0;
+#endif
+}
+
 long long env_ll(const char *name, long long dflt) {
+    if (!runtime_setting(name)) return dflt;
     const char *v = std::getenv(name);
     if (!v || !*v) return dflt;
     return std::atoll(v);
@@ -319,7 +337,7 @@ int check_knobs() {
 #ifndef LDE_DIAGNOSTICS
     static const char *const diag[] = {"LDE_ABLATE", "LDE_SIEVE_ABLATE", "LDE_COLD_SORT_ABLATE"};
     for (const char *n : diag)
-        if (env_ll(n, 0) != 0)
+        if (const char *v = std::getenv(n); v && std::atoll(v) != 0)
             return fail(nullptr, LDE_EINVAL,
                         "%s selects a diagnostic ablation (wrong results by design), which only "
                         "the LDE_DIAGNOSTICS build has",
@@ -327,16 +345,23 @@ int check_knobs() {
 #endif
     static std::once_flag once;
     std::call_once(once, [] {
-        std::string names;
+        std::string used, ignored;
         for (char **e = environ; e && *e; ++e)
             if (std::strncmp(*e, "LDE_", 4) == 0) {
-                names += ' ';
-                names.append(*e, std::strcspn(*e, "="));
+                std::string n(*e, std::strcspn(*e, "="));
+                // host-side (Python) settings are not the engine's
+                if (n == "LDE_LIBRARY" || n == "LDE_BENCH_BACKEND" || n == "LDE_BENCH_UNTIMED" ||
+                    n == "LDE_OFFLOAD_ARCH")
+                    continue;
+                (runtime_setting(n.c_str()) ? used : ignored) += ' ' + n;
             }
 #ifdef LDE_DIAGNOSTICS
-        names += " [diagnostics build]";
+        if (!used.empty()) used += " [diagnostics build]";
 #endif
-        if (!names.empty()) fprintf(stderr, "lde: non-default engine settings:%s\n", names.c_str());
+        if (!used.empty()) fprintf(stderr, "lde: engine settings from the environment:%s\n", used.c_str());
+        if (!ignored.empty())
+            fprintf(stderr, "lde: ignored (tuning knobs exist only in the diagnostics build):%s\n",
+                    ignored.c_str());
     });
     return LDE_OK;
 }
@@ -452,7 +477,7 @@ int build_toa_tables(lde_handle *h, const double *edges, int T, std::vector<unsi
     const long long span = tp.hi - tp.lo;  // 0 .. 2^32
     // fast layout: u32 relative thresholds, buckets narrower than every bin
     if (span >= 1 && span <= 0xffffffffLL && tp.lo <= 0x7fffffffLL &&
-        std::getenv("LDE_TOA_GENERAL") == nullptr) {
+        !(runtime_setting("LDE_TOA_GENERAL") && std::getenv("LDE_TOA_GENERAL") != nullptr)) {
         long long min_width = span;
         for (int i = 0; i < T; ++i)
             if (thr[i + 1] > thr[i]) min_width = std::min(min_width, thr[i + 1] - thr[i]);
@@ -1452,10 +1477,10 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
 }
 
 // validate the host LUT and copy it into the device format (allocated once)
-int upload_lut(lde_handle *h, const int32_t *out_lut) {
+// the device form of a host LUT (u16 screen or i32 screen * T), validated
+int convert_lut(lde_handle *h, const int32_t *out_lut, std::vector<uint16_t> &l16,
+                std::vector<int> &l32) {
     const long long n = (long long)h->R * h->L;
-    std::vector<uint16_t> l16;
-    std::vector<int> l32;
     if (h->lut16) l16.resize((size_t)n); else l32.resize((size_t)n);
     for (long long i = 0; i < n; ++i) {
         const int v = out_lut[i];
@@ -1464,6 +1489,14 @@ int upload_lut(lde_handle *h, const int32_t *out_lut) {
         if (h->lut16) l16[(size_t)i] = v < 0 ? (uint16_t)0xFFFF : (uint16_t)v;
         else l32[(size_t)i] = v < 0 ? -1 : (int)((long long)v * h->T);
     }
+    return LDE_OK;
+}
+
+int upload_lut(lde_handle *h, const int32_t *out_lut) {
+    const long long n = (long long)h->R * h->L;
+    std::vector<uint16_t> l16;
+    std::vector<int> l32;
+    if (int rc = convert_lut(h, out_lut, l16, l32)) return rc;
     const size_t bytes = (size_t)n * (h->lut16 ? 2 : 4);
     if (!h->d_lut) {
         if (h->lut16) {
@@ -1485,8 +1518,26 @@ int upload_lut(lde_handle *h, const int32_t *out_lut) {
 // footprint over every replica (sorted screen list) and every pixel's index
 // in its range's footprint.  Available when the ranges fit kPixMaxRanges and
 // the largest footprint's counters fit LDS (pix_acc_smem).
-int build_pixel(lde_handle *h, const int32_t *lut) {
-    h->pixel_ok = false;
+// PIXEL tables of a LUT, built into fresh device buffers without touching the
+// handle's current ones (lde_set_lut commits them only once everything it
+// needs has been built, so a failure leaves the old placement in place)
+struct PixStaged {
+    bool ok = false;  // PIXEL available for this LUT
+    lde::PixSetup pix{};
+    uint16_t *ploc = nullptr;
+    uint32_t *fp_off = nullptr, *fp_scr = nullptr;
+    PixStaged() = default;
+    PixStaged(const PixStaged &) = delete;
+    PixStaged &operator=(const PixStaged &) = delete;
+    ~PixStaged() {
+        dev_free(ploc);
+        dev_free(fp_off);
+        dev_free(fp_scr);
+    }
+};
+
+int stage_pixel(lde_handle *h, const int32_t *lut, PixStaged &st) {
+    st.ok = false;
     if (h->monitor || h->n_tiles == 0 || env_ll("LDE_PIXEL", 1) == 0) return LDE_OK;
     const long long L = h->L, R = h->R, S = h->S;
     const int T = h->T;
@@ -1537,17 +1588,37 @@ int build_pixel(lde_handle *h, const int32_t *lut) {
             }
         fp_off[(size_t)r + 1] = (uint32_t)fp.size();
     }
-    // (re)upload; the previous batch's kernels may still read the old tables
-    HIPCALL(h, hipStreamSynchronize(h->stream));
-    dev_free(h->d_ploc);
-    dev_free(h->d_pfp_off);
-    dev_free(h->d_pfp_scr);
-    if (int rc = dev_alloc(h, &h->d_ploc, loc.size())) return rc;
-    if (int rc = dev_alloc(h, &h->d_pfp_off, fp_off.size())) return rc;
-    if (int rc = dev_alloc(h, &h->d_pfp_scr, std::max<size_t>(1, fp.size()))) return rc;
-    HIPCALL(h, hipMemcpy(h->d_ploc, loc.data(), loc.size() * 2, hipMemcpyHostToDevice));
-    HIPCALL(h, hipMemcpy(h->d_pfp_off, fp_off.data(), fp_off.size() * 4, hipMemcpyHostToDevice));
-    if (!fp.empty()) HIPCALL(h, hipMemcpy(h->d_pfp_scr, fp.data(), fp.size() * 4, hipMemcpyHostToDevice));
+    if (int rc = dev_alloc(h, &st.ploc, loc.size())) return rc;
+    if (int rc = dev_alloc(h, &st.fp_off, fp_off.size())) return rc;
+    if (int rc = dev_alloc(h, &st.fp_scr, std::max<size_t>(1, fp.size()))) return rc;
+    HIPCALL(h, hipMemcpy(st.ploc, loc.data(), loc.size() * 2, hipMemcpyHostToDevice));
+    HIPCALL(h, hipMemcpy(st.fp_off, fp_off.data(), fp_off.size() * 4, hipMemcpyHostToDevice));
+    if (!fp.empty()) HIPCALL(h, hipMemcpy(st.fp_scr, fp.data(), fp.size() * 4, hipMemcpyHostToDevice));
+    // per-batch workspace (allocated once; harmless if the LUT is not committed)
+    if (!h->d_pcounts) {
+        if (int rc = dev_alloc(h, &h->d_pcounts, (size_t)h->cus * 4 * lde::kPixMaxRanges)) return rc;
+        if (int rc = dev_alloc(h, &h->d_pprev, (size_t)h->cus * 4 * lde::kPixMaxRanges)) return rc;
+        if (int rc = dev_alloc(h, &h->d_povf, 1)) return rc;
+        if (int rc = dev_alloc(h, &h->d_prstart, 2 * (size_t)lde::kPixMaxRanges + 1)) return rc;
+        if (int rc = dev_alloc(h, &h->d_pitem_count, 1)) return rc;
+    }
+    st.pix.rb = rb;
+    st.pix.nr = nr;
+    st.pix.rs = rs;
+    st.pix.fmax = fmax;
+    st.ok = true;
+    return LDE_OK;
+}
+
+// Swap the staged PIXEL tables in (no failure path: the handle state and the
+// staged buffers only exchange owners).  The caller has synchronized the
+// stream, so no kernel still reads the old tables.
+void commit_pixel(lde_handle *h, PixStaged &st) {
+    std::swap(h->d_ploc, st.ploc);
+    std::swap(h->d_pfp_off, st.fp_off);
+    std::swap(h->d_pfp_scr, st.fp_scr);
+    h->pixel_ok = st.ok;
+    if (!st.ok) return;
     // partition blocks: 4 x 512 or 2 x 1024 threads per CU (LDS ~36 / ~70 KB each)
     h->pix_unit = (int)std::max<long long>(1, std::min<long long>(2, env_ll("LDE_PIX_UNIT", 2)));
     h->pix_ept = h->pix_unit == 2 || env_ll("LDE_PIX_EPT", 8) == 16 ? 16 : 8;
@@ -1559,29 +1630,29 @@ int build_pixel(lde_handle *h, const int32_t *lut) {
     // relatively smaller margins: LOKI step 0.529 -> 0.520 ms)
     h->pix_pred = env_ll("LDE_PIX_PRED", 1) != 0;
     h->pix_grid = (int)std::max<long long>(
-        1, env_ll("LDE_PIX_GRID", (h->pix_ept == 16 && h->pix_unit == 1 ? 4 : h->pix_pred ? 1 : 2) *
-                                      (long long)h->cus));
+        1, std::min<long long>(4LL * h->cus,
+                               env_ll("LDE_PIX_GRID", (h->pix_ept == 16 && h->pix_unit == 1 ? 4 : h->pix_pred ? 1 : 2) *
+                                                          (long long)h->cus)));
     while (h->pix_unit > 1 && lde::pix_scatter_smem(h->tp, h->pix_unit) > 150 * 1024) --h->pix_unit;
-    if (lde::pix_scatter_smem(h->tp, h->pix_unit) > 160 * 1024) return LDE_OK;
-    if (!h->d_pcounts) {
-        if (int rc = dev_alloc(h, &h->d_pcounts, (size_t)h->pix_grid * lde::kPixMaxRanges)) return rc;
-        if (int rc = dev_alloc(h, &h->d_pprev, (size_t)h->pix_grid * lde::kPixMaxRanges)) return rc;
-        if (int rc = dev_alloc(h, &h->d_povf, 1)) return rc;
-        if (int rc = dev_alloc(h, &h->d_prstart, 2 * (size_t)lde::kPixMaxRanges + 1)) return rc;
-        if (int rc = dev_alloc(h, &h->d_pitem_count, 1)) return rc;
+    if (lde::pix_scatter_smem(h->tp, h->pix_unit) > 160 * 1024) {
+        h->pixel_ok = false;
+        return;
     }
     h->pix_prev_n = 0;  // ranges may have changed: the next batch counts
-    h->pix.rb = rb;
-    h->pix.nr = nr;
-    h->pix.rs = rs;
-    h->pix.fmax = fmax;
+    h->pix = st.pix;
     h->pix.loc = h->d_ploc;
     h->pix.fp_off = h->d_pfp_off;
     h->pix.fp_scr = h->d_pfp_scr;
-    h->pixel_ok = true;
     if (env_ll("LDE_VERBOSE", 0))
         fprintf(stderr, "lde pixel: %d ranges of 2^%d pixels, widest footprint %d screens (%zu B LDS)\n",
-                nr, rb, fmax, lde::pix_acc_smem(rb, fmax, T));
+                h->pix.nr, h->pix.rb, h->pix.fmax, lde::pix_acc_smem(h->pix.rb, h->pix.fmax, h->T));
+}
+
+int build_pixel(lde_handle *h, const int32_t *lut) {
+    PixStaged st;
+    if (int rc = stage_pixel(h, lut, st)) return rc;
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    commit_pixel(h, st);
     return LDE_OK;
 }
 
@@ -2878,8 +2949,27 @@ int lde_set_lut(lde_handle *h, const int32_t *out_lut) {
     if (h->monitor) return fail(h, LDE_EINVAL, "a monitor handle has no LUT");
     if (!out_lut) return fail(h, LDE_EINVAL, "out_lut is NULL");
     DeviceGuard guard(h->device);
-    if (int rc = upload_lut(h, out_lut)) return rc;
-    return build_pixel(h, out_lut);
+    // transactional: validate and build everything first (new LUT image, new
+    // PIXEL tables in fresh buffers); a failure up to here leaves the engine
+    // binning with the old placement (workflows.py _move relies on it)
+    std::vector<uint16_t> l16;
+    std::vector<int> l32;
+    if (int rc = convert_lut(h, out_lut, l16, l32)) return rc;
+    PixStaged st;
+    if (int rc = stage_pixel(h, out_lut, st)) return rc;
+    // commit: the previous batch's kernels may still read the old tables
+    HIPCALL(h, hipStreamSynchronize(h->stream));
+    const size_t bytes = (size_t)h->R * h->L * (h->lut16 ? 2 : 4);
+    const hipError_t e = hipMemcpy(h->d_lut, h->lut16 ? (const void *)l16.data() : (const void *)l32.data(),
+                                   bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {  // the device is failing: nothing consistent to keep
+        h->pixel_ok = false;
+        return fail(h, LDE_EHIP, "LUT upload failed: %s", hipGetErrorString(e));
+    }
+    // every replica's hot set / SIEVE tables derive from the LUT: rebuild lazily
+    for (auto &u : h->hot_uses) u = -1;
+    commit_pixel(h, st);
+    return LDE_OK;
 }
 
 int lde_get_stream(lde_handle *h, void **stream) {

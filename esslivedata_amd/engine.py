@@ -46,7 +46,7 @@ class _HostBlock:
     def __init__(self, nbytes: int, dtype: np.dtype, count: int) -> None:
         self._lib = _native.lib()
         p = ctypes.c_void_p()
-        check(self._lib.lde_host_alloc(int(nbytes), ctypes.byref(p)))
+        check(self._lib.lde_host_alloc(int(nbytes), ctypes.byref(p)), None, self._lib)
         self.ptr = int(p.value)
         self.__array_interface__ = {
             'shape': (count,), 'typestr': np.dtype(dtype).str, 'data': (self.ptr, False),
@@ -200,7 +200,7 @@ class BinningEngine:
         self._unknown_id = lo - 1 if lo > _I32_MIN else (hi if hi <= _I32_MAX else None)
         h = ctypes.c_void_p()
         rc = lib.lde_create(ctypes.byref(cfg), ctypes.byref(h))
-        check(rc, None)
+        check(rc, None, lib)
         self._h = h
         self._lib = lib
         self._device = int(device)
@@ -210,7 +210,7 @@ class BinningEngine:
         self._out = _native.LdeOutputs()  # reused by finalize (every field set per call)
         self._out_ref = ctypes.byref(self._out)
         sp = ctypes.c_void_p()
-        check(lib.lde_get_stream(h, ctypes.byref(sp)), h)
+        check(lib.lde_get_stream(h, ctypes.byref(sp)), h, lib)
         self._stream_ptr = int(sp.value or 0)
 
     # ------------------------------------------------------------------
@@ -235,7 +235,7 @@ class BinningEngine:
         return self._dtype
 
     def _call(self, fn, *args) -> None:
-        check(fn(self._h, *args), self._h)
+        check(fn(self._h, *args), self._h, self._lib)
 
     # ------------------------------------------------------------------
     def stage(self, pid, toa) -> None:
@@ -358,13 +358,13 @@ class BinningEngine:
         base = ctypes.addressof(arr)
         rc = self._lib.lde_stage_device_batch(self._h, n, base, base + 8 * n, base + 16 * n)
         if rc:
-            check(rc, self._h)
+            check(rc, self._h, self._lib)
         self._keepalive.append(messages)
 
     def accumulate(self, replica: int = 0) -> None:
         rc = self._lib.lde_accumulate(self._h, int(replica))
         if rc:
-            check(rc, self._h)
+            check(rc, self._h, self._lib)
         self._keepalive.clear()
 
     def finalize(self, *, images: bool = True, hists: bool = False) -> FinalizeResult:
@@ -383,7 +383,7 @@ class BinningEngine:
         out.cumulative_hist = mh.ctypes.data if mh is not None else None
         rc = self._lib.lde_finalize(self._h, self._out_ref)
         if rc:
-            check(rc, self._h)
+            check(rc, self._h, self._lib)
         t0, t1, t2, t3 = out.totals
         shape = (self._S, self._T)
         return FinalizeResult(
@@ -453,7 +453,7 @@ class BinningEngine:
         sharded per-push merge, ``lde_accumulate_push``)."""
         rc = self._lib.lde_accumulate_push(self._h, int(replica), dst_ptr)
         if rc:
-            check(rc, self._h)
+            check(rc, self._h, self._lib)
         self._keepalive.clear()
 
     def push_counts(self, src_ptr: int) -> None:

@@ -15,10 +15,32 @@ def pytest_configure(config):
 
 @pytest.fixture(scope='session')
 def engine_lib():
-    """The built HIP engine library (build it if missing)."""
+    """The built HIP engine library (build it if missing; also the diagnostics
+    build the ``knobs`` fixture loads)."""
     from esslivedata_amd import build
 
     build.build()
+    build.build(diagnostics=True)
     from esslivedata_amd import _native
 
     return _native.lib()
+
+
+@pytest.fixture
+def knobs(monkeypatch, engine_lib):
+    """Engine tuning knobs for one test: ``knobs(LDE_X=v, ...)`` sets the
+    variables, and every engine the test creates loads the diagnostics build,
+    the only one that reads them (the product library fixes its tuning)."""
+    from esslivedata_amd import _native
+
+    cm = _native.diagnostics_library()
+    cm.__enter__()
+
+    def set_(**kv):
+        for k, v in kv.items():
+            monkeypatch.setenv(k, str(v))
+
+    try:
+        yield set_
+    finally:
+        cm.__exit__(None, None, None)

@@ -161,9 +161,8 @@ def test_dummy_logical_view_multi_batch(strategy):
 
 @pytest.mark.parametrize('variant', range(len(VARIANTS)))
 @pytest.mark.parametrize('strategy', STRATEGIES)
-def test_dream_mantle_geometric_skewed(strategy, variant, monkeypatch):
-    for k, v in VARIANTS[variant].items():
-        monkeypatch.setenv(k, v)
+def test_dream_mantle_geometric_skewed(strategy, variant, knobs):
+    knobs(**VARIANTS[variant])
     from esslivedata_amd import projection, synthetic
 
     inst = synthetic.dream_mantle()
@@ -201,10 +200,10 @@ def test_dream_mantle_geometric_skewed(strategy, variant, monkeypatch):
 
 @pytest.mark.parametrize('general', [False, True])
 @pytest.mark.parametrize('strategy', STRATEGIES)
-def test_edge_ties_are_bit_exact(strategy, general, monkeypatch):
+def test_edge_ties_are_bit_exact(strategy, general, knobs):
     """Integer TOAs on, just below and just above every float64 edge."""
     if general:
-        monkeypatch.setenv('LDE_TOA_GENERAL', '1')
+        knobs(LDE_TOA_GENERAL='1')
     from esslivedata_amd import projection
 
     dn = np.arange(1, 65, dtype=np.int32)
@@ -460,15 +459,15 @@ def test_finalize_partials_match_finalize():
 
 @pytest.mark.parametrize('karg', ['1', '0'])
 @pytest.mark.parametrize('n_msgs', [1, 14, 24, 25, 40])
-def test_split_many_device_messages(n_msgs, karg, monkeypatch):
+def test_split_many_device_messages(n_msgs, karg, knobs):
     """SIEVE with the message descriptors passed as kernel arguments (<= 24
     messages) or uploaded (more, or LDE_KARG_SEGS=0): ragged, misaligned
     device segments, replica cycling, hot-set refresh every batch."""
     import torch
 
-    monkeypatch.setenv('LDE_KARG_SEGS', karg)
-    monkeypatch.setenv('LDE_LDS_CTAB', karg)  # '0': the k_chunk_tab paths
-    monkeypatch.setenv('LDE_HOT_REFRESH', '2')
+    knobs(LDE_KARG_SEGS=karg)
+    knobs(LDE_LDS_CTAB=karg)  # '0': the k_chunk_tab paths
+    knobs(LDE_HOT_REFRESH='2')
     from esslivedata_amd import projection, synthetic
 
     inst = synthetic.dream_mantle()
@@ -595,11 +594,11 @@ def test_default_stream_engine_outlives_recorded_tensors():
 
 
 @pytest.mark.parametrize('grid', ['1', '3'])
-def test_sieve_hot_cells_with_millions_of_events(grid, monkeypatch):
+def test_sieve_hot_cells_with_millions_of_events(grid, knobs):
     """One or three sieve blocks (one: its chunk range exceeds the LDS chunk
     table); two adjacent hot cells take 1.8 M and 0.6 M events per batch,
     far past any 16-bit count, plus a third hot screen and a uniform rest."""
-    monkeypatch.setenv('LDE_SPLIT_GRID', grid)
+    knobs(LDE_SPLIT_GRID=grid)
     from esslivedata_amd import projection
 
     dn = np.arange(1, 4097, dtype=np.int32)
@@ -627,12 +626,12 @@ def test_sieve_hot_cells_with_millions_of_events(grid, monkeypatch):
     np.testing.assert_array_equal(res.current_hist, exp)
 
 
-def test_sieve_hot_rows_mixed_u16_and_u32_blocks(monkeypatch):
+def test_sieve_hot_rows_mixed_u16_and_u32_blocks(knobs):
     """Eight sieve blocks over one batch whose first half piles millions of
     events into two hot cells: the first blocks' hot rows overflow 16 bits
     (flushed as u32), the last blocks' do not (flushed as u16); the reduce
     mixes both formats."""
-    monkeypatch.setenv('LDE_SPLIT_GRID', '8')
+    knobs(LDE_SPLIT_GRID='8')
     from esslivedata_amd import projection
 
     dn = np.arange(1, 4097, dtype=np.int32)
@@ -766,7 +765,7 @@ def test_loki_pixel_forced_on_skewed_stream_splits_hot_ranges():
         assert res.current_total == int(exp.sum())
 
 
-def test_loki_pixel_predicted_slots_exact_under_shifts(monkeypatch):
+def test_loki_pixel_predicted_slots_exact_under_shifts(knobs):
     """PIXEL with predicted slots (no count pass: each (block, range) slot is
     sized from the previous batch's run totals).  Four partition blocks make
     the 784 slots hold >= 256 events each at 1e6 events per batch, so every
@@ -777,7 +776,7 @@ def test_loki_pixel_predicted_slots_exact_under_shifts(monkeypatch):
     both replicas; counts stay bit-exact."""
     from esslivedata_amd import projection, synthetic
 
-    monkeypatch.setenv('LDE_PIX_GRID', '4')
+    knobs(LDE_PIX_GRID='4')
     inst = synthetic.loki_bank0(n_replicas=2)
     view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
     edges = inst.edges.edges_ns()
@@ -817,16 +816,15 @@ PIXEL_VARIANTS = [
 ]
 
 
-@pytest.mark.parametrize('knobs', PIXEL_VARIANTS, ids=lambda k: ','.join(f'{a}={b}' for a, b in k.items()) or 'default')
-def test_loki_pixel_variants(monkeypatch, knobs):
+@pytest.mark.parametrize('variant_knobs', PIXEL_VARIANTS, ids=lambda k: ','.join(f'{a}={b}' for a, b in k.items()) or 'default')
+def test_loki_pixel_variants(knobs, variant_knobs):
     """Every PIXEL shape knob, counted (first batch) and predicted (second
     and third: six partition blocks, so 1.2e6-event batches fill the slots),
     bit-exact against the oracle over two replicas."""
     from esslivedata_amd import projection, synthetic
 
-    monkeypatch.setenv('LDE_PIX_GRID', '6')
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
+    knobs(LDE_PIX_GRID='6')
+    knobs(**variant_knobs)
     inst = synthetic.loki_bank0(n_replicas=2)
     view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
     edges = inst.edges.edges_ns()

@@ -271,3 +271,44 @@ def test_coordinate_bins_for_unusual_edges(kind):
                                coordinate=ora.wavelength_mode(ltot, tab, 3.0, 0.5, 0.0, dt))
     o.accumulate(pid, toa)
     np.testing.assert_array_equal(res.current_hist, o.finalize()['histogram_current'])
+
+
+@pytest.mark.parametrize('strategy', ['pixel', 'auto'])
+def test_loki_wavelength_on_pixel_matches_oracle(strategy):
+    """PIXEL after the coordinate pre-pass: LOKI bank 0, whose
+    footprints fit LDS, in wavelength mode.  The pre-pass writes every
+    event's coordinate bin as its "time"; PIXEL then bins those against the
+    integer edges 0..T with the tables sized at create time.  Three batches
+    (counted, then predicted slots) over two replicas, bit-exact against the
+    NumPy oracle, and PIXEL is what ran."""
+    from esslivedata_amd import projection, synthetic, wavelength
+    from esslivedata_amd.edges import WavelengthEdges
+    from esslivedata_amd.engine import BinningEngine
+
+    inst = synthetic.loki_bank0(n_replicas=2)
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    tab = wavelength.ideal_lookup_table(27.5, 29.5, 41, 71.5e6, 287)
+    lt = wavelength.pixel_ltotal(inst.positions, source_position=(0.0, 0.0, -23.0))
+    d = wavelength.distance_per_pid(inst.detector_number, lt, view.pid_offset, view.lut.shape[1])
+    edges = WavelengthEdges(start=0.5, stop=10.0, num_bins=100).get_edges()
+    eng = BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                        n_screen=view.n_screen, strategy=strategy)
+    eng.set_coordinate_lut(d, tab.table, dist0=tab.distance0, dist_step=tab.distance_step,
+                           time0=tab.time0, time_step=tab.time_step)
+    o = ora.OracleDetectorView(
+        detector_number=inst.detector_number, pixel_screen=_pixel_screen(inst),
+        screen_shape=tuple(view.screen_shape), toa_edges_ns=edges,
+        coordinate=ora.wavelength_mode(lt, tab.table, tab.distance0, tab.distance_step,
+                                       tab.time0, tab.time_step))
+    for batch in range(3):
+        pid, toa = synthetic.uniform_events(1_500_001 + batch, 1, 802816, seed=500 + batch)
+        eng.stage(pid[:600_000], toa[:600_000])
+        eng.stage(pid[600_000:], toa[600_000:])
+        eng.accumulate(batch % 2)
+        assert eng.info()['last_strategy'] == 'pixel'
+        o.accumulate(pid, toa)
+    res = eng.finalize(hists=True)
+    exp = o.finalize()
+    assert exp['histogram_cumulative'].sum() > 3_000_000
+    np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
+    np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
