@@ -41,6 +41,15 @@ STRATEGIES = {'auto': 0, 'atomic': 1, 'partition': 2, 'paged': 3, 'split': 4, 'p
 LDE_CURRENT = 0
 LDE_CUMULATIVE = 1
 
+COUNTERS = {
+    'pix_overflow': 0,
+    'pix_overflow_cap': 1,
+    'pix_predicted': 2,
+    'waits': 3,
+    'waits_blocked': 4,
+    'wait_pred_us': 5,
+}
+
 KERNELS = {
     'atomic': 0,
     'partition': 1,
@@ -90,6 +99,7 @@ EXPORTED_SYMBOLS = (
     'lde_timing_select',
     'lde_kernel_stats',
     'lde_info',
+    'lde_counter',
     'lde_set_groups',
     'lde_group_spectra',
     'lde_host_alloc',
@@ -190,6 +200,7 @@ def _declare(lib: ctypes.CDLL) -> None:
             ctypes.c_int,
             [H, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)],
         ),
+        'lde_counter': (ctypes.c_int, [H, i32, ctypes.POINTER(i64)]),
         'lde_info': (
             ctypes.c_int,
             [

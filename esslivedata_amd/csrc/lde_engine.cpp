@@ -190,6 +190,7 @@ struct lde_handle {
     uint4 *d_povf_grp = nullptr;
     size_t povf_cap = 0;
     long long pix_prev_n = 0, pix_prev_units = 0;
+    bool pix_last_pred = false;  // the last PIXEL batch used predicted slots
     int pix_prev_grid = 0;
     std::vector<double> edges;  // the create-time edges (event unit)
     // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
@@ -197,6 +198,7 @@ struct lde_handle {
     int sieve_ablate = 0;
     bool early_gather = false;  // LDE_EARLY_GATHER
     bool sieve_pack = false;    // LDE_SIEVE_PACK
+    bool lane_compact = false;  // LDE_SIEVE_COMPACT: cold keys compacted per lane
     int cold_sort_mode = 2;     // LDE_COLD_SORT: 0 block, 1 wave-independent, 2 16-byte groups
     int cold_sort_kpt = 48;     // LDE_COLD_SORT_KPT: keys per thread per piece of mode 2 (16, 32, 48)
     bool key24 = true;          // LDE_KEY24: 24-bit cold keys when S * T < 2^24 - 1
@@ -1112,6 +1114,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         sa.ablate = h->sieve_ablate;
         sa.early_gather = h->early_gather ? 1 : 0;
         sa.pack = h->sieve_pack ? 1 : 0;
+        sa.lane_compact = h->lane_compact ? 1 : 0;
         // 24-bit cold keys need the 16-byte-group sort (the only reader)
         const bool key24 = pad8 && h->key24 && h->nbins < 0xFFFFFFLL;
         sa.key24 = key24 ? 1 : 0;
@@ -1254,7 +1257,11 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
                             20.0 * (double)slots + 4.0;
     const bool pred = h->pix_pred && h->pix_prev_grid == grid && ratio >= 0.5 && ratio <= 2.0 &&
                       total >= 256 * slots && pred_pay < 0x7FFFFFF0;
-    const size_t ovf_groups = n_pay / 4 + 1;  // every group of the batch, at most
+    // overflow list: 1/32 of the batch's groups (a Poisson stream overflows
+    // ~0.4 % of them at 2 sigma margins) -- groups past it are added by pass A
+    // itself with global atomics, so any stream stays exact
+    const long long cap_knob = env_ll("LDE_PIX_OVF_CAP", 0);  // diagnostics: force the fallback
+    const size_t ovf_groups = cap_knob > 0 ? (size_t)cap_knob : std::max<size_t>(65536, n_pay / 4 / 32 + 1);
     if (pred) {
         n_pay = std::max(n_pay, (size_t)pred_pay);
         if (int rc = grow(h, &h->d_povf_grp, h->povf_cap, ovf_groups)) return rc;
@@ -1282,6 +1289,8 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.pid_off = h->pid_off;
     a.L = (unsigned)h->L;
     a.rb = h->pix.rb;
+    a.rw = h->pix.rw;
+    a.rm = h->pix.rm;
     a.nr = h->pix.nr;
     a.rs = h->pix.rs;
     a.tab = h->d_tab;
@@ -1299,7 +1308,12 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         a.pred = (float)ratio;
         a.ovf_grp = h->d_povf_grp;
         a.ovf_cap = (uint32_t)ovf_groups;
+        a.ovf_loc = h->pix.loc + (size_t)replica * h->L;
+        a.ovf_fp_off = h->pix.fp_off;
+        a.ovf_fp_scr = h->pix.fp_scr;
+        a.ovf_hist = h->d_win32;
     }
+    h->pix_last_pred = pred;
     h->pix_prev_n = total;  // the scatter records this batch's run totals
     h->pix_prev_units = units;
     h->pix_prev_grid = grid;
@@ -1541,17 +1555,31 @@ int stage_pixel(lde_handle *h, const int32_t *lut, PixStaged &st) {
     if (h->monitor || h->n_tiles == 0 || env_ll("LDE_PIXEL", 1) == 0) return LDE_OK;
     const long long L = h->L, R = h->R, S = h->S;
     const int T = h->T;
-    // ranges of 2^rb pixels: the smallest rb with at most 256 ranges
-    // (LDE_PIX_MAX_RANGES, up to kPixMaxRanges; LOKI bank 0: 196 ranges of 4096
-    // pixels; 392 of 2048 keep the same 288-screen widest footprint, so pass B
-    // gains nothing and pass A's runs get shorter)
+    // ranges of rw consecutive pixels, one per CU: pass B runs about one item
+    // per range, so every CU gets one (LOKI bank 0: 256 ranges of 3,136
+    // pixels instead of 196 of 4,096 on 196 CUs).  LDE_PIX_RANGES=0 (a
+    // diagnostics variant): the smallest power of two giving at most
+    // LDE_PIX_MAX_RANGES ranges (up to kPixMaxRanges)
     const long long max_nr = std::max<long long>(
         1, std::min<long long>(lde::kPixMaxRanges, env_ll("LDE_PIX_MAX_RANGES", 256)));
+    const long long want = std::min<long long>(max_nr, env_ll("LDE_PIX_RANGES", h->cus));
+    long long rw;
+    if (want > 0) {
+        rw = std::max<long long>(256, (L + want - 1) / want);
+    } else {
+        rw = 256;
+        while (rw < (1LL << 20) && (L + rw - 1) / rw > max_nr) rw *= 2;
+    }
     int rb = 8;
-    while (rb < 20 && ((L + (1LL << rb) - 1) >> rb) > max_nr) ++rb;
+    while ((1LL << rb) < rw) ++rb;
     int tbits = 0;
     while ((1 << tbits) < T) ++tbits;
-    const int nr = (int)((L + (1LL << rb) - 1) >> rb);
+    const int nr = (int)((L + rw - 1) / rw);
+    if (nr > max_nr) return LDE_OK;
+    // q / rw as umulhi(q, rm), checked for every pixel
+    const uint32_t rm = (uint32_t)((1ULL << 32) / (unsigned long long)rw + 1);
+    for (long long q = 0; q < L; ++q)
+        if ((long long)(((unsigned long long)q * rm) >> 32) != q / rw) return LDE_OK;
     // scatter staging word: range (rbits, the all-ones range never used) above
     // an rs-bit payload whose all-ones value is the dropped marker; stored
     // payloads are 24-bit (0xFFFFFF dropped), so local pixel | bin << rb
@@ -1565,7 +1593,7 @@ int stage_pixel(lde_handle *h, const int32_t *lut, PixStaged &st) {
     std::vector<uint16_t> loc((size_t)(R * L), 0xFFFF);
     int fmax = 0;
     for (int r = 0; r < nr; ++r) {
-        const long long q0 = (long long)r << rb, q1 = std::min(L, q0 + (1LL << rb));
+        const long long q0 = (long long)r * rw, q1 = std::min(L, q0 + rw);
         const size_t first = fp.size();
         for (long long rep = 0; rep < R; ++rep)
             for (long long q = q0; q < q1; ++q) {
@@ -1603,6 +1631,8 @@ int stage_pixel(lde_handle *h, const int32_t *lut, PixStaged &st) {
         if (int rc = dev_alloc(h, &h->d_pitem_count, 1)) return rc;
     }
     st.pix.rb = rb;
+    st.pix.rw = (uint32_t)rw;
+    st.pix.rm = rm;
     st.pix.nr = nr;
     st.pix.rs = rs;
     st.pix.fmax = fmax;
@@ -1644,8 +1674,8 @@ void commit_pixel(lde_handle *h, PixStaged &st) {
     h->pix.fp_off = h->d_pfp_off;
     h->pix.fp_scr = h->d_pfp_scr;
     if (env_ll("LDE_VERBOSE", 0))
-        fprintf(stderr, "lde pixel: %d ranges of 2^%d pixels, widest footprint %d screens (%zu B LDS)\n",
-                h->pix.nr, h->pix.rb, h->pix.fmax, lde::pix_acc_smem(h->pix.rb, h->pix.fmax, h->T));
+        fprintf(stderr, "lde pixel: %d ranges of %u pixels, widest footprint %d screens (%zu B LDS)\n",
+                h->pix.nr, h->pix.rw, h->pix.fmax, lde::pix_acc_smem(h->pix.rb, h->pix.fmax, h->T));
 }
 
 int build_pixel(lde_handle *h, const int32_t *lut) {
@@ -2164,6 +2194,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->early_gather = env_ll("LDE_EARLY_GATHER", 0) != 0;
         h->probe = env_ll("LDE_HOST_PROBE", 0) != 0;
         h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
+        h->lane_compact = env_ll("LDE_SIEVE_COMPACT", 0) != 0;
         h->cold_sort_mode = (int)env_ll("LDE_COLD_SORT", 2);
         {
             const long long k = env_ll("LDE_COLD_SORT_KPT", 48);
@@ -3014,6 +3045,40 @@ int lde_kernel_stats(lde_handle *h, int32_t kernel_id, double *ms, int64_t *laun
     if (ms) *ms = h->kms[kernel_id];
     if (launches) *launches = h->kcount[kernel_id];
     return LDE_OK;
+}
+
+int lde_counter(lde_handle *h, int32_t id, int64_t *value) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!value) return fail(h, LDE_EINVAL, "value is NULL");
+    DeviceGuard guard(h->device);
+    switch (id) {
+    case LDE_C_PIX_OVERFLOW: {
+        *value = 0;
+        if (!h->d_povf || !h->pix_last_pred) return LDE_OK;
+        uint32_t n = 0;
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        HIPCALL(h, hipMemcpy(&n, h->d_povf, 4, hipMemcpyDeviceToHost));
+        *value = n;
+        return LDE_OK;
+    }
+    case LDE_C_PIX_OVERFLOW_CAP:
+        *value = (int64_t)h->povf_cap;
+        return LDE_OK;
+    case LDE_C_PIX_PREDICTED:
+        *value = h->pix_last_pred ? 1 : 0;
+        return LDE_OK;
+    case LDE_C_WAITS:
+        *value = h->waits_total;
+        return LDE_OK;
+    case LDE_C_WAITS_BLOCKED:
+        *value = h->waits_blocked;
+        return LDE_OK;
+    case LDE_C_WAIT_PRED_US:
+        *value = (int64_t)h->wait_pred_us;
+        return LDE_OK;
+    default:
+        return fail(h, LDE_EINVAL, "unknown counter id %d", id);
+    }
 }
 
 int lde_info(lde_handle *h, int64_t *n_screen, int32_t *n_toa_bins, int64_t *staged,

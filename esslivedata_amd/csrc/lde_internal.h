@@ -195,6 +195,7 @@ struct SieveArgs {
     int lds_ctab;                // 1: build the block's chunk table in LDS (no chunk_tab)
     int karg;                    // lds_ctab: descriptors from sk (else from segs)
     int early_gather;            // 1: gathers issued one iteration before they are binned
+    int lane_compact = 0;        // 1: cold keys compacted per lane (three ballots per half)
     int pack;                    // 1: TOA bin packed into the table word at the gather
     SegKarg sk;                  // lds_ctab: the message descriptors (n_segs <= kKargSegs)
     const int *dummy;            // the all-invalid chunk
@@ -392,7 +393,8 @@ struct PixArgs {
     long long n_chunks;
     int pid_off;
     unsigned L;
-    int rb;                      // range of pixel q: q >> rb
+    int rb;                      // local pixel bits (2^rb >= rw)
+    uint32_t rw = 0, rm = 0;     // range of pixel q: q / rw = umulhi(q, rm)
     int nr;                      // ranges (<= kPixMaxRanges)
     int rs;                      // scatter staging word: range << rs | payload (rs bits)
     const unsigned char *tab;    // TOA lookup image
@@ -414,10 +416,16 @@ struct PixArgs {
     uint32_t *prev = nullptr;    // [grid][nr] padded run totals of the last scatter
     uint32_t *ovf = nullptr;     // [1] overflow groups written (reset by k_pix_chunks)
     uint4 *ovf_grp = nullptr;    // [ovf_cap] staging words (range << rs | payload) x 4
-    uint32_t ovf_cap = 0;
+    uint32_t ovf_cap = 0;        // sized from the prediction margin; groups past it are
+                                 // added by pass A itself (global atomics, exact):
+    const uint16_t *ovf_loc = nullptr;     // the replica's footprint-local screens [L]
+    const uint32_t *ovf_fp_off = nullptr;  // [nr + 1]
+    const uint32_t *ovf_fp_scr = nullptr;
+    uint32_t *ovf_hist = nullptr;          // the window
 };
 struct PixSetup {                // setup-time tables (lde_create / lde_set_lut)
     int rb = 0, nr = 0, fmax = 0, rs = 24;
+    uint32_t rw = 0, rm = 0;           // range width (pixels) and its multiply-high reciprocal
     const uint16_t *loc = nullptr;     // [R][L] footprint-local screen of every pixel (0xFFFF: dropped)
     const uint32_t *fp_off = nullptr;  // [nr + 1] footprint list offsets
     const uint32_t *fp_scr = nullptr;  // footprint screens, range after range

@@ -51,6 +51,7 @@ constexpr int kEPT = kSplitEPT;               // 8 events per thread per chunk
 constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (half a chunk)
 constexpr int kSieveKeyed = 262144;           // mode bit: the stream holds finished words
 constexpr int kSieveToaLog = 1 << 20;         // mode bit: log-linear TOA buckets
+constexpr int kSieveLaneCompact = 1 << 21;    // mode bit: cold keys compacted per lane
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
@@ -443,6 +444,45 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             uint32_t tot = 0;
+            if (ABL & kSieveLaneCompact) {
+                // per lane: the half's events classified with per-lane
+                // compares only (no wave mask per event), one LDS atomic each;
+                // the lane's cold keys then go to consecutive staging words at
+                // a wave prefix built from three ballots of the lane's count
+                // (0..4) -- instead of three ballots, a prefix count and a
+                // mask round trip per event
+                uint32_t kk[kEPT / 2], cm = 0, nc = 0;
+#pragma unroll
+                for (int e = 0; e < kEPT / 2; ++e) {
+                    const int ev = h * kEPT / 2 + e;
+                    const uint32_t v = ws[ev] | g[ev];
+                    const uint32_t b = (ABL & kSieveKeyed) ? 0u
+                                       : (ABL & 65536) ? ((v >> kSieveTagShift) & 0xFFu)
+                                                       : (tw[ev] & 0xFFu) + (((dc[ev] & wmask) >= (tw[ev] >> 8)) ? 1u : 0u);
+                    const uint32_t fl = v >> 30;
+                    const uint32_t k4 = ((v & kSieveValueMask) + b) << 2;
+                    const bool in = b < T;
+                    const bool cold_e = in && fl == 2u;
+                    const bool hot_e = in && fl == 3u;
+                    const uint32_t aidx4 = hot_e ? k4 : cold_e ? ((k4 >> tsh) << 2) + o_tcnt4 : dum4;
+                    __hip_atomic_fetch_add(&lds_at(sm, aidx4), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    kk[e] = k4;
+                    cm |= (cold_e ? 1u : 0u) << e;
+                    nc += cold_e ? 1u : 0u;
+                }
+                const unsigned long long b0 = __builtin_amdgcn_ballot_w64((nc & 1u) != 0u);
+                const unsigned long long b1 = __builtin_amdgcn_ballot_w64((nc & 2u) != 0u);
+                const unsigned long long b2 = __builtin_amdgcn_ballot_w64((nc & 4u) != 0u);
+                uint32_t pos = o_stg_w + lanes_below(b0) + 2u * lanes_below(b1) + 4u * lanes_below(b2);
+                tot = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
+#pragma unroll
+                for (int e = 0; e < kEPT / 2; ++e) {
+                    const bool c = (cm >> e) & 1u;
+                    lds_at(sm, c ? pos << 2 : dum4) = kk[e];
+                    pos += c ? 1u : 0u;
+                }
+            } else {
 #pragma unroll
             for (int e = h * kEPT / 2; e < (h + 1) * kEPT / 2; ++e) {
                 const uint32_t v = ws[e] | g[e];
@@ -472,6 +512,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 const uint32_t aidx4 = (ABL & 1) ? tidx4 : vsel(hm, k4, tidx4);
                 __hip_atomic_fetch_add(&lds_at(sm, aidx4), 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
             }
             const uint32_t res = (tot + 3u) & ~3u;
             // the previous half's keys leave now (their LDS read is long done)
@@ -1559,9 +1600,10 @@ static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, h
 
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                         hipEvent_t stop) {
-    const int mode = a.keyed ? kSieveKeyed
+    const int mode = a.keyed ? kSieveKeyed | (a.lane_compact ? kSieveLaneCompact : 0)
                              : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0) |
-                                   (a.toa_log ? kSieveToaLog : 0);
+                                   (a.toa_log ? kSieveToaLog : 0) |
+                                   (a.lane_compact ? kSieveLaneCompact : 0);
     switch (mode) {
 #define LDE_SIEVE_MODE(m) \
     case m: return launch_sieve_t<m>(a, grid, st, start, stop);
@@ -1574,6 +1616,9 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     LDE_SIEVE_MODE(kSieveToaLog) LDE_SIEVE_MODE(kSieveToaLog | 256) LDE_SIEVE_MODE(kSieveToaLog | 2048)
     LDE_SIEVE_MODE(kSieveToaLog | 65536) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256)
     LDE_SIEVE_MODE(kSieveToaLog | 65536 | 2048) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256 | 2048)
+    // per-lane cold-key compaction
+    LDE_SIEVE_MODE(kSieveLaneCompact) LDE_SIEVE_MODE(kSieveLaneCompact | 65536)
+    LDE_SIEVE_MODE(kSieveLaneCompact | kSieveKeyed) LDE_SIEVE_MODE(kSieveLaneCompact | kSieveToaLog)
 #ifdef LDE_DIAGNOSTICS
     // timing probes (wrong results), diagnostics build only
     LDE_SIEVE_MODE(1) LDE_SIEVE_MODE(2) LDE_SIEVE_MODE(4) LDE_SIEVE_MODE(6)

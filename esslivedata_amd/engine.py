@@ -517,6 +517,12 @@ class BinningEngine:
         )
         return ms.value, n.value
 
+    def counter(self, name: str) -> int:
+        """An engine counter (``lde_counter``; names in ``_native.COUNTERS``)."""
+        v = ctypes.c_int64()
+        self._call(self._lib.lde_counter, _native.COUNTERS[name], ctypes.byref(v))
+        return v.value
+
     def info(self) -> dict:
         s, st, eb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         t, tb, nt, ls = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()

@@ -342,6 +342,23 @@ int lde_timing_enable(lde_handle *h, int32_t enable);
 int lde_timing_select(lde_handle *h, uint32_t mask);
 int lde_kernel_stats(lde_handle *h, int32_t kernel_id, double *ms, int64_t *launches);
 
+/* Counters for tests and reports (lde_counter):
+ *   LDE_C_PIX_OVERFLOW      groups of four events the last PIXEL batch could not
+ *                           place in their predicted slots (synchronizes the stream)
+ *   LDE_C_PIX_OVERFLOW_CAP  the overflow list's capacity in groups (groups past it
+ *                           are added by pass A itself, exactly)
+ *   LDE_C_PIX_PREDICTED     1 if the last PIXEL batch used predicted slots
+ *   LDE_C_WAITS             finalize waits that found the GPU still busy
+ *   LDE_C_WAITS_BLOCKED     ... of which ended in a blocking (interrupt) wait
+ *   LDE_C_WAIT_PRED_US      the predicted finalize wait (us), slept through */
+#define LDE_C_PIX_OVERFLOW 0
+#define LDE_C_PIX_OVERFLOW_CAP 1
+#define LDE_C_PIX_PREDICTED 2
+#define LDE_C_WAITS 3
+#define LDE_C_WAITS_BLOCKED 4
+#define LDE_C_WAIT_PRED_US 5
+int lde_counter(lde_handle *h, int32_t id, int64_t *value);
+
 /* Introspection for tests and reports. */
 int lde_info(lde_handle *h, int64_t *n_screen, int32_t *n_toa_bins, int64_t *staged,
              int32_t *tile_bits, int32_t *n_tiles, int64_t *events_binned,

@@ -104,4 +104,6 @@ def test_product_library_has_only_exact_sieve_variants():
     # the exact variants, and the keyed wavelength pass (262144)
     exact = {0, 256, 2048, 65536, 65536 | 256, 65536 | 2048, 65536 | 256 | 2048}
     log = 1 << 20  # log-linear TOA buckets (exact)
-    assert modes <= exact | {m | log for m in exact} | {262144}, modes
+    compact = 1 << 21  # cold keys compacted per lane (exact)
+    allowed = exact | {m | log for m in exact} | {262144}
+    assert modes <= allowed | {m | compact for m in allowed}, modes

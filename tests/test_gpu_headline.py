@@ -47,6 +47,10 @@ def test_bench_workload_bit_exact(workload):
 
 
 def _run(workload, dev):
+    """Three steps over three DIFFERENT batches (seeds 7, 8, 9, as the bench
+    rotates them), so LOKI's second and third batches run on slots predicted
+    from the previous, different batch: Poisson noise overflows some slots and
+    those groups take the overflow path."""
     import torch
 
     from esslivedata_amd import projection, synthetic
@@ -61,25 +65,28 @@ def _run(workload, dev):
                         n_screen=view.n_screen, device=0,
                         stream=torch.cuda.current_stream(dev).cuda_stream)
     n_step = N_PULSE * PULSES
-    seed = 7  # bench.py rank 0
-    if dream:
-        pid, toa = synthetic.torch_dream_events(n_step, inst, seed, dev)
-    else:
-        pid, toa = synthetic.torch_uniform_events(n_step, 1, 802816, seed, dev)
-    messages = [(pid[p * N_PULSE:(p + 1) * N_PULSE], toa[p * N_PULSE:(p + 1) * N_PULSE])
-                for p in range(PULSES)]
-    hp, ht = pid.cpu().numpy(), toa.cpu().numpy()
     ps = ora.geometric_pixel_screen(inst.coords, inst.resolution, flip_x=not dream)
     o = c_oracle.CDetectorView(inst.detector_number, ps, view.n_screen, edges,
                                threads=_threads())
     S, T = view.n_screen, len(edges) - 1
     lo, hi = 0, T
     prev = np.zeros(S * T, dtype=np.uint64)
-    for replica in (3, 4):  # bench warm-up steps 3 and 4 cycle i % R
+    overflow = []
+    for k, (seed, replica) in enumerate(((7, 3), (8, 4), (9, 0))):
+        if dream:
+            pid, toa = synthetic.torch_dream_events(n_step, inst, seed, dev)
+        else:
+            pid, toa = synthetic.torch_uniform_events(n_step, 1, 802816, seed, dev)
+        messages = [(pid[p * N_PULSE:(p + 1) * N_PULSE], toa[p * N_PULSE:(p + 1) * N_PULSE])
+                    for p in range(PULSES)]
         eng.stage_tensors_batch(messages)
         eng.accumulate(replica)
         res = eng.finalize(hists=True)
-        cum = o.accumulate(hp, ht, replica).copy()
+        if not dream:
+            assert eng.counter('pix_predicted') == (1 if k > 0 else 0)
+            overflow.append(eng.counter('pix_overflow'))
+        cum = o.accumulate(pid.cpu().numpy(), toa.cpu().numpy(), replica).copy()
+        del messages, pid, toa
         cur = (cum - prev).reshape(S, T)
         prev = cum
         cum = cum.reshape(S, T)
@@ -95,4 +102,9 @@ def _run(workload, dev):
         assert res.cumulative_total == int(cum.sum()) == res.cumulative_in_range
         # the count is a real fraction of the batch (LUT drops off-screen pixels only)
         assert res.current_total > 0.9 * n_step
+    if not dream:
+        # predicted slots of a fresh batch overflow (and stay exact)
+        assert overflow[0] == 0 and overflow[1] > 0 and overflow[2] > 0, overflow
+        # within the list's capacity: the fallback path is tested separately
+        assert max(overflow) < eng.counter('pix_overflow_cap')
     eng.close()

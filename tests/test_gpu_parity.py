@@ -46,6 +46,9 @@ VARIANTS = [
     {'LDE_SIEVE_TOA_LOG': '1'},
     {'LDE_SIEVE_TOA_LOG': '1', 'LDE_SIEVE_PACK': '1'},
     {'LDE_DEFER_STORES': '1'},
+    # cold keys compacted per lane (three ballots per half instead of per event)
+    {'LDE_SIEVE_COMPACT': '1'},
+    {'LDE_SIEVE_COMPACT': '1', 'LDE_SIEVE_PACK': '1'},
     # cold-key sorts: block-cooperative per-key stores, wave-independent,
     # 16-byte groups with 16 / 32 keys per thread (default: 16-byte groups, 48)
     {'LDE_COLD_SORT': '0'},
@@ -805,6 +808,9 @@ def test_loki_pixel_predicted_slots_exact_under_shifts(knobs):
 
 
 PIXEL_VARIANTS = [
+    # an overflow list of 16 groups: the overflow groups past it are added by
+    # pass A itself (global atomics), exactly
+    {'LDE_PIX_OVF_CAP': '16'},
     {},
     {'LDE_PIX_PRED': '0'},
     {'LDE_PIX24': '0'},
@@ -813,6 +819,9 @@ PIXEL_VARIANTS = [
     {'LDE_PIX_BU': '8'},
     {'LDE_PIX_ITEMS': '3'},
     {'LDE_PIX_MAX_RANGES': '512'},
+    # power-of-two ranges (196 of 4,096 pixels) / 200 ranges of 4,015 pixels
+    {'LDE_PIX_RANGES': '0'},
+    {'LDE_PIX_RANGES': '200'},
 ]
 
 
