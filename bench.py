@@ -208,6 +208,10 @@ def profiled_traffic(workload: str, kernel: str):
         'write': e['hbm_write_bytes'],
         'profiled_avg_ms': e['avg_ms'],
         'source': src,
+        # the committed profile's bench line, from the same traced run
+        'traced_line': (src.replace('_bench.json', '_traced_bench_line.json')
+                        if (ROOT / src.replace('_bench.json', '_traced_bench_line.json')).exists()
+                        else None),
     }
 
 
@@ -520,6 +524,10 @@ def main():
     prof_name = ('wavelength' if args.coordinate == 'wavelength' else
                  args.workload if args.view == 'geometric' else args.view)
     traffic = profiled_traffic(prof_name, dom)
+    if traffic is not None:
+        # per-dispatch tracing slows a kernel: the traced run's own line agrees
+        # with its profile; this untraced line records the difference
+        traffic['trace_overhead'] = traffic['profiled_avg_ms'] / max(ms / max(launches, 1), 1e-9) - 1.0
     bin_ms, bin_n = stats['binning']  # the extra steps
     n_acc = n_pulse if bifrost else n_step  # events one accumulate bins
     pipeline_gbs = bpe_step * n_acc / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0

@@ -199,6 +199,7 @@ struct lde_handle {
     bool early_gather = false;  // LDE_EARLY_GATHER
     bool sieve_pack = false;    // LDE_SIEVE_PACK
     bool lane_compact = false;  // LDE_SIEVE_COMPACT: cold keys compacted per lane
+    bool store_nt = false;      // LDE_SIEVE_STORE_NT: non-temporal cold-key stores
     int cold_sort_mode = 2;     // LDE_COLD_SORT: 0 block, 1 wave-independent, 2 16-byte groups
     int cold_sort_kpt = 48;     // LDE_COLD_SORT_KPT: keys per thread per piece of mode 2 (16, 32, 48)
     bool key24 = true;          // LDE_KEY24: 24-bit cold keys when S * T < 2^24 - 1
@@ -337,7 +338,8 @@ long long env_ll(const char *name, long long dflt) {
 // is exact); they are named once on stderr so a stray one is visible.
 int check_knobs() {
 #ifndef LDE_DIAGNOSTICS
-    static const char *const diag[] = {"LDE_ABLATE", "LDE_SIEVE_ABLATE", "LDE_COLD_SORT_ABLATE"};
+    static const char *const diag[] = {"LDE_ABLATE", "LDE_SIEVE_ABLATE", "LDE_COLD_SORT_ABLATE",
+                                       "LDE_PIX_ABLATE"};
     for (const char *n : diag)
         if (const char *v = std::getenv(n); v && std::atoll(v) != 0)
             return fail(nullptr, LDE_EINVAL,
@@ -1115,6 +1117,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         sa.early_gather = h->early_gather ? 1 : 0;
         sa.pack = h->sieve_pack ? 1 : 0;
         sa.lane_compact = h->lane_compact ? 1 : 0;
+        sa.store_nt = h->store_nt ? 1 : 0;
         // 24-bit cold keys need the 16-byte-group sort (the only reader)
         const bool key24 = pad8 && h->key24 && h->nbins < 0xFFFFFFLL;
         sa.key24 = key24 ? 1 : 0;
@@ -1289,8 +1292,7 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.pid_off = h->pid_off;
     a.L = (unsigned)h->L;
     a.rb = h->pix.rb;
-    a.rw = h->pix.rw;
-    a.rm = h->pix.rm;
+    a.ablate = (int)env_ll("LDE_PIX_ABLATE", 0);
     a.nr = h->pix.nr;
     a.rs = h->pix.rs;
     a.tab = h->d_tab;
@@ -1555,31 +1557,18 @@ int stage_pixel(lde_handle *h, const int32_t *lut, PixStaged &st) {
     if (h->monitor || h->n_tiles == 0 || env_ll("LDE_PIXEL", 1) == 0) return LDE_OK;
     const long long L = h->L, R = h->R, S = h->S;
     const int T = h->T;
-    // ranges of rw consecutive pixels, one per CU: pass B runs about one item
-    // per range, so every CU gets one (LOKI bank 0: 256 ranges of 3,136
-    // pixels instead of 196 of 4,096 on 196 CUs).  LDE_PIX_RANGES=0 (a
-    // diagnostics variant): the smallest power of two giving at most
-    // LDE_PIX_MAX_RANGES ranges (up to kPixMaxRanges)
+    // ranges of 2^rb pixels: the smallest rb with at most 256 ranges
+    // (LDE_PIX_MAX_RANGES, up to kPixMaxRanges; LOKI bank 0: 196 ranges of 4096
+    // pixels; 392 of 2048 keep the same 288-screen widest footprint, so pass B
+    // gains nothing and pass A's runs get shorter; 256 ranges of 3,136 pixels,
+    // one per CU by multiply-high, measured pass B -3.7 us and pass A +19 us)
     const long long max_nr = std::max<long long>(
         1, std::min<long long>(lde::kPixMaxRanges, env_ll("LDE_PIX_MAX_RANGES", 256)));
-    const long long want = std::min<long long>(max_nr, env_ll("LDE_PIX_RANGES", h->cus));
-    long long rw;
-    if (want > 0) {
-        rw = std::max<long long>(256, (L + want - 1) / want);
-    } else {
-        rw = 256;
-        while (rw < (1LL << 20) && (L + rw - 1) / rw > max_nr) rw *= 2;
-    }
     int rb = 8;
-    while ((1LL << rb) < rw) ++rb;
+    while (rb < 20 && ((L + (1LL << rb) - 1) >> rb) > max_nr) ++rb;
     int tbits = 0;
     while ((1 << tbits) < T) ++tbits;
-    const int nr = (int)((L + rw - 1) / rw);
-    if (nr > max_nr) return LDE_OK;
-    // q / rw as umulhi(q, rm), checked for every pixel
-    const uint32_t rm = (uint32_t)((1ULL << 32) / (unsigned long long)rw + 1);
-    for (long long q = 0; q < L; ++q)
-        if ((long long)(((unsigned long long)q * rm) >> 32) != q / rw) return LDE_OK;
+    const int nr = (int)((L + (1LL << rb) - 1) >> rb);
     // scatter staging word: range (rbits, the all-ones range never used) above
     // an rs-bit payload whose all-ones value is the dropped marker; stored
     // payloads are 24-bit (0xFFFFFF dropped), so local pixel | bin << rb
@@ -1593,7 +1582,7 @@ int stage_pixel(lde_handle *h, const int32_t *lut, PixStaged &st) {
     std::vector<uint16_t> loc((size_t)(R * L), 0xFFFF);
     int fmax = 0;
     for (int r = 0; r < nr; ++r) {
-        const long long q0 = (long long)r * rw, q1 = std::min(L, q0 + rw);
+        const long long q0 = (long long)r << rb, q1 = std::min(L, q0 + (1LL << rb));
         const size_t first = fp.size();
         for (long long rep = 0; rep < R; ++rep)
             for (long long q = q0; q < q1; ++q) {
@@ -1631,8 +1620,6 @@ int stage_pixel(lde_handle *h, const int32_t *lut, PixStaged &st) {
         if (int rc = dev_alloc(h, &h->d_pitem_count, 1)) return rc;
     }
     st.pix.rb = rb;
-    st.pix.rw = (uint32_t)rw;
-    st.pix.rm = rm;
     st.pix.nr = nr;
     st.pix.rs = rs;
     st.pix.fmax = fmax;
@@ -1674,8 +1661,8 @@ void commit_pixel(lde_handle *h, PixStaged &st) {
     h->pix.fp_off = h->d_pfp_off;
     h->pix.fp_scr = h->d_pfp_scr;
     if (env_ll("LDE_VERBOSE", 0))
-        fprintf(stderr, "lde pixel: %d ranges of %u pixels, widest footprint %d screens (%zu B LDS)\n",
-                h->pix.nr, h->pix.rw, h->pix.fmax, lde::pix_acc_smem(h->pix.rb, h->pix.fmax, h->T));
+        fprintf(stderr, "lde pixel: %d ranges of 2^%d pixels, widest footprint %d screens (%zu B LDS)\n",
+                h->pix.nr, h->pix.rb, h->pix.fmax, lde::pix_acc_smem(h->pix.rb, h->pix.fmax, h->T));
 }
 
 int build_pixel(lde_handle *h, const int32_t *lut) {
@@ -2195,6 +2182,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->probe = env_ll("LDE_HOST_PROBE", 0) != 0;
         h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
         h->lane_compact = env_ll("LDE_SIEVE_COMPACT", 0) != 0;
+        h->store_nt = env_ll("LDE_SIEVE_STORE_NT", 0) != 0;
         h->cold_sort_mode = (int)env_ll("LDE_COLD_SORT", 2);
         {
             const long long k = env_ll("LDE_COLD_SORT_KPT", 48);

@@ -196,6 +196,7 @@ struct SieveArgs {
     int karg;                    // lds_ctab: descriptors from sk (else from segs)
     int early_gather;            // 1: gathers issued one iteration before they are binned
     int lane_compact = 0;        // 1: cold keys compacted per lane (three ballots per half)
+    int store_nt = 0;            // 1: cold-key stores non-temporal
     int pack;                    // 1: TOA bin packed into the table word at the gather
     SegKarg sk;                  // lds_ctab: the message descriptors (n_segs <= kKargSegs)
     const int *dummy;            // the all-invalid chunk
@@ -393,8 +394,7 @@ struct PixArgs {
     long long n_chunks;
     int pid_off;
     unsigned L;
-    int rb;                      // local pixel bits (2^rb >= rw)
-    uint32_t rw = 0, rm = 0;     // range of pixel q: q / rw = umulhi(q, rm)
+    int rb;                      // range of pixel q: q >> rb
     int nr;                      // ranges (<= kPixMaxRanges)
     int rs;                      // scatter staging word: range << rs | payload (rs bits)
     const unsigned char *tab;    // TOA lookup image
@@ -422,10 +422,10 @@ struct PixArgs {
     const uint32_t *ovf_fp_off = nullptr;  // [nr + 1]
     const uint32_t *ovf_fp_scr = nullptr;
     uint32_t *ovf_hist = nullptr;          // the window
+    int ablate = 0;              // LDE_PIX_ABLATE (diagnostics build): 1 no payload stores
 };
 struct PixSetup {                // setup-time tables (lde_create / lde_set_lut)
     int rb = 0, nr = 0, fmax = 0, rs = 24;
-    uint32_t rw = 0, rm = 0;           // range width (pixels) and its multiply-high reciprocal
     const uint16_t *loc = nullptr;     // [R][L] footprint-local screen of every pixel (0xFFFF: dropped)
     const uint32_t *fp_off = nullptr;  // [nr + 1] footprint list offsets
     const uint32_t *fp_scr = nullptr;  // footprint screens, range after range

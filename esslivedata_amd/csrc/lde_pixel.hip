@@ -119,12 +119,6 @@ __device__ __forceinline__ int pix_toa_bin(int t, const unsigned char *s_tab, co
     return FAST ? toa_bin_nb(t, s_tab, tp) : toa_bin<false>(t, s_tab, tp);
 }
 
-// pixel range of local pixel index q: q / rw by multiply-high (rm =
-// floor(2^32 / rw) + 1, checked exact for every q < L at setup)
-__device__ __forceinline__ uint32_t pix_range(const PixArgs &a, uint32_t q) {
-    return __umulhi(q, a.rm);
-}
-
 __device__ __forceinline__ void block_units(long long n, long long &cb, long long &ce) {
     cb = (long long)blockIdx.x * n / gridDim.x;
     ce = ((long long)blockIdx.x + 1) * n / gridDim.x;
@@ -190,7 +184,7 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_count(PixArgs a) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t q = (uint32_t)p[e] - (uint32_t)a.pid_off;
-            if (q < a.L) atomicAdd(&s_cnt[pix_range(a, q)], 1u);
+            if (q < a.L) atomicAdd(&s_cnt[q >> a.rb], 1u);
         }
         __syncthreads();
         for (int r = threadIdx.x; r < a.nr; r += NT) {
@@ -270,8 +264,7 @@ size_t pix_scatter_smem(const ToaParams &tp, int unit) {
 __device__ __forceinline__ void pix_add_group(const uint16_t *__restrict__ loc,
                                               const uint32_t *__restrict__ fp_off,
                                               const uint32_t *__restrict__ fp_scr, int T,
-                                              uint32_t *__restrict__ hist, int rs, int rb, uint32_t rw,
-                                              uint4 w);
+                                              uint32_t *__restrict__ hist, int rs, int rb, uint4 w);
 
 template <int U, int E, bool P24, bool FAST>
 __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
@@ -295,6 +288,7 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
         s_end[r] = a.rstart[r] + ((int)blockIdx.x + 1 < a.grid ? a.counts[(size_t)(blockIdx.x + 1) * a.nr + r]
                                                                : rtot[r]);
     }
+    const uint32_t mask = (1u << a.rb) - 1u;
     // staging word: range << rs | payload (rs bits, all ones = dropped); the
     // stored payloads are 24-bit with 0xFFFFFF = dropped
     const uint32_t dmask = (1u << a.rs) - 1u;
@@ -312,8 +306,8 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
         for (int e = 0; e < E; ++e) {
             const uint32_t q = (uint32_t)p[e] - (uint32_t)a.pid_off;
             const int b = pix_toa_bin<FAST>(t[e], s_tab, a.tp);
-            const uint32_t r = pix_range(a, q);
-            word[e] = q < a.L ? ((r << a.rs) | (b < 0 ? dmask : ((q - r * a.rw) | ((uint32_t)b << a.rb))))
+            const uint32_t r = q >> a.rb;
+            word[e] = q < a.L ? ((r << a.rs) | (b < 0 ? dmask : ((q & mask) | ((uint32_t)b << a.rb))))
                               : 0xFFFFFFFFu;  // unknown id: no slot
             if (q < a.L) atomicAdd(&s_cnt[r], 1u);
             asm volatile("" : "+v"(word[e]));  // materialized here, not recomputed after the scan
@@ -348,7 +342,7 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
             };
             const uint32_t dst = s_cur[r] + (g - s_off[r]);
             const bool fits = dst < s_end[r];  // always, with exact slots
-            if (fits) {
+            if (fits && !(LDE_DIAG(a.ablate) & 1)) {
                 if (P24) {
                     *(g_v3u *)(reinterpret_cast<unsigned char *>(a.payload) + (size_t)dst * 3u) =
                         pack24(pl(w.x), pl(w.y), pl(w.z), pl(w.w));
@@ -373,7 +367,7 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
                         // the list is full (a stream far off its prediction):
                         // this group's events go straight to the window
                         pix_add_group(a.ovf_loc, a.ovf_fp_off, a.ovf_fp_scr, a.tp.T, a.ovf_hist,
-                                      a.rs, a.rb, a.rw, w);
+                                      a.rs, a.rb, w);
                     }
                 }
             }
@@ -410,15 +404,14 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
 __device__ __forceinline__ void pix_add_group(const uint16_t *__restrict__ loc,
                                               const uint32_t *__restrict__ fp_off,
                                               const uint32_t *__restrict__ fp_scr, int T,
-                                              uint32_t *__restrict__ hist, int rs, int rb, uint32_t rw,
-                                              uint4 w) {
+                                              uint32_t *__restrict__ hist, int rs, int rb, uint4 w) {
     const uint32_t dmask = (1u << rs) - 1u, mask = (1u << rb) - 1u;
     const uint32_t x[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t r = x[q] >> rs, v = x[q] & dmask;
         if (v == dmask) continue;  // pad or TOA outside the edges
-        const uint32_t f = loc[r * rw + (v & mask)];
+        const uint32_t f = loc[(r << rb) | (v & mask)];
         if (f != 0xFFFFu) atomicAdd(&hist[(size_t)fp_scr[fp_off[r] + f] * T + (v >> rb)], 1u);
     }
 }
@@ -432,7 +425,7 @@ __device__ __forceinline__ void pix_overflow(const PixArgs &a, const uint16_t *_
     const uint32_t n0 = *a.ovf;
     const uint32_t n = n0 < a.ovf_cap ? n0 : a.ovf_cap;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        pix_add_group(loc, fp_off, fp_scr, T, hist, a.rs, a.rb, a.rw, a.ovf_grp[i]);
+        pix_add_group(loc, fp_off, fp_scr, T, hist, a.rs, a.rb, a.ovf_grp[i]);
 }
 
 // LDS: LUT slice (2^rb u16) | footprint counters (F x T u32) | 64 dummies
@@ -456,12 +449,12 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
     const uint32_t r = it.x;
     const uint32_t f0 = fp_off[r], nf = fp_off[r + 1] - f0;
     const uint32_t nbin = nf * (uint32_t)T;
-    const uint32_t span = 1u << a.rb;  // >= rw; slots past the range read as dropped
+    const uint32_t span = 1u << a.rb;
     uint16_t *s_loc = reinterpret_cast<uint16_t *>(smem);
     uint32_t *s_cnt = reinterpret_cast<uint32_t *>(smem + align16((size_t)2 << a.rb));
-    const size_t q0 = (size_t)r * a.rw;
+    const size_t q0 = (size_t)r << a.rb;
     for (uint32_t j = threadIdx.x; j < span; j += blockDim.x)
-        s_loc[j] = j < a.rw && q0 + j < a.L ? loc[q0 + j] : (uint16_t)0xFFFFu;
+        s_loc[j] = q0 + j < a.L ? loc[q0 + j] : (uint16_t)0xFFFFu;
     for (uint32_t j = threadIdx.x; j < nbin; j += blockDim.x) s_cnt[j] = 0;
     const uint32_t mask = span - 1u;
     // events the view drops and pads count into a lane-private dummy word

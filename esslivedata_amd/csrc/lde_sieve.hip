@@ -52,6 +52,7 @@ constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (ha
 constexpr int kSieveKeyed = 262144;           // mode bit: the stream holds finished words
 constexpr int kSieveToaLog = 1 << 20;         // mode bit: log-linear TOA buckets
 constexpr int kSieveLaneCompact = 1 << 21;    // mode bit: cold keys compacted per lane
+constexpr int kSieveStoreNT = 1 << 22;        // mode bit: cold-key stores non-temporal (nt)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
@@ -258,12 +259,14 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                              (size_t)blockIdx.x * (size_t)(a.cold_cap + kSplitThreads / 64) * kbytes;
     const __amdgpu_buffer_rsrc_t cold = make_rsrc(my_cold, (uint32_t)a.cold_cap * kbytes);
     // one lane's four keys: offset = key index * 4 (kOOB: discarded)
+    // (kSieveStoreNT: aux 2 = nt, streamed past L2's normal replacement)
+    constexpr int kStoreAux = (ABL & kSieveStoreNT) ? 2 : 0;
     auto store_keys = [&](v4u kv, uint32_t off) __attribute__((always_inline)) {
         if (a.key24)
             __builtin_amdgcn_raw_buffer_store_b96(pack_keys24(kv), cold,
-                                                  (int)(off == kOOB ? kOOB : (off >> 2) * 3u), 0, 0);
+                                                  (int)(off == kOOB ? kOOB : (off >> 2) * 3u), 0, kStoreAux);
         else
-            __builtin_amdgcn_raw_buffer_store_b128(kv, cold, (int)off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(kv, cold, (int)off, 0, kStoreAux);
     };
     const uint32_t cmask = C - 1u;
     const uint32_t pid_off = (uint32_t)a.pid_off;
@@ -1603,7 +1606,8 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     const int mode = a.keyed ? kSieveKeyed | (a.lane_compact ? kSieveLaneCompact : 0)
                              : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0) |
                                    (a.toa_log ? kSieveToaLog : 0) |
-                                   (a.lane_compact ? kSieveLaneCompact : 0);
+                                   (a.lane_compact ? kSieveLaneCompact : 0) |
+                                   (a.store_nt ? kSieveStoreNT : 0);
     switch (mode) {
 #define LDE_SIEVE_MODE(m) \
     case m: return launch_sieve_t<m>(a, grid, st, start, stop);
@@ -1619,6 +1623,8 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     // per-lane cold-key compaction
     LDE_SIEVE_MODE(kSieveLaneCompact) LDE_SIEVE_MODE(kSieveLaneCompact | 65536)
     LDE_SIEVE_MODE(kSieveLaneCompact | kSieveKeyed) LDE_SIEVE_MODE(kSieveLaneCompact | kSieveToaLog)
+    // non-temporal cold-key stores
+    LDE_SIEVE_MODE(kSieveStoreNT) LDE_SIEVE_MODE(kSieveStoreNT | kSieveLaneCompact)
 #ifdef LDE_DIAGNOSTICS
     // timing probes (wrong results), diagnostics build only
     LDE_SIEVE_MODE(1) LDE_SIEVE_MODE(2) LDE_SIEVE_MODE(4) LDE_SIEVE_MODE(6)

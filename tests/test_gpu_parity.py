@@ -819,9 +819,6 @@ PIXEL_VARIANTS = [
     {'LDE_PIX_BU': '8'},
     {'LDE_PIX_ITEMS': '3'},
     {'LDE_PIX_MAX_RANGES': '512'},
-    # power-of-two ranges (196 of 4,096 pixels) / 200 ranges of 4,015 pixels
-    {'LDE_PIX_RANGES': '0'},
-    {'LDE_PIX_RANGES': '200'},
 ]
 
 

@@ -7,8 +7,8 @@ mkdir -p gpurun_out/profiles
 TAG=${TAG:-r3}
 prof() {  # name workload bench-args
   TAG=$TAG NAME=$1 WL=$2 BENCH_ARGS="$3" bash tools/prof_round.sh > gpurun_out/prof_$1.log 2>&1 || { echo "prof $1 failed"; tail -20 gpurun_out/prof_$1.log; exit 1; }
-  cp gpurun_out/prof_${TAG}_$1/${TAG}_$1_bench.json gpurun_out/prof_${TAG}_$1/${TAG}_$1_bench_kernel_stats.csv gpurun_out/profiles/ || exit 1
-  cp gpurun_out/profiles/${TAG}_$1_bench.json gpurun_out/profiles/${TAG}_$1_bench_kernel_stats.csv profiles/ || exit 1
+  cp gpurun_out/prof_${TAG}_$1/${TAG}_$1_bench.json gpurun_out/prof_${TAG}_$1/${TAG}_$1_bench_kernel_stats.csv gpurun_out/prof_${TAG}_$1/${TAG}_$1_traced_bench_line.json gpurun_out/profiles/ || exit 1
+  cp gpurun_out/profiles/${TAG}_$1_bench.json gpurun_out/profiles/${TAG}_$1_bench_kernel_stats.csv gpurun_out/profiles/${TAG}_$1_traced_bench_line.json profiles/ || exit 1
 }
 if [ -z "$SKIP_PROF" ]; then
   prof dream dream ""
