@@ -1293,6 +1293,7 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.L = (unsigned)h->L;
     a.rb = h->pix.rb;
     a.ablate = (int)env_ll("LDE_PIX_ABLATE", 0);
+    a.pf2 = env_ll("LDE_PIX_PF2", 0) != 0 ? 1 : 0;
     a.nr = h->pix.nr;
     a.rs = h->pix.rs;
     a.tab = h->d_tab;

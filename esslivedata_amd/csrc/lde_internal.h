@@ -423,6 +423,7 @@ struct PixArgs {
     const uint32_t *ovf_fp_scr = nullptr;
     uint32_t *ovf_hist = nullptr;          // the window
     int ablate = 0;              // LDE_PIX_ABLATE (diagnostics build): 1 no payload stores
+    int pf2 = 0;                 // two units of events in flight per block (LDE_PIX_PF2)
 };
 struct PixSetup {                // setup-time tables (lde_create / lde_set_lut)
     int rb = 0, nr = 0, fmax = 0, rs = 24;

@@ -266,7 +266,7 @@ __device__ __forceinline__ void pix_add_group(const uint16_t *__restrict__ loc,
                                               const uint32_t *__restrict__ fp_scr, int T,
                                               uint32_t *__restrict__ hist, int rs, int rb, uint4 w);
 
-template <int U, int E, bool P24, bool FAST>
+template <int U, int E, bool P24, bool FAST, bool PF2>
 __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     constexpr int NT = U * kChunk / E;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -295,9 +295,10 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     long long cb, ce;
     block_units((a.n_chunks + U - 1) / U, cb, ce);
     const PixChunk *s_ct = block_chunk_table<U>(a, s_ctab, cb, ce);  // (+ the barrier for s_cnt, s_cur)
-    int p[E], t[E];
-    if (cb < ce) unit_load<U, E, true>(a, s_ct, cb * U, cb, p, t);
-    for (long long c = cb; c < ce; ++c) {
+    // D units of events in flight (PF2: two register sets, A and B, used by
+    // alternate units, so a unit's loads have two units' work to arrive)
+    constexpr long long D = PF2 ? 2 : 1;
+    auto unit = [&](long long c, int (&p)[E], int (&t)[E]) __attribute__((always_inline)) {
         // pass 1: the events' words and their ranges' counts; only the words
         // stay live across the scan (registers: the next unit's loads are in
         // flight at the same time), pass 2 takes the slots
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
         // the next unit's events load while this one is partitioned (not
         // hoisted above the words: both sets live would double the registers)
         __builtin_amdgcn_sched_barrier(0);
-        if (c + 1 < ce) unit_load<U, E, true>(a, s_ct, cb * U, c + 1, p, t);
+        if (c + D < ce) unit_load<U, E, true>(a, s_ct, cb * U, c + D, p, t);
         __syncthreads();
         // runs padded to 4: staging offsets, slot cursors and the pads are
         // whole groups
@@ -378,6 +379,18 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
             s_cnt[r] = 0;
         }
         __syncthreads();
+        };
+    int pA[E], tA[E];
+    if (cb < ce) unit_load<U, E, true>(a, s_ct, cb * U, cb, pA, tA);
+    if (PF2) {
+        int pB[E], tB[E];
+        if (cb + 1 < ce) unit_load<U, E, true>(a, s_ct, cb * U, cb + 1, pB, tB);
+        for (long long c = cb; c < ce; c += 2) {
+            unit(c, pA, tA);
+            if (c + 1 < ce) unit(c + 1, pB, tB);
+        }
+    } else {
+        for (long long c = cb; c < ce; ++c) unit(c, pA, tA);
     }
     // this batch's run totals (the next batch's prediction), then each slot's
     // unused tail as dropped groups, one wave per range
@@ -536,14 +549,14 @@ void launch_pass_a(const PixArgs &a, uint32_t item_events, int max_items, uint4 
     hipLaunchKernelGGL(k_pix_scan, dim3(1), dim3(1024), 0, st, a, a.rstart + a.nr + 1, item_events,
                        items, item_count, max_items);
     const size_t sm = pix_scatter_smem(a.tp, U);
+    auto go = [&](auto kern) {
+        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL(kern, dim3(a.grid), dim3(NT), sm, st, a);
+    };
     if (a.tp.fast) {
-        (void)hipFuncSetAttribute((const void *)k_pix_scatter<U, E, P24, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL((k_pix_scatter<U, E, P24, true>), dim3(a.grid), dim3(NT), sm, st, a);
+        if (a.pf2) go(k_pix_scatter<U, E, P24, true, true>); else go(k_pix_scatter<U, E, P24, true, false>);
     } else {
-        (void)hipFuncSetAttribute((const void *)k_pix_scatter<U, E, P24, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL((k_pix_scatter<U, E, P24, false>), dim3(a.grid), dim3(NT), sm, st, a);
+        if (a.pf2) go(k_pix_scatter<U, E, P24, false, true>); else go(k_pix_scatter<U, E, P24, false, false>);
     }
 }
 template <bool P24>

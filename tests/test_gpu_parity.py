@@ -808,6 +808,8 @@ def test_loki_pixel_predicted_slots_exact_under_shifts(knobs):
 
 
 PIXEL_VARIANTS = [
+    # two units of events in flight per partition block
+    {'LDE_PIX_PF2': '1'},
     # an overflow list of 16 groups: the overflow groups past it are added by
     # pass A itself (global atomics), exactly
     {'LDE_PIX_OVF_CAP': '16'},
