@@ -206,7 +206,7 @@ def profiled_traffic(workload: str, kernel: str):
         'bytes': e['hbm_traffic_bytes'],
         'read': e['hbm_read_bytes'],
         'write': e['hbm_write_bytes'],
-        'profiled_avg_ms': e['avg_ms'],
+        'profiled_avg_ms': e.get('avg_ms_steady', e['avg_ms']),
         'source': src,
         # the committed profile's bench line, from the same traced run
         'traced_line': (src.replace('_bench.json', '_traced_bench_line.json')

@@ -30,6 +30,7 @@
 
 #include "../../include/lde.h"
 #include "lde_internal.h"
+#include "lde_window.h"
 
 namespace {
 
@@ -136,6 +137,12 @@ struct lde_handle {
     std::vector<int> hot_uses;         // per replica: -1 = not selected yet
     std::vector<double> hot_cov;
     std::vector<char> all_hot;         // per replica: every screen has a hot row
+    // SIEVE hot rows per replica: count, TOA window [lo, lo + w) (w = T: whole
+    // rows), chosen at each selection from the sampled TOA histogram
+    std::vector<int> hot_h, hot_w, hot_lo;
+    std::vector<double> hot_win;       // sampled fraction of events inside the window
+    size_t sieve_budget = 0;           // LDS bytes of one sieve block
+    uint32_t *d_toa_hist = nullptr, *h_toa_hist = nullptr, *h_screen_cnt = nullptr;
     uint32_t *d_hot_part = nullptr;
     size_t hot_part_cap = 0;
     uint32_t *d_cold = nullptr;
@@ -198,8 +205,6 @@ struct lde_handle {
     int sieve_ablate = 0;
     bool early_gather = false;  // LDE_EARLY_GATHER
     bool sieve_pack = false;    // LDE_SIEVE_PACK
-    bool lane_compact = false;  // LDE_SIEVE_COMPACT: cold keys compacted per lane
-    bool store_nt = false;      // LDE_SIEVE_STORE_NT: non-temporal cold-key stores
     int cold_sort_mode = 2;     // LDE_COLD_SORT: 0 block, 1 wave-independent, 2 16-byte groups
     int cold_sort_kpt = 48;     // LDE_COLD_SORT_KPT: keys per thread per piece of mode 2 (16, 32, 48)
     bool key24 = true;          // LDE_KEY24: 24-bit cold keys when S * T < 2^24 - 1
@@ -910,6 +915,59 @@ bool coord_keyed_candidate(const lde_handle *h, long long total) {
 // coord_deferred (wavelength mode): `sd` still holds times; the sieve path
 // runs the keyed coordinate pass, the k_split path the plain one (and `sd`
 // is updated to the bin stream).
+// SIEVE hot rows with a TOA window: a row holds bins [lo, lo + w) of its
+// screen, so narrower rows fit more screens into the same LDS.  Worth it when
+// the stream's TOA bins concentrate (DREAM: 99.8 % of the events in the top
+// 60 of 100 geometric bins, so 386 rows of 55-60 bins instead of 232 whole
+// rows: 78 % instead of 75 % of the events hot).  Views where every screen
+// can have a whole row, and wavelength mode (the keyed pass folds the bin
+// into the word), keep whole rows.
+// Measured on DREAM (4 interleaved runs, one box): 396-403 rows of bins
+// [40, 97-98) instead of 232 whole rows, 78 % instead of 75 % of the events
+// hot, cold path 0.0945 -> 0.0909 ms, sieve +1.2 us (the window test), step
+// +-0: off by default (LDE_HOT_WINDOW=1, diagnostics build; exact, in the
+// parity matrix).
+bool window_candidate(const lde_handle *h) {
+    return h->sieve_ok && !h->coord && h->d_toa_hist && h->S > h->hot_rows &&
+           env_ll("LDE_HOT_WINDOW", 0) != 0;
+}
+
+// the most rows of w bins (window starting at lo) the sieve block's LDS holds
+int window_rows(const lde_handle *h, int w, int lo) {
+    int a = 0, b = (int)std::min<long long>(lde::kHotMaxRows, h->S);
+    const long long cap = env_ll("LDE_HOT_ROWS", 0);  // diagnostics: a row budget
+    if (cap > 0) b = (int)std::min<long long>(b, cap);
+    auto fits = [&](int H) {
+        return lde::sieve_smem((lo + H * w + 7) & ~7, h->cache_bits, (int)h->ttab.size(), h->n_tiles,
+                               w == h->T ? 0 : H) <= h->sieve_budget;
+    };
+    if (fits(b)) return b;
+    while (a + 1 < b) {  // fits(a) (0 rows always fits), !fits(b)
+        const int m = (a + b) / 2;
+        if (fits(m)) a = m; else b = m;
+    }
+    return a;
+}
+
+// Host choice from this replica's sample (h_screen_cnt, h_toa_hist): the
+// window width w and start lo that maximize the sampled hot fraction
+// (top-H screens' share x the window's share of the TOA bins), against whole
+// rows; only a gain of at least 0.5 % of the events changes the rows.  Exact
+// whatever the choice (hot events outside the window leave as cold keys).
+void choose_window(lde_handle *h, int r) {
+    const lde::HotWindow c = lde::choose_hot_window(
+        h->h_screen_cnt, h->S, h->h_toa_hist, h->T, h->hot_rows,
+        [h](int w, int lo) { return window_rows(h, w, lo); });
+    h->hot_h[(size_t)r] = c.rows;
+    h->hot_w[(size_t)r] = c.w;
+    h->hot_lo[(size_t)r] = c.lo;
+    h->hot_win[(size_t)r] = c.win;
+    if (env_ll("LDE_VERBOSE", 0))
+        fprintf(stderr, "lde split: replica %d window: %d rows of bins [%d, %d) (%.4f of the sampled times), "
+                        "estimated hot %.3f\n",
+                r, c.rows, c.lo, c.lo + c.w, c.win, c.est);
+}
+
 int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
               long long total, int replica, bool forced, bool coord_deferred) {
     // the descriptor table is uploaded lazily: the SIEVE pass of a batch of
@@ -965,12 +1023,30 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             b.hlut = h->d_hlut + (size_t)h->L * r;
             b.pix_tab = h->d_pix_tab + ((size_t)r << h->cache_bits);
             Timed tm(h, LDE_K_SPLIT_AUX);
-            HIPCALL(h, lde::launch_hot_select(b, r, h->stream));
+            const bool window = window_candidate(h);
+            HIPCALL(h, lde::launch_hot_sample(b, r, window ? h->d_toa_hist : nullptr, h->stream));
+            if (window) {
+                // the host sizes this replica's rows from the sample (one sync
+                // per selection, i.e. per replica every hot_refresh batches)
+                HIPCALL(h, hipMemcpyAsync(h->h_screen_cnt, h->d_screen_cnt, (size_t)h->S * 4,
+                                          hipMemcpyDeviceToHost, h->stream));
+                HIPCALL(h, hipMemcpyAsync(h->h_toa_hist, h->d_toa_hist, (size_t)h->T * 4,
+                                          hipMemcpyDeviceToHost, h->stream));
+                HIPCALL(h, hipStreamSynchronize(h->stream));
+                choose_window(h, r);
+            } else {
+                h->hot_h[(size_t)r] = h->hot_rows;
+                h->hot_w[(size_t)r] = h->T;
+                h->hot_lo[(size_t)r] = 0;
+                h->hot_win[(size_t)r] = 1.0;
+            }
+            b.rows = h->hot_h[(size_t)r];
+            HIPCALL(h, lde::launch_hot_pick(b, r, h->stream));
             if (h->sieve_ok)
                 HIPCALL(h, lde::launch_sieve_tables(
                                (const unsigned char *)h->d_lut + (size_t)r * h->L * (h->lut16 ? 2 : 4),
-                               h->lut16, h->L, h->T, h->d_screen_row, h->d_pix_cnt, h->cache_bits,
-                               h->d_glut + (size_t)(h->L + 1) * r,
+                               h->lut16, h->L, h->T, h->hot_w[(size_t)r], h->d_screen_row, h->d_pix_cnt,
+                               h->cache_bits, h->d_glut + (size_t)(h->L + 1) * r,
                                h->d_sieve_tab + ((size_t)r << h->cache_bits), h->stream));
         }
         if (h->coord && h->d_pix_cnt) {
@@ -992,12 +1068,13 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         for (int r : todo) {
             const uint32_t *st = h->h_sel_stats + 4 * r;
             const double sampled = (double)st[0];
-            h->hot_cov[(size_t)r] = sampled > 0 ? (double)st[1] / sampled : 0.0;
+            h->hot_cov[(size_t)r] = sampled > 0 ? (double)st[1] / sampled * h->hot_win[(size_t)r] : 0.0;
             h->all_hot[(size_t)r] = st[2] == (uint32_t)h->S ? 1 : 0;
             h->hot_uses[(size_t)r] = 0;
             if (env_ll("LDE_VERBOSE", 0))
-                fprintf(stderr, "lde split: replica %d sampled %u, hot rows %u cover %.3f, pixel table covers %.3f\n",
-                        r, st[0], st[2], h->hot_cov[(size_t)r],
+                fprintf(stderr, "lde split: replica %d sampled %u, hot rows %u (bins %d..%d) cover %.3f, pixel table covers %.3f\n",
+                        r, st[0], st[2], h->hot_lo[(size_t)r], h->hot_lo[(size_t)r] + h->hot_w[(size_t)r] - 1,
+                        h->hot_cov[(size_t)r],
                         sampled > 0 && h->cache_bits ? (double)st[3] / sampled : 0.0);
         }
     }
@@ -1011,7 +1088,8 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
     const long long per_block = (chunks + a.grid - 1) / a.grid;
     // SIEVE reserves cold slots in multiples of 4 per wave and half chunk
     a.cold_cap = per_block * (lde::kChunk + (h->sieve_ok ? 4 * 2 * (lde::kSplitThreads / 64) : 0));
-    const int ht4 = lde::align4(h->hot_rows * h->T);
+    const int hr = h->hot_h[replica], hw = h->hot_w[replica], hlo = h->hot_lo[replica];
+    const int ht4 = (hlo + hr * hw + 7) & ~7;  // multiple of 8: u16 hot-row flush
     if (int rc = grow(h, &h->d_hot_part, h->hot_part_cap, (size_t)a.grid * ht4)) return rc;
     if (int rc = grow(h, &h->d_cold, h->cold_total_cap,
                       (size_t)a.grid * (size_t)(a.cold_cap + lde::kSplitThreads / 64)))
@@ -1021,6 +1099,9 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
     a.cold = h->d_cold;
     a.cold_cnt = h->d_cold_cnt;
     const bool sieve = h->sieve_ok && (unsigned long long)a.cold_cap * 4ULL < 0x80000000ULL;
+    // windowed rows exist only on the SIEVE path; the rare batch too large for
+    // its cold regions takes PAGED (exact) rather than whole-row k_split
+    if (!sieve && hw != h->T) return 1;
     if (sieve) {
         if (int rc = grow(h, &h->d_chunk_tab, h->chunk_tab_cap, (size_t)chunks + 1)) return rc;
         const size_t nt = (size_t)h->n_tiles;
@@ -1106,6 +1187,11 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         sa.pix_tab = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
         sa.cbits = h->cache_bits;
         sa.hot_words = ht4;
+        sa.hot_lo = hlo;
+        sa.hot_w = hw;
+        sa.hot_rows = hr;
+        sa.hot_inv_w = 1.0f / (float)hw;
+        sa.row_screen = a.row_screen;
         sa.hot_part = h->d_hot_part;
         sa.cold = h->d_cold;
         sa.cold_cap = a.cold_cap;
@@ -1116,8 +1202,6 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         sa.ablate = h->sieve_ablate;
         sa.early_gather = h->early_gather ? 1 : 0;
         sa.pack = h->sieve_pack ? 1 : 0;
-        sa.lane_compact = h->lane_compact ? 1 : 0;
-        sa.store_nt = h->store_nt ? 1 : 0;
         // 24-bit cold keys need the 16-byte-group sort (the only reader)
         const bool key24 = pad8 && h->key24 && h->nbins < 0xFFFFFFLL;
         sa.key24 = key24 ? 1 : 0;
@@ -1193,7 +1277,9 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         lde::ColdArgs c;
         c.hot_part = h->d_hot_part;
         c.row_screen = a.row_screen;
-        c.ht = h->hot_rows * h->T;
+        c.ht = hlo + hr * hw;
+        c.hot_lo = hlo;
+        c.hot_w = hw;
         c.ht4 = ht4;
         c.T = h->T;
         c.tile_bits = h->tile_bits;
@@ -1790,6 +1876,9 @@ void release(lde_handle *h) {
     dev_free(h->d_screen_cnt);
     dev_free(h->d_screen_row);
     if (h->h_sel_stats) (void)hipHostFree(h->h_sel_stats);
+    dev_free(h->d_toa_hist);
+    if (h->h_toa_hist) (void)hipHostFree(h->h_toa_hist);
+    if (h->h_screen_cnt) (void)hipHostFree(h->h_screen_cnt);
     dev_free(h->d_hot_part);
     dev_free(h->d_cold);
     dev_free(h->d_cold_cnt);
@@ -2077,7 +2166,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 if (h->S <= lde::kHotMaxRows && build_sieve_toa(h->tp, tab, tt0, tsh0, tcap0, &log0)) {
                     if (tt0.size() < (size_t)lde::align4(h->T + 2)) tt0.resize((size_t)lde::align4(h->T + 2), 0u);
                     auto sieve_fits_all = [&](int cb) {
-                        return lde::sieve_smem(lde::align4((int)h->S * h->T), cb, (int)tt0.size(), h->n_tiles) <= budget;
+                        return lde::sieve_smem(lde::align4((int)h->S * h->T), cb, (int)tt0.size(), h->n_tiles, 0) <= budget;
                     };
                     if (cbits > 0 && !sieve_fits_all(cbits) && env_ll("LDE_ALL_HOT", 1) != 0)
                         for (int cb = cbits - 1; cb >= 10; --cb)
@@ -2110,10 +2199,11 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                     // 0..T: T + 1 bucket words), so lde_set_coord_lut keeps the sieve
                     if (tt.size() < (size_t)lde::align4(h->T + 2)) tt.resize((size_t)lde::align4(h->T + 2), 0u);
                     int Hs = 0;
-                    const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size(), h->n_tiles);
+                    // whole rows: no row -> screen table (sieve_smem's last argument)
+                    const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size(), h->n_tiles, 0);
                     if (fixed < budget)
                         Hs = (int)std::min<long long>(lde::kHotMaxRows, (long long)((budget - fixed) / (4 * (size_t)h->T)));
-                    while (Hs > 0 && lde::sieve_smem(lde::align4(Hs * h->T), cbits, (int)tt.size(), h->n_tiles) > budget) --Hs;
+                    while (Hs > 0 && lde::sieve_smem(lde::align4(Hs * h->T), cbits, (int)tt.size(), h->n_tiles, 0) > budget) --Hs;
                     Hs = (int)std::min<long long>(Hs, h->S);
                     if (hmax > 0) Hs = (int)std::min<long long>(Hs, hmax);
                     if (Hs >= 8 && (unsigned long long)Hs * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL) {
@@ -2136,6 +2226,11 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 h->hot_uses.assign((size_t)h->R, -1);
                 h->hot_cov.assign((size_t)h->R, 0.0);
                 h->all_hot.assign((size_t)h->R, 0);
+                h->hot_h.assign((size_t)h->R, H);
+                h->hot_w.assign((size_t)h->R, h->T);
+                h->hot_lo.assign((size_t)h->R, 0);
+                h->hot_win.assign((size_t)h->R, 1.0);
+                h->sieve_budget = budget;
                 CREATE_CHECK(dev_alloc(h, &h->d_hlut, (size_t)h->R * h->L));
                 if (cbits > 0) {
                     CREATE_CHECK(dev_alloc(h, &h->d_pix_cnt, (size_t)h->L));
@@ -2168,6 +2263,11 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
                 CREATE_CHECK(dev_alloc(h, &h->d_dummy, 16));
                 CREATE_HIP(hipMemset(h->d_dummy, 0, 64));
                 CREATE_HIP(hipHostMalloc((void **)&h->h_sel_stats, (size_t)h->R * 16, hipHostMallocDefault));
+                if (h->sieve_ok) {  // the sample the TOA window is chosen from
+                    CREATE_CHECK(dev_alloc(h, &h->d_toa_hist, (size_t)h->T));
+                    CREATE_HIP(hipHostMalloc((void **)&h->h_toa_hist, (size_t)h->T * 4, hipHostMallocDefault));
+                    CREATE_HIP(hipHostMalloc((void **)&h->h_screen_cnt, (size_t)h->S * 4, hipHostMallocDefault));
+                }
             }
         }
         h->lds_ctab = env_ll("LDE_LDS_CTAB", 1) != 0;
@@ -2182,8 +2282,6 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->early_gather = env_ll("LDE_EARLY_GATHER", 0) != 0;
         h->probe = env_ll("LDE_HOST_PROBE", 0) != 0;
         h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
-        h->lane_compact = env_ll("LDE_SIEVE_COMPACT", 0) != 0;
-        h->store_nt = env_ll("LDE_SIEVE_STORE_NT", 0) != 0;
         h->cold_sort_mode = (int)env_ll("LDE_COLD_SORT", 2);
         {
             const long long k = env_ll("LDE_COLD_SORT_KPT", 48);

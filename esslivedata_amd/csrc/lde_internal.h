@@ -195,8 +195,6 @@ struct SieveArgs {
     int lds_ctab;                // 1: build the block's chunk table in LDS (no chunk_tab)
     int karg;                    // lds_ctab: descriptors from sk (else from segs)
     int early_gather;            // 1: gathers issued one iteration before they are binned
-    int lane_compact = 0;        // 1: cold keys compacted per lane (three ballots per half)
-    int store_nt = 0;            // 1: cold-key stores non-temporal
     int pack;                    // 1: TOA bin packed into the table word at the gather
     SegKarg sk;                  // lds_ctab: the message descriptors (n_segs <= kKargSegs)
     const int *dummy;            // the all-invalid chunk
@@ -210,7 +208,14 @@ struct SieveArgs {
     int T;
     const uint32_t *pix_tab;  // this replica's LDS table image (1 << cbits words)
     int cbits;
-    int hot_words;  // align4(rows * T)
+    int hot_words;  // align4(hot_lo + rows * hot_w)
+    // TOA window of the hot rows: row r holds bins [hot_lo, hot_lo + hot_w) at
+    // LDS words r * hot_w + bin (so words [0, hot_lo) stay unused); a hot
+    // screen's event outside the window leaves as a cold key, its screen from
+    // the row table (hot_w = T, hot_lo = 0: whole rows, no such events)
+    int hot_lo = 0, hot_w = 0, hot_rows = 0;
+    float hot_inv_w = 0.f;         // 1 / hot_w (row of a word value row * hot_w)
+    const uint32_t *row_screen = nullptr;  // [hot_rows] screen of each hot row
     uint32_t *hot_part;
     uint32_t *cold;
     long long cold_cap;  // keys per block region (region stride cold_cap + 16)
@@ -224,7 +229,7 @@ struct SieveArgs {
     int tail_release = 0;  // each block ends with an agent-scope release (L2 writeback of its stores)
     int keyed = 0;  // the 'toa' stream holds finished pixel words (k_event_key): no probe/gather/TOA
 };
-size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);
+size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles, int hot_rows = kHotMaxRows);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a
 // tile-major u16 array, pass B
 struct ColdArgs {
@@ -234,7 +239,8 @@ struct ColdArgs {
     // the per-tile scan (hot_part == nullptr: none)
     const uint32_t *hot_part = nullptr;
     const uint32_t *row_screen = nullptr;
-    int ht = 0, ht4 = 0, T = 1;  // hot bins (rows * T), their row stride
+    int ht = 0, ht4 = 0, T = 1;  // hot words (hot_lo + rows * hot_w), their row stride
+    int hot_lo = 0, hot_w = 1;   // the hot rows' TOA window (SieveArgs)
     const uint32_t *cold;
     long long stride, cap;  // region stride and capacity (keys)
     const uint32_t *cold_cnt, *tcnt;
@@ -262,7 +268,7 @@ constexpr int kSortThreadsHost = 64 * (kSplitThreads / 64) / kColdGroups;  // co
 // (hipExtLaunchKernelGGL), so timing adds no marker packets between kernels
 hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t stop = nullptr);
 hipError_t launch_hot_reduce(const SplitArgs &a, uint32_t *win, hipStream_t st);
-hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
+hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T, int W,
                                const uint16_t *screen_row, const uint32_t *pix_cnt, int cbits,
                                uint32_t *glut, uint32_t *tab, hipStream_t st);
 // dummy: kChunk x (pid_off - 1), the all-invalid chunk
@@ -275,7 +281,8 @@ hipError_t launch_chunk_tab_karg(const SegDesc *host_segs, int n_segs, long long
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start = nullptr,
                         hipEvent_t stop = nullptr);
 size_t split_smem(int ht4, int cache_words, const ToaParams &tp);
-hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st);
+hipError_t launch_hot_sample(const SplitArgs &a, int replica, uint32_t *toa_hist, hipStream_t st);
+hipError_t launch_hot_pick(const SplitArgs &a, int replica, hipStream_t st);
 hipError_t launch_split(const SplitArgs &a, hipStream_t st);
 hipError_t launch_split_tail(const SplitArgs &a, uint32_t *win, SegDesc *cold_segs,
                              long long *n_cold_chunks, hipStream_t st);

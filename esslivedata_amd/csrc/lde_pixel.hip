@@ -257,7 +257,7 @@ __global__ __launch_bounds__(1024) void k_pix_scan(PixArgs a, const uint32_t *__
 // staging positions, slot ends (nr each) | scan scratch (32) | chunk table |
 // TOA image
 size_t pix_scatter_smem(const ToaParams &tp, int unit) {
-    return 4 * ((size_t)unit * kChunk + 4 * (size_t)kPixMaxRanges + 5 * (size_t)kPixMaxRanges + 32) +
+    return 4 * ((size_t)unit * kChunk + 4 * (size_t)kPixMaxRanges + 6 * (size_t)kPixMaxRanges + 32) +
            sizeof(PixChunk) * kPixLdsChunks + toa_lds_bytes(tp);
 }
 
@@ -272,7 +272,11 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *s_stg = reinterpret_cast<uint32_t *>(smem);
     uint32_t *s_cnt = s_stg + U * kChunk + 4 * kPixMaxRanges;  // staging holds the pads too
-    uint32_t *s_off = s_cnt + kPixMaxRanges;
+    // run counts double-buffered by unit parity (s_cnt, s_cnt2): a unit's
+    // count atomics never race the previous unit's readers, so the cursor
+    // update and the counter reset need no barriers of their own
+    uint32_t *s_cnt2 = s_cnt + kPixMaxRanges;
+    uint32_t *s_off = s_cnt2 + kPixMaxRanges;
     uint32_t *s_cur = s_off + kPixMaxRanges;
     uint32_t *s_pos = s_cur + kPixMaxRanges;
     uint32_t *s_end = s_pos + kPixMaxRanges;
@@ -283,7 +287,7 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     const int tid = threadIdx.x;
     const uint32_t *rtot = a.rstart + a.nr + 1;  // k_pix_scan_blocks' range totals
     for (int r = tid; r < a.nr; r += NT) {
-        s_cnt[r] = 0;
+        s_cnt[r] = s_cnt2[r] = 0;
         s_cur[r] = a.rstart[r] + a.counts[(size_t)blockIdx.x * a.nr + r];  // this block's slot of range r
         s_end[r] = a.rstart[r] + ((int)blockIdx.x + 1 < a.grid ? a.counts[(size_t)(blockIdx.x + 1) * a.nr + r]
                                                                : rtot[r]);
@@ -298,7 +302,13 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     // D units of events in flight (PF2: two register sets, A and B, used by
     // alternate units, so a unit's loads have two units' work to arrive)
     constexpr long long D = PF2 ? 2 : 1;
+    // owner thread tid < nr (range tid): the previous unit's padded run, added
+    // to its cursor in this unit's scan step (after the barrier that ends the
+    // previous unit's write-out, the cursor's last reader)
+    uint32_t vprev = 0;
     auto unit = [&](long long c, int (&p)[E], int (&t)[E]) __attribute__((always_inline)) {
+        uint32_t *cnt = (c & 1) ? s_cnt2 : s_cnt;      // this unit's counts
+        uint32_t *cnt_next = (c & 1) ? s_cnt : s_cnt2;  // the next unit's, reset here
         // pass 1: the events' words and their ranges' counts; only the words
         // stay live across the scan (registers: the next unit's loads are in
         // flight at the same time), pass 2 takes the slots
@@ -310,7 +320,7 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
             const uint32_t r = q >> a.rb;
             word[e] = q < a.L ? ((r << a.rs) | (b < 0 ? dmask : ((q & mask) | ((uint32_t)b << a.rb))))
                               : 0xFFFFFFFFu;  // unknown id: no slot
-            if (q < a.L) atomicAdd(&s_cnt[r], 1u);
+            if (q < a.L) atomicAdd(&cnt[r], 1u);
             asm volatile("" : "+v"(word[e]));  // materialized here, not recomputed after the scan
         }
         // the next unit's events load while this one is partitioned (not
@@ -320,13 +330,19 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
         __syncthreads();
         // runs padded to 4: staging offsets, slot cursors and the pads are
         // whole groups
-        uint32_t v = 0, total;
-        if (tid < a.nr) v = (s_cnt[tid] + 3u) & ~3u;  // nr <= kPixMaxRanges <= NT
+        uint32_t v = 0, total, n = 0;
+        if (tid < a.nr) {
+            n = cnt[tid];
+            v = (n + 3u) & ~3u;  // nr <= kPixMaxRanges <= NT
+            s_cur[tid] += vprev;
+            vprev = v;
+            cnt_next[tid] = 0;
+        }
         const uint32_t off = block_exclusive_scan(v, s_w, &total);
         if (tid < a.nr) {
             s_off[tid] = off;
             s_pos[tid] = off;
-            for (uint32_t j = s_cnt[tid]; j < v; ++j) s_stg[off + j] = ((uint32_t)tid << a.rs) | dmask;
+            for (uint32_t j = n; j < v; ++j) s_stg[off + j] = ((uint32_t)tid << a.rs) | dmask;
         }
         __syncthreads();
 #pragma unroll
@@ -373,12 +389,6 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
                 }
             }
         }
-        __syncthreads();
-        for (int r = tid; r < a.nr; r += NT) {
-            s_cur[r] += (s_cnt[r] + 3u) & ~3u;
-            s_cnt[r] = 0;
-        }
-        __syncthreads();
         };
     int pA[E], tA[E];
     if (cb < ce) unit_load<U, E, true>(a, s_ct, cb * U, cb, pA, tA);
@@ -392,6 +402,10 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     } else {
         for (long long c = cb; c < ce; ++c) unit(c, pA, tA);
     }
+    // the last unit's runs into the cursors (after its write-out)
+    __syncthreads();
+    if (tid < a.nr) s_cur[tid] += vprev;
+    __syncthreads();
     // this batch's run totals (the next batch's prediction), then each slot's
     // unused tail as dropped groups, one wave per range
     for (int r = tid; r < a.nr; r += NT) {

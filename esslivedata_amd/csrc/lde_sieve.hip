@@ -51,8 +51,6 @@ constexpr int kEPT = kSplitEPT;               // 8 events per thread per chunk
 constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (half a chunk)
 constexpr int kSieveKeyed = 262144;           // mode bit: the stream holds finished words
 constexpr int kSieveToaLog = 1 << 20;         // mode bit: log-linear TOA buckets
-constexpr int kSieveLaneCompact = 1 << 21;    // mode bit: cold keys compacted per lane
-constexpr int kSieveStoreNT = 1 << 22;        // mode bit: cold-key stores non-temporal (nt)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
@@ -105,7 +103,7 @@ __device__ __forceinline__ void unpack_keys24(v3u w, uint32_t *k) {
 // tables (rebuilt with the hot set, i.e. every hot_refresh batches)
 // ---------------------------------------------------------------------------
 template <typename LT>
-__global__ __launch_bounds__(256) void k_sieve_glut(const LT *__restrict__ lut, long long L, int T,
+__global__ __launch_bounds__(256) void k_sieve_glut(const LT *__restrict__ lut, long long L, int T, int W,
                                                     const uint16_t *__restrict__ screen_row,
                                                     uint32_t *__restrict__ glut) {
     const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -115,7 +113,7 @@ __global__ __launch_bounds__(256) void k_sieve_glut(const LT *__restrict__ lut, 
         const int s = screen_of_lut(lut, q, T);
         if (s >= 0) {
             const uint32_t r1 = screen_row[s];
-            w = r1 ? (kSieveValid | kSieveHot | ((r1 - 1u) * (uint32_t)T))
+            w = r1 ? (kSieveValid | kSieveHot | ((r1 - 1u) * (uint32_t)W))
                    : (kSieveValid | ((uint32_t)s * (uint32_t)T));
         }
     }
@@ -234,6 +232,12 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t o_ctab = o_tcnt + (uint32_t)(kColdGroups * align4(a.n_tiles));
     const uint32_t o_seg = o_ctab + 4u * kSieveLdsChunks;
     SegDesc *s_seg = reinterpret_cast<SegDesc *>(sm + o_seg);
+    // hot row -> screen (u16), for hot-screen events outside the rows' window
+    const uint32_t o_rs = o_seg + (uint32_t)(sizeof(SegDesc) / 4 * kKargSegs);
+    uint16_t *s_rs = reinterpret_cast<uint16_t *>(sm + o_rs);
+    const bool windowed = a.hot_w != a.T;
+    if (windowed)
+        for (int i = tid; i < a.hot_rows; i += kSplitThreads) s_rs[i] = (uint16_t)a.row_screen[i];
     for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.hot_words; i += kSplitThreads * 4u)
         *reinterpret_cast<uint4 *>(sm + i) = make_uint4(0, 0, 0, 0);
     for (uint32_t i = (uint32_t)tid * 4u; i < C; i += kSplitThreads * 4u)
@@ -259,14 +263,12 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                              (size_t)blockIdx.x * (size_t)(a.cold_cap + kSplitThreads / 64) * kbytes;
     const __amdgpu_buffer_rsrc_t cold = make_rsrc(my_cold, (uint32_t)a.cold_cap * kbytes);
     // one lane's four keys: offset = key index * 4 (kOOB: discarded)
-    // (kSieveStoreNT: aux 2 = nt, streamed past L2's normal replacement)
-    constexpr int kStoreAux = (ABL & kSieveStoreNT) ? 2 : 0;
     auto store_keys = [&](v4u kv, uint32_t off) __attribute__((always_inline)) {
         if (a.key24)
             __builtin_amdgcn_raw_buffer_store_b96(pack_keys24(kv), cold,
-                                                  (int)(off == kOOB ? kOOB : (off >> 2) * 3u), 0, kStoreAux);
+                                                  (int)(off == kOOB ? kOOB : (off >> 2) * 3u), 0, 0);
         else
-            __builtin_amdgcn_raw_buffer_store_b128(kv, cold, (int)off, 0, kStoreAux);
+            __builtin_amdgcn_raw_buffer_store_b128(kv, cold, (int)off, 0, 0);
     };
     const uint32_t cmask = C - 1u;
     const uint32_t pid_off = (uint32_t)a.pid_off;
@@ -277,6 +279,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t wmask = (ABL & kSieveToaLog) ? 0xFFFFFFFFu : (1u << a.toa_shift) - 1u;
     const int toa_m = a.toa_shift;  // log-linear: 2^M buckets per octave
     const uint32_t T = (uint32_t)a.T;
+    const uint32_t hlo = (uint32_t)a.hot_lo, hw = (uint32_t)a.hot_w;
     const uint32_t dum_idx = o_dum + (uint32_t)lane;
     const uint32_t dum4 = dum_idx * 4u;
     const uint32_t o_stg_w = o_stg + kSieveStage * (uint32_t)(tid >> 6);
@@ -447,45 +450,6 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             uint32_t tot = 0;
-            if (ABL & kSieveLaneCompact) {
-                // per lane: the half's events classified with per-lane
-                // compares only (no wave mask per event), one LDS atomic each;
-                // the lane's cold keys then go to consecutive staging words at
-                // a wave prefix built from three ballots of the lane's count
-                // (0..4) -- instead of three ballots, a prefix count and a
-                // mask round trip per event
-                uint32_t kk[kEPT / 2], cm = 0, nc = 0;
-#pragma unroll
-                for (int e = 0; e < kEPT / 2; ++e) {
-                    const int ev = h * kEPT / 2 + e;
-                    const uint32_t v = ws[ev] | g[ev];
-                    const uint32_t b = (ABL & kSieveKeyed) ? 0u
-                                       : (ABL & 65536) ? ((v >> kSieveTagShift) & 0xFFu)
-                                                       : (tw[ev] & 0xFFu) + (((dc[ev] & wmask) >= (tw[ev] >> 8)) ? 1u : 0u);
-                    const uint32_t fl = v >> 30;
-                    const uint32_t k4 = ((v & kSieveValueMask) + b) << 2;
-                    const bool in = b < T;
-                    const bool cold_e = in && fl == 2u;
-                    const bool hot_e = in && fl == 3u;
-                    const uint32_t aidx4 = hot_e ? k4 : cold_e ? ((k4 >> tsh) << 2) + o_tcnt4 : dum4;
-                    __hip_atomic_fetch_add(&lds_at(sm, aidx4), 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                    kk[e] = k4;
-                    cm |= (cold_e ? 1u : 0u) << e;
-                    nc += cold_e ? 1u : 0u;
-                }
-                const unsigned long long b0 = __builtin_amdgcn_ballot_w64((nc & 1u) != 0u);
-                const unsigned long long b1 = __builtin_amdgcn_ballot_w64((nc & 2u) != 0u);
-                const unsigned long long b2 = __builtin_amdgcn_ballot_w64((nc & 4u) != 0u);
-                uint32_t pos = o_stg_w + lanes_below(b0) + 2u * lanes_below(b1) + 4u * lanes_below(b2);
-                tot = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
-#pragma unroll
-                for (int e = 0; e < kEPT / 2; ++e) {
-                    const bool c = (cm >> e) & 1u;
-                    lds_at(sm, c ? pos << 2 : dum4) = kk[e];
-                    pos += c ? 1u : 0u;
-                }
-            } else {
 #pragma unroll
             for (int e = h * kEPT / 2; e < (h + 1) * kEPT / 2; ++e) {
                 const uint32_t v = ws[e] | g[e];
@@ -500,11 +464,25 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 const uint32_t fl = v >> 30;
                 // hot rows start at LDS byte 0, so the scaled key is the hot
                 // counter's address; cold keys leave scaled by 4 as well
-                const uint32_t k4 = ((v & kSieveValueMask) + b) << 2;
+                uint32_t k4 = ((v & kSieveValueMask) + b) << 2;
                 // lane masks straight from the compares (no bool round trip)
                 const unsigned long long inb = __builtin_amdgcn_ballot_w64(b < T);
-                const unsigned long long bal = inb & __builtin_amdgcn_ballot_w64(fl == 2u);
-                const unsigned long long hm = inb & __builtin_amdgcn_ballot_w64(fl == 3u);
+                unsigned long long bal = inb & __builtin_amdgcn_ballot_w64(fl == 2u);
+                unsigned long long hm = inb & __builtin_amdgcn_ballot_w64(fl == 3u);
+                if (windowed) {
+                    // a hot screen's bin outside the rows' window: a cold key
+                    // screen * T + bin, the screen from the row table (rare;
+                    // the word value is row * hw, an exact float quotient)
+                    const unsigned long long oow = hm & __builtin_amdgcn_ballot_w64(b - hlo >= hw);
+                    if (oow) {
+                        const uint32_t row = min((uint32_t)((float)(v & kSieveValueMask) * a.hot_inv_w + 0.5f),
+                                                 (uint32_t)a.hot_rows - 1u);
+                        const uint32_t ck4 = ((uint32_t)s_rs[row] * T + b) << 2;
+                        k4 = vsel(oow, ck4, k4);
+                        bal |= oow;
+                        hm &= ~oow;
+                    }
+                }
                 const uint32_t pos4 = (lanes_below(bal) + o_stg_w + tot) << 2;
                 tot += (uint32_t)__popcll(bal);
                 lds_at(sm, vsel(bal, pos4, dum4)) = k4;
@@ -515,7 +493,6 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 const uint32_t aidx4 = (ABL & 1) ? tidx4 : vsel(hm, k4, tidx4);
                 __hip_atomic_fetch_add(&lds_at(sm, aidx4), 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
             }
             const uint32_t res = (tot + 3u) & ~3u;
             // the previous half's keys leave now (their LDS read is long done)
@@ -791,9 +768,10 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
                                                    : row[i];
             }
         }
-        if (sum) {
-            const int row = i / c.T;
-            atomicAdd(c.hist + (size_t)c.row_screen[row] * c.T + (i - row * c.T), sum);
+        const int j = i - c.hot_lo;  // words [0, hot_lo) hold no row
+        if (sum && j >= 0) {
+            const int row = j / c.hot_w;
+            atomicAdd(c.hist + (size_t)c.row_screen[row] * c.T + (i - row * c.hot_w), sum);
         }
         return;
     }
@@ -1474,21 +1452,22 @@ __global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
-size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles) {
+size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles, int hot_rows) {
     return 4 * ((size_t)hot_words + ((size_t)1 << cbits) + (size_t)toa_words4 + 64 + 4 +
+                (size_t)align4((hot_rows + 1) / 2) +
                 (size_t)kSieveStage * (kSplitThreads / 64) + (size_t)kColdGroups * align4(n_tiles) +
                 4 * (size_t)kSieveLdsChunks + sizeof(SegDesc) / 4 * (size_t)kKargSegs);
 }
 
-hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T,
+hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T, int W,
                                const uint16_t *screen_row, const uint32_t *pix_cnt, int cbits,
                                uint32_t *glut, uint32_t *tab, hipStream_t st) {
     const unsigned g = (unsigned)((L + 1 + 255) / 256);
     if (lut16)
         hipLaunchKernelGGL(k_sieve_glut<uint16_t>, dim3(g), dim3(256), 0, st,
-                           (const uint16_t *)lut, L, T, screen_row, glut);
+                           (const uint16_t *)lut, L, T, W, screen_row, glut);
     else
-        hipLaunchKernelGGL(k_sieve_glut<int>, dim3(g), dim3(256), 0, st, (const int *)lut, L, T,
+        hipLaunchKernelGGL(k_sieve_glut<int>, dim3(g), dim3(256), 0, st, (const int *)lut, L, T, W,
                            screen_row, glut);
     hipLaunchKernelGGL(k_sieve_table, dim3((unsigned)(((1LL << cbits) + 255) / 256)), dim3(256), 0,
                        st, pix_cnt, glut, L, cbits, tab);
@@ -1590,7 +1569,9 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
 template <int ABL>
 static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                                  hipEvent_t stop) {
-    if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles) > kSplitSmemMax)
+    if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles, a.hot_w != a.T ? a.hot_rows : 0) >
+            kSplitSmemMax ||
+        (a.hot_w != a.T && (a.hot_rows < 1 || !a.row_screen)))
         return hipErrorInvalidValue;
     if (a.lds_ctab)
         hipExtLaunchKernelGGL(k_sieve<ABL, 0>, dim3(grid), dim3(kSplitThreads), 0, st, start, stop, 0,
@@ -1603,11 +1584,9 @@ static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, h
 
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                         hipEvent_t stop) {
-    const int mode = a.keyed ? kSieveKeyed | (a.lane_compact ? kSieveLaneCompact : 0)
+    const int mode = a.keyed ? kSieveKeyed
                              : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0) |
-                                   (a.toa_log ? kSieveToaLog : 0) |
-                                   (a.lane_compact ? kSieveLaneCompact : 0) |
-                                   (a.store_nt ? kSieveStoreNT : 0);
+                                   (a.toa_log ? kSieveToaLog : 0);
     switch (mode) {
 #define LDE_SIEVE_MODE(m) \
     case m: return launch_sieve_t<m>(a, grid, st, start, stop);
@@ -1620,11 +1599,6 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     LDE_SIEVE_MODE(kSieveToaLog) LDE_SIEVE_MODE(kSieveToaLog | 256) LDE_SIEVE_MODE(kSieveToaLog | 2048)
     LDE_SIEVE_MODE(kSieveToaLog | 65536) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256)
     LDE_SIEVE_MODE(kSieveToaLog | 65536 | 2048) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256 | 2048)
-    // per-lane cold-key compaction
-    LDE_SIEVE_MODE(kSieveLaneCompact) LDE_SIEVE_MODE(kSieveLaneCompact | 65536)
-    LDE_SIEVE_MODE(kSieveLaneCompact | kSieveKeyed) LDE_SIEVE_MODE(kSieveLaneCompact | kSieveToaLog)
-    // non-temporal cold-key stores
-    LDE_SIEVE_MODE(kSieveStoreNT) LDE_SIEVE_MODE(kSieveStoreNT | kSieveLaneCompact)
 #ifdef LDE_DIAGNOSTICS
     // timing probes (wrong results), diagnostics build only
     LDE_SIEVE_MODE(1) LDE_SIEVE_MODE(2) LDE_SIEVE_MODE(4) LDE_SIEVE_MODE(6)

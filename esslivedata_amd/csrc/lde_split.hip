@@ -171,6 +171,32 @@ __global__ __launch_bounds__(kSplitThreads) void k_sample_screens(
     }
 }
 
+// TOA-bin histogram of the sampled chunks (those of k_sample_screens), for
+// the SIEVE hot rows' TOA window: global u32 [T], zeroed before
+template <bool FAST>
+__global__ __launch_bounds__(kSplitThreads) void k_sample_toa(const SegDesc *__restrict__ segs, int n_segs,
+                                                              long long n_chunks, int pid_off,
+                                                              const unsigned char *__restrict__ g_tab,
+                                                              ToaParams tp, uint32_t *__restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *s_h = reinterpret_cast<uint32_t *>(smem);
+    unsigned char *s_tab = smem + align16((size_t)tp.T * 4);
+    for (int i = threadIdx.x; i < tp.T; i += kSplitThreads) s_h[i] = 0;
+    load_toa_tables(s_tab, g_tab, tp);
+    __syncthreads();
+    const long long c = (long long)blockIdx.x * n_chunks / gridDim.x;
+    int p[kSplitEPT], t[kSplitEPT];
+    load_chunk_t<kSplitThreads, kSplitEPT, true>(segs, n_segs, c, pid_off - 1, p, t);
+#pragma unroll
+    for (int e = 0; e < kSplitEPT; ++e) {
+        const int b = toa_bin_nb<FAST>(t[e], s_tab, tp);
+        if (b >= 0 && p[e] != pid_off - 1) atomicAdd(&s_h[b], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < tp.T; i += kSplitThreads)
+        if (s_h[i]) atomicAdd(hist + i, s_h[i]);
+}
+
 __global__ __launch_bounds__(256) void k_screen_sum(const uint32_t *__restrict__ part, int rows,
                                                     int S, uint32_t *__restrict__ cnt) {
     const int s = blockIdx.x * 256 + threadIdx.x;
@@ -567,7 +593,11 @@ size_t split_smem(int ht4, int cache_words, const ToaParams &tp) {
     return (size_t)ht4 * 4 + (size_t)cache_words * 4 + 16 + toa_lds_bytes(tp);
 }
 
-hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st) {
+// Hot-set selection in two steps, so the host can size the rows from the
+// sample in between: launch_hot_sample (per-screen and per-pixel counts of the
+// sampled chunks; with toa_hist, also their TOA-bin histogram), then
+// launch_hot_pick (top a.rows screens, hot LUT, pixel table).
+hipError_t launch_hot_sample(const SplitArgs &a, int replica, uint32_t *toa_hist, hipStream_t st) {
     if (a.cache_bits > 0) {
         const hipError_t e = hipMemsetAsync(a.pix_cnt, 0, (size_t)a.L * 4, st);
         if (e != hipSuccess) return e;
@@ -599,6 +629,28 @@ hipError_t launch_hot_select(const SplitArgs &a, int replica, hipStream_t st) {
     }
     hipLaunchKernelGGL(k_screen_sum, dim3((a.S + 255) / 256), dim3(256), 0, st, a.sample_part,
                        a.sample_blocks, a.S, a.screen_cnt);
+    if (toa_hist) {
+        hipError_t e = hipMemsetAsync(toa_hist, 0, (size_t)a.tp.T * 4, st);
+        if (e != hipSuccess) return e;
+        const size_t smt = align16((size_t)a.tp.T * 4) + toa_lds_bytes(a.tp);
+        if (a.tp.fast) {
+            (void)hipFuncSetAttribute((const void *)k_sample_toa<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smt);
+            hipLaunchKernelGGL(k_sample_toa<true>, dim3(a.sample_blocks), dim3(kSplitThreads), smt, st,
+                               a.segs, a.n_segs, a.n_chunks, a.pid_off, a.tab, a.tp, toa_hist);
+        } else {
+            (void)hipFuncSetAttribute((const void *)k_sample_toa<false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smt);
+            hipLaunchKernelGGL(k_sample_toa<false>, dim3(a.sample_blocks), dim3(kSplitThreads), smt, st,
+                               a.segs, a.n_segs, a.n_chunks, a.pid_off, a.tab, a.tp, toa_hist);
+        }
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_hot_pick(const SplitArgs &a, int replica, hipStream_t st) {
+    const void *lut_r = a.lut16 ? (const void *)((const uint16_t *)a.lut + (size_t)replica * a.L)
+                                : (const void *)((const int *)a.lut + (size_t)replica * a.L);
     hipLaunchKernelGGL(k_select_hot, dim3(1), dim3(1024), 0, st, a.screen_cnt, a.S, a.rows,
                        a.screen_row, a.row_screen, a.stats);
     const unsigned g = (unsigned)((a.L + 255) / 256);

@@ -104,8 +104,4 @@ def test_product_library_has_only_exact_sieve_variants():
     # the exact variants, and the keyed wavelength pass (262144)
     exact = {0, 256, 2048, 65536, 65536 | 256, 65536 | 2048, 65536 | 256 | 2048}
     log = 1 << 20  # log-linear TOA buckets (exact)
-    compact = 1 << 21  # cold keys compacted per lane (exact)
-    nt = 1 << 22  # non-temporal cold-key stores (exact)
-    allowed = exact | {m | log for m in exact} | {262144}
-    allowed |= {m | compact for m in allowed}
-    assert modes <= allowed | {m | nt for m in allowed}, modes
+    assert modes <= exact | {m | log for m in exact} | {262144}, modes

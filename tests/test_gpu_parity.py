@@ -46,9 +46,10 @@ VARIANTS = [
     {'LDE_SIEVE_TOA_LOG': '1'},
     {'LDE_SIEVE_TOA_LOG': '1', 'LDE_SIEVE_PACK': '1'},
     {'LDE_DEFER_STORES': '1'},
-    # cold keys compacted per lane (three ballots per half instead of per event)
-    {'LDE_SIEVE_COMPACT': '1'},
-    {'LDE_SIEVE_COMPACT': '1', 'LDE_SIEVE_PACK': '1'},
+    # SIEVE hot rows narrowed to a TOA window (more rows; hot screens' events
+    # outside the window leave as cold keys), alone and with a tiny row count
+    {'LDE_HOT_WINDOW': '1'},
+    {'LDE_HOT_WINDOW': '1', 'LDE_HOT_ROWS': '8', 'LDE_HOT_REFRESH': '1'},
     # cold-key sorts: block-cooperative per-key stores, wave-independent,
     # 16-byte groups with 16 / 32 keys per thread (default: 16-byte groups, 48)
     {'LDE_COLD_SORT': '0'},

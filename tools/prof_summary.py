@@ -47,6 +47,15 @@ def main(prof: Path, stem: Path) -> None:
         d['total_ns'] += float(r['TotalDurationNs'])
     for d in kernels.values():
         d['avg_ms'] = d['total_ns'] / max(d['calls'], 1) / 1e6
+    # steady-state average from the per-dispatch trace: every dispatch but a
+    # kernel's first two (the bench's warm-up steps: first-touch allocations,
+    # hot-set selection), comparable with the bench's timed-region stamps
+    durs: dict[str, list[float]] = defaultdict(list)
+    trace = prof / 'kt' / 'run_kernel_trace.csv'
+    if trace.exists():
+        for r in csv.DictReader(open(trace)):
+            durs[short(r['Kernel_Name'])].append(
+                (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6)
     counters: dict[str, dict[str, list[float]]] = defaultdict(lambda: defaultdict(list))
     for sub in sorted(prof.glob('pmc_*')):
         f = sub / 'run_counter_collection.csv'
@@ -62,6 +71,8 @@ def main(prof: Path, stem: Path) -> None:
         if not k.startswith('k_'):
             continue
         e = {'calls': d['calls'], 'avg_ms': d['avg_ms']}
+        if len(durs.get(k, [])) > 2:
+            e['avg_ms_steady'] = sum(durs[k][2:]) / (len(durs[k]) - 2)
         pm = {c: sum(v) / len(v) for c, v in counters.get(k, {}).items()}
         # the first dispatches of each kernel include warm-up sizes; use the median-like mean
         e['pmc_per_dispatch'] = pm
@@ -86,6 +97,8 @@ def main(prof: Path, stem: Path) -> None:
         e = {'members': names, 'calls': n,
              'launches_per_call': {m: round(x, 4) for m, x in zip(names, w)},
              'avg_ms': sum(x * m['avg_ms'] for x, m in zip(w, ms))}
+        if all('avg_ms_steady' in m for m in ms):
+            e['avg_ms_steady'] = sum(x * m['avg_ms_steady'] for x, m in zip(w, ms))
         if all('hbm_traffic_bytes' in m for m in ms):
             for key in ('hbm_read_bytes', 'hbm_write_bytes', 'hbm_traffic_bytes'):
                 e[key] = sum(x * m[key] for x, m in zip(w, ms))
