@@ -25,6 +25,7 @@
 //               accumulates each item in an LDS sub-histogram and flushes the
 //               non-zero bins with coalesced atomics.
 //   monitors  : conflict-free per-lane-column LDS histogram.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -451,28 +452,32 @@ size_t partition_smem(int n_tiles, const ToaParams &tp) {
 template <typename LT>
 static hipError_t launch_bin_atomic_t(const SegKarg &seg, int n_segs, const LT *lut, int pid_off,
                                       unsigned L, const unsigned char *tab, const ToaParams &tp,
-                                      uint32_t *hist, int grid, hipStream_t st) {
+                                      uint32_t *hist, int grid, hipStream_t st, hipEvent_t start,
+                                      hipEvent_t stop) {
     const size_t sm = toa_lds_bytes(tp);
     if (tp.fast) {
         (void)hipFuncSetAttribute((const void *)k_bin_atomic<LT, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL((k_bin_atomic<LT, true>), dim3(grid), dim3(256), sm, st, seg, n_segs, lut,
-                           pid_off, L, tab, tp, hist);
+        hipExtLaunchKernelGGL((k_bin_atomic<LT, true>), dim3(grid), dim3(256), sm, st, start, stop, 0,
+                              seg, n_segs, lut, pid_off, L, tab, tp, hist);
     } else {
         (void)hipFuncSetAttribute((const void *)k_bin_atomic<LT, false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL((k_bin_atomic<LT, false>), dim3(grid), dim3(256), sm, st, seg, n_segs, lut,
-                           pid_off, L, tab, tp, hist);
+        hipExtLaunchKernelGGL((k_bin_atomic<LT, false>), dim3(grid), dim3(256), sm, st, start, stop, 0,
+                              seg, n_segs, lut, pid_off, L, tab, tp, hist);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_bin_atomic(const SegKarg &seg, int n_segs, const void *lut, bool lut16, int pid_off,
                              unsigned L, const unsigned char *tab, const ToaParams &tp,
-                             uint32_t *hist, int grid, hipStream_t st) {
+                             uint32_t *hist, int grid, hipStream_t st, hipEvent_t start,
+                             hipEvent_t stop) {
     if (n_segs < 1 || n_segs > kKargSegs) return hipErrorInvalidValue;
-    return lut16 ? launch_bin_atomic_t(seg, n_segs, (const uint16_t *)lut, pid_off, L, tab, tp, hist, grid, st)
-                 : launch_bin_atomic_t(seg, n_segs, (const int *)lut, pid_off, L, tab, tp, hist, grid, st);
+    return lut16 ? launch_bin_atomic_t(seg, n_segs, (const uint16_t *)lut, pid_off, L, tab, tp, hist, grid, st,
+                                       start, stop)
+                 : launch_bin_atomic_t(seg, n_segs, (const int *)lut, pid_off, L, tab, tp, hist, grid, st,
+                                       start, stop);
 }
 
 template <int TB, typename LT, bool FAST, bool PEEL>
@@ -544,7 +549,8 @@ hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const 
 }
 
 hipError_t launch_monitor(const SegKarg &segs, int n_segs, const unsigned char *tab,
-                          const ToaParams &tp, uint32_t *hist, int grid, hipStream_t st) {
+                          const ToaParams &tp, uint32_t *hist, int grid, hipStream_t st,
+                          hipEvent_t start, hipEvent_t stop) {
     if (n_segs < 1 || n_segs > kKargSegs) return hipErrorInvalidValue;
     const bool columns = tp.T <= kMonitorColumnsMaxT;
     const size_t hb = align16((size_t)((columns ? tp.T * 32 : tp.T) + 64) * 4);
@@ -553,8 +559,8 @@ hipError_t launch_monitor(const SegKarg &segs, int n_segs, const unsigned char *
     do {                                                                                       \
         (void)hipFuncSetAttribute((const void *)k_monitor<F, C>,                               \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);        \
-        hipLaunchKernelGGL((k_monitor<F, C>), dim3(grid), dim3(256), sm, st, segs, n_segs, tab, tp, \
-                           hist);                                                              \
+        hipExtLaunchKernelGGL((k_monitor<F, C>), dim3(grid), dim3(256), sm, st, start, stop, 0,   \
+                              segs, n_segs, tab, tp, hist);                                    \
     } while (0)
     if (tp.fast && columns) LDE_MON(true, true);
     else if (tp.fast) LDE_MON(true, false);

@@ -23,6 +23,7 @@
 // reads), and the bin from a bucket table over the edges (a start candidate,
 // then a few compares with the edges in LDS: exact for any sorted edges,
 // however the bucket arithmetic rounds).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -70,6 +71,7 @@ __global__ __launch_bounds__(256) void k_coord_cache(const uint32_t *__restrict_
 }
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t coord_rsrc(const void *p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes,
@@ -245,7 +247,7 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     const double *e = ELDS ? s_e : a.edges;
     const double *tab = TLDS ? s_t : a.table;
     const double xmax = (double)(a.nd - 1), ymax = (double)(a.nt - 1);
-    const __amdgpu_buffer_rsrc_t rrs = coord_rsrc(k.rec, (a.L + 1u) * 16u);
+    const __amdgpu_buffer_rsrc_t rrs = coord_rsrc(k.rec, (a.L + 1u) * 12u);
     const uint32_t cmask = C - 1u;
     const uint32_t pid_off = (uint32_t)a.pid_off;
     const uint32_t Lc = a.L;
@@ -322,10 +324,10 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
             // hits and ids outside the LUT load out of range (no request, 0);
             // the word of an id outside the LUT is 0 (dropped)
             const bool skip = hit || pq >= Lc;
-            const v4u r = __builtin_amdgcn_raw_buffer_load_b128(rrs, skip ? (int)0x80000000 : (int)(pq * 16u),
-                                                                 0, 0);
+            const v3u r = __builtin_amdgcn_raw_buffer_load_b96(rrs, skip ? (int)0x80000000 : (int)(pq * 12u),
+                                                                0, 0);
             g[q] = r[0];
-            d[q] = __builtin_bit_cast(double, ((unsigned long long)r[3] << 32) | r[2]);
+            d[q] = __builtin_bit_cast(double, ((unsigned long long)r[2] << 32) | r[1]);
             w[q] = hit ? (tw & (kSieveValid | kSieveHot | kSieveValueMask)) : 0u;
             slot[q] = hit ? slot[q] : 0xFFFFFFFFu;
         }
@@ -401,50 +403,55 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     }
 }
 
-// per pixel {word, 0, distance}: a table miss gathers one 16-byte record
-// instead of a word and a distance from two tables (entry L: word 0)
+// per pixel {word, distance}: a table miss gathers one 12-byte record
+// instead of a word and a distance from two tables (entry L: word 0).  12
+// bytes, not 16: the record array (5.9 MB for DREAM) is then mostly
+// L2/MALL-resident for the Zipf tail's random misses
 __global__ __launch_bounds__(256) void k_key_records(const uint32_t *__restrict__ glut,
                                                      const double *__restrict__ pix_d, unsigned L,
-                                                     uint4 *__restrict__ rec) {
+                                                     uint32_t *__restrict__ rec) {
     const unsigned q = blockIdx.x * 256u + threadIdx.x;
     if (q > L) return;
     const double d = q < L ? pix_d[q] : __builtin_nan("");
     const unsigned long long b = __builtin_bit_cast(unsigned long long, d);
-    rec[q] = make_uint4(q < L ? glut[q] : 0u, 0u, (uint32_t)b, (uint32_t)(b >> 32));
+    rec[3 * (size_t)q] = q < L ? glut[q] : 0u;
+    rec[3 * (size_t)q + 1] = (uint32_t)b;
+    rec[3 * (size_t)q + 2] = (uint32_t)(b >> 32);
 }
 
-hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, uint4 *rec,
+hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, uint32_t *rec,
                               hipStream_t st) {
     hipLaunchKernelGGL(k_key_records, dim3((L + 1u + 255u) / 256u), dim3(256), 0, st, glut, pix_d, L, rec);
     return hipGetLastError();
 }
 
 hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix_d, unsigned L,
-                           double *tab_d, hipStream_t st) {
-    hipLaunchKernelGGL(k_key_dist, dim3(((1u << cbits) + 255) / 256), dim3(256), 0, st, pix_tab, cbits,
-                       pix_d, L, tab_d);
+                           double *tab_d, hipStream_t st, hipEvent_t start) {
+    hipExtLaunchKernelGGL(k_key_dist, dim3(((1u << cbits) + 255) / 256), dim3(256), 0, st, start, nullptr, 0,
+                          pix_tab, cbits, pix_d, L, tab_d);
     return hipGetLastError();
 }
 
 template <bool TLDS, bool ELDS>
-static void launch_key_t(const KeyArgs &a, size_t sm, int grid, hipStream_t st) {
+static void launch_key_t(const KeyArgs &a, size_t sm, int grid, hipStream_t st, hipEvent_t stop) {
     (void)hipFuncSetAttribute((const void *)k_event_key<TLDS, ELDS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipLaunchKernelGGL((k_event_key<TLDS, ELDS>), dim3((unsigned)grid), dim3(1024), sm, st, a);
+    hipExtLaunchKernelGGL((k_event_key<TLDS, ELDS>), dim3((unsigned)grid), dim3(1024), sm, st, nullptr, stop, 0,
+                          a);
 }
 
-hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st) {
-    if (a.n_chunks <= 0) return hipSuccess;
+hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent_t stop) {
+    if (a.n_chunks <= 0) return stop ? hipEventRecord(stop, st) : hipSuccess;
     const bool tl = key_smem(a, true) <= kCoordSmemMax;
     const size_t sm = key_smem(a, tl);
     if (sm > kCoordSmemMax) return hipErrorInvalidValue;
     if (grid > a.n_chunks) grid = (int)a.n_chunks;
     if (tl) {
-        if (a.c.edges_lds) launch_key_t<true, true>(a, sm, grid, st);
-        else launch_key_t<true, false>(a, sm, grid, st);
+        if (a.c.edges_lds) launch_key_t<true, true>(a, sm, grid, st, stop);
+        else launch_key_t<true, false>(a, sm, grid, st, stop);
     } else {
-        if (a.c.edges_lds) launch_key_t<false, true>(a, sm, grid, st);
-        else launch_key_t<false, false>(a, sm, grid, st);
+        if (a.c.edges_lds) launch_key_t<false, true>(a, sm, grid, st, stop);
+        else launch_key_t<false, false>(a, sm, grid, st, stop);
     }
     return hipGetLastError();
 }

@@ -175,7 +175,7 @@ struct lde_handle {
     // sieve's finished words (LDE_COORD_KEYED, default 1)
     bool coord_keyed = true;
     double *d_key_dist = nullptr;  // [1 << cache_bits] distance of each pixel-table slot
-    uint4 *d_key_rec = nullptr;    // [L + 1] {word, 0, distance} of the batch's replica
+    uint32_t *d_key_rec = nullptr;  // [L + 1] x 12 B {word, distance} of the batch's replica
     // PIXEL strategy (lde_pixel.hip): pixel-range footprints built from the LUT
     bool pixel_ok = false;
     lde::PixSetup pix{};
@@ -648,6 +648,29 @@ struct Timed {
                 h->event_pool.push_back(a);
             }
         }
+    }
+};
+
+// Timing of a span of launches by the dispatches themselves: `a` is stamped
+// by the span's first dispatch, `b` by its last (hipExtLaunchKernelGGL), so no
+// marker packets sit between kernels (unlike Timed).  The launcher must stamp
+// both (or record them) when the span is non-empty.
+struct Stamp {
+    lde_handle *h;
+    int kid;
+    hipEvent_t a = nullptr, b = nullptr;
+    Stamp(lde_handle *h_, int kid_) : h(h_), kid(kid_) {
+        if (h->timing && ((h->timing_mask >> kid) & 1u)) {
+            a = pool_event(h);
+            b = a ? pool_event(h) : nullptr;
+            if (a && !b) {
+                h->event_pool.push_back(a);
+                a = nullptr;
+            }
+        }
+    }
+    ~Stamp() {
+        if (a) h->launches.push_back({kid, a, b});
     }
 };
 
@@ -1145,11 +1168,11 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             if (!h->d_key_dist)
                 if (int rc = dev_alloc(h, &h->d_key_dist, (size_t)1 << h->cache_bits)) return rc;
             const uint32_t *tab_r = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
-            Timed tm(h, LDE_K_COORD);
+            Stamp sp(h, LDE_K_COORD);  // key_dist .. event_key, stamped by the dispatches
             HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->d_key_dist,
-                                            h->stream));
+                                            h->stream, sp.a));
             if (!h->d_key_rec)
-                if (int rc = dev_alloc(h, &h->d_key_rec, (size_t)h->L + 1)) return rc;
+                if (int rc = dev_alloc(h, &h->d_key_rec, 3 * ((size_t)h->L + 1))) return rc;
             HIPCALL(h, lde::launch_key_records(h->d_glut + (size_t)(h->L + 1) * replica, h->d_cpd,
                                                (unsigned)h->L, h->d_key_rec, h->stream));
             lde::KeyArgs ka;
@@ -1164,7 +1187,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             ka.cbits = h->cache_bits;
             ka.keys = h->d_cbin;
             ka.dummy = h->d_sieve_dummy;
-            HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream));
+            HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream, sp.b));
             ksd.push_back({h->d_cbin, h->d_cbin, chunks * lde::kChunk, 0});
         }
         const std::vector<lde::SegDesc> &ssd = coord_deferred ? ksd : sd;
@@ -1407,14 +1430,14 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     h->pix_prev_units = units;
     h->pix_prev_grid = grid;
     {
-        Timed tm(h, LDE_K_PIXEL);
+        Stamp sp(h, LDE_K_PIXEL);
         HIPCALL(h, lde::launch_pixel(a, h->pix, replica, (uint32_t)per, (int)max_items, h->d_pitems,
-                                     h->d_pitem_count, h->d_win32, h->stream, 0));
+                                     h->d_pitem_count, h->d_win32, h->stream, 0, sp.a, sp.b));
     }
     {
-        Timed tm(h, LDE_K_PAGE_ACC);
+        Stamp sp(h, LDE_K_PAGE_ACC);
         HIPCALL(h, lde::launch_pixel(a, h->pix, replica, (uint32_t)per, (int)max_items, h->d_pitems,
-                                     h->d_pitem_count, h->d_win32, h->stream, 1));
+                                     h->d_pitem_count, h->d_win32, h->stream, 1, sp.a, sp.b));
     }
     return LDE_OK;
 }
@@ -1435,8 +1458,8 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             if (k == 0) return LDE_OK;
             long long g = (n / 16 + 255) / 256;  // 16 events per lane and iteration
             g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 4));
-            Timed tm(h, LDE_K_MONITOR);
-            HIPCALL(h, lde::launch_monitor(ka, k, h->d_tab, h->tp, h->d_win32, (int)g, h->stream));
+            Stamp sp(h, LDE_K_MONITOR);
+            HIPCALL(h, lde::launch_monitor(ka, k, h->d_tab, h->tp, h->d_win32, (int)g, h->stream, sp.a, sp.b));
             k = 0;
             n = 0;
             return LDE_OK;
@@ -1478,9 +1501,9 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             if (k == 0) return LDE_OK;
             long long g = (n / 4 + 255) / 256;
             g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 8));
-            Timed tm(h, LDE_K_ATOMIC);
+            Stamp sp(h, LDE_K_ATOMIC);
             HIPCALL(h, lde::launch_bin_atomic(ka, k, lut, h->lut16, h->pid_off, (unsigned)h->L, h->d_tab,
-                                              h->tp, h->d_win32, (int)g, h->stream));
+                                              h->tp, h->d_win32, (int)g, h->stream, sp.a, sp.b));
             k = 0;
             n = 0;
             return LDE_OK;

@@ -108,7 +108,8 @@ size_t partition_smem(int n_tiles, const ToaParams &tp);
 
 hipError_t launch_bin_atomic(const SegKarg &seg, int n_segs, const void *lut, bool lut16, int pid_off,
                              unsigned L, const unsigned char *tab, const ToaParams &tp,
-                             uint32_t *hist, int grid, hipStream_t st);
+                             uint32_t *hist, int grid, hipStream_t st, hipEvent_t start = nullptr,
+                             hipEvent_t stop = nullptr);
 hipError_t launch_partition(const PartitionArgs &a, hipStream_t st);
 struct PagedArgs {
     int tile_bits;
@@ -300,8 +301,10 @@ hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const 
                                   int n_tiles, long long n_chunks, const uint2 *items,
                                   const uint32_t *item_count, const uint32_t *tile_items,
                                   uint32_t *hist, long long n_bins, int grid, hipStream_t st);
+// start/stop (optional): HIP events stamped by the dispatch itself
 hipError_t launch_monitor(const SegKarg &segs, int n_segs, const unsigned char *tab,
-                          const ToaParams &tp, uint32_t *hist, int grid, hipStream_t st);
+                          const ToaParams &tp, uint32_t *hist, int grid, hipStream_t st,
+                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 hipError_t launch_fold_window(uint32_t *win32, unsigned long long *win64, long long n,
                               hipStream_t st);
 hipError_t launch_merge_f32(uint32_t *batch, unsigned long long *win64, float *winf, float *cumf,
@@ -371,18 +374,18 @@ struct KeyArgs {
     const uint32_t *glut;     // this replica's pixel words, L + 1 entries (entry L = 0)
     const uint32_t *pix_tab;  // this replica's LDS pixel-table image (1 << cbits words)
     const double *tab_d;      // distance of each table slot's pixel (1 << cbits)
-    const uint4 *rec;         // per pixel {word, 0, distance lo, hi}, L + 1 entries (k_key_records)
+    const uint32_t *rec;      // per pixel 12 bytes {word, distance lo, hi}, L + 1 entries (k_key_records)
     int cbits;
     int *keys;                // [n_chunks * kChunk]
     const int *dummy;         // kChunk x (pid_off - 1): the all-invalid chunk
 };
 constexpr int kKeyLdsChunks = 128;  // k_event_key: chunk pointers per LDS window
 size_t key_smem(const KeyArgs &a, bool table_lds);
-hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st);
+hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent_t stop = nullptr);
 // distance of every pixel-table slot's pixel (NaN for empty slots)
 hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix_d, unsigned L,
-                           double *tab_d, hipStream_t st);
-hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, uint4 *rec,
+                           double *tab_d, hipStream_t st, hipEvent_t start = nullptr);
+hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, uint32_t *rec,
                               hipStream_t st);
 
 // PIXEL strategy (lde_pixel.hip): events partitioned by pixel range, the
@@ -442,9 +445,11 @@ size_t pix_scatter_smem(const ToaParams &tp, int unit);
 size_t pix_acc_smem(int rb, int fmax, int T);
 // phase 0: count (exact slots) + scan + scatter; phase 1: accumulate (+ the
 // overflow groups with predicted slots)
+// phase 0 (pass A) takes optional start/stop events, stamped by its first and
+// last dispatch
 hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32_t item_events,
                         int max_items, uint4 *items, uint32_t *item_count, uint32_t *hist,
-                        hipStream_t st, int phase);
+                        hipStream_t st, int phase, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
 hipError_t launch_rebin_f64(const double *se, const double *sv, long long ns, const double *de,
                             long long nd, double *out_a, double *out_b, hipStream_t st);

@@ -35,6 +35,7 @@
 // items (pix_overflow).  Every
 // event is still counted exactly once: a prediction only decides where its
 // payload is stored.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -554,10 +555,10 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
 namespace {
 template <int U, int E, bool P24>
 void launch_pass_a(const PixArgs &a, uint32_t item_events, int max_items, uint4 *items,
-                   uint32_t *item_count, hipStream_t st) {
+                   uint32_t *item_count, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
     constexpr int NT = U * kChunk / E;
-    hipLaunchKernelGGL(k_pix_chunks, dim3((unsigned)((a.n_chunks + 255) / 256)), dim3(256), 0, st, a,
-                       const_cast<PixChunk *>(a.ctab));
+    hipExtLaunchKernelGGL(k_pix_chunks, dim3((unsigned)((a.n_chunks + 255) / 256)), dim3(256), 0, st, start,
+                          nullptr, 0, a, const_cast<PixChunk *>(a.ctab));
     if (a.pred <= 0.f) hipLaunchKernelGGL((k_pix_count<U, E>), dim3(a.grid), dim3(NT), 0, st, a);
     hipLaunchKernelGGL(k_pix_scan_blocks, dim3(a.nr), dim3(1024), 0, st, a, a.grid, a.rstart + a.nr + 1);
     hipLaunchKernelGGL(k_pix_scan, dim3(1), dim3(1024), 0, st, a, a.rstart + a.nr + 1, item_events,
@@ -565,7 +566,7 @@ void launch_pass_a(const PixArgs &a, uint32_t item_events, int max_items, uint4 
     const size_t sm = pix_scatter_smem(a.tp, U);
     auto go = [&](auto kern) {
         (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL(kern, dim3(a.grid), dim3(NT), sm, st, a);
+        hipExtLaunchKernelGGL(kern, dim3(a.grid), dim3(NT), sm, st, nullptr, stop, 0, a);
     };
     if (a.tp.fast) {
         if (a.pf2) go(k_pix_scatter<U, E, P24, true, true>); else go(k_pix_scatter<U, E, P24, true, false>);
@@ -575,29 +576,29 @@ void launch_pass_a(const PixArgs &a, uint32_t item_events, int max_items, uint4 
 }
 template <bool P24>
 void launch_pass_a_shape(const PixArgs &a, uint32_t item_events, int max_items, uint4 *items,
-                         uint32_t *item_count, hipStream_t st) {
-    if (a.unit == 2) launch_pass_a<2, 16, P24>(a, item_events, max_items, items, item_count, st);
-    else if (a.ept == 8) launch_pass_a<1, 8, P24>(a, item_events, max_items, items, item_count, st);
-    else launch_pass_a<1, 16, P24>(a, item_events, max_items, items, item_count, st);
+                         uint32_t *item_count, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
+    if (a.unit == 2) launch_pass_a<2, 16, P24>(a, item_events, max_items, items, item_count, st, start, stop);
+    else if (a.ept == 8) launch_pass_a<1, 8, P24>(a, item_events, max_items, items, item_count, st, start, stop);
+    else launch_pass_a<1, 16, P24>(a, item_events, max_items, items, item_count, st, start, stop);
 }
 }  // namespace
 
 hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32_t item_events,
                         int max_items, uint4 *items, uint32_t *item_count, uint32_t *hist,
-                        hipStream_t st, int phase) {
+                        hipStream_t st, int phase, hipEvent_t start, hipEvent_t stop) {
     if (a.nr > kPixMaxRanges || a.nr > 1024 || (item_events & 3u) || (a.unit != 1 && a.unit != 2) ||
         (a.ept != 8 && a.ept != 16) || (a.unit == 2 && a.ept != 16))
         return hipErrorInvalidValue;
     if (phase == 0) {
-        if (a.p24) launch_pass_a_shape<true>(a, item_events, max_items, items, item_count, st);
-        else launch_pass_a_shape<false>(a, item_events, max_items, items, item_count, st);
+        if (a.p24) launch_pass_a_shape<true>(a, item_events, max_items, items, item_count, st, start, stop);
+        else launch_pass_a_shape<false>(a, item_events, max_items, items, item_count, st, start, stop);
     } else {
         const size_t sm = pix_acc_smem(s.rb, s.fmax, a.tp.T);
         auto go = [&](auto kern) {
             (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-            hipLaunchKernelGGL(kern, dim3((unsigned)max_items), dim3(1024), sm, st, a,
-                               s.loc + (size_t)replica * a.L, s.fp_off, s.fp_scr, items, item_count,
-                               a.tp.T, hist);
+            hipExtLaunchKernelGGL(kern, dim3((unsigned)max_items), dim3(1024), sm, st, start, stop, 0, a,
+                                  s.loc + (size_t)replica * a.L, s.fp_off, s.fp_scr, items, item_count,
+                                  a.tp.T, hist);
         };
         if (a.p24) {
             if (a.bu == 8) go(k_pix_accumulate<true, 8>); else go(k_pix_accumulate<true, 4>);

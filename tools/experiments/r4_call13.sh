@@ -1,0 +1,5 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_gpu_wavelength.py -x -q --timeout 250 --timeout-method thread > gpurun_out/r4_call13_tests.log 2>&1; rc=$?; tail -2 gpurun_out/r4_call13_tests.log; [ $rc -eq 0 ] || exit $rc
+REPS=3 BENCH_ARGS="--coordinate wavelength" timeout -k 10 500 bash tools/ab.sh

@@ -97,8 +97,12 @@ def main(prof: Path, stem: Path) -> None:
         e = {'members': names, 'calls': n,
              'launches_per_call': {m: round(x, 4) for m, x in zip(names, w)},
              'avg_ms': sum(x * m['avg_ms'] for x, m in zip(w, ms))}
-        if all('avg_ms_steady' in m for m in ms):
-            e['avg_ms_steady'] = sum(x * m['avg_ms_steady'] for x, m in zip(w, ms))
+        # steady state: past each member's first two dispatches; a member
+        # launched only in the warm-up steps (k_pix_count: the first,
+        # counted batch) is not part of the steady step
+        n_last = len(durs.get(members[-1], []))
+        if n_last > 2:
+            e['avg_ms_steady'] = sum(sum(durs[m][2:]) for m in names) / (n_last - 2)
         if all('hbm_traffic_bytes' in m for m in ms):
             for key in ('hbm_read_bytes', 'hbm_write_bytes', 'hbm_traffic_bytes'):
                 e[key] = sum(x * m[key] for x, m in zip(w, ms))
