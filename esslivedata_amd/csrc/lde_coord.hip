@@ -35,12 +35,24 @@
 namespace lde {
 
 // largest b with e[b] <= v < e[b + 1] (half-open, last bin too; NaN dropped)
+// FIXED: the host checked that every bucket's candidate lies within [-1, +2]
+// of the true bin for any value whose bucket index rounds to it (buckets at
+// most half the narrowest bin wide), so one step down and two up, without
+// branches, give the loop's answer and the events of a lane interleave
+template <bool FIXED = false>
 __device__ __forceinline__ int coord_bin(double v, const double *e, const uint16_t *bk, int T,
                                          double e0, double inv_w, int G) {
     if (!(v >= e[0]) || !(v < e[T])) return -1;
     int g = (int)((v - e0) * inv_w);
     g = g < 0 ? 0 : (g >= G ? G - 1 : g);
     int b = bk[g];
+    if (FIXED) {
+        // v < e[T]: an up step never passes b = T - 1, so e[b + 1] stays in range
+        b -= (b > 0 && v < e[b]) ? 1 : 0;
+        b += (v >= e[b + 1]) ? 1 : 0;
+        b += (v >= e[b + 1]) ? 1 : 0;
+        return b;
+    }
     while (b > 0 && v < e[b]) --b;
     while (v >= e[b + 1]) ++b;
     return b;
@@ -196,9 +208,11 @@ __global__ __launch_bounds__(1024) void k_event_coord(CoordArgs a, const int *__
 // ---------------------------------------------------------------------------
 // keyed pass: coordinate bin + pixel word -> the sieve's final word per event
 // ---------------------------------------------------------------------------
+// per slot the pixel's grid coordinate x = (d - d0) * inv_dd, the event
+// pass's first two operations (same operations, no contraction: same bits)
 __global__ __launch_bounds__(256) void k_key_dist(const uint32_t *__restrict__ tab, int cbits,
-                                                  const double *__restrict__ pix_d, unsigned L,
-                                                  double *__restrict__ tab_d) {
+                                                  const double *__restrict__ pix_d, unsigned L, double d0,
+                                                  double inv_dd, double *__restrict__ tab_d) {
     const unsigned j = blockIdx.x * 256u + threadIdx.x;
     if (j >= (1u << cbits)) return;
     const uint32_t w = tab[j];
@@ -207,7 +221,7 @@ __global__ __launch_bounds__(256) void k_key_dist(const uint32_t *__restrict__ t
         const unsigned q = (((w >> kSieveTagShift) & 0xFFu) << cbits) | j;
         if (q < L) d = pix_d[q];
     }
-    tab_d[j] = d;
+    tab_d[j] = (d - d0) * inv_dd;
 }
 
 // LDS: pixel table (C words) | slot distances (C doubles) | edges | table | buckets
@@ -224,7 +238,7 @@ size_t key_smem(const KeyArgs &a, bool table_lds) {
 // its word and distance), else two gathers (word, distance; none for ids
 // outside the LUT); the coordinate bin as in k_event_coord; the word
 // (tag bits cleared) plus the bin, or 0 when the pixel or the bin is invalid.
-template <bool TLDS, bool ELDS>
+template <bool TLDS, bool ELDS, bool FIXED>
 __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     extern __shared__ double sm[];
     const CoordArgs &a = k.c;
@@ -251,8 +265,8 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     const uint32_t cmask = C - 1u;
     const uint32_t pid_off = (uint32_t)a.pid_off;
     const uint32_t Lc = a.L;
-    auto coord = [&](double d, int t) __attribute__((always_inline)) {
-        const double x = (d - a.d0) * a.inv_dd;
+    // x: the pixel's grid coordinate (k_key_dist / k_key_records)
+    auto coord = [&](double x, int t) __attribute__((always_inline)) {
         const double y = ((double)t - a.t0) * a.inv_dt;
         int bin = -1;
         if (x >= 0.0 && x <= xmax && y >= 0.0 && y <= ymax) {
@@ -267,7 +281,9 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
             const double v00 = r0[0], v01 = r0[1], v10 = r1[0], v11 = r1[1];
             const double ra = v00 + fy * (v01 - v00);
             const double rb = v10 + fy * (v11 - v10);
-            bin = coord_bin(ra + fx * (rb - ra), e, s_b, a.T, a.e0, a.inv_w, a.G);
+            const double v = ra + fx * (rb - ra);
+            bin = FIXED ? coord_bin<true>(v, e, s_b, a.T, a.e0, a.inv_w, a.G)
+                        : coord_bin<false>(v, e, s_b, a.T, a.e0, a.inv_w, a.G);
         }
         return bin;
     };
@@ -323,7 +339,7 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
             const bool hit = ((tw >> kSieveTagShift) & 0xFFu) == (pq >> k.cbits);
             // hits and ids outside the LUT load out of range (no request, 0);
             // the word of an id outside the LUT is 0 (dropped)
-            const bool skip = hit || pq >= Lc;
+            const bool skip = hit || pq >= Lc || (LDE_DIAG(k.ablate) & 1);
             const v3u r = __builtin_amdgcn_raw_buffer_load_b96(rrs, skip ? (int)0x80000000 : (int)(pq * 12u),
                                                                 0, 0);
             g[q] = r[0];
@@ -342,11 +358,19 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
         for (int q = 0; q < 8; ++q) {
             const double dq = slot[q] != 0xFFFFFFFFu ? s_d[slot[q]] : d[q];
             const uint32_t word = w[q] | g[q];
-            const int b = (word & kSieveValid) ? coord(dq, tc[q]) : -1;
+            const int b = (LDE_DIAG(k.ablate) & 2) ? (int)(((uint32_t)tc[q] ^ (uint32_t)dq) & 63u)
+                          : (word & kSieveValid) ? coord(dq, tc[q]) : -1;
             out[q] = b >= 0 ? (int)(word + (uint32_t)b) : 0;
         }
     };
     auto store = [&](long long c, const int (&out)[8]) __attribute__((always_inline)) {
+        if (LDE_DIAG(k.ablate) & 4) {  // diagnostics: one word per lane kept live, not stored
+            int x = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) x ^= out[q];
+            if (x == 0x7FFFFFFF) k.keys[tid] = x;
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j)
             *reinterpret_cast<int4 *>(k.keys + c * kChunk + ((long long)j * 1024 + tid) * 4) =
@@ -409,35 +433,37 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
 // L2/MALL-resident for the Zipf tail's random misses
 __global__ __launch_bounds__(256) void k_key_records(const uint32_t *__restrict__ glut,
                                                      const double *__restrict__ pix_d, unsigned L,
+                                                     double d0, double inv_dd,
                                                      uint32_t *__restrict__ rec) {
     const unsigned q = blockIdx.x * 256u + threadIdx.x;
     if (q > L) return;
-    const double d = q < L ? pix_d[q] : __builtin_nan("");
+    const double d = ((q < L ? pix_d[q] : __builtin_nan("")) - d0) * inv_dd;  // x, as k_key_dist
     const unsigned long long b = __builtin_bit_cast(unsigned long long, d);
     rec[3 * (size_t)q] = q < L ? glut[q] : 0u;
     rec[3 * (size_t)q + 1] = (uint32_t)b;
     rec[3 * (size_t)q + 2] = (uint32_t)(b >> 32);
 }
 
-hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, uint32_t *rec,
-                              hipStream_t st) {
-    hipLaunchKernelGGL(k_key_records, dim3((L + 1u + 255u) / 256u), dim3(256), 0, st, glut, pix_d, L, rec);
+hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, double d0,
+                              double inv_dd, uint32_t *rec, hipStream_t st) {
+    hipLaunchKernelGGL(k_key_records, dim3((L + 1u + 255u) / 256u), dim3(256), 0, st, glut, pix_d, L, d0,
+                       inv_dd, rec);
     return hipGetLastError();
 }
 
 hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix_d, unsigned L,
-                           double *tab_d, hipStream_t st, hipEvent_t start) {
+                           double d0, double inv_dd, double *tab_d, hipStream_t st, hipEvent_t start) {
     hipExtLaunchKernelGGL(k_key_dist, dim3(((1u << cbits) + 255) / 256), dim3(256), 0, st, start, nullptr, 0,
-                          pix_tab, cbits, pix_d, L, tab_d);
+                          pix_tab, cbits, pix_d, L, d0, inv_dd, tab_d);
     return hipGetLastError();
 }
 
-template <bool TLDS, bool ELDS>
+template <bool TLDS, bool ELDS, bool FIXED>
 static void launch_key_t(const KeyArgs &a, size_t sm, int grid, hipStream_t st, hipEvent_t stop) {
-    (void)hipFuncSetAttribute((const void *)k_event_key<TLDS, ELDS>,
+    (void)hipFuncSetAttribute((const void *)k_event_key<TLDS, ELDS, FIXED>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipExtLaunchKernelGGL((k_event_key<TLDS, ELDS>), dim3((unsigned)grid), dim3(1024), sm, st, nullptr, stop, 0,
-                          a);
+    hipExtLaunchKernelGGL((k_event_key<TLDS, ELDS, FIXED>), dim3((unsigned)grid), dim3(1024), sm, st, nullptr,
+                          stop, 0, a);
 }
 
 hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent_t stop) {
@@ -446,12 +472,16 @@ hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent
     const size_t sm = key_smem(a, tl);
     if (sm > kCoordSmemMax) return hipErrorInvalidValue;
     if (grid > a.n_chunks) grid = (int)a.n_chunks;
+    // branch-free bin correction only with the edges in LDS (the common case)
+    const bool fx = a.c.fixed_bin && a.c.edges_lds;
     if (tl) {
-        if (a.c.edges_lds) launch_key_t<true, true>(a, sm, grid, st, stop);
-        else launch_key_t<true, false>(a, sm, grid, st, stop);
+        if (fx) launch_key_t<true, true, true>(a, sm, grid, st, stop);
+        else if (a.c.edges_lds) launch_key_t<true, true, false>(a, sm, grid, st, stop);
+        else launch_key_t<true, false, false>(a, sm, grid, st, stop);
     } else {
-        if (a.c.edges_lds) launch_key_t<false, true>(a, sm, grid, st, stop);
-        else launch_key_t<false, false>(a, sm, grid, st, stop);
+        if (fx) launch_key_t<false, true, true>(a, sm, grid, st, stop);
+        else if (a.c.edges_lds) launch_key_t<false, true, false>(a, sm, grid, st, stop);
+        else launch_key_t<false, false, false>(a, sm, grid, st, stop);
     }
     return hipGetLastError();
 }

@@ -174,8 +174,8 @@ struct lde_handle {
     // keyed wavelength pass (SIEVE path): one k_event_key launch emits the
     // sieve's finished words (LDE_COORD_KEYED, default 1)
     bool coord_keyed = true;
-    double *d_key_dist = nullptr;  // [1 << cache_bits] distance of each pixel-table slot
-    uint32_t *d_key_rec = nullptr;  // [L + 1] x 12 B {word, distance} of the batch's replica
+    double *d_key_dist = nullptr;  // [1 << cache_bits] grid coordinate x of each pixel-table slot
+    uint32_t *d_key_rec = nullptr;  // [L + 1] x 12 B {word, x} of the batch's replica
     // PIXEL strategy (lde_pixel.hip): pixel-range footprints built from the LUT
     bool pixel_ok = false;
     lde::PixSetup pix{};
@@ -237,6 +237,13 @@ struct lde_handle {
     // copy command and no cache flush in front of one follows the kernel
     unsigned char *hd_pack = nullptr;
     hipEvent_t fin_event = nullptr;  // system-scope release after the kernel
+    // split finalize: running cumulative row sums {in range, all bins} per
+    // screen (valid while only the split finalize's fold writes d_cum), and the
+    // event the host waits for (the outputs, not the fold behind them)
+    unsigned long long *d_cum_rows = nullptr;
+    bool cum_rows_valid = false;
+    int fin_split = 0;  // LDE_FIN_SPLIT (diagnostics build)
+    hipEvent_t ready_event = nullptr;
     hipEvent_t block_event = nullptr;  // blocking-sync event: waits past the spin budget
     double wait_pred_us = 0.0;         // predicted stream wait of a finalize (EMA)
     long long waits_blocked = 0, waits_total = 0;
@@ -344,7 +351,7 @@ long long env_ll(const char *name, long long dflt) {
 int check_knobs() {
 #ifndef LDE_DIAGNOSTICS
     static const char *const diag[] = {"LDE_ABLATE", "LDE_SIEVE_ABLATE", "LDE_COLD_SORT_ABLATE",
-                                       "LDE_PIX_ABLATE"};
+                                       "LDE_PIX_ABLATE", "LDE_KEY_ABLATE"};
     for (const char *n : diag)
         if (const char *v = std::getenv(n); v && std::atoll(v) != 0)
             return fail(nullptr, LDE_EINVAL,
@@ -385,11 +392,14 @@ int check_knobs() {
 //   * block on an interrupt-driven (hipEventBlockingSync) event.
 // A steady stream of batches spins ~kWakeUs per finalize; a wait with no
 // history, or longer than predicted, spins kSpinCapUs and then sleeps.
-hipError_t wait_stream(lde_handle *h) {
+// ev (optional): wait for that event instead of the whole stream (created
+// with hipEventBlockingSync, so the blocking fallback sleeps on it)
+hipError_t wait_stream(lde_handle *h, hipEvent_t ev = nullptr) {
     using clk = std::chrono::steady_clock;
     constexpr double kWakeUs = 100.0;    // wake this long before the predicted end
     constexpr double kSpinCapUs = 150.0; // spin budget before the blocking wait
-    hipError_t e = hipStreamQuery(h->stream);
+    auto query = [&]() { return ev ? hipEventQuery(ev) : hipStreamQuery(h->stream); };
+    hipError_t e = query();
     if (e != hipErrorNotReady) return e;
     ++h->waits_total;
     const auto t0 = clk::now();
@@ -399,7 +409,7 @@ hipError_t wait_stream(lde_handle *h) {
     const double pred = h->wait_pred_us;
     if (pred > 2.0 * kWakeUs) {
         std::this_thread::sleep_for(std::chrono::microseconds((long long)(pred - kWakeUs)));
-        e = hipStreamQuery(h->stream);
+        e = query();
         if (e != hipErrorNotReady) {
             // done before the wake-up: the end is unknown, move the prediction earlier
             h->wait_pred_us = 0.8 * pred + 0.2 * std::min(pred, 0.8 * since(t0));
@@ -408,10 +418,14 @@ hipError_t wait_stream(lde_handle *h) {
     }
     const auto ts = clk::now();
     bool blocked = false;
-    while ((e = hipStreamQuery(h->stream)) == hipErrorNotReady) {
+    while ((e = query()) == hipErrorNotReady) {
         if (since(ts) > kSpinCapUs) {
             blocked = true;
             ++h->waits_blocked;
+            if (ev) {
+                e = hipEventSynchronize(ev);
+                break;
+            }
             if (!h->block_event) {
                 e = hipEventCreateWithFlags(&h->block_event,
                                             hipEventBlockingSync | hipEventDisableTiming);
@@ -1169,12 +1183,13 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
                 if (int rc = dev_alloc(h, &h->d_key_dist, (size_t)1 << h->cache_bits)) return rc;
             const uint32_t *tab_r = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
             Stamp sp(h, LDE_K_COORD);  // key_dist .. event_key, stamped by the dispatches
-            HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->d_key_dist,
-                                            h->stream, sp.a));
+            HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->cargs.d0,
+                                            h->cargs.inv_dd, h->d_key_dist, h->stream, sp.a));
             if (!h->d_key_rec)
                 if (int rc = dev_alloc(h, &h->d_key_rec, 3 * ((size_t)h->L + 1))) return rc;
             HIPCALL(h, lde::launch_key_records(h->d_glut + (size_t)(h->L + 1) * replica, h->d_cpd,
-                                               (unsigned)h->L, h->d_key_rec, h->stream));
+                                               (unsigned)h->L, h->cargs.d0, h->cargs.inv_dd, h->d_key_rec,
+                                               h->stream));
             lde::KeyArgs ka;
             ka.c = h->cargs;
             ka.segs = h->d_segs;
@@ -1187,6 +1202,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             ka.cbits = h->cache_bits;
             ka.keys = h->d_cbin;
             ka.dummy = h->d_sieve_dummy;
+            ka.ablate = (int)env_ll("LDE_KEY_ABLATE", 0);
             HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream, sp.b));
             ksd.push_back({h->d_cbin, h->d_cbin, chunks * lde::kChunk, 0});
         }
@@ -1794,6 +1810,7 @@ int zero_state(lde_handle *h) {
     const size_t nb = (size_t)h->nbins;
     HIPCALL(h, hipMemsetAsync(h->d_win32, 0, nb * 4, h->stream));
     HIPCALL(h, hipMemsetAsync(h->d_cum, 0, nb * 8, h->stream));
+    h->cum_rows_valid = false;
     if (h->d_win64) HIPCALL(h, hipMemsetAsync(h->d_win64, 0, nb * 8, h->stream));
     if (h->d_winf) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
     if (h->d_cumf) HIPCALL(h, hipMemsetAsync(h->d_cumf, 0, nb * 4, h->stream));
@@ -1848,6 +1865,7 @@ void release(lde_handle *h) {
     dev_free(h->d_win32);
     dev_free(h->d_win64);
     dev_free(h->d_cum);
+    dev_free(h->d_cum_rows);
     dev_free(h->d_winf);
     dev_free(h->d_cumf);
     dev_free(h->d_spid);
@@ -1927,6 +1945,8 @@ void release(lde_handle *h) {
     h->hd_pack = nullptr;
     if (h->fin_event) (void)hipEventDestroy(h->fin_event);
     h->fin_event = nullptr;
+    if (h->ready_event) (void)hipEventDestroy(h->ready_event);
+    h->ready_event = nullptr;
     if (h->block_event) (void)hipEventDestroy(h->block_event);
     h->block_event = nullptr;
     dev_free(h->d_snap);
@@ -2126,6 +2146,8 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     } else {
         CREATE_HIP(hipHostMalloc((void **)&h->h_pack, h->pack_bytes, hipHostMallocDefault));
     }
+    CREATE_HIP(hipEventCreateWithFlags(&h->ready_event, hipEventDisableTiming | hipEventBlockingSync));
+    h->fin_split = (int)env_ll("LDE_FIN_SPLIT", 0);  // measured +6.5 us per DREAM step: off
     h->d_img_cur = h->d_pack;
     h->d_img_cum = h->d_pack + (size_t)h->S * 8;
     CREATE_CHECK(zero_state(h));
@@ -2661,7 +2683,38 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
                                       hipMemcpyDeviceToHost, h->stream));
     }
     int n_parts = 0;
-    {
+    // split finalize: the host waits only for the images and totals (the
+    // window's rows); the window's fold into the cumulative histogram runs
+    // behind the ready event, while the host turns around
+    const bool split = !f32 && !want_cur_hist && !want_cum_hist && h->fin_split &&
+                       lde::finalize_split_ok(h->T);
+    if (split) {
+        unsigned char *d_tail = pk + (size_t)h->S * 16;
+        if (!h->d_cum_rows)
+            if (int rc = dev_alloc(h, &h->d_cum_rows, 2 * (size_t)h->S)) return rc;
+        if (!h->cum_rows_valid) {
+            HIPCALL(h, lde::launch_cum_rows(h->d_cum, h->S, h->T, h->range_lo, h->range_hi, h->d_cum_rows,
+                                            h->stream));
+            h->cum_rows_valid = true;
+        }
+        {
+            Stamp sp(h, LDE_K_FINALIZE);
+            HIPCALL(h, lde::launch_finalize_rows(
+                           0, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum_rows, h->S, h->T,
+                           h->range_lo, h->range_hi, out->current_image ? img_cur : nullptr,
+                           out->cumulative_image ? img_cum : nullptr, h->d_overflow,
+                           (uint32_t *)(d_tail + 32), (unsigned long long *)(d_tail + 48), &n_parts,
+                           h->stream, sp.a, sp.b));
+        }
+        if (!h->hd_pack)
+            HIPCALL(h, hipMemcpyAsync(h->h_pack, h->d_pack, (size_t)h->S * 16 + 48 + 32 * (size_t)n_parts,
+                                      hipMemcpyDeviceToHost, h->stream));
+        HIPCALL(h, hipEventRecord(h->ready_event, h->stream));
+        HIPCALL(h, lde::launch_fold_cumulative(h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
+                                               h->nbins, h->stream));
+        HIPCALL(h, wait_stream(h, h->ready_event));
+    } else {
+        h->cum_rows_valid = false;
         Timed tm(h, LDE_K_FINALIZE);
         // the per-block total partials and the overflow flag land in the
         // pack (summed here on the host: no k_sum_totals launch and gap)
@@ -2675,7 +2728,9 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
                        h->stream, (unsigned long long *)(d_tail + 48), &n_parts));
     }
     const size_t isz = f32 ? 4 : 8;
-    if (h->hd_pack) {
+    if (split) {
+        // waited above
+    } else if (h->hd_pack) {
         // a system-scope release after the kernel: its host writes are visible
         // once the stream has passed this point
         HIPCALL(h, hipEventRecord(h->fin_event, h->stream));
@@ -2698,7 +2753,7 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
         convert_u64(tmp.data(), out->cumulative_hist, (long long)nb, LDE_F64);
     }
     if (f32) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
-    HIPCALL(h, wait_stream(h));
+    if (!split) HIPCALL(h, wait_stream(h));
     const auto t_waited = h->probe ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
     struct PostProbe {
         lde_handle *h;
@@ -2741,6 +2796,7 @@ int lde_finalize_partials(lde_handle *h, void *d_out) {
                                         h->d_cum, nullptr, h->S, h->T, h->range_lo, h->range_hi,
                                         o, o + h->S, h->d_tot4, o + 2 * h->S, nullptr, nullptr,
                                         h->stream));
+        h->cum_rows_valid = false;
     }
     if (h->out_dtype == LDE_F32)  // the window's f32 accumulator restarts too
         HIPCALL(h, hipMemsetAsync(h->d_winf, 0, (size_t)h->nbins * 4, h->stream));
@@ -3020,6 +3076,20 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
         int b = (int)(std::upper_bound(ed.begin(), ed.end(), x) - ed.begin()) - 1;
         buck[(size_t)g] = (uint16_t)std::min(std::max(b, 0), std::min(T - 1, 65535));
     }
+    // branch-free correction (coord_bin<true>): one step down, two up cover
+    // every value whose bucket index rounds to g, even one bucket off either
+    // way, when bin(e0 + (g - 1) w) >= buck[g] - 1 and bin(e0 + (g + 2) w) <=
+    // buck[g] + 2 for every g (bins of the clamped, sorted edges)
+    auto bin_of = [&](double x) {
+        if (!(x >= ed[0])) return 0;
+        if (!(x < ed[(size_t)T])) return T - 1;
+        return std::max(0, (int)(std::upper_bound(ed.begin(), ed.end(), x) - ed.begin()) - 1);
+    };
+    bool fixed_bin = span > 0 && std::isfinite(span) && env_ll("LDE_COORD_FIXED_BIN", 1) != 0;
+    for (int g = 0; g < G && fixed_bin; ++g) {
+        const int lo_b = bin_of(ed[0] + (g - 1) * w), hi_b = bin_of(ed[0] + (g + 2) * w);
+        if (lo_b < (int)buck[(size_t)g] - 1 || hi_b > (int)buck[(size_t)g] + 2) fixed_bin = false;
+    }
     const size_t nt = (size_t)lut->n_dist * (size_t)lut->n_time;
     if (int rc = dev_alloc(h, &st.cpd, (size_t)n_pix)) return rc;
     if (int rc = dev_alloc(h, &st.ctable, nt)) return rc;
@@ -3070,6 +3140,7 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     c.G = G;
     c.e0 = ed[0];
     c.inv_w = 1.0 / w;
+    c.fixed_bin = fixed_bin ? 1 : 0;
     c.edges_lds = 1;
     if (lde::coord_smem(c, false, false) > lde::kCoordSmemMax) c.edges_lds = 0;  // huge T: edges from HBM
     c.cus = h->cus;

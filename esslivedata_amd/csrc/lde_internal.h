@@ -315,6 +315,18 @@ hipError_t launch_merge_f32_u64(const unsigned long long *src, unsigned long lon
 hipError_t launch_push_export(uint32_t *batch, unsigned long long *out, long long n, hipStream_t st);
 hipError_t launch_sum3(const unsigned long long *a, const unsigned long long *b, const uint32_t *c,
                        unsigned long long *out, long long n, hipStream_t st);
+// split finalize (lde_maint.hip): the rows part the host waits for, then the
+// fold of the window into the cumulative histogram
+bool finalize_split_ok(int T);
+hipError_t launch_finalize_rows(int img_kind, const uint32_t *win32, const unsigned long long *win64,
+                                unsigned long long *cum_rows, long long S, int T, int lo, int hi,
+                                void *cur_img, void *cum_img, const uint32_t *ovf_src, uint32_t *ovf_dst,
+                                unsigned long long *host_parts, int *n_parts, hipStream_t st,
+                                hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+hipError_t launch_fold_cumulative(uint32_t *win32, unsigned long long *win64, unsigned long long *cum,
+                                  long long nbins, hipStream_t st);
+hipError_t launch_cum_rows(const unsigned long long *cum, long long S, int T, int lo, int hi,
+                           unsigned long long *cum_rows, hipStream_t st);
 hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *win64,
                            unsigned long long *cum, unsigned long long *snap, long long S, int T,
                            int lo, int hi, void *cur_img, void *cum_img,
@@ -347,6 +359,8 @@ struct CoordArgs {
     const uint16_t *buckets;  // [G] first candidate bin per bucket of the edge range
     int G;
     double e0, inv_w;       // bucket g = (v - e0) * inv_w
+    int fixed_bin = 0;      // 1: every bucket's candidate is within [-1, +2] of the
+                            // true bin (checked on the host): branch-free correction
     const uint32_t *cache_q = nullptr;  // [1 << cache_bits] cached pixel per slot (-1: none)
     const double *cache_d = nullptr;    // its distance
     int cache_bits = 0;                 // 0: no distance cache
@@ -373,20 +387,24 @@ struct KeyArgs {
     long long n_chunks;
     const uint32_t *glut;     // this replica's pixel words, L + 1 entries (entry L = 0)
     const uint32_t *pix_tab;  // this replica's LDS pixel-table image (1 << cbits words)
-    const double *tab_d;      // distance of each table slot's pixel (1 << cbits)
-    const uint32_t *rec;      // per pixel 12 bytes {word, distance lo, hi}, L + 1 entries (k_key_records)
+    const double *tab_d;      // grid coordinate x of each table slot's pixel (1 << cbits)
+    const uint32_t *rec;      // per pixel 12 bytes {word, x lo, hi}, L + 1 entries (k_key_records)
     int cbits;
     int *keys;                // [n_chunks * kChunk]
     const int *dummy;         // kChunk x (pid_off - 1): the all-invalid chunk
+    int ablate = 0;           // diagnostics build (LDE_KEY_ABLATE): 1 no gathers, 2 no
+                              // coordinate arithmetic, 4 no stores (results invalid)
 };
 constexpr int kKeyLdsChunks = 128;  // k_event_key: chunk pointers per LDS window
 size_t key_smem(const KeyArgs &a, bool table_lds);
 hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent_t stop = nullptr);
 // distance of every pixel-table slot's pixel (NaN for empty slots)
+// x = (d - d0) * inv_dd of every pixel-table slot's pixel (NaN for empty slots)
 hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix_d, unsigned L,
-                           double *tab_d, hipStream_t st, hipEvent_t start = nullptr);
-hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, uint32_t *rec,
-                              hipStream_t st);
+                           double d0, double inv_dd, double *tab_d, hipStream_t st,
+                           hipEvent_t start = nullptr);
+hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, double d0,
+                              double inv_dd, uint32_t *rec, hipStream_t st);
 
 // PIXEL strategy (lde_pixel.hip): events partitioned by pixel range, the
 // LUT lookup done in pass B from the range's LDS slice
