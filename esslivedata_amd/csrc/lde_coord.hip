@@ -47,15 +47,27 @@ __device__ __forceinline__ int coord_bin(double v, const double *e, const uint16
     g = g < 0 ? 0 : (g >= G ? G - 1 : g);
     int b = bk[g];
     if (FIXED) {
-        // v < e[T]: an up step never passes b = T - 1, so e[b + 1] stays in range
-        b -= (b > 0 && v < e[b]) ? 1 : 0;
-        b += (v >= e[b + 1]) ? 1 : 0;
-        b += (v >= e[b + 1]) ? 1 : 0;
-        return b;
+        // true bin in [b - 1, b + 2]: below b iff v < e[b] (b > 0; at b = 0
+        // v >= e[0] holds), else b plus the edges e[b + 1], e[b + 2] <= v;
+        // the three reads are independent (e[T + 1] = +inf pads the table)
+        const double lo = e[b], h1 = e[b + 1], h2 = e[b + 2];
+        return b - ((v < lo) ? 1 : 0) + ((v >= h1) ? 1 : 0) + ((v >= h2) ? 1 : 0);
     }
     while (b > 0 && v < e[b]) --b;
     while (v >= e[b + 1]) ++b;
     return b;
+}
+
+// coord_bin<true> with the outer edges held in registers (e_first = e[0],
+// e_last = e[T]): two LDS reads fewer per event
+__device__ __forceinline__ int coord_bin_fast(double v, const double *e, const uint16_t *bk, double e_first,
+                                              double e_last, double e0, double inv_w, int G) {
+    if (!(v >= e_first) || !(v < e_last)) return -1;
+    int g = (int)((v - e0) * inv_w);
+    g = g < 0 ? 0 : (g >= G ? G - 1 : g);
+    const int b = bk[g];
+    const double lo = e[b], h1 = e[b + 1], h2 = e[b + 2];
+    return b - ((v < lo) ? 1 : 0) + ((v >= h1) ? 1 : 0) + ((v >= h2) ? 1 : 0);
 }
 
 // Distance cache image: slot j holds the most-sampled pixel q = j (mod C)
@@ -209,10 +221,22 @@ __global__ __launch_bounds__(1024) void k_event_coord(CoordArgs a, const int *__
 // keyed pass: coordinate bin + pixel word -> the sieve's final word per event
 // ---------------------------------------------------------------------------
 // per slot the pixel's grid coordinate x = (d - d0) * inv_dd, the event
-// pass's first two operations (same operations, no contraction: same bits)
+// pass's first two operations (same operations, no contraction: same bits).
+// pre (KeyArgs::pre): the distance row instead, i = min(floor(x), nd - 2) into
+// tab_i (0xFF: x outside [0, nd - 1] or NaN) and fx = x - i into tab_d, the
+// event pass's next five operations
+__device__ __forceinline__ void key_row(double x, int nd, double &fx, uint32_t &i) {
+    const double xmax = (double)(nd - 1);
+    int r = (int)floor(x);
+    if (r > nd - 2) r = nd - 2;
+    fx = x - (double)r;
+    i = (x >= 0.0 && x <= xmax) ? (uint32_t)r : 0xFFu;
+}
+
 __global__ __launch_bounds__(256) void k_key_dist(const uint32_t *__restrict__ tab, int cbits,
                                                   const double *__restrict__ pix_d, unsigned L, double d0,
-                                                  double inv_dd, double *__restrict__ tab_d) {
+                                                  double inv_dd, int pre_nd, double *__restrict__ tab_d,
+                                                  uint8_t *__restrict__ tab_i) {
     const unsigned j = blockIdx.x * 256u + threadIdx.x;
     if (j >= (1u << cbits)) return;
     const uint32_t w = tab[j];
@@ -221,15 +245,24 @@ __global__ __launch_bounds__(256) void k_key_dist(const uint32_t *__restrict__ t
         const unsigned q = (((w >> kSieveTagShift) & 0xFFu) << cbits) | j;
         if (q < L) d = pix_d[q];
     }
-    tab_d[j] = (d - d0) * inv_dd;
+    const double x = (d - d0) * inv_dd;
+    if (pre_nd) {
+        double fx;
+        uint32_t i;
+        key_row(x, pre_nd, fx, i);
+        tab_d[j] = fx;
+        tab_i[j] = (uint8_t)i;
+    } else {
+        tab_d[j] = x;
+    }
 }
 
 // LDS: pixel table (C words) | slot distances (C doubles) | edges | table | buckets
 size_t key_smem(const KeyArgs &a, bool table_lds) {
     const size_t C = (size_t)1 << a.cbits;
-    const int ne = a.c.edges_lds ? a.c.T + 1 : 0;
+    const int ne = a.c.edges_lds ? a.c.T + 2 : 0;
     return 12 * C + 8 * (size_t)((ne + 1) & ~1) + (table_lds ? 8 * (size_t)a.c.nd * a.c.nt : 0) +
-           2 * (size_t)((a.c.G + 7) & ~7) + 16 * (size_t)kKeyLdsChunks;
+           2 * (size_t)((a.c.G + 7) & ~7) + 16 * (size_t)kKeyLdsChunks + (a.pre ? C : 0);
 }
 
 // One block per CU walks a contiguous range of the batch's global chunks;
@@ -238,7 +271,7 @@ size_t key_smem(const KeyArgs &a, bool table_lds) {
 // its word and distance), else two gathers (word, distance; none for ids
 // outside the LUT); the coordinate bin as in k_event_coord; the word
 // (tag bits cleared) plus the bin, or 0 when the pixel or the bin is invalid.
-template <bool TLDS, bool ELDS, bool FIXED>
+template <bool TLDS, bool ELDS, bool FAST>
 __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     extern __shared__ double sm[];
     const CoordArgs &a = k.c;
@@ -246,35 +279,41 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     uint32_t *s_w = reinterpret_cast<uint32_t *>(sm);
     double *s_d = sm + C / 2;
     double *s_e = s_d + C;
-    const int ne = ELDS ? a.T + 1 : 0;
+    const int ne = ELDS ? a.T + 2 : 0;  // + e[T + 1] = +inf (FAST bin correction)
     double *s_t = s_e + ((ne + 1) & ~1);
     const int ntab = TLDS ? a.nd * a.nt : 0;
     uint16_t *s_b = reinterpret_cast<uint16_t *>(s_t + ntab);
+    // FAST: per slot the distance row (u8, after the chunk pointers) and fx
+    uint8_t *s_i = reinterpret_cast<uint8_t *>(s_b + ((a.G + 7) & ~7)) + 16 * kKeyLdsChunks;
     for (uint32_t i = threadIdx.x; i < C; i += blockDim.x) {
         s_w[i] = k.pix_tab[i];
         s_d[i] = k.tab_d[i];
+        if (FAST) s_i[i] = k.tab_i[i];
     }
-    for (int i = threadIdx.x; i < ne; i += blockDim.x) s_e[i] = a.edges[i];
+    for (int i = threadIdx.x; i < ne; i += blockDim.x) s_e[i] = i <= a.T ? a.edges[i] : __builtin_inf();
     for (int i = threadIdx.x; i < ntab; i += blockDim.x) s_t[i] = a.table[i];
     for (int i = threadIdx.x; i < a.G; i += blockDim.x) s_b[i] = a.buckets[i];
     __syncthreads();
     const double *e = ELDS ? s_e : a.edges;
     const double *tab = TLDS ? s_t : a.table;
+    const double e_first = FAST ? e[0] : 0.0, e_last = FAST ? e[a.T] : 0.0;
     const double xmax = (double)(a.nd - 1), ymax = (double)(a.nt - 1);
     const __amdgpu_buffer_rsrc_t rrs = coord_rsrc(k.rec, (a.L + 1u) * 12u);
     const uint32_t cmask = C - 1u;
     const uint32_t pid_off = (uint32_t)a.pid_off;
     const uint32_t Lc = a.L;
-    // x: the pixel's grid coordinate (k_key_dist / k_key_records)
-    auto coord = [&](double x, int t) __attribute__((always_inline)) {
+    // x: the pixel's grid coordinate (k_key_dist / k_key_records); FAST: x is
+    // fx and ir its distance row (0xFF: x outside the grid), both precomputed
+    auto coord = [&](double x, uint32_t ir, int t) __attribute__((always_inline)) {
         const double y = ((double)t - a.t0) * a.inv_dt;
         int bin = -1;
-        if (x >= 0.0 && x <= xmax && y >= 0.0 && y <= ymax) {
-            int i = (int)floor(x);
-            if (i > a.nd - 2) i = a.nd - 2;
+        const bool xin = FAST ? ir != 0xFFu : (x >= 0.0 && x <= xmax);
+        if (xin && y >= 0.0 && y <= ymax) {
+            int i = FAST ? (int)ir : (int)floor(x);
+            if (!FAST && i > a.nd - 2) i = a.nd - 2;
             int j = (int)floor(y);
             if (j > a.nt - 2) j = a.nt - 2;
-            const double fx = x - (double)i;
+            const double fx = FAST ? x : x - (double)i;
             const double fy = y - (double)j;
             const double *r0 = tab + (size_t)i * a.nt + j;
             const double *r1 = r0 + a.nt;
@@ -282,8 +321,8 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
             const double ra = v00 + fy * (v01 - v00);
             const double rb = v10 + fy * (v11 - v10);
             const double v = ra + fx * (rb - ra);
-            bin = FIXED ? coord_bin<true>(v, e, s_b, a.T, a.e0, a.inv_w, a.G)
-                        : coord_bin<false>(v, e, s_b, a.T, a.e0, a.inv_w, a.G);
+            bin = FAST ? coord_bin_fast(v, e, s_b, e_first, e_last, a.e0, a.inv_w, a.G)
+                       : coord_bin<false>(v, e, s_b, a.T, a.e0, a.inv_w, a.G);
         }
         return bin;
     };
@@ -356,10 +395,13 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const double dq = slot[q] != 0xFFFFFFFFu ? s_d[slot[q]] : d[q];
-            const uint32_t word = w[q] | g[q];
+            const bool h = slot[q] != 0xFFFFFFFFu;
+            const double dq = h ? s_d[slot[q]] : d[q];
+            // FAST: a record's distance row rides in its word's (zero) tag bits
+            const uint32_t ir = FAST ? (h ? (uint32_t)s_i[slot[q]] : (g[q] >> kSieveTagShift) & 0xFFu) : 0u;
+            const uint32_t word = w[q] | (FAST ? g[q] & ~(0xFFu << kSieveTagShift) : g[q]);
             const int b = (LDE_DIAG(k.ablate) & 2) ? (int)(((uint32_t)tc[q] ^ (uint32_t)dq) & 63u)
-                          : (word & kSieveValid) ? coord(dq, tc[q]) : -1;
+                          : (word & kSieveValid) ? coord(dq, ir, tc[q]) : -1;
             out[q] = b >= 0 ? (int)(word + (uint32_t)b) : 0;
         }
     };
@@ -433,28 +475,31 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
 // L2/MALL-resident for the Zipf tail's random misses
 __global__ __launch_bounds__(256) void k_key_records(const uint32_t *__restrict__ glut,
                                                      const double *__restrict__ pix_d, unsigned L,
-                                                     double d0, double inv_dd,
+                                                     double d0, double inv_dd, int pre_nd,
                                                      uint32_t *__restrict__ rec) {
     const unsigned q = blockIdx.x * 256u + threadIdx.x;
     if (q > L) return;
-    const double d = ((q < L ? pix_d[q] : __builtin_nan("")) - d0) * inv_dd;  // x, as k_key_dist
+    double d = ((q < L ? pix_d[q] : __builtin_nan("")) - d0) * inv_dd;  // x, as k_key_dist
+    uint32_t ir = 0;
+    if (pre_nd) key_row(d, pre_nd, d, ir);  // fx; the row in the word's tag bits
     const unsigned long long b = __builtin_bit_cast(unsigned long long, d);
-    rec[3 * (size_t)q] = q < L ? glut[q] : 0u;
+    rec[3 * (size_t)q] = q < L ? (glut[q] | (pre_nd ? ir << kSieveTagShift : 0u)) : 0u;
     rec[3 * (size_t)q + 1] = (uint32_t)b;
     rec[3 * (size_t)q + 2] = (uint32_t)(b >> 32);
 }
 
 hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, double d0,
-                              double inv_dd, uint32_t *rec, hipStream_t st) {
+                              double inv_dd, int pre_nd, uint32_t *rec, hipStream_t st) {
     hipLaunchKernelGGL(k_key_records, dim3((L + 1u + 255u) / 256u), dim3(256), 0, st, glut, pix_d, L, d0,
-                       inv_dd, rec);
+                       inv_dd, pre_nd, rec);
     return hipGetLastError();
 }
 
 hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix_d, unsigned L,
-                           double d0, double inv_dd, double *tab_d, hipStream_t st, hipEvent_t start) {
+                           double d0, double inv_dd, int pre_nd, double *tab_d, uint8_t *tab_i,
+                           hipStream_t st, hipEvent_t start) {
     hipExtLaunchKernelGGL(k_key_dist, dim3(((1u << cbits) + 255) / 256), dim3(256), 0, st, start, nullptr, 0,
-                          pix_tab, cbits, pix_d, L, d0, inv_dd, tab_d);
+                          pix_tab, cbits, pix_d, L, d0, inv_dd, pre_nd, tab_d, tab_i);
     return hipGetLastError();
 }
 
@@ -472,8 +517,10 @@ hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent
     const size_t sm = key_smem(a, tl);
     if (sm > kCoordSmemMax) return hipErrorInvalidValue;
     if (grid > a.n_chunks) grid = (int)a.n_chunks;
-    // branch-free bin correction only with the edges in LDS (the common case)
-    const bool fx = a.c.fixed_bin && a.c.edges_lds;
+    // FAST (branch-free bin correction, precomputed distance rows) only with
+    // the edges in LDS (the common case)
+    const bool fx = a.pre && a.c.fixed_bin && a.c.edges_lds;
+    if (a.pre && !fx) return hipErrorInvalidValue;  // the caller pairs pre with FAST
     if (tl) {
         if (fx) launch_key_t<true, true, true>(a, sm, grid, st, stop);
         else if (a.c.edges_lds) launch_key_t<true, true, false>(a, sm, grid, st, stop);

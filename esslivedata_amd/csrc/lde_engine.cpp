@@ -175,6 +175,7 @@ struct lde_handle {
     // sieve's finished words (LDE_COORD_KEYED, default 1)
     bool coord_keyed = true;
     double *d_key_dist = nullptr;  // [1 << cache_bits] grid coordinate x of each pixel-table slot
+    uint8_t *d_key_tabi = nullptr;  // [1 << cache_bits] distance row of each slot (FAST pass)
     uint32_t *d_key_rec = nullptr;  // [L + 1] x 12 B {word, x} of the batch's replica
     // PIXEL strategy (lde_pixel.hip): pixel-range footprints built from the LUT
     bool pixel_ok = false;
@@ -1182,14 +1183,22 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             if (!h->d_key_dist)
                 if (int rc = dev_alloc(h, &h->d_key_dist, (size_t)1 << h->cache_bits)) return rc;
             const uint32_t *tab_r = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
+            // FAST event pass: fixed bin correction + each pixel's distance row
+            // and fx precomputed (rows fit the record word's 8 tag bits)
+            const bool pre = h->cargs.fixed_bin && h->cargs.edges_lds && h->cargs.nd <= 256 &&
+                             env_ll("LDE_KEY_PRE", 1) != 0;
+            const int pre_nd = pre ? h->cargs.nd : 0;
+            if (pre && !h->d_key_tabi)
+                if (int rc = dev_alloc(h, &h->d_key_tabi, (size_t)1 << h->cache_bits)) return rc;
             Stamp sp(h, LDE_K_COORD);  // key_dist .. event_key, stamped by the dispatches
             HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->cargs.d0,
-                                            h->cargs.inv_dd, h->d_key_dist, h->stream, sp.a));
+                                            h->cargs.inv_dd, pre_nd, h->d_key_dist, h->d_key_tabi, h->stream,
+                                            sp.a));
             if (!h->d_key_rec)
                 if (int rc = dev_alloc(h, &h->d_key_rec, 3 * ((size_t)h->L + 1))) return rc;
             HIPCALL(h, lde::launch_key_records(h->d_glut + (size_t)(h->L + 1) * replica, h->d_cpd,
-                                               (unsigned)h->L, h->cargs.d0, h->cargs.inv_dd, h->d_key_rec,
-                                               h->stream));
+                                               (unsigned)h->L, h->cargs.d0, h->cargs.inv_dd, pre_nd,
+                                               h->d_key_rec, h->stream));
             lde::KeyArgs ka;
             ka.c = h->cargs;
             ka.segs = h->d_segs;
@@ -1198,6 +1207,8 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             ka.glut = h->d_glut + (size_t)(h->L + 1) * replica;
             ka.pix_tab = tab_r;
             ka.tab_d = h->d_key_dist;
+            ka.tab_i = h->d_key_tabi;
+            ka.pre = pre ? 1 : 0;
             ka.rec = h->d_key_rec;
             ka.cbits = h->cache_bits;
             ka.keys = h->d_cbin;
@@ -1850,6 +1861,7 @@ void release(lde_handle *h) {
     dev_free(h->d_cbin);
     dev_free(h->d_key_dist);
     dev_free(h->d_key_rec);
+    dev_free(h->d_key_tabi);
     dev_free(h->d_ploc);
     dev_free(h->d_pfp_off);
     dev_free(h->d_pfp_scr);

@@ -392,6 +392,9 @@ struct KeyArgs {
     int cbits;
     int *keys;                // [n_chunks * kChunk]
     const int *dummy;         // kChunk x (pid_off - 1): the all-invalid chunk
+    const uint8_t *tab_i = nullptr;  // pre: distance row of each slot's pixel (0xFF: outside)
+    int pre = 0;              // 1: tab_d / rec hold fx and the row (k_key_dist / k_key_records
+                              // with pre_nd = nd), the FAST event pass
     int ablate = 0;           // diagnostics build (LDE_KEY_ABLATE): 1 no gathers, 2 no
                               // coordinate arithmetic, 4 no stores (results invalid)
 };
@@ -400,11 +403,12 @@ size_t key_smem(const KeyArgs &a, bool table_lds);
 hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent_t stop = nullptr);
 // distance of every pixel-table slot's pixel (NaN for empty slots)
 // x = (d - d0) * inv_dd of every pixel-table slot's pixel (NaN for empty slots)
+// (pre_nd > 0: fx and the distance row instead, see k_key_dist)
 hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix_d, unsigned L,
-                           double d0, double inv_dd, double *tab_d, hipStream_t st,
-                           hipEvent_t start = nullptr);
+                           double d0, double inv_dd, int pre_nd, double *tab_d, uint8_t *tab_i,
+                           hipStream_t st, hipEvent_t start = nullptr);
 hipError_t launch_key_records(const uint32_t *glut, const double *pix_d, unsigned L, double d0,
-                              double inv_dd, uint32_t *rec, hipStream_t st);
+                              double inv_dd, int pre_nd, uint32_t *rec, hipStream_t st);
 
 // PIXEL strategy (lde_pixel.hip): events partitioned by pixel range, the
 // LUT lookup done in pass B from the range's LDS slice

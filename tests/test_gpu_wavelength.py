@@ -91,6 +91,17 @@ def test_dream_wavelength_matches_oracle(strategy, scale, table_min):
     assert res.cumulative_total == exp['counts_total_cumulative']
 
 
+# keyed SPLIT pass variants (diagnostics build): the general event pass
+# (bin loops, grid coordinate per event) beside the default FAST one
+KEYED_VARIANTS = [{'LDE_KEY_PRE': '0'}, {'LDE_COORD_FIXED_BIN': '0'}]
+
+
+@pytest.mark.parametrize('variant', range(len(KEYED_VARIANTS)))
+def test_dream_wavelength_keyed_variants(variant, knobs):
+    knobs(**KEYED_VARIANTS[variant])
+    test_dream_wavelength_matches_oracle('split', 'log', 77.75)
+
+
 @pytest.mark.parametrize('strategy', STRATEGIES)
 def test_coordinates_on_edges_are_half_open(strategy):
     """Grid nodes carry the edge values themselves: an event at a node has
@@ -239,8 +250,9 @@ def test_monitor_wavelength_mode(unit):
     assert float(out['counts_total'].values) == exp.sum()
 
 
+@pytest.mark.parametrize('strategy', ['atomic', 'split'])
 @pytest.mark.parametrize('kind', ['duplicates', 'many_bins'])
-def test_coordinate_bins_for_unusual_edges(kind):
+def test_coordinate_bins_for_unusual_edges(kind, strategy):
     """Edges with empty (repeated) bins, and 20000 bins (edges too large for
     LDS: read from HBM): the bucketed search still gives scipp's bins."""
     from esslivedata_amd import projection
@@ -258,7 +270,7 @@ def test_coordinate_bins_for_unusual_edges(kind):
     view = projection.logical_lut(dn)
     ltot = (np.arange(64) % nd) * 0.5 + 3.0
     eng = BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
-                        n_screen=view.n_screen, strategy='atomic')
+                        n_screen=view.n_screen, strategy=strategy)
     eng.set_coordinate_lut(ltot, tab, dist0=3.0, dist_step=0.5, time0=0.0, time_step=dt)
     n = 300_000
     pid = rng.integers(1, 65, n).astype(np.int32)
