@@ -309,9 +309,10 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
         int bin = -1;
         const bool xin = FAST ? ir != 0xFFu : (x >= 0.0 && x <= xmax);
         if (xin && y >= 0.0 && y <= ymax) {
-            int i = FAST ? (int)ir : (int)floor(x);
+            // x, y >= 0 here: truncation is the floor (one conversion, no v_floor)
+            int i = FAST ? (int)ir : (int)x;
             if (!FAST && i > a.nd - 2) i = a.nd - 2;
-            int j = (int)floor(y);
+            int j = (int)y;
             if (j > a.nt - 2) j = a.nt - 2;
             const double fx = FAST ? x : x - (double)i;
             const double fy = y - (double)j;
@@ -413,6 +414,21 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
             if (x == 0x7FFFFFFF) k.keys[tid] = x;
             return;
         }
+        if (k.k24) {  // flags (bits 31, 30) to bits 23, 22 above the 22-bit value
+            unsigned char *base = reinterpret_cast<unsigned char *>(k.keys) + (size_t)c * (kChunk * 3);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                uint32_t kk[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t w = (uint32_t)out[j * 4 + q];
+                    kk[q] = ((w >> 30) << kSieveTagShift) | (w & kSieveValueMask);
+                }
+                *(__attribute__((address_space(1))) v3u *)(base + (size_t)(j * 1024 + tid) * 12u) =
+                    v3u{kk[0] | (kk[1] << 24), (kk[1] >> 8) | (kk[2] << 16), (kk[2] >> 16) | (kk[3] << 8)};
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j)
             *reinterpret_cast<int4 *>(k.keys + c * kChunk + ((long long)j * 1024 + tid) * 4) =
@@ -504,15 +520,19 @@ hipError_t launch_key_dist(const uint32_t *pix_tab, int cbits, const double *pix
 }
 
 template <bool TLDS, bool ELDS, bool FIXED>
-static void launch_key_t(const KeyArgs &a, size_t sm, int grid, hipStream_t st, hipEvent_t stop) {
+static void launch_key_t(const KeyArgs &a, size_t sm, int grid, hipStream_t st, hipEvent_t start,
+                         hipEvent_t stop) {
     (void)hipFuncSetAttribute((const void *)k_event_key<TLDS, ELDS, FIXED>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipExtLaunchKernelGGL((k_event_key<TLDS, ELDS, FIXED>), dim3((unsigned)grid), dim3(1024), sm, st, nullptr,
+    hipExtLaunchKernelGGL((k_event_key<TLDS, ELDS, FIXED>), dim3((unsigned)grid), dim3(1024), sm, st, start,
                           stop, 0, a);
 }
 
-hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent_t stop) {
-    if (a.n_chunks <= 0) return stop ? hipEventRecord(stop, st) : hipSuccess;
+hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
+    if (a.n_chunks <= 0) {
+        if (start) (void)hipEventRecord(start, st);
+        return stop ? hipEventRecord(stop, st) : hipSuccess;
+    }
     const bool tl = key_smem(a, true) <= kCoordSmemMax;
     const size_t sm = key_smem(a, tl);
     if (sm > kCoordSmemMax) return hipErrorInvalidValue;
@@ -522,13 +542,13 @@ hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent
     const bool fx = a.pre && a.c.fixed_bin && a.c.edges_lds;
     if (a.pre && !fx) return hipErrorInvalidValue;  // the caller pairs pre with FAST
     if (tl) {
-        if (fx) launch_key_t<true, true, true>(a, sm, grid, st, stop);
-        else if (a.c.edges_lds) launch_key_t<true, true, false>(a, sm, grid, st, stop);
-        else launch_key_t<true, false, false>(a, sm, grid, st, stop);
+        if (fx) launch_key_t<true, true, true>(a, sm, grid, st, start, stop);
+        else if (a.c.edges_lds) launch_key_t<true, true, false>(a, sm, grid, st, start, stop);
+        else launch_key_t<true, false, false>(a, sm, grid, st, start, stop);
     } else {
-        if (fx) launch_key_t<false, true, true>(a, sm, grid, st, stop);
-        else if (a.c.edges_lds) launch_key_t<false, true, false>(a, sm, grid, st, stop);
-        else launch_key_t<false, false, false>(a, sm, grid, st, stop);
+        if (fx) launch_key_t<false, true, true>(a, sm, grid, st, start, stop);
+        else if (a.c.edges_lds) launch_key_t<false, true, false>(a, sm, grid, st, start, stop);
+        else launch_key_t<false, false, false>(a, sm, grid, st, start, stop);
     }
     return hipGetLastError();
 }

@@ -175,6 +175,8 @@ struct lde_handle {
     // sieve's finished words (LDE_COORD_KEYED, default 1)
     bool coord_keyed = true;
     double *d_key_dist = nullptr;  // [1 << cache_bits] grid coordinate x of each pixel-table slot
+    std::vector<char> key_ok;  // per replica: its key tables are current (1: x layout, 2: FAST layout)
+    unsigned char *d_zero24 = nullptr;  // kChunk * 3 zero bytes: the 24-bit keyed stream's dummy chunk
     uint8_t *d_key_tabi = nullptr;  // [1 << cache_bits] distance row of each slot (FAST pass)
     uint32_t *d_key_rec = nullptr;  // [L + 1] x 12 B {word, x} of the batch's replica
     // PIXEL strategy (lde_pixel.hip): pixel-range footprints built from the LUT
@@ -1080,6 +1082,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             }
             b.rows = h->hot_h[(size_t)r];
             HIPCALL(h, lde::launch_hot_pick(b, r, h->stream));
+            if ((size_t)r < h->key_ok.size()) h->key_ok[(size_t)r] = 0;  // new glut / table image
             if (h->sieve_ok)
                 HIPCALL(h, lde::launch_sieve_tables(
                                (const unsigned char *)h->d_lut + (size_t)r * h->L * (h->lut16 ? 2 : 4),
@@ -1177,11 +1180,16 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         // wavelength mode: the keyed pass turns (pid, toa) into the sieve's
         // finished words, one chunk-aligned stream (ssd) the sieve reads
         std::vector<lde::SegDesc> ksd;
+        bool key_w24 = false;
         if (coord_deferred) {
             if (int rc = upload()) return rc;  // k_event_key reads the messages from d_segs
             if (int rc = grow(h, &h->d_cbin, h->cbin_cap, (size_t)chunks * lde::kChunk)) return rc;
+            // per replica: each table slot's distance row / fx (or x) and each
+            // pixel's 12-byte record, built once after the replica's hot-set
+            // selection (or a new coordinate LUT) and reused by its batches
+            const size_t C = (size_t)1 << h->cache_bits;
             if (!h->d_key_dist)
-                if (int rc = dev_alloc(h, &h->d_key_dist, (size_t)1 << h->cache_bits)) return rc;
+                if (int rc = dev_alloc(h, &h->d_key_dist, C * (size_t)h->R)) return rc;
             const uint32_t *tab_r = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
             // FAST event pass: fixed bin correction + each pixel's distance row
             // and fx precomputed (rows fit the record word's 8 tag bits)
@@ -1189,16 +1197,25 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
                              env_ll("LDE_KEY_PRE", 1) != 0;
             const int pre_nd = pre ? h->cargs.nd : 0;
             if (pre && !h->d_key_tabi)
-                if (int rc = dev_alloc(h, &h->d_key_tabi, (size_t)1 << h->cache_bits)) return rc;
-            Stamp sp(h, LDE_K_COORD);  // key_dist .. event_key, stamped by the dispatches
-            HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->cargs.d0,
-                                            h->cargs.inv_dd, pre_nd, h->d_key_dist, h->d_key_tabi, h->stream,
-                                            sp.a));
+                if (int rc = dev_alloc(h, &h->d_key_tabi, C * (size_t)h->R)) return rc;
             if (!h->d_key_rec)
-                if (int rc = dev_alloc(h, &h->d_key_rec, 3 * ((size_t)h->L + 1))) return rc;
-            HIPCALL(h, lde::launch_key_records(h->d_glut + (size_t)(h->L + 1) * replica, h->d_cpd,
-                                               (unsigned)h->L, h->cargs.d0, h->cargs.inv_dd, pre_nd,
-                                               h->d_key_rec, h->stream));
+                if (int rc = dev_alloc(h, &h->d_key_rec, 3 * ((size_t)h->L + 1) * (size_t)h->R)) return rc;
+            if (h->key_ok.size() != (size_t)h->R) h->key_ok.assign((size_t)h->R, 0);
+            double *kd_r = h->d_key_dist + C * (size_t)replica;
+            uint8_t *ki_r = pre ? h->d_key_tabi + C * (size_t)replica : nullptr;
+            uint32_t *kr_r = h->d_key_rec + 3 * ((size_t)h->L + 1) * (size_t)replica;
+            Stamp sp(h, LDE_K_COORD);  // [key_dist, key_records,] event_key, stamped by the dispatches
+            hipEvent_t k_start = sp.a;
+            const char want = pre ? 2 : 1;  // the layout the replica's tables hold
+            if (h->key_ok[(size_t)replica] != want) {
+                HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->cargs.d0,
+                                                h->cargs.inv_dd, pre_nd, kd_r, ki_r, h->stream, k_start));
+                k_start = nullptr;
+                HIPCALL(h, lde::launch_key_records(h->d_glut + (size_t)(h->L + 1) * replica, h->d_cpd,
+                                                   (unsigned)h->L, h->cargs.d0, h->cargs.inv_dd, pre_nd, kr_r,
+                                                   h->stream));
+                h->key_ok[(size_t)replica] = want;
+            }
             lde::KeyArgs ka;
             ka.c = h->cargs;
             ka.segs = h->d_segs;
@@ -1206,20 +1223,31 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             ka.n_chunks = chunks;
             ka.glut = h->d_glut + (size_t)(h->L + 1) * replica;
             ka.pix_tab = tab_r;
-            ka.tab_d = h->d_key_dist;
-            ka.tab_i = h->d_key_tabi;
+            ka.tab_d = kd_r;
+            ka.tab_i = ki_r;
             ka.pre = pre ? 1 : 0;
-            ka.rec = h->d_key_rec;
+            ka.rec = kr_r;
             ka.cbits = h->cache_bits;
             ka.keys = h->d_cbin;
             ka.dummy = h->d_sieve_dummy;
             ka.ablate = (int)env_ll("LDE_KEY_ABLATE", 0);
-            HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream, sp.b));
+            // words packed to 24 bits (flags + the 22-bit value): 3 bytes per
+            // event written and read back instead of 4
+            ka.k24 = env_ll("LDE_KEY_WORD24", 0) != 0 ? 1 : 0;  // measured +-0 (the sieve reads 12-byte groups slower): off
+            if (ka.k24 && !h->d_zero24) {
+                if (int rc = dev_alloc(h, &h->d_zero24, (size_t)lde::kChunk * 3)) return rc;
+                HIPCALL(h, hipMemsetAsync(h->d_zero24, 0, (size_t)lde::kChunk * 3, h->stream));
+            }
+            key_w24 = ka.k24 != 0;
+            HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream, k_start, sp.b));
             ksd.push_back({h->d_cbin, h->d_cbin, chunks * lde::kChunk, 0});
         }
         const std::vector<lde::SegDesc> &ssd = coord_deferred ? ksd : sd;
         lde::SieveArgs sa;
         sa.keyed = coord_deferred ? 1 : 0;
+        sa.keyed24 = key_w24 ? 1 : 0;
+        sa.keyed_base = h->d_cbin;
+        sa.zero24 = h->d_zero24;
         sa.segs = h->d_segs;
         sa.n_segs = (int)ssd.size();
         sa.n_chunks = chunks;
@@ -1862,6 +1890,7 @@ void release(lde_handle *h) {
     dev_free(h->d_key_dist);
     dev_free(h->d_key_rec);
     dev_free(h->d_key_tabi);
+    dev_free(h->d_zero24);
     dev_free(h->d_ploc);
     dev_free(h->d_pfp_off);
     dev_free(h->d_pfp_scr);
@@ -3163,6 +3192,7 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
         c.cache_bits = lde::kCoordCacheBits;
     }
     h->coord = true;
+    h->key_ok.assign(h->key_ok.size(), 0);  // new distances, grid or edges
     if (!rebind)
         for (auto &u : h->hot_uses) u = -1;  // hot sets re-select on the new value
     return LDE_OK;

@@ -229,6 +229,12 @@ struct SieveArgs {
     unsigned long long *trace = nullptr;  // diagnostic [grid][3]: start, stream end, end (realtime)
     int tail_release = 0;  // each block ends with an agent-scope release (L2 writeback of its stores)
     int keyed = 0;  // the 'toa' stream holds finished pixel words (k_event_key): no probe/gather/TOA
+    // keyed24: the words packed to 24 bits (flags << 22 | value, 4 in 12 bytes);
+    // chunk c's pointer base + 4 c kChunk reads bytes base + 3 c kChunk, the
+    // dummy chunk reads zero24 (kChunk * 3 zero bytes)
+    int keyed24 = 0;
+    const void *keyed_base = nullptr;
+    const void *zero24 = nullptr;
 };
 size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles, int hot_rows = kHotMaxRows);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a
@@ -393,6 +399,8 @@ struct KeyArgs {
     int *keys;                // [n_chunks * kChunk]
     const int *dummy;         // kChunk x (pid_off - 1): the all-invalid chunk
     const uint8_t *tab_i = nullptr;  // pre: distance row of each slot's pixel (0xFF: outside)
+    int k24 = 0;              // 1: words packed to 24 bits (SieveArgs::keyed24), chunk c at
+                              // byte 3 c kChunk of keys
     int pre = 0;              // 1: tab_d / rec hold fx and the row (k_key_dist / k_key_records
                               // with pre_nd = nd), the FAST event pass
     int ablate = 0;           // diagnostics build (LDE_KEY_ABLATE): 1 no gathers, 2 no
@@ -400,7 +408,8 @@ struct KeyArgs {
 };
 constexpr int kKeyLdsChunks = 128;  // k_event_key: chunk pointers per LDS window
 size_t key_smem(const KeyArgs &a, bool table_lds);
-hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent_t stop = nullptr);
+hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent_t start = nullptr,
+                            hipEvent_t stop = nullptr);
 // distance of every pixel-table slot's pixel (NaN for empty slots)
 // x = (d - d0) * inv_dd of every pixel-table slot's pixel (NaN for empty slots)
 // (pre_nd > 0: fx and the distance row instead, see k_key_dist)

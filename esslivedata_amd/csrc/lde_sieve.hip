@@ -51,6 +51,7 @@ constexpr int kEPT = kSplitEPT;               // 8 events per thread per chunk
 constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (half a chunk)
 constexpr int kSieveKeyed = 262144;           // mode bit: the stream holds finished words
 constexpr int kSieveToaLog = 1 << 20;         // mode bit: log-linear TOA buckets
+constexpr int kSieveKeyed24 = 1 << 21;        // with kSieveKeyed: 24-bit packed words
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
@@ -348,6 +349,23 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
 #pragma unroll
         for (int j = 0; j < kEPT / 4; ++j) {
             const int off = (j * kSplitThreads + tid) * 4;
+            if (ABL & kSieveKeyed24) {  // 24-bit words, 4 in 12 bytes (k_event_key, k24)
+                const unsigned char *src =
+                    tq == a.dummy ? reinterpret_cast<const unsigned char *>(a.zero24)
+                                  : reinterpret_cast<const unsigned char *>(a.keyed_base) +
+                                        (((size_t)(reinterpret_cast<const unsigned char *>(tq) -
+                                                   reinterpret_cast<const unsigned char *>(a.keyed_base))) >> 2) * 3u;
+                const v3u w = __builtin_nontemporal_load(
+                    (const __attribute__((address_space(1))) v3u *)(src + (size_t)off * 3u));
+                const uint32_t kk[4] = {w[0] & 0xFFFFFFu, (w[0] >> 24) | ((w[1] & 0xFFFFu) << 8),
+                                        (w[1] >> 16) | ((w[2] & 0xFFu) << 16), w[2] >> 8};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    p[j * 4 + q] = 0;
+                    t[j * 4 + q] = (int)(((kk[q] >> kSieveTagShift) << 30) | (kk[q] & kSieveValueMask));
+                }
+                continue;
+            }
             if (ABL & kSieveKeyed) {  // finished words only (k_event_key)
                 const v4i tv = ld_stream4(tq + off);
 #pragma unroll
@@ -1584,7 +1602,7 @@ static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, h
 
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                         hipEvent_t stop) {
-    const int mode = a.keyed ? kSieveKeyed
+    const int mode = a.keyed ? (kSieveKeyed | (a.keyed24 ? kSieveKeyed24 : 0))
                              : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0) |
                                    (a.toa_log ? kSieveToaLog : 0);
     switch (mode) {
@@ -1594,7 +1612,7 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     // the packed table word (65536)
     LDE_SIEVE_MODE(0) LDE_SIEVE_MODE(256) LDE_SIEVE_MODE(2048) LDE_SIEVE_MODE(65536)
     LDE_SIEVE_MODE(65536 | 256) LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048)
-    LDE_SIEVE_MODE(kSieveKeyed)
+    LDE_SIEVE_MODE(kSieveKeyed) LDE_SIEVE_MODE(kSieveKeyed | kSieveKeyed24)
     // the same with log-linear TOA buckets (tables of geometric edges)
     LDE_SIEVE_MODE(kSieveToaLog) LDE_SIEVE_MODE(kSieveToaLog | 256) LDE_SIEVE_MODE(kSieveToaLog | 2048)
     LDE_SIEVE_MODE(kSieveToaLog | 65536) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256)
