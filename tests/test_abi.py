@@ -101,7 +101,8 @@ def test_product_library_has_only_exact_sieve_variants():
     out = subprocess.run(['nm', '-C', str(lib)], capture_output=True, text=True).stdout
     modes = {int(m) for m in re.findall(r'lde::k_sieve<(\d+), \d>\(', out)}
     assert 0 in modes
-    # the exact variants, and the keyed wavelength pass (262144)
+    # the exact variants, and the keyed wavelength pass (262144; with 24-bit
+    # words 262144 | 2^21)
     exact = {0, 256, 2048, 65536, 65536 | 256, 65536 | 2048, 65536 | 256 | 2048}
     log = 1 << 20  # log-linear TOA buckets (exact)
-    assert modes <= exact | {m | log for m in exact} | {262144}, modes
+    assert modes <= exact | {m | log for m in exact} | {262144, 262144 | (1 << 21)}, modes
