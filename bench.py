@@ -38,8 +38,8 @@ KERNEL_SYMBOL = {
     'paged': 'k_paged_partition',
     'page_accumulate': 'k_page_accumulate',
     'split': 'k_sieve',  # SPLIT's event pass (k_split when LDE_SIEVE=0)
-    'coord': 'coord_keyed',  # wavelength-mode coordinate pass: k_key_dist + k_key_records + k_event_key
-    'pixel': 'pix_pass_a',  # PIXEL pass A: k_pix_chunks + k_pix_count + scans + k_pix_scatter
+    'coord': 'k_event_key',  # wavelength-mode keyed coordinate pass (its per-replica tables cached)
+    'pixel': 'k_pix_scatter',  # PIXEL pass A's partition kernel (after k_pix_chunks and the scans)
     'page_accumulate': 'k_page_accumulate',
     'monitor': 'k_monitor',  # monitor TOA histogram (--workload monitor)
     'finalize': 'k_finalize_v4',
@@ -577,7 +577,10 @@ def main():
             'launches': launches,
             'timed_steps': len(sampled),
             'launches_note': f'dominant kernel stamped by its own dispatch (HIP events) on '
-                             f'{len(sampled)} of the {args.steps} timed steps (every {stride}th)',
+                             f'{len(sampled)} of the {args.steps} timed steps (every {stride}th); '
+                             'the span includes the start marker the runtime enqueues just ahead '
+                             'of the kernel (about 10 us), traffic_detail.profiled_avg_ms is the '
+                             'rocprofv3 kernel duration',
             'pipeline_achieved': pipeline_gbs,
             'pipeline_frac': pipeline_gbs / HBM_PEAK_GBS,
             # whole step (incl. finalize and host gaps): SURVEY 8(d)'s

@@ -1204,13 +1204,10 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             double *kd_r = h->d_key_dist + C * (size_t)replica;
             uint8_t *ki_r = pre ? h->d_key_tabi + C * (size_t)replica : nullptr;
             uint32_t *kr_r = h->d_key_rec + 3 * ((size_t)h->L + 1) * (size_t)replica;
-            Stamp sp(h, LDE_K_COORD);  // [key_dist, key_records,] event_key, stamped by the dispatches
-            hipEvent_t k_start = sp.a;
             const char want = pre ? 2 : 1;  // the layout the replica's tables hold
             if (h->key_ok[(size_t)replica] != want) {
                 HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->cargs.d0,
-                                                h->cargs.inv_dd, pre_nd, kd_r, ki_r, h->stream, k_start));
-                k_start = nullptr;
+                                                h->cargs.inv_dd, pre_nd, kd_r, ki_r, h->stream));
                 HIPCALL(h, lde::launch_key_records(h->d_glut + (size_t)(h->L + 1) * replica, h->d_cpd,
                                                    (unsigned)h->L, h->cargs.d0, h->cargs.inv_dd, pre_nd, kr_r,
                                                    h->stream));
@@ -1239,7 +1236,8 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
                 HIPCALL(h, hipMemsetAsync(h->d_zero24, 0, (size_t)lde::kChunk * 3, h->stream));
             }
             key_w24 = ka.k24 != 0;
-            HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream, k_start, sp.b));
+            Stamp sp(h, LDE_K_COORD);  // k_event_key, stamped by its own dispatch
+            HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream, sp.a, sp.b));
             ksd.push_back({h->d_cbin, h->d_cbin, chunks * lde::kChunk, 0});
         }
         const std::vector<lde::SegDesc> &ssd = coord_deferred ? ksd : sd;

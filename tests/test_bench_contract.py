@@ -87,7 +87,14 @@ def test_traced_line_agrees_with_its_profile(wl):
     r = d['roofline']
     prof = json.loads((ROOT / 'profiles' / f'{R}_{wl}_bench.json').read_text())
     e = prof[bench.KERNEL_SYMBOL[r['kernel']]]
-    assert r['avg_launch_ms'] == pytest.approx(e['avg_ms_steady'], rel=0.03)
+    # one dispatch, two clocks: the HIP events stamped by hipExtLaunchKernelGGL
+    # span the kernel plus the lead of the start marker the runtime enqueues
+    # just ahead of it (DREAM: 11 us of 0.335 ms), rocprofv3 the kernel alone;
+    # never shorter, and longer by at most that lead (3 %, or 15 us for short
+    # kernels)
+    lead = r['avg_launch_ms'] - e['avg_ms_steady']
+    assert -0.005 * e['avg_ms_steady'] <= lead <= max(0.035 * e['avg_ms_steady'], 0.015), (
+        r['avg_launch_ms'], e['avg_ms_steady'])
 
 
 def test_committed_headline_line_has_baseline_and_check():
