@@ -275,6 +275,9 @@ template <bool TLDS, bool ELDS, bool FAST>
 __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     extern __shared__ double sm[];
     const CoordArgs &a = k.c;
+    // the messages: kernel-argument descriptors (<= kKargSegs, no upload in
+    // front of the pass) or the device table
+    const SegDesc *segs = k.karg ? k.sk.s : k.segs;
     const uint32_t C = 1u << k.cbits;
     uint32_t *s_w = reinterpret_cast<uint32_t *>(sm);
     double *s_d = sm + C / 2;
@@ -343,9 +346,9 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
         int lo = 0, hi = k.n_segs - 1;  // last segment with chunk0 <= c
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (k.segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+            if (segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
         }
-        const SegDesc sd = k.segs[lo];
+        const SegDesc sd = segs[lo];
         const long long base = (c - sd.chunk0) * kChunk;
         pp = sd.pid + base;
         tp = sd.toa + base;
@@ -465,9 +468,9 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
                 int lo = 0, hi = k.n_segs - 1;
                 while (lo < hi) {
                     const int mid = (lo + hi + 1) >> 1;
-                    if (k.segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+                    if (segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
                 }
-                left = k.segs[lo].n - (c - k.segs[lo].chunk0) * kChunk;
+                left = segs[lo].n - (c - segs[lo].chunk0) * kChunk;
             }
             int pe[8], te[8], out[8];
 #pragma unroll

@@ -1182,7 +1182,11 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         std::vector<lde::SegDesc> ksd;
         bool key_w24 = false;
         if (coord_deferred) {
-            if (int rc = upload()) return rc;  // k_event_key reads the messages from d_segs
+            // k_event_key takes the messages as kernel arguments when they fit
+            // (no H2D copy in front of it), else from d_segs
+            const bool kkarg = (long long)sd.size() <= lde::kKargSegs;
+            if (!kkarg)
+                if (int rc = upload()) return rc;
             if (int rc = grow(h, &h->d_cbin, h->cbin_cap, (size_t)chunks * lde::kChunk)) return rc;
             // per replica: each table slot's distance row / fx (or x) and each
             // pixel's 12-byte record, built once after the replica's hot-set
@@ -1216,6 +1220,9 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             lde::KeyArgs ka;
             ka.c = h->cargs;
             ka.segs = h->d_segs;
+            ka.karg = kkarg ? 1 : 0;
+            if (kkarg)
+                for (size_t i = 0; i < sd.size(); ++i) ka.sk.s[i] = sd[i];
             ka.n_segs = (int)sd.size();
             ka.n_chunks = chunks;
             ka.glut = h->d_glut + (size_t)(h->L + 1) * replica;

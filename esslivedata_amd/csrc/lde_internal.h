@@ -389,6 +389,8 @@ hipError_t launch_event_coord(const CoordArgs &a, const int *pid, const int *toa
 struct KeyArgs {
     CoordArgs c;              // coordinate arithmetic (its cache fields unused)
     const SegDesc *segs;      // the batch's messages (device table)
+    SegKarg sk;               // karg: the messages as kernel arguments (n_segs <= kKargSegs)
+    int karg = 0;
     int n_segs;
     long long n_chunks;
     const uint32_t *glut;     // this replica's pixel words, L + 1 entries (entry L = 0)
