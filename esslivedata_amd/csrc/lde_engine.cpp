@@ -1733,7 +1733,7 @@ int stage_pixel(lde_handle *h, const int32_t *lut, PixStaged &st) {
     // gains nothing and pass A's runs get shorter; 256 ranges of 3,136 pixels,
     // one per CU by multiply-high, measured pass B -3.7 us and pass A +19 us)
     const long long max_nr = std::max<long long>(
-        1, std::min<long long>(lde::kPixMaxRanges, env_ll("LDE_PIX_MAX_RANGES", 256)));
+        1, std::min<long long>(lde::kPixMaxRanges - 1, env_ll("LDE_PIX_MAX_RANGES", 256)));
     int rb = 8;
     while (rb < 20 && ((L + (1LL << rb) - 1) >> rb) > max_nr) ++rb;
     int tbits = 0;

@@ -264,10 +264,10 @@ __global__ __launch_bounds__(1024) void k_pix_scan(PixArgs a, const uint32_t *__
 }
 
 // LDS: staging (unit events + pads, u32) | counts, unit offsets, cursors,
-// staging positions, slot ends (nr each) | scan scratch (32) | chunk table |
-// TOA image
+// staging positions, slot ends (nr each) | scan scratch (32) | lane dummies
+// (64) | chunk table | TOA image
 size_t pix_scatter_smem(const ToaParams &tp, int unit) {
-    return 4 * ((size_t)unit * kChunk + 4 * (size_t)kPixMaxRanges + 6 * (size_t)kPixMaxRanges + 32) +
+    return 4 * ((size_t)unit * kChunk + 4 * (size_t)kPixMaxRanges + 6 * (size_t)kPixMaxRanges + 32 + 64) +
            sizeof(PixChunk) * kPixLdsChunks + toa_lds_bytes(tp);
 }
 
@@ -291,11 +291,17 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     uint32_t *s_pos = s_cur + kPixMaxRanges;
     uint32_t *s_end = s_pos + kPixMaxRanges;
     uint32_t *s_w = s_end + kPixMaxRanges;
-    PixChunk *s_ctab = reinterpret_cast<PixChunk *>(s_w + 32);
+    // lane-private dummy staging words: events without a slot store there,
+    // so the rank atomics and staging stores need no per-event branches
+    uint32_t *s_dum = s_w + 32;
+    PixChunk *s_ctab = reinterpret_cast<PixChunk *>(s_dum + 64);
     unsigned char *s_tab = reinterpret_cast<unsigned char *>(s_ctab + kPixLdsChunks);
     load_toa_tables(s_tab, a.tab, a.tp);
     const int tid = threadIdx.x;
     const uint32_t *rtot = a.rstart + a.nr + 1;  // k_pix_scan_blocks' range totals
+    // counter of the events without a range (unknown ids): the last slot,
+    // never a range (nr < kPixMaxRanges), never read
+    constexpr uint32_t kNoRange = kPixMaxRanges - 1;
     for (int r = tid; r < a.nr; r += NT) {
         s_cnt[r] = s_cnt2[r] = 0;
         s_cur[r] = a.rstart[r] + a.counts[(size_t)blockIdx.x * a.nr + r];  // this block's slot of range r
@@ -323,14 +329,20 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
         // stay live across the scan (registers: the next unit's loads are in
         // flight at the same time), pass 2 takes the slots
         uint32_t word[E];
+        // every event's TOA lookup first, unconditionally (a lookup sunk into
+        // a per-event `q < L` branch waited twice on LDS per event, serially)
+        int bt[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) bt[e] = pix_toa_bin<FAST>(t[e], s_tab, a.tp);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t q = (uint32_t)p[e] - (uint32_t)a.pid_off;
-            const int b = pix_toa_bin<FAST>(t[e], s_tab, a.tp);
+            const int b = bt[e];
             const uint32_t r = q >> a.rb;
-            word[e] = q < a.L ? ((r << a.rs) | (b < 0 ? dmask : ((q & mask) | ((uint32_t)b << a.rb))))
-                              : 0xFFFFFFFFu;  // unknown id: no slot
-            if (q < a.L) atomicAdd(&cnt[r], 1u);
+            const bool ok = q < a.L;
+            word[e] = ok ? ((r << a.rs) | (b < 0 ? dmask : ((q & mask) | ((uint32_t)b << a.rb))))
+                         : 0xFFFFFFFFu;  // unknown id: no slot
+            atomicAdd(&cnt[ok ? r : kNoRange], 1u);
             asm volatile("" : "+v"(word[e]));  // materialized here, not recomputed after the scan
         }
         // the next unit's events load while this one is partitioned (not
@@ -355,9 +367,16 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
             for (uint32_t j = n; j < v; ++j) s_stg[off + j] = ((uint32_t)tid << a.rs) | dmask;
         }
         __syncthreads();
+        // ranks: every returning atomic issued before any staging store
+        uint32_t pos[E];
 #pragma unroll
         for (int e = 0; e < E; ++e)
-            if (word[e] != 0xFFFFFFFFu) s_stg[atomicAdd(&s_pos[word[e] >> a.rs], 1u)] = word[e];
+            pos[e] = atomicAdd(&s_pos[word[e] != 0xFFFFFFFFu ? word[e] >> a.rs : kNoRange], 1u);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            uint32_t *dst = word[e] != 0xFFFFFFFFu ? s_stg + pos[e] : s_dum + (tid & 63);
+            *dst = word[e];
+        }
         __syncthreads();
         // a group never straddles two runs; its slot position is 4-aligned
         for (uint32_t g = (uint32_t)tid * 4u; g < total; g += NT * 4u) {
@@ -603,7 +622,7 @@ void launch_pass_a_shape(const PixArgs &a, uint32_t item_events, int max_items, 
 hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32_t item_events,
                         int max_items, uint4 *items, uint32_t *item_count, uint32_t *hist,
                         hipStream_t st, int phase, hipEvent_t start, hipEvent_t stop) {
-    if (a.nr > kPixMaxRanges || a.nr > 1024 || (item_events & 3u) || (a.unit != 1 && a.unit != 2) ||
+    if (a.nr >= kPixMaxRanges || a.nr > 1024 || (item_events & 3u) || (a.unit != 1 && a.unit != 2) ||
         (a.ept != 8 && a.ept != 16) || (a.unit == 2 && a.ept != 16))
         return hipErrorInvalidValue;
     if (phase == 0) {

@@ -69,8 +69,10 @@ def test_committed_bench_line_contract(wl):
     assert r['traffic'] == t['bytes'] == pytest.approx(t['read'] + t['write'])
     prof = json.loads((ROOT / t['source']).read_text())[bench.KERNEL_SYMBOL[r['kernel']]]
     assert prof['hbm_traffic_bytes'] == t['bytes']
-    # this untraced line records how far per-dispatch tracing moved the kernel
+    # this untraced line records how far per-dispatch tracing moved the kernel;
+    # the untraced HIP-event time and the rocprofv3 kernel time agree (3 %)
     assert t['trace_overhead'] == pytest.approx(t['profiled_avg_ms'] / r['avg_launch_ms'] - 1.0)
+    assert abs(t['trace_overhead']) <= 0.03, t
     # the kernel reads at least its algorithmic bytes
     events_per_launch = d['config']['events_per_step'] * r.get('timed_steps', d['steps']) / r['launches']
     assert t['read'] >= 0.95 * bench.BYTES_PER_EVENT * events_per_launch
@@ -87,14 +89,14 @@ def test_traced_line_agrees_with_its_profile(wl):
     r = d['roofline']
     prof = json.loads((ROOT / 'profiles' / f'{R}_{wl}_bench.json').read_text())
     e = prof[bench.KERNEL_SYMBOL[r['kernel']]]
-    # one dispatch, two clocks: the HIP events stamped by hipExtLaunchKernelGGL
-    # span the kernel plus the lead of the start marker the runtime enqueues
-    # just ahead of it (DREAM: 11 us of 0.335 ms), rocprofv3 the kernel alone;
-    # never shorter, and longer by at most that lead (3 %, or 15 us for short
-    # kernels)
+    # one dispatch, two clocks: the HIP events of hipExtLaunchKernelGGL start
+    # at a marker the runtime enqueues just ahead of the kernel, rocprofv3
+    # times the kernel alone.  Under tracing the profiler's dispatch hook runs
+    # between the two, so the span leads the kernel by up to the idle gap the
+    # trace shows before it (untraced, the lines agree within 3 %: below)
     lead = r['avg_launch_ms'] - e['avg_ms_steady']
-    assert -0.005 * e['avg_ms_steady'] <= lead <= max(0.035 * e['avg_ms_steady'], 0.015), (
-        r['avg_launch_ms'], e['avg_ms_steady'])
+    assert -0.005 * e['avg_ms_steady'] <= lead <= 0.03 * e['avg_ms_steady'] + e['gap_before_ms_steady'], (
+        r['avg_launch_ms'], e['avg_ms_steady'], e['gap_before_ms_steady'])
 
 
 def test_committed_headline_line_has_baseline_and_check():

@@ -51,11 +51,20 @@ def main(prof: Path, stem: Path) -> None:
     # kernel's first two (the bench's warm-up steps: first-touch allocations,
     # hot-set selection), comparable with the bench's timed-region stamps
     durs: dict[str, list[float]] = defaultdict(list)
+    # and the idle time before each dispatch (previous dispatch's end to its
+    # start): under tracing the dispatch lags the HIP start marker enqueued
+    # ahead of it by about this much (the bench's event span includes it)
+    gaps: dict[str, list[float]] = defaultdict(list)
     trace = prof / 'kt' / 'run_kernel_trace.csv'
     if trace.exists():
-        for r in csv.DictReader(open(trace)):
-            durs[short(r['Kernel_Name'])].append(
-                (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6)
+        rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r['Start_Timestamp']))
+        prev_end = None
+        for r in rows:
+            s0, e0 = int(r['Start_Timestamp']), int(r['End_Timestamp'])
+            k = short(r['Kernel_Name'])
+            durs[k].append((e0 - s0) / 1e6)
+            gaps[k].append(max(0, s0 - prev_end) / 1e6 if prev_end is not None else 0.0)
+            prev_end = e0 if prev_end is None else max(prev_end, e0)
     counters: dict[str, dict[str, list[float]]] = defaultdict(lambda: defaultdict(list))
     for sub in sorted(prof.glob('pmc_*')):
         f = sub / 'run_counter_collection.csv'
@@ -73,6 +82,8 @@ def main(prof: Path, stem: Path) -> None:
         e = {'calls': d['calls'], 'avg_ms': d['avg_ms']}
         if len(durs.get(k, [])) > 2:
             e['avg_ms_steady'] = sum(durs[k][2:]) / (len(durs[k]) - 2)
+            g = sorted(gaps[k][2:])  # median: the steps after the timed region wait on the host
+            e['gap_before_ms_steady'] = g[len(g) // 2]
         pm = {c: sum(v) / len(v) for c, v in counters.get(k, {}).items()}
         # the first dispatches of each kernel include warm-up sizes; use the median-like mean
         e['pmc_per_dispatch'] = pm
