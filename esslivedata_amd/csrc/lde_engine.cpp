@@ -968,8 +968,9 @@ bool coord_keyed_candidate(const lde_handle *h, long long total) {
 // +-0: off by default (LDE_HOT_WINDOW=1, diagnostics build; exact, in the
 // parity matrix).
 bool window_candidate(const lde_handle *h) {
-    return h->sieve_ok && !h->coord && h->d_toa_hist && h->S > h->hot_rows &&
-           env_ll("LDE_HOT_WINDOW", 0) != 0;
+    // (the windowed sieve is compiled for the default pipeline only)
+    return h->sieve_ok && !h->coord && h->d_toa_hist && h->S > h->hot_rows && !h->sieve_pack &&
+           !h->early_gather && !h->ttab_log && h->sieve_ablate == 0 && env_ll("LDE_HOT_WINDOW", 0) != 0;
 }
 
 // the most rows of w bins (window starting at lo) the sieve block's LDS holds

@@ -52,6 +52,8 @@ constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (ha
 constexpr int kSieveKeyed = 262144;           // mode bit: the stream holds finished words
 constexpr int kSieveToaLog = 1 << 20;         // mode bit: log-linear TOA buckets
 constexpr int kSieveKeyed24 = 1 << 21;        // with kSieveKeyed: 24-bit packed words
+constexpr int kSieveWindow = 1 << 23;         // hot rows narrowed to a TOA window (the
+                                              // default pipeline only; no cost when off)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // hot row -> screen (u16), for hot-screen events outside the rows' window
     const uint32_t o_rs = o_seg + (uint32_t)(sizeof(SegDesc) / 4 * kKargSegs);
     uint16_t *s_rs = reinterpret_cast<uint16_t *>(sm + o_rs);
-    const bool windowed = a.hot_w != a.T;
+    constexpr bool windowed = (ABL & kSieveWindow) != 0;
     if (windowed)
         for (int i = tid; i < a.hot_rows; i += kSplitThreads) s_rs[i] = (uint16_t)a.row_screen[i];
     for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.hot_words; i += kSplitThreads * 4u)
@@ -1602,9 +1604,13 @@ static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, h
 
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                         hipEvent_t stop) {
-    const int mode = a.keyed ? (kSieveKeyed | (a.keyed24 ? kSieveKeyed24 : 0))
-                             : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0) |
-                                   (a.toa_log ? kSieveToaLog : 0);
+    int mode = a.keyed ? (kSieveKeyed | (a.keyed24 ? kSieveKeyed24 : 0))
+                       : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0) |
+                             (a.toa_log ? kSieveToaLog : 0);
+    if (a.hot_w != a.T) {  // windowed hot rows: the default pipeline only
+        if (mode != 0) return hipErrorInvalidValue;
+        mode = kSieveWindow;
+    }
     switch (mode) {
 #define LDE_SIEVE_MODE(m) \
     case m: return launch_sieve_t<m>(a, grid, st, start, stop);
@@ -1612,7 +1618,7 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     // the packed table word (65536)
     LDE_SIEVE_MODE(0) LDE_SIEVE_MODE(256) LDE_SIEVE_MODE(2048) LDE_SIEVE_MODE(65536)
     LDE_SIEVE_MODE(65536 | 256) LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048)
-    LDE_SIEVE_MODE(kSieveKeyed) LDE_SIEVE_MODE(kSieveKeyed | kSieveKeyed24)
+    LDE_SIEVE_MODE(kSieveKeyed) LDE_SIEVE_MODE(kSieveKeyed | kSieveKeyed24) LDE_SIEVE_MODE(kSieveWindow)
     // the same with log-linear TOA buckets (tables of geometric edges)
     LDE_SIEVE_MODE(kSieveToaLog) LDE_SIEVE_MODE(kSieveToaLog | 256) LDE_SIEVE_MODE(kSieveToaLog | 2048)
     LDE_SIEVE_MODE(kSieveToaLog | 65536) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256)

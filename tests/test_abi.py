@@ -105,4 +105,4 @@ def test_product_library_has_only_exact_sieve_variants():
     # words 262144 | 2^21)
     exact = {0, 256, 2048, 65536, 65536 | 256, 65536 | 2048, 65536 | 256 | 2048}
     log = 1 << 20  # log-linear TOA buckets (exact)
-    assert modes <= exact | {m | log for m in exact} | {262144, 262144 | (1 << 21)}, modes
+    assert modes <= exact | {m | log for m in exact} | {262144, 262144 | (1 << 21), 1 << 23}, modes
