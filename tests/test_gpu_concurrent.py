@@ -1,0 +1,104 @@
+"""Five jobs finalizing concurrently.
+
+The reference service runs its jobs on five threads
+(``SRC/service_factory.py:65``, ``job_threads=5``), each job an accumulate +
+finalize loop.  Here five engines, each on its own stream and its own Python
+thread (ctypes releases the GIL inside the C ABI), bin different DREAM batches
+at the same time.  Every job's cumulative image and totals must stay bit-exact
+against ``oracle/binning_ref.c``, and the finalize waits must not spin a host
+core each: ``wait_stream`` sleeps through the predicted part of a wait and
+blocks on an event past a short spin, so the process's CPU time stays well
+below five cores' worth of the wall time (five spinning waiters would use
+about 5x).
+"""
+
+import os
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from oracle import c_oracle
+from oracle import scipp_semantics as ora
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
+
+N_JOBS = 5
+STEPS = 8
+N_EVENTS = 20_000_000
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu(engine_lib):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+
+
+def test_five_jobs_finalize_concurrently_exact_and_without_spinning():
+    import torch
+
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.engine import BinningEngine
+
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    inst = synthetic.dream_mantle()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    S, T = view.n_screen, len(edges) - 1
+    lo, hi = 10, 90
+    batches = [synthetic.torch_dream_events(N_EVENTS, inst, 300 + j, dev) for j in range(N_JOBS)]
+    streams = [torch.cuda.Stream(dev) for _ in range(N_JOBS)]
+    engines = [BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                             n_screen=S, device=0, stream=streams[j].cuda_stream, toa_range=(lo, hi))
+               for j in range(N_JOBS)]
+    torch.cuda.synchronize(dev)
+    results = [None] * N_JOBS
+    errors = []
+    go = threading.Barrier(N_JOBS + 1)
+
+    def job(j):
+        try:
+            eng = engines[j]
+            pid, toa = batches[j]
+            go.wait()
+            for s in range(STEPS):
+                eng.stage_tensors_batch([(pid, toa)])
+                eng.accumulate(s % view.n_replicas)
+                results[j] = eng.finalize(images=True)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append((j, repr(e)))
+
+    threads = [threading.Thread(target=job, args=(j,)) for j in range(N_JOBS)]
+    for t in threads:
+        t.start()
+    go.wait()
+    t0, c0 = time.perf_counter(), time.process_time()
+    for t in threads:
+        t.join()
+    wall, cpu = time.perf_counter() - t0, time.process_time() - c0
+    assert not errors, errors
+    waits = sum(e.counter('waits') for e in engines)
+    blocked = sum(e.counter('waits_blocked') for e in engines)
+    print(f'five jobs: wall {wall * 1e3:.1f} ms, host cpu {cpu * 1e3:.1f} ms '
+          f'({cpu / wall:.2f} cores), waits {waits}, blocked {blocked}')
+    # five spinning waiters would burn ~5 cores for the whole run
+    assert cpu / wall < 3.0, (cpu, wall, waits, blocked)
+
+    ps = ora.geometric_pixel_screen(inst.coords, inst.resolution, flip_x=False)
+    threads_cpu = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
+    for j in range(N_JOBS):
+        o = c_oracle.CDetectorView(inst.detector_number, ps, S, edges, threads=threads_cpu)
+        pid, toa = (x.cpu().numpy() for x in batches[j])
+        cum = None
+        for s in range(STEPS):
+            cum = o.accumulate(pid, toa, s % view.n_replicas)
+        cum = cum.reshape(S, T)
+        res = results[j]
+        np.testing.assert_array_equal(res.cumulative_image, cum[:, lo:hi].sum(1).astype(np.float64))
+        assert res.cumulative_total == int(cum.sum())
+        assert res.cumulative_in_range == int(cum[:, lo:hi].sum())
+        engines[j].close()
