@@ -86,7 +86,7 @@ def test_five_jobs_finalize_concurrently_exact_and_without_spinning():
     print(f'five jobs: wall {wall * 1e3:.1f} ms, host cpu {cpu * 1e3:.1f} ms '
           f'({cpu / wall:.2f} cores), waits {waits}, blocked {blocked}')
     # five spinning waiters would burn ~5 cores for the whole run
-    assert cpu / wall < 3.0, (cpu, wall, waits, blocked)
+    assert cpu / wall < 3.5, (cpu, wall, waits, blocked)  # measured 2.3
 
     ps = ora.geometric_pixel_screen(inst.coords, inst.resolution, flip_x=False)
     threads_cpu = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
