@@ -235,6 +235,12 @@ struct SieveArgs {
     int keyed24 = 0;
     const void *keyed_base = nullptr;
     const void *zero24 = nullptr;
+    // pair: hot counters as u16 pairs (hot_words = LDS words = counters / 2,
+    // whole rows, the default pipeline only); hist: the window, which a block
+    // whose u16 counters wrapped adds its hot events to with global atomics
+    int pair = 0;
+    uint32_t *hist = nullptr;
+    uint32_t *wraps = nullptr;  // (pair) +1 per block whose counters wrapped
 };
 size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles, int hot_rows = kHotMaxRows);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a

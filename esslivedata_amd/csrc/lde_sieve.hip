@@ -52,6 +52,11 @@ constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (ha
 constexpr int kSieveKeyed = 262144;           // mode bit: the stream holds finished words
 constexpr int kSieveToaLog = 1 << 20;         // mode bit: log-linear TOA buckets
 constexpr int kSieveKeyed24 = 1 << 21;        // with kSieveKeyed: 24-bit packed words
+// mode bit: hot counters as u16 pairs (two per LDS word, twice the hot rows);
+// exact: a wrap is detected at the end of the pass (the counters' sum against
+// the wave-counted hot events) and that block's hot events are re-added with
+// global atomics (see k_sieve)
+constexpr int kSievePair = 1 << 24;
 constexpr int kSieveWindow = 1 << 23;         // hot rows narrowed to a TOA window (the
                                               // default pipeline only; no cost when off)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -239,6 +244,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t o_rs = o_seg + (uint32_t)(sizeof(SegDesc) / 4 * kKargSegs);
     uint16_t *s_rs = reinterpret_cast<uint16_t *>(sm + o_rs);
     constexpr bool windowed = (ABL & kSieveWindow) != 0;
+    constexpr bool pair = (ABL & kSievePair) != 0;
     if (windowed)
         for (int i = tid; i < a.hot_rows; i += kSplitThreads) s_rs[i] = (uint16_t)a.row_screen[i];
     for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.hot_words; i += kSplitThreads * 4u)
@@ -248,7 +254,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.toa_words4; i += kSplitThreads * 4u)
         *reinterpret_cast<uint4 *>(sm + o_tt + i) = *reinterpret_cast<const uint4 *>(a.ttab + i);
     if (tid < 64) sm[o_dum + tid] = 0;
-    if (tid == 0) sm[o_cur] = sm[o_cur + 1] = 0;  // cursor, hot-count overflow vote
+    // cursor, hot-count overflow vote, (pair) hot events, hot counter sum
+    if (tid == 0) sm[o_cur] = sm[o_cur + 1] = sm[o_cur + 2] = sm[o_cur + 3] = 0;
     for (uint32_t i = (uint32_t)tid; i < kSieveStage * (kSplitThreads / 64); i += kSplitThreads)
         sm[o_stg + i] = 0xFFFFFFFFu;
     for (int i = tid; i < kColdGroups * align4(a.n_tiles); i += kSplitThreads) sm[o_tcnt + i] = 0;
@@ -284,6 +291,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t T = (uint32_t)a.T;
     const uint32_t hlo = (uint32_t)a.hot_lo, hw = (uint32_t)a.hot_w;
     const uint32_t dum_idx = o_dum + (uint32_t)lane;
+    const uint32_t hw4 = (uint32_t)a.hot_words * 4u;  // (pair) first high-half counter, scaled by 4
     const uint32_t dum4 = dum_idx * 4u;
     const uint32_t o_stg_w = o_stg + kSieveStage * (uint32_t)(tid >> 6);
     // cold keys are counted per tile for each of the kColdGroups wave groups
@@ -464,6 +472,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     v4u pend_kv1 = pend_kv;
     uint32_t pend_off1 = kOOB;
     uint32_t wcur = 0;  // this wave's cold keys so far (wave-uniform)
+    uint32_t hcnt = 0;  // (pair) this wave's hot events (wave-uniform, wraps like the check)
     uint32_t junk = 0;  // ABL 512/1024 probes: extra VALU / LDS work per event
     auto bin = [&](const uint32_t (&ws)[kEPT], const uint32_t (&g)[kEPT], const uint32_t (&dc)[kEPT],
                    const uint32_t (&tw)[kEPT]) __attribute__((always_inline)) {
@@ -510,9 +519,21 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 // hot counter (hot lanes), the tile's cold-key count (cold
                 // lanes) or the lane's dummy word (the rest)
                 const uint32_t tidx4 = vsel(bal, ((k4 >> tsh) << 2) + o_tcnt4, dum4);
-                const uint32_t aidx4 = (ABL & 1) ? tidx4 : vsel(hm, k4, tidx4);
-                __hip_atomic_fetch_add(&lds_at(sm, aidx4), 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (pair) {
+                    // counter i < hot_words: low half of LDS word i; else the
+                    // high half of word i - hot_words (neighbouring bins stay
+                    // in neighbouring words, i.e. banks)
+                    hcnt += (uint32_t)__popcll(hm);
+                    const bool up = k4 >= hw4;
+                    const uint32_t aidx4 = vsel(hm, up ? k4 - hw4 : k4, tidx4);
+                    const uint32_t add = vsel(hm, up ? 0x10000u : 1u, 1u);
+                    __hip_atomic_fetch_add(&lds_at(sm, aidx4), add, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    const uint32_t aidx4 = (ABL & 1) ? tidx4 : vsel(hm, k4, tidx4);
+                    __hip_atomic_fetch_add(&lds_at(sm, aidx4), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             }
             const uint32_t res = (tot + 3u) & ~3u;
             // the previous half's keys leave now (their LDS read is long done)
@@ -705,7 +726,69 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // k_hot_reduce_scan) unless a count of this block exceeds 0xFFFF
     uint32_t *dst = a.hot_part + (size_t)blockIdx.x * a.hot_words;
     bool packed = false;
-    if (a.hot_fmt && (a.hot_words & 7) == 0) {
+    if (pair) {
+        // u16 pairs: a counter that wrapped lost 65536 and carried 1 into its
+        // neighbour (or out of the word), so the counters' sum is the hot
+        // event count minus 65535 or 65536 per wrap (mod 2^32, exact below
+        // 2^32 events per block): equal iff nothing wrapped
+        if (lane == 0) atomicAdd(&sm[o_cur + 2], hcnt);
+        uint32_t s = 0;
+        for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(sm + i);
+            s += (v.x & 0xFFFFu) + (v.x >> 16) + (v.y & 0xFFFFu) + (v.y >> 16) + (v.z & 0xFFFFu) +
+                 (v.z >> 16) + (v.w & 0xFFFFu) + (v.w >> 16);
+        }
+        atomicAdd(&sm[o_cur + 3], s);
+        __syncthreads();
+        const bool wrapped = sm[o_cur + 2] != sm[o_cur + 3];
+        // u16 counts in counter order (row stride hot_words * 2): the low
+        // halves of 8 words, then their high halves hot_words counters on
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+        for (int i = tid * 8; i < a.hot_words; i += kSplitThreads * 8) {
+            const uint4 v0 = *reinterpret_cast<const uint4 *>(sm + i);
+            const uint4 v1 = *reinterpret_cast<const uint4 *>(sm + i + 4);
+            auto lo2 = [](uint32_t x, uint32_t y) { return (x & 0xFFFFu) | (y << 16); };
+            auto hi2 = [](uint32_t x, uint32_t y) { return (x >> 16) | (y & 0xFFFF0000u); };
+            d4[i >> 3] = wrapped ? make_uint4(0, 0, 0, 0)
+                                 : make_uint4(lo2(v0.x, v0.y), lo2(v0.z, v0.w), lo2(v1.x, v1.y), lo2(v1.z, v1.w));
+            d4[(a.hot_words + i) >> 3] =
+                wrapped ? make_uint4(0, 0, 0, 0)
+                        : make_uint4(hi2(v0.x, v0.y), hi2(v0.z, v0.w), hi2(v1.x, v1.y), hi2(v1.z, v1.w));
+        }
+        if (tid == 0) a.hot_fmt[blockIdx.x] = 1u;
+        if (wrapped) {
+            // rare (a bin past 65535 events of one block): this block's hot
+            // events again, straight into the window with global atomics
+            // (its cold keys are already out; k_hot_reduce_scan adds the
+            // other blocks' rows with atomics too)
+            if (tid == 0 && a.wraps) atomicAdd(a.wraps, 1u);
+            const SegDesc *segs = (!GCT && a.karg) ? s_seg : a.segs;
+            for (long long c = cb; c < ce; ++c) {
+                int lo = 0, hi = a.n_segs - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+                }
+                const SegDesc sd = segs[lo];
+                const long long base = (c - sd.chunk0) * kChunk;
+                for (int e = tid; e < kChunk; e += kSplitThreads) {
+                    const long long ei = base + e;
+                    if (ei >= sd.n) break;
+                    const uint32_t q = (uint32_t)sd.pid[ei] - pid_off;
+                    const uint32_t d = min((uint32_t)sd.toa[ei] - toa_lo, toa_cap);
+                    const uint32_t w = lds_at(sm, o_pc4 + ((q & cmask) << 2));
+                    const uint32_t tw = lds_at(sm, o_tt4 + ((d >> a.toa_shift) << 2));
+                    const bool hit = ((w >> kSieveTagShift) & 0xFFu) == (q >> a.cbits);
+                    const uint32_t v = hit ? w : a.glut[min(q, Lc)];
+                    const uint32_t b = (tw & 0xFFu) + (((d & wmask) >= (tw >> 8)) ? 1u : 0u);
+                    if ((v >> 30) == 3u && b < T) {
+                        const uint32_t row = (v & kSieveValueMask) / T;
+                        atomicAdd(a.hist + (size_t)a.row_screen[row] * T + b, 1u);
+                    }
+                }
+            }
+        }
+    } else if (a.hot_fmt && (a.hot_words & 7) == 0) {
         uint32_t big = 0;
         for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4) {
             const uint4 v = *reinterpret_cast<const uint4 *>(sm + i);
@@ -715,7 +798,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         __syncthreads();
         packed = sm[o_cur + 1] == 0u;
     }
-    if (packed) {
+    if (pair) {
+    } else if (packed) {
         uint4 *d16 = reinterpret_cast<uint4 *>(dst);  // 8 counts per 16 bytes
         for (int i = tid * 8; i < a.hot_words; i += kSplitThreads * 8) {
             const uint4 v0 = *reinterpret_cast<const uint4 *>(sm + i);
@@ -727,7 +811,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4)
             *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(sm + i);
     }
-    if (a.hot_fmt && tid == 0) a.hot_fmt[blockIdx.x] = packed ? 1u : 0u;
+    if (!pair && a.hot_fmt && tid == 0) a.hot_fmt[blockIdx.x] = packed ? 1u : 0u;
     if (a.trace) {  // diagnostic: per-block timeline (LDE_SIEVE_TRACE)
         __syncthreads();
         if (tid < 3)
@@ -1608,8 +1692,13 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
                        : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0) |
                              (a.toa_log ? kSieveToaLog : 0);
     if (a.hot_w != a.T) {  // windowed hot rows: the default pipeline only
-        if (mode != 0) return hipErrorInvalidValue;
+        if (mode != 0 || a.pair) return hipErrorInvalidValue;
         mode = kSieveWindow;
+    }
+    if (a.pair) {  // u16 hot pairs: the default pipeline, whole rows
+        if (mode != 0 || !a.hot_fmt || !a.hist || !a.row_screen || (a.T & 1) || (a.hot_words & 7))
+            return hipErrorInvalidValue;
+        mode = kSievePair;
     }
     switch (mode) {
 #define LDE_SIEVE_MODE(m) \
@@ -1619,6 +1708,7 @@ hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t
     LDE_SIEVE_MODE(0) LDE_SIEVE_MODE(256) LDE_SIEVE_MODE(2048) LDE_SIEVE_MODE(65536)
     LDE_SIEVE_MODE(65536 | 256) LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048)
     LDE_SIEVE_MODE(kSieveKeyed) LDE_SIEVE_MODE(kSieveKeyed | kSieveKeyed24) LDE_SIEVE_MODE(kSieveWindow)
+    LDE_SIEVE_MODE(kSievePair)
     // the same with log-linear TOA buckets (tables of geometric edges)
     LDE_SIEVE_MODE(kSieveToaLog) LDE_SIEVE_MODE(kSieveToaLog | 256) LDE_SIEVE_MODE(kSieveToaLog | 2048)
     LDE_SIEVE_MODE(kSieveToaLog | 65536) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256)

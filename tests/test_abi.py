@@ -102,7 +102,8 @@ def test_product_library_has_only_exact_sieve_variants():
     modes = {int(m) for m in re.findall(r'lde::k_sieve<(\d+), \d>\(', out)}
     assert 0 in modes
     # the exact variants, and the keyed wavelength pass (262144; with 24-bit
-    # words 262144 | 2^21)
+    # words 262144 | 2^21), windowed rows (2^23), u16 hot pairs (2^24)
     exact = {0, 256, 2048, 65536, 65536 | 256, 65536 | 2048, 65536 | 256 | 2048}
     log = 1 << 20  # log-linear TOA buckets (exact)
-    assert modes <= exact | {m | log for m in exact} | {262144, 262144 | (1 << 21), 1 << 23}, modes
+    assert modes <= exact | {m | log for m in exact} | {262144, 262144 | (1 << 21), 1 << 23, 1 << 24}, modes
+    assert 1 << 24 in modes

@@ -93,6 +93,8 @@ def _run(workload, dev):
         # AUTO: the skewed DREAM stream takes SPLIT; LOKI's uniform stream
         # PIXEL (4096-pixel ranges, footprints of <= 288 screens in LDS)
         assert eng.info()['last_strategy'] == ('split' if dream else 'pixel')
+        if dream:  # u32 hot rows (u16 pairs are an exact variant, off)
+            assert eng.counter('sieve_pair') == 0
         np.testing.assert_array_equal(res.current_hist, cur.astype(np.float64))
         np.testing.assert_array_equal(res.cumulative_hist, cum.astype(np.float64))
         np.testing.assert_array_equal(res.current_image, cur[:, lo:hi].sum(1).astype(np.float64))
@@ -108,3 +110,62 @@ def _run(workload, dev):
         # within the list's capacity: the fallback path is tested separately
         assert max(overflow) < eng.counter('pix_overflow_cap')
     eng.close()
+
+
+def test_sieve_pair_wrap_exact(knobs):
+    """(LDE_HOT_PAIR=1, diagnostics build) u16 hot pairs past 65535 counts of one block in one bin: each block of
+    the sieve detects its wrapped counters (their sum against the wave-counted
+    hot events) and re-adds its hot events with global atomics; the counts
+    stay bit-exact.  3e7 events, 90 % on one pixel at one TOA (about 100 K of
+    that bin per block), the rest DREAM-like; a second, normal batch after it
+    must not wrap."""
+    import torch
+
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.engine import BinningEngine
+
+    knobs(LDE_HOT_PAIR='1')
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    inst = synthetic.dream_mantle()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution, flip_x=False)
+    edges = inst.edges.edges_ns()
+    ps = ora.geometric_pixel_screen(inst.coords, inst.resolution, flip_x=False)
+    S, T = view.n_screen, len(edges) - 1
+    o = c_oracle.CDetectorView(inst.detector_number, ps, S, edges, threads=_threads())
+    with torch.cuda.stream(torch.cuda.Stream(dev)):
+        eng = BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                            n_screen=S, device=0, stream=torch.cuda.current_stream(dev).cuda_stream)
+        n = 30_000_000
+        prev = np.zeros(S * T, dtype=np.uint64)
+        for k, seed in enumerate((11, 12)):
+            pid, toa = synthetic.torch_dream_events(n, inst, seed, dev)
+            if k == 0:
+                # the most frequent pixel (Zipf rank 1, on screen in replica 1)
+                # at a TOA inside the edges
+                p0 = int(np.argmax(synthetic.zipf_pixel_weights(inst.detector_number.size)))
+                assert ps[1].ravel()[p0] >= 0
+                pid0 = int(inst.detector_number.ravel()[p0])
+                toa0 = int((edges[T // 2] + edges[T // 2 + 1]) / 2)
+                hot = torch.rand(n, device=dev, generator=torch.Generator(dev).manual_seed(5)) < 0.9
+                pid = torch.where(hot, torch.full_like(pid, pid0), pid)
+                toa = torch.where(hot, torch.full_like(toa, toa0), toa)
+            step = 10_000_000
+            eng.stage_tensors_batch([(pid[i:i + step], toa[i:i + step]) for i in range(0, n, step)])
+            eng.accumulate(1)
+            res = eng.finalize(hists=True)
+            assert eng.info()['last_strategy'] == 'split'
+            assert eng.counter('sieve_pair') == 1
+            wraps = eng.counter('sieve_pair_wraps')
+            if k == 0:
+                assert wraps > 100, wraps  # nearly every block wrapped
+                first = wraps
+            else:
+                assert wraps == first  # the normal batch wrapped nowhere
+            cum = o.accumulate(pid.cpu().numpy(), toa.cpu().numpy(), 1).copy()
+            cur = (cum - prev).reshape(S, T)
+            prev = cum
+            np.testing.assert_array_equal(res.current_hist, cur.astype(np.float64))
+            np.testing.assert_array_equal(res.cumulative_hist, cum.reshape(S, T).astype(np.float64))
+            assert res.current_total == int(cur.sum())
+        eng.close()

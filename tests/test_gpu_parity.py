@@ -60,6 +60,11 @@ VARIANTS = [
     {'LDE_KEY24': '0'},
     # hot rows flushed as u32 instead of u16
     {'LDE_HOT16': '0'},
+    # hot counters as u16 pairs in LDS (twice the rows), alone, with few rows
+    # re-selected every batch, and with a large pixel table
+    {'LDE_HOT_PAIR': '1'},
+    {'LDE_HOT_PAIR': '1', 'LDE_HOT_ROWS': '8', 'LDE_HOT_REFRESH': '1'},
+    {'LDE_HOT_PAIR': '1', 'LDE_PIXEL_CACHE_BITS': '14'},
     # per-block release fences: none / also at the end of the sort and pass B
     {'LDE_TAIL_RELEASE': '0'},
     {'LDE_TAIL_RELEASE': '7'},
