@@ -377,10 +377,13 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_accumulate(
 // Monitor: 1-D TOA histogram, LDS layout [bin][32 columns] so the 32 lanes of
 // each half-wave always hit 32 distinct banks (conflict-free for any skew).
 // ---------------------------------------------------------------------------
-template <bool FAST, bool COLUMNS>
+// PF: the next iteration's U groups are loaded before this one's are binned
+// (twice the bytes in flight per lane)
+template <bool FAST, bool COLUMNS, bool PF>
 __global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
                                                  const unsigned char *__restrict__ g_tab,
-                                                 ToaParams tp, uint32_t *__restrict__ hist) {
+                                                 ToaParams tp, uint32_t *__restrict__ hist,
+                                                 int block_ranges) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *s_h = reinterpret_cast<uint32_t *>(smem);
     const int HB = COLUMNS ? tp.T * 32 : tp.T;
@@ -403,14 +406,55 @@ __global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
     // events in flight (indices clamped, so the loads are unconditional)
     constexpr int U = 4;
     int rot = 0;  // as in k_bin_atomic: small messages side by side
-    for (int si = 0; si < n_segs; ++si) {
+    // block ranges (host: every message at least a block; chunk0 = its first
+    // block): each block streams one message with that message's own stride,
+    // so no lane sweeps a message's partial last stride and moves on
+    int s_lo = 0, s_hi = n_segs;
+    long long stride_b = stride, i0_b = 0;
+    if (block_ranges) {
+        int si = 0;
+        for (int j = 1; j < n_segs; ++j)
+            if ((long long)blockIdx.x >= segs.s[j].chunk0) si = j;
+        const long long b0 = segs.s[si].chunk0;
+        const long long b1 = si + 1 < n_segs ? segs.s[si + 1].chunk0 : (long long)gridDim.x;
+        s_lo = si;
+        s_hi = si + 1;
+        stride_b = (b1 - b0) * blockDim.x;
+        i0_b = ((long long)blockIdx.x - b0) * blockDim.x + threadIdx.x;
+    }
+    for (int si = s_lo; si < s_hi; ++si) {
         const SegDesc seg = segs.s[si];
         const long long n = seg.n;
-        const long long i0 = (long long)seg_block(rot) * blockDim.x + threadIdx.x;
-        rot = next_rot(rot, n);
+        const long long stride = stride_b;
+        const long long i0 = block_ranges ? i0_b : (long long)seg_block(rot) * blockDim.x + threadIdx.x;
+        if (!block_ranges) rot = next_rot(rot, n);
         long long tail = 0;
         if (((uintptr_t)seg.toa & 15u) == 0 && n >= 4) {
             const long long n4 = n >> 2;
+            if (PF) {
+                v4i t[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const long long k = i0 + u * stride;
+                    t[u] = ld_stream4(seg.toa + 4 * (k < n4 ? k : n4 - 1));
+                }
+                for (long long i = i0; i < n4; i += stride * U) {
+                    v4i tn[U];  // the next iteration's groups (clamped: always valid addresses)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const long long k = i + (U + u) * stride;
+                        tn[u] = ld_stream4(seg.toa + 4 * (k < n4 ? k : n4 - 1));
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const bool ok = i + u * stride < n4;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) add(t[u][q], ok);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) t[u] = tn[u];
+                }
+            } else {
             for (long long i = i0; i < n4; i += stride * U) {
                 v4i t[U];
 #pragma unroll
@@ -424,6 +468,7 @@ __global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
 #pragma unroll
                     for (int q = 0; q < 4; ++q) add(t[u][q], ok);
                 }
+            }
             }
             tail = n4 << 2;
         }
@@ -550,23 +595,25 @@ hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const 
 
 hipError_t launch_monitor(const SegKarg &segs, int n_segs, const unsigned char *tab,
                           const ToaParams &tp, uint32_t *hist, int grid, hipStream_t st,
-                          hipEvent_t start, hipEvent_t stop) {
+                          hipEvent_t start, hipEvent_t stop, bool pf, bool block_ranges) {
     if (n_segs < 1 || n_segs > kKargSegs) return hipErrorInvalidValue;
     const bool columns = tp.T <= kMonitorColumnsMaxT;
     const size_t hb = align16((size_t)((columns ? tp.T * 32 : tp.T) + 64) * 4);
     const size_t sm = hb + toa_lds_bytes(tp);
-#define LDE_MON(F, C)                                                                          \
+#define LDE_MON2(F, C, P)                                                                      \
     do {                                                                                       \
-        (void)hipFuncSetAttribute((const void *)k_monitor<F, C>,                               \
+        (void)hipFuncSetAttribute((const void *)k_monitor<F, C, P>,                            \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);        \
-        hipExtLaunchKernelGGL((k_monitor<F, C>), dim3(grid), dim3(256), sm, st, start, stop, 0,   \
-                              segs, n_segs, tab, tp, hist);                                    \
+        hipExtLaunchKernelGGL((k_monitor<F, C, P>), dim3(grid), dim3(256), sm, st, start, stop, 0, \
+                              segs, n_segs, tab, tp, hist, block_ranges ? 1 : 0);             \
     } while (0)
+#define LDE_MON(F, C) do { if (pf) LDE_MON2(F, C, true); else LDE_MON2(F, C, false); } while (0)
     if (tp.fast && columns) LDE_MON(true, true);
     else if (tp.fast) LDE_MON(true, false);
     else if (columns) LDE_MON(false, true);
     else LDE_MON(false, false);
 #undef LDE_MON
+#undef LDE_MON2
     return hipGetLastError();
 }
 

@@ -1545,9 +1545,26 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
         auto flush = [&]() -> int {
             if (k == 0) return LDE_OK;
             long long g = (n / 16 + 255) / 256;  // 16 events per lane and iteration
-            g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 4));
+            g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * env_ll("LDE_MON_GRID", 4)));
+            // large messages: blocks in ranges proportional to the message
+            // sizes (each block streams one message); small ones rotate
+            bool ranges = false;
+            if (env_ll("LDE_MON_RANGES", 1) != 0 && k <= g / 4) {
+                long long mn = ka.s[0].n;
+                for (int i = 1; i < k; ++i) mn = std::min(mn, ka.s[i].n);
+                if (mn >= 65536) {
+                    ranges = true;
+                    long long acc = 0;
+                    for (int i = 0; i < k; ++i) {
+                        // first block of message i: i + its share of the other g - k blocks
+                        ka.s[i].chunk0 = i + (long long)((double)(g - k) * (double)acc / (double)n);
+                        acc += ka.s[i].n;
+                    }
+                }
+            }
             Stamp sp(h, LDE_K_MONITOR);
-            HIPCALL(h, lde::launch_monitor(ka, k, h->d_tab, h->tp, h->d_win32, (int)g, h->stream, sp.a, sp.b));
+            HIPCALL(h, lde::launch_monitor(ka, k, h->d_tab, h->tp, h->d_win32, (int)g, h->stream, sp.a, sp.b,
+                                           env_ll("LDE_MON_PF", 0) != 0, ranges));
             k = 0;
             n = 0;
             return LDE_OK;

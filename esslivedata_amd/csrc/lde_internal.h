@@ -316,7 +316,8 @@ hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const 
 // start/stop (optional): HIP events stamped by the dispatch itself
 hipError_t launch_monitor(const SegKarg &segs, int n_segs, const unsigned char *tab,
                           const ToaParams &tp, uint32_t *hist, int grid, hipStream_t st,
-                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr, bool pf = false,
+                          bool block_ranges = false);
 hipError_t launch_fold_window(uint32_t *win32, unsigned long long *win64, long long n,
                               hipStream_t st);
 hipError_t launch_merge_f32(uint32_t *batch, unsigned long long *win64, float *winf, float *cumf,

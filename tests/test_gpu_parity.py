@@ -115,10 +115,23 @@ def test_monitor_kat_reference_fixture():
     )
 
 
+MONITOR_VARIANTS = [{}, {'LDE_MON_PF': '1'}, {'LDE_MON_PF': '1', 'LDE_MON_GRID': '1'},
+                    {'LDE_MON_RANGES': '1'}, {'LDE_MON_RANGES': '1', 'LDE_MON_PF': '1'},
+                    {'LDE_MON_RANGES': '0'}]
+
+
+@pytest.mark.parametrize('layout', ['large', 'small'])
+@pytest.mark.parametrize('variant', range(len(MONITOR_VARIANTS)))
 @pytest.mark.parametrize('n_bins', [100, 7, 1000, 3000])
-def test_monitor_matches_oracle(n_bins):
+def test_monitor_matches_oracle(n_bins, variant, layout, request):
+    """Several messages per launch, message sizes not multiples of 4 or of
+    the grid; variants: next groups loaded before the current are binned
+    (LDE_MON_PF), one block per CU (many iterations per lane), blocks in
+    ranges per message (LDE_MON_RANGES)."""
     from esslivedata_amd.engine import BinningEngine
 
+    if MONITOR_VARIANTS[variant]:  # the diagnostics build reads the knobs
+        request.getfixturevalue('knobs')(**MONITOR_VARIANTS[variant])
     rng = np.random.default_rng(n_bins)
     edges = np.geomspace(0.5, 71.43, n_bins + 1) * 1e6
     toa = np.concatenate(
@@ -130,7 +143,12 @@ def test_monitor_matches_oracle(n_bins):
         ]
     )
     eng = BinningEngine.monitor(edges)
-    eng.stage(None, toa)
+    # three messages; block ranges per message need messages of >= 65536
+    # three messages: all >= 65536 events (block ranges per message, the
+    # default) or one of 3 events (the grid rotates over the messages)
+    cuts = (0, 100_000, 180_000) if layout == 'large' else (0, 3, 100_003)
+    for lo, hi in zip(cuts, cuts[1:] + (len(toa),)):
+        eng.stage(None, toa[lo:hi])
     eng.accumulate()
     res = eng.finalize(hists=True)
     np.testing.assert_array_equal(res.current_hist.ravel(), ora.monitor_histogram(toa, edges))
