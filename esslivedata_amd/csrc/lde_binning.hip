@@ -53,7 +53,7 @@ __device__ __forceinline__ int next_rot(int rot, long long n) {
 // ATOMIC strategy: one pass, global u32 atomics (agent scope)
 // ---------------------------------------------------------------------------
 template <typename LT, bool FAST>
-__global__ __launch_bounds__(256) void k_bin_atomic(const SegKarg segs, int n_segs,
+__global__ __launch_bounds__(256) void k_bin_atomic(const SegKargAtomic segs, int n_segs,
                                                     const LT *__restrict__ lut, int pid_off,
                                                     unsigned L,
                                                     const unsigned char *__restrict__ g_tab,
@@ -62,8 +62,8 @@ __global__ __launch_bounds__(256) void k_bin_atomic(const SegKarg segs, int n_se
     load_toa_tables(smem, g_tab, tp);
     __syncthreads();
     const long long stride = (long long)gridDim.x * blockDim.x;
-    // up to kKargSegs messages per launch (small batches: BIFROST's 45 bank
-    // messages of 1,000 events take two launches instead of 45); each message
+    // up to kKargSegsAtomic messages per launch (small batches: BIFROST's 45
+    // bank messages of 1,000 events take one launch instead of 45); each message
     // starts on the block after the last one the previous message used, so
     // messages smaller than the grid run on different blocks side by side
     int rot = 0;
@@ -495,7 +495,7 @@ size_t partition_smem(int n_tiles, const ToaParams &tp) {
 }
 
 template <typename LT>
-static hipError_t launch_bin_atomic_t(const SegKarg &seg, int n_segs, const LT *lut, int pid_off,
+static hipError_t launch_bin_atomic_t(const SegKargAtomic &seg, int n_segs, const LT *lut, int pid_off,
                                       unsigned L, const unsigned char *tab, const ToaParams &tp,
                                       uint32_t *hist, int grid, hipStream_t st, hipEvent_t start,
                                       hipEvent_t stop) {
@@ -514,11 +514,11 @@ static hipError_t launch_bin_atomic_t(const SegKarg &seg, int n_segs, const LT *
     return hipGetLastError();
 }
 
-hipError_t launch_bin_atomic(const SegKarg &seg, int n_segs, const void *lut, bool lut16, int pid_off,
+hipError_t launch_bin_atomic(const SegKargAtomic &seg, int n_segs, const void *lut, bool lut16, int pid_off,
                              unsigned L, const unsigned char *tab, const ToaParams &tp,
                              uint32_t *hist, int grid, hipStream_t st, hipEvent_t start,
                              hipEvent_t stop) {
-    if (n_segs < 1 || n_segs > kKargSegs) return hipErrorInvalidValue;
+    if (n_segs < 1 || n_segs > kKargSegsAtomic) return hipErrorInvalidValue;
     return lut16 ? launch_bin_atomic_t(seg, n_segs, (const uint16_t *)lut, pid_off, L, tab, tp, hist, grid, st,
                                        start, stop)
                  : launch_bin_atomic_t(seg, n_segs, (const int *)lut, pid_off, L, tab, tp, hist, grid, st,

@@ -1598,8 +1598,11 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
     }
     h->last_strategy = strat;
     if (strat == LDE_STRATEGY_ATOMIC) {
-        // one launch per kKargSegs messages, descriptors as kernel arguments
-        lde::SegKarg ka{};
+        // one launch per kKargSegsAtomic messages, descriptors as kernel
+        // arguments (LDE_ATOMIC_SEGS: fewer per launch, diagnostics build)
+        lde::SegKargAtomic ka{};
+        const int seg_cap = (int)std::max<long long>(
+            1, std::min<long long>(lde::kKargSegsAtomic, env_ll("LDE_ATOMIC_SEGS", lde::kKargSegsAtomic)));
         int k = 0;
         long long n = 0;
         auto flush = [&]() -> int {
@@ -1617,7 +1620,7 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             if (s.n == 0) continue;
             ka.s[k++] = {s.pid, s.toa, s.n, 0};
             n += s.n;
-            if (k == lde::kKargSegs)
+            if (k == seg_cap)
                 if (int rc = flush()) return rc;
         }
         return flush();

@@ -58,6 +58,12 @@ constexpr int kKargSegs = 24;
 struct SegKarg {
     SegDesc s[kKargSegs];
 };
+// the ATOMIC strategy's launches take up to 64 (BIFROST: a pulse's 45 bank
+// messages in one launch instead of two; 2 KB of kernel arguments)
+constexpr int kKargSegsAtomic = 64;
+struct SegKargAtomic {
+    SegDesc s[kKargSegsAtomic];
+};
 
 struct ToaParams {
     long long lo;   // ceil(edge[0])  (clamped to [INT32_MIN, INT32_MAX + 1])
@@ -106,7 +112,7 @@ inline unsigned grid_for(long long n) {
 
 size_t partition_smem(int n_tiles, const ToaParams &tp);
 
-hipError_t launch_bin_atomic(const SegKarg &seg, int n_segs, const void *lut, bool lut16, int pid_off,
+hipError_t launch_bin_atomic(const SegKargAtomic &seg, int n_segs, const void *lut, bool lut16, int pid_off,
                              unsigned L, const unsigned char *tab, const ToaParams &tp,
                              uint32_t *hist, int grid, hipStream_t st, hipEvent_t start = nullptr,
                              hipEvent_t stop = nullptr);

@@ -285,6 +285,44 @@ def test_bifrost_float32_accumulation():
             np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
 
 
+@pytest.mark.parametrize('segs', [None, '24'])
+@pytest.mark.parametrize('n_msgs', [1, 24, 45, 64, 65, 130])
+def test_atomic_many_messages(n_msgs, segs, request):
+    """ATOMIC with many small messages per accumulate (BIFROST: 45 bank
+    messages of 1,000 events per pulse): up to 64 descriptors per launch
+    (default) or 24 (LDE_ATOMIC_SEGS, diagnostics build); messages of ragged
+    sizes, some not 16-byte aligned, bit-exact against the oracle."""
+    from esslivedata_amd import projection, synthetic
+
+    if segs:
+        request.getfixturevalue('knobs')(LDE_ATOMIC_SEGS=segs)
+    inst = synthetic.bifrost_unified()
+    view = projection.logical_lut(inst.detector_number, transform=synthetic.bifrost_transform)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, 'atomic')
+    ps = ora.logical_screen_index((5, 3, 9, 100), synthetic.bifrost_transform)[0][None, :]
+    o = ora.OracleDetectorView(detector_number=inst.detector_number, pixel_screen=ps,
+                               screen_shape=(15, 900), toa_edges_ns=edges)
+    import torch
+
+    rng = np.random.default_rng(n_msgs)
+    for batch in range(2):
+        pid, toa = synthetic.fake_detector_events(1000 * n_msgs + 37, 1, 13500, seed=batch)
+        dp = torch.as_tensor(pid, device='cuda')
+        dt = torch.as_tensor(toa, device='cuda')
+        cuts = np.sort(rng.choice(np.arange(1, len(pid)), n_msgs - 1, replace=False)) if n_msgs > 1 else []
+        bounds = [0, *[int(c) for c in cuts], len(pid)]
+        # one device segment per message (ragged, mostly misaligned)
+        eng.stage_tensors_batch([(dp[a:b], dt[a:b]) for a, b in zip(bounds[:-1], bounds[1:])])
+        eng.accumulate(0)
+        o.accumulate(pid, toa)
+        assert eng.info()['last_strategy'] == 'atomic'
+        res = eng.finalize(hists=True)
+        exp = o.finalize()
+        np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
+        np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
+
+
 def test_bifrost_float32_partials_match_finalize():
     """float32 views export their exact integer counts as partial outputs;
     rounded once to f32 they equal the handle's own f32 finalize images (every
