@@ -1609,6 +1609,10 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             if (k == 0) return LDE_OK;
             long long g = (n / 4 + 255) / 256;
             g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 8));
+            // at least a block per message: the rotation then starts every
+            // small message on its own block (45 messages of 1,000 events on
+            // 44 blocks ran two messages in series on one)
+            g = std::max<long long>(g, std::min<long long>(k, (long long)h->cus * 8));
             Stamp sp(h, LDE_K_ATOMIC);
             HIPCALL(h, lde::launch_bin_atomic(ka, k, lut, h->lut16, h->pid_off, (unsigned)h->L, h->d_tab,
                                               h->tp, h->d_win32, (int)g, h->stream, sp.a, sp.b));
