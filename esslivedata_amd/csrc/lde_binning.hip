@@ -61,17 +61,24 @@ __global__ __launch_bounds__(256) void k_bin_atomic(const SegKargAtomic segs, in
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     load_toa_tables(smem, g_tab, tp);
     __syncthreads();
-    const long long stride = (long long)gridDim.x * blockDim.x;
     // up to kKargSegsAtomic messages per launch (small batches: BIFROST's 45
-    // bank messages of 1,000 events take one launch instead of 45); each message
-    // starts on the block after the last one the previous message used, so
-    // messages smaller than the grid run on different blocks side by side
-    int rot = 0;
-    for (int si = 0; si < n_segs; ++si) {
-    const SegDesc seg = segs.s[si];
+    // bank messages of 1,000 events take one launch instead of 45).  The host
+    // gives every message a contiguous range of blocks (SegDesc::chunk0 = its
+    // first block; at least one each): a block finds its message with a
+    // binary search and streams it at the range's stride.  (Before, every
+    // block walked the messages in order to find its own, a chain of
+    // dependent descriptor loads that grew the launch by ~0.4 us per message.)
+    int lo = 0, hi = n_segs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (segs.s[mid].chunk0 <= (long long)blockIdx.x) lo = mid; else hi = mid - 1;
+    }
+    const SegDesc seg = segs.s[lo];
+    const long long b0 = seg.chunk0;
+    const long long b1 = lo + 1 < n_segs ? segs.s[lo + 1].chunk0 : (long long)gridDim.x;
+    const long long stride = (b1 - b0) * blockDim.x;
+    const long long i0 = ((long long)blockIdx.x - b0) * blockDim.x + threadIdx.x;
     const long long n = seg.n;
-    const long long i0 = (long long)seg_block(rot) * blockDim.x + threadIdx.x;
-    rot = next_rot(rot, n);
     long long tail = 0;
     if ((((uintptr_t)seg.pid | (uintptr_t)seg.toa) & 15u) == 0) {
         const long long n4 = n >> 2;
@@ -88,7 +95,6 @@ __global__ __launch_bounds__(256) void k_bin_atomic(const SegKargAtomic segs, in
     for (long long i = tail + i0; i < n; i += stride) {
         wave_add_aggregated<4>(hist, event_key<LT, FAST>(ld_global(seg.pid + i), ld_global(seg.toa + i),
                                                          lut, pid_off, L, smem, tp));
-    }
     }
 }
 

@@ -1546,20 +1546,18 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             if (k == 0) return LDE_OK;
             long long g = (n / 16 + 255) / 256;  // 16 events per lane and iteration
             g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * env_ll("LDE_MON_GRID", 4)));
-            // large messages: blocks in ranges proportional to the message
-            // sizes (each block streams one message); small ones rotate
+            // blocks in ranges proportional to the message sizes, at least one
+            // per message (each block streams one message at its own stride;
+            // LDE_MON_RANGES=0: every block walks all messages, rotated)
             bool ranges = false;
-            if (env_ll("LDE_MON_RANGES", 1) != 0 && k <= g / 4) {
-                long long mn = ka.s[0].n;
-                for (int i = 1; i < k; ++i) mn = std::min(mn, ka.s[i].n);
-                if (mn >= 65536) {
-                    ranges = true;
-                    long long acc = 0;
-                    for (int i = 0; i < k; ++i) {
-                        // first block of message i: i + its share of the other g - k blocks
-                        ka.s[i].chunk0 = i + (long long)((double)(g - k) * (double)acc / (double)n);
-                        acc += ka.s[i].n;
-                    }
+            if (env_ll("LDE_MON_RANGES", 1) != 0) {
+                g = std::max<long long>(g, k);
+                ranges = true;
+                long long acc = 0;
+                for (int i = 0; i < k; ++i) {
+                    // first block of message i: i + its share of the other g - k blocks
+                    ka.s[i].chunk0 = i + (long long)((double)(g - k) * (double)acc / (double)n);
+                    acc += ka.s[i].n;
                 }
             }
             Stamp sp(h, LDE_K_MONITOR);
@@ -1607,12 +1605,26 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
         long long n = 0;
         auto flush = [&]() -> int {
             if (k == 0) return LDE_OK;
-            long long g = (n / 4 + 255) / 256;
-            g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 8));
-            // at least a block per message: the rotation then starts every
-            // small message on its own block (45 messages of 1,000 events on
-            // 44 blocks ran two messages in series on one)
-            g = std::max<long long>(g, std::min<long long>(k, (long long)h->cus * 8));
+            // block ranges per message (k_bin_atomic): a group of 4 events per
+            // lane when the grid allows, else ranges proportional to the sizes,
+            // at least one block per message
+            const long long cap = std::max<long long>((long long)h->cus * 8, k);
+            long long g = 0;
+            for (int i = 0; i < k; ++i) g += std::max<long long>(1, (ka.s[i].n + 1023) / 1024);
+            if (g <= cap) {
+                long long b = 0;
+                for (int i = 0; i < k; ++i) {
+                    ka.s[i].chunk0 = b;
+                    b += std::max<long long>(1, (ka.s[i].n + 1023) / 1024);
+                }
+            } else {
+                g = cap;
+                long long acc = 0;
+                for (int i = 0; i < k; ++i) {
+                    ka.s[i].chunk0 = i + (long long)((double)(g - k) * (double)acc / (double)n);
+                    acc += ka.s[i].n;
+                }
+            }
             Stamp sp(h, LDE_K_ATOMIC);
             HIPCALL(h, lde::launch_bin_atomic(ka, k, lut, h->lut16, h->pid_off, (unsigned)h->L, h->d_tab,
                                               h->tp, h->d_win32, (int)g, h->stream, sp.a, sp.b));

@@ -144,8 +144,8 @@ def test_monitor_matches_oracle(n_bins, variant, layout, request):
     )
     eng = BinningEngine.monitor(edges)
     # three messages; block ranges per message need messages of >= 65536
-    # three messages: all >= 65536 events (block ranges per message, the
-    # default) or one of 3 events (the grid rotates over the messages)
+    # three messages: large, or one of 3 events (its block range holds one
+    # block; LDE_MON_RANGES=0: the grid rotates over the messages)
     cuts = (0, 100_000, 180_000) if layout == 'large' else (0, 3, 100_003)
     for lo, hi in zip(cuts, cuts[1:] + (len(toa),)):
         eng.stage(None, toa[lo:hi])
