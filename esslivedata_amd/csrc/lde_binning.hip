@@ -411,7 +411,7 @@ __global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
     // arguments (no descriptor upload in front); per lane U groups of four
     // events in flight (indices clamped, so the loads are unconditional)
     constexpr int U = 4;
-    int rot = 0;  // as in k_bin_atomic: small messages side by side
+    int rot = 0;  // LDE_MON_RANGES=0: small messages side by side, rotated
     // block ranges (host: every message at least a block; chunk0 = its first
     // block): each block streams one message with that message's own stride,
     // so no lane sweeps a message's partial last stride and moves on
@@ -461,20 +461,20 @@ __global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
                     for (int u = 0; u < U; ++u) t[u] = tn[u];
                 }
             } else {
-            for (long long i = i0; i < n4; i += stride * U) {
-                v4i t[U];
+                for (long long i = i0; i < n4; i += stride * U) {
+                    v4i t[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const long long k = i + u * stride;
-                    t[u] = ld_stream4(seg.toa + 4 * (k < n4 ? k : n4 - 1));
+                    for (int u = 0; u < U; ++u) {
+                        const long long k = i + u * stride;
+                        t[u] = ld_stream4(seg.toa + 4 * (k < n4 ? k : n4 - 1));
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const bool ok = i + u * stride < n4;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) add(t[u][q], ok);
+                    }
                 }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const bool ok = i + u * stride < n4;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) add(t[u][q], ok);
-                }
-            }
             }
             tail = n4 << 2;
         }
