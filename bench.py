@@ -85,6 +85,17 @@ def parse():
     ap.add_argument('--batches', type=int, default=3,
                     help='distinct pre-generated batches rotated through the steps (a stream '
                          'never repeats the previous batch, so per-batch predictions are tested)')
+    ap.add_argument('--bifrost-cadence', default='batch', choices=['batch', 'pulse'],
+                    help='batch (the reference cadence, core/job.py:413-433): one accumulate of '
+                         'all 14 x 45 bank messages (one float32 push) and one finalize per step; '
+                         'pulse: one push per pulse, 14 per finalize')
+    ap.add_argument('--shard', default='events', choices=['events', 'banks'],
+                    help='events: every rank bins its own DREAM batches (event-batch sharding); '
+                         "banks: LOKI's nine banks placed on the ranks by assign_banks, each rank "
+                         "binning its banks' streams with no collective (pixel-range sharding)")
+    ap.add_argument('--bank-steps', type=int, default=5,
+                    help='timed steps of the bank-sharded LOKI leg reported beside the DREAM line '
+                         '(bank_sharding; 0 = skip)')
     return ap.parse_args()
 
 
@@ -238,6 +249,145 @@ def profiled_lds(workload: str, kernel: str):
     return out
 
 
+def bank_leg(args, rank: int, world: int, dev, stream, steps: int, warmup: int) -> dict | None:
+    """Pixel-range (bank) sharding, SURVEY 8(e) axis 2: LOKI's nine banks
+    (config/instruments/loki/streams.py:17-27) placed on the ranks with
+    ``assign_banks``; each rank bins its banks' event streams with one engine
+    per bank (one workflow per bank, as the reference's jobs) and no
+    collective touches the data path.  Events per bank and step: pulses x
+    events_per_pulse x (bank pixels / bank-0 pixels), uniform over the bank's
+    pixels.  Returns the whole-node line fields on rank 0 (None elsewhere),
+    with every rank's banks checked bit-exactly against oracle/binning_ref.c."""
+    import torch
+    import torch.distributed as dist
+
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.distributed import assign_banks
+    from esslivedata_amd.engine import BinningEngine
+
+    banks = synthetic.LOKI_BANKS
+    sizes = {name: hi - lo + 1 for name, (lo, hi) in banks.items()}
+    place = assign_banks(sizes, world)
+    p0 = sizes['loki_detector_0']
+    per_pulse = {name: int(round(args.events_per_pulse * sz / p0)) for name, sz in sizes.items()}
+    mine = sorted((name for name, r in place.items() if r == rank), key=lambda n: int(n.rsplit('_', 1)[1]))
+    local = []
+    for name in mine:
+        b = int(name.rsplit('_', 1)[1])
+        inst = synthetic.loki_bank(b)
+        view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution, flip_x=True)
+        eng = BinningEngine(toa_edges_ns=inst.edges.edges_ns(), out_lut=view.lut,
+                            pid_offset=view.pid_offset, n_screen=view.n_screen,
+                            device=dev.index, stream=stream.cuda_stream)
+        lo, hi = banks[name]
+        n_p = per_pulse[name]
+        msgs = []
+        for k in range(2):  # two rotated batches per bank
+            pid, toa = synthetic.torch_uniform_events(n_p * args.pulses, lo, hi, 500 + 37 * b + k, dev)
+            msgs.append((pid, toa, [(pid[p * n_p:(p + 1) * n_p], toa[p * n_p:(p + 1) * n_p])
+                                    for p in range(args.pulses)]))
+        local.append((name, inst, view, eng, msgs))
+    torch.cuda.synchronize(dev)
+
+    def step(i: int) -> None:
+        for _, _, view, eng, msgs in local:
+            eng.stage_tensors_batch(msgs[i % 2][2])
+            eng.accumulate(i % view.n_replicas)
+        for *_, eng, _ in local:  # the first waits for the stream, the others find it done
+            eng.finalize(images=True)
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    # parity: every rank's banks, one more step each, full current histogram
+    # against the C oracle on the same events
+    from oracle import c_oracle
+    from oracle import scipp_semantics as ora
+
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
+    exact = 1
+    for name, inst, view, eng, msgs in local:
+        r_chk = (warmup + steps) % view.n_replicas
+        eng.stage_tensors_batch(msgs[1][2])
+        eng.accumulate(r_chk)
+        chk = eng.finalize(hists=True)
+        ps = ora.geometric_pixel_screen(inst.coords, inst.resolution, flip_x=True)
+        c = c_oracle.CDetectorView(inst.detector_number, ps, view.n_screen, inst.edges.edges_ns(),
+                                   threads=threads)
+        c.accumulate(msgs[1][0].cpu().numpy(), msgs[1][1].cpu().numpy(), r_chk)
+        ref = c.hist.reshape(chk.current_hist.shape).astype(np.float64)
+        exact &= int(np.array_equal(ref, chk.current_hist))
+        eng.close()
+    if world > 1:
+        t = torch.tensor([elapsed, -float(exact)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, exact = float(t[0].item()), int(-t[1].item())
+    if rank != 0:
+        return None
+    total = sum(per_pulse.values()) * args.pulses * steps
+    n_step = sum(per_pulse.values()) * args.pulses
+    return {
+        'value': total / elapsed,
+        'unit': 'events/s',
+        'ms_per_step': 1e3 * elapsed / steps,
+        'steps': steps,
+        'events_per_step': n_step,
+        'step_frac': (BYTES_PER_EVENT * n_step + 4 * 100 * (20736 + 8 * 3888)) / (elapsed / steps) / 1e9
+                     / HBM_PEAK_GBS / world,
+        'banks_per_rank': {str(r): sorted(n for n, d in place.items() if d == r) for r in range(world)},
+        'placement': 'assign_banks (LPT by pixel count), no collective on the data path',
+        'bit_exact_vs_oracle': bool(exact),
+        'note': "LOKI's 9 banks (loki/streams.py:17-27), xy_plane views at loki/factories.py:101-112 "
+                'resolutions, 5 replicas; events per bank proportional to its pixels '
+                f'({args.events_per_pulse} per pulse for bank 0); one engine per bank on each rank',
+    }
+
+
+def bank_main(args, rank: int, world: int, dev) -> None:
+    """``--shard banks``: the bank-sharded LOKI leg as the line itself."""
+    import torch
+    import torch.distributed as dist
+
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    leg = bank_leg(args, rank, world, dev, stream, args.steps, args.warmup)
+    if rank == 0:
+        result = {
+            'metric': 'binned events/sec (whole node), DREAM-scale detector view; % HBM roofline',
+            'value': leg['value'],
+            'unit': 'events/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': leg['ms_per_step'],
+            'higher_is_better': True,
+            'scaling': 'weak' if world <= 9 else 'strong',
+            'vs_baseline': None,
+            'dtype': 'int32',
+            'data': 'synthetic (seeded ev44-shaped streams generated in HBM; no recorded data offline)',
+            'config': {
+                'workload': 'loki_9_banks_xy_plane',
+                'events_per_step': leg['events_per_step'],
+                'pulses_per_step': args.pulses,
+                'parallelism': f'bank sharding x{world} (assign_banks, no collective)',
+            },
+            'bank_sharding': leg,
+            'check': {'bit_exact_vs_oracle': leg['bit_exact_vs_oracle']},
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
@@ -265,6 +415,8 @@ def main():
     from esslivedata_amd import projection, synthetic
     from esslivedata_amd.engine import BinningEngine
 
+    if args.shard == 'banks':
+        return bank_main(args, rank, world, dev)
     monitor = args.workload == 'monitor'
     bifrost = args.workload == 'bifrost'
     if (monitor or bifrost) and (args.view != 'geometric' or args.coordinate != 'toa'):
@@ -326,6 +478,13 @@ def main():
         eng.set_coordinate_lut(d, tab.table, dist0=tab.distance0, dist_step=tab.distance_step,
                                time0=tab.time0, time_step=tab.time_step)
     n_pulse = 45 * 1000 if bifrost else args.events_per_pulse  # bifrost/streams.py:22-43
+    # BIFROST at the reference cadence: the batch's 14 x 45 bank messages are
+    # one push, accumulated once and finalized once per step
+    bifrost_batch = bifrost and args.bifrost_cadence == 'batch'
+    if bifrost:  # the device symbols of the float32 path (profile lookup)
+        KERNEL_SYMBOL['finalize'] = 'k_finalize_f32'
+        if bifrost_batch:
+            KERNEL_SYMBOL['atomic'] = 'k_bin_atomic_blocks'
     n_step = n_pulse * args.pulses
     n_batches = max(1, args.batches)
 
@@ -349,12 +508,19 @@ def main():
     torch.cuda.synchronize(dev)
     nbins = (1 if monitor else view.n_screen) * eng.n_toa_bins
     bpe_step = MONITOR_BYTES_PER_EVENT if monitor else BYTES_PER_EVENT
-    from esslivedata_amd.distributed import OutputReducer
+    from esslivedata_amd.distributed import OutputReducer, PushReducer
 
     # N > 1: every rank keeps its own histograms; per finalize only the
     # published outputs (u64 partial images + totals, 2*S + 4 words) are
-    # RCCL-reduced onto rank 0 (bit-exact integer sums)
-    reducer = OutputReducer(eng, dev) if world > 1 else None
+    # RCCL-reduced onto rank 0 (bit-exact integer sums).  The float32 BIFROST
+    # view merges per push instead (PushReducer: the ranks' exact counts of a
+    # push summed onto rank 0 before its f32 adds, accumulators.py:129-135)
+    reducer = push_reducer = None
+    if world > 1:
+        if bifrost:
+            push_reducer = PushReducer(eng, dev)
+        else:
+            reducer = OutputReducer(eng, dev)
 
     # one device buffer view per ev44 message, made once: in the service each
     # message arrives as its own buffer, slicing here is only how the
@@ -368,6 +534,11 @@ def main():
         batch_pushes = [[[(pid[p * n_pulse + b * 1000 : p * n_pulse + (b + 1) * 1000],
                            toa[p * n_pulse + b * 1000 : p * n_pulse + (b + 1) * 1000])
                           for b in range(45)] for p in range(args.pulses)] for pid, toa in batches]
+        if bifrost_batch:  # one push of all the batch's messages
+            batch_pushes = [[[m for push in pushes for m in push]] for pushes in batch_pushes]
+        # the messages' device pointers, as they arrive (one descriptor table
+        # per push, staged with one call in the step)
+        push_tables = [[eng.device_messages(push) for push in pushes] for pushes in batch_pushes]
 
     # A step bins the batch staged before it, then stages the next batch's
     # messages and finalizes the window: the next pulses' messages reach the
@@ -380,11 +551,15 @@ def main():
     # events (a stream's batches differ; per-batch predictions such as PIXEL's
     # slot sizes are exercised as in the service).
     def step(i: int, stage_next: bool = True):
-        if bifrost:  # every pulse is one accumulate (a float32 push, reference order)
-            for push in batch_pushes[i % n_batches]:
-                eng.stage_tensors_batch(push)
-                eng.accumulate(0)
-            eng.finalize(images=True)
+        if bifrost:  # every push is one accumulate (float32 adds in the reference order)
+            for table in push_tables[i % n_batches]:
+                eng.stage_device_messages(table)
+                if push_reducer is not None:
+                    push_reducer.push(0)
+                else:
+                    eng.accumulate(0)
+            if rank == 0:
+                eng.finalize(images=True)
             return
         eng.accumulate(i % n_rep)
         if stage_next:
@@ -529,7 +704,7 @@ def main():
         # with its profile; this untraced line records the difference
         traffic['trace_overhead'] = traffic['profiled_avg_ms'] / max(ms / max(launches, 1), 1e-9) - 1.0
     bin_ms, bin_n = stats['binning']  # the extra steps
-    n_acc = n_pulse if bifrost else n_step  # events one accumulate bins
+    n_acc = n_pulse if (bifrost and not bifrost_batch) else n_step  # events one accumulate bins
     pipeline_gbs = bpe_step * n_acc / ((bin_ms / max(bin_n, 1)) / 1e3) / 1e9 if bin_ms else 0.0
 
     result = {
@@ -559,6 +734,9 @@ def main():
             'events_per_step': n_step,
             'pulses_per_step': args.pulses,
             'strategy': info['last_strategy'],
+            **({'bifrost_cadence': args.bifrost_cadence,
+                'pushes_per_step': len(batch_pushes[0]),
+                'messages_per_push': len(batch_pushes[0][0])} if bifrost else {}),
             'tile_bits': info['tile_bits'],
             'parallelism': (f'event-batch sharding x{world} + '
                             f'{"RCCL" if dist.get_backend() == "nccl" else dist.get_backend()} '
@@ -624,7 +802,7 @@ def main():
                           f'of the bench batch, {t_c:.2f} s',
             }
     elif rank == 0 and world == 1 and bifrost:
-        # parity leg: one more step (14 f32 pushes) from zeroed accumulators
+        # parity leg: one more step (its f32 pushes) from zeroed accumulators
         # against the oracle's float32 per-push sums (accumulators.py:86-163)
         from oracle import scipp_semantics as ora
 
@@ -640,8 +818,11 @@ def main():
                                                   synthetic.bifrost_transform)[0][None],
             screen_shape=(15, 900), toa_edges_ns=edges, dtype=np.float32)
         t_c = time.perf_counter()
-        for p in range(args.pulses):
-            o.accumulate(pid_h[p * n_pulse : (p + 1) * n_pulse], toa_h[p * n_pulse : (p + 1) * n_pulse])
+        if bifrost_batch:  # one push of the whole batch
+            o.accumulate(pid_h, toa_h)
+        else:
+            for p in range(args.pulses):
+                o.accumulate(pid_h[p * n_pulse : (p + 1) * n_pulse], toa_h[p * n_pulse : (p + 1) * n_pulse])
         exp = o.finalize()
         t_c = time.perf_counter() - t_c
         result['check'] = {
@@ -655,7 +836,7 @@ def main():
             result['cpu_baseline'] = {
                 'value': n_step / t_c, 'unit': 'events/s', 'cores': 1, 'kind': 'port',
                 'sample': f'oracle.scipp_semantics.OracleDetectorView (NumPy, 1 core, float32 '
-                          f'per-push sums) on one step ({args.pulses} pushes, {n_step} events), '
+                          f'per-push sums) on one step ({len(pushes)} push(es), {n_step} events), '
                           f'{t_c:.2f} s',
             }
     elif rank == 0 and world == 1 and not args.no_cpu_baseline and coord is None:
@@ -743,6 +924,16 @@ def main():
                             "rank's partial outputs) vs oracle/binning_ref.c over all ranks' batches",
             }
         dist.barrier()
+    if (args.bank_steps > 0 and args.workload == 'dream' and args.view == 'geometric'
+            and coord is None):
+        # the second 8(e) axis beside the event-batch-sharded line: LOKI's banks
+        # placed on the ranks, no collective (every rank takes part)
+        eng.close()
+        del batches, batch_msgs
+        torch.cuda.empty_cache()
+        leg = bank_leg(args, rank, world, dev, stream, args.bank_steps, 2)
+        if rank == 0:
+            result['bank_sharding'] = leg
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -52,6 +52,32 @@ __device__ __forceinline__ int next_rot(int rot, long long n) {
 // ---------------------------------------------------------------------------
 // ATOMIC strategy: one pass, global u32 atomics (agent scope)
 // ---------------------------------------------------------------------------
+// events i0, i0 + stride, ... of one message, wave-aggregated atomics
+template <typename LT, bool FAST>
+__device__ __forceinline__ void atomic_stream(const SegDesc &seg, long long i0, long long stride,
+                                              const LT *__restrict__ lut, int pid_off, unsigned L,
+                                              const unsigned char *smem, const ToaParams &tp,
+                                              uint32_t *__restrict__ hist) {
+    const long long n = seg.n;
+    long long tail = 0;
+    if ((((uintptr_t)seg.pid | (uintptr_t)seg.toa) & 15u) == 0) {
+        const long long n4 = n >> 2;
+        for (long long i = i0; i < n4; i += stride) {
+            const v4i p = ld_stream4(seg.pid + 4 * i);
+            const v4i t = ld_stream4(seg.toa + 4 * i);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                wave_add_aggregated<4>(hist, event_key<LT, FAST>(p[q], t[q], lut, pid_off, L, smem, tp));
+            }
+        }
+        tail = n4 << 2;
+    }
+    for (long long i = tail + i0; i < n; i += stride) {
+        wave_add_aggregated<4>(hist, event_key<LT, FAST>(ld_global(seg.pid + i), ld_global(seg.toa + i),
+                                                         lut, pid_off, L, smem, tp));
+    }
+}
+
 template <typename LT, bool FAST>
 __global__ __launch_bounds__(256) void k_bin_atomic(const SegKargAtomic segs, int n_segs,
                                                     const LT *__restrict__ lut, int pid_off,
@@ -76,26 +102,29 @@ __global__ __launch_bounds__(256) void k_bin_atomic(const SegKargAtomic segs, in
     const SegDesc seg = segs.s[lo];
     const long long b0 = seg.chunk0;
     const long long b1 = lo + 1 < n_segs ? segs.s[lo + 1].chunk0 : (long long)gridDim.x;
-    const long long stride = (b1 - b0) * blockDim.x;
-    const long long i0 = ((long long)blockIdx.x - b0) * blockDim.x + threadIdx.x;
-    const long long n = seg.n;
-    long long tail = 0;
-    if ((((uintptr_t)seg.pid | (uintptr_t)seg.toa) & 15u) == 0) {
-        const long long n4 = n >> 2;
-        for (long long i = i0; i < n4; i += stride) {
-            const v4i p = ld_stream4(seg.pid + 4 * i);
-            const v4i t = ld_stream4(seg.toa + 4 * i);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                wave_add_aggregated<4>(hist, event_key<LT, FAST>(p[q], t[q], lut, pid_off, L, smem, tp));
-            }
-        }
-        tail = n4 << 2;
-    }
-    for (long long i = tail + i0; i < n; i += stride) {
-        wave_add_aggregated<4>(hist, event_key<LT, FAST>(ld_global(seg.pid + i), ld_global(seg.toa + i),
-                                                         lut, pid_off, L, smem, tp));
-    }
+    atomic_stream<LT, FAST>(seg, ((long long)blockIdx.x - b0) * blockDim.x + threadIdx.x,
+                            (b1 - b0) * blockDim.x, lut, pid_off, L, smem, tp, hist);
+}
+
+// More messages than fit the kernel arguments (BIFROST at the reference
+// cadence: a batch of 14 pulses x 45 bank messages is one push): one
+// descriptor per block in device memory, chunk0 = (the block's index inside
+// its message's block range) << 32 | (that range's length), so a block reads
+// its message with one descriptor load, no search.
+template <typename LT, bool FAST>
+__global__ __launch_bounds__(256) void k_bin_atomic_blocks(const SegDesc *__restrict__ blocks,
+                                                           const LT *__restrict__ lut, int pid_off,
+                                                           unsigned L,
+                                                           const unsigned char *__restrict__ g_tab,
+                                                           ToaParams tp, uint32_t *__restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    load_toa_tables(smem, g_tab, tp);
+    __syncthreads();
+    const SegDesc seg = blocks[blockIdx.x];
+    const long long j = (long long)((unsigned long long)seg.chunk0 >> 32);
+    const long long nb = seg.chunk0 & 0xffffffffLL;
+    atomic_stream<LT, FAST>(seg, j * blockDim.x + threadIdx.x, nb * blockDim.x, lut, pid_off, L, smem,
+                            tp, hist);
 }
 
 // ---------------------------------------------------------------------------
@@ -518,6 +547,36 @@ static hipError_t launch_bin_atomic_t(const SegKargAtomic &seg, int n_segs, cons
                               seg, n_segs, lut, pid_off, L, tab, tp, hist);
     }
     return hipGetLastError();
+}
+
+template <typename LT>
+static hipError_t launch_bin_atomic_blocks_t(const SegDesc *blocks, int grid, const LT *lut, int pid_off,
+                                             unsigned L, const unsigned char *tab, const ToaParams &tp,
+                                             uint32_t *hist, hipStream_t st, hipEvent_t start,
+                                             hipEvent_t stop) {
+    const size_t sm = toa_lds_bytes(tp);
+    if (tp.fast) {
+        (void)hipFuncSetAttribute((const void *)k_bin_atomic_blocks<LT, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipExtLaunchKernelGGL((k_bin_atomic_blocks<LT, true>), dim3(grid), dim3(256), sm, st, start, stop, 0,
+                              blocks, lut, pid_off, L, tab, tp, hist);
+    } else {
+        (void)hipFuncSetAttribute((const void *)k_bin_atomic_blocks<LT, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipExtLaunchKernelGGL((k_bin_atomic_blocks<LT, false>), dim3(grid), dim3(256), sm, st, start, stop, 0,
+                              blocks, lut, pid_off, L, tab, tp, hist);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_atomic_blocks(const SegDesc *blocks, int grid, const void *lut, bool lut16, int pid_off,
+                                    unsigned L, const unsigned char *tab, const ToaParams &tp, uint32_t *hist,
+                                    hipStream_t st, hipEvent_t start, hipEvent_t stop) {
+    if (grid < 1) return hipErrorInvalidValue;
+    return lut16 ? launch_bin_atomic_blocks_t(blocks, grid, (const uint16_t *)lut, pid_off, L, tab, tp, hist,
+                                              st, start, stop)
+                 : launch_bin_atomic_blocks_t(blocks, grid, (const int *)lut, pid_off, L, tab, tp, hist, st,
+                                              start, stop);
 }
 
 hipError_t launch_bin_atomic(const SegKargAtomic &seg, int n_segs, const void *lut, bool lut16, int pid_off,

@@ -273,6 +273,11 @@ struct lde_handle {
     // state
     bool window_has_data = false;
     bool cum_has_data = false;
+    // float32 views: the last push's counts wait in the u32 batch (d_win32)
+    // until the next accumulate merges them or the finalize fuses their f32
+    // adds (k_finalize_f32); the first-push flags are those of that push
+    bool f32_pending = false;
+    int pend_first_win = 0, pend_first_cum = 0;
     bool win64_dirty = false;
     unsigned long long win_events = 0;
     long long events_binned = 0;
@@ -421,8 +426,11 @@ hipError_t wait_stream(lde_handle *h, hipEvent_t ev = nullptr) {
         std::this_thread::sleep_for(std::chrono::microseconds((long long)(pred - kWakeUs)));
         e = query();
         if (e != hipErrorNotReady) {
-            // done before the wake-up: the end is unknown, move the prediction earlier
-            h->wait_pred_us = 0.8 * pred + 0.2 * std::min(pred, 0.8 * since(t0));
+            // done before the wake-up: the end is unknown, so the prediction
+            // drops to half the time slept at once (a load drop, e.g. a 5 ms
+            // wait becoming 0.5 ms, must not oversleep finalize after finalize;
+            // the spin phase re-learns the true wait from the next one)
+            h->wait_pred_us = 0.5 * since(t0);
             return e;
         }
     }
@@ -693,8 +701,17 @@ struct Stamp {
             }
         }
     }
+    // set once the stamped launch succeeded: a launch that failed recorded
+    // neither event, so they go back to the pool instead of being resolved
+    bool done = false;
     ~Stamp() {
-        if (a) h->launches.push_back({kid, a, b});
+        if (!a) return;
+        if (done) {
+            h->launches.push_back({kid, a, b});
+        } else {
+            h->event_pool.push_back(a);
+            h->event_pool.push_back(b);
+        }
     }
 };
 
@@ -1269,6 +1286,7 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             key_w24 = ka.k24 != 0;
             Stamp sp(h, LDE_K_COORD);  // k_event_key, stamped by its own dispatch
             HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream, sp.a, sp.b));
+            sp.done = true;
             ksd.push_back({h->d_cbin, h->d_cbin, chunks * lde::kChunk, 0});
         }
         const std::vector<lde::SegDesc> &ssd = coord_deferred ? ksd : sd;
@@ -1521,11 +1539,13 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         Stamp sp(h, LDE_K_PIXEL);
         HIPCALL(h, lde::launch_pixel(a, h->pix, replica, (uint32_t)per, (int)max_items, h->d_pitems,
                                      h->d_pitem_count, h->d_win32, h->stream, 0, sp.a, sp.b));
+        sp.done = true;
     }
     {
         Stamp sp(h, LDE_K_PAGE_ACC);
         HIPCALL(h, lde::launch_pixel(a, h->pix, replica, (uint32_t)per, (int)max_items, h->d_pitems,
                                      h->d_pitem_count, h->d_win32, h->stream, 1, sp.a, sp.b));
+        sp.done = true;
     }
     return LDE_OK;
 }
@@ -1563,6 +1583,7 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             Stamp sp(h, LDE_K_MONITOR);
             HIPCALL(h, lde::launch_monitor(ka, k, h->d_tab, h->tp, h->d_win32, (int)g, h->stream, sp.a, sp.b,
                                            env_ll("LDE_MON_PF", 0) != 0, ranges));
+            sp.done = true;
             k = 0;
             n = 0;
             return LDE_OK;
@@ -1601,6 +1622,37 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
         lde::SegKargAtomic ka{};
         const int seg_cap = (int)std::max<long long>(
             1, std::min<long long>(lde::kKargSegsAtomic, env_ll("LDE_ATOMIC_SEGS", lde::kKargSegsAtomic)));
+        long long n_msgs = 0;
+        for (const Segment &s : segs) n_msgs += s.n > 0 ? 1 : 0;
+        if (n_msgs > lde::kKargSegsAtomic && seg_cap == lde::kKargSegsAtomic) {
+            // more messages than fit the kernel arguments (BIFROST's 630 bank
+            // messages of a 14-pulse batch, one push): one launch with a
+            // descriptor per block in device memory -- per message
+            // ceil(n / 1024) blocks, or (beyond 8 blocks per CU in all) a share
+            // proportional to its size, at least one
+            const long long cap = std::max<long long>((long long)h->cus * 8, n_msgs);
+            long long g = 0;
+            for (const Segment &s : segs)
+                if (s.n > 0) g += std::max<long long>(1, (s.n + 1023) / 1024);
+            const bool prop = g > cap;
+            std::vector<lde::SegDesc> bd;
+            bd.reserve((size_t)std::min(g, cap + n_msgs));
+            for (const Segment &s : segs) {
+                if (s.n == 0) continue;
+                const long long nb = prop ? std::max<long long>(1, (long long)((double)cap * (double)s.n /
+                                                                                (double)total))
+                                          : std::max<long long>(1, (s.n + 1023) / 1024);
+                for (long long j = 0; j < nb; ++j)
+                    bd.push_back({s.pid, s.toa, s.n, (long long)(((unsigned long long)j << 32) | (unsigned long long)nb)});
+            }
+            if (int rc = upload_segments(h, bd)) return rc;
+            Stamp sp(h, LDE_K_ATOMIC);
+            HIPCALL(h, lde::launch_bin_atomic_blocks(h->d_segs, (int)bd.size(), lut, h->lut16, h->pid_off,
+                                                     (unsigned)h->L, h->d_tab, h->tp, h->d_win32, h->stream,
+                                                     sp.a, sp.b));
+            sp.done = true;
+            return LDE_OK;
+        }
         int k = 0;
         long long n = 0;
         auto flush = [&]() -> int {
@@ -1628,6 +1680,7 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             Stamp sp(h, LDE_K_ATOMIC);
             HIPCALL(h, lde::launch_bin_atomic(ka, k, lut, h->lut16, h->pid_off, (unsigned)h->L, h->d_tab,
                                               h->tp, h->d_win32, (int)g, h->stream, sp.a, sp.b));
+            sp.done = true;
             k = 0;
             n = 0;
             return LDE_OK;
@@ -1926,6 +1979,18 @@ int zero_state(lde_handle *h) {
     h->cum_has_data = false;
     h->win64_dirty = false;
     h->win_events = 0;
+    h->f32_pending = false;
+    return LDE_OK;
+}
+
+// float32 views: the pending push's f32 adds (k_merge_f32), before anything
+// else reads or writes the f32 accumulators or the batch
+int flush_f32(lde_handle *h) {
+    if (!h->f32_pending) return LDE_OK;
+    Timed tm(h, LDE_K_FINALIZE);
+    HIPCALL(h, lde::launch_merge_f32(h->d_win32, h->d_win64, h->d_winf, h->d_cumf, h->nbins,
+                                     h->pend_first_win, h->pend_first_cum, h->stream));
+    h->f32_pending = false;
     return LDE_OK;
 }
 
@@ -2656,6 +2721,7 @@ int lde_push_u64(lde_handle *h, const void *d_counts) {
     if (h->out_dtype != LDE_F32) return fail(h, LDE_EINVAL, "lde_push_u64 is for float32 views");
     DeviceGuard guard(h->device);
     if (int rc = ensure_win64(h)) return rc;
+    if (int rc = flush_f32(h)) return rc;
     {
         Timed tm(h, LDE_K_FINALIZE);
         HIPCALL(h, lde::launch_merge_f32_u64((const unsigned long long *)d_counts, h->d_win64,
@@ -2676,6 +2742,8 @@ int accumulate_impl(lde_handle *h, int32_t replica, unsigned long long *d_push) 
         return fail(h, LDE_EINVAL, "replica %d out of range [0, %d)", replica, h->R);
     DeviceGuard guard(h->device);
     if (h->probe) h->t_acc0 = std::chrono::steady_clock::now();
+    // the batch buffer is about to be binned into: the last push merges first
+    if (int rc = flush_f32(h)) return rc;
     std::vector<Segment> segs;
     if (h->staged_host > 0) segs.push_back({h->d_spid, h->d_stoa, h->staged_host});
     for (const Segment &s : h->dev_segments) segs.push_back(s);
@@ -2763,10 +2831,10 @@ int accumulate_impl(lde_handle *h, int32_t replica, unsigned long long *d_push) 
         return LDE_OK;
     }
     if (f32) {
-        Timed tm(h, LDE_K_FINALIZE);
-        HIPCALL(h, lde::launch_merge_f32(h->d_win32, h->d_win64, h->d_winf, h->d_cumf, h->nbins,
-                                         h->window_has_data ? 0 : 1, h->cum_has_data ? 0 : 1,
-                                         h->stream));
+        // this push's f32 adds wait for the next accumulate or the finalize
+        h->f32_pending = true;
+        h->pend_first_win = h->window_has_data ? 0 : 1;
+        h->pend_first_cum = h->cum_has_data ? 0 : 1;
         h->win64_dirty = true;
         h->win_events = 0;
     }
@@ -2801,28 +2869,39 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
     void *const map_cum = mapped_device_ptr(out->cumulative_image, img_bytes);
     if (map_cur) img_cur = map_cur;
     if (map_cum) img_cum = map_cum;
-    if (f32) {
-        // images/hists come from the f32 accumulators (mirrors f32 += order)
-        if (out->current_image)
-            HIPCALL(h, lde::launch_rows_f32(h->d_winf, h->S, h->T, h->range_lo, h->range_hi,
-                                            (float *)img_cur, h->stream));
-        if (out->cumulative_image)
-            HIPCALL(h, lde::launch_rows_f32(h->d_cumf, h->S, h->T, h->range_lo, h->range_hi,
-                                            (float *)img_cum, h->stream));
-        if (want_cur_hist)
-            HIPCALL(h, hipMemcpyAsync(out->current_hist, h->d_winf, nb * 4, hipMemcpyDeviceToHost,
-                                      h->stream));
-        if (want_cum_hist)
-            HIPCALL(h, hipMemcpyAsync(out->cumulative_hist, h->d_cumf, nb * 4,
-                                      hipMemcpyDeviceToHost, h->stream));
-    }
     int n_parts = 0;
     // split finalize: the host waits only for the images and totals (the
     // window's rows); the window's fold into the cumulative histogram runs
     // behind the ready event, while the host turns around
     const bool split = !f32 && !want_cur_hist && !want_cum_hist && h->fin_split &&
                        lde::finalize_split_ok(h->T);
-    if (split) {
+    if (f32) {
+        // one pass: the pending push's f32 adds, images, exact totals and
+        // cumulative, window reset (k_finalize_f32)
+        unsigned char *d_tail = pk + (size_t)h->S * 16;
+        float *snap = nullptr;
+        if (want_cur_hist) {
+            if (!h->d_snap)
+                if (int rc = dev_alloc(h, &h->d_snap, nb)) return rc;
+            snap = reinterpret_cast<float *>(h->d_snap);
+        }
+        {
+            Stamp sp(h, LDE_K_FINALIZE);
+            HIPCALL(h, lde::launch_finalize_f32(
+                           h->f32_pending ? h->d_win32 : nullptr, h->d_win64, h->d_cum, h->d_winf, h->d_cumf, snap,
+                           h->S, h->T, h->range_lo, h->range_hi, h->pend_first_win, h->pend_first_cum,
+                           out->current_image ? (float *)img_cur : nullptr,
+                           out->cumulative_image ? (float *)img_cum : nullptr, (unsigned long long *)(d_tail + 48),
+                           h->d_overflow, (uint32_t *)(d_tail + 32), &n_parts, h->stream, sp.a, sp.b));
+            sp.done = true;
+        }
+        h->f32_pending = false;
+        if (want_cur_hist)
+            HIPCALL(h, hipMemcpyAsync(out->current_hist, snap, nb * 4, hipMemcpyDeviceToHost, h->stream));
+        if (want_cum_hist)
+            HIPCALL(h, hipMemcpyAsync(out->cumulative_hist, h->d_cumf, nb * 4, hipMemcpyDeviceToHost,
+                                      h->stream));
+    } else if (split) {
         unsigned char *d_tail = pk + (size_t)h->S * 16;
         if (!h->d_cum_rows)
             if (int rc = dev_alloc(h, &h->d_cum_rows, 2 * (size_t)h->S)) return rc;
@@ -2839,6 +2918,7 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
                            out->cumulative_image ? img_cum : nullptr, h->d_overflow,
                            (uint32_t *)(d_tail + 32), (unsigned long long *)(d_tail + 48), &n_parts,
                            h->stream, sp.a, sp.b));
+            sp.done = true;
         }
         if (!h->hd_pack)
             HIPCALL(h, hipMemcpyAsync(h->h_pack, h->d_pack, (size_t)h->S * 16 + 48 + 32 * (size_t)n_parts,
@@ -2854,10 +2934,10 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
         // pack (summed here on the host: no k_sum_totals launch and gap)
         unsigned char *d_tail = pk + (size_t)h->S * 16;
         HIPCALL(h, lde::launch_finalize(
-                       f32 ? 1 : 0, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
-                       (want_cur_hist && !f32) ? h->d_snap : nullptr, h->S, h->T, h->range_lo,
-                       h->range_hi, (!f32 && out->current_image) ? img_cur : nullptr,
-                       (!f32 && out->cumulative_image) ? img_cum : nullptr, h->d_tot4,
+                       0, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
+                       want_cur_hist ? h->d_snap : nullptr, h->S, h->T, h->range_lo,
+                       h->range_hi, out->current_image ? img_cur : nullptr,
+                       out->cumulative_image ? img_cum : nullptr, h->d_tot4,
                        (unsigned long long *)d_tail, h->d_overflow, (uint32_t *)(d_tail + 32),
                        h->stream, (unsigned long long *)(d_tail + 48), &n_parts));
     }
@@ -2886,7 +2966,6 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
         HIPCALL(h, hipStreamSynchronize(h->stream));
         convert_u64(tmp.data(), out->cumulative_hist, (long long)nb, LDE_F64);
     }
-    if (f32) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
     if (!split) HIPCALL(h, wait_stream(h));
     const auto t_waited = h->probe ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
     struct PostProbe {
@@ -2921,6 +3000,7 @@ int lde_finalize_partials(lde_handle *h, void *d_out) {
     if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
     if (!d_out) return fail(h, LDE_EINVAL, "output buffer is NULL");
     DeviceGuard guard(h->device);
+    if (int rc = flush_f32(h)) return rc;  // the pending push's f32 adds before the window restarts
     unsigned long long *o = (unsigned long long *)d_out;
     {
         // float32 views keep exact integer window (win64) and cumulative
@@ -2952,6 +3032,7 @@ int lde_read_histogram(lde_handle *h, int32_t which, void *host_out) {
     DeviceGuard guard(h->device);
     const size_t nb = (size_t)h->nbins;
     if (h->out_dtype == LDE_F32) {
+        if (int rc = flush_f32(h)) return rc;
         HIPCALL(h, hipMemcpyAsync(host_out, which == LDE_CURRENT ? h->d_winf : h->d_cumf, nb * 4,
                                   hipMemcpyDeviceToHost, h->stream));
         HIPCALL(h, hipStreamSynchronize(h->stream));
@@ -3042,6 +3123,8 @@ int lde_group_spectra(lde_handle *h, int32_t slot, int32_t which, void *host_out
     DeviceGuard guard(h->device);
     const size_t n = (size_t)gs.n_groups * h->T;
     const bool f32 = h->out_dtype == LDE_F32;
+    if (f32)
+        if (int rc = flush_f32(h)) return rc;
     if (!gs.all_single) HIPCALL(h, hipMemsetAsync(gs.d_out, 0, n * 8, h->stream));
     {
         Timed tm(h, LDE_K_FINALIZE);

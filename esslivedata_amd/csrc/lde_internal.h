@@ -116,6 +116,11 @@ hipError_t launch_bin_atomic(const SegKargAtomic &seg, int n_segs, const void *l
                              unsigned L, const unsigned char *tab, const ToaParams &tp,
                              uint32_t *hist, int grid, hipStream_t st, hipEvent_t start = nullptr,
                              hipEvent_t stop = nullptr);
+// one descriptor per block (chunk0 = block index in its message << 32 | the
+// message's block count), any number of messages
+hipError_t launch_bin_atomic_blocks(const SegDesc *blocks, int grid, const void *lut, bool lut16, int pid_off,
+                                    unsigned L, const unsigned char *tab, const ToaParams &tp, uint32_t *hist,
+                                    hipStream_t st, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 hipError_t launch_partition(const PartitionArgs &a, hipStream_t st);
 struct PagedArgs {
     int tile_bits;
@@ -354,6 +359,14 @@ hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *wi
                            unsigned long long *host_parts = nullptr, int *n_parts = nullptr);
 hipError_t launch_rows_f32(const float *h, long long S, int T, int lo, int hi, float *img,
                            hipStream_t st);
+// float32 finalize in one pass with the window's pending push (batch, may be
+// null): f32 adds, images, exact totals and cumulative, window reset
+hipError_t launch_finalize_f32(uint32_t *batch, unsigned long long *win64, unsigned long long *cum,
+                               float *winf, float *cumf, float *snap, long long S, int T, int lo, int hi,
+                               int first_win, int first_cum, float *cur_img, float *cum_img,
+                               unsigned long long *host_parts, const uint32_t *ovf_src, uint32_t *ovf_dst,
+                               int *n_parts, hipStream_t st, hipEvent_t start = nullptr,
+                               hipEvent_t stop = nullptr);
 // items: {group, begin, end, group has a single item}; out zeroed unless every
 // group is a single item
 constexpr int GROUP_ITEM = 64;  // screens per work item of k_group_spectra

@@ -393,6 +393,81 @@ __global__ __launch_bounds__(1024) void k_sum_totals(unsigned long long *__restr
     if (ovf_dst && threadIdx.x == 4) *ovf_dst = ovf_src ? *ovf_src : 0u;
 }
 
+// Finalize of a float32 view (BIFROST) in one pass, with the window's last
+// push still in the u32 batch (the reference cadence is one push per
+// finalize, SRC/core/job.py:413-433): per bin that push's f32 adds in the
+// reference order (window += f32(b), cumulative += f32(b); the adds k_merge_f32
+// would have made), the images as k_rows_f32 sums them (f32 values over the
+// TOA range in f64, rounded once), the exact integer totals and cumulative
+// (cum += win64 + b), and the window reset (f32, u64 and the batch).  batch =
+// nullptr: no pending push.  snap (optional): the f32 window before its reset.
+// One wave per screen row; per-block total partials at totals[4 + 4 b].
+__global__ __launch_bounds__(256) void k_finalize_f32(
+    uint32_t *__restrict__ batch, unsigned long long *__restrict__ win64,
+    unsigned long long *__restrict__ cum, float *__restrict__ winf, float *__restrict__ cumf,
+    float *__restrict__ snap, long long S, int T, int lo, int hi, int first_win, int first_cum,
+    float *__restrict__ cur_img, float *__restrict__ cum_img, unsigned long long *__restrict__ totals,
+    const uint32_t *__restrict__ ovf_src, uint32_t *__restrict__ ovf_dst) {
+    typedef unsigned long long u64;
+    __shared__ u64 s_tot[4][4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    u64 acc[4] = {0, 0, 0, 0};
+    for (long long s = (long long)blockIdx.x * 4 + wid; s < S; s += (long long)gridDim.x * 4) {
+        double rwf = 0.0, rcf = 0.0;
+        u64 rw = 0, rc = 0, tw = 0, tc = 0;
+        for (int i = lane; i < T; i += 64) {
+            const long long k = s * T + i;
+            const uint32_t b = batch ? batch[k] : 0u;
+            float wf = winf[k], cf = cumf[k];
+            if (batch) {
+                const float fb = (float)b;
+                wf = first_win ? fb : wf + fb;
+                cf = first_cum ? fb : cf + fb;
+                batch[k] = 0;
+            }
+            cumf[k] = cf;
+            winf[k] = 0.f;
+            if (snap) snap[k] = wf;
+            const u64 w = win64[k] + b;
+            const u64 c = cum[k] + w;
+            win64[k] = 0;
+            cum[k] = c;
+            tw += w;
+            tc += c;
+            if (i >= lo && i < hi) {
+                rw += w;
+                rc += c;
+                rwf += (double)wf;
+                rcf += (double)cf;
+            }
+        }
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) {
+            rwf += __shfl_xor(rwf, d, 64);
+            rcf += __shfl_xor(rcf, d, 64);
+            rw += __shfl_xor(rw, d, 64);
+            rc += __shfl_xor(rc, d, 64);
+            tw += __shfl_xor(tw, d, 64);
+            tc += __shfl_xor(tc, d, 64);
+        }
+        if (lane == 0) {
+            if (cur_img) cur_img[s] = (float)rwf;
+            if (cum_img) cum_img[s] = (float)rcf;
+            acc[0] += tw;
+            acc[1] += rw;
+            acc[2] += tc;
+            acc[3] += rc;
+        }
+    }
+    if (lane == 0)
+        for (int q = 0; q < 4; ++q) s_tot[wid][q] = acc[q];
+    __syncthreads();
+    if (ovf_dst && blockIdx.x == 0 && threadIdx.x == 4) *ovf_dst = ovf_src ? *ovf_src : 0u;
+    if (threadIdx.x < 4)
+        totals[4 + (size_t)blockIdx.x * 4 + threadIdx.x] =
+            s_tot[0][threadIdx.x] + s_tot[1][threadIdx.x] + s_tot[2][threadIdx.x] + s_tot[3][threadIdx.x];
+}
+
 // f32-mode image rows: sum of f32 values over the TOA range in f64, rounded once
 __global__ __launch_bounds__(256) void k_rows_f32(const float *__restrict__ h, long long S, int T,
                                                   int lo, int hi, float *__restrict__ img) {
@@ -581,6 +656,21 @@ hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *wi
     else
         launch_finalize_t<double>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals,
                                   tot_copy, ovf_src, ovf_dst, host_parts, n_parts, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize_f32(uint32_t *batch, unsigned long long *win64, unsigned long long *cum,
+                               float *winf, float *cumf, float *snap, long long S, int T, int lo, int hi,
+                               int first_win, int first_cum, float *cur_img, float *cum_img,
+                               unsigned long long *host_parts, const uint32_t *ovf_src, uint32_t *ovf_dst,
+                               int *n_parts, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
+    long long blocks = (S + 3) / 4;
+    if (blocks > kHostPartials) blocks = kHostPartials;
+    if (blocks < 1) blocks = 1;
+    hipExtLaunchKernelGGL(k_finalize_f32, dim3((unsigned)blocks), dim3(256), 0, st, start, stop, 0, batch,
+                          win64, cum, winf, cumf, snap, S, T, lo, hi, first_win, first_cum, cur_img, cum_img,
+                          host_parts - 4, ovf_src, ovf_dst);
+    *n_parts = (int)blocks;
     return hipGetLastError();
 }
 

@@ -1,10 +1,13 @@
-"""Minimal labelled-array container for workflow outputs.
+"""Labelled-array outputs of the workflows.
 
-The reference returns ``scipp.DataArray`` outputs that downstream code only
-serialises to da00 (SRC/kafka/sink_serializers.py:75-89).  scipp is not part
-of this image, so outputs use this small stand-in with the same information:
-dims, values (numpy), unit and named coords.  ``to_scipp()`` converts when
-scipp is importable.
+The reference returns ``scipp.DataArray`` outputs: the unchanged caller
+``Job._add_time_coords`` stamps them (SRC/core/job.py:212-262) and
+``Da00Serializer`` serialises them (SRC/kafka/sink_serializers.py:75-89,
+``scipp_to_da00``, SRC/kafka/scipp_da00_compat.py:22-116).  The workflows
+build their outputs in this small stand-in (dims, numpy values, unit, named
+coords) and :func:`publish` hands them over as ``scipp.DataArray`` whenever
+``import scipp`` succeeds, so both callers work unchanged; without scipp (this
+image) the stand-ins are returned, with the same information.
 """
 
 from __future__ import annotations
@@ -63,21 +66,78 @@ class DataArray:
     def assign_coords(self, **coords) -> 'DataArray':
         new = dict(self.coords)
         for k, v in coords.items():
-            new[k] = v if isinstance(v, Variable) else Variable((), v)
+            # variables (stand-in or scipp) are kept; plain values become 0-D
+            new[k] = v if isinstance(v, Variable) or hasattr(v, 'dims') else Variable((), v)
         return DataArray(self.values, self.dims, self.unit, new, self.name)
 
-    def to_scipp(self):  # pragma: no cover - scipp absent in this image
-        import scipp as sc
+    def to_scipp(self):
+        """The same array as a ``scipp.DataArray`` (dtypes kept: float32
+        BIFROST counts stay float32, the int64 'ns' time coords int64)."""
+        sc = scipp_module()
+        if sc is None:
+            raise ImportError('scipp is not importable')
+        coords = {k: _sc_variable(sc, v.dims, v.values, v.unit) if isinstance(v, Variable) else v
+                  for k, v in self.coords.items()}
+        return sc.DataArray(_sc_variable(sc, self.dims, self.values, self.unit), coords=coords)
 
-        coords = {
-            k: sc.array(dims=list(v.dims), values=v.values, unit=v.unit)
-            if v.dims
-            else sc.scalar(v.values, unit=v.unit)
-            for k, v in self.coords.items()
-        }
-        data = (
-            sc.array(dims=list(self.dims), values=self.values, unit=self.unit)
-            if self.dims
-            else sc.scalar(self.value, unit=self.unit)
-        )
-        return sc.DataArray(data, coords=coords)
+
+# ``import scipp`` is attempted once per process: a failing import costs a
+# path search, and finalize runs per batch (reset_scipp_module() re-probes)
+_SCIPP: list = []
+
+
+def scipp_module():
+    """The scipp module, or None when it is not importable."""
+    if not _SCIPP:
+        try:
+            import scipp
+        except ImportError:
+            scipp = None
+        _SCIPP.append(scipp)
+    return _SCIPP[0]
+
+
+def reset_scipp_module() -> None:
+    _SCIPP.clear()
+
+
+def _sc_variable(sc, dims, values, unit):
+    a = np.asarray(values)
+    if not dims:
+        return sc.scalar(a.item(), unit=unit, dtype=str(a.dtype))
+    return sc.array(dims=list(dims), values=a, unit=unit, dtype=str(a.dtype))
+
+
+def scalar(value, *, unit: str | None = None):
+    """A 0-D variable: ``sc.scalar`` when scipp is importable, else the stand-in
+    (``Timestamp.to_scipp``, SRC/core/timestamp.py:216-220)."""
+    sc = scipp_module()
+    if sc is not None:
+        return _sc_variable(sc, (), value, unit)
+    return Variable((), np.asarray(value), unit)
+
+
+def publish(outputs: dict) -> dict:
+    """The workflow's output dict as the reference's callers receive it:
+    stand-ins converted to ``scipp.DataArray`` when scipp is importable (other
+    values, e.g. a caller's own ROI request echoed back, pass unchanged)."""
+    if scipp_module() is None:
+        return outputs
+    return {k: v.to_scipp() if isinstance(v, DataArray) else v for k, v in outputs.items()}
+
+
+def add_time_coords(data: dict, start_time, end_time) -> dict:
+    """``Job._add_time_coords`` (SRC/core/job.py:212-262) for stand-in
+    outputs: 0-D ``start_time`` / ``time`` (int64, 'ns') on every DataArray
+    that carries neither yet; no time bounds -> ValueError."""
+    if start_time is None or end_time is None:
+        raise ValueError('Job has no time bounds to stamp on its outputs: finalized before '
+                         'accumulating any primary data.')
+    st, tt = start_time.to_scipp(), end_time.to_scipp()
+
+    def stamp(v):
+        if 'start_time' in v.coords or 'time' in v.coords:
+            return v
+        return v.assign_coords(start_time=st, time=tt)
+
+    return {k: stamp(v) if isinstance(v, DataArray) else v for k, v in data.items()}

@@ -127,6 +127,16 @@ def _as_i32(a, what: str, unknown_id: int | None = None) -> np.ndarray:
     return out
 
 
+@dataclass
+class DeviceMessages:
+    """A batch's message descriptors (device pointers and lengths) and the
+    tensors they point into (kept alive while staged)."""
+
+    messages: list
+    arr: object
+    n: int
+
+
 class BinningEngine:
     """Device-resident event binning for one view (see include/lde.h)."""
 
@@ -331,14 +341,20 @@ class BinningEngine:
     def stage_tensors_batch(self, messages) -> None:
         """Stage a batch of ``(pid, toa)`` int32 device tensors in one call
         (``pid`` may be None for a monitor)."""
-        n = len(messages)
-        if n == 0:
+        if len(messages) == 0:
             return
+        self.stage_device_messages(self.device_messages(messages))
+
+    def device_messages(self, messages) -> 'DeviceMessages':
+        """The descriptor table of a batch of ``(pid, toa)`` int32 device
+        tensors (checked here), for :meth:`stage_device_messages`: a service
+        builds it as the messages arrive, the engine stages it in one call."""
+        import torch
+
+        n = len(messages)
         # host time here is GPU idle time between batches: one pass over the
         # messages filling a ctypes array (pid pointers | toa pointers |
         # lengths), identity dtype test first (torch attribute calls dominate)
-        import torch
-
         i32 = torch.int32
         arr = (ctypes.c_int64 * (3 * n))()
         for i, (pid, toa) in enumerate(messages):
@@ -353,13 +369,21 @@ class BinningEngine:
                 arr[i] = pid.data_ptr()
             arr[n + i] = toa.data_ptr()
             arr[2 * n + i] = nn
-        if _current_raw_stream(messages[0][1].device.index) != self._stream_ptr:
-            self._order_after_producer([t for m in messages for t in m if t is not None])
-        base = ctypes.addressof(arr)
+        return DeviceMessages(messages, arr, n)
+
+    def stage_device_messages(self, table: 'DeviceMessages') -> None:
+        """Stage a :meth:`device_messages` table (``lde_stage_device_batch``)."""
+        n = table.n
+        if n == 0:
+            return
+        msgs = table.messages
+        if _current_raw_stream(msgs[0][1].device.index) != self._stream_ptr:
+            self._order_after_producer([t for m in msgs for t in m if t is not None])
+        base = ctypes.addressof(table.arr)
         rc = self._lib.lde_stage_device_batch(self._h, n, base, base + 8 * n, base + 16 * n)
         if rc:
             check(rc, self._h, self._lib)
-        self._keepalive.append(messages)
+        self._keepalive.append(msgs)
 
     def accumulate(self, replica: int = 0) -> None:
         rc = self._lib.lde_accumulate(self._h, int(replica))

@@ -46,6 +46,13 @@ class Timestamp:
     def to_ns(self) -> int:
         return self._ns
 
+    def to_scipp(self):
+        """A 0-D int64 scalar with unit 'ns' (SRC/core/timestamp.py:216-220):
+        a scipp scalar when scipp is importable, else the stand-in variable."""
+        from .dataarray import scalar
+
+        return scalar(np.int64(self._ns), unit='ns')
+
     def __eq__(self, other) -> bool:
         return isinstance(other, Timestamp) and other._ns == self._ns
 

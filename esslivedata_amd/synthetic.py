@@ -9,7 +9,9 @@ follow the reference's instrument configs and fakes:
   (tests/helpers/livedata_app.py:189) or ``normal(30e6, 1e7)``
   (services/fake_detectors.py:98-99, 142-145).
 * LOKI bank 0: pids 1..802816 (loki/streams.py:18), xy_plane 144 x 144
-  (loki/factories.py:101-121); TOA ``uniform(0, 71e6)``.
+  (loki/factories.py:101-121); TOA ``uniform(0, 71e6)``.  Banks 1-8
+  (``loki_bank``): the window-frame panels with their pid ranges and
+  resolutions (loki/streams.py:17-27, loki/factories.py:101-112).
 * DREAM mantle: pids 229377..720896 (dream/streams.py:19), cylinder_mantle_z
   80 x 320 (dream/factories.py:59-66), sigma 4 mm noise, 4 noisy replicas + the
   original; Zipf(1.2) pixel skew over a random permutation; TOA 80 % normal(30 ms,
@@ -86,6 +88,73 @@ def dream_wavelength_table(distance_min: float = 77.5, distance_max: float = 78.
 
     n_d = int(round((distance_max - distance_min) / 0.05)) + 1
     return ideal_lookup_table(distance_min, distance_max, n_d, 71.5e6, 287)
+
+
+# LOKI's nine detector banks: pixel-id ranges (config/instruments/loki/streams.py:
+# 17-27) and xy_plane resolutions (loki/factories.py:101-112)
+LOKI_BANKS: dict[str, tuple[int, int]] = {
+    'loki_detector_0': (1, 802816),
+    'loki_detector_1': (802817, 1032192),
+    'loki_detector_2': (1032193, 1204224),
+    'loki_detector_3': (1204225, 1433600),
+    'loki_detector_4': (1433601, 1605632),
+    'loki_detector_5': (1605633, 2007040),
+    'loki_detector_6': (2007041, 2465792),
+    'loki_detector_7': (2465793, 2752512),
+    'loki_detector_8': (2752513, 3211264),
+}
+LOKI_RESOLUTIONS: dict[str, dict[str, int]] = {
+    'loki_detector_0': {'y': 144, 'x': 144},
+    **{f'loki_detector_{b}': ({'y': 36, 'x': 108} if b % 2 else {'y': 108, 'x': 36})
+       for b in range(1, 9)},
+}
+
+
+def loki_bank(bank: int, n_replicas: int = 5, seed: int = 42) -> Instrument:
+    """LOKI bank ``bank``: bank 0 is :func:`loki_bank0`; banks 1-8 are the two
+    window frames (z = 3.5 m and 1.5 m) of 448-pixel-wide panels, the odd banks above / below the beam (wide, 36 x
+    108 screens), the even ones left / right of it (tall, 108 x 36).  Projected
+    with the restated ``xy_plane`` and cylindrical-pixel noise replicas
+    (loki/factories.py:101-121: straw pixels along x, flip_x)."""
+    from .geometry import GeometricSource, PixelNoise
+
+    if bank == 0:
+        return loki_bank0(n_replicas, seed)
+    name = f'loki_detector_{bank}'
+    first, last = LOKI_BANKS[name]
+    p = last - first + 1
+    n_long = p // 448
+    frame = (bank - 1) // 4          # 0: first window frame, 1: second
+    side = (bank - 1) % 4            # above, left, below, right of the beam
+    z = 3.5 if frame == 0 else 1.5
+    off = 0.7 if frame == 0 else 0.9
+    if bank % 2:                     # wide: straws along x
+        nx, ny = n_long, 448
+        x0, y0 = 0.0, off if side == 0 else -off
+    else:                            # tall
+        nx, ny = 448, n_long
+        x0, y0 = -off if side == 1 else off, 0.0
+    w = 0.6
+    xs = x0 + np.linspace(-w / 2, w / 2, nx)
+    ys = y0 + np.linspace(-w / 2, w / 2, ny) * (ny / max(nx, ny))
+    xx, yy = np.meshgrid(xs, ys, indexing='xy')
+    pos = np.stack([xx.ravel(), yy.ravel(), np.full(p, z)], -1)
+    dn = np.arange(first, last + 1, dtype=np.int32)
+    res = dict(LOKI_RESOLUTIONS[name])
+    dx = w / max(nx - 1, 1)
+    noise = (PixelNoise(cylinder_axis=(dx, 0.0, 0.0), cylinder_radius=dx / 2,
+                        replicas=n_replicas - 1, seed=seed + bank) if n_replicas > 1 else None)
+    src = GeometricSource(dn, pos, projection_type='xy_plane', resolution=res, pixel_noise=noise)
+    return Instrument(
+        name=name,
+        detector_number=dn,
+        coords=src.coords(),
+        resolution=res,
+        edges=TOAEdges(),
+        positions=pos,
+        projection_type='xy_plane',
+        pixel_noise=noise,
+    )
 
 
 def loki_bank0(n_replicas: int = 5, seed: int = 42) -> Instrument:

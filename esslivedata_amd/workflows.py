@@ -27,7 +27,7 @@ from typing import TYPE_CHECKING, Any, Callable, Iterable, Mapping, Sequence
 
 import numpy as np
 
-from .dataarray import DataArray, Variable
+from .dataarray import DataArray, Variable, publish
 from .edges import TOAEdges, WavelengthEdges, convert_time, convert_wavelength, label_slice
 from .engine import BinningEngine
 from .preprocessors import DetectorEvents, MonitorEvents, StagedEvents, Timestamp
@@ -125,6 +125,21 @@ class SpectrumViewConfig:
     transform: Callable[[np.ndarray], np.ndarray] | None
     output_dims: tuple[str, ...]
     reduction_axes: Sequence[int] = ()
+
+
+def _stamp_window(out: dict, names: Sequence[str], start: Timestamp | None,
+                  end: Timestamp | None) -> None:
+    """Window outputs get 0-D ``start_time`` (first accumulate since the last
+    finalize) and ``time`` (last end) coords: int64 scalars with unit 'ns', as
+    ``Timestamp.to_scipp()`` makes them (SRC/workflows/stream_processor_workflow.py:
+    229-238, SRC/core/timestamp.py:216-220); cumulative outputs stay unstamped
+    (``Job._add_time_coords`` stamps them, SRC/core/job.py:212-262)."""
+    if start is None:
+        return
+    st, tt = start.to_scipp(), end.to_scipp()
+    for name in names:
+        if name in out:
+            out[name] = out[name].assign_coords(start_time=st, time=tt)
 
 
 def _histogram_slice(edges, toa_range) -> tuple[int, int] | None:
@@ -407,7 +422,8 @@ class GpuDetectorViewWorkflow:
         if self._params.pixel_weighting and self._view.pixel_weights is not None:
             with np.errstate(divide='ignore', invalid='ignore'):
                 img = img / self._view.pixel_weights
-        coords = {d: Variable((d,), c) for d, c in self._view.screen_coords.items()}
+        units = self._view.screen_units
+        coords = {d: Variable((d,), c, units.get(d)) for d, c in self._view.screen_coords.items()}
         return DataArray(img, self._view.screen_dims, 'counts', coords)
 
     def finalize(self) -> dict[str, Any]:
@@ -448,15 +464,10 @@ class GpuDetectorViewWorkflow:
         if self._roi_support:
             out['roi_rectangle'] = self._roi_readback('roi_rectangle')
             out['roi_polygon'] = self._roi_readback('roi_polygon')
-        if self._start is not None:
-            st = Variable((), np.datetime64(self._start.to_ns(), 'ns'), 'ns')
-            tt = Variable((), np.datetime64(self._end.to_ns(), 'ns'), 'ns')
-            names = DETECTOR_WINDOW_OUTPUTS + (ROI_WINDOW_OUTPUTS if self._roi_support else ())
-            for name in names:
-                if name in out:
-                    out[name] = out[name].assign_coords(start_time=st, time=tt)
+        names = DETECTOR_WINDOW_OUTPUTS + (ROI_WINDOW_OUTPUTS if self._roi_support else ())
+        _stamp_window(out, names, self._start, self._end)
         self._start = self._end = None
-        return out
+        return publish(out)
 
     @property
     def source_name(self) -> str:
@@ -740,13 +751,9 @@ class GpuMonitorWorkflow:
     def finalize(self) -> dict[str, Any]:
         if self._hist_mode:
             out = self._finalize_histogram_mode()
-            if self._start is not None:
-                st = Variable((), np.datetime64(self._start.to_ns(), 'ns'), 'ns')
-                tt = Variable((), np.datetime64(self._end.to_ns(), 'ns'), 'ns')
-                for name in MONITOR_WINDOW_OUTPUTS:
-                    out[name] = out[name].assign_coords(start_time=st, time=tt)
+            _stamp_window(out, MONITOR_WINDOW_OUTPUTS, self._start, self._end)
             self._start = self._end = None
-            return out
+            return publish(out)
         res = self._engine.finalize(images=False, hists=True)
         out = {
             'cumulative': self._hist(res.cumulative_hist),
@@ -758,13 +765,9 @@ class GpuMonitorWorkflow:
                 np.asarray(float(res.cumulative_in_range)), (), 'counts'
             ),
         }
-        if self._start is not None:
-            st = Variable((), np.datetime64(self._start.to_ns(), 'ns'), 'ns')
-            tt = Variable((), np.datetime64(self._end.to_ns(), 'ns'), 'ns')
-            for name in MONITOR_WINDOW_OUTPUTS:
-                out[name] = out[name].assign_coords(start_time=st, time=tt)
+        _stamp_window(out, MONITOR_WINDOW_OUTPUTS, self._start, self._end)
         self._start = self._end = None
-        return out
+        return publish(out)
 
     def clear(self) -> None:
         self._engine.clear()

@@ -229,6 +229,43 @@ def reference_kats_r2() -> list[dict]:
     ]
 
 
+def reference_kats_r5() -> list[dict]:
+    """Window time coords (round 5): integer ns scalars as Timestamp.to_scipp()
+    makes them (SRC/core/timestamp.py:216-220)."""
+    return [
+        {
+            'name': 'window_outputs_time_coords',
+            'source': 'tests/workflows/detector_view/integration_test.py:28-84',
+            'note': '4x4 logical view (fold detector_number 1..16 to y, x), 10 events per '
+                    'pixel, ROI rectangle x [0, 2), y [0, 2) (index bounds, unit None)',
+            'detector_number': list(range(1, 17)),
+            'fold_sizes': {'y': 4, 'x': 4},
+            'events': _fake_nexus_events(4, 4, 10),
+            'roi_rectangle': {'x': [0, 2], 'y': [0, 2]},
+            'start_time_ns': 1000,
+            'end_time_ns': 2000,
+            'expected': {'start_time': 1000, 'time': 2000, 'unit': 'ns', 'dtype': 'int64'},
+            'stamped': ['current', 'counts_total', 'counts_in_toa_range', 'roi_spectra_current'],
+            'unstamped': ['cumulative', 'roi_spectra_cumulative', 'counts_total_cumulative',
+                          'counts_in_toa_range_cumulative'],
+        },
+        {
+            'name': 'window_time_tracking',
+            'source': 'tests/workflows/stream_processor_workflow_test.py:407-516',
+            'note': 'each period: accumulate calls [start, end] ns, then finalize (or clear); '
+                    'expected (start_time, time) of the window output, null after clear',
+            'periods': [
+                {'accumulate': [[1000, 2000]], 'then': 'finalize', 'expected': [1000, 2000]},
+                {'accumulate': [[1000, 2000], [3000, 4000]], 'then': 'finalize',
+                 'expected': [1000, 4000]},
+                {'accumulate': [[5000, 6000]], 'then': 'finalize', 'expected': [5000, 6000]},
+                {'accumulate': [[7000, 8000]], 'then': 'clear', 'expected': None},
+                {'accumulate': [[9000, 10000]], 'then': 'finalize', 'expected': [9000, 10000]},
+            ],
+        },
+    ]
+
+
 # hand-derived: toa -> expected bin (-1 = dropped)
 TIE_KATS = [
     {
@@ -281,8 +318,13 @@ SCREEN_EDGE_KATS = [
 
 
 def main() -> None:
-    (HERE / 'reference_kats.json').write_text(
-        json.dumps(REFERENCE_KATS + reference_kats_r2(), indent=1))
+    # entries transcribed by hand into the JSON (the round-3 logical-view KATs)
+    # are kept; the generated ones are replaced in place or appended
+    path = HERE / 'reference_kats.json'
+    gen = {k['name']: k for k in REFERENCE_KATS + reference_kats_r2() + reference_kats_r5()}
+    old = json.loads(path.read_text()) if path.exists() else []
+    out = [gen.pop(k['name'], k) for k in old] + list(gen.values())
+    path.write_text(json.dumps(out, indent=1))
     (HERE / 'tie_kats.json').write_text(
         json.dumps({'toa': TIE_KATS, 'screen': SCREEN_EDGE_KATS}, indent=1)
     )

@@ -167,3 +167,67 @@ def test_bench_gpus2_launches_ranks_and_checks_merge(workload):
     assert d['check']['ranks'] == 2
     assert d['check']['bit_exact_vs_oracle'] is True, d['check']
     assert d['check']['current_total'] == d['check']['oracle_total'] > 0
+    if workload == 'dream':  # the bank-sharded LOKI leg rides along (8(e) axis 2)
+        _check_bank_leg(d['bank_sharding'], 2)
+
+
+def _run_bench(args, env_extra=None, timeout=380):
+    env = dict(os.environ)
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, str(ROOT / 'bench.py'), *args], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def _check_bank_leg(leg: dict, world: int):
+    """The bank-sharded LOKI leg: every bank on exactly one rank, whole-node
+    events over the max-over-ranks time, bit-exact on every rank's banks."""
+    placed = [b for banks in leg['banks_per_rank'].values() for b in banks]
+    assert sorted(placed) == sorted(f'loki_detector_{b}' for b in range(9))
+    assert len(leg['banks_per_rank']) == world
+    assert leg['value'] == pytest.approx(leg['events_per_step'] / (leg['ms_per_step'] / 1e3), rel=1e-9)
+    assert leg['bit_exact_vs_oracle'] is True
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize('cadence', ['batch', 'pulse'])
+def test_bench_bifrost_cadence_exact(cadence):
+    """BIFROST at the reference cadence (one push of the batch's 14 x 45 bank
+    messages, one finalize; core/job.py:413-433) and per pulse: bit-exact
+    against the oracle's float32 per-push sums."""
+    d = _run_bench(['--workload', 'bifrost', '--bifrost-cadence', cadence, '--steps', '3',
+                    '--warmup', '1', '--e2e-steps', '0'])
+    _check_line(d)
+    cfg = d['config']
+    assert cfg['bifrost_cadence'] == cadence and cfg['messages_per_push'] * cfg['pushes_per_step'] == 630
+    assert cfg['pushes_per_step'] == (1 if cadence == 'batch' else 14)
+    assert d['check']['bit_exact_vs_oracle'] is True
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_bifrost_gpus2_merges_per_push():
+    """``--workload bifrost --gpus 2``: the float32 view merges
+    per push (PushReducer), no OutputReducer is built."""
+    d = _run_bench(['--gpus', '2', '--workload', 'bifrost', '--steps', '2', '--warmup', '1',
+                    '--no-cpu-baseline', '--e2e-steps', '0'], {'LDE_BENCH_BACKEND': 'gloo'})
+    _check_line(d, n_gpus=2)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_shard_banks_gpus2():
+    """``--shard banks --gpus 2``: LOKI's nine banks placed by assign_banks on
+    two ranks (sharing cuda:0 over gloo), no collective on the data path,
+    every rank's banks bit-exact."""
+    d = _run_bench(['--gpus', '2', '--shard', 'banks', '--steps', '2', '--warmup', '1', '--pulses', '2',
+                    '--events-per-pulse', '1000000'], {'LDE_BENCH_BACKEND': 'gloo'})
+    assert d['n_gpus'] == 2 and 'bank sharding x2' in d['config']['parallelism']
+    _check_bank_leg(d['bank_sharding'], 2)
+    assert d['value'] == d['bank_sharding']['value']

@@ -244,3 +244,95 @@ def test_finalize_outputs_round_trip_through_da00():
         assert set(back.coords) == set(da.coords)
         for k, v in da.coords.items():
             np.testing.assert_array_equal(back.coords[k].values, v.values)
+
+
+def _assert_window_coords(da, start, end, key=''):
+    st, tt = da.coords['start_time'], da.coords['time']
+    assert st.value == start and tt.value == end, key
+    assert st.unit == 'ns' and tt.unit == 'ns', key
+    # int64 scalars, as Timestamp.to_scipp() makes them (core/timestamp.py:216-220)
+    assert np.asarray(st.values).dtype == np.int64 and np.asarray(tt.values).dtype == np.int64, key
+
+
+def test_window_outputs_time_coords_kat():
+    """integration_test.py:28-84 through GpuDetectorViewFactory: window outputs
+    carry start_time = 1000 / time = 2000 (int64, 'ns'); cumulative outputs none."""
+    from esslivedata_amd import roi
+    from esslivedata_amd.workflows import GpuDetectorViewFactory, LogicalViewConfig
+
+    kat = REF['window_outputs_time_coords']
+    sizes = kat['fold_sizes']
+    cfg = LogicalViewConfig(transform=lambda da, _s: da.fold(dim='detector_number', sizes=sizes))
+    fac = GpuDetectorViewFactory(detector_numbers={'detector': np.array(kat['detector_number'])},
+                                 view_config=cfg)
+    aux = {'roi_rectangle': 'roi_rectangle', 'roi_polygon': 'roi_polygon'}
+    wf = fac.make_workflow('detector', None, aux)
+    wf.build()
+    r = kat['roi_rectangle']
+    req = roi.to_concatenated({0: roi.RectangleROI(x=roi.Interval(*r['x']), y=roi.Interval(*r['y']))},
+                              'rectangle')
+    wf.accumulate({'detector': _events(kat), 'roi_rectangle': req},
+                  start_time=_t(kat['start_time_ns']), end_time=_t(kat['end_time_ns']))
+    out = wf.finalize()
+    exp = kat['expected']
+    for key in kat['stamped']:
+        _assert_window_coords(out[key], exp['start_time'], exp['time'], key)
+    for key in kat['unstamped']:
+        assert 'start_time' not in out[key].coords and 'time' not in out[key].coords, key
+    assert out['roi_spectra_current'].values.sum() > 0  # the ROI output is not empty
+    assert float(out['counts_total'].values) == 160
+
+
+def _run_time_tracking(wf, feed):
+    kat = REF['window_time_tracking']
+    for period in kat['periods']:
+        for s, e in period['accumulate']:
+            feed(wf, _t(s), _t(e))
+        if period['then'] == 'clear':
+            wf.clear()
+            continue
+        out = wf.finalize()
+        _assert_window_coords(out['current'], *period['expected'])
+        _assert_window_coords(out['counts_total'], *period['expected'])
+        assert 'start_time' not in out['cumulative'].coords
+
+
+def test_window_time_tracking_kat_detector():
+    """stream_processor_workflow_test.py:407-516: start_time of the first
+    accumulate, time of the last; both reset by finalize and by clear."""
+    from esslivedata_amd.workflows import GpuDetectorViewFactory, LogicalViewConfig
+
+    fac = GpuDetectorViewFactory(detector_numbers={'det': np.arange(1, 17)},
+                                 view_config=LogicalViewConfig())
+    wf = fac.make_workflow('det', None, {})
+    pid = np.arange(1, 17, dtype=np.int32)
+    toa = np.full(16, 1_000_000, dtype=np.int32)
+    _run_time_tracking(wf, lambda w, s, e: w.accumulate({'det': (pid, toa)}, start_time=s, end_time=e))
+
+
+def test_window_time_tracking_kat_monitor():
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.workflows import GpuMonitorWorkflow
+
+    wf = GpuMonitorWorkflow('monitor_1', TOAEdges())
+    toa = np.arange(0, 70_000_000, 1_000_000, dtype=np.int32)
+    _run_time_tracking(wf, lambda w, s, e: w.accumulate({'monitor_1': (None, toa)}, start_time=s,
+                                                        end_time=e))
+
+
+def test_window_time_coords_survive_da00():
+    """The int64 'ns' window coords travel through da00 as int64 with unit 'ns'
+    (scipp_da00_compat.py:22-44 on an int64 scalar) and decode unchanged."""
+    from esslivedata_amd import da00
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.workflows import GpuMonitorWorkflow
+
+    wf = GpuMonitorWorkflow('monitor_1', TOAEdges())
+    wf.accumulate({'monitor_1': (None, np.arange(100, dtype=np.int32))}, start_time=_t(1000),
+                  end_time=_t(2000))
+    cur = wf.finalize()['current']
+    variables = da00.dataarray_to_da00(cur)
+    by = {v.name: v for v in variables}
+    assert by['time'].unit == 'ns' and by['time'].data.dtype == np.int64
+    back = da00.da00_to_dataarray(da00.deserialise_da00(da00.serialise_da00('m', 0, variables))[2])
+    _assert_window_coords(back, 1000, 2000)

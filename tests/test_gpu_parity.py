@@ -285,8 +285,80 @@ def test_bifrost_float32_accumulation():
             np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
 
 
+@pytest.mark.parametrize('pushes', [1, 2, 5])
+def test_bifrost_float32_fused_finalize_cadences(pushes):
+    """float32 views keep a push's counts in the batch until the next
+    accumulate or the finalize, which fuses its f32 adds (k_finalize_f32);
+    one push per finalize is the reference cadence (core/job.py:413-433).
+    Histogram reads, ROI-like group spectra and a clear between pushes merge
+    the pending push first; every output equals the oracle's per-push float32
+    sums, images over a TOA range included."""
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.bifrost_unified()
+    view = projection.logical_lut(inst.detector_number, transform=synthetic.bifrost_transform)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, 'auto', out_dtype='float32', toa_range=(10, 90))
+    ps = ora.logical_screen_index((5, 3, 9, 100), synthetic.bifrost_transform)[0][None, :]
+    o = ora.OracleDetectorView(detector_number=inst.detector_number, pixel_screen=ps,
+                               screen_shape=(15, 900), toa_edges_ns=edges, dtype=np.float32,
+                               toa_slice=(10, 90))
+    groups = [np.arange(0, 900), np.arange(450, 2000)]
+    eng.set_groups(0, groups)
+    for k in range(4 * pushes):
+        pid, toa = synthetic.fake_detector_events(30_000 + 977 * k, 1, 13500, seed=300 + k)
+        if k == 2 * pushes:  # a clear drops the window's pending push too
+            eng.clear()
+            o.clear()
+        eng.stage(pid, toa)
+        eng.accumulate(0)
+        o.accumulate(pid, toa)
+        if k % 3 == 1:  # reads between pushes see every push so far
+            win = o._acc.window
+            np.testing.assert_array_equal(eng.read_histogram('current'), win)
+            np.testing.assert_array_equal(eng.read_histogram('cumulative'), o._acc.cumulative)
+            sp = eng.group_spectra(0, 'current')
+            np.testing.assert_array_equal(sp, np.stack([win[g].sum(0) for g in groups]))
+        if k % pushes == pushes - 1:
+            res = eng.finalize(images=True, hists=True)
+            exp = o.finalize()
+            assert res.current_hist.dtype == np.float32 and res.current_image.dtype == np.float32
+            np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
+            np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
+            np.testing.assert_array_equal(res.current_image, exp['current'].ravel())
+            np.testing.assert_array_equal(res.cumulative_image, exp['cumulative'].ravel())
+            assert res.current_total == exp['counts_total']
+            assert res.cumulative_in_range == exp['counts_in_toa_range_cumulative']
+
+
+def test_atomic_many_large_messages_proportional_blocks():
+    """More messages than fit the kernel arguments, large enough that their
+    block ranges are shares of 8 blocks per CU (k_bin_atomic_blocks)."""
+    import torch
+
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.bifrost_unified()
+    view = projection.logical_lut(inst.detector_number, transform=synthetic.bifrost_transform)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, 'atomic')
+    ps = ora.logical_screen_index((5, 3, 9, 100), synthetic.bifrost_transform)[0][None, :]
+    o = ora.OracleDetectorView(detector_number=inst.detector_number, pixel_screen=ps,
+                               screen_shape=(15, 900), toa_edges_ns=edges)
+    pid, toa = synthetic.fake_detector_events(100 * 40_000, 1, 13500, seed=5)
+    dp, dt = torch.as_tensor(pid, device='cuda'), torch.as_tensor(toa, device='cuda')
+    sizes = np.random.default_rng(1).integers(1, 80_000, 100)
+    bounds = np.minimum(np.concatenate([[0], np.cumsum(sizes)]), len(pid))
+    eng.stage_tensors_batch([(dp[a:b], dt[a:b]) for a, b in zip(bounds[:-1], bounds[1:]) if b > a])
+    eng.accumulate(0)
+    n = int(bounds[-1])
+    o.accumulate(pid[:n], toa[:n])
+    res = eng.finalize(hists=True)
+    np.testing.assert_array_equal(res.current_hist, o.finalize()['histogram_current'])
+
+
 @pytest.mark.parametrize('segs', [None, '24'])
-@pytest.mark.parametrize('n_msgs', [1, 24, 45, 64, 65, 130])
+@pytest.mark.parametrize('n_msgs', [1, 24, 45, 64, 65, 130, 630])
 def test_atomic_many_messages(n_msgs, segs, request):
     """ATOMIC with many small messages per accumulate (BIFROST: 45 bank
     messages of 1,000 events per pulse): up to 64 descriptors per launch

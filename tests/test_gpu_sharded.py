@@ -141,6 +141,11 @@ def _sharded_worker(rank, world, port, q, merge):
                     why.append('no counts')
                 if roi_on and not out['roi_spectra_current'].values.sum() > 0:
                     why.append('empty ROI spectra')
+                # the root stamps the window like one workflow: int64 ns scalars
+                st, tt = out['current'].coords['start_time'], out['current'].coords['time']
+                if (st.value, tt.value, tt.unit, np.asarray(st.values).dtype) != (b, b + 1, 'ns', np.int64) \
+                        or 'time' in out['cumulative'].coords:
+                    why.append(f'window time coords {st}, {tt}')
                 # the move (batch 2) and the clear (batch 3) restart the
                 # cumulative: it equals the current image there
                 same_cc = bool(np.array_equal(out['cumulative'].values, out['current'].values))
