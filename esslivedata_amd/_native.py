@@ -48,8 +48,6 @@ COUNTERS = {
     'waits': 3,
     'waits_blocked': 4,
     'wait_pred_us': 5,
-    'sieve_pair': 6,
-    'sieve_pair_wraps': 7,
 }
 
 KERNELS = {

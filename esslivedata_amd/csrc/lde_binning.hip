@@ -34,21 +34,6 @@
 
 namespace lde {
 
-// Kernel-argument message lists: this block's place in message si when the
-// message starts at block `rot`, and the next message's start (after the
-// blocks this one fills with one group of four events per thread; a message
-// that fills the whole grid leaves it where it was).
-__device__ __forceinline__ int seg_block(int rot) {
-    const int b = (int)blockIdx.x - rot;  // no division: 0 <= rot < gridDim.x
-    return b < 0 ? b + (int)gridDim.x : b;
-}
-__device__ __forceinline__ int next_rot(int rot, long long n) {
-    const long long n4 = n >> 2;
-    if (n4 >= (long long)gridDim.x * blockDim.x) return rot;  // large ones fill the grid
-    const int r = rot + (int)(((unsigned)n4 + blockDim.x - 1u) / blockDim.x);
-    return r >= (int)gridDim.x ? r - (int)gridDim.x : r;
-}
-
 // ---------------------------------------------------------------------------
 // ATOMIC strategy: one pass, global u32 atomics (agent scope)
 // ---------------------------------------------------------------------------
@@ -136,7 +121,7 @@ __global__ __launch_bounds__(256) void k_bin_atomic_blocks(const SegDesc *__rest
 //   starts[c*(NT+1) + t].  The next chunk's events are prefetched into
 //   registers while the current chunk runs its LDS phases.
 // ---------------------------------------------------------------------------
-template <int TILE_BITS, typename LT, bool FAST, bool PEEL>
+template <int TILE_BITS, typename LT, bool FAST>
 __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_partition(
     const SegDesc *__restrict__ segs, int n_segs, long long c_begin, long long n_chunks,
     const LT *__restrict__ lut, int pid_off, unsigned L, const unsigned char *__restrict__ g_tab,
@@ -184,27 +169,15 @@ __global__ __launch_bounds__(kPartThreads, kPartMinWavesPerEU) void k_partition(
         }
         // the next chunk's events load while this chunk runs its LDS phases
         if (c + gridDim.x < n_chunks) load_chunk(s_seg, n_segs, c + gridDim.x, pid_off, nxt);
-        // ---- rank inside tile: LDS returning atomics; with PEEL the most
-        // common tile of the wave (sampled lane) is ranked with one atomic
+        // ---- rank inside tile: LDS returning atomics
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
             const int tile = key[e] >= 0 ? (key[e] >> TILE_BITS) : -1;
             rank[e] = 0;
             if (LDE_DIAG(tp.pad) & 4) {
                 rank[e] = (uint32_t)(e * 64 + lane) & 255u;
-            } else if (PEEL) {
-                const int lead = __builtin_amdgcn_readlane(tile, (e * 5) & 63);
-                const unsigned long long m = __ballot(tile == lead);
-                if (lead >= 0) {
-                    const int first = __builtin_ctzll(m);
-                    uint32_t base = 0;
-                    if (lane == first) base = atomicAdd(&s_cnt[lead], (uint32_t)__popcll(m));
-                    base = __builtin_amdgcn_readlane(base, first);
-                    if (tile == lead) rank[e] = base + lanes_below(m);
-                }
-                if (tile >= 0 && tile != lead) rank[e] = atomicAdd(&s_cnt[tile], 1u);
-            } else {
-                if (tile >= 0) rank[e] = atomicAdd(&s_cnt[tile], 1u);
+            } else if (tile >= 0) {
+                rank[e] = atomicAdd(&s_cnt[tile], 1u);
             }
         }
         __syncthreads();
@@ -414,11 +387,10 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_accumulate(
 // ---------------------------------------------------------------------------
 // PF: the next iteration's U groups are loaded before this one's are binned
 // (twice the bytes in flight per lane)
-template <bool FAST, bool COLUMNS, bool PF>
+template <bool FAST, bool COLUMNS>
 __global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
                                                  const unsigned char *__restrict__ g_tab,
-                                                 ToaParams tp, uint32_t *__restrict__ hist,
-                                                 int block_ranges) {
+                                                 ToaParams tp, uint32_t *__restrict__ hist) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *s_h = reinterpret_cast<uint32_t *>(smem);
     const int HB = COLUMNS ? tp.T * 32 : tp.T;
@@ -428,7 +400,6 @@ __global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
     __syncthreads();
     const int col = threadIdx.x & 31;
     const uint32_t dummy = (uint32_t)HB + (threadIdx.x & 63u);  // dropped events count here
-    const long long stride = (long long)gridDim.x * blockDim.x;
     // branch-free: every event adds 1 to its bin's counter or to the lane's
     // dummy word, so no lane waits inside a branch around its LDS atomic
     auto add = [&](int t, bool valid) __attribute__((always_inline)) {
@@ -438,77 +409,40 @@ __global__ __launch_bounds__(256) void k_monitor(const SegKarg segs, int n_segs,
     };
     // up to kKargSegs messages per launch, their descriptors passed as kernel
     // arguments (no descriptor upload in front); per lane U groups of four
-    // events in flight (indices clamped, so the loads are unconditional)
-    constexpr int U = 4;
-    int rot = 0;  // LDE_MON_RANGES=0: small messages side by side, rotated
-    // block ranges (host: every message at least a block; chunk0 = its first
+    // events in flight (indices clamped, so the loads are unconditional).
+    // Block ranges (host: every message at least a block; chunk0 = its first
     // block): each block streams one message with that message's own stride,
     // so no lane sweeps a message's partial last stride and moves on
-    int s_lo = 0, s_hi = n_segs;
-    long long stride_b = stride, i0_b = 0;
-    if (block_ranges) {
-        int si = 0;
-        for (int j = 1; j < n_segs; ++j)
-            if ((long long)blockIdx.x >= segs.s[j].chunk0) si = j;
-        const long long b0 = segs.s[si].chunk0;
-        const long long b1 = si + 1 < n_segs ? segs.s[si + 1].chunk0 : (long long)gridDim.x;
-        s_lo = si;
-        s_hi = si + 1;
-        stride_b = (b1 - b0) * blockDim.x;
-        i0_b = ((long long)blockIdx.x - b0) * blockDim.x + threadIdx.x;
-    }
-    for (int si = s_lo; si < s_hi; ++si) {
-        const SegDesc seg = segs.s[si];
-        const long long n = seg.n;
-        const long long stride = stride_b;
-        const long long i0 = block_ranges ? i0_b : (long long)seg_block(rot) * blockDim.x + threadIdx.x;
-        if (!block_ranges) rot = next_rot(rot, n);
-        long long tail = 0;
-        if (((uintptr_t)seg.toa & 15u) == 0 && n >= 4) {
-            const long long n4 = n >> 2;
-            if (PF) {
-                v4i t[U];
+    constexpr int U = 4;
+    int si = 0;
+    for (int j = 1; j < n_segs; ++j)
+        if ((long long)blockIdx.x >= segs.s[j].chunk0) si = j;
+    const long long b0 = segs.s[si].chunk0;
+    const long long b1 = si + 1 < n_segs ? segs.s[si + 1].chunk0 : (long long)gridDim.x;
+    const SegDesc seg = segs.s[si];
+    const long long n = seg.n;
+    const long long stride = (b1 - b0) * blockDim.x;
+    const long long i0 = ((long long)blockIdx.x - b0) * blockDim.x + threadIdx.x;
+    long long tail = 0;
+    if (((uintptr_t)seg.toa & 15u) == 0 && n >= 4) {
+        const long long n4 = n >> 2;
+        for (long long i = i0; i < n4; i += stride * U) {
+            v4i t[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const long long k = i0 + u * stride;
-                    t[u] = ld_stream4(seg.toa + 4 * (k < n4 ? k : n4 - 1));
-                }
-                for (long long i = i0; i < n4; i += stride * U) {
-                    v4i tn[U];  // the next iteration's groups (clamped: always valid addresses)
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const long long k = i + (U + u) * stride;
-                        tn[u] = ld_stream4(seg.toa + 4 * (k < n4 ? k : n4 - 1));
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const bool ok = i + u * stride < n4;
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) add(t[u][q], ok);
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) t[u] = tn[u];
-                }
-            } else {
-                for (long long i = i0; i < n4; i += stride * U) {
-                    v4i t[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const long long k = i + u * stride;
-                        t[u] = ld_stream4(seg.toa + 4 * (k < n4 ? k : n4 - 1));
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const bool ok = i + u * stride < n4;
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) add(t[u][q], ok);
-                    }
-                }
+            for (int u = 0; u < U; ++u) {
+                const long long k = i + u * stride;
+                t[u] = ld_stream4(seg.toa + 4 * (k < n4 ? k : n4 - 1));
             }
-            tail = n4 << 2;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool ok = i + u * stride < n4;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) add(t[u][q], ok);
+            }
         }
-        for (long long i = tail + i0; i < n; i += stride) add(ld_global(seg.toa + i), true);
+        tail = n4 << 2;
     }
+    for (long long i = tail + i0; i < n; i += stride) add(ld_global(seg.toa + i), true);
     __syncthreads();
     for (int b = threadIdx.x; b < tp.T; b += blockDim.x) {
         uint32_t v = 0;
@@ -590,12 +524,12 @@ hipError_t launch_bin_atomic(const SegKargAtomic &seg, int n_segs, const void *l
                                        start, stop);
 }
 
-template <int TB, typename LT, bool FAST, bool PEEL>
+template <int TB, typename LT, bool FAST>
 static hipError_t launch_partition_t(const PartitionArgs &a, const LT *lut, hipStream_t st) {
     const size_t sm = partition_smem(a.n_tiles, a.tp);
-    (void)hipFuncSetAttribute((const void *)k_partition<TB, LT, FAST, PEEL>,
+    (void)hipFuncSetAttribute((const void *)k_partition<TB, LT, FAST>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipLaunchKernelGGL((k_partition<TB, LT, FAST, PEEL>), dim3(a.grid), dim3(kPartThreads), sm,
+    hipLaunchKernelGGL((k_partition<TB, LT, FAST>), dim3(a.grid), dim3(kPartThreads), sm,
                        st, a.segs, a.n_segs, a.c_begin, a.n_chunks, lut, a.pid_off, a.L, a.tab,
                        a.tp, a.n_tiles, a.payload, a.starts, a.part);
     return hipGetLastError();
@@ -603,11 +537,8 @@ static hipError_t launch_partition_t(const PartitionArgs &a, const LT *lut, hipS
 
 template <int TB, typename LT>
 static hipError_t launch_partition_tl(const PartitionArgs &a, const LT *lut, hipStream_t st) {
-    if (a.tp.fast)
-        return a.peel ? launch_partition_t<TB, LT, true, true>(a, lut, st)
-                      : launch_partition_t<TB, LT, true, false>(a, lut, st);
-    return a.peel ? launch_partition_t<TB, LT, false, true>(a, lut, st)
-                  : launch_partition_t<TB, LT, false, false>(a, lut, st);
+    return a.tp.fast ? launch_partition_t<TB, LT, true>(a, lut, st)
+                     : launch_partition_t<TB, LT, false>(a, lut, st);
 }
 
 template <int TB>
@@ -618,7 +549,6 @@ static hipError_t launch_partition_tb(const PartitionArgs &a, hipStream_t st) {
 
 hipError_t launch_partition(const PartitionArgs &a, hipStream_t st) {
     switch (a.tile_bits) {
-    case 13: return launch_partition_tb<13>(a, st);
     case 14: return launch_partition_tb<14>(a, st);
     case 15: return launch_partition_tb<15>(a, st);
     default: return hipErrorInvalidValue;
@@ -640,10 +570,6 @@ hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const 
                                   const uint32_t *item_count, const uint32_t *tile_items,
                                   uint32_t *hist, long long n_bins, int grid, hipStream_t st) {
     switch (tile_bits) {
-    case 13:
-        hipLaunchKernelGGL(k_tile_accumulate<13>, dim3(grid), dim3(kTileThreads), 0, st, payload,
-                           starts, n_tiles, n_chunks, items, item_count, tile_items, hist, n_bins);
-        break;
     case 14:
         hipLaunchKernelGGL(k_tile_accumulate<14>, dim3(grid), dim3(kTileThreads), 0, st, payload,
                            starts, n_tiles, n_chunks, items, item_count, tile_items, hist, n_bins);
@@ -660,25 +586,23 @@ hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const 
 
 hipError_t launch_monitor(const SegKarg &segs, int n_segs, const unsigned char *tab,
                           const ToaParams &tp, uint32_t *hist, int grid, hipStream_t st,
-                          hipEvent_t start, hipEvent_t stop, bool pf, bool block_ranges) {
+                          hipEvent_t start, hipEvent_t stop) {
     if (n_segs < 1 || n_segs > kKargSegs) return hipErrorInvalidValue;
     const bool columns = tp.T <= kMonitorColumnsMaxT;
     const size_t hb = align16((size_t)((columns ? tp.T * 32 : tp.T) + 64) * 4);
     const size_t sm = hb + toa_lds_bytes(tp);
-#define LDE_MON2(F, C, P)                                                                      \
-    do {                                                                                       \
-        (void)hipFuncSetAttribute((const void *)k_monitor<F, C, P>,                            \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);        \
-        hipExtLaunchKernelGGL((k_monitor<F, C, P>), dim3(grid), dim3(256), sm, st, start, stop, 0, \
-                              segs, n_segs, tab, tp, hist, block_ranges ? 1 : 0);             \
+#define LDE_MON(F, C)                                                                              \
+    do {                                                                                           \
+        (void)hipFuncSetAttribute((const void *)k_monitor<F, C>,                                   \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);            \
+        hipExtLaunchKernelGGL((k_monitor<F, C>), dim3(grid), dim3(256), sm, st, start, stop, 0, segs, \
+                              n_segs, tab, tp, hist);                                              \
     } while (0)
-#define LDE_MON(F, C) do { if (pf) LDE_MON2(F, C, true); else LDE_MON2(F, C, false); } while (0)
     if (tp.fast && columns) LDE_MON(true, true);
     else if (tp.fast) LDE_MON(true, false);
     else if (columns) LDE_MON(false, true);
     else LDE_MON(false, false);
 #undef LDE_MON
-#undef LDE_MON2
     return hipGetLastError();
 }
 

@@ -70,30 +70,6 @@ __device__ __forceinline__ int coord_bin_fast(double v, const double *e, const u
     return b - ((v < lo) ? 1 : 0) + ((v >= h1) ? 1 : 0) + ((v >= h2) ? 1 : 0);
 }
 
-// Distance cache image: slot j holds the most-sampled pixel q = j (mod C)
-// with a distance (q, else -1) and that distance.  Built after a hot-set
-// selection from the sampled pixel counts; the coordinate pass keeps it in
-// LDS so the frequent pixels need no gather.
-__global__ __launch_bounds__(256) void k_coord_cache(const uint32_t *__restrict__ cnt,
-                                                     const double *__restrict__ pix_d, long long L,
-                                                     int cbits, uint32_t *__restrict__ cq,
-                                                     double *__restrict__ cd) {
-    const long long C = 1LL << cbits;
-    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (j >= C) return;
-    uint32_t best = 0;
-    long long bq = -1;
-    for (long long q = j; q < L; q += C) {
-        const uint32_t c = cnt[q];
-        if (c > best) {
-            best = c;
-            bq = q;
-        }
-    }
-    cq[j] = bq < 0 ? 0xFFFFFFFFu : (uint32_t)bq;
-    cd[j] = bq < 0 ? 0.0 : pix_d[bq];
-}
-
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
@@ -102,30 +78,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t coord_rsrc(const void *p, uint
                                              (int)0x00020000);  // raw buffer, 32-bit format
 }
 
-template <bool TLDS, bool CACHE, bool ELDS>
-__global__ __launch_bounds__(1024) void k_event_coord(CoordArgs a, const int *__restrict__ pid,
-                                                      const int *__restrict__ toa, long long n,
-                                                      int *__restrict__ out) {
+template <bool TLDS, bool ELDS>
+__global__ __launch_bounds__(256) void k_event_coord(CoordArgs a, const int *__restrict__ pid,
+                                                     const int *__restrict__ toa, long long n,
+                                                     int *__restrict__ out) {
     extern __shared__ double sm[];
-    // LDS: distance cache (CACHE: C doubles + C pixel ids) | edges (T + 1,
-    // when they fit) | table (TLDS) | bucket table (u16)
-    const int C = CACHE ? 1 << a.cache_bits : 0;
-    double *s_cd = sm;
-    uint32_t *s_cq = reinterpret_cast<uint32_t *>(sm + C);
-    double *s_e = sm + C + C / 2;
+    // LDS: edges (T + 1, when they fit) | table (TLDS) | bucket table (u16)
+    double *s_e = sm;
     const int ne = ELDS ? a.T + 1 : 0;
     double *s_t = s_e + ((ne + 1) & ~1);
     const int ntab = TLDS ? a.nd * a.nt : 0;
     uint16_t *s_b = reinterpret_cast<uint16_t *>(s_t + ntab);
-    for (int i = threadIdx.x; i < C; i += blockDim.x) {
-        s_cd[i] = a.cache_d[i];
-        s_cq[i] = a.cache_q[i];
-    }
     for (int i = threadIdx.x; i < ne; i += blockDim.x) s_e[i] = a.edges[i];
     for (int i = threadIdx.x; i < ntab; i += blockDim.x) s_t[i] = a.table[i];
     for (int i = threadIdx.x; i < a.G; i += blockDim.x) s_b[i] = a.buckets[i];
     __syncthreads();
-    const __amdgpu_buffer_rsrc_t drs = coord_rsrc(a.pix_d, a.L * 8u);
     // compile-time LDS or global: a runtime choice makes every edge read a
     // flat load (counted by both vmcnt and lgkmcnt)
     const double *e = ELDS ? s_e : a.edges;
@@ -155,14 +122,7 @@ __global__ __launch_bounds__(1024) void k_event_coord(CoordArgs a, const int *__
     auto dist = [&](int p) __attribute__((always_inline)) {
         // monitors carry no pixel ids: every event is at the one distance
         const unsigned q = pid ? (unsigned)p - (unsigned)a.pid_off : 0u;
-        if (!CACHE) return q < a.L ? a.pix_d[q] : __builtin_nan("");
-        // cached pixels load out of range (no request, returns 0), the others
-        // gather; ids outside the LUT read the NaN past its end... as -1 below
-        const unsigned slot = q & (unsigned)(C - 1);
-        const bool hit = s_cq[slot] == q;
-        const int off = (hit || q >= a.L) ? (int)0x80000000 : (int)(q * 8u);
-        const double g = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(drs, off, 0, 0));
-        return hit ? s_cd[slot] : (q < a.L ? g : __builtin_nan(""));
+        return q < a.L ? a.pix_d[q] : __builtin_nan("");
     };
     constexpr int V = 8;  // events per thread and iteration: every load issued first
     const bool vec = ((((uintptr_t)pid | (uintptr_t)toa | (uintptr_t)out) & 15u) == 0) && pid;
@@ -417,21 +377,6 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
             if (x == 0x7FFFFFFF) k.keys[tid] = x;
             return;
         }
-        if (k.k24) {  // flags (bits 31, 30) to bits 23, 22 above the 22-bit value
-            unsigned char *base = reinterpret_cast<unsigned char *>(k.keys) + (size_t)c * (kChunk * 3);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                uint32_t kk[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t w = (uint32_t)out[j * 4 + q];
-                    kk[q] = ((w >> 30) << kSieveTagShift) | (w & kSieveValueMask);
-                }
-                *(__attribute__((address_space(1))) v3u *)(base + (size_t)(j * 1024 + tid) * 12u) =
-                    v3u{kk[0] | (kk[1] << 24), (kk[1] >> 8) | (kk[2] << 16), (kk[2] >> 16) | (kk[3] << 8)};
-            }
-            return;
-        }
 #pragma unroll
         for (int j = 0; j < 2; ++j)
             *reinterpret_cast<int4 *>(k.keys + c * kChunk + ((long long)j * 1024 + tid) * 4) =
@@ -556,56 +501,35 @@ hipError_t launch_event_key(const KeyArgs &a, int grid, hipStream_t st, hipEvent
     return hipGetLastError();
 }
 
-size_t coord_smem(const CoordArgs &a, bool table_lds, bool cache) {
+size_t coord_smem(const CoordArgs &a, bool table_lds) {
     const int ne = a.edges_lds ? a.T + 1 : 0;
-    const size_t C = cache ? (size_t)1 << a.cache_bits : 0;
-    return 12 * C + 8 * (size_t)((ne + 1) & ~1) + (table_lds ? 8 * (size_t)a.nd * a.nt : 0) +
-           2 * (size_t)a.G;
+    return 8 * (size_t)((ne + 1) & ~1) + (table_lds ? 8 * (size_t)a.nd * a.nt : 0) + 2 * (size_t)a.G;
 }
 
-hipError_t launch_coord_cache(const uint32_t *pix_cnt, const double *pix_d, long long L, int cbits,
-                              uint32_t *cq, double *cd, hipStream_t st) {
-    hipLaunchKernelGGL(k_coord_cache, dim3((unsigned)(((1LL << cbits) + 255) / 256)), dim3(256), 0, st,
-                       pix_cnt, pix_d, L, cbits, cq, cd);
-    return hipGetLastError();
-}
-
-template <bool TLDS, bool CACHE, bool ELDS>
+template <bool TLDS, bool ELDS>
 static void launch_coord_t(const CoordArgs &a, const int *pid, const int *toa, long long n, int *out,
-                           size_t sm, int threads, long long g, hipStream_t st) {
-    (void)hipFuncSetAttribute((const void *)k_event_coord<TLDS, CACHE, ELDS>,
+                           size_t sm, long long g, hipStream_t st) {
+    (void)hipFuncSetAttribute((const void *)k_event_coord<TLDS, ELDS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipLaunchKernelGGL((k_event_coord<TLDS, CACHE, ELDS>), dim3((unsigned)g), dim3(threads), sm, st, a,
-                       pid, toa, n, out);
-}
-
-template <bool TLDS, bool CACHE>
-static void launch_coord_e(const CoordArgs &a, const int *pid, const int *toa, long long n, int *out,
-                           size_t sm, int threads, long long g, hipStream_t st) {
-    if (a.edges_lds) launch_coord_t<TLDS, CACHE, true>(a, pid, toa, n, out, sm, threads, g, st);
-    else launch_coord_t<TLDS, CACHE, false>(a, pid, toa, n, out, sm, threads, g, st);
+    hipLaunchKernelGGL((k_event_coord<TLDS, ELDS>), dim3((unsigned)g), dim3(256), sm, st, a, pid, toa, n,
+                       out);
 }
 
 hipError_t launch_event_coord(const CoordArgs &a, const int *pid, const int *toa, long long n,
                               int *out, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    // with the distance cache: one 1024-thread block per CU (the cache fills
-    // most of the LDS); without: 256-thread blocks, several per CU
-    const bool cache = a.cache_bits > 0 && a.cache_q && pid &&
-                       coord_smem(a, false, true) <= kCoordSmemMax;
-    const bool tl = coord_smem(a, true, cache) <= kCoordSmemMax;
-    const size_t sm = coord_smem(a, tl, cache);
+    // 256-thread blocks, several per CU; the table in LDS when it fits
+    const bool tl = coord_smem(a, true) <= kCoordSmemMax;
+    const size_t sm = coord_smem(a, tl);
     if (sm > kCoordSmemMax) return hipErrorInvalidValue;
-    const int threads = cache ? 1024 : 256;
-    long long g = (n + (long long)threads * 8 - 1) / ((long long)threads * 8);
-    const long long gmax = cache ? a.cus : 4096;
-    if (g > gmax) g = gmax;
-    if (cache) {
-        if (tl) launch_coord_e<true, true>(a, pid, toa, n, out, sm, threads, g, st);
-        else launch_coord_e<false, true>(a, pid, toa, n, out, sm, threads, g, st);
+    long long g = (n + 256LL * 8 - 1) / (256LL * 8);
+    if (g > 4096) g = 4096;
+    if (tl) {
+        if (a.edges_lds) launch_coord_t<true, true>(a, pid, toa, n, out, sm, g, st);
+        else launch_coord_t<true, false>(a, pid, toa, n, out, sm, g, st);
     } else {
-        if (tl) launch_coord_e<true, false>(a, pid, toa, n, out, sm, threads, g, st);
-        else launch_coord_e<false, false>(a, pid, toa, n, out, sm, threads, g, st);
+        if (a.edges_lds) launch_coord_t<false, true>(a, pid, toa, n, out, sm, g, st);
+        else launch_coord_t<false, false>(a, pid, toa, n, out, sm, g, st);
     }
     return hipGetLastError();
 }

@@ -30,7 +30,6 @@
 
 #include "../../include/lde.h"
 #include "lde_internal.h"
-#include "lde_window.h"
 
 namespace {
 
@@ -70,7 +69,6 @@ struct lde_handle {
     void *d_lut = nullptr;
     bool lut16 = false;
     unsigned char *d_tab = nullptr;
-    bool peel = true;
     int subc = 4;
 
     uint32_t *d_win32 = nullptr;
@@ -86,13 +84,10 @@ struct lde_handle {
     long long pin_cap = 0;
     hipEvent_t pin_done = nullptr;
     bool pin_pending = false;
-    // optional second copy stream for host staging (LDE_STAGE_STREAMS=2)
-    hipStream_t stream2 = nullptr;
-    hipEvent_t ev_s1 = nullptr, ev_s2 = nullptr;
     std::vector<Segment> dev_segments;
 
     // partition workspace
-    int tile_bits = 13, n_tiles = 0;
+    int tile_bits = 14, n_tiles = 0;
     uint16_t *d_payload = nullptr;
     uint32_t *d_starts = nullptr;
     long long chunk_cap = 0;
@@ -116,19 +111,16 @@ struct lde_handle {
     long long segs_cap = 0;
     hipEvent_t segs_done = nullptr;
     bool segs_pending = false;
-    long long item_events_override = 0;
-    long long atomic_threshold = -1;
-    int auto_partition = LDE_STRATEGY_PAGED;
-    // SPLIT workspace (hot rows in LDS + cold keys through the paged path)
+    long long item_events_override = 0;  // diagnostics: pass-B item size
+    // SPLIT (SIEVE event pass, lde_sieve.hip): hot rows in LDS, cold keys
+    // through an exact counting sort and a tile pass
     bool split_ok = false;
     int hot_rows = 0;
     int split_grid = 0;
-    int cache_bits = 0, row_bits = 0, screen_bits = 0;
+    int cache_bits = 0;
     int hot_refresh = 256;      // re-select a replica's hot set after this many batches
     double split_min_cov = 0.3; // sampled hot fraction below which AUTO stays PAGED
-    uint32_t *d_hlut = nullptr;        // [R][L] (row + 1) << 22 | screen * T
     uint32_t *d_pix_cnt = nullptr;     // [L] sampled events per pixel
-    uint32_t *d_pix_tab = nullptr;     // [R][1 << cache_bits] LDS pixel table images
     uint32_t *d_row_screen = nullptr;  // [R][kHotMaxRows]
     uint32_t *d_sel_stats = nullptr;   // [R][4]
     uint32_t *d_sample_part = nullptr, *d_screen_cnt = nullptr;
@@ -137,55 +129,47 @@ struct lde_handle {
     std::vector<int> hot_uses;         // per replica: -1 = not selected yet
     std::vector<double> hot_cov;
     std::vector<char> all_hot;         // per replica: every screen has a hot row
-    // SIEVE hot rows per replica: count, TOA window [lo, lo + w) (w = T: whole
-    // rows), chosen at each selection from the sampled TOA histogram
-    std::vector<int> hot_h, hot_w, hot_lo;
-    std::vector<double> hot_win;       // sampled fraction of events inside the window
-    // SIEVE hot rows as u16 pairs (twice the rows of u32 counters, exact; see
-    // lde_sieve.hip kSievePair): rows that fit, 0 = unavailable; per replica
-    // whether its selection was made for pairs
-    int hot_rows_pair = 0;
-    std::vector<char> hot_pairsel;
-    bool pair_last = false;             // the last SIEVE batch used pairs
-    uint32_t *d_pair_wraps = nullptr;   // blocks whose pairs wrapped (cumulative)
-    size_t sieve_budget = 0;           // LDS bytes of one sieve block
-    uint32_t *d_toa_hist = nullptr, *h_toa_hist = nullptr, *h_screen_cnt = nullptr;
     uint32_t *d_hot_part = nullptr;
     size_t hot_part_cap = 0;
     uint32_t *d_cold = nullptr;
     size_t cold_total_cap = 0;
     uint32_t *d_cold_cnt = nullptr;
-    uint32_t *d_hot_fmt = nullptr;  // SIEVE: per block, hot rows flushed as u16 (LDE_HOT16)
+    uint32_t *d_hot_fmt = nullptr;  // per sieve block: hot rows flushed as u16 (1) or u32 (0)
     unsigned long long *d_trace = nullptr;  // LDE_SIEVE_TRACE: per-block sieve timeline
     std::vector<double> trace_stats;        // per launch: start spread, end spread, mean span (us)
-    lde::SegDesc *d_cold_segs = nullptr;
-    long long *d_cold_chunks = nullptr;
-    int *d_dummy = nullptr;  // 64 zero bytes
-    // SIEVE: lean event pass of SPLIT (lde_sieve.hip), used when its encodings fit
-    bool sieve_ok = false;
     uint32_t *d_glut = nullptr;       // [R][L + 1] pixel words
     uint32_t *d_sieve_tab = nullptr;  // [R][1 << cache_bits] LDS table images
     std::vector<uint32_t> ttab;       // TOA bucket words (host copy)
     uint32_t *d_ttab = nullptr;
-    // wavelength mode (lde_set_coord_lut): per-pixel distance rows/fractions,
-    // the lookup table, the coordinate edges, per-event bin scratch
+    uint32_t ttab_cap = 0;
+    int ttab_shift = 0;
+    lde::ChunkPtrs *d_chunk_tab = nullptr;
+    size_t chunk_tab_cap = 0;
+    int *d_sieve_dummy = nullptr;     // kChunk x (pid_off - 1): the all-invalid chunk
+    // SIEVE cold keys: per (block, tile) counts and offsets, tile-major u16 keys, items
+    uint32_t *d_cold_tcnt = nullptr, *d_cold_boff = nullptr;
+    size_t cold_tcnt_cap = 0, cold_boff_cap = 0;
+    uint16_t *d_cold_keys = nullptr;
+    size_t cold_keys_cap = 0;
+    uint4 *d_cold_items = nullptr;
+    size_t cold_items_cap = 0;
+    uint32_t *d_cold_ttot = nullptr;  // [n_tiles]
+    int sieve_ablate = 0;             // LDE_SIEVE_ABLATE (diagnostics build)
+    int cold_sort_ablate = 0;         // LDE_COLD_SORT_ABLATE (diagnostics build)
+    // wavelength mode (lde_set_coord_lut): per-pixel distances, the lookup
+    // table, the coordinate edges, per-event bin scratch
     bool coord = false;
     lde::CoordArgs cargs{};
     uint16_t *d_cbuck = nullptr;  // coordinate bucket table
-    uint32_t *d_ccq = nullptr;    // coordinate distance cache: pixel per slot
-    double *d_ccd = nullptr;      // ... and its distance
-    bool coord_cache_built = false;
     double *d_cpd = nullptr, *d_ctable = nullptr, *d_cedges = nullptr;
     int *d_cbin = nullptr;
     size_t cbin_cap = 0;
     // keyed wavelength pass (SIEVE path): one k_event_key launch emits the
-    // sieve's finished words (LDE_COORD_KEYED, default 1)
-    bool coord_keyed = true;
-    double *d_key_dist = nullptr;  // [1 << cache_bits] grid coordinate x of each pixel-table slot
+    // sieve's finished words
+    double *d_key_dist = nullptr;  // [R][1 << cache_bits] grid coordinate x (or fx) of each slot
     std::vector<char> key_ok;  // per replica: its key tables are current (1: x layout, 2: FAST layout)
-    unsigned char *d_zero24 = nullptr;  // kChunk * 3 zero bytes: the 24-bit keyed stream's dummy chunk
-    uint8_t *d_key_tabi = nullptr;  // [1 << cache_bits] distance row of each slot (FAST pass)
-    uint32_t *d_key_rec = nullptr;  // [L + 1] x 12 B {word, x} of the batch's replica
+    uint8_t *d_key_tabi = nullptr;  // [R][1 << cache_bits] distance row of each slot (FAST pass)
+    uint32_t *d_key_rec = nullptr;  // [R][L + 1] x 12 B {word, x} per pixel
     // PIXEL strategy (lde_pixel.hip): pixel-range footprints built from the LUT
     bool pixel_ok = false;
     lde::PixSetup pix{};
@@ -198,11 +182,9 @@ struct lde_handle {
     lde::PixChunk *d_pctab = nullptr;
     size_t pctab_cap = 0;
     uint32_t *d_pitem_count = nullptr;
-    int pix_grid = 0, pix_unit = 2, pix_ept = 16, pix_bu = 4, pix_items_per_cu = 0;
-    bool pix24 = true;
-    // predicted slots (LDE_PIX_PRED, default on): the last scatter's run
-    // totals (d_pprev) size this batch's slots, no count pass
-    bool pix_pred = true;
+    int pix_grid = 0, pix_unit = 2;
+    // predicted slots: the last scatter's run totals (d_pprev) size this
+    // batch's slots, no count pass
     uint32_t *d_pprev = nullptr, *d_povf = nullptr;
     uint4 *d_povf_grp = nullptr;
     size_t povf_cap = 0;
@@ -210,50 +192,15 @@ struct lde_handle {
     bool pix_last_pred = false;  // the last PIXEL batch used predicted slots
     int pix_prev_grid = 0;
     std::vector<double> edges;  // the create-time edges (event unit)
-    // knobs read once at create (LDE_LDS_CTAB, LDE_KARG_SEGS, LDE_SIEVE_ABLATE)
-    bool lds_ctab = true, karg_segs = true;
-    int sieve_ablate = 0;
-    bool early_gather = false;  // LDE_EARLY_GATHER
-    bool sieve_pack = false;    // LDE_SIEVE_PACK
-    int cold_sort_mode = 2;     // LDE_COLD_SORT: 0 block, 1 wave-independent, 2 16-byte groups
-    int cold_sort_kpt = 48;     // LDE_COLD_SORT_KPT: keys per thread per piece of mode 2 (16, 32, 48)
-    bool key24 = true;          // LDE_KEY24: 24-bit cold keys when S * T < 2^24 - 1
-    int tail_release = 1;       // LDE_TAIL_RELEASE: per-block L2 writeback at the end of
-                                // 1 the sieve, 2 the cold sort, 4 pass B, 8 PAGED pass A
-    int cold_sort_ablate = 0;   // LDE_COLD_SORT_ABLATE (LDE_DIAGNOSTICS build only)
-    uint32_t ttab_cap = 0;
-    int ttab_shift = 0;
-    bool ttab_log = false;   // log-linear TOA buckets (ttab_shift = M)
-    lde::ChunkPtrs *d_chunk_tab = nullptr;
-    size_t chunk_tab_cap = 0;
-    int *d_sieve_dummy = nullptr;     // kChunk x (pid_off - 1): the all-invalid chunk
-    // SIEVE cold keys: per (block, tile) counts and offsets, tile-major u16 keys, items
-    uint32_t *d_cold_tcnt = nullptr, *d_cold_boff = nullptr;
-    size_t cold_tcnt_cap = 0, cold_boff_cap = 0;
-    uint16_t *d_cold_keys = nullptr;
-    size_t cold_keys_cap = 0;
-    uint4 *d_cold_items = nullptr;
-    size_t cold_items_cap = 0;
-    uint32_t *d_cold_ttot = nullptr;  // [n_tiles]
 
     // finalize scratch
     unsigned long long *d_tot4 = nullptr;
-    void *d_img_cur = nullptr, *d_img_cum = nullptr;  // inside d_pack
-    // finalize outputs leave in one D2H copy: [current image S x 8 B]
-    // [cumulative image S x 8 B][totals 32 B][overflow flag 16 B]
-    unsigned char *d_pack = nullptr, *h_pack = nullptr;  // h_pack pinned
-    // LDE_FINALIZE_MAPPED (default): h_pack is coherent host memory the
-    // finalize kernel writes directly (hd_pack = its device address), so no
-    // copy command and no cache flush in front of one follows the kernel
-    unsigned char *hd_pack = nullptr;
+    // finalize outputs: [current image S x 8 B][cumulative image S x 8 B]
+    // [totals 32 B][overflow flag 16 B][per-block total partials], in coherent
+    // host memory the finalize kernel writes directly (hd_pack = its device
+    // address): no copy command after the kernel
+    unsigned char *h_pack = nullptr, *hd_pack = nullptr;
     hipEvent_t fin_event = nullptr;  // system-scope release after the kernel
-    // split finalize: running cumulative row sums {in range, all bins} per
-    // screen (valid while only the split finalize's fold writes d_cum), and the
-    // event the host waits for (the outputs, not the fold behind them)
-    unsigned long long *d_cum_rows = nullptr;
-    bool cum_rows_valid = false;
-    int fin_split = 0;  // LDE_FIN_SPLIT (diagnostics build)
-    hipEvent_t ready_event = nullptr;
     hipEvent_t block_event = nullptr;  // blocking-sync event: waits past the spin budget
     double wait_pred_us = 0.0;         // predicted stream wait of a finalize (EMA)
     long long waits_blocked = 0, waits_total = 0;
@@ -569,17 +516,13 @@ int build_toa_tables(lde_handle *h, const double *edges, int T, std::vector<unsi
 
 // SIEVE TOA image: one u32 per bucket, (offset of the next threshold inside
 // the bucket, capped at the bucket width) << 8 | bin of the bucket start.
-// Buckets hold at most one threshold, so bin = (w & 0xFF) + (offset of d in
-// its bucket >= (w >> 8)); d >= span (and TOAs before the first edge, which
-// wrap) clamp to `cap` and land on a word whose bin comes out as T (dropped).
-// Linear buckets (2^shift2 wide, the fast layout's) or, with LDE_SIEVE_TOA_LOG=1
-// and a table at least twice smaller, log-linear ones (geometric edges: DREAM's log edges
-// need 4,330 linear buckets for a 25 us narrowest bin, 705 log-linear ones):
-// for d with floor(log2 d) = e, s = max(0, e - M), bucket (s << M) + (d >> s)
-// of width 2^s, i.e. 2^M buckets per octave (*is_log, shift2 = M).
+// Buckets (2^shift2 wide, the fast layout's) hold at most one threshold, so
+// bin = (w & 0xFF) + (offset of d in its bucket >= (w >> 8)); d >= span (and
+// TOAs before the first edge, which wrap) clamp to `cap` and land on a word
+// whose bin comes out as T (dropped).  (Log-linear buckets, 2^M per octave,
+// were measured +-0 in round 3 and removed in round 5.)
 bool build_sieve_toa(const lde::ToaParams &tp, const std::vector<unsigned char> &img,
-                     std::vector<uint32_t> &words, int &shift2, uint32_t &cap, bool *is_log) {
-    if (is_log) *is_log = false;
+                     std::vector<uint32_t> &words, int &shift2, uint32_t &cap) {
     if (!tp.fast || tp.T > lde::kSieveMaxT || tp.span == 0) return false;
     const uint32_t *rthr = reinterpret_cast<const uint32_t *>(img.data());
     const int T = tp.T;
@@ -587,58 +530,15 @@ bool build_sieve_toa(const lde::ToaParams &tp, const std::vector<unsigned char> 
     const unsigned long long span = tp.span;
     const unsigned long long G = ((span - 1) >> shift2) + 1;
     if (G > (unsigned long long)lde::kMaxFastBuckets) return false;
-    // bucket [start, start + width) -> its word, or false when a second
-    // threshold falls inside it
-    auto word = [&](unsigned long long start, unsigned long long width, int &b, uint32_t &w) {
-        while (b + 1 < T && rthr[b + 1] <= start) ++b;
-        if (b + 2 <= T && (unsigned long long)rthr[b + 2] < start + width && start < span) return false;
-        const unsigned long long nxt = rthr[b + 1] > start ? rthr[b + 1] - start : 0;
-        w = (uint32_t)(std::min<unsigned long long>(nxt, width) << 8) | (uint32_t)b;
-        return true;
-    };
-    // (off by default: the log-linear index costs the sieve a few VALU ops per
-    // event and, in its default pipeline, register spills; with the packed
-    // table word it measured +2 us sieve / -2.4 us cold path, net zero, for
-    // 36 more hot rows on DREAM)
-    if (is_log && span < (1ULL << 31) && env_ll("LDE_SIEVE_TOA_LOG", 0) != 0) {
-        const int e_max = 63 - __builtin_clzll(span | 1ULL);  // d <= span
-        for (int M = 0; M <= 12; ++M) {
-            const int s_max = std::max(0, e_max - M);
-            if (s_max > 23) continue;  // offsets stay below 2^24
-            const unsigned long long Gl = ((unsigned long long)s_max << M) + (span >> s_max) + 1;
-            if (2 * Gl > G + 1) break;  // not worth it: finer M only grows the table
-            std::vector<uint32_t> lw((size_t)lde::align4((int)Gl), 0xFFu);
-            int b = 0;
-            bool ok = true;
-            for (unsigned long long g = 0; g < Gl && ok; ++g) {
-                unsigned long long start, width;
-                if (g < (2ULL << M)) {
-                    start = g;
-                    width = 1;
-                } else {
-                    const int sg = (int)(g >> M) - 1;
-                    start = (g - ((unsigned long long)sg << M)) << sg;
-                    width = 1ULL << sg;
-                }
-                uint32_t w = 0;
-                ok = word(start, width, b, w);
-                lw[(size_t)g] = w;
-            }
-            if (!ok) continue;
-            words = std::move(lw);
-            shift2 = M;
-            cap = (uint32_t)span;
-            *is_log = true;
-            return true;
-        }
-    }
     const unsigned long long W = 1ULL << shift2;
     words.assign((size_t)lde::align4((int)G + 1), 0u);
     int b = 0;
     for (unsigned long long g = 0; g < G; ++g) {
-        uint32_t w = 0;
-        (void)word(g << shift2, W, b, w);  // the fast layout guarantees one threshold at most
-        words[(size_t)g] = w;
+        const unsigned long long start = g << shift2;
+        while (b + 1 < T && rthr[b + 1] <= start) ++b;
+        // the fast layout guarantees one threshold per bucket at most
+        const unsigned long long nxt = rthr[b + 1] > start ? rthr[b + 1] - start : 0;
+        words[(size_t)g] = (uint32_t)(std::min<unsigned long long>(nxt, W) << 8) | (uint32_t)b;
     }
     words[(size_t)G] = 0xFFu;
     cap = (G << shift2) > 0xffffffffULL ? 0xffffffffu : (uint32_t)(G << shift2);
@@ -831,29 +731,22 @@ int grow(lde_handle *h, T **p, size_t &cap, size_t need) {
     return LDE_OK;
 }
 
-// PAGED pass A + plan + pass B over `segs` (device table).  Key mode (cold keys
-// of the SPLIT strategy) when n_chunks_dev != nullptr: `chunks` is then an
-// upper bound and the real count is read on the device.  `events` sizes the
-// pass-B work items.
+// PAGED pass A + plan + pass B over `segs` (device table).
 int paged_core(lde_handle *h, const lde::SegDesc *segs, int n_segs, long long chunks,
-               long long total, long long events, const void *lut,
-               const long long *n_chunks_dev) {
+               long long total, const void *lut) {
     const int grid = (int)std::min<long long>(chunks, (long long)h->part_grid);
     const long long per_block = (chunks + grid - 1) / grid;
     const int cap = (int)((per_block * lde::kChunk + lde::kPage - 1) / lde::kPage) + 2 * h->n_tiles + 2;
     const size_t pages = (size_t)grid * (size_t)cap;
     if (pages > 0xffffffffULL) return fail(h, LDE_EINVAL, "batch too large for the page pool");
-    // pass-B work items: ~2 per CU for a full batch; the (smaller) cold-key
-    // stream of SPLIT gets ~1 per 2 CUs, since every item pays a flush of its
-    // whole tile (measured: 64K -> 256K events per item, pass B -23 %)
-    // (full batch: as many items as fit resident, as for the SIEVE cold keys)
+    // pass-B work items: as many as fit resident at once (as for the SIEVE
+    // cold keys), every item pays a flush of its whole tile
     const long long resident =
         (long long)h->cus * std::max<long long>(1, (160LL * 1024) / (4LL << h->tile_bits));
-    const long long per_items = n_chunks_dev ? std::max(1, h->cus / 2)
-                                             : std::max<long long>(h->cus, resident - h->n_tiles);
+    const long long per_items = std::max<long long>(h->cus, resident - h->n_tiles);
     long long item_events = h->item_events_override > 0
                                 ? h->item_events_override
-                                : std::max<long long>(32768, (events + per_items - 1) / per_items);
+                                : std::max<long long>(32768, (total + per_items - 1) / per_items);
     if (item_events > 0x7fffffffLL) item_events = 0x7fffffffLL;
     const long long max_items = (total + item_events - 1) / item_events + h->n_tiles;
     if (int rc = grow(h, &h->d_pages, h->pages_cap, pages * lde::kPage)) return rc;
@@ -903,11 +796,9 @@ int paged_core(lde_handle *h, const lde::SegDesc *segs, int n_segs, long long ch
     a.cap = cap;
     a.overflow = h->d_overflow;
     a.grid = grid;
-    a.tail_release = (h->tail_release & 8) ? 1 : 0;
     {
         Timed tm(h, LDE_K_PAGED);
-        if (n_chunks_dev) HIPCALL(h, lde::launch_paged_keys(a, n_chunks_dev, h->stream));
-        else HIPCALL(h, lde::launch_paged_partition(a, h->stream));
+        HIPCALL(h, lde::launch_paged_partition(a, h->stream));
     }
     {
         Timed tm(h, LDE_K_PAGE_PLAN);
@@ -928,7 +819,7 @@ int paged_core(lde_handle *h, const lde::SegDesc *segs, int n_segs, long long ch
 int bin_paged(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks,
               long long total, const void *lut) {
     if (int rc = upload_segments(h, sd)) return rc;
-    return paged_core(h, h->d_segs, (int)sd.size(), chunks, total, total, lut, nullptr);
+    return paged_core(h, h->d_segs, (int)sd.size(), chunks, total, lut);
 }
 
 // Wavelength mode, bin stream: every event's coordinate bin (k_event_coord)
@@ -958,91 +849,25 @@ int coord_prepass(lde_handle *h, std::vector<lde::SegDesc> &sd) {
 
 int auto_strategy(const lde_handle *h, long long total) {
     if (h->strategy != LDE_STRATEGY_AUTO) return h->strategy;
-    const long long thr = h->atomic_threshold >= 0 ? h->atomic_threshold
-                                                   : std::max<long long>(1 << 20, h->nbins / 2);
-    return (h->n_tiles > 0 && total >= thr) ? h->auto_partition : LDE_STRATEGY_ATOMIC;
+    const long long thr = std::max<long long>(1 << 20, h->nbins / 2);
+    return (h->n_tiles > 0 && total >= thr) ? LDE_STRATEGY_PAGED : LDE_STRATEGY_ATOMIC;
 }
 
 // Wavelength mode: the coordinate pass can be deferred into the SIEVE path
 // (keyed pass) when the batch may take it; bin_segments runs the plain
 // pass for whatever does not.
 bool coord_keyed_candidate(const lde_handle *h, long long total) {
-    if (!h->coord || !h->coord_keyed || h->monitor || !h->sieve_ok || !h->split_ok || h->n_tiles == 0)
-        return false;
+    if (!h->coord || h->monitor || !h->split_ok || h->n_tiles == 0) return false;
     const int strat = auto_strategy(h, total);
     return strat == LDE_STRATEGY_SPLIT ||
            (h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED);
 }
 
-// SPLIT: hot rows of this replica in LDS, cold keys through paged_core.
-// Returns 1 (nothing launched) when AUTO should fall back to PAGED.
-// coord_deferred (wavelength mode): `sd` still holds times; the sieve path
-// runs the keyed coordinate pass, the k_split path the plain one (and `sd`
-// is updated to the bin stream).
-// SIEVE hot rows with a TOA window: a row holds bins [lo, lo + w) of its
-// screen, so narrower rows fit more screens into the same LDS.  Worth it when
-// the stream's TOA bins concentrate (DREAM: 99.8 % of the events in the top
-// 60 of 100 geometric bins, so 386 rows of 55-60 bins instead of 232 whole
-// rows: 78 % instead of 75 % of the events hot).  Views where every screen
-// can have a whole row, and wavelength mode (the keyed pass folds the bin
-// into the word), keep whole rows.
-// Measured on DREAM (4 interleaved runs, one box): 396-403 rows of bins
-// [40, 97-98) instead of 232 whole rows, 78 % instead of 75 % of the events
-// hot, cold path 0.0945 -> 0.0909 ms, sieve +1.2 us (the window test), step
-// +-0: off by default (LDE_HOT_WINDOW=1, diagnostics build; exact, in the
-// parity matrix).
-bool window_candidate(const lde_handle *h) {
-    // (the windowed sieve is compiled for the default pipeline only)
-    return h->sieve_ok && !h->coord && h->d_toa_hist && h->S > h->hot_rows && !h->sieve_pack &&
-           !h->early_gather && !h->ttab_log && h->sieve_ablate == 0 && env_ll("LDE_HOT_WINDOW", 0) != 0;
-}
-
-// SIEVE hot rows as u16 pairs (the default pipeline, whole rows, integer
-// counts): twice the rows in the same LDS, so fewer cold keys.  Measured on
-// DREAM: 464 rows cover 79 % instead of 75 %,
-// cold path -2.7 us, sieve +2.5 us, step +-0: off by default (LDE_HOT_PAIR=1,
-// diagnostics build; exact, in the parity matrix).
-bool pair_candidate(const lde_handle *h) {
-    return h->hot_rows_pair > 0 && h->sieve_ok && !h->coord && h->d_hot_fmt && !h->sieve_pack &&
-           !h->early_gather && !h->ttab_log && h->sieve_ablate == 0 && !window_candidate(h);
-}
-
-// the most rows of w bins (window starting at lo) the sieve block's LDS holds
-int window_rows(const lde_handle *h, int w, int lo) {
-    int a = 0, b = (int)std::min<long long>(lde::kHotMaxRows, h->S);
-    const long long cap = env_ll("LDE_HOT_ROWS", 0);  // diagnostics: a row budget
-    if (cap > 0) b = (int)std::min<long long>(b, cap);
-    auto fits = [&](int H) {
-        return lde::sieve_smem((lo + H * w + 7) & ~7, h->cache_bits, (int)h->ttab.size(), h->n_tiles,
-                               w == h->T ? 0 : H) <= h->sieve_budget;
-    };
-    if (fits(b)) return b;
-    while (a + 1 < b) {  // fits(a) (0 rows always fits), !fits(b)
-        const int m = (a + b) / 2;
-        if (fits(m)) a = m; else b = m;
-    }
-    return a;
-}
-
-// Host choice from this replica's sample (h_screen_cnt, h_toa_hist): the
-// window width w and start lo that maximize the sampled hot fraction
-// (top-H screens' share x the window's share of the TOA bins), against whole
-// rows; only a gain of at least 0.5 % of the events changes the rows.  Exact
-// whatever the choice (hot events outside the window leave as cold keys).
-void choose_window(lde_handle *h, int r) {
-    const lde::HotWindow c = lde::choose_hot_window(
-        h->h_screen_cnt, h->S, h->h_toa_hist, h->T, h->hot_rows,
-        [h](int w, int lo) { return window_rows(h, w, lo); });
-    h->hot_h[(size_t)r] = c.rows;
-    h->hot_w[(size_t)r] = c.w;
-    h->hot_lo[(size_t)r] = c.lo;
-    h->hot_win[(size_t)r] = c.win;
-    if (env_ll("LDE_VERBOSE", 0))
-        fprintf(stderr, "lde split: replica %d window: %d rows of bins [%d, %d) (%.4f of the sampled times), "
-                        "estimated hot %.3f\n",
-                r, c.rows, c.lo, c.lo + c.w, c.win, c.est);
-}
-
+// SPLIT: the SIEVE pass bins this replica's hot rows in LDS and emits cold
+// keys, sorted into tiles and accumulated by the cold pipeline.  Returns 1
+// (nothing launched) when AUTO should take another strategy.  coord_deferred
+// (wavelength mode): `sd` still holds times; the keyed pass (k_event_key)
+// turns them into the sieve's finished words.
 int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
               long long total, int replica, bool forced, bool coord_deferred) {
     // the descriptor table is uploaded lazily: the SIEVE pass of a batch of
@@ -1063,22 +888,16 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
     a.L = h->L;
     a.pid_off = h->pid_off;
     a.S = (int)h->S;
-    a.tab = h->d_tab;
     a.tp = h->tp;
     a.rows = h->hot_rows;
     a.sample_blocks = (int)std::min<long long>(lde::kSampleBlocks, chunks);
     a.sample_part = h->d_sample_part;
     a.screen_cnt = h->d_screen_cnt;
-    a.stats = h->d_sel_stats + 4 * replica;
     a.screen_row = h->d_screen_row;
-    a.row_screen = h->d_row_screen + (size_t)lde::kHotMaxRows * replica;
-    a.hlut = h->d_hlut + (size_t)h->L * replica;
-    a.grid = (int)std::min<long long>(chunks, (long long)h->split_grid);
     a.cache_bits = h->cache_bits;
-    a.row_bits = h->row_bits;
-    a.screen_bits = h->screen_bits;
     a.pix_cnt = h->d_pix_cnt;
-    a.pix_tab = h->d_pix_tab + ((size_t)replica << h->cache_bits);
+    const int grid = (int)std::min<long long>(chunks, (long long)h->split_grid);
+    const uint32_t *row_screen = h->d_row_screen + (size_t)lde::kHotMaxRows * replica;
     // Hot-set selection samples this batch.  The first time any replica is
     // needed, every replica is selected from the same batch (one host sync in
     // all, instead of one per replica on its first batch); afterwards each
@@ -1086,9 +905,6 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
     // tables are built right after each selection, while d_screen_row holds
     // that replica's rows.
     int &uses = h->hot_uses[replica];
-    const char pair_now = pair_candidate(h) ? 1 : 0;
-    // a selection made for the other row size (u16 pairs / u32) is redone
-    if (uses >= 0 && h->hot_pairsel[(size_t)replica] != pair_now) uses = h->hot_refresh;
     if (uses < 0 || uses >= h->hot_refresh) {
         if (int rc = upload()) return rc;
         std::vector<int> todo;
@@ -1098,49 +914,15 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
             lde::SplitArgs b = a;
             b.stats = h->d_sel_stats + 4 * r;
             b.row_screen = h->d_row_screen + (size_t)lde::kHotMaxRows * r;
-            b.hlut = h->d_hlut + (size_t)h->L * r;
-            b.pix_tab = h->d_pix_tab + ((size_t)r << h->cache_bits);
             Timed tm(h, LDE_K_SPLIT_AUX);
-            const bool window = window_candidate(h);
-            HIPCALL(h, lde::launch_hot_sample(b, r, window ? h->d_toa_hist : nullptr, h->stream));
-            if (window) {
-                // the host sizes this replica's rows from the sample (one sync
-                // per selection, i.e. per replica every hot_refresh batches)
-                HIPCALL(h, hipMemcpyAsync(h->h_screen_cnt, h->d_screen_cnt, (size_t)h->S * 4,
-                                          hipMemcpyDeviceToHost, h->stream));
-                HIPCALL(h, hipMemcpyAsync(h->h_toa_hist, h->d_toa_hist, (size_t)h->T * 4,
-                                          hipMemcpyDeviceToHost, h->stream));
-                HIPCALL(h, hipStreamSynchronize(h->stream));
-                choose_window(h, r);
-            } else {
-                h->hot_h[(size_t)r] = pair_now ? h->hot_rows_pair : h->hot_rows;
-                h->hot_w[(size_t)r] = h->T;
-                h->hot_lo[(size_t)r] = 0;
-                h->hot_win[(size_t)r] = 1.0;
-            }
-            b.rows = h->hot_h[(size_t)r];
-            h->hot_pairsel[(size_t)r] = window ? 0 : pair_now;
-            HIPCALL(h, lde::launch_hot_pick(b, r, h->stream));
+            HIPCALL(h, lde::launch_hot_sample(b, r, h->stream));
+            HIPCALL(h, lde::launch_hot_pick(b, h->stream));
             if ((size_t)r < h->key_ok.size()) h->key_ok[(size_t)r] = 0;  // new glut / table image
-            if (h->sieve_ok)
-                HIPCALL(h, lde::launch_sieve_tables(
-                               (const unsigned char *)h->d_lut + (size_t)r * h->L * (h->lut16 ? 2 : 4),
-                               h->lut16, h->L, h->T, h->hot_w[(size_t)r], h->d_screen_row, h->d_pix_cnt,
-                               h->cache_bits, h->d_glut + (size_t)(h->L + 1) * r,
-                               h->d_sieve_tab + ((size_t)r << h->cache_bits), h->stream));
-        }
-        if (h->coord && h->d_pix_cnt) {
-            // wavelength mode: the sampled hottest pixels' distances in LDS
-            if (!h->d_ccq) {
-                if (int rc = dev_alloc(h, &h->d_ccq, (size_t)1 << lde::kCoordCacheBits)) return rc;
-                if (int rc = dev_alloc(h, &h->d_ccd, (size_t)1 << lde::kCoordCacheBits)) return rc;
-            }
-            HIPCALL(h, lde::launch_coord_cache(h->d_pix_cnt, h->d_cpd, h->L, lde::kCoordCacheBits,
-                                               h->d_ccq, h->d_ccd, h->stream));
-            h->cargs.cache_q = h->d_ccq;
-            h->cargs.cache_d = h->d_ccd;
-            h->cargs.cache_bits = lde::kCoordCacheBits;
-            h->coord_cache_built = true;
+            HIPCALL(h, lde::launch_sieve_tables(
+                           (const unsigned char *)h->d_lut + (size_t)r * h->L * (h->lut16 ? 2 : 4), h->lut16,
+                           h->L, h->T, h->T, h->d_screen_row, h->d_pix_cnt, h->cache_bits,
+                           h->d_glut + (size_t)(h->L + 1) * r, h->d_sieve_tab + ((size_t)r << h->cache_bits),
+                           b.stats, h->stream));
         }
         HIPCALL(h, hipMemcpyAsync(h->h_sel_stats, h->d_sel_stats, (size_t)h->R * 16,
                                   hipMemcpyDeviceToHost, h->stream));
@@ -1148,14 +930,12 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         for (int r : todo) {
             const uint32_t *st = h->h_sel_stats + 4 * r;
             const double sampled = (double)st[0];
-            h->hot_cov[(size_t)r] = sampled > 0 ? (double)st[1] / sampled * h->hot_win[(size_t)r] : 0.0;
+            h->hot_cov[(size_t)r] = sampled > 0 ? (double)st[1] / sampled : 0.0;
             h->all_hot[(size_t)r] = st[2] == (uint32_t)h->S ? 1 : 0;
             h->hot_uses[(size_t)r] = 0;
             if (env_ll("LDE_VERBOSE", 0))
-                fprintf(stderr, "lde split: replica %d sampled %u, hot rows %u (bins %d..%d) cover %.3f, pixel table covers %.3f\n",
-                        r, st[0], st[2], h->hot_lo[(size_t)r], h->hot_lo[(size_t)r] + h->hot_w[(size_t)r] - 1,
-                        h->hot_cov[(size_t)r],
-                        sampled > 0 && h->cache_bits ? (double)st[3] / sampled : 0.0);
+                fprintf(stderr, "lde split: replica %d sampled %u, hot rows %u cover %.3f, pixel table covers %.3f\n",
+                        r, st[0], st[2], h->hot_cov[(size_t)r], sampled > 0 ? (double)st[3] / sampled : 0.0);
         }
     }
     ++uses;
@@ -1165,297 +945,220 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
                     h->hot_cov[replica], h->split_min_cov);
         return 1;
     }
-    const long long per_block = (chunks + a.grid - 1) / a.grid;
-    // SIEVE reserves cold slots in multiples of 4 per wave and half chunk
-    a.cold_cap = per_block * (lde::kChunk + (h->sieve_ok ? 4 * 2 * (lde::kSplitThreads / 64) : 0));
-    const int hr = h->hot_h[replica], hw = h->hot_w[replica], hlo = h->hot_lo[replica];
-    // multiple of 8: u16 hot-row flush; of 16 for u16 pairs (8 LDS words per flush step)
-    const int ht4 = h->hot_pairsel[(size_t)replica] ? (hlo + hr * hw + 15) & ~15 : (hlo + hr * hw + 7) & ~7;
-    if (int rc = grow(h, &h->d_hot_part, h->hot_part_cap, (size_t)a.grid * ht4)) return rc;
+    const long long per_block = (chunks + grid - 1) / grid;
+    // cold slots are reserved in multiples of 4 per wave and half chunk
+    const long long cold_cap = per_block * (lde::kChunk + 4 * 2 * (lde::kSplitThreads / 64));
+    // the rare batch too large for the regions' 32-bit offsets takes PAGED (exact)
+    if ((unsigned long long)cold_cap * 4ULL >= 0x80000000ULL) return 1;
+    const int hr = h->hot_rows;
+    const int ht4 = (hr * h->T + 7) & ~7;  // multiple of 8: the u16 hot-row flush
+    if (int rc = grow(h, &h->d_hot_part, h->hot_part_cap, (size_t)grid * ht4)) return rc;
+    // regions of 24-bit keys (as u32 units: 3 / 4 of that would do)
     if (int rc = grow(h, &h->d_cold, h->cold_total_cap,
-                      (size_t)a.grid * (size_t)(a.cold_cap + lde::kSplitThreads / 64)))
+                      (size_t)grid * (size_t)(cold_cap + lde::kSplitThreads / 64)))
         return rc;
-    a.dummy = h->d_dummy;
-    a.hot_part = h->d_hot_part;
-    a.cold = h->d_cold;
-    a.cold_cnt = h->d_cold_cnt;
-    const bool sieve = h->sieve_ok && (unsigned long long)a.cold_cap * 4ULL < 0x80000000ULL;
-    // windowed rows exist only on the SIEVE path; the rare batch too large for
-    // its cold regions takes PAGED (exact) rather than whole-row k_split
-    const bool pairsel = h->hot_pairsel[(size_t)replica] != 0;  // u16 pair rows (SIEVE only)
-    if (!sieve && (hw != h->T || pairsel)) return 1;
-    if (sieve) {
-        if (int rc = grow(h, &h->d_chunk_tab, h->chunk_tab_cap, (size_t)chunks + 1)) return rc;
-        const size_t nt = (size_t)h->n_tiles;
-        if (int rc = grow(h, &h->d_cold_tcnt, h->cold_tcnt_cap, (size_t)a.grid * lde::kColdGroups * nt)) return rc;
-        if (int rc = grow(h, &h->d_cold_boff, h->cold_boff_cap, (size_t)a.grid * lde::kColdGroups * nt)) return rc;
-        // tile-major u16 keys: at most every staged slot, + the 8-key padding
-        // of every (row, tile) range (k_cold_sort_a), + slack for pass B's
-        // 16-byte loads
-        // the widest sort piece whose LDS still fits two blocks per CU
-        int sort_kpt = h->cold_sort_kpt;
-        while (sort_kpt > 16 && lde::cold_sort_a_smem(h->n_tiles, sort_kpt) > 80 * 1024) sort_kpt -= 16;
-        const bool pad8 = h->cold_sort_mode == 2 && h->n_tiles <= lde::kSortThreadsHost &&
-                          lde::cold_sort_a_smem(h->n_tiles, sort_kpt) <= 80 * 1024;
-        if (int rc = grow(h, &h->d_cold_keys, h->cold_keys_cap,
-                          (size_t)a.grid * (size_t)a.cold_cap +
-                              (pad8 ? (size_t)a.grid * lde::kColdGroups * nt * 8 : 0) + 64))
-            return rc;
-        const double cold_est = std::min(1.0, std::max(0.05, 1.0 - h->hot_cov[replica])) * (double)total;
-        // pass B items: as many as fit resident at once (LDS: one 2^tile_bits
-        // u32 tile per block), so no second round of blocks; a tile with n keys
-        // gets ceil(n / item_keys) <= n / item_keys + 1 items, hence the
-        // n_tiles subtracted (DREAM: 2 x 256 slots, 157 tiles -> ~96K keys per
-        // item, 3 items per tile; one item per tile measured 12 us slower)
-        const long long resident =
-            (long long)h->cus * std::max<long long>(1, (160LL * 1024) / (4LL << h->tile_bits));
-        const long long slots = resident - h->n_tiles;
-        const long long item_keys =
-            h->item_events_override > 0
-                ? h->item_events_override
-                : std::max<long long>(32768, (long long)(cold_est / (double)(slots >= h->cus / 2
-                                                                              ? slots
-                                                                              : std::max(1, h->cus / 2))));
-        const long long max_items = ((long long)a.grid * a.cold_cap) / item_keys + h->n_tiles + 1;
-        if (int rc = grow(h, &h->d_cold_items, h->cold_items_cap, (size_t)max_items)) return rc;
-        // wavelength mode: the keyed pass turns (pid, toa) into the sieve's
-        // finished words, one chunk-aligned stream (ssd) the sieve reads
-        std::vector<lde::SegDesc> ksd;
-        bool key_w24 = false;
-        if (coord_deferred) {
-            // k_event_key takes the messages as kernel arguments when they fit
-            // (no H2D copy in front of it), else from d_segs
-            const bool kkarg = (long long)sd.size() <= lde::kKargSegs;
-            if (!kkarg)
-                if (int rc = upload()) return rc;
-            if (int rc = grow(h, &h->d_cbin, h->cbin_cap, (size_t)chunks * lde::kChunk)) return rc;
-            // per replica: each table slot's distance row / fx (or x) and each
-            // pixel's 12-byte record, built once after the replica's hot-set
-            // selection (or a new coordinate LUT) and reused by its batches
-            const size_t C = (size_t)1 << h->cache_bits;
-            if (!h->d_key_dist)
-                if (int rc = dev_alloc(h, &h->d_key_dist, C * (size_t)h->R)) return rc;
-            const uint32_t *tab_r = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
-            // FAST event pass: fixed bin correction + each pixel's distance row
-            // and fx precomputed (rows fit the record word's 8 tag bits)
-            const bool pre = h->cargs.fixed_bin && h->cargs.edges_lds && h->cargs.nd <= 256 &&
-                             env_ll("LDE_KEY_PRE", 1) != 0;
-            const int pre_nd = pre ? h->cargs.nd : 0;
-            if (pre && !h->d_key_tabi)
-                if (int rc = dev_alloc(h, &h->d_key_tabi, C * (size_t)h->R)) return rc;
-            if (!h->d_key_rec)
-                if (int rc = dev_alloc(h, &h->d_key_rec, 3 * ((size_t)h->L + 1) * (size_t)h->R)) return rc;
-            if (h->key_ok.size() != (size_t)h->R) h->key_ok.assign((size_t)h->R, 0);
-            double *kd_r = h->d_key_dist + C * (size_t)replica;
-            uint8_t *ki_r = pre ? h->d_key_tabi + C * (size_t)replica : nullptr;
-            uint32_t *kr_r = h->d_key_rec + 3 * ((size_t)h->L + 1) * (size_t)replica;
-            const char want = pre ? 2 : 1;  // the layout the replica's tables hold
-            if (h->key_ok[(size_t)replica] != want) {
-                HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->cargs.d0,
-                                                h->cargs.inv_dd, pre_nd, kd_r, ki_r, h->stream));
-                HIPCALL(h, lde::launch_key_records(h->d_glut + (size_t)(h->L + 1) * replica, h->d_cpd,
-                                                   (unsigned)h->L, h->cargs.d0, h->cargs.inv_dd, pre_nd, kr_r,
-                                                   h->stream));
-                h->key_ok[(size_t)replica] = want;
-            }
-            lde::KeyArgs ka;
-            ka.c = h->cargs;
-            ka.segs = h->d_segs;
-            ka.karg = kkarg ? 1 : 0;
-            if (kkarg)
-                for (size_t i = 0; i < sd.size(); ++i) ka.sk.s[i] = sd[i];
-            ka.n_segs = (int)sd.size();
-            ka.n_chunks = chunks;
-            ka.glut = h->d_glut + (size_t)(h->L + 1) * replica;
-            ka.pix_tab = tab_r;
-            ka.tab_d = kd_r;
-            ka.tab_i = ki_r;
-            ka.pre = pre ? 1 : 0;
-            ka.rec = kr_r;
-            ka.cbits = h->cache_bits;
-            ka.keys = h->d_cbin;
-            ka.dummy = h->d_sieve_dummy;
-            ka.ablate = (int)env_ll("LDE_KEY_ABLATE", 0);
-            // words packed to 24 bits (flags + the 22-bit value): 3 bytes per
-            // event written and read back instead of 4
-            ka.k24 = env_ll("LDE_KEY_WORD24", 0) != 0 ? 1 : 0;  // measured +-0 (the sieve reads 12-byte groups slower): off
-            if (ka.k24 && !h->d_zero24) {
-                if (int rc = dev_alloc(h, &h->d_zero24, (size_t)lde::kChunk * 3)) return rc;
-                HIPCALL(h, hipMemsetAsync(h->d_zero24, 0, (size_t)lde::kChunk * 3, h->stream));
-            }
-            key_w24 = ka.k24 != 0;
-            Stamp sp(h, LDE_K_COORD);  // k_event_key, stamped by its own dispatch
-            HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream, sp.a, sp.b));
-            sp.done = true;
-            ksd.push_back({h->d_cbin, h->d_cbin, chunks * lde::kChunk, 0});
+    if (int rc = grow(h, &h->d_chunk_tab, h->chunk_tab_cap, (size_t)chunks + 1)) return rc;
+    const size_t nt = (size_t)h->n_tiles;
+    if (int rc = grow(h, &h->d_cold_tcnt, h->cold_tcnt_cap, (size_t)grid * lde::kColdGroups * nt)) return rc;
+    if (int rc = grow(h, &h->d_cold_boff, h->cold_boff_cap, (size_t)grid * lde::kColdGroups * nt)) return rc;
+    // tile-major u16 keys: at most every staged slot, + the 8-key padding of
+    // every (row, tile) range, + slack for pass B's 16-byte loads
+    if (int rc = grow(h, &h->d_cold_keys, h->cold_keys_cap,
+                      (size_t)grid * (size_t)cold_cap + (size_t)grid * lde::kColdGroups * nt * 8 + 64))
+        return rc;
+    const double cold_est = std::min(1.0, std::max(0.05, 1.0 - h->hot_cov[replica])) * (double)total;
+    // pass B items: as many as fit resident at once (LDS: one 2^tile_bits
+    // u32 tile per block), so no second round of blocks; a tile with n keys
+    // gets ceil(n / item_keys) <= n / item_keys + 1 items, hence the
+    // n_tiles subtracted (DREAM: 2 x 256 slots, 157 tiles -> ~96K keys per
+    // item, 3 items per tile; one item per tile measured 12 us slower)
+    const long long resident =
+        (long long)h->cus * std::max<long long>(1, (160LL * 1024) / (4LL << h->tile_bits));
+    const long long slots = resident - h->n_tiles;
+    const long long item_keys =
+        h->item_events_override > 0
+            ? h->item_events_override
+            : std::max<long long>(32768, (long long)(cold_est / (double)(slots >= h->cus / 2
+                                                                          ? slots
+                                                                          : std::max(1, h->cus / 2))));
+    const long long max_items = ((long long)grid * cold_cap) / item_keys + h->n_tiles + 1;
+    if (int rc = grow(h, &h->d_cold_items, h->cold_items_cap, (size_t)max_items)) return rc;
+    // wavelength mode: the keyed pass turns (pid, toa) into the sieve's
+    // finished words, one chunk-aligned stream (ssd) the sieve reads
+    std::vector<lde::SegDesc> ksd;
+    if (coord_deferred) {
+        // k_event_key takes the messages as kernel arguments when they fit
+        // (no H2D copy in front of it), else from d_segs
+        const bool kkarg = (long long)sd.size() <= lde::kKargSegs;
+        if (!kkarg)
+            if (int rc = upload()) return rc;
+        if (int rc = grow(h, &h->d_cbin, h->cbin_cap, (size_t)chunks * lde::kChunk)) return rc;
+        // per replica: each table slot's distance row / fx (or x) and each
+        // pixel's 12-byte record, built once after the replica's hot-set
+        // selection (or a new coordinate LUT) and reused by its batches
+        const size_t C = (size_t)1 << h->cache_bits;
+        if (!h->d_key_dist)
+            if (int rc = dev_alloc(h, &h->d_key_dist, C * (size_t)h->R)) return rc;
+        const uint32_t *tab_r = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
+        // FAST event pass: fixed bin correction + each pixel's distance row
+        // and fx precomputed (rows fit the record word's 8 tag bits)
+        const bool pre = h->cargs.fixed_bin && h->cargs.edges_lds && h->cargs.nd <= 256;
+        const int pre_nd = pre ? h->cargs.nd : 0;
+        if (pre && !h->d_key_tabi)
+            if (int rc = dev_alloc(h, &h->d_key_tabi, C * (size_t)h->R)) return rc;
+        if (!h->d_key_rec)
+            if (int rc = dev_alloc(h, &h->d_key_rec, 3 * ((size_t)h->L + 1) * (size_t)h->R)) return rc;
+        if (h->key_ok.size() != (size_t)h->R) h->key_ok.assign((size_t)h->R, 0);
+        double *kd_r = h->d_key_dist + C * (size_t)replica;
+        uint8_t *ki_r = pre ? h->d_key_tabi + C * (size_t)replica : nullptr;
+        uint32_t *kr_r = h->d_key_rec + 3 * ((size_t)h->L + 1) * (size_t)replica;
+        const char want = pre ? 2 : 1;  // the layout the replica's tables hold
+        if (h->key_ok[(size_t)replica] != want) {
+            HIPCALL(h, lde::launch_key_dist(tab_r, h->cache_bits, h->d_cpd, (unsigned)h->L, h->cargs.d0,
+                                            h->cargs.inv_dd, pre_nd, kd_r, ki_r, h->stream));
+            HIPCALL(h, lde::launch_key_records(h->d_glut + (size_t)(h->L + 1) * replica, h->d_cpd,
+                                               (unsigned)h->L, h->cargs.d0, h->cargs.inv_dd, pre_nd, kr_r,
+                                               h->stream));
+            h->key_ok[(size_t)replica] = want;
         }
-        const std::vector<lde::SegDesc> &ssd = coord_deferred ? ksd : sd;
-        lde::SieveArgs sa;
-        sa.keyed = coord_deferred ? 1 : 0;
-        sa.keyed24 = key_w24 ? 1 : 0;
-        sa.keyed_base = h->d_cbin;
-        sa.zero24 = h->d_zero24;
-        sa.segs = h->d_segs;
-        sa.n_segs = (int)ssd.size();
-        sa.n_chunks = chunks;
-        sa.chunk_tab = h->d_chunk_tab;
-        sa.glut = h->d_glut + (size_t)(h->L + 1) * replica;
-        sa.L = (uint32_t)h->L;
-        sa.pid_off = h->pid_off;
-        sa.ttab = h->d_ttab;
-        sa.toa_lo = (uint32_t)h->tp.lo;
-        sa.toa_cap = h->ttab_cap;
-        sa.toa_shift = h->ttab_shift;
-        sa.toa_log = h->ttab_log ? 1 : 0;
-        sa.toa_words4 = (int)h->ttab.size();
-        sa.T = h->T;
-        sa.pix_tab = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
-        sa.cbits = h->cache_bits;
-        sa.hot_words = pairsel ? ht4 / 2 : ht4;  // LDS words (u16 pairs: two counters each)
-        sa.pair = pairsel ? 1 : 0;
-        sa.hist = h->d_win32;
-        sa.wraps = h->d_pair_wraps;
-        h->pair_last = pairsel;
-        sa.hot_lo = hlo;
-        sa.hot_w = hw;
-        sa.hot_rows = hr;
-        sa.hot_inv_w = 1.0f / (float)hw;
-        sa.row_screen = a.row_screen;
-        sa.hot_part = h->d_hot_part;
-        sa.cold = h->d_cold;
-        sa.cold_cap = a.cold_cap;
-        sa.cold_cnt = h->d_cold_cnt;
-        sa.tile_bits = h->tile_bits;
-        sa.n_tiles = h->n_tiles;
-        sa.cold_tcnt = h->d_cold_tcnt;
-        sa.ablate = h->sieve_ablate;
-        sa.early_gather = h->early_gather ? 1 : 0;
-        sa.pack = h->sieve_pack ? 1 : 0;
-        // 24-bit cold keys need the 16-byte-group sort (the only reader)
-        const bool key24 = pad8 && h->key24 && h->nbins < 0xFFFFFFLL;
-        sa.key24 = key24 ? 1 : 0;
-        sa.hot_fmt = h->d_hot_fmt;
-        sa.tail_release = h->tail_release;
-        sa.trace = h->d_trace;
-        {
-            // k_sieve is timed by its own dispatch (start/stop events stamped
-            // by hipExtLaunchKernelGGL): no marker packets around it
-            hipEvent_t ea = nullptr, eb = nullptr;
-            if (h->timing && ((h->timing_mask >> LDE_K_SPLIT) & 1u)) {
-                ea = pool_event(h);
-                eb = ea ? pool_event(h) : nullptr;
-                if (!eb && ea) {
-                    h->event_pool.push_back(ea);
-                    ea = nullptr;
-                }
-            }
-            // the sieve builds its chunk table in LDS (no launch in front of
-            // it) when the block's chunk range fits, from descriptors passed
-            // as kernel arguments when they fit too, else from d_segs
-            const long long per_block = (chunks + a.grid - 1) / a.grid;
-            sa.lds_ctab = per_block + 1 <= lde::kSieveLdsChunks && h->lds_ctab;
-            sa.karg = (long long)ssd.size() <= lde::kKargSegs;
-            sa.dummy = h->d_sieve_dummy;
-            if (sa.lds_ctab && sa.karg) {
-                for (size_t i = 0; i < ssd.size(); ++i) sa.sk.s[i] = ssd[i];
-            } else if (sa.lds_ctab) {
-                if (int rc = upload()) return rc;
-            } else if ((!uploaded || coord_deferred) && (long long)ssd.size() <= lde::kKargSegs &&
-                       (h->karg_segs || coord_deferred)) {
-                // (keyed: also rewrites d_segs to the key stream's descriptor,
-                // which the sieve's deferred-chunk pass reads)
-                HIPCALL(h, lde::launch_chunk_tab_karg(ssd.data(), sa.n_segs, chunks, h->d_sieve_dummy,
-                                                      h->d_chunk_tab, h->d_segs, h->stream));
-            } else {
-                if (int rc = upload()) return rc;
-                HIPCALL(h, lde::launch_chunk_tab(h->d_segs, a.n_segs, chunks, h->d_sieve_dummy,
-                                                 h->d_chunk_tab, h->stream));
-            }
-            HIPCALL(h, lde::launch_sieve(sa, a.grid, h->stream, ea, eb));
-            if (h->d_trace) {  // diagnostic only: a host sync per batch
-                std::vector<unsigned long long> tr((size_t)a.grid * 3);
-                HIPCALL(h, hipMemcpyAsync(tr.data(), h->d_trace, tr.size() * 8, hipMemcpyDeviceToHost,
-                                          h->stream));
-                HIPCALL(h, hipStreamSynchronize(h->stream));
-                unsigned long long s0 = ~0ull, s1 = 0, m0 = ~0ull, m1 = 0, e0 = ~0ull, e1 = 0;
-                for (int b = 0; b < a.grid; ++b) {
-                    s0 = std::min(s0, tr[3 * b]); s1 = std::max(s1, tr[3 * b]);
-                    m0 = std::min(m0, tr[3 * b + 1]); m1 = std::max(m1, tr[3 * b + 1]);
-                    e0 = std::min(e0, tr[3 * b + 2]); e1 = std::max(e1, tr[3 * b + 2]);
-                }
-                const double us = 1e6 / 100e6;  // s_memrealtime: 100 MHz
-                h->trace_stats.push_back((s1 - s0) * us);
-                h->trace_stats.push_back((m1 - m0) * us);
-                h->trace_stats.push_back((e1 - e0) * us);
-                h->trace_stats.push_back((e1 - s0) * us);
-                if (env_ll("LDE_SIEVE_TRACE", 0) > 1) {  // per block: stream end after the first start
-                    fprintf(stderr, "lde sieve trace blocks:");
-                    for (int b = 0; b < a.grid; ++b) fprintf(stderr, " %.1f", (tr[3 * b + 1] - s0) * us);
-                    fprintf(stderr, "\n");
-                }
-            }
-            if (h->probe) {
-                const double us = std::chrono::duration<double, std::micro>(
-                                      std::chrono::steady_clock::now() - h->t_acc0).count();
-                h->probe_us += us;
-                h->probe_min = h->probe_n ? std::min(h->probe_min, us) : us;
-                ++h->probe_n;
-            }
-            if (ea) h->launches.push_back({LDE_K_SPLIT, ea, eb});
-        }
-        lde::ColdArgs c;
-        c.hot_part = h->d_hot_part;
-        c.row_screen = a.row_screen;
-        c.ht = hlo + hr * hw;
-        c.hot_lo = hlo;
-        c.hot_w = hw;
-        c.ht4 = pairsel ? ht4 / 2 : ht4;  // a block's partial rows: c.ht4 u32 words (2 c.ht4 u16)
-        c.T = h->T;
-        c.tile_bits = h->tile_bits;
-        c.n_tiles = h->n_tiles;
-        c.rows = a.grid;
-        c.cold = h->d_cold;
-        c.stride = a.cold_cap + lde::kSplitThreads / 64;
-        c.cap = a.cold_cap;
-        c.cold_cnt = h->d_cold_cnt;
-        c.tcnt = h->d_cold_tcnt;
-        c.boff = h->d_cold_boff;
-        c.tile_total = h->d_cold_ttot;
-        c.item_keys = (uint32_t)std::min<long long>(item_keys, 0x7fffffffLL);
-        c.max_items = (uint32_t)max_items;
-        c.items = h->d_cold_items;
-        c.item_count = h->d_item_count;
-        c.keys = h->d_cold_keys;
-        c.hist = h->d_win32;
-        c.n_bins = h->nbins;
-        c.wave_sort = h->cold_sort_mode == 1 ? 1 : 0;
-        c.pad8 = pad8 ? 1 : 0;
-        c.sort_kpt = sort_kpt;
-        c.key24 = key24 ? 1 : 0;
-        c.hot_fmt = h->d_hot_fmt;
-        c.tail_release = h->tail_release;
-        c.ablate = h->cold_sort_ablate;
-        c.all_hot = h->all_hot[replica];
-        Timed tm(h, LDE_K_PAGED);
-        HIPCALL(h, lde::launch_cold_pipeline(c, h->stream, h->bin_stop_ext));
-        if (h->bin_stop_ext) h->bin_stop_used = true;
-        return LDE_OK;
-    } else {
-        if (coord_deferred) {
-            if (int rc = coord_prepass(h, sd)) return rc;
-            uploaded = false;
-        }
-        if (int rc = upload()) return rc;
-        Timed tm(h, LDE_K_SPLIT);
-        HIPCALL(h, lde::launch_split(a, h->stream));
+        lde::KeyArgs ka;
+        ka.c = h->cargs;
+        ka.segs = h->d_segs;
+        ka.karg = kkarg ? 1 : 0;
+        if (kkarg)
+            for (size_t i = 0; i < sd.size(); ++i) ka.sk.s[i] = sd[i];
+        ka.n_segs = (int)sd.size();
+        ka.n_chunks = chunks;
+        ka.glut = h->d_glut + (size_t)(h->L + 1) * replica;
+        ka.pix_tab = tab_r;
+        ka.tab_d = kd_r;
+        ka.tab_i = ki_r;
+        ka.pre = pre ? 1 : 0;
+        ka.rec = kr_r;
+        ka.cbits = h->cache_bits;
+        ka.keys = h->d_cbin;
+        ka.dummy = h->d_sieve_dummy;
+        ka.ablate = (int)env_ll("LDE_KEY_ABLATE", 0);
+        Stamp sp(h, LDE_K_COORD);  // k_event_key, stamped by its own dispatch
+        HIPCALL(h, lde::launch_event_key(ka, h->cus, h->stream, sp.a, sp.b));
+        sp.done = true;
+        ksd.push_back({h->d_cbin, h->d_cbin, chunks * lde::kChunk, 0});
     }
+    const std::vector<lde::SegDesc> &ssd = coord_deferred ? ksd : sd;
+    lde::SieveArgs sa;
+    sa.keyed = coord_deferred ? 1 : 0;
+    sa.segs = h->d_segs;
+    sa.n_segs = (int)ssd.size();
+    sa.n_chunks = chunks;
+    sa.chunk_tab = h->d_chunk_tab;
+    sa.glut = h->d_glut + (size_t)(h->L + 1) * replica;
+    sa.L = (uint32_t)h->L;
+    sa.pid_off = h->pid_off;
+    sa.ttab = h->d_ttab;
+    sa.toa_lo = (uint32_t)h->tp.lo;
+    sa.toa_cap = h->ttab_cap;
+    sa.toa_shift = h->ttab_shift;
+    sa.toa_words4 = (int)h->ttab.size();
+    sa.T = h->T;
+    sa.pix_tab = h->d_sieve_tab + ((size_t)replica << h->cache_bits);
+    sa.cbits = h->cache_bits;
+    sa.hot_words = ht4;
+    sa.hot_part = h->d_hot_part;
+    sa.cold = h->d_cold;
+    sa.cold_cap = cold_cap;
+    sa.cold_cnt = h->d_cold_cnt;
+    sa.tile_bits = h->tile_bits;
+    sa.n_tiles = h->n_tiles;
+    sa.cold_tcnt = h->d_cold_tcnt;
+    sa.ablate = h->sieve_ablate;
+    sa.hot_fmt = h->d_hot_fmt;
+    sa.trace = h->d_trace;
     {
-        Timed tm(h, LDE_K_SPLIT_AUX);
-        HIPCALL(h, lde::launch_split_tail(a, h->d_win32, h->d_cold_segs, h->d_cold_chunks, h->stream));
+        // k_sieve is timed by its own dispatch (start/stop events stamped
+        // by hipExtLaunchKernelGGL): no marker packets around it
+        Stamp sp(h, LDE_K_SPLIT);
+        // the sieve builds its chunk table in LDS (no launch in front of
+        // it) when the block's chunk range fits, from descriptors passed
+        // as kernel arguments when they fit too, else from d_segs
+        sa.lds_ctab = per_block + 1 <= lde::kSieveLdsChunks;
+        sa.karg = (long long)ssd.size() <= lde::kKargSegs;
+        sa.dummy = h->d_sieve_dummy;
+        if (sa.lds_ctab && sa.karg) {
+            for (size_t i = 0; i < ssd.size(); ++i) sa.sk.s[i] = ssd[i];
+        } else if (sa.lds_ctab) {
+            if (int rc = upload()) return rc;
+        } else if ((!uploaded || coord_deferred) && (long long)ssd.size() <= lde::kKargSegs) {
+            // (keyed: also rewrites d_segs to the key stream's descriptor,
+            // which the sieve's deferred-chunk pass reads)
+            HIPCALL(h, lde::launch_chunk_tab_karg(ssd.data(), sa.n_segs, chunks, h->d_sieve_dummy,
+                                                  h->d_chunk_tab, h->d_segs, h->stream));
+        } else {
+            if (int rc = upload()) return rc;
+            HIPCALL(h, lde::launch_chunk_tab(h->d_segs, sa.n_segs, chunks, h->d_sieve_dummy,
+                                             h->d_chunk_tab, h->stream));
+        }
+        HIPCALL(h, lde::launch_sieve(sa, grid, h->stream, sp.a, sp.b));
+        sp.done = true;
+        if (h->d_trace) {  // diagnostic only: a host sync per batch
+            std::vector<unsigned long long> tr((size_t)grid * 3);
+            HIPCALL(h, hipMemcpyAsync(tr.data(), h->d_trace, tr.size() * 8, hipMemcpyDeviceToHost,
+                                      h->stream));
+            HIPCALL(h, hipStreamSynchronize(h->stream));
+            unsigned long long s0 = ~0ull, s1 = 0, m0 = ~0ull, m1 = 0, e0 = ~0ull, e1 = 0;
+            for (int b = 0; b < grid; ++b) {
+                s0 = std::min(s0, tr[3 * b]); s1 = std::max(s1, tr[3 * b]);
+                m0 = std::min(m0, tr[3 * b + 1]); m1 = std::max(m1, tr[3 * b + 1]);
+                e0 = std::min(e0, tr[3 * b + 2]); e1 = std::max(e1, tr[3 * b + 2]);
+            }
+            const double us = 1e6 / 100e6;  // s_memrealtime: 100 MHz
+            h->trace_stats.push_back((s1 - s0) * us);
+            h->trace_stats.push_back((m1 - m0) * us);
+            h->trace_stats.push_back((e1 - e0) * us);
+            h->trace_stats.push_back((e1 - s0) * us);
+            if (env_ll("LDE_SIEVE_TRACE", 0) > 1) {  // per block: stream end after the first start
+                fprintf(stderr, "lde sieve trace blocks:");
+                for (int b = 0; b < grid; ++b) fprintf(stderr, " %.1f", (tr[3 * b + 1] - s0) * us);
+                fprintf(stderr, "\n");
+            }
+        }
+        if (h->probe) {
+            const double us = std::chrono::duration<double, std::micro>(
+                                  std::chrono::steady_clock::now() - h->t_acc0).count();
+            h->probe_us += us;
+            h->probe_min = h->probe_n ? std::min(h->probe_min, us) : us;
+            ++h->probe_n;
+        }
     }
-    const double cold_frac = std::min(1.0, std::max(0.05, 1.0 - h->hot_cov[replica]));
-    return paged_core(h, h->d_cold_segs, a.grid, chunks, total, (long long)(cold_frac * total),
-                      nullptr, h->d_cold_chunks);
+    lde::ColdArgs c;
+    c.hot_part = h->d_hot_part;
+    c.row_screen = row_screen;
+    c.ht = hr * h->T;
+    c.ht4 = ht4;
+    c.T = h->T;
+    c.tile_bits = h->tile_bits;
+    c.n_tiles = h->n_tiles;
+    c.rows = grid;
+    c.cold = h->d_cold;
+    c.stride = cold_cap + lde::kSplitThreads / 64;
+    c.cap = cold_cap;
+    c.cold_cnt = h->d_cold_cnt;
+    c.tcnt = h->d_cold_tcnt;
+    c.boff = h->d_cold_boff;
+    c.tile_total = h->d_cold_ttot;
+    c.item_keys = (uint32_t)std::min<long long>(item_keys, 0x7fffffffLL);
+    c.max_items = (uint32_t)max_items;
+    c.items = h->d_cold_items;
+    c.item_count = h->d_item_count;
+    c.keys = h->d_cold_keys;
+    c.hist = h->d_win32;
+    c.n_bins = h->nbins;
+    c.hot_fmt = h->d_hot_fmt;
+    c.ablate = h->cold_sort_ablate;
+    c.all_hot = h->all_hot[replica];
+    Timed tm(h, LDE_K_PAGED);
+    HIPCALL(h, lde::launch_cold_pipeline(c, h->stream, h->bin_stop_ext));
+    if (h->bin_stop_ext) h->bin_stop_used = true;
+    return LDE_OK;
 }
 
 int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks, long long total,
@@ -1473,7 +1176,7 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     const double ratio = h->pix_prev_n > 0 ? (double)total / (double)h->pix_prev_n : 0.0;
     const double pred_pay = 1.25 * ratio * (double)(h->pix_prev_n + 3 * h->pix_prev_units * h->pix.nr) +
                             20.0 * (double)slots + 4.0;
-    const bool pred = h->pix_pred && h->pix_prev_grid == grid && ratio >= 0.5 && ratio <= 2.0 &&
+    const bool pred = h->pix_prev_grid == grid && ratio >= 0.5 && ratio <= 2.0 &&
                       total >= 256 * slots && pred_pay < 0x7FFFFFF0;
     // overflow list: 1/32 of the batch's groups (a Poisson stream overflows
     // ~0.4 % of them at 2 sigma margins) -- groups past it are added by pass A
@@ -1484,23 +1187,18 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
         n_pay = std::max(n_pay, (size_t)pred_pay);
         if (int rc = grow(h, &h->d_povf_grp, h->povf_cap, ovf_groups)) return rc;
     }
-    if (int rc = grow(h, &h->d_ppayload, h->ppayload_cap, h->pix24 ? (n_pay * 3 + 3) / 4 + 4 : n_pay))
-        return rc;
+    if (int rc = grow(h, &h->d_ppayload, h->ppayload_cap, (n_pay * 3 + 3) / 4 + 4)) return rc;
     // pass-B items: each flushes its range's whole footprint (F x T
     // atomics), so as few as keep the CUs busy: one per range up to twice the
     // mean range total, larger ranges (skewed streams) split (LOKI: 196
-    // items, pass B 0.157 -> 0.120 ms against ~600 items of total / 2 CUs);
-    // LDE_PIX_ITEMS=k: total / (k x CUs) events per item instead
-    const long long ipc = h->pix_items_per_cu;
-    const long long per =
-        (std::max<long long>(65536, ipc == 0 ? (2 * total + h->pix.nr - 1) / h->pix.nr
-                                              : (total + ipc * h->cus - 1) / (ipc * h->cus)) + 3) & ~3LL;
+    // items, pass B 0.157 -> 0.120 ms against ~600 items of total / 2 CUs)
+    const long long per = (std::max<long long>(65536, (2 * total + h->pix.nr - 1) / h->pix.nr) + 3) & ~3LL;
     const long long max_items = (long long)(n_pay / (size_t)per) + h->pix.nr + 1;
     if (int rc = grow(h, &h->d_pitems, h->pitems_cap, (size_t)max_items)) return rc;
     if (int rc = grow(h, &h->d_pctab, h->pctab_cap, (size_t)chunks)) return rc;
     lde::PixArgs a;
     a.ctab = h->d_pctab;
-    a.ept = h->pix_ept;
+    a.ept = h->pix_unit == 2 ? 16 : 8;
     a.segs = h->d_segs;
     a.n_segs = (int)sd.size();
     a.n_chunks = chunks;
@@ -1508,7 +1206,6 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.L = (unsigned)h->L;
     a.rb = h->pix.rb;
     a.ablate = (int)env_ll("LDE_PIX_ABLATE", 0);
-    a.pf2 = env_ll("LDE_PIX_PF2", 0) != 0 ? 1 : 0;
     a.nr = h->pix.nr;
     a.rs = h->pix.rs;
     a.tab = h->d_tab;
@@ -1517,8 +1214,6 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     a.rstart = h->d_prstart;
     a.payload = h->d_ppayload;
     a.unit = h->pix_unit;
-    a.p24 = h->pix24 ? 1 : 0;
-    a.bu = h->pix_bu;
     a.grid = grid;
     a.prev = h->d_pprev;
     a.ovf = h->d_povf;
@@ -1565,24 +1260,18 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
         auto flush = [&]() -> int {
             if (k == 0) return LDE_OK;
             long long g = (n / 16 + 255) / 256;  // 16 events per lane and iteration
-            g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * env_ll("LDE_MON_GRID", 4)));
+            g = std::max<long long>(1, std::min<long long>(g, (long long)h->cus * 4));
             // blocks in ranges proportional to the message sizes, at least one
-            // per message (each block streams one message at its own stride;
-            // LDE_MON_RANGES=0: every block walks all messages, rotated)
-            bool ranges = false;
-            if (env_ll("LDE_MON_RANGES", 1) != 0) {
-                g = std::max<long long>(g, k);
-                ranges = true;
-                long long acc = 0;
-                for (int i = 0; i < k; ++i) {
-                    // first block of message i: i + its share of the other g - k blocks
-                    ka.s[i].chunk0 = i + (long long)((double)(g - k) * (double)acc / (double)n);
-                    acc += ka.s[i].n;
-                }
+            // per message (each block streams one message at its own stride)
+            g = std::max<long long>(g, k);
+            long long acc = 0;
+            for (int i = 0; i < k; ++i) {
+                // first block of message i: i + its share of the other g - k blocks
+                ka.s[i].chunk0 = i + (long long)((double)(g - k) * (double)acc / (double)n);
+                acc += ka.s[i].n;
             }
             Stamp sp(h, LDE_K_MONITOR);
-            HIPCALL(h, lde::launch_monitor(ka, k, h->d_tab, h->tp, h->d_win32, (int)g, h->stream, sp.a, sp.b,
-                                           env_ll("LDE_MON_PF", 0) != 0, ranges));
+            HIPCALL(h, lde::launch_monitor(ka, k, h->d_tab, h->tp, h->d_win32, (int)g, h->stream, sp.a, sp.b));
             sp.done = true;
             k = 0;
             n = 0;
@@ -1617,14 +1306,12 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
     }
     h->last_strategy = strat;
     if (strat == LDE_STRATEGY_ATOMIC) {
-        // one launch per kKargSegsAtomic messages, descriptors as kernel
-        // arguments (LDE_ATOMIC_SEGS: fewer per launch, diagnostics build)
+        // up to kKargSegsAtomic messages: one launch, descriptors as kernel
+        // arguments; more: one launch with per-block descriptors in HBM
         lde::SegKargAtomic ka{};
-        const int seg_cap = (int)std::max<long long>(
-            1, std::min<long long>(lde::kKargSegsAtomic, env_ll("LDE_ATOMIC_SEGS", lde::kKargSegsAtomic)));
         long long n_msgs = 0;
         for (const Segment &s : segs) n_msgs += s.n > 0 ? 1 : 0;
-        if (n_msgs > lde::kKargSegsAtomic && seg_cap == lde::kKargSegsAtomic) {
+        if (n_msgs > lde::kKargSegsAtomic) {
             // more messages than fit the kernel arguments (BIFROST's 630 bank
             // messages of a 14-pulse batch, one push): one launch with a
             // descriptor per block in device memory -- per message
@@ -1689,8 +1376,6 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             if (s.n == 0) continue;
             ka.s[k++] = {s.pid, s.toa, s.n, 0};
             n += s.n;
-            if (k == seg_cap)
-                if (int rc = flush()) return rc;
         }
         return flush();
     }
@@ -1710,15 +1395,17 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             if (rc == LDE_OK) h->last_strategy = LDE_STRATEGY_SPLIT;
             return rc;
         }
-        if (coord_deferred) {  // AUTO fell back to PAGED: the plain coordinate pass
+        // AUTO falls back (or a forced SPLIT batch is too large for its
+        // regions): in wavelength mode the plain coordinate pass first
+        if (coord_deferred)
             if (int rc2 = coord_prepass(h, sd)) return rc2;
-            if (int rc2 = upload_segments(h, sd)) return rc2;
-        }
         if (auto_pixel) {
             h->last_strategy = LDE_STRATEGY_PIXEL;
             return bin_pixel(h, sd, chunks, total, replica);
         }
-        return paged_core(h, h->d_segs, (int)sd.size(), chunks, total, total, lut, nullptr);
+        // (bin_split uploads the descriptors lazily: this batch's may not be)
+        h->last_strategy = LDE_STRATEGY_PAGED;
+        return bin_paged(h, sd, chunks, total, lut);
     }
     if (strat == LDE_STRATEGY_PIXEL) return bin_pixel(h, sd, chunks, total, replica);
     if (strat == LDE_STRATEGY_PAGED) return bin_paged(h, sd, chunks, total, lut);
@@ -1740,7 +1427,6 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
         lde::PartitionArgs pa;
         pa.tile_bits = h->tile_bits;
         pa.lut16 = h->lut16;
-        pa.peel = h->peel;
         pa.segs = h->d_segs + s0;
         pa.n_segs = ns;
         pa.c_begin = c_lo;
@@ -1841,16 +1527,15 @@ struct PixStaged {
 
 int stage_pixel(lde_handle *h, const int32_t *lut, PixStaged &st) {
     st.ok = false;
-    if (h->monitor || h->n_tiles == 0 || env_ll("LDE_PIXEL", 1) == 0) return LDE_OK;
+    if (h->monitor || h->n_tiles == 0 || env_ll("LDE_PIXEL", 1) == 0) return LDE_OK;  // (diagnostics: off)
     const long long L = h->L, R = h->R, S = h->S;
     const int T = h->T;
-    // ranges of 2^rb pixels: the smallest rb with at most 256 ranges
-    // (LDE_PIX_MAX_RANGES, up to kPixMaxRanges; LOKI bank 0: 196 ranges of 4096
-    // pixels; 392 of 2048 keep the same 288-screen widest footprint, so pass B
-    // gains nothing and pass A's runs get shorter; 256 ranges of 3,136 pixels,
-    // one per CU by multiply-high, measured pass B -3.7 us and pass A +19 us)
-    const long long max_nr = std::max<long long>(
-        1, std::min<long long>(lde::kPixMaxRanges - 1, env_ll("LDE_PIX_MAX_RANGES", 256)));
+    // ranges of 2^rb pixels: the smallest rb with at most 256 ranges (LOKI
+    // bank 0: 196 ranges of 4096 pixels; 392 of 2048 keep the same 288-screen
+    // widest footprint, so pass B gains nothing and pass A's runs get shorter;
+    // 256 ranges of 3,136 pixels, one per CU by multiply-high, measured pass B
+    // -3.7 us and pass A +19 us)
+    const long long max_nr = 256;
     int rb = 8;
     while (rb < 20 && ((L + (1LL << rb) - 1) >> rb) > max_nr) ++rb;
     int tbits = 0;
@@ -1923,20 +1608,14 @@ void commit_pixel(lde_handle *h, PixStaged &st) {
     std::swap(h->d_pfp_scr, st.fp_scr);
     h->pixel_ok = st.ok;
     if (!st.ok) return;
-    // partition blocks: 4 x 512 or 2 x 1024 threads per CU (LDS ~36 / ~70 KB each)
-    h->pix_unit = (int)std::max<long long>(1, std::min<long long>(2, env_ll("LDE_PIX_UNIT", 2)));
-    h->pix_ept = h->pix_unit == 2 || env_ll("LDE_PIX_EPT", 8) == 16 ? 16 : 8;
-    h->pix24 = env_ll("LDE_PIX24", 1) != 0;
-    h->pix_bu = env_ll("LDE_PIX_BU", 4) == 8 ? 8 : 4;
-    h->pix_items_per_cu = (int)std::max<long long>(0, std::min<long long>(16, env_ll("LDE_PIX_ITEMS", 0)));
-    // blocks of unit * kChunk / ept threads: 4 x 512 or 2 x 1024 per CU; one
-    // 1024-thread block per CU with predicted slots (half the slots, so
-    // relatively smaller margins: LOKI step 0.529 -> 0.520 ms)
-    h->pix_pred = env_ll("LDE_PIX_PRED", 1) != 0;
-    h->pix_grid = (int)std::max<long long>(
-        1, std::min<long long>(4LL * h->cus,
-                               env_ll("LDE_PIX_GRID", (h->pix_ept == 16 && h->pix_unit == 1 ? 4 : h->pix_pred ? 1 : 2) *
-                                                          (long long)h->cus)));
+    // partition blocks of 1024 threads, one per CU (half the slots of two,
+    // so relatively smaller prediction margins: LOKI step 0.529 -> 0.520 ms);
+    // units of two chunks (16 events per thread), or one (8) when the TOA
+    // table leaves no room for a two-chunk staging area
+    h->pix_unit = 2;
+    // fewer partition blocks (diagnostics: the tests' way to fill the slots
+    // of small batches, so predicted slots are exercised)
+    h->pix_grid = (int)std::max<long long>(1, env_ll("LDE_PIX_GRID", h->cus));
     while (h->pix_unit > 1 && lde::pix_scatter_smem(h->tp, h->pix_unit) > 150 * 1024) --h->pix_unit;
     if (lde::pix_scatter_smem(h->tp, h->pix_unit) > 160 * 1024) {
         h->pixel_ok = false;
@@ -1971,7 +1650,6 @@ int zero_state(lde_handle *h) {
     const size_t nb = (size_t)h->nbins;
     HIPCALL(h, hipMemsetAsync(h->d_win32, 0, nb * 4, h->stream));
     HIPCALL(h, hipMemsetAsync(h->d_cum, 0, nb * 8, h->stream));
-    h->cum_rows_valid = false;
     if (h->d_win64) HIPCALL(h, hipMemsetAsync(h->d_win64, 0, nb * 8, h->stream));
     if (h->d_winf) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
     if (h->d_cumf) HIPCALL(h, hipMemsetAsync(h->d_cumf, 0, nb * 4, h->stream));
@@ -2012,94 +1690,31 @@ void release(lde_handle *h) {
         (void)hipEventDestroy(l.b);
     }
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
-    dev_free(h->d_lut);
-    dev_free(h->d_tab);
-    dev_free(h->d_cbuck);
-    dev_free(h->d_cpd);
-    dev_free(h->d_ctable);
-    dev_free(h->d_cedges);
-    dev_free(h->d_ccq);
-    dev_free(h->d_ccd);
-    dev_free(h->d_cbin);
-    dev_free(h->d_key_dist);
-    dev_free(h->d_key_rec);
-    dev_free(h->d_key_tabi);
-    dev_free(h->d_zero24);
-    dev_free(h->d_ploc);
-    dev_free(h->d_pfp_off);
-    dev_free(h->d_pfp_scr);
-    dev_free(h->d_pcounts);
-    dev_free(h->d_prstart);
-    dev_free(h->d_ppayload);
-    dev_free(h->d_pctab);
-    dev_free(h->d_pitems);
-    dev_free(h->d_pitem_count);
-    dev_free(h->d_pprev);
-    dev_free(h->d_povf);
-    dev_free(h->d_povf_grp);
-    dev_free(h->d_win32);
-    dev_free(h->d_win64);
-    dev_free(h->d_cum);
-    dev_free(h->d_cum_rows);
-    dev_free(h->d_winf);
-    dev_free(h->d_cumf);
-    dev_free(h->d_spid);
-    dev_free(h->d_stoa);
-    if (h->h_ppid) (void)hipHostFree(h->h_ppid);
-    if (h->h_ptoa) (void)hipHostFree(h->h_ptoa);
-    if (h->pin_done) (void)hipEventDestroy(h->pin_done);
-    if (h->ev_s1) (void)hipEventDestroy(h->ev_s1);
-    if (h->ev_s2) (void)hipEventDestroy(h->ev_s2);
-    if (h->stream2) (void)hipStreamDestroy(h->stream2);
-    dev_free(h->d_payload);
-    dev_free(h->d_starts);
-    dev_free(h->d_part);
-    dev_free(h->d_ttot);
-    dev_free(h->d_tile_items);
-    dev_free(h->d_item_count);
-    dev_free(h->d_items);
-    dev_free(h->d_segs);
-    if (h->h_segs) (void)hipHostFree(h->h_segs);
-    if (h->segs_done) (void)hipEventDestroy(h->segs_done);
-    dev_free(h->d_pages);
-    dev_free(h->d_page_tile);
-    dev_free(h->d_page_cnt);
-    dev_free(h->d_list);
-    dev_free(h->d_pool_used);
-    dev_free(h->d_cntp);
-    dev_free(h->d_evp);
-    dev_free(h->d_tile_pages);
-    dev_free(h->d_tile_events);
-    dev_free(h->d_tile_base);
-    dev_free(h->d_overflow);
-    dev_free(h->d_items4);
-    dev_free(h->d_hlut);
-    dev_free(h->d_pix_cnt);
-    dev_free(h->d_pix_tab);
-    dev_free(h->d_glut);
-    dev_free(h->d_sieve_tab);
-    dev_free(h->d_ttab);
-    dev_free(h->d_chunk_tab);
-    dev_free(h->d_sieve_dummy);
-    dev_free(h->d_cold_tcnt);
-    dev_free(h->d_cold_boff);
-    dev_free(h->d_cold_keys);
-    dev_free(h->d_cold_items);
-    dev_free(h->d_cold_ttot);
-    dev_free(h->d_row_screen);
-    dev_free(h->d_sel_stats);
-    dev_free(h->d_sample_part);
-    dev_free(h->d_screen_cnt);
-    dev_free(h->d_screen_row);
-    if (h->h_sel_stats) (void)hipHostFree(h->h_sel_stats);
-    dev_free(h->d_toa_hist);
-    if (h->h_toa_hist) (void)hipHostFree(h->h_toa_hist);
-    if (h->h_screen_cnt) (void)hipHostFree(h->h_screen_cnt);
-    dev_free(h->d_hot_part);
-    dev_free(h->d_cold);
-    dev_free(h->d_cold_cnt);
-    dev_free(h->d_hot_fmt);
-    dev_free(h->d_pair_wraps);
+    for (void *p : {(void *)h->d_lut, (void *)h->d_tab, (void *)h->d_cbuck, (void *)h->d_cpd,
+                    (void *)h->d_ctable, (void *)h->d_cedges, (void *)h->d_cbin, (void *)h->d_key_dist,
+                    (void *)h->d_key_rec, (void *)h->d_key_tabi, (void *)h->d_ploc, (void *)h->d_pfp_off,
+                    (void *)h->d_pfp_scr, (void *)h->d_pcounts, (void *)h->d_prstart, (void *)h->d_ppayload,
+                    (void *)h->d_pctab, (void *)h->d_pitems, (void *)h->d_pitem_count, (void *)h->d_pprev,
+                    (void *)h->d_povf, (void *)h->d_povf_grp, (void *)h->d_win32, (void *)h->d_win64,
+                    (void *)h->d_cum, (void *)h->d_winf, (void *)h->d_cumf, (void *)h->d_spid,
+                    (void *)h->d_stoa, (void *)h->d_payload, (void *)h->d_starts, (void *)h->d_part,
+                    (void *)h->d_ttot, (void *)h->d_tile_items, (void *)h->d_item_count, (void *)h->d_items,
+                    (void *)h->d_segs, (void *)h->d_pages, (void *)h->d_page_tile, (void *)h->d_page_cnt,
+                    (void *)h->d_list, (void *)h->d_pool_used, (void *)h->d_cntp, (void *)h->d_evp,
+                    (void *)h->d_tile_pages, (void *)h->d_tile_events, (void *)h->d_tile_base,
+                    (void *)h->d_overflow, (void *)h->d_items4, (void *)h->d_pix_cnt, (void *)h->d_glut,
+                    (void *)h->d_sieve_tab, (void *)h->d_ttab, (void *)h->d_chunk_tab, (void *)h->d_sieve_dummy,
+                    (void *)h->d_cold_tcnt, (void *)h->d_cold_boff, (void *)h->d_cold_keys,
+                    (void *)h->d_cold_items, (void *)h->d_cold_ttot, (void *)h->d_row_screen,
+                    (void *)h->d_sel_stats, (void *)h->d_sample_part, (void *)h->d_screen_cnt,
+                    (void *)h->d_screen_row, (void *)h->d_hot_part, (void *)h->d_cold, (void *)h->d_cold_cnt,
+                    (void *)h->d_hot_fmt, (void *)h->d_tot4, (void *)h->d_snap})
+        if (p) (void)hipFree(p);
+    for (void *p : {(void *)h->h_ppid, (void *)h->h_ptoa, (void *)h->h_segs, (void *)h->h_sel_stats,
+                    (void *)h->h_pack})
+        if (p) (void)hipHostFree(p);
+    for (hipEvent_t e : {h->pin_done, h->segs_done, h->fin_event, h->block_event})
+        if (e) (void)hipEventDestroy(e);
     if (h->d_trace && !h->trace_stats.empty()) {
         const size_t n = h->trace_stats.size() / 4;
         double a[4] = {0, 0, 0, 0};
@@ -2111,21 +1726,6 @@ void release(lde_handle *h) {
                 n, a[0] / n, a[1] / n, a[2] / n, a[3] / n);
     }
     dev_free(h->d_trace);
-    dev_free(h->d_cold_segs);
-    dev_free(h->d_cold_chunks);
-    dev_free(h->d_dummy);
-    dev_free(h->d_tot4);
-    dev_free(h->d_pack);
-    if (h->h_pack) (void)hipHostFree(h->h_pack);
-    h->h_pack = nullptr;
-    h->hd_pack = nullptr;
-    if (h->fin_event) (void)hipEventDestroy(h->fin_event);
-    h->fin_event = nullptr;
-    if (h->ready_event) (void)hipEventDestroy(h->ready_event);
-    h->ready_event = nullptr;
-    if (h->block_event) (void)hipEventDestroy(h->block_event);
-    h->block_event = nullptr;
-    dev_free(h->d_snap);
     for (auto &g : h->groups) {
         dev_free(g.d_items);
         dev_free(g.d_screens);
@@ -2300,7 +1900,6 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     }
     CREATE_CHECK(dev_alloc(h, &h->d_tab, tab.size()));
     CREATE_HIP(hipMemcpy(h->d_tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
-    h->peel = env_ll("LDE_PEEL", 0) != 0;
 
     // histograms
     CREATE_CHECK(dev_alloc(h, &h->d_win32, (size_t)nbins));
@@ -2311,27 +1910,19 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         CREATE_CHECK(ensure_win64(h));
     }
     CREATE_CHECK(dev_alloc(h, &h->d_tot4, 4 + 4 * 8192));  // totals + per-block partials
+    // the finalize pack in coherent host memory the finalize kernel writes:
     // [current image S x 8][cumulative image S x 8][totals 32][overflow 16]
     // [per-block total partials, kHostPartials x 32] (summed on the host)
     h->pack_bytes = (size_t)h->S * 16 + 48 + 32 * (size_t)lde::kHostPartials;
-    CREATE_CHECK(dev_alloc(h, &h->d_pack, h->pack_bytes));
-    if (env_ll("LDE_FINALIZE_MAPPED", 1) != 0) {
-        CREATE_HIP(hipHostMalloc((void **)&h->h_pack, h->pack_bytes, hipHostMallocCoherent));
-        CREATE_HIP(hipHostGetDevicePointer((void **)&h->hd_pack, h->h_pack, 0));
-        CREATE_HIP(hipEventCreateWithFlags(&h->fin_event, hipEventDisableTiming));
-    } else {
-        CREATE_HIP(hipHostMalloc((void **)&h->h_pack, h->pack_bytes, hipHostMallocDefault));
-    }
-    CREATE_HIP(hipEventCreateWithFlags(&h->ready_event, hipEventDisableTiming | hipEventBlockingSync));
-    h->fin_split = (int)env_ll("LDE_FIN_SPLIT", 0);  // measured +6.5 us per DREAM step: off
-    h->d_img_cur = h->d_pack;
-    h->d_img_cum = h->d_pack + (size_t)h->S * 8;
+    CREATE_HIP(hipHostMalloc((void **)&h->h_pack, h->pack_bytes, hipHostMallocCoherent));
+    CREATE_HIP(hipHostGetDevicePointer((void **)&h->hd_pack, h->h_pack, 0));
+    CREATE_HIP(hipEventCreateWithFlags(&h->fin_event, hipEventDisableTiming));
     CREATE_CHECK(zero_state(h));
 
-    // partition workspace: choose the smallest tile that keeps <= kMaxTiles tiles
+    // partition workspace: tiles of 2^14 bins, or 2^15 when that keeps the
+    // tiles <= kMaxTiles and the PAGED pass-A carve within its LDS
     if (!monitor) {
-        int tb = (int)env_ll("LDE_TILE_BITS", 14);
-        tb = std::max(13, std::min(tb, 15));
+        int tb = (int)std::max<long long>(14, std::min<long long>(15, env_ll("LDE_TILE_BITS", 14)));
         auto tiles = [&](int b) { return (nbins + (1LL << b) - 1) >> b; };
         while (tb < 15 && (tiles(tb) > lde::kMaxTiles ||
                            lde::paged_smem((int)std::min<long long>(tiles(tb), lde::kMaxTiles), 1,
@@ -2341,8 +1932,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         const bool smem_ok = nt <= lde::kMaxTiles &&
                              lde::partition_smem((int)nt, h->tp) <= 64 * 1024 &&
                              lde::paged_smem((int)nt, 1, h->tp) <= lde::kPagedSmemMax;
-        h->subc = (env_ll("LDE_SUBC", 4) == 4 && smem_ok &&
-                   lde::paged_smem((int)nt, 4, h->tp) <= lde::kPagedSmemMax) ? 4 : 1;
+        h->subc = (smem_ok && lde::paged_smem((int)nt, 4, h->tp) <= lde::kPagedSmemMax) ? 4 : 1;
         if (nt <= lde::kMaxTiles && smem_ok) {
             h->tile_bits = tb;
             h->n_tiles = (int)nt;
@@ -2356,186 +1946,91 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         } else {
             h->n_tiles = 0;  // partition unavailable -> atomic strategy
         }
-        // SPLIT: needs the paged path for its cold keys and the sampled screen
-        // histogram in LDS; the pixel cache needs tag + row + screen <= 31 bits
-        if (h->n_tiles > 0 && h->S * 4 <= 160 * 1024 && env_ll("LDE_SPLIT", 1) != 0) {
-            auto bits = [](long long n) { int b = 0; while ((1LL << b) < n) ++b; return b; };
-            int cbits = (int)std::max<long long>(0, std::min<long long>(16, env_ll("LDE_PIXEL_CACHE_BITS", 13)));
-            if ((1LL << cbits) >= 2 * h->L) cbits = std::max(0, bits(h->L));  // whole LUT fits
-            // LDS budget per split block: 160 KB = one block per CU; 80 KB = two
-            const size_t budget = (size_t)std::max<long long>(32, std::min<long long>(160, env_ll("LDE_SPLIT_SMEM_KB", 160))) * 1024;
+        // SPLIT (the SIEVE pass): needs the LDS pixel table, the fast TOA
+        // layout with T <= 254, keys below 2^22, table tags below 255 and a
+        // tile-sorted cold pipeline of <= kSortThreads tiles; its LDS carve
+        // bounds the hot rows
+        auto bits = [](long long n) { int b = 0; while ((1LL << b) < n) ++b; return b; };
+        int cbits = (int)std::max<long long>(0, std::min<long long>(16, env_ll("LDE_PIXEL_CACHE_BITS", 13)));
+        if ((1LL << cbits) >= 2 * h->L) cbits = std::max(0, bits(h->L));  // whole LUT fits
+        std::vector<uint32_t> tt;
+        int tsh = 0;
+        uint32_t tcap = 0;
+        const size_t budget = lde::kSplitSmemMax;
+        if (h->n_tiles > 0 && h->n_tiles <= lde::kSortThreadsHost && h->S * 4 <= 160 * 1024 && cbits > 0 &&
+            env_ll("LDE_SPLIT", 1) != 0 && build_sieve_toa(h->tp, tab, tt, tsh, tcap) &&
+            (unsigned long long)h->S * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL &&
+            ((h->L - 1) >> cbits) < 255 && h->L < 0x3fffffffLL) {
+            // room for the integer-edge table of wavelength mode (edges 0..T:
+            // T + 1 bucket words), so lde_set_coord_lut keeps the sieve
+            if (tt.size() < (size_t)lde::align4(h->T + 2)) tt.resize((size_t)lde::align4(h->T + 2), 0u);
             auto rows_for = [&](int cb) {
-                const size_t fixed = lde::split_smem(0, cb ? (1 << cb) : 0, h->tp);
+                const size_t fixed = lde::sieve_smem(0, cb, (int)tt.size(), h->n_tiles);
                 int H = 0;
                 if (fixed < budget)
                     H = (int)std::min<long long>(lde::kHotMaxRows, (long long)((budget - fixed) / (4 * (size_t)h->T)));
-                while (H > 0 && lde::split_smem(lde::align4(H * h->T), cb ? (1 << cb) : 0, h->tp) > budget) --H;
-                return H;
+                while (H > 0 && lde::sieve_smem((H * h->T + 7) & ~7, cb, (int)tt.size(), h->n_tiles) > budget) --H;
+                return (int)std::min<long long>(H, h->S);
             };
-            // the cache never takes the room of the last 64 hot rows
+            // the pixel table never takes the room of the last 64 hot rows
             while (cbits > 8 && rows_for(cbits) < std::min<long long>(64, h->S)) --cbits;
             // views with few screens (DREAM strip_view: 256): a smaller pixel
             // table (down to 2^10 slots) when it makes room for a hot row per
             // screen, so that no event is cold and the cold-key pipeline never
-            // runs (the table's misses cost a gather; a cold key a sort and a
-            // second pass)
-            {
-                std::vector<uint32_t> tt0;
-                int tsh0 = 0;
-                uint32_t tcap0 = 0;
-                bool log0 = false;
-                if (h->S <= lde::kHotMaxRows && build_sieve_toa(h->tp, tab, tt0, tsh0, tcap0, &log0)) {
-                    if (tt0.size() < (size_t)lde::align4(h->T + 2)) tt0.resize((size_t)lde::align4(h->T + 2), 0u);
-                    auto sieve_fits_all = [&](int cb) {
-                        return lde::sieve_smem(lde::align4((int)h->S * h->T), cb, (int)tt0.size(), h->n_tiles, 0) <= budget;
-                    };
-                    if (cbits > 0 && !sieve_fits_all(cbits) && env_ll("LDE_ALL_HOT", 1) != 0)
-                        for (int cb = cbits - 1; cb >= 10; --cb)
-                            if (sieve_fits_all(cb)) {
-                                cbits = cb;
-                                break;
-                            }
-                }
-            }
-            int H = rows_for(cbits);
-            H = (int)std::min<long long>(H, h->S);
-            const long long hmax = env_ll("LDE_HOT_ROWS", 0);
-            if (hmax > 0) H = (int)std::min<long long>(H, hmax);
-            h->row_bits = bits(H + 2);
-            h->screen_bits = std::max(1, bits(h->S));
-            const int tag_bits = std::max(0, bits(h->L) - cbits);
-            if (cbits > 0 && tag_bits + h->row_bits + h->screen_bits > 31) cbits = 0;
-            h->cache_bits = cbits;
-            // SIEVE: needs the pixel table, the fast TOA layout with T <= 254,
-            // keys below 2^22 and table tags below 255; its LDS carve bounds H
-            {
-                std::vector<uint32_t> tt;
-                int tsh = 0;
-                uint32_t tcap = 0;
-                bool tlog = false;
-                if (cbits > 0 && env_ll("LDE_SIEVE", 1) != 0 && build_sieve_toa(h->tp, tab, tt, tsh, tcap, &tlog) &&
-                    (unsigned long long)h->S * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL &&
-                    ((h->L - 1) >> cbits) < 255 && h->L < 0x3fffffffLL) {
-                    // room for the integer-edge table of wavelength mode (edges
-                    // 0..T: T + 1 bucket words), so lde_set_coord_lut keeps the sieve
-                    if (tt.size() < (size_t)lde::align4(h->T + 2)) tt.resize((size_t)lde::align4(h->T + 2), 0u);
-                    int Hs = 0;
-                    // whole rows: no row -> screen table (sieve_smem's last argument)
-                    const size_t fixed = lde::sieve_smem(0, cbits, (int)tt.size(), h->n_tiles, 0);
-                    if (fixed < budget)
-                        Hs = (int)std::min<long long>(lde::kHotMaxRows, (long long)((budget - fixed) / (4 * (size_t)h->T)));
-                    while (Hs > 0 && lde::sieve_smem(lde::align4(Hs * h->T), cbits, (int)tt.size(), h->n_tiles, 0) > budget) --Hs;
-                    Hs = (int)std::min<long long>(Hs, h->S);
-                    if (hmax > 0) Hs = (int)std::min<long long>(Hs, hmax);
-                    if (Hs >= 8 && (unsigned long long)Hs * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL) {
-                        h->sieve_ok = true;
-                        // u16 pairs: 2 bytes per counter (T even: a row is whole words)
-                        int Hp = 0;
-                        if (h->T % 2 == 0 && env_ll("LDE_HOT_PAIR", 0) != 0) {
-                            auto fits_p = [&](int n) {
-                                return lde::sieve_smem(((n * h->T + 15) & ~15) / 2, cbits, (int)tt.size(), h->n_tiles,
-                                                       0) <= budget;
-                            };
-                            Hp = (int)std::min<long long>(lde::kHotMaxRows, h->S);
-                            if (hmax > 0) Hp = (int)std::min<long long>(Hp, hmax);
-                            while (Hp > 0 && !fits_p(Hp)) --Hp;
-                            if ((unsigned long long)Hp * h->T > (unsigned long long)lde::kSieveValueMask + 1ULL)
-                                Hp = 0;
-                            // the split path's hot LUT packs rows into row_bits
-                            const int rb = bits(Hp + 2);
-                            if (cbits > 0 && tag_bits + rb + h->screen_bits > 31) Hp = 0;
-                            if (Hp > std::min(H, Hs)) h->row_bits = std::max(h->row_bits, rb);
-                        }
-                        h->hot_rows_pair = Hp > std::min(H, Hs) ? Hp : 0;
-                        H = std::min(H, Hs);
-                        h->ttab = std::move(tt);
-                        h->ttab_shift = tsh;
-                        h->ttab_cap = tcap;
-                        h->ttab_log = tlog;
+            // runs (a table miss costs a gather; a cold key a sort and a pass)
+            if (h->S <= lde::kHotMaxRows && rows_for(cbits) < h->S)
+                for (int cb = cbits - 1; cb >= 10; --cb)
+                    if (rows_for(cb) >= h->S) {
+                        cbits = cb;
+                        break;
                     }
-                }
-            }
-            if (H >= 8) {
+            int H = rows_for(cbits);
+            const long long hmax = env_ll("LDE_HOT_ROWS", 0);  // diagnostics: a row budget
+            if (hmax > 0) H = (int)std::min<long long>(H, hmax);
+            if (H >= 8 && (unsigned long long)H * h->T <= (unsigned long long)lde::kSieveValueMask + 1ULL &&
+                ((h->L - 1) >> cbits) < 255) {
                 h->split_ok = true;
                 h->hot_rows = H;
-                h->split_grid = (int)std::max<long long>(
-                    1, env_ll("LDE_SPLIT_GRID", (long long)h->cus * (long long)std::max<size_t>(1, (160 * 1024) / budget)));
-                h->hot_refresh = (int)std::max<long long>(1, env_ll("LDE_HOT_REFRESH", 256));
-                h->split_min_cov = (double)env_ll("LDE_SPLIT_MIN_COV_PCT", 30) / 100.0;
-                h->hot_uses.assign((size_t)h->R, -1);
-                h->hot_cov.assign((size_t)h->R, 0.0);
-                h->all_hot.assign((size_t)h->R, 0);
-                h->hot_h.assign((size_t)h->R, H);
-                h->hot_w.assign((size_t)h->R, h->T);
-                h->hot_lo.assign((size_t)h->R, 0);
-                h->hot_win.assign((size_t)h->R, 1.0);
-                h->hot_pairsel.assign((size_t)h->R, 0);
-                h->sieve_budget = budget;
-                CREATE_CHECK(dev_alloc(h, &h->d_hlut, (size_t)h->R * h->L));
-                if (cbits > 0) {
-                    CREATE_CHECK(dev_alloc(h, &h->d_pix_cnt, (size_t)h->L));
-                    CREATE_CHECK(dev_alloc(h, &h->d_pix_tab, (size_t)h->R << cbits));
-                }
-                if (h->sieve_ok) {
-                    CREATE_CHECK(dev_alloc(h, &h->d_glut, (size_t)h->R * (size_t)(h->L + 1)));
-                    CREATE_CHECK(dev_alloc(h, &h->d_sieve_tab, (size_t)h->R << cbits));
-                    CREATE_CHECK(dev_alloc(h, &h->d_ttab, h->ttab.size()));
-                    CREATE_HIP(hipMemcpy(h->d_ttab, h->ttab.data(), h->ttab.size() * 4, hipMemcpyHostToDevice));
-                    std::vector<int> dum((size_t)lde::kChunk, (int)((unsigned)h->pid_off - 1u));
-                    CREATE_CHECK(dev_alloc(h, &h->d_sieve_dummy, dum.size()));
-                    CREATE_CHECK(dev_alloc(h, &h->d_cold_ttot, (size_t)h->n_tiles));
-                    CREATE_HIP(hipMemcpy(h->d_sieve_dummy, dum.data(), dum.size() * 4, hipMemcpyHostToDevice));
-                }
-                CREATE_CHECK(dev_alloc(h, &h->d_row_screen, (size_t)h->R * lde::kHotMaxRows));
-                CREATE_CHECK(dev_alloc(h, &h->d_sel_stats, (size_t)h->R * 4));
-                CREATE_CHECK(dev_alloc(h, &h->d_sample_part, (size_t)lde::kSampleBlocks * h->S));
-                CREATE_CHECK(dev_alloc(h, &h->d_screen_cnt, (size_t)h->S));
-                CREATE_CHECK(dev_alloc(h, &h->d_screen_row, (size_t)h->S));
-                CREATE_CHECK(dev_alloc(h, &h->d_cold_cnt, (size_t)h->split_grid * (lde::kSplitThreads / 64)));  // SIEVE: per wave
-                if (env_ll("LDE_SIEVE_TRACE", 0) != 0) {
-                    CREATE_CHECK(dev_alloc(h, &h->d_trace, (size_t)h->split_grid * 3));
-                }
-                if (env_ll("LDE_HOT16", 1) != 0) {
-                    CREATE_CHECK(dev_alloc(h, &h->d_hot_fmt, (size_t)h->split_grid));
-                }
-                if (h->hot_rows_pair > 0) {
-                    CREATE_CHECK(dev_alloc(h, &h->d_pair_wraps, 1));
-                    CREATE_HIP(hipMemset(h->d_pair_wraps, 0, 4));
-                }
-                CREATE_CHECK(dev_alloc(h, &h->d_cold_segs, (size_t)h->split_grid));
-                CREATE_CHECK(dev_alloc(h, &h->d_cold_chunks, 1));
-                CREATE_CHECK(dev_alloc(h, &h->d_dummy, 16));
-                CREATE_HIP(hipMemset(h->d_dummy, 0, 64));
-                CREATE_HIP(hipHostMalloc((void **)&h->h_sel_stats, (size_t)h->R * 16, hipHostMallocDefault));
-                if (h->sieve_ok) {  // the sample the TOA window is chosen from
-                    CREATE_CHECK(dev_alloc(h, &h->d_toa_hist, (size_t)h->T));
-                    CREATE_HIP(hipHostMalloc((void **)&h->h_toa_hist, (size_t)h->T * 4, hipHostMallocDefault));
-                    CREATE_HIP(hipHostMalloc((void **)&h->h_screen_cnt, (size_t)h->S * 4, hipHostMallocDefault));
-                }
+                h->cache_bits = cbits;
+                h->ttab = std::move(tt);
+                h->ttab_shift = tsh;
+                h->ttab_cap = tcap;
             }
         }
-        h->lds_ctab = env_ll("LDE_LDS_CTAB", 1) != 0;
-        h->karg_segs = env_ll("LDE_KARG_SEGS", 1) != 0;
+        if (h->split_ok) {
+            h->split_grid = (int)std::max<long long>(1, env_ll("LDE_SPLIT_GRID", (long long)h->cus));
+            h->hot_refresh = (int)std::max<long long>(1, env_ll("LDE_HOT_REFRESH", 256));
+            h->split_min_cov = (double)env_ll("LDE_SPLIT_MIN_COV_PCT", 30) / 100.0;
+            h->hot_uses.assign((size_t)h->R, -1);
+            h->hot_cov.assign((size_t)h->R, 0.0);
+            h->all_hot.assign((size_t)h->R, 0);
+            const int cbits2 = h->cache_bits;
+            CREATE_CHECK(dev_alloc(h, &h->d_pix_cnt, (size_t)h->L));
+            CREATE_CHECK(dev_alloc(h, &h->d_glut, (size_t)h->R * (size_t)(h->L + 1)));
+            CREATE_CHECK(dev_alloc(h, &h->d_sieve_tab, (size_t)h->R << cbits2));
+            CREATE_CHECK(dev_alloc(h, &h->d_ttab, h->ttab.size()));
+            CREATE_HIP(hipMemcpy(h->d_ttab, h->ttab.data(), h->ttab.size() * 4, hipMemcpyHostToDevice));
+            std::vector<int> dum((size_t)lde::kChunk, (int)((unsigned)h->pid_off - 1u));
+            CREATE_CHECK(dev_alloc(h, &h->d_sieve_dummy, dum.size()));
+            CREATE_HIP(hipMemcpy(h->d_sieve_dummy, dum.data(), dum.size() * 4, hipMemcpyHostToDevice));
+            CREATE_CHECK(dev_alloc(h, &h->d_cold_ttot, (size_t)h->n_tiles));
+            CREATE_CHECK(dev_alloc(h, &h->d_row_screen, (size_t)h->R * lde::kHotMaxRows));
+            CREATE_CHECK(dev_alloc(h, &h->d_sel_stats, (size_t)h->R * 4));
+            CREATE_CHECK(dev_alloc(h, &h->d_sample_part, (size_t)lde::kSampleBlocks * h->S));
+            CREATE_CHECK(dev_alloc(h, &h->d_screen_cnt, (size_t)h->S));
+            CREATE_CHECK(dev_alloc(h, &h->d_screen_row, (size_t)h->S));
+            CREATE_CHECK(dev_alloc(h, &h->d_cold_cnt, (size_t)h->split_grid * (lde::kSplitThreads / 64)));
+            CREATE_CHECK(dev_alloc(h, &h->d_hot_fmt, (size_t)h->split_grid));
+            if (env_ll("LDE_SIEVE_TRACE", 0) != 0)
+                CREATE_CHECK(dev_alloc(h, &h->d_trace, (size_t)h->split_grid * 3));
+            CREATE_HIP(hipHostMalloc((void **)&h->h_sel_stats, (size_t)h->R * 16, hipHostMallocDefault));
+        }
 #ifdef LDE_DIAGNOSTICS
         h->sieve_ablate = (int)env_ll("LDE_SIEVE_ABLATE", 0);
         h->cold_sort_ablate = (int)env_ll("LDE_COLD_SORT_ABLATE", 0);
 #endif
-        // exact variant: cold-key stores deferred behind the next gathers
-        if (env_ll("LDE_DEFER_STORES", 0) != 0) h->sieve_ablate |= 2048;
-        h->coord_keyed = env_ll("LDE_COORD_KEYED", 1) != 0;
-        h->early_gather = env_ll("LDE_EARLY_GATHER", 0) != 0;
         h->probe = env_ll("LDE_HOST_PROBE", 0) != 0;
-        h->sieve_pack = env_ll("LDE_SIEVE_PACK", 0) != 0;
-        h->cold_sort_mode = (int)env_ll("LDE_COLD_SORT", 2);
-        {
-            const long long k = env_ll("LDE_COLD_SORT_KPT", 48);
-            h->cold_sort_kpt = k == 16 ? 16 : k == 32 ? 32 : 48;
-        }
-        h->key24 = env_ll("LDE_KEY24", 1) != 0;
-        h->tail_release = (int)env_ll("LDE_TAIL_RELEASE", 1);
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
-        h->atomic_threshold = env_ll("LDE_ATOMIC_THRESHOLD", -1);
-        h->auto_partition = (int)env_ll("LDE_AUTO_PARTITION", LDE_STRATEGY_PAGED);
     }
     if (!monitor) CREATE_CHECK(build_pixel(h, cfg->out_lut));
     CREATE_HIP(hipEventCreateWithFlags(&h->pin_done, hipEventDisableTiming));
@@ -2577,23 +2072,11 @@ int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n) 
     // into the pinned ring and queue its H2D right away, so the host copies
     // run in parallel and overlap the PCIe transfers of earlier chunks.  The
     // single-thread memcpy, not PCIe, bounded the end-to-end rate.
-    const long long chunk = std::max<long long>(1 << 18, env_ll("LDE_STAGE_CHUNK", 1 << 20));
+    const long long chunk = 1 << 20;
     const int arrays = h->monitor ? 1 : 2;
     const long long n_chunks = (n + chunk - 1) / chunk;
     const int workers = (int)std::min<long long>(
         std::max<long long>(1, env_ll("LDE_STAGE_THREADS", 8)), n_chunks * arrays);
-    // two copy streams: odd chunks go on stream2, which first waits for the
-    // handle's stream (the previous batch's kernels may still read the ring)
-    const bool two = n_chunks * arrays > 1 && env_ll("LDE_STAGE_STREAMS", 1) > 1;
-    if (two) {
-        if (!h->stream2) {
-            HIPCALL(h, hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
-            HIPCALL(h, hipEventCreateWithFlags(&h->ev_s1, hipEventDisableTiming));
-            HIPCALL(h, hipEventCreateWithFlags(&h->ev_s2, hipEventDisableTiming));
-        }
-        HIPCALL(h, hipEventRecord(h->ev_s1, h->stream));
-        HIPCALL(h, hipStreamWaitEvent(h->stream2, h->ev_s1, 0));
-    }
     auto copy_chunk = [&](long long item) -> hipError_t {
         const int a = (int)(item % arrays);
         const long long c0 = (item / arrays) * chunk;
@@ -2602,8 +2085,7 @@ int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n) 
         int *dp = (a == 0 ? h->d_stoa : h->d_spid) + off + c0;
         const int32_t *src = (a == 0 ? toa : pid) + c0;
         std::memcpy(hp, src, (size_t)cn * 4);
-        return hipMemcpyAsync(dp, hp, (size_t)cn * 4, hipMemcpyHostToDevice,
-                              (two && ((item / arrays) & 1)) ? h->stream2 : h->stream);
+        return hipMemcpyAsync(dp, hp, (size_t)cn * 4, hipMemcpyHostToDevice, h->stream);
     };
     if (workers <= 1) {
         for (long long it = 0; it < n_chunks * arrays; ++it) HIPCALL(h, copy_chunk(it));
@@ -2623,10 +2105,6 @@ int lde_stage(lde_handle *h, const int32_t *pid, const int32_t *toa, int64_t n) 
         work();
         for (auto &t : pool) t.join();
         HIPCALL(h, (hipError_t)err.load());
-    }
-    if (two) {
-        HIPCALL(h, hipEventRecord(h->ev_s2, h->stream2));
-        HIPCALL(h, hipStreamWaitEvent(h->stream, h->ev_s2, 0));
     }
     HIPCALL(h, hipEventRecord(h->pin_done, h->stream));
     h->pin_pending = true;
@@ -2860,25 +2338,22 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
     const bool want_cum_hist = out->cumulative_hist != nullptr;
     if (want_cur_hist && !f32 && !h->d_snap)
         if (int rc = dev_alloc(h, &h->d_snap, nb)) return rc;
-    // outputs go straight into the host-mapped pack, or into d_pack and one copy
-    unsigned char *pk = h->hd_pack ? h->hd_pack : h->d_pack;
+    // outputs go straight into the host-mapped pack, images into the caller's
+    // lde_host_alloc memory in place when they live there
+    unsigned char *pk = h->hd_pack;
     void *img_cur = pk, *img_cum = pk + (size_t)h->S * 8;
-    // images into lde_host_alloc memory are written by the kernel in place
     const size_t img_bytes = (size_t)h->S * (f32 ? 4 : 8);
     void *const map_cur = mapped_device_ptr(out->current_image, img_bytes);
     void *const map_cum = mapped_device_ptr(out->cumulative_image, img_bytes);
     if (map_cur) img_cur = map_cur;
     if (map_cum) img_cum = map_cum;
     int n_parts = 0;
-    // split finalize: the host waits only for the images and totals (the
-    // window's rows); the window's fold into the cumulative histogram runs
-    // behind the ready event, while the host turns around
-    const bool split = !f32 && !want_cur_hist && !want_cum_hist && h->fin_split &&
-                       lde::finalize_split_ok(h->T);
+    // the per-block total partials and the overflow flag land in the pack
+    // (summed here on the host: no k_sum_totals launch and gap)
+    unsigned char *d_tail = pk + (size_t)h->S * 16;
     if (f32) {
         // one pass: the pending push's f32 adds, images, exact totals and
         // cumulative, window reset (k_finalize_f32)
-        unsigned char *d_tail = pk + (size_t)h->S * 16;
         float *snap = nullptr;
         if (want_cur_hist) {
             if (!h->d_snap)
@@ -2901,38 +2376,8 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
         if (want_cum_hist)
             HIPCALL(h, hipMemcpyAsync(out->cumulative_hist, h->d_cumf, nb * 4, hipMemcpyDeviceToHost,
                                       h->stream));
-    } else if (split) {
-        unsigned char *d_tail = pk + (size_t)h->S * 16;
-        if (!h->d_cum_rows)
-            if (int rc = dev_alloc(h, &h->d_cum_rows, 2 * (size_t)h->S)) return rc;
-        if (!h->cum_rows_valid) {
-            HIPCALL(h, lde::launch_cum_rows(h->d_cum, h->S, h->T, h->range_lo, h->range_hi, h->d_cum_rows,
-                                            h->stream));
-            h->cum_rows_valid = true;
-        }
-        {
-            Stamp sp(h, LDE_K_FINALIZE);
-            HIPCALL(h, lde::launch_finalize_rows(
-                           0, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum_rows, h->S, h->T,
-                           h->range_lo, h->range_hi, out->current_image ? img_cur : nullptr,
-                           out->cumulative_image ? img_cum : nullptr, h->d_overflow,
-                           (uint32_t *)(d_tail + 32), (unsigned long long *)(d_tail + 48), &n_parts,
-                           h->stream, sp.a, sp.b));
-            sp.done = true;
-        }
-        if (!h->hd_pack)
-            HIPCALL(h, hipMemcpyAsync(h->h_pack, h->d_pack, (size_t)h->S * 16 + 48 + 32 * (size_t)n_parts,
-                                      hipMemcpyDeviceToHost, h->stream));
-        HIPCALL(h, hipEventRecord(h->ready_event, h->stream));
-        HIPCALL(h, lde::launch_fold_cumulative(h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
-                                               h->nbins, h->stream));
-        HIPCALL(h, wait_stream(h, h->ready_event));
     } else {
-        h->cum_rows_valid = false;
         Timed tm(h, LDE_K_FINALIZE);
-        // the per-block total partials and the overflow flag land in the
-        // pack (summed here on the host: no k_sum_totals launch and gap)
-        unsigned char *d_tail = pk + (size_t)h->S * 16;
         HIPCALL(h, lde::launch_finalize(
                        0, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr, h->d_cum,
                        want_cur_hist ? h->d_snap : nullptr, h->S, h->T, h->range_lo,
@@ -2942,18 +2387,9 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
                        h->stream, (unsigned long long *)(d_tail + 48), &n_parts));
     }
     const size_t isz = f32 ? 4 : 8;
-    if (split) {
-        // waited above
-    } else if (h->hd_pack) {
-        // a system-scope release after the kernel: its host writes are visible
-        // once the stream has passed this point
-        HIPCALL(h, hipEventRecord(h->fin_event, h->stream));
-    } else {
-        // images, partials and the overflow flag leave in one pinned D2H copy
-        // (separate copies into pageable memory cost ~25 us each)
-        HIPCALL(h, hipMemcpyAsync(h->h_pack, h->d_pack, (size_t)h->S * 16 + 48 + 32 * (size_t)n_parts,
-                                  hipMemcpyDeviceToHost, h->stream));
-    }
+    // a system-scope release after the kernel: its host writes are visible
+    // once the stream has passed this point
+    HIPCALL(h, hipEventRecord(h->fin_event, h->stream));
     std::vector<unsigned long long> tmp;
     if (!f32 && (want_cur_hist || want_cum_hist)) tmp.resize(nb);
     if (!f32 && want_cur_hist) {
@@ -2966,7 +2402,7 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
         HIPCALL(h, hipStreamSynchronize(h->stream));
         convert_u64(tmp.data(), out->cumulative_hist, (long long)nb, LDE_F64);
     }
-    if (!split) HIPCALL(h, wait_stream(h));
+    HIPCALL(h, wait_stream(h));
     const auto t_waited = h->probe ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
     struct PostProbe {
         lde_handle *h;
@@ -3010,7 +2446,6 @@ int lde_finalize_partials(lde_handle *h, void *d_out) {
                                         h->d_cum, nullptr, h->S, h->T, h->range_lo, h->range_hi,
                                         o, o + h->S, h->d_tot4, o + 2 * h->S, nullptr, nullptr,
                                         h->stream));
-        h->cum_rows_valid = false;
     }
     if (h->out_dtype == LDE_F32)  // the window's f32 accumulator restarts too
         HIPCALL(h, hipMemsetAsync(h->d_winf, 0, (size_t)h->nbins * 4, h->stream));
@@ -3255,8 +2690,7 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     std::vector<uint32_t> tt;
     int tsh = 0;
     uint32_t tcap = 0;
-    bool tlog = false;
-    bool sieve_fits = h->sieve_ok;
+    bool sieve_fits = h->split_ok;
     if (!rebind) {
         // the binning stage now sees integer bins: edges 0..T
         std::vector<double> idx((size_t)T + 1);
@@ -3265,8 +2699,8 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
         if (int rc = build_toa_tables(h, idx.data(), T, tab, tp)) return rc;
         if (int rc = dev_alloc(h, &st.tab, tab.size())) return rc;
         HIPCALL(h, hipMemcpy(st.tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
-        if (h->sieve_ok) {
-            sieve_fits = build_sieve_toa(tp, tab, tt, tsh, tcap, &tlog) && tt.size() <= h->ttab.size();
+        if (h->split_ok) {
+            sieve_fits = build_sieve_toa(tp, tab, tt, tsh, tcap) && tt.size() <= h->ttab.size();
             if (sieve_fits) {
                 if (int rc = dev_alloc(h, &st.ttab, h->ttab.size())) return rc;
                 HIPCALL(h, hipMemcpy(st.ttab, tt.data(), tt.size() * 4, hipMemcpyHostToDevice));
@@ -3302,6 +2736,7 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
         if (!(x < ed[(size_t)T])) return T - 1;
         return std::max(0, (int)(std::upper_bound(ed.begin(), ed.end(), x) - ed.begin()) - 1);
     };
+    // LDE_COORD_FIXED_BIN=0 (diagnostics): the general bin search, for tests
     bool fixed_bin = span > 0 && std::isfinite(span) && env_ll("LDE_COORD_FIXED_BIN", 1) != 0;
     for (int g = 0; g < G && fixed_bin; ++g) {
         const int lo_b = bin_of(ed[0] + (g - 1) * w), hi_b = bin_of(ed[0] + (g + 2) * w);
@@ -3316,24 +2751,17 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     HIPCALL(h, hipMemcpy(st.ctable, lut->table, nt * 8, hipMemcpyHostToDevice));
     HIPCALL(h, hipMemcpy(st.cedges, ed.data(), ((size_t)T + 1) * 8, hipMemcpyHostToDevice));
     HIPCALL(h, hipMemcpy(st.cbuck, buck.data(), (size_t)G * 2, hipMemcpyHostToDevice));
-    // the distance cache follows the pixel distances: rebuilt from the last
-    // sampled pixel counts (into the existing cache buffers, from the new
-    // distances), else off until the next hot-set selection
-    if (h->coord_cache_built)
-        HIPCALL(h, lde::launch_coord_cache(h->d_pix_cnt, st.cpd, h->L, lde::kCoordCacheBits,
-                                           h->d_ccq, h->d_ccd, h->stream));
     // ---- commit (no failure past this point)
     if (!rebind) {
         std::swap(h->d_tab, st.tab);
         h->tp = tp;
-        if (h->sieve_ok && sieve_fits) {
+        if (h->split_ok && sieve_fits) {
             std::swap(h->d_ttab, st.ttab);
             h->ttab = std::move(tt);
             h->ttab_shift = tsh;
             h->ttab_cap = tcap;
-            h->ttab_log = tlog;
         } else {
-            h->sieve_ok = false;
+            h->split_ok = false;
         }
     }
     std::swap(h->d_cpd, st.cpd);
@@ -3359,14 +2787,7 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     c.inv_w = 1.0 / w;
     c.fixed_bin = fixed_bin ? 1 : 0;
     c.edges_lds = 1;
-    if (lde::coord_smem(c, false, false) > lde::kCoordSmemMax) c.edges_lds = 0;  // huge T: edges from HBM
-    c.cus = h->cus;
-    c.cache_bits = 0;
-    if (h->coord_cache_built) {
-        c.cache_q = h->d_ccq;
-        c.cache_d = h->d_ccd;
-        c.cache_bits = lde::kCoordCacheBits;
-    }
+    if (lde::coord_smem(c, false) > lde::kCoordSmemMax) c.edges_lds = 0;  // huge T: edges from HBM
     h->coord = true;
     h->key_ok.assign(h->key_ok.size(), 0);  // new distances, grid or edges
     if (!rebind)
@@ -3475,18 +2896,6 @@ int lde_counter(lde_handle *h, int32_t id, int64_t *value) {
     case LDE_C_WAIT_PRED_US:
         *value = (int64_t)h->wait_pred_us;
         return LDE_OK;
-    case LDE_C_SIEVE_PAIR:
-        *value = h->pair_last ? 1 : 0;
-        return LDE_OK;
-    case LDE_C_SIEVE_PAIR_WRAPS: {
-        *value = 0;
-        if (!h->d_pair_wraps) return LDE_OK;
-        uint32_t n = 0;
-        HIPCALL(h, hipStreamSynchronize(h->stream));
-        HIPCALL(h, hipMemcpy(&n, h->d_pair_wraps, 4, hipMemcpyDeviceToHost));
-        *value = n;
-        return LDE_OK;
-    }
     default:
         return fail(h, LDE_EINVAL, "unknown counter id %d", id);
     }

@@ -38,9 +38,6 @@ constexpr size_t kPagedSmemMax = 80 * 1024;        // two pass-A blocks per CU (
 constexpr int kSplitThreads = 1024;                // SPLIT event pass block (one per CU)
 constexpr int kSplitEPT = kChunk / kSplitThreads;  // 8 events per thread per chunk
 constexpr size_t kSplitSmemMax = 160 * 1024;       // hot rows + TOA image, one block per CU
-constexpr uint32_t kHotDrop = 0xFFFFFFFFu;         // hot-LUT entry of a dropped pixel
-constexpr int kHotRowShift = 22;                   // hot LUT: (row + 1) << 22 | screen
-constexpr uint32_t kHotBaseMask = (1u << kHotRowShift) - 1u;
 constexpr int kHotMaxRows = 1022;
 constexpr int kSampleBlocks = 64;                  // sampled chunks per hot-set selection
 
@@ -87,7 +84,6 @@ __host__ __device__ inline size_t toa_lds_bytes(const ToaParams &tp) {
 struct PartitionArgs {
     int tile_bits;
     bool lut16;
-    bool peel;
     const SegDesc *segs;
     int n_segs;
     long long c_begin, n_chunks;
@@ -147,9 +143,8 @@ struct PagedArgs {
 
 size_t paged_smem(int n_tiles, int subc, const ToaParams &tp);
 hipError_t launch_paged_partition(const PagedArgs &a, hipStream_t st);
-// key mode: segments hold u32 (screen * T + bin) keys, chunk count read on the device
-hipError_t launch_paged_keys(const PagedArgs &a, const long long *n_chunks_dev, hipStream_t st);
 
+// hot-set selection of the SPLIT strategy (lde_hotset.hip)
 struct SplitArgs {
     const SegDesc *segs;  // staged event segments
     int n_segs;
@@ -159,23 +154,14 @@ struct SplitArgs {
     long long L;
     int pid_off;
     int S;
-    const unsigned char *tab;
     ToaParams tp;
     int rows;  // hot rows H
     int sample_blocks;
     uint32_t *sample_part, *screen_cnt, *stats;
     uint16_t *screen_row;
     uint32_t *row_screen;  // this replica's row -> screen
-    uint32_t *hlut;        // this replica's hot LUT
-    int grid;
-    uint32_t *hot_part;
-    uint32_t *cold;
-    long long cold_cap;  // keys per block region
-    uint32_t *cold_cnt;
-    int cache_bits, row_bits, screen_bits;  // LDS pixel table (cache_bits 0: off)
-    uint32_t *pix_cnt;  // [L] sampled events per pixel (zeroed before each selection)
-    uint32_t *pix_tab;  // this replica's pixel table image (1 << cache_bits words)
-    const int *dummy;  // 16-byte aligned zeros: load target of non-live chunk slots
+    int cache_bits;        // LDS pixel table bits (0: off)
+    uint32_t *pix_cnt;     // [L] sampled events per pixel (zeroed before each selection)
 };
 // SIEVE: the lean SPLIT event pass (lde_sieve.hip).  Pixel word, in the LDS
 // table and in the HBM LUT: valid | hot | tag (table only) | value, where
@@ -206,8 +192,6 @@ struct SieveArgs {
     const ChunkPtrs *chunk_tab;  // [n_chunks + 1]; deferred chunks and entry n_chunks: dummy
     int lds_ctab;                // 1: build the block's chunk table in LDS (no chunk_tab)
     int karg;                    // lds_ctab: descriptors from sk (else from segs)
-    int early_gather;            // 1: gathers issued one iteration before they are binned
-    int pack;                    // 1: TOA bin packed into the table word at the gather
     SegKarg sk;                  // lds_ctab: the message descriptors (n_segs <= kKargSegs)
     const int *dummy;            // the all-invalid chunk
     const uint32_t *glut;  // this replica's pixel words, L + 1 entries (entry L = 0)
@@ -215,56 +199,33 @@ struct SieveArgs {
     int pid_off;
     const uint32_t *ttab;  // TOA bucket words (+ sentinel), padded to toa_words4
     uint32_t toa_lo, toa_cap;
-    int toa_shift, toa_words4;  // toa_log: toa_shift = M (2^M log-linear buckets per octave)
-    int toa_log = 0;
+    int toa_shift, toa_words4;
     int T;
     const uint32_t *pix_tab;  // this replica's LDS table image (1 << cbits words)
     int cbits;
-    int hot_words;  // align4(hot_lo + rows * hot_w)
-    // TOA window of the hot rows: row r holds bins [hot_lo, hot_lo + hot_w) at
-    // LDS words r * hot_w + bin (so words [0, hot_lo) stay unused); a hot
-    // screen's event outside the window leaves as a cold key, its screen from
-    // the row table (hot_w = T, hot_lo = 0: whole rows, no such events)
-    int hot_lo = 0, hot_w = 0, hot_rows = 0;
-    float hot_inv_w = 0.f;         // 1 / hot_w (row of a word value row * hot_w)
-    const uint32_t *row_screen = nullptr;  // [hot_rows] screen of each hot row
+    int hot_words;  // align8(rows * T): the hot rows' LDS words
     uint32_t *hot_part;
     uint32_t *cold;
-    long long cold_cap;  // keys per block region (region stride cold_cap + 16)
+    long long cold_cap;  // 24-bit keys per block region (region stride cold_cap + 16)
     uint32_t *cold_cnt;
     int tile_bits, n_tiles;  // cold keys are counted per tile of 2^tile_bits bins
     uint32_t *cold_tcnt;     // [grid][kColdGroups][n_tiles]
-    int ablate;  // benchmark ablation variant (0 = the real pass)
-    int key24 = 0;  // cold keys leave as 24-bit keys (3 bytes; S * T < 2^24 - 1)
-    uint32_t *hot_fmt = nullptr;  // [grid] 1: the block's hot rows left as u16 (null: u32)
+    int ablate;  // diagnostics build: timing ablation (0 = the real pass)
+    uint32_t *hot_fmt = nullptr;  // [grid] 1: the block's hot rows left as u16, 0: as u32
     unsigned long long *trace = nullptr;  // diagnostic [grid][3]: start, stream end, end (realtime)
-    int tail_release = 0;  // each block ends with an agent-scope release (L2 writeback of its stores)
     int keyed = 0;  // the 'toa' stream holds finished pixel words (k_event_key): no probe/gather/TOA
-    // keyed24: the words packed to 24 bits (flags << 22 | value, 4 in 12 bytes);
-    // chunk c's pointer base + 4 c kChunk reads bytes base + 3 c kChunk, the
-    // dummy chunk reads zero24 (kChunk * 3 zero bytes)
-    int keyed24 = 0;
-    const void *keyed_base = nullptr;
-    const void *zero24 = nullptr;
-    // pair: hot counters as u16 pairs (hot_words = LDS words = counters / 2,
-    // whole rows, the default pipeline only); hist: the window, which a block
-    // whose u16 counters wrapped adds its hot events to with global atomics
-    int pair = 0;
-    uint32_t *hist = nullptr;
-    uint32_t *wraps = nullptr;  // (pair) +1 per block whose counters wrapped
 };
-size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles, int hot_rows = kHotMaxRows);
+size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);
 // cold keys of SIEVE: per-tile scan, plan, exact counting sort into a
 // tile-major u16 array, pass B
 struct ColdArgs {
     int tile_bits, n_tiles;
-    int rows;    // sieve blocks (one sort block each)
+    int rows;    // sieve blocks (one sort block per wave group)
     // hot rows of the sieve blocks, reduced into hist in the same launch as
     // the per-tile scan (hot_part == nullptr: none)
     const uint32_t *hot_part = nullptr;
     const uint32_t *row_screen = nullptr;
-    int ht = 0, ht4 = 0, T = 1;  // hot words (hot_lo + rows * hot_w), their row stride
-    int hot_lo = 0, hot_w = 1;   // the hot rows' TOA window (SieveArgs)
+    int ht = 0, ht4 = 0, T = 1;  // hot words (rows * T) and their row stride
     const uint32_t *cold;
     long long stride, cap;  // region stride and capacity (keys)
     const uint32_t *cold_cnt, *tcnt;
@@ -275,26 +236,18 @@ struct ColdArgs {
     uint16_t *keys;  // tile-major, 16-byte aligned, >= total + 8 entries
     uint32_t *hist;
     long long n_bins;
-    int wave_sort = 0;  // 1: k_cold_sort_w (wave-independent) when its LDS fits
-    int pad8 = 0;       // 1: k_cold_sort_a (16-byte groups; ranges padded to 8 keys)
-    int sort_kpt = 48;  // k_cold_sort_a keys per thread per piece (16, 32 or 48)
-    int key24 = 0;      // the sieve wrote 24-bit keys (k_cold_sort_a only)
     const uint32_t *hot_fmt = nullptr;  // per sieve block: hot rows as u16 (1) or u32 (0)
-    int tail_release = 0;  // bit 1: sort blocks, bit 2: pass-B blocks end with an agent release
-    int ablate = 0;     // cold-sort diagnostics (wrong results): 1 no writes, 2 no loads
+    int ablate = 0;     // cold-sort diagnostics (wrong results): 1 no writes
     int all_hot = 0;    // every screen has a hot row (no cold keys): hot-row reduce only
 };
-size_t cold_sort_smem(int n_tiles);
-size_t cold_sort_w_smem(int n_tiles);
 size_t cold_sort_a_smem(int n_tiles, int kpt);
 constexpr int kSortThreadsHost = 64 * (kSplitThreads / 64) / kColdGroups;  // cold-sort block
 // start/stop: optional HIP events stamped by the kernel dispatch itself
 // (hipExtLaunchKernelGGL), so timing adds no marker packets between kernels
 hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t stop = nullptr);
-hipError_t launch_hot_reduce(const SplitArgs &a, uint32_t *win, hipStream_t st);
 hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T, int W,
                                const uint16_t *screen_row, const uint32_t *pix_cnt, int cbits,
-                               uint32_t *glut, uint32_t *tab, hipStream_t st);
+                               uint32_t *glut, uint32_t *tab, uint32_t *stats, hipStream_t st);
 // dummy: kChunk x (pid_off - 1), the all-invalid chunk
 hipError_t launch_chunk_tab(const SegDesc *segs, int n_segs, long long n_chunks, const int *dummy,
                             ChunkPtrs *tab, hipStream_t st,
@@ -304,12 +257,8 @@ hipError_t launch_chunk_tab_karg(const SegDesc *host_segs, int n_segs, long long
                                  hipStream_t st);
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start = nullptr,
                         hipEvent_t stop = nullptr);
-size_t split_smem(int ht4, int cache_words, const ToaParams &tp);
-hipError_t launch_hot_sample(const SplitArgs &a, int replica, uint32_t *toa_hist, hipStream_t st);
-hipError_t launch_hot_pick(const SplitArgs &a, int replica, hipStream_t st);
-hipError_t launch_split(const SplitArgs &a, hipStream_t st);
-hipError_t launch_split_tail(const SplitArgs &a, uint32_t *win, SegDesc *cold_segs,
-                             long long *n_cold_chunks, hipStream_t st);
+hipError_t launch_hot_sample(const SplitArgs &a, int replica, hipStream_t st);
+hipError_t launch_hot_pick(const SplitArgs &a, hipStream_t st);
 hipError_t launch_page_plan(const PagedArgs &a, uint32_t item_events, uint32_t *cntp,
                             uint32_t *evp, uint32_t *tile_pages, uint32_t *tile_events,
                             uint32_t *tile_base, uint4 *items, uint32_t *item_count,
@@ -325,10 +274,10 @@ hipError_t launch_tile_accumulate(int tile_bits, const uint16_t *payload, const 
                                   const uint32_t *item_count, const uint32_t *tile_items,
                                   uint32_t *hist, long long n_bins, int grid, hipStream_t st);
 // start/stop (optional): HIP events stamped by the dispatch itself
+// messages in block ranges: SegDesc::chunk0 = the message's first block
 hipError_t launch_monitor(const SegKarg &segs, int n_segs, const unsigned char *tab,
                           const ToaParams &tp, uint32_t *hist, int grid, hipStream_t st,
-                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr, bool pf = false,
-                          bool block_ranges = false);
+                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 hipError_t launch_fold_window(uint32_t *win32, unsigned long long *win64, long long n,
                               hipStream_t st);
 hipError_t launch_merge_f32(uint32_t *batch, unsigned long long *win64, float *winf, float *cumf,
@@ -339,26 +288,12 @@ hipError_t launch_merge_f32_u64(const unsigned long long *src, unsigned long lon
 hipError_t launch_push_export(uint32_t *batch, unsigned long long *out, long long n, hipStream_t st);
 hipError_t launch_sum3(const unsigned long long *a, const unsigned long long *b, const uint32_t *c,
                        unsigned long long *out, long long n, hipStream_t st);
-// split finalize (lde_maint.hip): the rows part the host waits for, then the
-// fold of the window into the cumulative histogram
-bool finalize_split_ok(int T);
-hipError_t launch_finalize_rows(int img_kind, const uint32_t *win32, const unsigned long long *win64,
-                                unsigned long long *cum_rows, long long S, int T, int lo, int hi,
-                                void *cur_img, void *cum_img, const uint32_t *ovf_src, uint32_t *ovf_dst,
-                                unsigned long long *host_parts, int *n_parts, hipStream_t st,
-                                hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
-hipError_t launch_fold_cumulative(uint32_t *win32, unsigned long long *win64, unsigned long long *cum,
-                                  long long nbins, hipStream_t st);
-hipError_t launch_cum_rows(const unsigned long long *cum, long long S, int T, int lo, int hi,
-                           unsigned long long *cum_rows, hipStream_t st);
 hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *win64,
                            unsigned long long *cum, unsigned long long *snap, long long S, int T,
                            int lo, int hi, void *cur_img, void *cum_img,
                            unsigned long long *totals, unsigned long long *tot_copy,
                            const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st,
                            unsigned long long *host_parts = nullptr, int *n_parts = nullptr);
-hipError_t launch_rows_f32(const float *h, long long S, int T, int lo, int hi, float *img,
-                           hipStream_t st);
 // float32 finalize in one pass with the window's pending push (batch, may be
 // null): f32 adds, images, exact totals and cumulative, window reset
 hipError_t launch_finalize_f32(uint32_t *batch, unsigned long long *win64, unsigned long long *cum,
@@ -393,16 +328,9 @@ struct CoordArgs {
     double e0, inv_w;       // bucket g = (v - e0) * inv_w
     int fixed_bin = 0;      // 1: every bucket's candidate is within [-1, +2] of the
                             // true bin (checked on the host): branch-free correction
-    const uint32_t *cache_q = nullptr;  // [1 << cache_bits] cached pixel per slot (-1: none)
-    const double *cache_d = nullptr;    // its distance
-    int cache_bits = 0;                 // 0: no distance cache
-    int cus = 256;                      // grid of the cached variant (one block per CU)
 };
 constexpr size_t kCoordSmemMax = 160 * 1024;
-constexpr int kCoordCacheBits = 13;  // 8192-slot distance cache (96 KB of LDS)
-size_t coord_smem(const CoordArgs &a, bool table_lds, bool cache);
-hipError_t launch_coord_cache(const uint32_t *pix_cnt, const double *pix_d, long long L, int cbits,
-                              uint32_t *cq, double *cd, hipStream_t st);
+size_t coord_smem(const CoordArgs &a, bool table_lds);
 hipError_t launch_event_coord(const CoordArgs &a, const int *pid, const int *toa, long long n,
                               int *out, hipStream_t st);
 
@@ -427,8 +355,6 @@ struct KeyArgs {
     int *keys;                // [n_chunks * kChunk]
     const int *dummy;         // kChunk x (pid_off - 1): the all-invalid chunk
     const uint8_t *tab_i = nullptr;  // pre: distance row of each slot's pixel (0xFF: outside)
-    int k24 = 0;              // 1: words packed to 24 bits (SieveArgs::keyed24), chunk c at
-                              // byte 3 c kChunk of keys
     int pre = 0;              // 1: tab_d / rec hold fx and the row (k_key_dist / k_key_records
                               // with pre_nd = nd), the FAST event pass
     int ablate = 0;           // diagnostics build (LDE_KEY_ABLATE): 1 no gathers, 2 no
@@ -471,12 +397,10 @@ struct PixArgs {
     uint32_t *counts;            // [grid][nr] events, then payload offsets
     uint32_t *rstart;            // [nr + 1] range starts, then [nr] range totals (scratch)
     uint32_t *payload;           // local pixel | bin << rb per event, range-major
-                                 // (24-bit payloads packed 4 per 12 bytes when p24)
+                                 // (24-bit payloads packed 4 per 12 bytes)
     int grid;
     int unit = 1;                // chunks per partition step (runs padded per unit)
     int ept = 8;                 // events per thread and load: unit * kChunk / ept threads
-    int p24 = 1;                 // 3-byte payloads
-    int bu = 4;                  // pass B: groups per lane in flight (4 or 8)
     // predicted slots (no count pass): every (block, range) slot is sized
     // from the previous batch's run totals (prev) scaled by pred; a run past
     // its slot goes to the overflow groups, added at the end of pass B.  pred = 0:
@@ -492,7 +416,6 @@ struct PixArgs {
     const uint32_t *ovf_fp_scr = nullptr;
     uint32_t *ovf_hist = nullptr;          // the window
     int ablate = 0;              // LDE_PIX_ABLATE (diagnostics build): 1 no payload stores
-    int pf2 = 0;                 // two units of events in flight per block (LDE_PIX_PF2)
 };
 struct PixSetup {                // setup-time tables (lde_create / lde_set_lut)
     int rb = 0, nr = 0, fmax = 0, rs = 24;

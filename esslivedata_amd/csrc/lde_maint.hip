@@ -239,133 +239,6 @@ __global__ __launch_bounds__(256) void k_finalize_v4(uint32_t *__restrict__ win3
     }
 }
 
-// Split finalize (T % 4 == 0, T <= 128; no histograms requested).  The part
-// the host waits for reads only the window: per screen row its in-range and
-// all-bin counts give the current image, and running cumulative row sums
-// (cum_rows[2 s]: in range, [2 s + 1]: all bins) give the cumulative image and
-// totals without touching the cumulative histogram.  k_fold_cumulative then
-// folds the window into the cumulative histogram and clears it, on the stream
-// after the host's wake-up event, i.e. while the host turns around (the
-// previous single kernel read and wrote 60 MB for DREAM before the host could
-// go on; this part reads 10 MB).  Totals and images are those of k_finalize_v4.
-template <typename OUT>
-__global__ __launch_bounds__(256) void k_finalize_rows(const uint32_t *__restrict__ win32,
-                                                       const unsigned long long *__restrict__ win64,
-                                                       unsigned long long *__restrict__ cum_rows,
-                                                       long long S, int T, int lo, int hi,
-                                                       OUT *__restrict__ cur_img,
-                                                       OUT *__restrict__ cum_img,
-                                                       unsigned long long *__restrict__ totals,
-                                                       const uint32_t *__restrict__ ovf_src,
-                                                       uint32_t *__restrict__ ovf_dst) {
-    typedef unsigned long long u64;
-    __shared__ u64 s_tot[8][4];
-    __shared__ OUT s_img[2][8];
-    const int gl = threadIdx.x & 31, grp = threadIdx.x >> 5;
-    u64 acc[4] = {0, 0, 0, 0};
-    const int i0 = gl * 4;
-    const bool act = i0 < T;
-    for (long long base = (long long)blockIdx.x * 8; base < S; base += (long long)gridDim.x * 8) {
-        const long long s = base + grp;
-        u64 rw = 0, tw = 0;
-        if (act && s < S) {
-            const long long k = s * T + i0;
-            const uint4 w4 = *reinterpret_cast<const uint4 *>(win32 + k);
-            u64 w[4] = {w4.x, w4.y, w4.z, w4.w};
-            if (win64) {
-                const ulonglong2 a = *reinterpret_cast<const ulonglong2 *>(win64 + k);
-                const ulonglong2 b = *reinterpret_cast<const ulonglong2 *>(win64 + k + 2);
-                w[0] += a.x; w[1] += a.y; w[2] += b.x; w[3] += b.y;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                tw += w[q];
-                if (i0 + q >= lo && i0 + q < hi) rw += w[q];
-            }
-        }
-#pragma unroll
-        for (int d = 16; d > 0; d >>= 1) {
-            rw += __shfl_xor(rw, d, 32);
-            tw += __shfl_xor(tw, d, 32);
-        }
-        if (gl == 0 && s < S) {
-            ulonglong2 *cr = reinterpret_cast<ulonglong2 *>(cum_rows) + s;
-            const ulonglong2 c = *cr;
-            const u64 rc = c.x + rw, tc = c.y + tw;
-            *cr = make_ulonglong2(rc, tc);
-            s_img[0][grp] = (OUT)rw;
-            s_img[1][grp] = (OUT)rc;
-            acc[0] += tw;
-            acc[1] += rw;
-            acc[2] += tc;
-            acc[3] += rc;
-        }
-        __syncthreads();
-        if (threadIdx.x < 16) {
-            const int r = threadIdx.x & 7;
-            OUT *img = threadIdx.x < 8 ? cur_img : cum_img;
-            if (img && base + r < S) img[base + r] = s_img[threadIdx.x >> 3][r];
-        }
-        __syncthreads();
-    }
-    if (gl == 0)
-        for (int q = 0; q < 4; ++q) s_tot[grp][q] = acc[q];
-    __syncthreads();
-    if (ovf_dst && blockIdx.x == 0 && threadIdx.x == 4) *ovf_dst = ovf_src ? *ovf_src : 0u;
-    if (threadIdx.x < 4) {
-        u64 v = 0;
-        for (int g = 0; g < 8; ++g) v += s_tot[g][threadIdx.x];
-        totals[4 + (size_t)blockIdx.x * 4 + threadIdx.x] = v;
-    }
-}
-
-// cum += window (win32 + win64), window = 0; four bins per thread (n4 = bins / 4)
-__global__ __launch_bounds__(256) void k_fold_cumulative(uint32_t *__restrict__ win32,
-                                                         unsigned long long *__restrict__ win64,
-                                                         unsigned long long *__restrict__ cum,
-                                                         long long n4) {
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-        const uint4 w4 = reinterpret_cast<const uint4 *>(win32)[i];
-        unsigned long long w[4] = {w4.x, w4.y, w4.z, w4.w};
-        if (win64) {
-            ulonglong2 *p = reinterpret_cast<ulonglong2 *>(win64) + 2 * i;
-            const ulonglong2 a = p[0], b = p[1];
-            w[0] += a.x; w[1] += a.y; w[2] += b.x; w[3] += b.y;
-            p[0] = make_ulonglong2(0, 0);
-            p[1] = make_ulonglong2(0, 0);
-        }
-        ulonglong2 *c = reinterpret_cast<ulonglong2 *>(cum) + 2 * i;
-        const ulonglong2 c01 = c[0], c23 = c[1];
-        c[0] = make_ulonglong2(c01.x + w[0], c01.y + w[1]);
-        c[1] = make_ulonglong2(c23.x + w[2], c23.y + w[3]);
-        reinterpret_cast<uint4 *>(win32)[i] = make_uint4(0, 0, 0, 0);
-    }
-}
-
-// cum_rows from the cumulative histogram (after a reset of the running sums)
-__global__ __launch_bounds__(256) void k_cum_rows(const unsigned long long *__restrict__ cum, long long S,
-                                                  int T, int lo, int hi,
-                                                  unsigned long long *__restrict__ cum_rows) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (long long s = (long long)blockIdx.x * 4 + wid; s < S; s += (long long)gridDim.x * 4) {
-        unsigned long long r = 0, t = 0;
-        for (int i = lane; i < T; i += 64) {
-            const unsigned long long c = cum[s * T + i];
-            t += c;
-            if (i >= lo && i < hi) r += c;
-        }
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) {
-            r += __shfl_xor(r, d, 64);
-            t += __shfl_xor(t, d, 64);
-        }
-        if (lane == 0) {
-            cum_rows[2 * s] = r;
-            cum_rows[2 * s + 1] = t;
-        }
-    }
-}
-
 // totals[q] = sum over blocks of the partials at totals[4 + 4 * block + q].
 // Thread i sums the partials i, i + 1024, ... (all of quantity i & 3) with
 // independent loads, then the 256 threads of each quantity reduce in LDS.
@@ -466,19 +339,6 @@ __global__ __launch_bounds__(256) void k_finalize_f32(
     if (threadIdx.x < 4)
         totals[4 + (size_t)blockIdx.x * 4 + threadIdx.x] =
             s_tot[0][threadIdx.x] + s_tot[1][threadIdx.x] + s_tot[2][threadIdx.x] + s_tot[3][threadIdx.x];
-}
-
-// f32-mode image rows: sum of f32 values over the TOA range in f64, rounded once
-__global__ __launch_bounds__(256) void k_rows_f32(const float *__restrict__ h, long long S, int T,
-                                                  int lo, int hi, float *__restrict__ img) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (long long s = (long long)blockIdx.x * 4 + wid; s < S; s += (long long)gridDim.x * 4) {
-        double r = 0.0;
-        for (int i = lane + lo; i < hi; i += 64) r += (double)h[s * T + i];
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) r += __shfl_xor(r, d, 64);
-        if (lane == 0) img[s] = (float)r;
-    }
 }
 
 
@@ -598,58 +458,16 @@ static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsign
                            ovf_src, ovf_dst);
 }
 
-bool finalize_split_ok(int T) { return T % 4 == 0 && T <= 128; }
-
-hipError_t launch_finalize_rows(int img_kind, const uint32_t *win32, const unsigned long long *win64,
-                                unsigned long long *cum_rows, long long S, int T, int lo, int hi,
-                                void *cur_img, void *cum_img, const uint32_t *ovf_src, uint32_t *ovf_dst,
-                                unsigned long long *host_parts, int *n_parts, hipStream_t st,
-                                hipEvent_t start, hipEvent_t stop) {
-    if (!finalize_split_ok(T) || img_kind == 1) return hipErrorInvalidValue;
-    long long blocks = (S + 7) / 8;
-    if (blocks > kHostPartials) blocks = kHostPartials;
-    if (blocks < 1) blocks = 1;
-    if (img_kind == 2)
-        hipExtLaunchKernelGGL(k_finalize_rows<unsigned long long>, dim3((unsigned)blocks), dim3(256), 0, st,
-                              start, stop, 0, win32, win64, cum_rows, S, T, lo, hi,
-                              (unsigned long long *)cur_img, (unsigned long long *)cum_img, host_parts - 4,
-                              ovf_src, ovf_dst);
-    else
-        hipExtLaunchKernelGGL(k_finalize_rows<double>, dim3((unsigned)blocks), dim3(256), 0, st, start, stop,
-                              0, win32, win64, cum_rows, S, T, lo, hi, (double *)cur_img, (double *)cum_img,
-                              host_parts - 4, ovf_src, ovf_dst);
-    *n_parts = (int)blocks;
-    return hipGetLastError();
-}
-
-hipError_t launch_fold_cumulative(uint32_t *win32, unsigned long long *win64, unsigned long long *cum,
-                                  long long nbins, hipStream_t st) {
-    const long long n4 = nbins / 4;
-    long long g = (n4 + 255) / 256;
-    g = g < 1 ? 1 : (g > 8192 ? 8192 : g);
-    hipLaunchKernelGGL(k_fold_cumulative, dim3((unsigned)g), dim3(256), 0, st, win32, win64, cum, n4);
-    return hipGetLastError();
-}
-
-hipError_t launch_cum_rows(const unsigned long long *cum, long long S, int T, int lo, int hi,
-                           unsigned long long *cum_rows, hipStream_t st) {
-    long long g = (S + 3) / 4;
-    g = g < 1 ? 1 : (g > 4096 ? 4096 : g);
-    hipLaunchKernelGGL(k_cum_rows, dim3((unsigned)g), dim3(256), 0, st, cum, S, T, lo, hi, cum_rows);
-    return hipGetLastError();
-}
-
-// image element type: 0 f64, 1 f32, 2 u64 (exact partial sums for multi-GPU)
+// image element type: 0 f64, 2 u64 (exact partial sums for multi-GPU); float32
+// views finalize with k_finalize_f32
 hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *win64,
                            unsigned long long *cum, unsigned long long *snap, long long S, int T,
                            int lo, int hi, void *cur_img, void *cum_img,
                            unsigned long long *totals, unsigned long long *tot_copy,
                            const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st,
                            unsigned long long *host_parts, int *n_parts) {
-    if (img_kind == 1)
-        launch_finalize_t<float>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals,
-                                 tot_copy, ovf_src, ovf_dst, host_parts, n_parts, st);
-    else if (img_kind == 2)
+    if (img_kind == 1) return hipErrorInvalidValue;
+    if (img_kind == 2)
         launch_finalize_t<unsigned long long>(win32, win64, cum, snap, S, T, lo, hi, cur_img,
                                               cum_img, totals, tot_copy, ovf_src, ovf_dst,
                                               host_parts, n_parts, st);
@@ -671,15 +489,6 @@ hipError_t launch_finalize_f32(uint32_t *batch, unsigned long long *win64, unsig
                           win64, cum, winf, cumf, snap, S, T, lo, hi, first_win, first_cum, cur_img, cum_img,
                           host_parts - 4, ovf_src, ovf_dst);
     *n_parts = (int)blocks;
-    return hipGetLastError();
-}
-
-hipError_t launch_rows_f32(const float *h, long long S, int T, int lo, int hi, float *img,
-                           hipStream_t st) {
-    long long blocks = (S + 3) / 4;
-    if (blocks > 2048) blocks = 2048;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_rows_f32, dim3((unsigned)blocks), dim3(256), 0, st, h, S, T, lo, hi, img);
     return hipGetLastError();
 }
 

@@ -581,24 +581,8 @@ static hipError_t launch_paged_tb(const PagedArgs &a, hipStream_t st) {
 
 hipError_t launch_paged_partition(const PagedArgs &a, hipStream_t st) {
     switch (a.tile_bits) {
-    case 13: return launch_paged_tb<13>(a, st);
     case 14: return launch_paged_tb<14>(a, st);
     case 15: return launch_paged_tb<15>(a, st);
-    default: return hipErrorInvalidValue;
-    }
-}
-
-template <int TB>
-static hipError_t launch_paged_keys_tb(const PagedArgs &a, const long long *nc, hipStream_t st) {
-    return a.subc == 4 ? launch_paged_t<TB, uint16_t, true, 4, true>(a, nullptr, st, nc)
-                       : launch_paged_t<TB, uint16_t, true, 1, true>(a, nullptr, st, nc);
-}
-
-hipError_t launch_paged_keys(const PagedArgs &a, const long long *n_chunks_dev, hipStream_t st) {
-    switch (a.tile_bits) {
-    case 13: return launch_paged_keys_tb<13>(a, n_chunks_dev, st);
-    case 14: return launch_paged_keys_tb<14>(a, n_chunks_dev, st);
-    case 15: return launch_paged_keys_tb<15>(a, n_chunks_dev, st);
     default: return hipErrorInvalidValue;
     }
 }
@@ -624,10 +608,6 @@ hipError_t launch_page_accumulate(int tile_bits, const PagedArgs &a, const uint3
                                   const uint4 *items, const uint32_t *item_count, uint32_t *hist,
                                   long long n_bins, int grid, hipStream_t st) {
     switch (tile_bits) {
-    case 13:
-        hipLaunchKernelGGL(k_page_accumulate<13>, dim3(grid), dim3(kTileThreads), 0, st, a.pages,
-                           a.page_cnt, list, items, item_count, hist, n_bins);
-        break;
     case 14:
         hipLaunchKernelGGL(k_page_accumulate<14>, dim3(grid), dim3(kTileThreads), 0, st, a.pages,
                            a.page_cnt, list, items, item_count, hist, n_bins);

@@ -51,7 +51,7 @@ constexpr int kPixLdsChunks = 128;                 // chunk-table entries a bloc
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 typedef __attribute__((address_space(1))) v3u g_v3u;
 
-// Four 24-bit payloads in 12 bytes (P24) or 16 (u32 payloads)
+// Four 24-bit payloads in 12 bytes
 __device__ __forceinline__ v3u pack24(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3) {
     return v3u{p0 | (p1 << 24), (p1 >> 8) | (p2 << 16), (p2 >> 16) | (p3 << 8)};
 }
@@ -276,7 +276,7 @@ __device__ __forceinline__ void pix_add_group(const uint16_t *__restrict__ loc,
                                               const uint32_t *__restrict__ fp_scr, int T,
                                               uint32_t *__restrict__ hist, int rs, int rb, uint4 w);
 
-template <int U, int E, bool P24, bool FAST, bool PF2>
+template <int U, int E, bool FAST>
 __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     constexpr int NT = U * kChunk / E;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -315,9 +315,6 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     long long cb, ce;
     block_units((a.n_chunks + U - 1) / U, cb, ce);
     const PixChunk *s_ct = block_chunk_table<U>(a, s_ctab, cb, ce);  // (+ the barrier for s_cnt, s_cur)
-    // D units of events in flight (PF2: two register sets, A and B, used by
-    // alternate units, so a unit's loads have two units' work to arrive)
-    constexpr long long D = PF2 ? 2 : 1;
     // owner thread tid < nr (range tid): the previous unit's padded run, added
     // to its cursor in this unit's scan step (after the barrier that ends the
     // previous unit's write-out, the cursor's last reader)
@@ -348,7 +345,7 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
         // the next unit's events load while this one is partitioned (not
         // hoisted above the words: both sets live would double the registers)
         __builtin_amdgcn_sched_barrier(0);
-        if (c + D < ce) unit_load<U, E, true>(a, s_ct, cb * U, c + D, p, t);
+        if (c + 1 < ce) unit_load<U, E, true>(a, s_ct, cb * U, c + 1, p, t);
         __syncthreads();
         // runs padded to 4: staging offsets, slot cursors and the pads are
         // whole groups
@@ -389,13 +386,8 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
             const uint32_t dst = s_cur[r] + (g - s_off[r]);
             const bool fits = dst < s_end[r];  // always, with exact slots
             if (fits && !(LDE_DIAG(a.ablate) & 1)) {
-                if (P24) {
-                    *(g_v3u *)(reinterpret_cast<unsigned char *>(a.payload) + (size_t)dst * 3u) =
-                        pack24(pl(w.x), pl(w.y), pl(w.z), pl(w.w));
-                } else {
-                    *reinterpret_cast<uint4 *>(a.payload + dst) =
-                        make_uint4(pl(w.x), pl(w.y), pl(w.z), pl(w.w));
-                }
+                *(g_v3u *)(reinterpret_cast<unsigned char *>(a.payload) + (size_t)dst * 3u) =
+                    pack24(pl(w.x), pl(w.y), pl(w.z), pl(w.w));
             }
             // predicted slot too small: the raw group to the overflow list,
             // one counter atomic per wave
@@ -421,16 +413,7 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
         };
     int pA[E], tA[E];
     if (cb < ce) unit_load<U, E, true>(a, s_ct, cb * U, cb, pA, tA);
-    if (PF2) {
-        int pB[E], tB[E];
-        if (cb + 1 < ce) unit_load<U, E, true>(a, s_ct, cb * U, cb + 1, pB, tB);
-        for (long long c = cb; c < ce; c += 2) {
-            unit(c, pA, tA);
-            if (c + 1 < ce) unit(c + 1, pB, tB);
-        }
-    } else {
-        for (long long c = cb; c < ce; ++c) unit(c, pA, tA);
-    }
+    for (long long c = cb; c < ce; ++c) unit(c, pA, tA);
     // the last unit's runs into the cursors (after its write-out)
     __syncthreads();
     if (tid < a.nr) s_cur[tid] += vprev;
@@ -444,13 +427,8 @@ __global__ __launch_bounds__(U * kChunk / E) void k_pix_scatter(PixArgs a) {
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int r = wv; r < a.nr; r += NT / 64)
         for (uint32_t d = s_cur[r] + (uint32_t)(tid & 63) * 4u; d < s_end[r]; d += 256u) {
-            if (P24) {
-                *(g_v3u *)(reinterpret_cast<unsigned char *>(a.payload) + (size_t)d * 3u) =
-                    v3u{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-            } else {
-                *reinterpret_cast<uint4 *>(a.payload + d) =
-                    make_uint4(kPixDropped, kPixDropped, kPixDropped, kPixDropped);
-            }
+            *(g_v3u *)(reinterpret_cast<unsigned char *>(a.payload) + (size_t)d * 3u) =
+                v3u{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
         }
 }
 
@@ -489,7 +467,7 @@ size_t pix_acc_smem(int rb, int fmax, int T) {
     return align16(((size_t)2 << rb)) + 4 * (size_t)fmax * (size_t)T + 4 * 64;
 }
 
-template <bool P24, int U>
+template <int U>
 __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16_t *__restrict__ loc,
                                                          const uint32_t *__restrict__ fp_off,
                                                          const uint32_t *__restrict__ fp_scr,
@@ -524,26 +502,18 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
     // the compiler does not wait for each inside its own branch.
     const uint32_t g0 = it.y >> 2, n4 = (it.z - it.y) >> 2;  // n4 >= 1 (items of non-empty ranges)
     const uint32_t step = blockDim.x * U;
-    // raw groups (4 words; 3 used with 24-bit payloads), unpacked at use
+    // raw groups (three words: four 24-bit payloads), unpacked at use
     auto ld = [&](uint32_t i) __attribute__((always_inline)) -> v4i {
         const uint32_t ic = i < n4 ? i : n4 - 1u;
-        if (P24) {
-            const v3u w = __builtin_nontemporal_load(
-                (const g_v3u *)(reinterpret_cast<const unsigned char *>(a.payload) + (size_t)(g0 + ic) * 12u));
-            return v4i{(int)w[0], (int)w[1], (int)w[2], 0};
-        }
-        return ld_stream4(reinterpret_cast<const int *>(a.payload) + (size_t)(g0 + ic) * 4u);
+        const v3u w = __builtin_nontemporal_load(
+            (const g_v3u *)(reinterpret_cast<const unsigned char *>(a.payload) + (size_t)(g0 + ic) * 12u));
+        return v4i{(int)w[0], (int)w[1], (int)w[2], 0};
     };
     auto add4 = [&](const v4i (&raw)[U], uint32_t ib) __attribute__((always_inline)) {
         uint32_t w[U][4], f[U][4];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (P24) {
-                unpack24(v3u{(uint32_t)raw[u][0], (uint32_t)raw[u][1], (uint32_t)raw[u][2]}, w[u]);
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) w[u][q] = (uint32_t)raw[u][q] & 0xFFFFFFu;
-            }
+            unpack24(v3u{(uint32_t)raw[u][0], (uint32_t)raw[u][1], (uint32_t)raw[u][2]}, w[u]);
             if (ib + u * blockDim.x >= n4) w[u][0] = w[u][1] = w[u][2] = w[u][3] = kPixDropped;
 #pragma unroll
             for (int q = 0; q < 4; ++q) f[u][q] = s_loc[w[u][q] & mask];
@@ -581,7 +551,7 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
 }
 
 namespace {
-template <int U, int E, bool P24>
+template <int U, int E>
 void launch_pass_a(const PixArgs &a, uint32_t item_events, int max_items, uint4 *items,
                    uint32_t *item_count, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
     constexpr int NT = U * kChunk / E;
@@ -604,44 +574,29 @@ void launch_pass_a(const PixArgs &a, uint32_t item_events, int max_items, uint4 
         (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipExtLaunchKernelGGL(kern, dim3(a.grid), dim3(NT), sm, st, start, stop, 0, a);
     };
-    if (a.tp.fast) {
-        if (a.pf2) go(k_pix_scatter<U, E, P24, true, true>); else go(k_pix_scatter<U, E, P24, true, false>);
-    } else {
-        if (a.pf2) go(k_pix_scatter<U, E, P24, false, true>); else go(k_pix_scatter<U, E, P24, false, false>);
-    }
-}
-template <bool P24>
-void launch_pass_a_shape(const PixArgs &a, uint32_t item_events, int max_items, uint4 *items,
-                         uint32_t *item_count, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
-    if (a.unit == 2) launch_pass_a<2, 16, P24>(a, item_events, max_items, items, item_count, st, start, stop);
-    else if (a.ept == 8) launch_pass_a<1, 8, P24>(a, item_events, max_items, items, item_count, st, start, stop);
-    else launch_pass_a<1, 16, P24>(a, item_events, max_items, items, item_count, st, start, stop);
+    if (a.tp.fast) go(k_pix_scatter<U, E, true>);
+    else go(k_pix_scatter<U, E, false>);
 }
 }  // namespace
 
 hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32_t item_events,
                         int max_items, uint4 *items, uint32_t *item_count, uint32_t *hist,
                         hipStream_t st, int phase, hipEvent_t start, hipEvent_t stop) {
+    // units of two chunks (1024 threads x 16 events) or, for TOA tables too
+    // large for that LDS carve, one (1024 threads x 8 events)
     if (a.nr >= kPixMaxRanges || a.nr > 1024 || (item_events & 3u) || (a.unit != 1 && a.unit != 2) ||
-        (a.ept != 8 && a.ept != 16) || (a.unit == 2 && a.ept != 16))
+        a.ept != (a.unit == 2 ? 16 : 8))
         return hipErrorInvalidValue;
     if (phase == 0) {
-        if (a.p24) launch_pass_a_shape<true>(a, item_events, max_items, items, item_count, st, start, stop);
-        else launch_pass_a_shape<false>(a, item_events, max_items, items, item_count, st, start, stop);
+        if (a.unit == 2) launch_pass_a<2, 16>(a, item_events, max_items, items, item_count, st, start, stop);
+        else launch_pass_a<1, 8>(a, item_events, max_items, items, item_count, st, start, stop);
     } else {
         const size_t sm = pix_acc_smem(s.rb, s.fmax, a.tp.T);
-        auto go = [&](auto kern) {
-            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-            hipExtLaunchKernelGGL(kern, dim3((unsigned)max_items), dim3(1024), sm, st, start, stop, 0, a,
-                                  s.loc + (size_t)replica * a.L, s.fp_off, s.fp_scr, items, item_count,
-                                  a.tp.T, hist);
-        };
-        if (a.p24) {
-            if (a.bu == 8) go(k_pix_accumulate<true, 8>); else go(k_pix_accumulate<true, 4>);
-        } else {
-            if (a.bu == 8) go(k_pix_accumulate<false, 8>); else go(k_pix_accumulate<false, 4>);
-        }
-
+        (void)hipFuncSetAttribute((const void *)k_pix_accumulate<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        hipExtLaunchKernelGGL(k_pix_accumulate<4>, dim3((unsigned)max_items), dim3(1024), sm, st, start, stop, 0,
+                              a, s.loc + (size_t)replica * a.L, s.fp_off, s.fp_scr, items, item_count, a.tp.T,
+                              hist);
     }
     return hipGetLastError();
 }

@@ -50,15 +50,6 @@ constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data fo
 constexpr int kEPT = kSplitEPT;               // 8 events per thread per chunk
 constexpr uint32_t kSieveStage = 256;         // cold staging words per wave (half a chunk)
 constexpr int kSieveKeyed = 262144;           // mode bit: the stream holds finished words
-constexpr int kSieveToaLog = 1 << 20;         // mode bit: log-linear TOA buckets
-constexpr int kSieveKeyed24 = 1 << 21;        // with kSieveKeyed: 24-bit packed words
-// mode bit: hot counters as u16 pairs (two per LDS word, twice the hot rows);
-// exact: a wrap is detected at the end of the pass (the counters' sum against
-// the wave-counted hot events) and that block's hot events are re-added with
-// global atomics (see k_sieve)
-constexpr int kSievePair = 1 << 24;
-constexpr int kSieveWindow = 1 << 23;         // hot rows narrowed to a TOA window (the
-                                              // default pipeline only; no cost when off)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 
@@ -89,9 +80,9 @@ __device__ __forceinline__ uint32_t &lds_at(uint32_t *sm, uint32_t byte_off) {
     return *reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(sm) + byte_off);
 }
 
-// Four cold keys (scaled by 4; pads all ones) as 24-bit keys in 12 bytes:
-// the key stream of the sieve when S * T < 2^24 - 1 (key24 mode), 25 % fewer
-// bytes written by the sieve and read by the sort.  The pad is 0xFFFFFF.
+// Four cold keys (scaled by 4; pads all ones) as 24-bit keys in 12 bytes (the
+// sieve's S * T <= 2^22): 25 % fewer bytes written by the sieve and read by
+// the sort than 32-bit keys.  The pad is 0xFFFFFF.
 __device__ __forceinline__ v3u pack_keys24(v4u k4) {
     const uint32_t k0 = (k4[0] >> 2) & 0xFFFFFFu, k1 = (k4[1] >> 2) & 0xFFFFFFu;
     const uint32_t k2 = (k4[2] >> 2) & 0xFFFFFFu, k3 = (k4[3] >> 2) & 0xFFFFFFu;
@@ -132,7 +123,8 @@ __global__ __launch_bounds__(256) void k_sieve_glut(const LT *__restrict__ lut, 
 // the pixel's word (0 for a dropped pixel: valid bit clear) and its tag
 __global__ __launch_bounds__(256) void k_sieve_table(const uint32_t *__restrict__ cnt,
                                                      const uint32_t *__restrict__ glut, long long L,
-                                                     int cbits, uint32_t *__restrict__ tab) {
+                                                     int cbits, uint32_t *__restrict__ tab,
+                                                     uint32_t *__restrict__ stats) {
     const long long C = 1LL << cbits;
     const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
     if (j >= C) return;
@@ -147,6 +139,7 @@ __global__ __launch_bounds__(256) void k_sieve_table(const uint32_t *__restrict_
     }
     tab[j] = bq < 0 ? kSieveEmpty
                     : (glut[bq] | ((uint32_t)(bq >> cbits) << kSieveTagShift));
+    if (best) atomicAdd(stats + 3, best);  // sampled events the table catches
 }
 
 // chunk c -> its event pointers, or the dummy chunk (deferred / past the end)
@@ -204,21 +197,16 @@ __global__ __launch_bounds__(256) void k_chunk_tab_karg(SegKarg sk, int n_segs, 
 // ---------------------------------------------------------------------------
 // the event pass
 // ---------------------------------------------------------------------------
-// ABL (benchmark ablations only, results are wrong when nonzero): 1 no hot
-// LDS atomics, 2 no gathers, 4 no cold stores, 8 no LDS probes, 16 every
-// gather lane out of range, 32 every gather lane on the first two words,
-// 64 cold stores exec-masked to the lanes with keys (results exact), 128
-// cold stores every other half only; 256 (exact) the early-gather pipeline;
-// 512 / 1024: 8 extra VALU ops / one extra LDS read per event (load probes);
-// 2048 (exact): cold-key stores deferred behind the next gathers and loads;
-// 4096: loads only (stream skeleton); 8192 (exact): cached instead of
-// nontemporal event loads
+// ABL: kSieveKeyed (the stream holds finished words, wavelength mode) or, in
+// the diagnostics build only, a timing ablation (results wrong by design): 1
+// no hot LDS atomics, 2 no gathers, 4 no cold stores, 4096 loads only (the
+// stream skeleton), 16384 loads + probes with the binning folded into a
+// register (+ the gathers with 32768), 131072 gathers confined to 64 KB.
 // GCT: the chunk table comes from global memory (k_chunk_tab), for blocks
 // whose chunk range exceeds kSieveLdsChunks.  Otherwise each block builds its
 // own in LDS, and GCT is a template switch rather than a runtime branch so
 // that the loop has one fetch path: with both, the compiler's wait-count
-// insertion merged the paths into a vmcnt(0) at the loop head (measured
-// neutral on DREAM, but the single path keeps the waits as written).
+// insertion merged the paths into a vmcnt(0) at the loop head.
 template <int ABL, int GCT>
 __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     // static, so LDS addresses need no runtime base (one block per CU anyway)
@@ -240,13 +228,6 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     const uint32_t o_ctab = o_tcnt + (uint32_t)(kColdGroups * align4(a.n_tiles));
     const uint32_t o_seg = o_ctab + 4u * kSieveLdsChunks;
     SegDesc *s_seg = reinterpret_cast<SegDesc *>(sm + o_seg);
-    // hot row -> screen (u16), for hot-screen events outside the rows' window
-    const uint32_t o_rs = o_seg + (uint32_t)(sizeof(SegDesc) / 4 * kKargSegs);
-    uint16_t *s_rs = reinterpret_cast<uint16_t *>(sm + o_rs);
-    constexpr bool windowed = (ABL & kSieveWindow) != 0;
-    constexpr bool pair = (ABL & kSievePair) != 0;
-    if (windowed)
-        for (int i = tid; i < a.hot_rows; i += kSplitThreads) s_rs[i] = (uint16_t)a.row_screen[i];
     for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.hot_words; i += kSplitThreads * 4u)
         *reinterpret_cast<uint4 *>(sm + i) = make_uint4(0, 0, 0, 0);
     for (uint32_t i = (uint32_t)tid * 4u; i < C; i += kSplitThreads * 4u)
@@ -254,7 +235,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.toa_words4; i += kSplitThreads * 4u)
         *reinterpret_cast<uint4 *>(sm + o_tt + i) = *reinterpret_cast<const uint4 *>(a.ttab + i);
     if (tid < 64) sm[o_dum + tid] = 0;
-    // cursor, hot-count overflow vote, (pair) hot events, hot counter sum
+    // cursor, hot-count overflow vote
     if (tid == 0) sm[o_cur] = sm[o_cur + 1] = sm[o_cur + 2] = sm[o_cur + 3] = 0;
     for (uint32_t i = (uint32_t)tid; i < kSieveStage * (kSplitThreads / 64); i += kSplitThreads)
         sm[o_stg + i] = 0xFFFFFFFFu;
@@ -267,31 +248,23 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     __syncthreads();
 
     const __amdgpu_buffer_rsrc_t glut = make_rsrc(a.glut, (a.L + 1u) * 4u);
-    // this block's cold region: cold_cap keys of 4 bytes, or of 3 (key24)
-    const uint32_t kbytes = a.key24 ? 3u : 4u;
+    // this block's cold region: cold_cap 24-bit keys (3 bytes each)
     unsigned char *my_cold = reinterpret_cast<unsigned char *>(a.cold) +
-                             (size_t)blockIdx.x * (size_t)(a.cold_cap + kSplitThreads / 64) * kbytes;
-    const __amdgpu_buffer_rsrc_t cold = make_rsrc(my_cold, (uint32_t)a.cold_cap * kbytes);
-    // one lane's four keys: offset = key index * 4 (kOOB: discarded)
+                             (size_t)blockIdx.x * (size_t)(a.cold_cap + kSplitThreads / 64) * 3u;
+    const __amdgpu_buffer_rsrc_t cold = make_rsrc(my_cold, (uint32_t)a.cold_cap * 3u);
+    // one lane's four keys (scaled by 4) as 12 bytes at key index off / 4
+    // (kOOB: discarded)
     auto store_keys = [&](v4u kv, uint32_t off) __attribute__((always_inline)) {
-        if (a.key24)
-            __builtin_amdgcn_raw_buffer_store_b96(pack_keys24(kv), cold,
-                                                  (int)(off == kOOB ? kOOB : (off >> 2) * 3u), 0, 0);
-        else
-            __builtin_amdgcn_raw_buffer_store_b128(kv, cold, (int)off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b96(pack_keys24(kv), cold,
+                                              (int)(off == kOOB ? kOOB : (off >> 2) * 3u), 0, 0);
     };
     const uint32_t cmask = C - 1u;
     const uint32_t pid_off = (uint32_t)a.pid_off;
     const uint32_t Lc = a.L;
     const uint32_t toa_lo = a.toa_lo, toa_cap = a.toa_cap;
-    // log-linear TOA buckets (ABL & kSieveToaLog): the offset inside the
-    // bucket is already masked in probe(), so bin() masks nothing
-    const uint32_t wmask = (ABL & kSieveToaLog) ? 0xFFFFFFFFu : (1u << a.toa_shift) - 1u;
-    const int toa_m = a.toa_shift;  // log-linear: 2^M buckets per octave
+    const uint32_t wmask = (1u << a.toa_shift) - 1u;
     const uint32_t T = (uint32_t)a.T;
-    const uint32_t hlo = (uint32_t)a.hot_lo, hw = (uint32_t)a.hot_w;
     const uint32_t dum_idx = o_dum + (uint32_t)lane;
-    const uint32_t hw4 = (uint32_t)a.hot_words * 4u;  // (pair) first high-half counter, scaled by 4
     const uint32_t dum4 = dum_idx * 4u;
     const uint32_t o_stg_w = o_stg + kSieveStage * (uint32_t)(tid >> 6);
     // cold keys are counted per tile for each of the kColdGroups wave groups
@@ -359,23 +332,6 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
 #pragma unroll
         for (int j = 0; j < kEPT / 4; ++j) {
             const int off = (j * kSplitThreads + tid) * 4;
-            if (ABL & kSieveKeyed24) {  // 24-bit words, 4 in 12 bytes (k_event_key, k24)
-                const unsigned char *src =
-                    tq == a.dummy ? reinterpret_cast<const unsigned char *>(a.zero24)
-                                  : reinterpret_cast<const unsigned char *>(a.keyed_base) +
-                                        (((size_t)(reinterpret_cast<const unsigned char *>(tq) -
-                                                   reinterpret_cast<const unsigned char *>(a.keyed_base))) >> 2) * 3u;
-                const v3u w = __builtin_nontemporal_load(
-                    (const __attribute__((address_space(1))) v3u *)(src + (size_t)off * 3u));
-                const uint32_t kk[4] = {w[0] & 0xFFFFFFu, (w[0] >> 24) | ((w[1] & 0xFFFFu) << 8),
-                                        (w[1] >> 16) | ((w[2] & 0xFFu) << 16), w[2] >> 8};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    p[j * 4 + q] = 0;
-                    t[j * 4 + q] = (int)(((kk[q] >> kSieveTagShift) << 30) | (kk[q] & kSieveValueMask));
-                }
-                continue;
-            }
             if (ABL & kSieveKeyed) {  // finished words only (k_event_key)
                 const v4i tv = ld_stream4(tq + off);
 #pragma unroll
@@ -385,8 +341,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 }
                 continue;
             }
-            const v4i pv = (ABL & 8192) ? *(const g_v4i *)(pp + off) : ld_stream4(pp + off);
-            const v4i tv = (ABL & 8192) ? *(const g_v4i *)(tq + off) : ld_stream4(tq + off);
+            const v4i pv = ld_stream4(pp + off);
+            const v4i tv = ld_stream4(tq + off);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 p[j * 4 + q] = pv[q];
@@ -409,71 +365,38 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             const uint32_t q = (uint32_t)p[e] - pid_off;
             qs[e] = q;
             const uint32_t d = min((uint32_t)t[e] - toa_lo, toa_cap);
-            // bucket of d: linear (d >> shift), or log-linear: s = max(0,
-            // floor(log2 d) - M), bucket (s << M) + (d >> s), width 2^s
-            uint32_t bk;
-            if (ABL & kSieveToaLog) {
-                const int sh = max(0, 31 - (int)__builtin_clz(d | 1u) - toa_m);
-                bk = ((uint32_t)sh << toa_m) + (d >> sh);
-                dc[e] = d & ((1u << sh) - 1u);
-            } else {
-                bk = d >> a.toa_shift;
-                dc[e] = d;
-            }
-            if (ABL & 8) {
-                w[e] = q ^ d;
-                tw[e] = d & 0xFFFu;
-            } else {
-                w[e] = lds_at(sm, o_pc4 + ((q & cmask) << 2));
-                tw[e] = lds_at(sm, o_tt4 + (bk << 2));
-            }
+            dc[e] = d;
+            w[e] = lds_at(sm, o_pc4 + ((q & cmask) << 2));
+            tw[e] = lds_at(sm, o_tt4 + ((d >> a.toa_shift) << 2));
         }
     };
     // stage 2b: tag check, one gather per event (a table hit or an
     // out-of-range pixel loads out of range: no request, returns 0); w -> the
     // table word of hits (0 otherwise), qs -> the gathered word
-    // PACK (ABL & 65536): the TOA bin is computed here and kept in the hit
-    // word's tag bits (free once the tag has been checked; the gathered words
-    // have tag 0), so dc / tw die here and bin() reads one word per event
-    auto finish = [&](uint32_t (&w)[kEPT], uint32_t (&qs)[kEPT], const uint32_t (&dc)[kEPT],
-                      const uint32_t (&tw)[kEPT]) __attribute__((always_inline)) {
+    auto finish = [&](uint32_t (&w)[kEPT], uint32_t (&qs)[kEPT]) __attribute__((always_inline)) {
         if (ABL & kSieveKeyed) return;
 #pragma unroll
         for (int e = 0; e < kEPT; ++e) {
             const unsigned long long hit =
                 __builtin_amdgcn_ballot_w64(((w[e] >> kSieveTagShift) & 0xFFu) == (qs[e] >> a.cbits));
             uint32_t off = vsel(hit, kOOBi, min(qs[e], Lc) << 2);
-            if (ABL & 16) off = kOOB | (off & 4u);
-            if (ABL & 32) off = off & 4u;
-            if (ABL & 131072) off = (off & 0x80000000u) | (off & 0xFFFCu);  // gathers confined to 64 KB
-            if (ABL & 65536) {
-                // T <= kSieveMaxT (254): bins >= 255 (past the edges) stay dropped
-                const uint32_t b = min((tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u), 255u);
-                w[e] = vsel(hit, w[e] & ~(0xFFu << kSieveTagShift), 0u) | (b << kSieveTagShift);
-            } else {
-                w[e] = vsel(hit, w[e], 0u);
-            }
-            qs[e] = (ABL & 2) ? (off & 0x3u) : __builtin_amdgcn_raw_buffer_load_b32(glut, (int)off, 0, 0);
+            if (LDE_DIAG(ABL & 131072)) off = (off & 0x80000000u) | (off & 0xFFFCu);  // gathers in 64 KB
+            w[e] = vsel(hit, w[e], 0u);
+            qs[e] = LDE_DIAG(ABL & 2) ? (off & 0x3u) : __builtin_amdgcn_raw_buffer_load_b32(glut, (int)off, 0, 0);
         }
     };
     // stage 3: bin, in two halves of four events per lane.  Hot lanes add 1
     // to their LDS row (the others to a lane-private dummy); cold keys are
     // compacted into the wave's 256-word LDS staging area (the others write a
-    // dummy) and leave as one 16-byte store per lane into the wave's own
+    // dummy) and leave as one 12-byte store per lane into the wave's own
     // sub-region of the block's cold region, at an SGPR cursor (no atomics).
     // The staged words are read back right away but stored one half later,
     // so that read's LDS latency is not waited for.  Staging words are reset
     // to -1, so the <= 3 pad keys of round4(count) are dropped by the sort.
     v4u pend_kv = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     uint32_t pend_off = kOOB;
-    // ABL 2048 (exact): both halves' stores wait for flush(), issued after the
-    // next chunk's gathers and loads, so that waiting for those (vmcnt is in
-    // order and counts stores) never waits for a store's acknowledgement
-    v4u pend_kv1 = pend_kv;
-    uint32_t pend_off1 = kOOB;
     uint32_t wcur = 0;  // this wave's cold keys so far (wave-uniform)
-    uint32_t hcnt = 0;  // (pair) this wave's hot events (wave-uniform, wraps like the check)
-    uint32_t junk = 0;  // ABL 512/1024 probes: extra VALU / LDS work per event
+    uint32_t junk = 0;  // diagnostic probes: folded words
     auto bin = [&](const uint32_t (&ws)[kEPT], const uint32_t (&g)[kEPT], const uint32_t (&dc)[kEPT],
                    const uint32_t (&tw)[kEPT]) __attribute__((always_inline)) {
 #pragma unroll
@@ -482,36 +405,16 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
 #pragma unroll
             for (int e = h * kEPT / 2; e < (h + 1) * kEPT / 2; ++e) {
                 const uint32_t v = ws[e] | g[e];
-                if (ABL & 512) {
-#pragma unroll
-                    for (int x = 0; x < 8; ++x) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(junk) : "v"(v));
-                }
-                if (ABL & 1024) junk += lds_at(sm, dum4 ^ ((v & 1u) << 2));
                 const uint32_t b = (ABL & kSieveKeyed) ? 0u
-                                   : (ABL & 65536) ? ((v >> kSieveTagShift) & 0xFFu)
-                                                   : (tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u);
+                                                        : (tw[e] & 0xFFu) + (((dc[e] & wmask) >= (tw[e] >> 8)) ? 1u : 0u);
                 const uint32_t fl = v >> 30;
                 // hot rows start at LDS byte 0, so the scaled key is the hot
                 // counter's address; cold keys leave scaled by 4 as well
-                uint32_t k4 = ((v & kSieveValueMask) + b) << 2;
+                const uint32_t k4 = ((v & kSieveValueMask) + b) << 2;
                 // lane masks straight from the compares (no bool round trip)
                 const unsigned long long inb = __builtin_amdgcn_ballot_w64(b < T);
-                unsigned long long bal = inb & __builtin_amdgcn_ballot_w64(fl == 2u);
-                unsigned long long hm = inb & __builtin_amdgcn_ballot_w64(fl == 3u);
-                if (windowed) {
-                    // a hot screen's bin outside the rows' window: a cold key
-                    // screen * T + bin, the screen from the row table (rare;
-                    // the word value is row * hw, an exact float quotient)
-                    const unsigned long long oow = hm & __builtin_amdgcn_ballot_w64(b - hlo >= hw);
-                    if (oow) {
-                        const uint32_t row = min((uint32_t)((float)(v & kSieveValueMask) * a.hot_inv_w + 0.5f),
-                                                 (uint32_t)a.hot_rows - 1u);
-                        const uint32_t ck4 = ((uint32_t)s_rs[row] * T + b) << 2;
-                        k4 = vsel(oow, ck4, k4);
-                        bal |= oow;
-                        hm &= ~oow;
-                    }
-                }
+                const unsigned long long bal = inb & __builtin_amdgcn_ballot_w64(fl == 2u);
+                const unsigned long long hm = inb & __builtin_amdgcn_ballot_w64(fl == 3u);
                 const uint32_t pos4 = (lanes_below(bal) + o_stg_w + tot) << 2;
                 tot += (uint32_t)__popcll(bal);
                 lds_at(sm, vsel(bal, pos4, dum4)) = k4;
@@ -519,67 +422,31 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 // hot counter (hot lanes), the tile's cold-key count (cold
                 // lanes) or the lane's dummy word (the rest)
                 const uint32_t tidx4 = vsel(bal, ((k4 >> tsh) << 2) + o_tcnt4, dum4);
-                if (pair) {
-                    // counter i < hot_words: low half of LDS word i; else the
-                    // high half of word i - hot_words (neighbouring bins stay
-                    // in neighbouring words, i.e. banks)
-                    hcnt += (uint32_t)__popcll(hm);
-                    const bool up = k4 >= hw4;
-                    const uint32_t aidx4 = vsel(hm, up ? k4 - hw4 : k4, tidx4);
-                    const uint32_t add = vsel(hm, up ? 0x10000u : 1u, 1u);
-                    __hip_atomic_fetch_add(&lds_at(sm, aidx4), add, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                } else {
-                    const uint32_t aidx4 = (ABL & 1) ? tidx4 : vsel(hm, k4, tidx4);
-                    __hip_atomic_fetch_add(&lds_at(sm, aidx4), 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
+                const uint32_t aidx4 = LDE_DIAG(ABL & 1) ? tidx4 : vsel(hm, k4, tidx4);
+                __hip_atomic_fetch_add(&lds_at(sm, aidx4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             const uint32_t res = (tot + 3u) & ~3u;
             // the previous half's keys leave now (their LDS read is long done)
-            if (ABL & 2048) {
-            } else if (ABL & 64) {  // diagnostic: only the lanes that hold keys issue the store
-                if (pend_off != kOOB) store_keys(pend_kv, pend_off);
-            } else if (ABL & 128) {  // diagnostic: every other half stores (keys lost)
-                if (h == 0) store_keys(pend_kv, pend_off);
-            } else if (!(ABL & 4)) {
-                store_keys(pend_kv, pend_off);
-            }
+            if (!LDE_DIAG(ABL & 4)) store_keys(pend_kv, pend_off);
             else sm[o_dum + lane] += pend_kv[0] ^ pend_off;
             __builtin_amdgcn_wave_barrier();
             uint4 *slot = reinterpret_cast<uint4 *>(sm + o_stg_w + 4u * (uint32_t)lane);
             const uint4 kv = *slot;
             *slot = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
             __builtin_amdgcn_wave_barrier();
-            const uint32_t off = 4u * (uint32_t)lane < res ? (wave_base + wcur + 4u * (uint32_t)lane) << 2 : kOOB;
-            if ((ABL & 2048) && h == 1) {
-                pend_kv1 = v4u{kv.x, kv.y, kv.z, kv.w};
-                pend_off1 = off;
-            } else {
-                pend_kv = v4u{kv.x, kv.y, kv.z, kv.w};
-                pend_off = off;
-            }
+            pend_off = 4u * (uint32_t)lane < res ? (wave_base + wcur + 4u * (uint32_t)lane) << 2 : kOOB;
+            pend_kv = v4u{kv.x, kv.y, kv.z, kv.w};
             wcur += res;
         }
     };
-    auto flush = [&]() __attribute__((always_inline)) {
-        if (ABL & 2048) {
-            store_keys(pend_kv, pend_off);
-            store_keys(pend_kv1, pend_off1);
-            pend_off = pend_off1 = kOOB;
-        }
-    };
 
-    // ---- pipeline (register sets A/B and X/Y alternate).
-    // ABL 256 (LDE_EARLY_GATHER): iteration i issues chunk i+1's gathers, bins chunk i
-    // (gathered one iteration ago), probes chunk i+2 and streams in chunk i+4,
-    // so a table-miss gather has a whole iteration to return; the probe's LDS
-    // latency is what is left exposed.  Otherwise chunk i is binned while
-    // chunk i+1 is probed (before) and gathered (after).
+    // ---- pipeline (register sets A/B and X/Y alternate): chunk i is binned
+    // while chunk i+1 is probed (before) and gathered (after), chunks i+2..3
+    // are in flight and chunk i+4..5's descriptors are fetched
     int pA[kEPT], tA[kEPT], pB[kEPT], tB[kEPT];
     uint32_t wsX[kEPT], gX[kEPT], dX[kEPT], twX[kEPT];
     uint32_t wsY[kEPT], gY[kEPT], dY[kEPT], twY[kEPT];
-    if ((ABL & 16384) && cb < ce) {
+    if (LDE_DIAG(ABL & 16384) && cb < ce) {
         // decomposition probe: the main loop with bin() replaced by folding
         // the chunk's words into junk (+ finish() when ABL & 32768)
         auto eat = [&](const uint32_t (&ws)[kEPT], const uint32_t (&g)[kEPT], const uint32_t (&dc)[kEPT],
@@ -593,23 +460,23 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         dA = fetch(cb + 2);
         dB = fetch(cb + 3);
         probe(pA, tA, wsX, gX, dX, twX);
-        if (ABL & 32768) finish(wsX, gX, dX, twX);
+        if (ABL & 32768) finish(wsX, gX);
         load(dA, pA, tA);
         dA = fetch(cb + 4);
         for (long long c = cb; c < ce; c += 2) {
             probe(pB, tB, wsY, gY, dY, twY);
             eat(wsX, gX, dX, twX);
-            if (ABL & 32768) finish(wsY, gY, dY, twY);
+            if (ABL & 32768) finish(wsY, gY);
             load(dB, pB, tB);
             dB = fetch(c + 5);
             if (c + 1 >= ce) break;
             probe(pA, tA, wsX, gX, dX, twX);
             eat(wsY, gY, dY, twY);
-            if (ABL & 32768) finish(wsX, gX, dX, twX);
+            if (ABL & 32768) finish(wsX, gX);
             load(dA, pA, tA);
             dA = fetch(c + 6);
         }
-    } else if ((ABL & 4096) && cb < ce) {  // stream skeleton: loads only
+    } else if (LDE_DIAG(ABL & 4096) && cb < ce) {  // stream skeleton: loads only
         uint32_t dA = fetch(cb), dB = fetch(cb + 1);
         load(dA, pA, tA);
         load(dB, pB, tB);
@@ -625,32 +492,6 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             load(dB, pB, tB);
             dB = fetch(c + 5);
         }
-    } else if ((ABL & 256) && cb < ce) {
-        uint32_t dA = fetch(cb), dB = fetch(cb + 1);
-        load(dA, pA, tA);
-        load(dB, pB, tB);
-        dA = fetch(cb + 2);
-        dB = fetch(cb + 3);
-        probe(pA, tA, wsX, gX, dX, twX);  // chunk cb
-        finish(wsX, gX, dX, twX);
-        load(dA, pA, tA);  // chunk cb + 2
-        dA = fetch(cb + 4);
-        probe(pB, tB, wsY, gY, dY, twY);  // chunk cb + 1
-        load(dB, pB, tB);  // chunk cb + 3
-        dB = fetch(cb + 5);
-        for (long long c = cb; c < ce; c += 2) {
-            finish(wsY, gY, dY, twY);                   // chunk c + 1
-            bin(wsX, gX, dX, twX);             // chunk c
-            probe(pA, tA, wsX, gX, dX, twX);  // chunk c + 2
-            load(dA, pA, tA);                  // chunk c + 4
-            dA = fetch(c + 6);
-            if (c + 1 >= ce) break;
-            finish(wsX, gX, dX, twX);                   // chunk c + 2
-            bin(wsY, gY, dY, twY);             // chunk c + 1
-            probe(pB, tB, wsY, gY, dY, twY);  // chunk c + 3
-            load(dB, pB, tB);                  // chunk c + 5
-            dB = fetch(c + 7);
-        }
     } else if (cb < ce) {
         uint32_t dA = fetch(cb), dB = fetch(cb + 1);
         load(dA, pA, tA);
@@ -658,22 +499,20 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         dA = fetch(cb + 2);
         dB = fetch(cb + 3);
         probe(pA, tA, wsX, gX, dX, twX);
-        finish(wsX, gX, dX, twX);
+        finish(wsX, gX);
         load(dA, pA, tA);
         dA = fetch(cb + 4);
         for (long long c = cb; c < ce; c += 2) {
             probe(pB, tB, wsY, gY, dY, twY);  // chunk c + 1
             bin(wsX, gX, dX, twX);             // chunk c
-            finish(wsY, gY, dY, twY);
+            finish(wsY, gY);
             load(dB, pB, tB);  // chunk c + 3
-            flush();           // chunk c's keys
             dB = fetch(c + 5);
             if (c + 1 >= ce) break;
             probe(pA, tA, wsX, gX, dX, twX);  // chunk c + 2
             bin(wsY, gY, dY, twY);             // chunk c + 1
-            finish(wsX, gX, dX, twX);
+            finish(wsX, gX);
             load(dA, pA, tA);  // chunk c + 4
-            flush();           // chunk c + 1's keys
             dA = fetch(c + 6);
         }
     }
@@ -711,95 +550,28 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
                 }
             }
             probe(p, t, wsX, gX, dX, twX);
-            finish(wsX, gX, dX, twX);
+            finish(wsX, gX);
             bin(wsX, gX, dX, twX);
-            flush();
         }
     }
     // the last half's keys
-    if (!(ABL & 4)) store_keys(pend_kv, pend_off);
-    if (ABL & (512 | 1024 | 4096 | 16384)) sm[o_dum + lane] = junk;
+    if (!LDE_DIAG(ABL & 4)) store_keys(pend_kv, pend_off);
+    if (LDE_DIAG(ABL & (4096 | 16384))) sm[o_dum + lane] = junk;
     if (lane == 0) a.cold_cnt[(size_t)blockIdx.x * (kSplitThreads / 64) + (tid >> 6)] = wcur;
     __syncthreads();
     const unsigned long long t_stream = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     // hot rows leave as u16 counts (half the bytes written here and read by
     // k_hot_reduce_scan) unless a count of this block exceeds 0xFFFF
     uint32_t *dst = a.hot_part + (size_t)blockIdx.x * a.hot_words;
-    bool packed = false;
-    if (pair) {
-        // u16 pairs: a counter that wrapped lost 65536 and carried 1 into its
-        // neighbour (or out of the word), so the counters' sum is the hot
-        // event count minus 65535 or 65536 per wrap (mod 2^32, exact below
-        // 2^32 events per block): equal iff nothing wrapped
-        if (lane == 0) atomicAdd(&sm[o_cur + 2], hcnt);
-        uint32_t s = 0;
-        for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(sm + i);
-            s += (v.x & 0xFFFFu) + (v.x >> 16) + (v.y & 0xFFFFu) + (v.y >> 16) + (v.z & 0xFFFFu) +
-                 (v.z >> 16) + (v.w & 0xFFFFu) + (v.w >> 16);
-        }
-        atomicAdd(&sm[o_cur + 3], s);
-        __syncthreads();
-        const bool wrapped = sm[o_cur + 2] != sm[o_cur + 3];
-        // u16 counts in counter order (row stride hot_words * 2): the low
-        // halves of 8 words, then their high halves hot_words counters on
-        uint4 *d4 = reinterpret_cast<uint4 *>(dst);
-        for (int i = tid * 8; i < a.hot_words; i += kSplitThreads * 8) {
-            const uint4 v0 = *reinterpret_cast<const uint4 *>(sm + i);
-            const uint4 v1 = *reinterpret_cast<const uint4 *>(sm + i + 4);
-            auto lo2 = [](uint32_t x, uint32_t y) { return (x & 0xFFFFu) | (y << 16); };
-            auto hi2 = [](uint32_t x, uint32_t y) { return (x >> 16) | (y & 0xFFFF0000u); };
-            d4[i >> 3] = wrapped ? make_uint4(0, 0, 0, 0)
-                                 : make_uint4(lo2(v0.x, v0.y), lo2(v0.z, v0.w), lo2(v1.x, v1.y), lo2(v1.z, v1.w));
-            d4[(a.hot_words + i) >> 3] =
-                wrapped ? make_uint4(0, 0, 0, 0)
-                        : make_uint4(hi2(v0.x, v0.y), hi2(v0.z, v0.w), hi2(v1.x, v1.y), hi2(v1.z, v1.w));
-        }
-        if (tid == 0) a.hot_fmt[blockIdx.x] = 1u;
-        if (wrapped) {
-            // rare (a bin past 65535 events of one block): this block's hot
-            // events again, straight into the window with global atomics
-            // (its cold keys are already out; k_hot_reduce_scan adds the
-            // other blocks' rows with atomics too)
-            if (tid == 0 && a.wraps) atomicAdd(a.wraps, 1u);
-            const SegDesc *segs = (!GCT && a.karg) ? s_seg : a.segs;
-            for (long long c = cb; c < ce; ++c) {
-                int lo = 0, hi = a.n_segs - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
-                }
-                const SegDesc sd = segs[lo];
-                const long long base = (c - sd.chunk0) * kChunk;
-                for (int e = tid; e < kChunk; e += kSplitThreads) {
-                    const long long ei = base + e;
-                    if (ei >= sd.n) break;
-                    const uint32_t q = (uint32_t)sd.pid[ei] - pid_off;
-                    const uint32_t d = min((uint32_t)sd.toa[ei] - toa_lo, toa_cap);
-                    const uint32_t w = lds_at(sm, o_pc4 + ((q & cmask) << 2));
-                    const uint32_t tw = lds_at(sm, o_tt4 + ((d >> a.toa_shift) << 2));
-                    const bool hit = ((w >> kSieveTagShift) & 0xFFu) == (q >> a.cbits);
-                    const uint32_t v = hit ? w : a.glut[min(q, Lc)];
-                    const uint32_t b = (tw & 0xFFu) + (((d & wmask) >= (tw >> 8)) ? 1u : 0u);
-                    if ((v >> 30) == 3u && b < T) {
-                        const uint32_t row = (v & kSieveValueMask) / T;
-                        atomicAdd(a.hist + (size_t)a.row_screen[row] * T + b, 1u);
-                    }
-                }
-            }
-        }
-    } else if (a.hot_fmt && (a.hot_words & 7) == 0) {
-        uint32_t big = 0;
-        for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(sm + i);
-            big |= (v.x | v.y | v.z | v.w) >> 16;
-        }
-        if (big) sm[o_cur + 1] = 1u;  // benign race: every writer stores 1
-        __syncthreads();
-        packed = sm[o_cur + 1] == 0u;
+    uint32_t big = 0;
+    for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(sm + i);
+        big |= (v.x | v.y | v.z | v.w) >> 16;
     }
-    if (pair) {
-    } else if (packed) {
+    if (big) sm[o_cur + 1] = 1u;  // benign race: every writer stores 1
+    __syncthreads();
+    const bool packed = sm[o_cur + 1] == 0u;
+    if (packed) {
         uint4 *d16 = reinterpret_cast<uint4 *>(dst);  // 8 counts per 16 bytes
         for (int i = tid * 8; i < a.hot_words; i += kSplitThreads * 8) {
             const uint4 v0 = *reinterpret_cast<const uint4 *>(sm + i);
@@ -811,7 +583,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         for (int i = tid * 4; i < a.hot_words; i += kSplitThreads * 4)
             *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(sm + i);
     }
-    if (!pair && a.hot_fmt && tid == 0) a.hot_fmt[blockIdx.x] = packed ? 1u : 0u;
+    if (tid == 0) a.hot_fmt[blockIdx.x] = packed ? 1u : 0u;
     if (a.trace) {  // diagnostic: per-block timeline (LDE_SIEVE_TRACE)
         __syncthreads();
         if (tid < 3)
@@ -823,12 +595,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         a.cold_tcnt[((size_t)blockIdx.x * kColdGroups + g) * a.n_tiles + t] =
             sm[o_tcnt + g * align4(a.n_tiles) + t];
     }
-    if (a.tail_release & 1) {
-        // write this XCD's dirty lines back while other blocks still stream,
-        // instead of all at the end-of-kernel release (LDE_SIEVE_TAIL_RELEASE)
-        __syncthreads();
-        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    }
+    // write this XCD's dirty lines back while other blocks still stream,
+    // instead of all at the end-of-kernel release (round 2: -10 to -15 us)
+    __syncthreads();
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 }
 
 // ---------------------------------------------------------------------------
@@ -872,10 +642,9 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
                                                    : row[i];
             }
         }
-        const int j = i - c.hot_lo;  // words [0, hot_lo) hold no row
-        if (sum && j >= 0) {
-            const int row = j / c.hot_w;
-            atomicAdd(c.hist + (size_t)c.row_screen[row] * c.T + (i - row * c.hot_w), sum);
+        if (sum) {
+            const int row = i / c.T;
+            atomicAdd(c.hist + (size_t)c.row_screen[row] * c.T + (i - row * c.T), sum);
         }
         return;
     }
@@ -885,7 +654,7 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
     for (int r0 = 0; r0 < rows; r0 += 256) {
         const int r = r0 + threadIdx.x;
         uint32_t v = r < rows ? c.tcnt[(size_t)r * c.n_tiles + t] : 0u;
-        if (c.pad8) v = (v + 7u) & ~7u;  // k_cold_sort_a: 16-byte aligned (row, tile) ranges
+        v = (v + 7u) & ~7u;  // k_cold_sort_a: 16-byte aligned (row, tile) ranges
         uint32_t tot;
         const uint32_t ex = block_exclusive_scan(v, s_w, &tot);
         if (r < rows) c.boff[(size_t)r * c.n_tiles + t] = carry + ex;
@@ -897,10 +666,7 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
 
 constexpr int kSortThreads = kSortThreadsHost;  // one wave per sieve wave
 constexpr int kSortWaves = kSortThreads / 64;
-constexpr int kSortKPT = 16;                           // keys per lane per piece
-constexpr int kSortPiece = kSortThreads * kSortKPT;    // 8192
-// the piece's sorted image (also the scratch of plan_items)
-constexpr int kSortImage = align4(kSortPiece > 2 * (kMaxTiles + 1) ? kSortPiece : 2 * (kMaxTiles + 1));
+constexpr int kSortKPT = 48;                     // keys per lane per piece
 
 // Balanced pass-B items (tile, first key, end key, tile has one item) of the
 // tile-major key array: a tile with n keys gets ceil(n / item_keys) items.
@@ -957,325 +723,6 @@ __device__ void plan_items(const uint32_t *__restrict__ tile_total, int n_tiles,
     __syncthreads();
 }
 
-// One 1024-thread block per sieve block.  Sort wave w reads sieve wave w's
-// sub-region of the block's cold region (keys scaled by 4, written in
-// multiples of 4 with -1 pads), 1024 keys per wave per piece, so the load
-// address is a plain offset.  Per piece: rank each key among its wave's keys
-// of the same tile (wave-private LDS counters: ~16x less same-address
-// contention than block counters), turn the counters into per-(wave, tile)
-// bases of the piece's tile-sorted LDS image, scatter, and write each tile
-// run as u16 tile-local keys to its exact place in the tile-major array (the
-// sieve's per-tile counts, scanned by k_cold_scan / k_cold_plan).
-size_t cold_sort_smem(int n_tiles) {
-    const size_t nt4 = (size_t)align4(n_tiles);
-    static_assert(64 % kSortWaves == 0, "tiles per wave in the prefix scan");
-    return 4 * ((size_t)kSortImage + (size_t)kSortWaves * nt4 + 3 * nt4 + 32);
-}
-
-template <int TB>
-__global__ __launch_bounds__(kSortThreads) void k_cold_sort(ColdArgs c) {
-    const uint32_t *__restrict__ cold = c.cold;
-    const long long stride = c.stride, cap = c.cap;
-    const uint32_t *__restrict__ cold_cnt = c.cold_cnt;
-    const uint32_t *__restrict__ boff = c.boff;
-    const int n_tiles = c.n_tiles;
-    uint16_t *__restrict__ out = c.keys;
-    constexpr uint32_t MASK = (1u << TB) - 1u;
-    constexpr int SH = TB + 2;  // keys are scaled by 4
-    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
-    const int nt4 = align4(n_tiles);
-    uint32_t *s_sorted = sm;
-    uint32_t *s_cnt = sm + kSortImage;             // [wave][tile]: count -> base
-    uint32_t *s_pos = s_cnt + kSortWaves * nt4;    // [tile] next global position
-    uint32_t *s_delta = s_pos + nt4;               // [tile] global - LDS position
-    uint32_t *s_tot = s_delta + nt4;               // [tile] piece total -> run base
-    uint32_t *s_w = s_tot + nt4;
-    const int tid = threadIdx.x;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave-uniform: SGPR buffer descriptors
-    // block = (sieve block, wave group); boff / tcnt rows are (block, group)
-    const int b = blockIdx.x / kColdGroups, grp = blockIdx.x % kColdGroups;
-    const int row = blockIdx.x;
-    constexpr int NW = kSplitThreads / 64;  // sieve waves per sieve block
-    const uint32_t capw = (uint32_t)(cap / NW);
-    const int sw = grp * kSortWaves + wv;   // my sieve wave
-    const uint32_t n_w = cold_cnt[(size_t)b * NW + sw];  // its keys (incl. pads)
-    // the items of pass B (block 0, in the LDS of the sorted image)
-    if (row == 0)
-        plan_items(c.tile_total, n_tiles, c.item_keys, c.items, c.item_count, c.max_items, s_w,
-                   s_sorted, s_sorted + kMaxTiles + 1);
-    // tile bases of the tile-major array: exclusive scan of the tile totals
-    {
-        constexpr int TPT = (kMaxTiles + kSortThreads - 1) / kSortThreads;
-        uint32_t tt[TPT], sum = 0;
-#pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-            const int t = tid * TPT + q;
-            tt[q] = t < n_tiles ? c.tile_total[t] : 0u;
-            sum += tt[q];
-        }
-        uint32_t total;
-        uint32_t run = block_exclusive_scan(sum, s_w, &total);
-#pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-            const int t = tid * TPT + q;
-            if (t < n_tiles) s_pos[t] = run + boff[(size_t)row * n_tiles + t];
-            run += tt[q];
-        }
-    }
-    __syncthreads();
-    if (lane == 0) s_w[wv] = (n_w + 64 * kSortKPT - 1) / (64 * kSortKPT);
-    __syncthreads();
-    uint32_t npieces = 0;
-#pragma unroll
-    for (int q = 0; q < kSortWaves; ++q) npieces = max(npieces, s_w[q]);
-    __syncthreads();  // s_w is the scans' scratch below
-    const __amdgpu_buffer_rsrc_t rs =
-        make_rsrc(cold + (size_t)b * (size_t)stride + (size_t)sw * capw, n_w * 4u);
-    uint32_t *my_cnt = s_cnt + wv * nt4;
-    // the next piece's keys are requested before the current piece is sorted
-    v4u nk[kSortKPT / 4];
-    auto fetch = [&](uint32_t p) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < kSortKPT / 4; ++j) {
-            const uint32_t e0 = p * (uint32_t)(64 * kSortKPT) + (uint32_t)j * 256u + (uint32_t)lane * 4u;
-            nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
-        }
-    };
-    if (npieces) fetch(0);
-    for (uint32_t p = 0; p < npieces; ++p) {
-        for (int i = lane; i < nt4; i += 64) my_cnt[i] = 0;
-        uint32_t key[kSortKPT], rank[kSortKPT];
-#pragma unroll
-        for (int j = 0; j < kSortKPT / 4; ++j) {
-            const uint32_t e0 = p * (uint32_t)(64 * kSortKPT) + (uint32_t)j * 256u + (uint32_t)lane * 4u;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n_w ? nk[j][q] : 0xFFFFFFFFu;
-        }
-        if (p + 1 < npieces) fetch(p + 1);
-        __builtin_amdgcn_wave_barrier();  // my counters zeroed before the wave ranks
-#pragma unroll
-        for (int e = 0; e < kSortKPT; ++e) {
-            rank[e] = 0;
-            if (key[e] != 0xFFFFFFFFu)
-                rank[e] = __hip_atomic_fetch_add(my_cnt + (key[e] >> SH), 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        __syncthreads();
-        // per tile: wave counts -> wave bases inside the tile's run (a 16-lane
-        // shuffle scan per tile, 4 tiles per wave at a time), tile totals
-        {
-            constexpr int TPW = 64 / kSortWaves;  // tiles per wave and pass
-            const int g = lane / kSortWaves, w2 = lane % kSortWaves;
-            for (int t0 = wv * TPW; t0 < n_tiles; t0 += kSortWaves * TPW) {
-                const int t = t0 + g;
-                const uint32_t v = t < n_tiles ? s_cnt[w2 * nt4 + t] : 0u;
-                uint32_t x = v;
-#pragma unroll
-                for (int d = 1; d < kSortWaves; d <<= 1) {
-                    const uint32_t y = __shfl_up(x, d, kSortWaves);
-                    if (w2 >= d) x += y;
-                }
-                if (t < n_tiles) {
-                    s_cnt[w2 * nt4 + t] = x - v;
-                    if (w2 == kSortWaves - 1) s_tot[t] = x;
-                }
-            }
-        }
-        __syncthreads();
-        // runs of the piece's tile-sorted image: exclusive scan of the totals
-        constexpr int TPT = (kMaxTiles + kSortThreads - 1) / kSortThreads;
-        uint32_t tot[TPT], sum = 0;
-#pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-            const int t = tid * TPT + q;
-            tot[q] = t < n_tiles ? s_tot[t] : 0u;
-            sum += tot[q];
-        }
-        uint32_t total;
-        uint32_t run = block_exclusive_scan(sum, s_w, &total);
-#pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-            const int t = tid * TPT + q;
-            if (t < n_tiles) {
-                s_tot[t] = run;  // now the run's base in the image
-                s_delta[t] = s_pos[t] - run;
-                s_pos[t] += tot[q];
-            }
-            run += tot[q];
-        }
-        __syncthreads();
-        for (int i = tid; i < kSortWaves * nt4; i += kSortThreads) {
-            const int t = i % nt4;
-            if (t < n_tiles) s_cnt[i] += s_tot[t];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < kSortKPT; ++e)
-            if (key[e] != 0xFFFFFFFFu) s_sorted[my_cnt[key[e] >> SH] + rank[e]] = key[e];
-        __syncthreads();
-        for (uint32_t i = (uint32_t)tid; i < total; i += kSortThreads) {
-            const uint32_t k = s_sorted[i];
-            if (!(LDE_DIAG(c.ablate) & 1)) out[s_delta[k >> SH] + i] = (uint16_t)((k >> 2) & MASK);
-        }
-        __syncthreads();
-    }
-}
-
-// Wave-independent variant of k_cold_sort: same block <-> region mapping and
-// the same tile-major output, but every sort wave sorts its own pieces of
-// kWsPiece keys in wave-private LDS with no block barrier after the set-up.
-// A wave's run of tile t is placed by one LDS atomicAdd on the block's tile
-// cursor s_pos[t] (pass B counts keys per tile, so the order of the runs
-// inside a (block, tile) range does not matter).  Per key: one LDS count
-// atomic, one returning LDS atomic for its slot, the scatter into the wave's
-// image, one sequential read back and one read of the run's offset -- about
-// half the LDS instructions of the block-cooperative sort, no barrier stalls.
-constexpr int kWsKPT = 32;                 // keys per lane per wave piece
-constexpr int kWsPiece = 64 * kWsKPT;      // 2048 keys
-size_t cold_sort_w_smem(int n_tiles) {
-    const size_t nt4 = (size_t)align4(n_tiles);
-    return 4 * (nt4 + 32 + (size_t)kSortWaves * ((size_t)kWsPiece + 2 * nt4));
-}
-
-template <int TB>
-__global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_cold_sort_w(ColdArgs c) {
-    const int n_tiles = c.n_tiles;
-    uint16_t *__restrict__ out = c.keys;
-    constexpr uint32_t MASK = (1u << TB) - 1u;
-    constexpr int SH = TB + 2;  // keys are scaled by 4
-    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
-    const int nt4 = align4(n_tiles);
-    const int tid = threadIdx.x;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave-uniform: SGPR buffer descriptors
-    uint32_t *s_pos = sm;         // [tile] the block's next global position
-    uint32_t *s_w = sm + nt4;     // scan scratch
-    uint32_t *s_wave = s_w + 32;  // per wave: image | base | delta
-    uint32_t *img = s_wave + wv * (kWsPiece + 2 * nt4);
-    uint32_t *base = img + kWsPiece;
-    uint32_t *dlt = base + nt4;
-    const int b = blockIdx.x / kColdGroups, grp = blockIdx.x % kColdGroups;
-    const int row = blockIdx.x;
-    constexpr int NW = kSplitThreads / 64;
-    const uint32_t capw = (uint32_t)(c.cap / NW);
-    const int sw = grp * kSortWaves + wv;
-    const uint32_t n_w = c.cold_cnt[(size_t)b * NW + sw];
-    // the items of pass B (block 0; the wave images are its scratch)
-    if (row == 0)
-        plan_items(c.tile_total, n_tiles, c.item_keys, c.items, c.item_count, c.max_items, s_w,
-                   s_wave, s_wave + kMaxTiles + 1);
-    {
-        constexpr int TPT = (kMaxTiles + kSortThreads - 1) / kSortThreads;
-        uint32_t tt[TPT], sum = 0;
-#pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-            const int t = tid * TPT + q;
-            tt[q] = t < n_tiles ? c.tile_total[t] : 0u;
-            sum += tt[q];
-        }
-        uint32_t total;
-        uint32_t run = block_exclusive_scan(sum, s_w, &total);
-#pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-            const int t = tid * TPT + q;
-            if (t < n_tiles) s_pos[t] = run + c.boff[(size_t)row * n_tiles + t];
-            run += tt[q];
-        }
-    }
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t rs =
-        make_rsrc(c.cold + (size_t)b * (size_t)c.stride + (size_t)sw * capw, n_w * 4u);
-    const uint32_t npieces = (n_w + kWsPiece - 1) / kWsPiece;
-    const int tpl = (n_tiles + 63) / 64;  // tiles per lane in the wave scan
-    const int t0 = lane * tpl;
-    v4u nk[kWsKPT / 4];
-    auto fetch = [&](uint32_t p) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < kWsKPT / 4; ++j) {
-            const uint32_t e0 = p * (uint32_t)kWsPiece + (uint32_t)j * 256u + (uint32_t)lane * 4u;
-            nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
-        }
-    };
-    if (npieces && !(LDE_DIAG(c.ablate) & 2)) fetch(0);
-    for (uint32_t p = 0; p < npieces; ++p) {
-        for (int i = lane; i < nt4; i += 64) base[i] = 0;
-        uint32_t key[kWsKPT];
-#pragma unroll
-        for (int j = 0; j < kWsKPT / 4; ++j) {
-            const uint32_t e0 = p * (uint32_t)kWsPiece + (uint32_t)j * 256u + (uint32_t)lane * 4u;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n_w ? nk[j][q] : 0xFFFFFFFFu;
-        }
-        if (LDE_DIAG(c.ablate) & 2) {  // diagnostic: keys synthesized, not loaded
-#pragma unroll
-            for (int e = 0; e < kWsKPT; ++e)
-                key[e] = ((((uint32_t)(lane * kWsKPT + e) + p * 977u) * 2654435761u) %
-                          ((uint32_t)n_tiles << TB)) << 2;
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int e = 0; e < kWsKPT; ++e)
-            if (key[e] != 0xFFFFFFFFu)
-                __hip_atomic_fetch_add(base + (key[e] >> SH), 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-        __builtin_amdgcn_wave_barrier();
-        // counts -> run bases in the image (wave scan, tpl tiles per lane);
-        // each non-empty run reserves its place in the block's tile range
-        uint32_t lsum = 0;
-        for (int j = 0; j < tpl; ++j) {
-            const int t = t0 + j;
-            if (t < n_tiles) lsum += base[t];
-        }
-        const uint32_t inc = wave_inclusive_scan(lsum);
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        uint32_t run = inc - lsum;
-        for (int j = 0; j < tpl; ++j) {
-            const int t = t0 + j;
-            if (t < n_tiles) {
-                const uint32_t n = base[t];
-                base[t] = run;
-                if (n)
-                    dlt[t] = __hip_atomic_fetch_add(s_pos + t, n, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_WORKGROUP) - run;
-                run += n;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        // scatter: each key takes the next slot of its run (order inside a
-        // run is irrelevant), so no per-key rank is kept in registers
-#pragma unroll
-        for (int e = 0; e < kWsKPT; ++e) {
-            // the tile index is recomputed (opaque to CSE), so the count
-            // pass's LDS addresses do not stay live in registers
-            uint32_t k = key[e];
-            asm volatile("" : "+v"(k));
-            if (k != 0xFFFFFFFFu)
-                img[__hip_atomic_fetch_add(base + (k >> SH), 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP)] = k;
-        }
-        // the next piece's keys are requested once this piece's are dead (the
-        // register budget of two blocks per CU), ahead of the write-out
-        if (p + 1 < npieces && !(LDE_DIAG(c.ablate) & 2)) fetch(p + 1);
-        __builtin_amdgcn_wave_barrier();
-        // runs leave as u16 tile-local keys, four image words per lane in flight
-        for (uint32_t i0 = (uint32_t)lane; i0 < total; i0 += 256u) {
-            uint32_t k[4], d[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t i = i0 + 64u * (uint32_t)u;
-                k[u] = i < total ? img[i] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) d[u] = dlt[k[u] >> SH];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t i = i0 + 64u * (uint32_t)u;
-                if (i < total && !(LDE_DIAG(c.ablate) & 1)) out[d[u] + i] = (uint16_t)((k[u] >> 2) & MASK);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
 // Block-cooperative sort with whole 16-byte output groups (n_tiles <=
 // kSortThreads: thread t owns tile t).  The scan gives every (row, tile)
 // range a length rounded up to 8 keys, so each range starts 16-byte aligned.
@@ -1283,8 +730,8 @@ __global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4,
 // keys the tile carried over from earlier pieces; the full 8-key groups leave
 // as one 16-byte store each and the rest is carried again; the last carry of
 // each tile leaves padded with 0xFFFF (skipped by pass B).  The image holds
-// u16 tile-local keys.  Compared with k_cold_sort's per-key u16 stores into
-// short unaligned runs this issues 8x fewer store lanes and no partial lines.
+// u16 tile-local keys.  Compared with per-key u16 stores into short unaligned
+// runs (round 1) this issues 8x fewer store lanes and no partial lines.
 size_t cold_sort_a_smem(int n_tiles, int kpt) {
     const size_t nt4 = (size_t)align4(n_tiles);
     const size_t img_words = ((size_t)kSortThreads * kpt + 16 * nt4) / 2;
@@ -1295,9 +742,11 @@ size_t cold_sort_a_smem(int n_tiles, int kpt) {
     return 4 * ((size_t)align4((int)scratch) + (size_t)kSortWaves * nt4 + 5 * nt4 + 4 * nt4 + 32 + gt_words);
 }
 
-template <int TB, int KPT, bool KEY24>
+template <int TB>
 __global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void k_cold_sort_a(ColdArgs c) {
+    constexpr int KPT = kSortKPT;
+    constexpr bool KEY24 = true;  // the sieve writes 24-bit keys
     constexpr int PIECE = kSortThreads * KPT;
     const int n_tiles = c.n_tiles;
     uint16_t *__restrict__ out = c.keys;
@@ -1466,18 +915,13 @@ void k_cold_sort_a(ColdArgs c) {
         if (!(LDE_DIAG(c.ablate) & 1))
             *reinterpret_cast<uint4 *>(out + s_pos[tid]) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
     }
-    if (c.tail_release & 2) {  // this block's keys written back before the kernel ends
-        __syncthreads();
-        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    }
 }
 
 // pass B: one item = a contiguous key range of one tile
 template <int TB>
 __global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
     const uint16_t *__restrict__ keys, const uint4 *__restrict__ items,
-    const uint32_t *__restrict__ item_count, uint32_t *__restrict__ hist, long long n_bins,
-    int tail_release) {
+    const uint32_t *__restrict__ item_count, uint32_t *__restrict__ hist, long long n_bins) {
     constexpr int NB = 1 << TB;
     // + 64 lane-private dummy counters: pads and keys outside the item count
     // there, so no lane branches around its LDS atomic
@@ -1547,25 +991,20 @@ __global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
             if (v != 0u && base + i < n_bins) atomicAdd(hist + base + i, v);
         }
     }
-    if (tail_release) {  // this block's window lines written back before the kernel ends
-        __syncthreads();
-        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    }
 }
 
 // ---------------------------------------------------------------------------
 // launch wrappers
 // ---------------------------------------------------------------------------
-size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles, int hot_rows) {
+size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles) {
     return 4 * ((size_t)hot_words + ((size_t)1 << cbits) + (size_t)toa_words4 + 64 + 4 +
-                (size_t)align4((hot_rows + 1) / 2) +
                 (size_t)kSieveStage * (kSplitThreads / 64) + (size_t)kColdGroups * align4(n_tiles) +
                 4 * (size_t)kSieveLdsChunks + sizeof(SegDesc) / 4 * (size_t)kKargSegs);
 }
 
 hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T, int W,
                                const uint16_t *screen_row, const uint32_t *pix_cnt, int cbits,
-                               uint32_t *glut, uint32_t *tab, hipStream_t st) {
+                               uint32_t *glut, uint32_t *tab, uint32_t *stats, hipStream_t st) {
     const unsigned g = (unsigned)((L + 1 + 255) / 256);
     if (lut16)
         hipLaunchKernelGGL(k_sieve_glut<uint16_t>, dim3(g), dim3(256), 0, st,
@@ -1574,7 +1013,7 @@ hipError_t launch_sieve_tables(const void *lut, bool lut16, long long L, int T, 
         hipLaunchKernelGGL(k_sieve_glut<int>, dim3(g), dim3(256), 0, st, (const int *)lut, L, T, W,
                            screen_row, glut);
     hipLaunchKernelGGL(k_sieve_table, dim3((unsigned)(((1LL << cbits) + 255) / 256)), dim3(256), 0,
-                       st, pix_cnt, glut, L, cbits, tab);
+                       st, pix_cnt, glut, L, cbits, tab, stats);
     return hipGetLastError();
 }
 
@@ -1598,26 +1037,6 @@ hipError_t launch_chunk_tab_karg(const SegDesc *host_segs, int n_segs, long long
     return hipGetLastError();
 }
 
-template <int TB, int KPT, bool K24>
-static void launch_sort_a(const ColdArgs &c, size_t sma, hipStream_t st) {
-    (void)hipFuncSetAttribute((const void *)k_cold_sort_a<TB, KPT, K24>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);
-    hipLaunchKernelGGL((k_cold_sort_a<TB, KPT, K24>), dim3(c.rows * kColdGroups), dim3(kSortThreads),
-                       sma, st, c);
-}
-
-template <int TB>
-static void launch_sort_a_tb(const ColdArgs &c, size_t sma, hipStream_t st) {
-    switch (c.sort_kpt) {
-    case 48:
-        return c.key24 ? launch_sort_a<TB, 48, true>(c, sma, st) : launch_sort_a<TB, 48, false>(c, sma, st);
-    case 32:
-        return c.key24 ? launch_sort_a<TB, 32, true>(c, sma, st) : launch_sort_a<TB, 32, false>(c, sma, st);
-    default:
-        return c.key24 ? launch_sort_a<TB, 16, true>(c, sma, st) : launch_sort_a<TB, 16, false>(c, sma, st);
-    }
-}
-
 hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t stop) {
     const int hot_blocks = c.hot_part ? ((c.ht + 255) / 256) * 8 : 0;
     if (c.all_hot && hot_blocks > 0) {
@@ -1629,53 +1048,34 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
     }
     hipLaunchKernelGGL(k_hot_reduce_scan, dim3(hot_blocks + c.n_tiles), dim3(256), 0, st, c,
                        hot_blocks);
-    const size_t sm = cold_sort_smem(c.n_tiles);
-    // the wave-independent sort when its LDS (2 blocks per CU) fits
-    const size_t smw = cold_sort_w_smem(c.n_tiles);
-    const bool wave = c.wave_sort == 1 && smw <= 80 * 1024;
-    const size_t sma = cold_sort_a_smem(c.n_tiles, c.sort_kpt);
-    const bool aligned = c.pad8 != 0;
-    hipError_t e = hipSuccess;
+    const size_t sma = cold_sort_a_smem(c.n_tiles, kSortKPT);
     switch (c.tile_bits) {
 #define LDE_COLD(TB)                                                                              \
     case TB:                                                                                      \
-        if (aligned) {                                                                            \
-            launch_sort_a_tb<TB>(c, sma, st);                                                     \
-        } else if (wave) {                                                                        \
-            (void)hipFuncSetAttribute((const void *)k_cold_sort_w<TB>,                            \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smw);      \
-            hipLaunchKernelGGL(k_cold_sort_w<TB>, dim3(c.rows * kColdGroups), dim3(kSortThreads), \
-                               smw, st, c);                                                       \
-        } else {                                                                                  \
-            (void)hipFuncSetAttribute((const void *)k_cold_sort<TB>,                              \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);       \
-            hipLaunchKernelGGL(k_cold_sort<TB>, dim3(c.rows * kColdGroups), dim3(kSortThreads),   \
-                               sm, st, c);                                                        \
-        }                                                                                         \
+        (void)hipFuncSetAttribute((const void *)k_cold_sort_a<TB>,                                \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);          \
+        hipLaunchKernelGGL((k_cold_sort_a<TB>), dim3(c.rows * kColdGroups), dim3(kSortThreads),   \
+                           sma, st, c);                                                           \
         if (!LDE_DIAG(c.ablate)) /* diagnostics: the keys are not valid */                       \
             hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, \
                                   st, nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist,   \
-                                  c.n_bins, (c.tail_release & 4) ? 1 : 0);                       \
+                                  c.n_bins);                                                     \
         else if (stop) /* the binning's end marker is still recorded */                          \
             (void)hipEventRecord(stop, st);                                                      \
         break;
-        LDE_COLD(13)
         LDE_COLD(14)
         LDE_COLD(15)
 #undef LDE_COLD
     default:
-        e = hipErrorInvalidValue;
+        return hipErrorInvalidValue;
     }
-    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
 template <int ABL>
 static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                                  hipEvent_t stop) {
-    if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles, a.hot_w != a.T ? a.hot_rows : 0) >
-            kSplitSmemMax ||
-        (a.hot_w != a.T && (a.hot_rows < 1 || !a.row_screen)))
+    if (sieve_smem(a.hot_words, a.cbits, a.toa_words4, a.n_tiles) > kSplitSmemMax || !a.hot_fmt)
         return hipErrorInvalidValue;
     if (a.lds_ctab)
         hipExtLaunchKernelGGL(k_sieve<ABL, 0>, dim3(grid), dim3(kSplitThreads), 0, st, start, stop, 0,
@@ -1688,37 +1088,15 @@ static hipError_t launch_sieve_t(const SieveArgs &a, int grid, hipStream_t st, h
 
 hipError_t launch_sieve(const SieveArgs &a, int grid, hipStream_t st, hipEvent_t start,
                         hipEvent_t stop) {
-    int mode = a.keyed ? (kSieveKeyed | (a.keyed24 ? kSieveKeyed24 : 0))
-                       : a.ablate | (a.early_gather ? 256 : 0) | (a.pack ? 65536 : 0) |
-                             (a.toa_log ? kSieveToaLog : 0);
-    if (a.hot_w != a.T) {  // windowed hot rows: the default pipeline only
-        if (mode != 0 || a.pair) return hipErrorInvalidValue;
-        mode = kSieveWindow;
-    }
-    if (a.pair) {  // u16 hot pairs: the default pipeline, whole rows
-        if (mode != 0 || !a.hot_fmt || !a.hist || !a.row_screen || (a.T & 1) || (a.hot_words & 7))
-            return hipErrorInvalidValue;
-        mode = kSievePair;
-    }
+    const int mode = a.keyed ? kSieveKeyed : LDE_DIAG(a.ablate);
     switch (mode) {
 #define LDE_SIEVE_MODE(m) \
     case m: return launch_sieve_t<m>(a, grid, st, start, stop);
-    // exact variants: the pass, early gathers (256), deferred stores (2048),
-    // the packed table word (65536)
-    LDE_SIEVE_MODE(0) LDE_SIEVE_MODE(256) LDE_SIEVE_MODE(2048) LDE_SIEVE_MODE(65536)
-    LDE_SIEVE_MODE(65536 | 256) LDE_SIEVE_MODE(65536 | 2048) LDE_SIEVE_MODE(65536 | 256 | 2048)
-    LDE_SIEVE_MODE(kSieveKeyed) LDE_SIEVE_MODE(kSieveKeyed | kSieveKeyed24) LDE_SIEVE_MODE(kSieveWindow)
-    LDE_SIEVE_MODE(kSievePair)
-    // the same with log-linear TOA buckets (tables of geometric edges)
-    LDE_SIEVE_MODE(kSieveToaLog) LDE_SIEVE_MODE(kSieveToaLog | 256) LDE_SIEVE_MODE(kSieveToaLog | 2048)
-    LDE_SIEVE_MODE(kSieveToaLog | 65536) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256)
-    LDE_SIEVE_MODE(kSieveToaLog | 65536 | 2048) LDE_SIEVE_MODE(kSieveToaLog | 65536 | 256 | 2048)
+    LDE_SIEVE_MODE(0) LDE_SIEVE_MODE(kSieveKeyed)
 #ifdef LDE_DIAGNOSTICS
     // timing probes (wrong results), diagnostics build only
-    LDE_SIEVE_MODE(1) LDE_SIEVE_MODE(2) LDE_SIEVE_MODE(4) LDE_SIEVE_MODE(6)
-    LDE_SIEVE_MODE(8) LDE_SIEVE_MODE(16) LDE_SIEVE_MODE(32) LDE_SIEVE_MODE(64) LDE_SIEVE_MODE(128)
-    LDE_SIEVE_MODE(512) LDE_SIEVE_MODE(1024) LDE_SIEVE_MODE(4096) LDE_SIEVE_MODE(8192)
-    LDE_SIEVE_MODE(12288) LDE_SIEVE_MODE(16384) LDE_SIEVE_MODE(49152) LDE_SIEVE_MODE(131072)
+    LDE_SIEVE_MODE(1) LDE_SIEVE_MODE(2) LDE_SIEVE_MODE(4) LDE_SIEVE_MODE(6) LDE_SIEVE_MODE(4096)
+    LDE_SIEVE_MODE(16384) LDE_SIEVE_MODE(49152) LDE_SIEVE_MODE(131072)
 #endif
 #undef LDE_SIEVE_MODE
     default: return hipErrorInvalidValue;

@@ -350,19 +350,13 @@ int lde_kernel_stats(lde_handle *h, int32_t kernel_id, double *ms, int64_t *laun
  *   LDE_C_PIX_PREDICTED     1 if the last PIXEL batch used predicted slots
  *   LDE_C_WAITS             finalize waits that found the GPU still busy
  *   LDE_C_WAITS_BLOCKED     ... of which ended in a blocking (interrupt) wait
- *   LDE_C_WAIT_PRED_US      the predicted finalize wait (us), slept through
- *   LDE_C_SIEVE_PAIR        1 if the last SIEVE batch kept its hot rows as u16 pairs
- *   LDE_C_SIEVE_PAIR_WRAPS  sieve blocks, since creation, whose u16 hot counters
- *                           wrapped and whose hot events were re-added exactly
- *                           with global atomics (synchronizes the stream) */
+ *   LDE_C_WAIT_PRED_US      the predicted finalize wait (us), slept through */
 #define LDE_C_PIX_OVERFLOW 0
 #define LDE_C_PIX_OVERFLOW_CAP 1
 #define LDE_C_PIX_PREDICTED 2
 #define LDE_C_WAITS 3
 #define LDE_C_WAITS_BLOCKED 4
 #define LDE_C_WAIT_PRED_US 5
-#define LDE_C_SIEVE_PAIR 6
-#define LDE_C_SIEVE_PAIR_WRAPS 7
 int lde_counter(lde_handle *h, int32_t id, int64_t *value);
 
 /* Introspection for tests and reports. */

@@ -100,10 +100,6 @@ def test_product_library_has_only_exact_sieve_variants():
     lib = ROOT / 'esslivedata_amd' / 'libesslivedata_amd.so'
     out = subprocess.run(['nm', '-C', str(lib)], capture_output=True, text=True).stdout
     modes = {int(m) for m in re.findall(r'lde::k_sieve<(\d+), \d>\(', out)}
-    assert 0 in modes
-    # the exact variants, and the keyed wavelength pass (262144; with 24-bit
-    # words 262144 | 2^21), windowed rows (2^23), u16 hot pairs (2^24)
-    exact = {0, 256, 2048, 65536, 65536 | 256, 65536 | 2048, 65536 | 256 | 2048}
-    log = 1 << 20  # log-linear TOA buckets (exact)
-    assert modes <= exact | {m | log for m in exact} | {262144, 262144 | (1 << 21), 1 << 23, 1 << 24}, modes
-    assert 1 << 24 in modes
+    # the product build has the plain sieve and the keyed wavelength pass
+    # (262144) only: no ablation modes
+    assert modes == {0, 262144}, modes

@@ -90,15 +90,13 @@ def test_monitor_ev44_staging_ignores_pixel_id():
     np.testing.assert_array_equal(b.read_histogram().ravel(), np.histogram(toa, edges)[0])
 
 
-@pytest.mark.parametrize('chunk', ['262144', '1048576'])
-def test_threaded_host_staging_large_messages(knobs, chunk):
+def test_threaded_host_staging_large_messages():
     """lde_stage splits large messages over worker threads (each chunk's H2D
     queued by the thread that copied it): detector and monitor handles, ragged
     chunk tails, a message that starts mid-ring."""
     from esslivedata_amd import ev44, projection, synthetic
     from esslivedata_amd.engine import BinningEngine
 
-    knobs(LDE_STAGE_CHUNK=chunk)
     inst = synthetic.dummy_panel()
     view = projection.logical_lut(inst.detector_number)
     edges = inst.edges.edges_ns()

@@ -18,56 +18,18 @@ VARIANTS = [
     {},
     {'LDE_LUT32': '1'},
     {'LDE_TOA_GENERAL': '1'},
-    {'LDE_PEEL': '1'},
-    {'LDE_SUBC': '1'},
     {'LDE_TILE_BITS': '15', 'LDE_PART_GRID': '7'},
-    {'LDE_TILE_BITS': '13', 'LDE_PART_GRID': '3'},  # long per-block page chains + tails
     # SPLIT: few hot rows (mostly cold keys), few split blocks (long cold regions),
     # hot set re-selected every batch
     {'LDE_HOT_ROWS': '8', 'LDE_SPLIT_GRID': '3', 'LDE_HOT_REFRESH': '1'},
-    # SPLIT pixel cache: off, tiny (constant tag conflicts), large
-    {'LDE_PIXEL_CACHE_BITS': '0'},
-    {'LDE_PIXEL_CACHE_BITS': '6', 'LDE_SPLIT_GRID': '17'},
+    # SPLIT pixel table: tiny (constant tag conflicts), large
+    {'LDE_PIXEL_CACHE_BITS': '10', 'LDE_SPLIT_GRID': '17'},
     {'LDE_PIXEL_CACHE_BITS': '15'},
-    # SPLIT with the original event pass instead of the SIEVE pass
     # SIEVE with few hot rows and few blocks: long cold regions, many sort
     # pieces per wave, tiles split over several accumulate items
     {'LDE_HOT_ROWS': '8', 'LDE_SPLIT_GRID': '3', 'LDE_ITEM_EVENTS': '40000'},
-    {'LDE_SIEVE': '0'},
-    {'LDE_SIEVE': '0', 'LDE_PIXEL_CACHE_BITS': '6', 'LDE_SPLIT_GRID': '17'},
     # one sieve block: its chunk range exceeds the LDS chunk table (global table)
     {'LDE_SPLIT_GRID': '1'},
-    # sieve pipeline variants (exact): TOA bin packed into the table word,
-    # gathers issued an iteration early, cold-key stores deferred
-    {'LDE_SIEVE_PACK': '1'},
-    {'LDE_SIEVE_PACK': '1', 'LDE_EARLY_GATHER': '1'},
-    # log-linear TOA buckets (2^M per octave) instead of linear ones, alone
-    # and with the packed table word
-    {'LDE_SIEVE_TOA_LOG': '1'},
-    {'LDE_SIEVE_TOA_LOG': '1', 'LDE_SIEVE_PACK': '1'},
-    {'LDE_DEFER_STORES': '1'},
-    # SIEVE hot rows narrowed to a TOA window (more rows; hot screens' events
-    # outside the window leave as cold keys), alone and with a tiny row count
-    {'LDE_HOT_WINDOW': '1'},
-    {'LDE_HOT_WINDOW': '1', 'LDE_HOT_ROWS': '8', 'LDE_HOT_REFRESH': '1'},
-    # cold-key sorts: block-cooperative per-key stores, wave-independent,
-    # 16-byte groups with 16 / 32 keys per thread (default: 16-byte groups, 48)
-    {'LDE_COLD_SORT': '0'},
-    {'LDE_COLD_SORT': '1'},
-    {'LDE_COLD_SORT_KPT': '16'},
-    {'LDE_COLD_SORT_KPT': '32'},
-    # cold keys as 32-bit words instead of packed 24-bit keys
-    {'LDE_KEY24': '0'},
-    # hot rows flushed as u32 instead of u16
-    {'LDE_HOT16': '0'},
-    # hot counters as u16 pairs in LDS (twice the rows), alone, with few rows
-    # re-selected every batch, and with a large pixel table
-    {'LDE_HOT_PAIR': '1'},
-    {'LDE_HOT_PAIR': '1', 'LDE_HOT_ROWS': '8', 'LDE_HOT_REFRESH': '1'},
-    {'LDE_HOT_PAIR': '1', 'LDE_PIXEL_CACHE_BITS': '14'},
-    # per-block release fences: none / also at the end of the sort and pass B
-    {'LDE_TAIL_RELEASE': '0'},
-    {'LDE_TAIL_RELEASE': '7'},
 ]
 
 
@@ -115,9 +77,7 @@ def test_monitor_kat_reference_fixture():
     )
 
 
-MONITOR_VARIANTS = [{}, {'LDE_MON_PF': '1'}, {'LDE_MON_PF': '1', 'LDE_MON_GRID': '1'},
-                    {'LDE_MON_RANGES': '1'}, {'LDE_MON_RANGES': '1', 'LDE_MON_PF': '1'},
-                    {'LDE_MON_RANGES': '0'}]
+MONITOR_VARIANTS = [{}]
 
 
 @pytest.mark.parametrize('layout', ['large', 'small'])
@@ -125,9 +85,7 @@ MONITOR_VARIANTS = [{}, {'LDE_MON_PF': '1'}, {'LDE_MON_PF': '1', 'LDE_MON_GRID':
 @pytest.mark.parametrize('n_bins', [100, 7, 1000, 3000])
 def test_monitor_matches_oracle(n_bins, variant, layout, request):
     """Several messages per launch, message sizes not multiples of 4 or of
-    the grid; variants: next groups loaded before the current are binned
-    (LDE_MON_PF), one block per CU (many iterations per lane), blocks in
-    ranges per message (LDE_MON_RANGES)."""
+    the grid; each message gets its own range of blocks."""
     from esslivedata_amd.engine import BinningEngine
 
     if MONITOR_VARIANTS[variant]:  # the diagnostics build reads the knobs
@@ -143,9 +101,7 @@ def test_monitor_matches_oracle(n_bins, variant, layout, request):
         ]
     )
     eng = BinningEngine.monitor(edges)
-    # three messages; block ranges per message need messages of >= 65536
-    # three messages: large, or one of 3 events (its block range holds one
-    # block; LDE_MON_RANGES=0: the grid rotates over the messages)
+    # three messages: large, or one of 3 events (its block range holds one block)
     cuts = (0, 100_000, 180_000) if layout == 'large' else (0, 3, 100_003)
     for lo, hi in zip(cuts, cuts[1:] + (len(toa),)):
         eng.stage(None, toa[lo:hi])
@@ -357,17 +313,14 @@ def test_atomic_many_large_messages_proportional_blocks():
     np.testing.assert_array_equal(res.current_hist, o.finalize()['histogram_current'])
 
 
-@pytest.mark.parametrize('segs', [None, '24'])
 @pytest.mark.parametrize('n_msgs', [1, 24, 45, 64, 65, 130, 630])
-def test_atomic_many_messages(n_msgs, segs, request):
+def test_atomic_many_messages(n_msgs):
     """ATOMIC with many small messages per accumulate (BIFROST: 45 bank
-    messages of 1,000 events per pulse): up to 64 descriptors per launch
-    (default) or 24 (LDE_ATOMIC_SEGS, diagnostics build); messages of ragged
+    messages of 1,000 events per pulse): up to 64 descriptors per launch, or
+    one descriptor per block past that (k_bin_atomic_blocks); messages of ragged
     sizes, some not 16-byte aligned, bit-exact against the oracle."""
     from esslivedata_amd import projection, synthetic
 
-    if segs:
-        request.getfixturevalue('knobs')(LDE_ATOMIC_SEGS=segs)
     inst = synthetic.bifrost_unified()
     view = projection.logical_lut(inst.detector_number, transform=synthetic.bifrost_transform)
     edges = inst.edges.edges_ns()
@@ -594,16 +547,13 @@ def test_finalize_partials_match_finalize():
             assert not h[:S].any() and int(h[2 * S]) == 0 and int(h[2 * S + 2]) > 0
 
 
-@pytest.mark.parametrize('karg', ['1', '0'])
 @pytest.mark.parametrize('n_msgs', [1, 14, 24, 25, 40])
-def test_split_many_device_messages(n_msgs, karg, knobs):
+def test_split_many_device_messages(n_msgs, knobs):
     """SIEVE with the message descriptors passed as kernel arguments (<= 24
-    messages) or uploaded (more, or LDE_KARG_SEGS=0): ragged, misaligned
-    device segments, replica cycling, hot-set refresh every batch."""
+    messages) or uploaded (more): ragged, misaligned device segments, replica
+    cycling, hot-set refresh every other batch."""
     import torch
 
-    knobs(LDE_KARG_SEGS=karg)
-    knobs(LDE_LDS_CTAB=karg)  # '0': the k_chunk_tab paths
     knobs(LDE_HOT_REFRESH='2')
     from esslivedata_amd import projection, synthetic
 
@@ -942,19 +892,10 @@ def test_loki_pixel_predicted_slots_exact_under_shifts(knobs):
 
 
 PIXEL_VARIANTS = [
-    # two units of events in flight per partition block
-    {'LDE_PIX_PF2': '1'},
+    {},
     # an overflow list of 16 groups: the overflow groups past it are added by
     # pass A itself (global atomics), exactly
     {'LDE_PIX_OVF_CAP': '16'},
-    {},
-    {'LDE_PIX_PRED': '0'},
-    {'LDE_PIX24': '0'},
-    {'LDE_PIX_UNIT': '1', 'LDE_PIX_EPT': '8'},
-    {'LDE_PIX_UNIT': '1', 'LDE_PIX_EPT': '16'},
-    {'LDE_PIX_BU': '8'},
-    {'LDE_PIX_ITEMS': '3'},
-    {'LDE_PIX_MAX_RANGES': '512'},
 ]
 
 

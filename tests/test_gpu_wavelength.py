@@ -91,10 +91,9 @@ def test_dream_wavelength_matches_oracle(strategy, scale, table_min):
     assert res.cumulative_total == exp['counts_total_cumulative']
 
 
-# keyed SPLIT pass variants (diagnostics build): the general event pass
-# (bin loops, grid coordinate per event) beside the default FAST one, and
-# 24-bit instead of 32-bit words between the keyed pass and the sieve
-KEYED_VARIANTS = [{'LDE_KEY_PRE': '0'}, {'LDE_COORD_FIXED_BIN': '0'}, {'LDE_KEY_WORD24': '1'}]
+# keyed SPLIT pass variant (diagnostics build): the general event pass (bin
+# loops, grid coordinate per event) beside the default FAST one
+KEYED_VARIANTS = [{'LDE_COORD_FIXED_BIN': '0'}]
 
 
 @pytest.mark.parametrize('variant', range(len(KEYED_VARIANTS)))
