@@ -1154,6 +1154,8 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
     c.n_bins = h->nbins;
     c.hot_fmt = h->d_hot_fmt;
     c.ablate = h->cold_sort_ablate;
+    c.depth = (int)env_ll("LDE_COLD_DEPTH", 0);
+    c.xcd = (int)env_ll("LDE_COLD_XCD", 0);
     c.all_hot = h->all_hot[replica];
     Timed tm(h, LDE_K_PAGED);
     HIPCALL(h, lde::launch_cold_pipeline(c, h->stream, h->bin_stop_ext));
@@ -1627,8 +1629,10 @@ void commit_pixel(lde_handle *h, PixStaged &st) {
     h->pix.fp_off = h->d_pfp_off;
     h->pix.fp_scr = h->d_pfp_scr;
     if (env_ll("LDE_VERBOSE", 0))
-        fprintf(stderr, "lde pixel: %d ranges of 2^%d pixels, widest footprint %d screens (%zu B LDS)\n",
-                h->pix.nr, h->pix.rb, h->pix.fmax, lde::pix_acc_smem(h->pix.rb, h->pix.fmax, h->T));
+        fprintf(stderr, "lde pixel: %d ranges of 2^%d pixels, widest footprint %d screens (%zu B LDS); "
+                        "pass A unit %d, %zu B LDS\n",
+                h->pix.nr, h->pix.rb, h->pix.fmax, lde::pix_acc_smem(h->pix.rb, h->pix.fmax, h->T), h->pix_unit,
+                lde::pix_scatter_smem(h->tp, h->pix_unit));
 }
 
 int build_pixel(lde_handle *h, const int32_t *lut) {

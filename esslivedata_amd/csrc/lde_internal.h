@@ -174,7 +174,7 @@ constexpr uint32_t kSieveEmpty = 0xFFu << kSieveTagShift;  // tag 255, not valid
 constexpr int kSieveMaxT = 254;
 // finalize: per-block total partials summed on the host (at most this many blocks)
 constexpr int kHostPartials = 1024;
-constexpr int kColdGroups = 2;  // SIEVE cold keys: wave groups per block, one sort block each
+constexpr int kColdGroups = 8;  // SIEVE cold keys: wave groups per block, one sort block each
 
 // SIEVE: chunk tables of up to this many entries per block live in LDS,
 // built by the sieve itself from kernel-argument descriptors
@@ -237,11 +237,14 @@ struct ColdArgs {
     uint32_t *hist;
     long long n_bins;
     const uint32_t *hot_fmt = nullptr;  // per sieve block: hot rows as u16 (1) or u32 (0)
-    int ablate = 0;     // cold-sort diagnostics (wrong results): 1 no writes
+    int ablate = 0;     // cold-sort diagnostics (wrong results): 1 no writes, 2 no scatter,
+                        // 16 prologue only
+    int depth = 0;      // diagnostics: 1 = one load step in flight in the direct sort
+    int xcd = 0;        // diagnostics: sort rows on the XCD of their sieve block
     int all_hot = 0;    // every screen has a hot row (no cold keys): hot-row reduce only
 };
-size_t cold_sort_a_smem(int n_tiles, int kpt);
-constexpr int kSortThreadsHost = 64 * (kSplitThreads / 64) / kColdGroups;  // cold-sort block
+constexpr int kSortThreadsHost = 256;          // cold-sort block (thread t owns tile t)
+constexpr size_t kColdSortSmem = 52 * 1024;    // cold-sort LDS: three blocks per CU
 // start/stop: optional HIP events stamped by the kernel dispatch itself
 // (hipExtLaunchKernelGGL), so timing adds no marker packets between kernels
 hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t stop = nullptr);

@@ -1,11 +1,10 @@
-// lde_sieve.hip -- lean event pass of the SPLIT strategy ("sieve").
+// lde_sieve.hip -- the event pass of the SPLIT strategy ("sieve") and its
+// cold-key path.
 //
-// Same contract as k_split (lde_split.hip): every event of the batch is
-// binned either into a hot screen row privatized in LDS or emitted as a cold
-// (screen * T + bin) key for the paged pass, so the counts are bit-exact
-// whatever the hot set is.  What changes is the per-event instruction stream,
-// which in k_split was ~66 VALU operations per event with a vmcnt(0) drain per
-// chunk (rocprofv3 SQ_INSTS_VALU, round 1):
+// Every event of the batch is binned either into a hot screen row
+// privatized in LDS or emitted as a cold (screen * T + bin) key, so the
+// counts are bit-exact whatever the hot set is (lde_hotset.hip picks it from
+// a sample).  The per-event instruction stream is kept short and branch-free:
 //
 //   * one 32-bit word per pixel, in LDS (direct-mapped table of the sampled
 //     hottest pixels) and in HBM (the replica's LUT), with the same payload:
@@ -19,8 +18,8 @@
 //     bin = word & 0xFF + (low bits >= word >> 8); a sentinel bucket past the
 //     last edge gives bin 256 (dropped);
 //   * hot lanes add 1 to their LDS row, the others to a lane-private dummy
-//     word; cold keys are compacted per wave in LDS and leave as one 16-byte
-//     store per lane per half chunk (lanes past the count store out of range,
+//     word; cold keys are compacted per wave in LDS and leave as one 12-byte
+//     store (four 24-bit keys) per lane per half chunk (lanes past the count store out of range,
 //     which is discarded) -- so every iteration issues the same memory
 //     operations and the compiler's in-order vmcnt / lgkmcnt accounting can
 //     wait for exactly the operation a value comes from;
@@ -31,6 +30,12 @@
 // Deferred chunks (partial tails, segments that are not 16-byte aligned) are
 // replaced by an all-invalid dummy chunk in the pipeline and binned afterwards
 // by a plain element-wise pass.
+//
+// Cold path (three launches): k_hot_reduce_scan adds the blocks' hot rows to
+// the window and scans the sieve's exact per-(block, wave group, tile) cold
+// counts into range offsets; k_cold_sort moves every group's keys into its
+// ranges of a tile-major u16 array (one LDS atomic + one u16 store per key);
+// k_cold_accumulate histograms each tile's keys in LDS.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -650,23 +655,39 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
     }
     const int t = blockIdx.x - hot_blocks;
     const int rows = c.rows * kColdGroups;
+    // eight rows per thread per round, all loads issued before the scan
+    constexpr int R = 8;
     uint32_t carry = 0;
-    for (int r0 = 0; r0 < rows; r0 += 256) {
-        const int r = r0 + threadIdx.x;
-        uint32_t v = r < rows ? c.tcnt[(size_t)r * c.n_tiles + t] : 0u;
-        v = (v + 7u) & ~7u;  // k_cold_sort_a: 16-byte aligned (row, tile) ranges
+    for (int r0 = 0; r0 < rows; r0 += 256 * R) {
+        const int rb = r0 + (int)threadIdx.x * R;
+        uint32_t v[R], sum = 0;
+#pragma unroll
+        for (int u = 0; u < R; ++u) v[u] = rb + u < rows ? c.tcnt[(size_t)(rb + u) * c.n_tiles + t] : 0u;
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            v[u] = (v[u] + 7u) & ~7u;  // k_cold_sort: 16-byte aligned (row, tile) ranges
+            sum += v[u];
+        }
         uint32_t tot;
-        const uint32_t ex = block_exclusive_scan(v, s_w, &tot);
-        if (r < rows) c.boff[(size_t)r * c.n_tiles + t] = carry + ex;
+        uint32_t ex = carry + block_exclusive_scan(sum, s_w, &tot);
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            if (rb + u < rows) c.boff[(size_t)(rb + u) * c.n_tiles + t] = ex;
+            ex += v[u];
+        }
         carry += tot;
         __syncthreads();
     }
     if (threadIdx.x == 0) c.tile_total[t] = carry;
 }
 
-constexpr int kSortThreads = kSortThreadsHost;  // one wave per sieve wave
+constexpr int kSortThreads = kSortThreadsHost;
 constexpr int kSortWaves = kSortThreads / 64;
-constexpr int kSortKPT = 48;                     // keys per lane per piece
+constexpr int kGroupWaves = (kSplitThreads / 64) / kColdGroups;  // sieve waves per group
+constexpr int kSortSPW = kSortWaves / kGroupWaves;               // sort waves per sieve wave
+static_assert(kSortSPW >= 1 && kSortWaves % kGroupWaves == 0, "sort waves per sieve wave");
+constexpr int kSortKPT = 48;    // keys per lane per piece (piece path)
+constexpr int kColdDepth = 3;   // direct path: steps of 16 keys per lane per load round
 
 // Balanced pass-B items (tile, first key, end key, tile has one item) of the
 // tile-major key array: a tile with n keys gets ceil(n / item_keys) items.
@@ -723,43 +744,159 @@ __device__ void plan_items(const uint32_t *__restrict__ tile_total, int n_tiles,
     __syncthreads();
 }
 
-// Block-cooperative sort with whole 16-byte output groups (n_tiles <=
-// kSortThreads: thread t owns tile t).  The scan gives every (row, tile)
-// range a length rounded up to 8 keys, so each range starts 16-byte aligned.
-// A piece's run of a tile is placed in the tile-sorted image behind the <= 7
-// keys the tile carried over from earlier pieces; the full 8-key groups leave
-// as one 16-byte store each and the rest is carried again; the last carry of
-// each tile leaves padded with 0xFFFF (skipped by pass B).  The image holds
-// u16 tile-local keys.  Compared with per-key u16 stores into short unaligned
-// runs (round 1) this issues 8x fewer store lanes and no partial lines.
-size_t cold_sort_a_smem(int n_tiles, int kpt) {
-    const size_t nt4 = (size_t)align4(n_tiles);
-    const size_t img_words = ((size_t)kSortThreads * kpt + 16 * nt4) / 2;
-    const size_t scratch = std::max(img_words, (size_t)2 * (kMaxTiles + 1));
-    // scratch | s_cnt [waves][nt4] | tot, pos, B, full, ng | carry [nt4][4] | s_w |
-    // group -> tile (u16, one per 8-key group of a piece)
-    const size_t gt_words = ((size_t)kSortThreads * kpt / 8 + nt4 + 1) / 2;
-    return 4 * ((size_t)align4((int)scratch) + (size_t)kSortWaves * nt4 + 5 * nt4 + 4 * nt4 + 32 + gt_words);
+// The keys one sort wave reads: part (wv % kSortSPW) of the region of sieve
+// wave (grp * kGroupWaves + wv / kSortSPW), split at multiples of 4 keys (one
+// 12-byte group)
+struct WaveKeys {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t n;
+};
+__device__ __forceinline__ WaveKeys wave_keys(const ColdArgs &c, int b, int grp, int wv) {
+    constexpr int NW = kSplitThreads / 64;
+    const int sw = grp * kGroupWaves + wv / kSortSPW, part = wv % kSortSPW;
+    const uint32_t n_w = c.cold_cnt[(size_t)b * NW + sw];
+    const uint32_t q = (n_w + 4u * kSortSPW - 1u) / (4u * kSortSPW) * 4u;
+    const uint32_t lo = min(n_w, (uint32_t)part * q), hi = min(n_w, lo + q);
+    const uint32_t capw = (uint32_t)(c.cap / NW);
+    const unsigned char *base = reinterpret_cast<const unsigned char *>(c.cold) +
+                                ((size_t)b * (size_t)c.stride + (size_t)sw * capw + lo) * 3u;
+    return WaveKeys{make_rsrc(base, (hi - lo) * 3u), hi - lo};
+}
+
+// Cold-key sort of one (sieve block, wave group) row into its tile ranges of
+// the tile-major u16 key array.  The sieve counted the row's keys per tile
+// exactly, so its ranges are known before any key is read (range (row, t) at
+// tile base + boff, length rounded up to 8 keys, 16-byte aligned).
+//
+// Direct path (the row's keys fit the LDS image, cap keys): each key takes
+// the next slot of its tile's segment with one LDS atomic and lands there as
+// u16 (two random LDS operations per key, no count pass, no pieces); the
+// image then leaves as whole 16-byte groups, pads (0xFFFF, skipped by pass B)
+// pre-filled.  Piece path (a row larger than the image, rare): pieces of
+// kSortThreads * kSortKPT keys are counted, scanned and scattered with
+// per-wave cursors, carrying partial 8-key groups between pieces.
+template <int TB, int D>
+__device__ void cold_sort_direct(const ColdArgs &c, uint32_t *sm, int row, uint32_t cap, uint32_t cnt,
+                                 uint32_t B, uint32_t tot8, uint32_t gpos) {
+    constexpr uint32_t MASK = (1u << TB) - 1u;
+    constexpr int SH = TB + 2;  // keys are scaled by 4
+    const int n_tiles = c.n_tiles;
+    const int nt4 = align4(n_tiles);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = row / kColdGroups, grp = row % kColdGroups;
+    // LDS: cursors [tile] + 64 lane dummies | segment base [tile] | global
+    // position [tile] | 8-key groups [tile] | image (cap + 64 lane dummies) |
+    // group -> tile (u16)
+    uint32_t *s_cur = sm;
+    uint32_t *s_B = s_cur + nt4 + 64;
+    uint32_t *s_pos = s_B + nt4;
+    uint32_t *s_ng = s_pos + nt4;
+    uint16_t *img = reinterpret_cast<uint16_t *>(s_ng + nt4);
+    uint16_t *s_gt = img + cap + 64;
+    const bool own = tid < n_tiles;
+    if (own) {
+        s_cur[tid] = B;
+        s_B[tid] = B;
+        s_pos[tid] = gpos;
+        const uint32_t n8 = (cnt + 7u) & ~7u;
+        s_ng[tid] = n8 >> 3;
+        for (uint32_t i = B + cnt; i < B + n8; ++i) img[i] = 0xFFFFu;  // the range's pads
+    }
+    if (tid < 64) s_cur[nt4 + tid] = cap + (uint32_t)tid;  // lane dummies never move far
+    __syncthreads();
+    if (LDE_DIAG(c.ablate) & 16) return;  // diagnostics: the prologue only
+    const WaveKeys wk = wave_keys(c, b, grp, wv);
+    const uint32_t dcur = (uint32_t)(nt4 + lane);
+    // The wave's keys in rounds of D steps of 64 x 16 keys, two rounds in
+    // flight: a wave's region (about 4K keys on DREAM) is requested almost at
+    // once, so a block waits for about one memory latency, not one per step
+    // (one step in flight: 57 us for DREAM's 3.4e7 keys, 40 of them loads)
+    constexpr uint32_t STEP = 64u * 16u, ROUND = STEP * (uint32_t)D;
+    typedef v3u Round[D][4];
+    auto fetch = [&](Round &buf, uint32_t r0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)  // past the region: zeros (masked at use)
+                buf[d][j] = __builtin_amdgcn_raw_buffer_load_b96(
+                    wk.rs, (int)((r0 + (uint32_t)d * STEP + (uint32_t)j * 256u + (uint32_t)lane * 4u) * 3u),
+                    0, 0);
+    };
+    auto scatter = [&](const Round &buf, uint32_t r0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const uint32_t p0 = r0 + (uint32_t)d * STEP;
+            if (p0 >= wk.n) break;  // wave-uniform
+            uint32_t key[16];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t kk[4];
+                unpack_keys24(buf[d][j], kk);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t e = p0 + (uint32_t)j * 256u + (uint32_t)lane * 4u + (uint32_t)q;
+                    key[j * 4 + q] = e < wk.n ? kk[q] : 0xFFFFFFFFu;
+                }
+            }
+            if (LDE_DIAG(c.ablate) & 2) {  // diagnostics: loads only, keys folded into one word
+                uint32_t x = 0;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) x ^= key[e];
+                if (x == 0x12345678u) img[lane] = (uint16_t)x;
+                continue;
+            }
+            uint32_t slot[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const bool ok = key[e] != 0xFFFFFFFFu;
+                slot[e] = __hip_atomic_fetch_add(s_cur + (ok ? (key[e] >> SH) : dcur), 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const bool ok = key[e] != 0xFFFFFFFFu;
+                img[ok ? slot[e] : cap + (uint32_t)lane] = (uint16_t)((key[e] >> 2) & MASK);
+            }
+        }
+    };
+    Round bA, bB;
+    if (wk.n) fetch(bA, 0);
+    for (uint32_t r0 = 0; r0 < wk.n; r0 += 2 * ROUND) {
+        if (r0 + ROUND < wk.n) fetch(bB, r0 + ROUND);
+        scatter(bA, r0);
+        if (r0 + ROUND >= wk.n) break;
+        if (r0 + 2 * ROUND < wk.n) fetch(bA, r0 + 2 * ROUND);
+        scatter(bB, r0 + ROUND);
+    }
+    // every group's tile, a wave per tile (its lanes over the tile's groups)
+    for (int t = wv; t < n_tiles; t += kSortWaves) {
+        const uint32_t g0 = s_B[t] >> 3, ng = s_ng[t];
+        for (uint32_t j = (uint32_t)lane; j < ng; j += 64u) s_gt[g0 + j] = (uint16_t)t;
+    }
+    __syncthreads();
+    const uint4 *img4 = reinterpret_cast<const uint4 *>(img);
+    for (uint32_t gi = (uint32_t)tid; gi < (tot8 >> 3); gi += kSortThreads) {
+        const int t = s_gt[gi];
+        const uint32_t k = gi - (s_B[t] >> 3);
+        if (!(LDE_DIAG(c.ablate) & 1))
+            *reinterpret_cast<uint4 *>(c.keys + s_pos[t] + 8u * k) = img4[gi];
+    }
 }
 
 template <int TB>
-__global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(4, 4)))
-void k_cold_sort_a(ColdArgs c) {
+__device__ void cold_sort_pieces(const ColdArgs &c, uint32_t *sm, int row, uint32_t gpos) {
     constexpr int KPT = kSortKPT;
-    constexpr bool KEY24 = true;  // the sieve writes 24-bit keys
     constexpr int PIECE = kSortThreads * KPT;
     const int n_tiles = c.n_tiles;
     uint16_t *__restrict__ out = c.keys;
     constexpr uint32_t MASK = (1u << TB) - 1u;
     constexpr int SH = TB + 2;  // keys are scaled by 4
-    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     const int nt4 = align4(n_tiles);
-    const int img_words = (PIECE + 16 * nt4) / 2;
-    const int scratch = align4(max(img_words, 2 * (kMaxTiles + 1)));
+    const int img_words = align4((PIECE + 16 * nt4) / 2);
     uint16_t *img = reinterpret_cast<uint16_t *>(sm);   // tile segments, 16-byte aligned
-    uint32_t *s_cnt = sm + scratch;                      // [wave][tile]
-    uint32_t *s_tot = s_cnt + kSortWaves * nt4;          // [tile] keys of this piece
-    uint32_t *s_pos = s_tot + nt4;                       // [tile] next global position (8-aligned)
+    uint32_t *s_cnt = sm + img_words;                    // [wave][tile]
+    uint32_t *s_pos = s_cnt + kSortWaves * nt4;          // [tile] next global position (8-aligned)
     uint32_t *s_B = s_pos + nt4;                         // [tile] segment base in the image (u16)
     uint32_t *s_full = s_B + nt4;                        // [tile] full groups of this piece
     uint32_t *s_ng = s_full + nt4;                       // [tile] 8-key groups of its segment
@@ -767,50 +904,18 @@ void k_cold_sort_a(ColdArgs c) {
     uint32_t *s_w = reinterpret_cast<uint32_t *>(s_carry + nt4);
     uint16_t *s_gt = reinterpret_cast<uint16_t *>(s_w + 32);  // [group] its tile
     const int tid = threadIdx.x;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave-uniform: SGPR buffer descriptors
-    const int b = blockIdx.x / kColdGroups, grp = blockIdx.x % kColdGroups;
-    const int row = blockIdx.x;
-    constexpr int NW = kSplitThreads / 64;
-    const uint32_t capw = (uint32_t)(c.cap / NW);
-    const int sw = grp * kSortWaves + wv;
-    const uint32_t n_w = c.cold_cnt[(size_t)b * NW + sw];
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int b = row / kColdGroups, grp = row % kColdGroups;
     const bool own = tid < n_tiles;  // thread tid owns tile tid
-    if (row == 0)
-        plan_items(c.tile_total, n_tiles, c.item_keys, c.items, c.item_count, c.max_items, s_w,
-                   sm, sm + kMaxTiles + 1);
-    {
-        const uint32_t tt = own ? c.tile_total[tid] : 0u;
-        uint32_t total;
-        const uint32_t ex = block_exclusive_scan(tt, s_w, &total);
-        if (own) {
-            s_pos[tid] = ex + c.boff[(size_t)row * n_tiles + tid];
-        }
-    }
-    if (lane == 0) s_w[20 + wv] = (n_w + 64 * KPT - 1) / (64 * KPT);
+    const WaveKeys wk = wave_keys(c, b, grp, wv);
+    if (own) s_pos[tid] = gpos;
+    if (lane == 0) s_w[20 + wv] = (wk.n + 64 * KPT - 1) / (64 * KPT);
     __syncthreads();
     uint32_t npieces = 0;
 #pragma unroll
     for (int q = 0; q < kSortWaves; ++q) npieces = max(npieces, s_w[20 + q]);
-    constexpr uint32_t KB = KEY24 ? 3u : 4u;  // bytes per key in the sieve's regions
-    const __amdgpu_buffer_rsrc_t rs =
-        make_rsrc(reinterpret_cast<const unsigned char *>(c.cold) +
-                      ((size_t)b * (size_t)c.stride + (size_t)sw * capw) * KB,
-                  n_w * KB);
+    __syncthreads();  // s_w is the scan's scratch below
     uint32_t *my_cnt = s_cnt + wv * nt4;
-    v4u nk[KPT / 4];
-    auto fetch = [&](uint32_t p) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < KPT / 4; ++j) {
-            const uint32_t e0 = p * (uint32_t)(64 * KPT) + (uint32_t)j * 256u + (uint32_t)lane * 4u;
-            if (KEY24) {
-                const v3u w = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(e0 * 3u), 0, 0);
-                nk[j] = v4u{w[0], w[1], w[2], 0u};
-            } else {
-                nk[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(e0 * 4u), 0, 0);
-            }
-        }
-    };
-    if (npieces) fetch(0);
     uint32_t cn = 0;  // own tile: carried keys
     for (uint32_t p = 0; p < npieces; ++p) {
         for (int i = lane; i < nt4; i += 64) my_cnt[i] = 0;
@@ -819,14 +924,10 @@ void k_cold_sort_a(ColdArgs c) {
         for (int j = 0; j < KPT / 4; ++j) {
             const uint32_t e0 = p * (uint32_t)(64 * KPT) + (uint32_t)j * 256u + (uint32_t)lane * 4u;
             uint32_t kk[4];
-            if (KEY24)
-                unpack_keys24(v3u{nk[j][0], nk[j][1], nk[j][2]}, kk);
-            else
-                for (int q = 0; q < 4; ++q) kk[q] = nk[j][q];
+            unpack_keys24(__builtin_amdgcn_raw_buffer_load_b96(wk.rs, (int)(e0 * 3u), 0, 0), kk);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < n_w ? kk[q] : 0xFFFFFFFFu;
+            for (int q = 0; q < 4; ++q) key[j * 4 + q] = e0 + (uint32_t)q < wk.n ? kk[q] : 0xFFFFFFFFu;
         }
-        if (KPT <= 16 && p + 1 < npieces) fetch(p + 1);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int e = 0; e < KPT; ++e)
@@ -835,7 +936,7 @@ void k_cold_sort_a(ColdArgs c) {
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
         __syncthreads();
         // own tile: wave counts -> wave offsets inside the run (serial over
-        // the 8 waves), run length, segment [carry | run] rounded up to 8
+        // the waves), run length, segment [carry | run] rounded up to 8
         uint32_t n = 0;
         if (own) {
 #pragma unroll
@@ -874,14 +975,10 @@ void k_cold_sort_a(ColdArgs c) {
                     (uint16_t)((k >> 2) & MASK);
             }
         }
-        // every group's tile, a wave per tile (its lanes over the tile's
-        // groups), so the write-out below reads it instead of searching s_B
         for (int t = wv; t < n_tiles; t += kSortWaves) {
             const uint32_t g0 = s_B[t] >> 3, ng = s_ng[t];
             for (uint32_t j = (uint32_t)lane; j < ng; j += 64u) s_gt[g0 + j] = (uint16_t)t;
         }
-        // wide pieces: the next keys are requested once this piece's are dead
-        if (KPT > 16 && p + 1 < npieces) fetch(p + 1);
         __syncthreads();
         // one thread per 8-key group: full groups leave as 16-byte stores,
         // a segment's partial last group becomes the tile's new carry
@@ -915,6 +1012,57 @@ void k_cold_sort_a(ColdArgs c) {
         if (!(LDE_DIAG(c.ablate) & 1))
             *reinterpret_cast<uint4 *>(out + s_pos[tid]) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
     }
+}
+
+size_t cold_sort_pieces_smem(int n_tiles) {
+    const size_t nt4 = (size_t)align4(n_tiles);
+    const size_t img_words = (size_t)align4((int)(((size_t)kSortThreads * kSortKPT + 16 * nt4) / 2));
+    const size_t gt_words = ((size_t)kSortThreads * kSortKPT / 8 + nt4 + 1) / 2;
+    return 4 * (img_words + (size_t)kSortWaves * nt4 + 5 * nt4 + 4 * nt4 + 32 + gt_words);
+}
+
+// keys of the direct path's image in smem bytes of LDS
+uint32_t cold_sort_cap(int n_tiles, size_t smem) {
+    const long long nt4 = align4(n_tiles);
+    const long long words = (long long)(smem / 4) - (4 * nt4 + 64) - 32;  // headers, image dummies
+    if (words <= 0) return 0;
+    // cap / 2 image words + cap / 16 group-tile words
+    return (uint32_t)((words * 16 / 9) & ~63LL);
+}
+
+// One block per (sieve block, wave group) row; block 0 also plans pass B's
+// items.  cap: the direct path's image size in keys (from the launch's LDS).
+template <int TB, int D>
+__global__ __launch_bounds__(kSortThreads) void k_cold_sort(ColdArgs c, uint32_t cap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    __shared__ uint32_t s_w[32];
+    const int n_tiles = c.n_tiles;
+    const int tid = threadIdx.x;
+    int row = blockIdx.x;
+    if (LDE_DIAG(c.xcd) && (c.rows & 7) == 0) {
+        // diagnostics: the rows of sieve block b on XCD b % 8, where that
+        // block ran (workgroups go round-robin over the eight XCDs)
+        const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+        row = ((k / kColdGroups) * 8 + x) * kColdGroups + k % kColdGroups;
+    }
+    if (blockIdx.x == 0)
+        plan_items(c.tile_total, n_tiles, c.item_keys, c.items, c.item_count, c.max_items, s_w, sm,
+                   sm + kMaxTiles + 1);
+    const bool own = tid < n_tiles;
+    // own tile: global position of this row's range, the row's exact count
+    const uint32_t tt = own ? c.tile_total[tid] : 0u;
+    const uint32_t cnt = own ? c.tcnt[(size_t)row * n_tiles + tid] : 0u;
+    uint32_t total;
+    const uint32_t base = block_exclusive_scan(tt, s_w, &total);
+    const uint32_t gpos = own ? base + c.boff[(size_t)row * n_tiles + tid] : 0u;
+    __syncthreads();
+    uint32_t tot8;
+    const uint32_t B = block_exclusive_scan((cnt + 7u) & ~7u, s_w, &tot8);
+    __syncthreads();
+    if (tot8 <= cap)
+        cold_sort_direct<TB, D>(c, sm, row, cap, cnt, B, tot8, gpos);
+    else
+        cold_sort_pieces<TB>(c, sm, row, gpos);
 }
 
 // pass B: one item = a contiguous key range of one tile
@@ -1048,14 +1196,24 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
     }
     hipLaunchKernelGGL(k_hot_reduce_scan, dim3(hot_blocks + c.n_tiles), dim3(256), 0, st, c,
                        hot_blocks);
-    const size_t sma = cold_sort_a_smem(c.n_tiles, kSortKPT);
+    const size_t sma = kColdSortSmem;
+    const uint32_t cap = cold_sort_cap(c.n_tiles, sma);
+    if (cold_sort_pieces_smem(c.n_tiles) > sma || 4 * (size_t)(2 * (kMaxTiles + 1)) > sma)
+        return hipErrorInvalidValue;
     switch (c.tile_bits) {
 #define LDE_COLD(TB)                                                                              \
     case TB:                                                                                      \
-        (void)hipFuncSetAttribute((const void *)k_cold_sort_a<TB>,                                \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);          \
-        hipLaunchKernelGGL((k_cold_sort_a<TB>), dim3(c.rows * kColdGroups), dim3(kSortThreads),   \
-                           sma, st, c);                                                           \
+        if (LDE_DIAG(c.depth) == 1) {                                                             \
+            (void)hipFuncSetAttribute((const void *)k_cold_sort<TB, 1>,                           \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);      \
+            hipLaunchKernelGGL((k_cold_sort<TB, 1>), dim3(c.rows * kColdGroups),                  \
+                               dim3(kSortThreads), sma, st, c, cap);                              \
+        } else {                                                                                  \
+            (void)hipFuncSetAttribute((const void *)k_cold_sort<TB, kColdDepth>,                  \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);      \
+            hipLaunchKernelGGL((k_cold_sort<TB, kColdDepth>), dim3(c.rows * kColdGroups),         \
+                               dim3(kSortThreads), sma, st, c, cap);                              \
+        }                                                                                         \
         if (!LDE_DIAG(c.ablate)) /* diagnostics: the keys are not valid */                       \
             hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, \
                                   st, nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist,   \

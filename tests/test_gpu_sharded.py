@@ -223,6 +223,72 @@ def _subgroup_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _push_worker(rank, world, port, q):
+    """merge='push' (float32 views): a BIFROST-like float32 view
+    with its spectrum view over batches where the root, the other rank or
+    both have no share of the events, one batch without events at all and a
+    window in which only the other rank had events; the root's outputs equal
+    one workflow's after every finalize."""
+    import torch
+    import torch.distributed as dist
+
+    from esslivedata_amd import synthetic
+    from esslivedata_amd.distributed import shard_bounds
+    from esslivedata_amd.sharded import ShardedDetectorViewWorkflow
+    from esslivedata_amd.workflows import GpuDetectorViewFactory, LogicalViewConfig
+
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        inst = synthetic.bifrost_unified()
+        cfg = LogicalViewConfig(transform=lambda a, _s: synthetic.bifrost_transform(a),
+                                output_dims=('arc/tube', 'channel/pixel'),
+                                spectrum_view=synthetic.bifrost_spectrum_config(10))
+        fac = GpuDetectorViewFactory(detector_numbers={'unified_detector': inst.detector_number},
+                                     view_config=cfg, out_dtype='float32')
+        sw = ShardedDetectorViewWorkflow(fac.make_workflow('unified_detector', None, {}),
+                                         torch.device('cuda', 0))
+        assert sw._merge == 'push'
+        full = fac.make_workflow('unified_detector', None, {}) if rank == 0 else None
+        # (ranks with a share of the batch, finalize after it)
+        plan = [((0, 1), False), ((1,), True), ((0,), False), ((), False), ((1,), True),
+                ((0, 1), True), ((1,), True), ((0, 1), True)]
+        ok = True
+        for b, (owners, fin) in enumerate(plan):
+            n = 45_000 * 14 + b
+            pid, toa = synthetic.uniform_events(n, 1, 13_500, seed=500 + b)
+            data = {}
+            if rank in owners:
+                lo, hi = shard_bounds(n, owners.index(rank), len(owners))
+                data['unified_detector'] = (pid[lo:hi], toa[lo:hi])
+            sw.accumulate(data, start_time=_t(b), end_time=_t(b + 1))
+            if rank == 0:
+                full.accumulate({'unified_detector': (pid, toa)} if owners else {},
+                                start_time=_t(b), end_time=_t(b + 1))
+            if not fin:
+                continue
+            out = sw.finalize()
+            if rank == 0:
+                ref = full.finalize()
+                if out is None or not _same(out, ref):
+                    ok = f'batch {b}: root outputs differ from one workflow'
+                    break
+                if out['current'].values.dtype != np.float32 or not out['current'].values.sum() > 0:
+                    ok = f'batch {b}: float32 image expected'
+                    break
+            elif out is not None:
+                ok = 'non-root returned outputs'
+                break
+        q.put((rank, ok))
+    except Exception as e:  # pragma: no cover - reported through the queue
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
 def _outputs_merge(rank, world, port, q):
     _sharded_worker(rank, world, port, q, 'outputs')
 
@@ -264,6 +330,10 @@ def test_sharded_workflow_outputs_merge_with_move_and_clear():
 
 def test_sharded_workflow_window_merge_with_roi_spectra():
     _run(_window_merge)
+
+
+def test_sharded_workflow_push_merge_float32_ranks_without_events():
+    _run(_push_worker)
 
 
 def test_sharded_workflow_subgroup_root_is_global_rank():
