@@ -1154,8 +1154,6 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
     c.n_bins = h->nbins;
     c.hot_fmt = h->d_hot_fmt;
     c.ablate = h->cold_sort_ablate;
-    c.depth = (int)env_ll("LDE_COLD_DEPTH", 0);
-    c.xcd = (int)env_ll("LDE_COLD_XCD", 0);
     c.all_hot = h->all_hot[replica];
     Timed tm(h, LDE_K_PAGED);
     HIPCALL(h, lde::launch_cold_pipeline(c, h->stream, h->bin_stop_ext));

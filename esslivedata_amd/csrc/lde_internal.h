@@ -209,7 +209,7 @@ struct SieveArgs {
     long long cold_cap;  // 24-bit keys per block region (region stride cold_cap + 16)
     uint32_t *cold_cnt;
     int tile_bits, n_tiles;  // cold keys are counted per tile of 2^tile_bits bins
-    uint32_t *cold_tcnt;     // [grid][kColdGroups][n_tiles]
+    uint32_t *cold_tcnt;     // [n_tiles][grid][kColdGroups]
     int ablate;  // diagnostics build: timing ablation (0 = the real pass)
     uint32_t *hot_fmt = nullptr;  // [grid] 1: the block's hot rows left as u16, 0: as u32
     unsigned long long *trace = nullptr;  // diagnostic [grid][3]: start, stream end, end (realtime)
@@ -239,8 +239,6 @@ struct ColdArgs {
     const uint32_t *hot_fmt = nullptr;  // per sieve block: hot rows as u16 (1) or u32 (0)
     int ablate = 0;     // cold-sort diagnostics (wrong results): 1 no writes, 2 no scatter,
                         // 16 prologue only
-    int depth = 0;      // diagnostics: 1 = one load step in flight in the direct sort
-    int xcd = 0;        // diagnostics: sort rows on the XCD of their sieve block
     int all_hot = 0;    // every screen has a hot row (no cold keys): hot-row reduce only
 };
 constexpr int kSortThreadsHost = 256;          // cold-sort block (thread t owns tile t)

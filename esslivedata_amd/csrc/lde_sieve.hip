@@ -595,10 +595,11 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
             a.trace[(size_t)blockIdx.x * 3 + tid] =
                 tid == 0 ? t_start : tid == 1 ? t_stream : __builtin_amdgcn_s_memrealtime();
     }
+    // tile-major [tile][block][group]: each tile's counts contiguous for
+    // k_hot_reduce_scan (a block's eight groups are one 32-byte piece)
     for (int i = tid; i < kColdGroups * a.n_tiles; i += kSplitThreads) {
-        const int g = i / a.n_tiles, t = i - g * a.n_tiles;
-        a.cold_tcnt[((size_t)blockIdx.x * kColdGroups + g) * a.n_tiles + t] =
-            sm[o_tcnt + g * align4(a.n_tiles) + t];
+        const int t = i / kColdGroups, g = i % kColdGroups;
+        a.cold_tcnt[((size_t)t * gridDim.x + blockIdx.x) * kColdGroups + g] = sm[o_tcnt + g * align4(a.n_tiles) + t];
     }
     // write this XCD's dirty lines back while other blocks still stream,
     // instead of all at the end-of-kernel release (round 2: -10 to -15 us)
@@ -655,14 +656,25 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
     }
     const int t = blockIdx.x - hot_blocks;
     const int rows = c.rows * kColdGroups;
-    // eight rows per thread per round, all loads issued before the scan
-    constexpr int R = 8;
+    // eight rows per thread per round (one sieve block's groups: two 16-byte
+    // loads of the tile-major counts), all loads issued before the scan
+    constexpr int R = kColdGroups;
+    static_assert(R == 8, "one sieve block per thread");
+    const uint32_t *col = c.tcnt + (size_t)t * rows;
+    uint32_t *ocol = c.boff + (size_t)t * rows;
     uint32_t carry = 0;
     for (int r0 = 0; r0 < rows; r0 += 256 * R) {
         const int rb = r0 + (int)threadIdx.x * R;
         uint32_t v[R], sum = 0;
+        if (rb < rows) {
+            const uint4 a = *reinterpret_cast<const uint4 *>(col + rb);
+            const uint4 b = *reinterpret_cast<const uint4 *>(col + rb + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+            v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        } else {
 #pragma unroll
-        for (int u = 0; u < R; ++u) v[u] = rb + u < rows ? c.tcnt[(size_t)(rb + u) * c.n_tiles + t] : 0u;
+            for (int u = 0; u < R; ++u) v[u] = 0u;
+        }
 #pragma unroll
         for (int u = 0; u < R; ++u) {
             v[u] = (v[u] + 7u) & ~7u;  // k_cold_sort: 16-byte aligned (row, tile) ranges
@@ -672,8 +684,13 @@ __global__ __launch_bounds__(256) void k_hot_reduce_scan(ColdArgs c, int hot_blo
         uint32_t ex = carry + block_exclusive_scan(sum, s_w, &tot);
 #pragma unroll
         for (int u = 0; u < R; ++u) {
-            if (rb + u < rows) c.boff[(size_t)(rb + u) * c.n_tiles + t] = ex;
+            const uint32_t x = ex;
             ex += v[u];
+            v[u] = x;
+        }
+        if (rb < rows) {
+            *reinterpret_cast<uint4 *>(ocol + rb) = make_uint4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<uint4 *>(ocol + rb + 4) = make_uint4(v[4], v[5], v[6], v[7]);
         }
         carry += tot;
         __syncthreads();
@@ -687,7 +704,8 @@ constexpr int kGroupWaves = (kSplitThreads / 64) / kColdGroups;  // sieve waves 
 constexpr int kSortSPW = kSortWaves / kGroupWaves;               // sort waves per sieve wave
 static_assert(kSortSPW >= 1 && kSortWaves % kGroupWaves == 0, "sort waves per sieve wave");
 constexpr int kSortKPT = 48;    // keys per lane per piece (piece path)
-constexpr int kColdDepth = 3;   // direct path: steps of 16 keys per lane per load round
+constexpr int kColdDepth = 1;   // direct path: steps of 16 keys per lane per load round
+                                // (two rounds in flight; 3: +1.4 us on DREAM)
 
 // Balanced pass-B items (tile, first key, end key, tile has one item) of the
 // tile-major key array: a tile with n keys gets ceil(n / item_keys) items.
@@ -809,9 +827,8 @@ __device__ void cold_sort_direct(const ColdArgs &c, uint32_t *sm, int row, uint3
     const WaveKeys wk = wave_keys(c, b, grp, wv);
     const uint32_t dcur = (uint32_t)(nt4 + lane);
     // The wave's keys in rounds of D steps of 64 x 16 keys, two rounds in
-    // flight: a wave's region (about 4K keys on DREAM) is requested almost at
-    // once, so a block waits for about one memory latency, not one per step
-    // (one step in flight: 57 us for DREAM's 3.4e7 keys, 40 of them loads)
+    // flight (D = 3, most of a wave's keys requested at once, measured no
+    // better: the sort is bound by its read + write traffic, not latency)
     constexpr uint32_t STEP = 64u * 16u, ROUND = STEP * (uint32_t)D;
     typedef v3u Round[D][4];
     auto fetch = [&](Round &buf, uint32_t r0) __attribute__((always_inline)) {
@@ -1039,9 +1056,10 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(ColdArgs c, uint32_t
     const int n_tiles = c.n_tiles;
     const int tid = threadIdx.x;
     int row = blockIdx.x;
-    if (LDE_DIAG(c.xcd) && (c.rows & 7) == 0) {
-        // diagnostics: the rows of sieve block b on XCD b % 8, where that
-        // block ran (workgroups go round-robin over the eight XCDs)
+    if ((c.rows & 7) == 0) {
+        // the rows of sieve block b on XCD b % 8, where that block ran and
+        // wrote its keys (workgroups go round-robin over the eight XCDs):
+        // DREAM -1.5 us
         const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
         row = ((k / kColdGroups) * 8 + x) * kColdGroups + k % kColdGroups;
     }
@@ -1051,10 +1069,11 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(ColdArgs c, uint32_t
     const bool own = tid < n_tiles;
     // own tile: global position of this row's range, the row's exact count
     const uint32_t tt = own ? c.tile_total[tid] : 0u;
-    const uint32_t cnt = own ? c.tcnt[(size_t)row * n_tiles + tid] : 0u;
+    const size_t rows_all = (size_t)c.rows * kColdGroups;
+    const uint32_t cnt = own ? c.tcnt[(size_t)tid * rows_all + row] : 0u;
     uint32_t total;
     const uint32_t base = block_exclusive_scan(tt, s_w, &total);
-    const uint32_t gpos = own ? base + c.boff[(size_t)row * n_tiles + tid] : 0u;
+    const uint32_t gpos = own ? base + c.boff[(size_t)tid * rows_all + row] : 0u;
     __syncthreads();
     uint32_t tot8;
     const uint32_t B = block_exclusive_scan((cnt + 7u) & ~7u, s_w, &tot8);
@@ -1203,17 +1222,10 @@ hipError_t launch_cold_pipeline(const ColdArgs &c, hipStream_t st, hipEvent_t st
     switch (c.tile_bits) {
 #define LDE_COLD(TB)                                                                              \
     case TB:                                                                                      \
-        if (LDE_DIAG(c.depth) == 1) {                                                             \
-            (void)hipFuncSetAttribute((const void *)k_cold_sort<TB, 1>,                           \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);      \
-            hipLaunchKernelGGL((k_cold_sort<TB, 1>), dim3(c.rows * kColdGroups),                  \
-                               dim3(kSortThreads), sma, st, c, cap);                              \
-        } else {                                                                                  \
-            (void)hipFuncSetAttribute((const void *)k_cold_sort<TB, kColdDepth>,                  \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);      \
-            hipLaunchKernelGGL((k_cold_sort<TB, kColdDepth>), dim3(c.rows * kColdGroups),         \
-                               dim3(kSortThreads), sma, st, c, cap);                              \
-        }                                                                                         \
+        (void)hipFuncSetAttribute((const void *)k_cold_sort<TB, kColdDepth>,                      \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sma);          \
+        hipLaunchKernelGGL((k_cold_sort<TB, kColdDepth>), dim3(c.rows * kColdGroups),             \
+                           dim3(kSortThreads), sma, st, c, cap);                                  \
         if (!LDE_DIAG(c.ablate)) /* diagnostics: the keys are not valid */                       \
             hipExtLaunchKernelGGL(k_cold_accumulate<TB>, dim3(c.max_items), dim3(kTileThreads), 0, \
                                   st, nullptr, stop, 0, c.keys, c.items, c.item_count, c.hist,   \

@@ -549,6 +549,40 @@ def test_finalize_partials_match_finalize():
             assert not h[:S].any() and int(h[2 * S]) == 0 and int(h[2 * S + 2]) > 0
 
 
+@pytest.mark.parametrize('grid', ['8', '17'])
+def test_sieve_few_blocks_ragged_messages(grid, knobs):
+    """Few sieve blocks (long chunk ranges, chunk tables in LDS) over ragged
+    device messages (partial and misaligned chunks inside the ranges), three
+    batches on rotating replicas, bit-exact against the oracle."""
+    import torch
+
+    knobs(LDE_SPLIT_GRID=grid)
+    from esslivedata_amd import projection, synthetic
+
+    inst = synthetic.dream_mantle()
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    eng = _engine(view, edges, 'split')
+    o = ora.OracleDetectorView(detector_number=inst.detector_number,
+                               pixel_screen=_oracle_pixel_screen_geometric(inst),
+                               screen_shape=(80, 320), toa_edges_ns=edges)
+    rng = np.random.default_rng(int(grid))
+    for batch in range(3):
+        pid, toa = synthetic.dream_events(2_400_007 + batch, inst, seed=400 + batch)
+        dp = torch.as_tensor(pid, device='cuda')
+        dt = torch.as_tensor(toa, device='cuda')
+        cuts = np.sort(rng.choice(np.arange(1, len(pid)), 6, replace=False))
+        bounds = [0, *cuts.tolist(), len(pid)]
+        eng.stage_tensors_batch([(dp[a:b], dt[a:b]) for a, b in zip(bounds[:-1], bounds[1:])])
+        eng.accumulate(batch % view.n_replicas)
+        o.accumulate(pid, toa)
+        assert eng.info()['last_strategy'] == 'split'
+    res = eng.finalize(hists=True)
+    exp = o.finalize()
+    np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
+    np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
+
+
 @pytest.mark.parametrize('n_msgs', [1, 14, 24, 25, 40])
 def test_split_many_device_messages(n_msgs, knobs):
     """SIEVE with the message descriptors passed as kernel arguments (<= 24

@@ -93,7 +93,9 @@ def test_dream_wavelength_matches_oracle(strategy, scale, table_min):
 
 # keyed SPLIT pass variant (diagnostics build): the general event pass (bin
 # loops, grid coordinate per event) beside the default FAST one
-KEYED_VARIANTS = [{'LDE_COORD_FIXED_BIN': '0'}]
+KEYED_VARIANTS = [{'LDE_COORD_FIXED_BIN': '0'},
+                  # few sieve blocks over the key stream
+                  {'LDE_SPLIT_GRID': '9'}]
 
 
 @pytest.mark.parametrize('variant', range(len(KEYED_VARIANTS)))
