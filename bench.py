@@ -29,7 +29,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-PROFILE_ROUND = 'r4'  # profiles/<round>_<workload>_bench.json (tools/prof_round.sh)
+PROFILE_ROUND = 'r5'  # profiles/<round>_<workload>_bench.json (tools/prof_round.sh)
 # bench kernel name -> device symbol in the rocprofv3 summary
 KERNEL_SYMBOL = {
     'atomic': 'k_bin_atomic',
@@ -37,7 +37,7 @@ KERNEL_SYMBOL = {
     'tile_accumulate': 'k_tile_accumulate',
     'paged': 'k_paged_partition',
     'page_accumulate': 'k_page_accumulate',
-    'split': 'k_sieve',  # SPLIT's event pass (k_split when LDE_SIEVE=0)
+    'split': 'k_sieve',  # SPLIT's event pass
     'coord': 'k_event_key',  # wavelength-mode keyed coordinate pass (its per-replica tables cached)
     'pixel': 'k_pix_scatter',  # PIXEL pass A's partition kernel (after k_pix_chunks and the scans)
     'page_accumulate': 'k_page_accumulate',
@@ -45,9 +45,9 @@ KERNEL_SYMBOL = {
     'finalize': 'k_finalize_v4',
 }
 # engine timing buckets (include/lde.h LDE_K_*) as they are used by the SPLIT
-# strategy's SIEVE pass: 'split' = k_chunk_tab + k_sieve, 'split_aux' = hot-set
-# selection + k_hot_reduce, 'paged' = the cold-key pipeline (k_cold_scan,
-# k_cold_plan, k_cold_sort, k_cold_accumulate)
+# strategy's SIEVE pass: 'split' = k_sieve, 'split_aux' = hot-set selection,
+# 'paged' = the cold-key pipeline (k_hot_reduce_scan, k_cold_sort,
+# k_cold_accumulate)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_EVENT = 8  # int32 pixel_id + int32 time_of_flight
 # the wavelength-mode coordinate pass also writes its 4-byte per-event word

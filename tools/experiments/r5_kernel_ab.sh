@@ -15,4 +15,5 @@ for cfg in ${CFGS:-X=0}; do
   for kv in ${cfg//,/ }; do unset ${kv%%=*}; done
   echo "== $cfg"
   python tools/kstats_db.py $(find /tmp/prof_$tag/$i -name "*results.db" | head -1) 40 | grep "_ZN3lde" | grep -v "pix_chunks\|sample\|select\|screen_sum\|sieve_table\|glut"
+  grep -o "\"ms_per_step\": [0-9.]*\|\"bit_exact_vs_oracle\": [a-z]*" gpurun_out/${tag}_$i.log | head -2 | tr "\n" " "; echo
 done
