@@ -745,6 +745,7 @@ def main():
         'roofline': {
             'bound': 'hbm',
             'kernel': dom,
+            'symbol': KERNEL_SYMBOL.get(dom),  # its device symbol in the rocprofv3 summary
             'achieved': achieved,
             'peak': HBM_PEAK_GBS,
             'unit': 'GB/s',
