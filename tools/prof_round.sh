@@ -8,7 +8,7 @@ WL=${WL:-dream}
 TAG=${TAG:-r3}
 NAME=${NAME:-$WL}  # profile name (e.g. wavelength with BENCH_ARGS="--coordinate wavelength")
 OUT=gpurun_out/prof_${TAG}_${NAME}
-ARGS="bench.py --workload $WL --steps ${STEPS:-10} --warmup 2 --timing-stride 1 --no-cpu-baseline --e2e-steps 0 ${BENCH_ARGS}"
+ARGS="bench.py --workload $WL --steps ${STEPS:-10} --warmup 2 --timing-stride 1 --no-cpu-baseline --e2e-steps 0 --bank-steps 0 ${BENCH_ARGS}"
 rm -rf $OUT
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 $ARGS > $OUT/kt.log 2>&1
