@@ -89,9 +89,9 @@ __global__ __launch_bounds__(256) void k_event_coord(CoordArgs a, const int *__r
     double *s_t = s_e + ((ne + 1) & ~1);
     const int ntab = TLDS ? a.nd * a.nt : 0;
     uint16_t *s_b = reinterpret_cast<uint16_t *>(s_t + ntab);
-    for (int i = threadIdx.x; i < ne; i += blockDim.x) s_e[i] = a.edges[i];
-    for (int i = threadIdx.x; i < ntab; i += blockDim.x) s_t[i] = a.table[i];
-    for (int i = threadIdx.x; i < a.G; i += blockDim.x) s_b[i] = a.buckets[i];
+    if (ne) lds_fill<2>(s_e, ne, [&](int i) { return g_ld(a.edges + i); });
+    if (ntab) lds_fill<4>(s_t, ntab, [&](int i) { return g_ld(a.table + i); });
+    if (a.G) lds_fill<4>(s_b, a.G, [&](int i) { return g_ld(a.buckets + i); });
     __syncthreads();
     // compile-time LDS or global: a runtime choice makes every edge read a
     // flat load (counted by both vmcnt and lgkmcnt)
@@ -248,14 +248,16 @@ __global__ __launch_bounds__(1024) void k_event_key(KeyArgs k) {
     uint16_t *s_b = reinterpret_cast<uint16_t *>(s_t + ntab);
     // FAST: per slot the distance row (u8, after the chunk pointers) and fx
     uint8_t *s_i = reinterpret_cast<uint8_t *>(s_b + ((a.G + 7) & ~7)) + 16 * kKeyLdsChunks;
-    for (uint32_t i = threadIdx.x; i < C; i += blockDim.x) {
-        s_w[i] = k.pix_tab[i];
-        s_d[i] = k.tab_d[i];
-        if (FAST) s_i[i] = k.tab_i[i];
-    }
-    for (int i = threadIdx.x; i < ne; i += blockDim.x) s_e[i] = i <= a.T ? a.edges[i] : __builtin_inf();
-    for (int i = threadIdx.x; i < ntab; i += blockDim.x) s_t[i] = a.table[i];
-    for (int i = threadIdx.x; i < a.G; i += blockDim.x) s_b[i] = a.buckets[i];
+    lds_fill<8>(s_w, (int)C, [&](int i) { return g_ld(k.pix_tab + i); });
+    lds_fill<8>(s_d, (int)C, [&](int i) { return g_ld(k.tab_d + i); });
+    if (FAST) lds_fill<8>(s_i, (int)C, [&](int i) { return g_ld(k.tab_i + i); });
+    if (ne)
+        lds_fill<2>(s_e, ne, [&](int i) {
+            const double v = g_ld(a.edges + (i <= a.T ? i : a.T));
+            return i <= a.T ? v : __builtin_inf();
+        });
+    if (ntab) lds_fill<4>(s_t, ntab, [&](int i) { return g_ld(a.table + i); });
+    if (a.G) lds_fill<4>(s_b, a.G, [&](int i) { return g_ld(a.buckets + i); });
     __syncthreads();
     const double *e = ELDS ? s_e : a.edges;
     const double *tab = TLDS ? s_t : a.table;

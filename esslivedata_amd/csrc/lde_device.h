@@ -25,14 +25,49 @@ __device__ __forceinline__ uint32_t ld_global_u32(const uint32_t *p) {
 }
 
 // ---------------------------------------------------------------------------
+// Kernel prologues: tables from global memory into LDS.  dst[i] = val(i) for
+// i < n, with the R loads of a thread issued before any of its stores.  A
+// plain `dst[i] = src[i]` loop waits for each load in turn (the compiler
+// cannot rule out that the LDS stores alias a generic source), which made
+// the sieve's 49 KB prologue four serial global round trips (~6 us).
+// val(i) must read global memory through address_space(1) (g_ld).
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T g_ld(const T *p) {
+    return *(const __attribute__((address_space(1))) T *)p;
+}
+__device__ __forceinline__ uint4 g_ld(const uint4 *p) {  // (HIP's uint4 is a class)
+    typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+    const v4u_t v = *(const __attribute__((address_space(1))) v4u_t *)p;
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+template <int R, typename T, typename F>
+__device__ __forceinline__ void lds_fill(T *dst, int n, F val) {
+    const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
+    for (int b = 0; b < n; b += R * nt) {
+        T v[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int i = b + k * nt + tid;
+            v[k] = val(i < n ? i : n - 1);
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int i = b + k * nt + tid;
+            if (i < n) dst[i] = v[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // TOA lookup
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void load_toa_tables(unsigned char *s_tab,
                                                 const unsigned char *__restrict__ g_tab,
                                                 const ToaParams &tp) {
-    const int n16 = (int)(toa_lds_bytes(tp) / 16);
-    for (int i = threadIdx.x; i < n16; i += blockDim.x)
-        reinterpret_cast<uint4 *>(s_tab)[i] = reinterpret_cast<const uint4 *>(g_tab)[i];
+    const uint4 *src = reinterpret_cast<const uint4 *>(g_tab);
+    lds_fill<4>(reinterpret_cast<uint4 *>(s_tab), (int)(toa_lds_bytes(tp) / 16),
+                [&](int i) { return g_ld(src + i); });
 }
 
 template <bool FAST>

@@ -1100,24 +1100,29 @@ int bin_split(lde_handle *h, std::vector<lde::SegDesc> &sd, long long chunks,
         HIPCALL(h, lde::launch_sieve(sa, grid, h->stream, sp.a, sp.b));
         sp.done = true;
         if (h->d_trace) {  // diagnostic only: a host sync per batch
-            std::vector<unsigned long long> tr((size_t)grid * 3);
+            std::vector<unsigned long long> tr((size_t)grid * 4);
             HIPCALL(h, hipMemcpyAsync(tr.data(), h->d_trace, tr.size() * 8, hipMemcpyDeviceToHost,
                                       h->stream));
             HIPCALL(h, hipStreamSynchronize(h->stream));
             unsigned long long s0 = ~0ull, s1 = 0, m0 = ~0ull, m1 = 0, e0 = ~0ull, e1 = 0;
+            double span = 0, init = 0;  // mean block init -> stream end, start -> init
             for (int b = 0; b < grid; ++b) {
-                s0 = std::min(s0, tr[3 * b]); s1 = std::max(s1, tr[3 * b]);
-                m0 = std::min(m0, tr[3 * b + 1]); m1 = std::max(m1, tr[3 * b + 1]);
-                e0 = std::min(e0, tr[3 * b + 2]); e1 = std::max(e1, tr[3 * b + 2]);
+                span += (double)(tr[4 * b + 1] - tr[4 * b + 3]) / grid;
+                init += (double)(tr[4 * b + 3] - tr[4 * b]) / grid;
+                s0 = std::min(s0, tr[4 * b]); s1 = std::max(s1, tr[4 * b]);
+                m0 = std::min(m0, tr[4 * b + 1]); m1 = std::max(m1, tr[4 * b + 1]);
+                e0 = std::min(e0, tr[4 * b + 2]); e1 = std::max(e1, tr[4 * b + 2]);
             }
             const double us = 1e6 / 100e6;  // s_memrealtime: 100 MHz
             h->trace_stats.push_back((s1 - s0) * us);
             h->trace_stats.push_back((m1 - m0) * us);
             h->trace_stats.push_back((e1 - e0) * us);
             h->trace_stats.push_back((e1 - s0) * us);
+            h->trace_stats.push_back(span * us);
+            h->trace_stats.push_back(init * us);
             if (env_ll("LDE_SIEVE_TRACE", 0) > 1) {  // per block: stream end after the first start
                 fprintf(stderr, "lde sieve trace blocks:");
-                for (int b = 0; b < grid; ++b) fprintf(stderr, " %.1f", (tr[3 * b + 1] - s0) * us);
+                for (int b = 0; b < grid; ++b) fprintf(stderr, " %.1f", (tr[4 * b + 1] - s0) * us);
                 fprintf(stderr, "\n");
             }
         }
@@ -1718,14 +1723,15 @@ void release(lde_handle *h) {
     for (hipEvent_t e : {h->pin_done, h->segs_done, h->fin_event, h->block_event})
         if (e) (void)hipEventDestroy(e);
     if (h->d_trace && !h->trace_stats.empty()) {
-        const size_t n = h->trace_stats.size() / 4;
-        double a[4] = {0, 0, 0, 0};
+        const size_t n = h->trace_stats.size() / 6;
+        double a[6] = {0, 0, 0, 0, 0, 0};
         for (size_t i = 0; i < n; ++i)
-            for (int q = 0; q < 4; ++q) a[q] += h->trace_stats[4 * i + q];
+            for (int q = 0; q < 6; ++q) a[q] += h->trace_stats[6 * i + q];
         fprintf(stderr,
                 "lde sieve trace (%zu launches, us): block start spread %.2f, stream-end spread %.2f, "
-                "end spread %.2f, first start -> last end %.2f\n",
-                n, a[0] / n, a[1] / n, a[2] / n, a[3] / n);
+                "end spread %.2f, first start -> last end %.2f, mean block init -> stream end %.2f, "
+                "mean block start -> init %.2f\n",
+                n, a[0] / n, a[1] / n, a[2] / n, a[3] / n, a[4] / n, a[5] / n);
     }
     dev_free(h->d_trace);
     for (auto &g : h->groups) {
@@ -2024,7 +2030,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
             CREATE_CHECK(dev_alloc(h, &h->d_cold_cnt, (size_t)h->split_grid * (lde::kSplitThreads / 64)));
             CREATE_CHECK(dev_alloc(h, &h->d_hot_fmt, (size_t)h->split_grid));
             if (env_ll("LDE_SIEVE_TRACE", 0) != 0)
-                CREATE_CHECK(dev_alloc(h, &h->d_trace, (size_t)h->split_grid * 3));
+                CREATE_CHECK(dev_alloc(h, &h->d_trace, (size_t)h->split_grid * 4));
             CREATE_HIP(hipHostMalloc((void **)&h->h_sel_stats, (size_t)h->R * 16, hipHostMallocDefault));
         }
 #ifdef LDE_DIAGNOSTICS

@@ -212,7 +212,7 @@ struct SieveArgs {
     uint32_t *cold_tcnt;     // [n_tiles][grid][kColdGroups]
     int ablate;  // diagnostics build: timing ablation (0 = the real pass)
     uint32_t *hot_fmt = nullptr;  // [grid] 1: the block's hot rows left as u16, 0: as u32
-    unsigned long long *trace = nullptr;  // diagnostic [grid][3]: start, stream end, end (realtime)
+    unsigned long long *trace = nullptr;  // diagnostic [grid][4]: start, stream end, end, init done (realtime)
     int keyed = 0;  // the 'toa' stream holds finished pixel words (k_event_key): no probe/gather/TOA
 };
 size_t sieve_smem(int hot_words, int cbits, int toa_words4, int n_tiles);

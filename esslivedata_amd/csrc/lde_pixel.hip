@@ -474,12 +474,15 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
                                                          const uint4 *__restrict__ items,
                                                          const uint32_t *__restrict__ item_count,
                                                          int T, uint32_t *__restrict__ hist) {
-    if (blockIdx.x >= *item_count) {
+    // the item and the count together (items holds the grid's max_items
+    // entries), one round trip before the item's loads instead of two
+    const uint32_t n_items = *item_count;
+    const uint4 it = items[blockIdx.x];
+    if (blockIdx.x >= n_items) {
         if (a.pred > 0.f) pix_overflow(a, loc, fp_off, fp_scr, T, hist);
         return;
     }
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint4 it = items[blockIdx.x];
     const uint32_t r = it.x;
     const uint32_t f0 = fp_off[r], nf = fp_off[r + 1] - f0;
     const uint32_t nbin = nf * (uint32_t)T;
@@ -487,8 +490,11 @@ __global__ __launch_bounds__(1024) void k_pix_accumulate(PixArgs a, const uint16
     uint16_t *s_loc = reinterpret_cast<uint16_t *>(smem);
     uint32_t *s_cnt = reinterpret_cast<uint32_t *>(smem + align16((size_t)2 << a.rb));
     const size_t q0 = (size_t)r << a.rb;
-    for (uint32_t j = threadIdx.x; j < span; j += blockDim.x)
-        s_loc[j] = q0 + j < a.L ? loc[q0 + j] : (uint16_t)0xFFFFu;
+    lds_fill<4>(s_loc, (int)span, [&](int j) {
+        const size_t q = q0 + (size_t)j;
+        const uint16_t v = g_ld(loc + (q < a.L ? q : 0));
+        return q < a.L ? v : (uint16_t)0xFFFFu;
+    });
     for (uint32_t j = threadIdx.x; j < nbin; j += blockDim.x) s_cnt[j] = 0;
     const uint32_t mask = span - 1u;
     // events the view drops and pads count into a lane-private dummy word

@@ -235,10 +235,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     SegDesc *s_seg = reinterpret_cast<SegDesc *>(sm + o_seg);
     for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.hot_words; i += kSplitThreads * 4u)
         *reinterpret_cast<uint4 *>(sm + i) = make_uint4(0, 0, 0, 0);
-    for (uint32_t i = (uint32_t)tid * 4u; i < C; i += kSplitThreads * 4u)
-        *reinterpret_cast<uint4 *>(sm + o_pc + i) = *reinterpret_cast<const uint4 *>(a.pix_tab + i);
-    for (uint32_t i = (uint32_t)tid * 4u; i < (uint32_t)a.toa_words4; i += kSplitThreads * 4u)
-        *reinterpret_cast<uint4 *>(sm + o_tt + i) = *reinterpret_cast<const uint4 *>(a.ttab + i);
+    {  // pixel table and TOA buckets (contiguous in LDS): one round of loads
+        const uint4 *pt = reinterpret_cast<const uint4 *>(a.pix_tab);
+        const uint4 *tt = reinterpret_cast<const uint4 *>(a.ttab);
+        const int c4 = (int)(C / 4u);
+        lds_fill<4>(reinterpret_cast<uint4 *>(sm + o_pc), c4 + a.toa_words4 / 4,
+                    [&](int i) { return g_ld(i < c4 ? pt + i : tt + (i - c4)); });
+    }
     if (tid < 64) sm[o_dum + tid] = 0;
     // cursor, hot-count overflow vote
     if (tid == 0) sm[o_cur] = sm[o_cur + 1] = sm[o_cur + 2] = sm[o_cur + 3] = 0;
@@ -314,6 +317,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
         }
         __syncthreads();
     }
+    const unsigned long long t_init = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint32_t o_ctab4 = o_ctab * 4u;
     auto fetch = [&](long long c) __attribute__((always_inline)) {
         if (!GCT) {
@@ -591,9 +595,9 @@ __global__ __launch_bounds__(kSplitThreads) void k_sieve(SieveArgs a) {
     if (tid == 0) a.hot_fmt[blockIdx.x] = packed ? 1u : 0u;
     if (a.trace) {  // diagnostic: per-block timeline (LDE_SIEVE_TRACE)
         __syncthreads();
-        if (tid < 3)
-            a.trace[(size_t)blockIdx.x * 3 + tid] =
-                tid == 0 ? t_start : tid == 1 ? t_stream : __builtin_amdgcn_s_memrealtime();
+        if (tid < 4)
+            a.trace[(size_t)blockIdx.x * 4 + tid] =
+                tid == 0 ? t_start : tid == 1 ? t_stream : tid == 2 ? __builtin_amdgcn_s_memrealtime() : t_init;
     }
     // tile-major [tile][block][group]: each tile's counts contiguous for
     // k_hot_reduce_scan (a block's eight groups are one 32-byte piece)
@@ -781,6 +785,22 @@ __device__ __forceinline__ WaveKeys wave_keys(const ColdArgs &c, int b, int grp,
     return WaveKeys{make_rsrc(base, (hi - lo) * 3u), hi - lo};
 }
 
+// The wave's keys in rounds of D steps of 64 x 16 keys (lane: 4 x 4 keys of
+// each step as 12-byte groups; past the region: zeros, masked at use)
+constexpr uint32_t kSortStep = 64u * 16u;
+template <int D>
+using SortRound = v3u[D][4];
+template <int D>
+__device__ __forceinline__ void sort_fetch(const WaveKeys &wk, SortRound<D> &buf, uint32_t r0, int lane) {
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            buf[d][j] = __builtin_amdgcn_raw_buffer_load_b96(
+                wk.rs, (int)((r0 + (uint32_t)d * kSortStep + (uint32_t)j * 256u + (uint32_t)lane * 4u) * 3u), 0,
+                0);
+}
+
 // Cold-key sort of one (sieve block, wave group) row into its tile ranges of
 // the tile-major u16 key array.  The sieve counted the row's keys per tile
 // exactly, so its ranges are known before any key is read (range (row, t) at
@@ -795,14 +815,14 @@ __device__ __forceinline__ WaveKeys wave_keys(const ColdArgs &c, int b, int grp,
 // per-wave cursors, carrying partial 8-key groups between pieces.
 template <int TB, int D>
 __device__ void cold_sort_direct(const ColdArgs &c, uint32_t *sm, int row, uint32_t cap, uint32_t cnt,
-                                 uint32_t B, uint32_t tot8, uint32_t gpos) {
+                                 uint32_t B, uint32_t tot8, uint32_t gpos, const WaveKeys &wk,
+                                 SortRound<D> &bA) {
     constexpr uint32_t MASK = (1u << TB) - 1u;
     constexpr int SH = TB + 2;  // keys are scaled by 4
     const int n_tiles = c.n_tiles;
     const int nt4 = align4(n_tiles);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int b = row / kColdGroups, grp = row % kColdGroups;
     // LDS: cursors [tile] + 64 lane dummies | segment base [tile] | global
     // position [tile] | 8-key groups [tile] | image (cap + 64 lane dummies) |
     // group -> tile (u16)
@@ -824,22 +844,13 @@ __device__ void cold_sort_direct(const ColdArgs &c, uint32_t *sm, int row, uint3
     if (tid < 64) s_cur[nt4 + tid] = cap + (uint32_t)tid;  // lane dummies never move far
     __syncthreads();
     if (LDE_DIAG(c.ablate) & 16) return;  // diagnostics: the prologue only
-    const WaveKeys wk = wave_keys(c, b, grp, wv);
     const uint32_t dcur = (uint32_t)(nt4 + lane);
-    // The wave's keys in rounds of D steps of 64 x 16 keys, two rounds in
-    // flight (D = 3, most of a wave's keys requested at once, measured no
-    // better: the sort is bound by its read + write traffic, not latency)
-    constexpr uint32_t STEP = 64u * 16u, ROUND = STEP * (uint32_t)D;
-    typedef v3u Round[D][4];
-    auto fetch = [&](Round &buf, uint32_t r0) __attribute__((always_inline)) {
-#pragma unroll
-        for (int d = 0; d < D; ++d)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)  // past the region: zeros (masked at use)
-                buf[d][j] = __builtin_amdgcn_raw_buffer_load_b96(
-                    wk.rs, (int)((r0 + (uint32_t)d * STEP + (uint32_t)j * 256u + (uint32_t)lane * 4u) * 3u),
-                    0, 0);
-    };
+    // two rounds in flight (D = 3, most of a wave's keys requested at once,
+    // measured no better: the sort is bound by its read + write traffic, not
+    // latency); the first round was requested before the prologue's scans
+    constexpr uint32_t STEP = kSortStep, ROUND = STEP * (uint32_t)D;
+    typedef SortRound<D> Round;
+    auto fetch = [&](Round &buf, uint32_t r0) __attribute__((always_inline)) { sort_fetch<D>(wk, buf, r0, lane); };
     auto scatter = [&](const Round &buf, uint32_t r0) __attribute__((always_inline)) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
@@ -877,8 +888,7 @@ __device__ void cold_sort_direct(const ColdArgs &c, uint32_t *sm, int row, uint3
             }
         }
     };
-    Round bA, bB;
-    if (wk.n) fetch(bA, 0);
+    Round bB;
     for (uint32_t r0 = 0; r0 < wk.n; r0 += 2 * ROUND) {
         if (r0 + ROUND < wk.n) fetch(bB, r0 + ROUND);
         scatter(bA, r0);
@@ -902,7 +912,7 @@ __device__ void cold_sort_direct(const ColdArgs &c, uint32_t *sm, int row, uint3
 }
 
 template <int TB>
-__device__ void cold_sort_pieces(const ColdArgs &c, uint32_t *sm, int row, uint32_t gpos) {
+__device__ void cold_sort_pieces(const ColdArgs &c, uint32_t *sm, int row, uint32_t gpos, const WaveKeys &wk) {
     constexpr int KPT = kSortKPT;
     constexpr int PIECE = kSortThreads * KPT;
     const int n_tiles = c.n_tiles;
@@ -922,9 +932,7 @@ __device__ void cold_sort_pieces(const ColdArgs &c, uint32_t *sm, int row, uint3
     uint16_t *s_gt = reinterpret_cast<uint16_t *>(s_w + 32);  // [group] its tile
     const int tid = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int b = row / kColdGroups, grp = row % kColdGroups;
     const bool own = tid < n_tiles;  // thread tid owns tile tid
-    const WaveKeys wk = wave_keys(c, b, grp, wv);
     if (own) s_pos[tid] = gpos;
     if (lane == 0) s_w[20 + wv] = (wk.n + 64 * KPT - 1) / (64 * KPT);
     __syncthreads();
@@ -1067,6 +1075,13 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(ColdArgs c, uint32_t
         plan_items(c.tile_total, n_tiles, c.item_keys, c.items, c.item_count, c.max_items, s_w, sm,
                    sm + kMaxTiles + 1);
     const bool own = tid < n_tiles;
+    // the wave's key region and its first round of keys, requested before
+    // the scans below (they only feed the direct path's loop: a row taking
+    // the piece path reads its keys again)
+    const WaveKeys wk = wave_keys(c, row / kColdGroups, row % kColdGroups,
+                                  __builtin_amdgcn_readfirstlane(tid >> 6));
+    SortRound<D> bA;
+    if (wk.n) sort_fetch<D>(wk, bA, 0, tid & 63);
     // own tile: global position of this row's range, the row's exact count
     const uint32_t tt = own ? c.tile_total[tid] : 0u;
     const size_t rows_all = (size_t)c.rows * kColdGroups;
@@ -1079,9 +1094,9 @@ __global__ __launch_bounds__(kSortThreads) void k_cold_sort(ColdArgs c, uint32_t
     const uint32_t B = block_exclusive_scan((cnt + 7u) & ~7u, s_w, &tot8);
     __syncthreads();
     if (tot8 <= cap)
-        cold_sort_direct<TB, D>(c, sm, row, cap, cnt, B, tot8, gpos);
+        cold_sort_direct<TB, D>(c, sm, row, cap, cnt, B, tot8, gpos, wk, bA);
     else
-        cold_sort_pieces<TB>(c, sm, row, gpos);
+        cold_sort_pieces<TB>(c, sm, row, gpos, wk);
 }
 
 // pass B: one item = a contiguous key range of one tile
@@ -1093,8 +1108,11 @@ __global__ __launch_bounds__(kTileThreads) void k_cold_accumulate(
     // + 64 lane-private dummy counters: pads and keys outside the item count
     // there, so no lane branches around its LDS atomic
     __shared__ __attribute__((aligned(16))) uint32_t s_tile[NB + 64];
-    if (blockIdx.x >= *item_count) return;
+    // the item and the count together (items holds the grid's max_items
+    // entries), one round trip before the first key load instead of two
+    const uint32_t n_items = *item_count;
     const uint4 it = items[blockIdx.x];
+    if (blockIdx.x >= n_items) return;
     for (int i = threadIdx.x * 4; i < NB + 64; i += kTileThreads * 4)
         *reinterpret_cast<uint4 *>(s_tile + i) = make_uint4(0, 0, 0, 0);
     __syncthreads();
