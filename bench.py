@@ -36,11 +36,10 @@ KERNEL_SYMBOL = {
     'partition': 'k_partition',
     'tile_accumulate': 'k_tile_accumulate',
     'paged': 'k_paged_partition',
-    'page_accumulate': 'k_page_accumulate',
+    'page_accumulate': 'k_page_accumulate',  # (PIXEL's pass B, k_pix_accumulate, shares the bucket)
     'split': 'k_sieve',  # SPLIT's event pass
     'coord': 'k_event_key',  # wavelength-mode keyed coordinate pass (its per-replica tables cached)
     'pixel': 'k_pix_scatter',  # PIXEL pass A's partition kernel (after k_pix_chunks and the scans)
-    'page_accumulate': 'k_page_accumulate',
     'monitor': 'k_monitor',  # monitor TOA histogram (--workload monitor)
     'finalize': 'k_finalize_v4',
 }

@@ -328,13 +328,13 @@ int lde_synchronize(lde_handle *h);
 #define LDE_K_MONITOR 4   /* k_monitor: 1-D TOA histogram                    */
 #define LDE_K_FINALIZE 5  /* k_finalize / merge kernels                      */
 #define LDE_K_BINNING 6   /* whole binning sequence of one accumulate        */
-#define LDE_K_PAGED 7     /* k_paged_partition: PAGED pass A                  */
+#define LDE_K_PAGED 7     /* PAGED pass A (k_paged_partition); SPLIT: the cold-key path (k_hot_reduce_scan + k_cold_sort + k_cold_accumulate) */
 #define LDE_K_PAGE_PLAN 8 /* k_page_count/scan/plan/scatter                   */
-#define LDE_K_PAGE_ACC 9  /* k_page_accumulate: PAGED pass B                  */
-#define LDE_K_SPLIT 10    /* k_split: SPLIT event pass (hot rows in LDS, cold keys out) */
+#define LDE_K_PAGE_ACC 9  /* pass B: k_page_accumulate (PAGED), k_pix_accumulate (PIXEL) */
+#define LDE_K_SPLIT 10    /* k_sieve: SPLIT event pass (hot rows in LDS, cold keys out) */
 #define LDE_K_SPLIT_AUX 11 /* hot-set selection, hot-row reduce, cold segment table */
 #define LDE_K_COORD 12    /* k_event_coord / k_event_key: wavelength-mode coordinate pass */
-#define LDE_K_PIXEL 13    /* k_pix_count + k_pix_scan + k_pix_scatter: PIXEL pass A */
+#define LDE_K_PIXEL 13    /* k_pix_scatter: PIXEL pass A (stamped by its own dispatch) */
 #define LDE_K_COUNT 14
 int lde_timing_enable(lde_handle *h, int32_t enable);
 /* Record only the kernels whose bit (1 << LDE_K_*) is set in mask (default:
