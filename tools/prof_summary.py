@@ -81,7 +81,13 @@ def main(prof: Path, stem: Path) -> None:
             continue
         e = {'calls': d['calls'], 'avg_ms': d['avg_ms']}
         if len(durs.get(k, [])) > 2:
-            e['avg_ms_steady'] = sum(durs[k][2:]) / (len(durs[k]) - 2)
+            # past the first two, the dispatches of the bench's step batch:
+            # launches under half the median are other sizes (the wavelength
+            # bench's parity check bins a smaller batch after the timed steps)
+            st = durs[k][2:]
+            med = sorted(st)[len(st) // 2]
+            st = [x for x in st if x >= 0.5 * med]
+            e['avg_ms_steady'] = sum(st) / len(st)
             g = sorted(gaps[k][2:])  # median: the steps after the timed region wait on the host
             e['gap_before_ms_steady'] = g[len(g) // 2]
         pm = {c: sum(v) / len(v) for c, v in counters.get(k, {}).items()}
