@@ -231,8 +231,25 @@ def reference_kats_r2() -> list[dict]:
 
 def reference_kats_r5() -> list[dict]:
     """Window time coords (round 5): integer ns scalars as Timestamp.to_scipp()
-    makes them (SRC/core/timestamp.py:216-220)."""
+    makes them (SRC/core/timestamp.py:216-220); the monitor's cumulative
+    against its clearing window over two cycles."""
     return [
+        {
+            'name': 'monitor_cumulative_accumulates_window_clears',
+            'source': 'tests/workflows/monitor_workflow_test.py:484-516',
+            'note': 'the class fixtures of :349-360: edges linspace(0, 10, 11) ns, '
+                    'event_time_offset [1.5, 2.5, 3.5, 7.5, 8.5] ns (floored to int32 ns on '
+                    'the ev44 wire: same bins); the same events accumulated in two cycles',
+            'toa_ns': [1, 2, 3, 7, 8],
+            'edges_ns': np.linspace(0, 10, 11).tolist(),
+            'cycles': [[0, 1000], [1000, 2000]],
+            'expected': [
+                {'cumulative_sum': 5.0, 'current_sum': 5.0},
+                {'cumulative_sum': 10.0, 'counts_total_cumulative': 10.0,
+                 'counts_in_toa_range_cumulative': 10.0, 'current_sum': 5.0,
+                 'counts_total': 5.0, 'counts_in_toa_range': 5.0},
+            ],
+        },
         {
             'name': 'window_outputs_time_coords',
             'source': 'tests/workflows/detector_view/integration_test.py:28-84',

@@ -183,6 +183,27 @@ def test_monitor_full_workflow_cycle():
         assert float(out[k].values) == exp[k]
 
 
+def test_monitor_cumulative_accumulates_window_clears():
+    from esslivedata_amd.edges import TOAEdges
+    from esslivedata_amd.workflows import GpuMonitorWorkflow
+
+    kat = REF['monitor_cumulative_accumulates_window_clears']
+    e = np.array(kat['edges_ns'])
+    wf = GpuMonitorWorkflow('monitor_1', TOAEdges(start=e[0], stop=e[-1], num_bins=len(e) - 1,
+                                                  unit='ns'))
+    wf.build()
+    for (t0, t1), exp in zip(kat['cycles'], kat['expected']):
+        wf.accumulate({'monitor_1': (None, np.array(kat['toa_ns'], dtype=np.int32))},
+                      start_time=_t(t0), end_time=_t(t1))
+        out = wf.finalize()
+        assert float(out['cumulative'].values.sum()) == exp['cumulative_sum']
+        assert float(out['current'].values.sum()) == exp['current_sum']
+        for k in ('counts_total', 'counts_in_toa_range', 'counts_total_cumulative',
+                  'counts_in_toa_range_cumulative'):
+            if k in exp:
+                assert float(out[k].values) == exp[k]
+
+
 def test_detector_move_rebuilds_lut_and_resets():
     """geometry_signal.py:27-51 + accumulators.py:116-131: a new detector
     transform re-projects the moved pixels (new LUT on the device) and drops

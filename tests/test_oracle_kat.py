@@ -45,6 +45,18 @@ def test_monitor_histogram_kat():
     np.testing.assert_array_equal(h, kat['expected_hist'])
 
 
+def test_monitor_cumulative_window_kat():
+    """monitor_workflow_test.py:484-516 through the oracle's accumulator pair:
+    the cumulative keeps both cycles, the window only the last."""
+    kat = REF['monitor_cumulative_accumulates_window_clears']
+    h = ora.monitor_histogram(np.array(kat['toa_ns'], np.int32), np.array(kat['edges_ns']))
+    cum = np.zeros_like(h)
+    for exp in kat['expected']:
+        cum = cum + h
+        assert cum.sum() == exp['cumulative_sum']
+        assert h.sum() == exp['current_sum']
+
+
 def test_counts_in_range_kat():
     kat = REF['monitor_counts_in_range']
     lo, hi = ora.label_slice(np.array(kat['edges_ns']), *kat['range_ns'])
