@@ -42,6 +42,8 @@ KERNEL_SYMBOL = {
     'pixel': 'k_pix_scatter',  # PIXEL pass A's partition kernel (after k_pix_chunks and the scans)
     'monitor': 'k_monitor',  # monitor TOA histogram (--workload monitor)
     'finalize': 'k_finalize_v4',
+    'wide': 'k_wide_scatter',  # WIDE first pass (keys into page chains)
+    'wide_accumulate': 'k_wide_accumulate',  # WIDE pass B (tiles in LDS)
 }
 # engine timing buckets (include/lde.h LDE_K_*) as they are used by the SPLIT
 # strategy's SIEVE pass: 'split' = k_sieve, 'split_aux' = hot-set selection,
@@ -69,7 +71,7 @@ def parse():
                          'lookup table (diagnostic line, not the headline metric)')
     ap.add_argument('--pulses', type=int, default=14)
     ap.add_argument('--events-per-pulse', type=int, default=10_000_000)
-    ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition', 'paged', 'split', 'pixel'])
+    ap.add_argument('--strategy', default='auto', choices=['auto', 'atomic', 'partition', 'paged', 'split', 'pixel', 'wide'])
     ap.add_argument('--view', default='geometric',
                     choices=['geometric', 'mantle_front_layer', 'wire_view', 'strip_view'],
                     help='DREAM logical views (dream/specs.py:151-180) instead of the '
@@ -92,6 +94,13 @@ def parse():
                     help='events: every rank bins its own DREAM batches (event-batch sharding); '
                          "banks: LOKI's nine banks placed on the ranks by assign_banks, each rank "
                          "binning its banks' streams with no collective (pixel-range sharding)")
+    ap.add_argument('--num-bins', type=int, default=None,
+                    help='TOA bins of the detector view (EdgesModel.num_bins, 1..10000, '
+                         'parameter_models.py:87); default: the instrument\'s (100)')
+    ap.add_argument('--toa-scale', default=None, choices=['linear', 'log'],
+                    help="TOA edge scale (default: the instrument's)")
+    ap.add_argument('--toa-start', type=float, default=None,
+                    help="first TOA edge in ms (default: the instrument's; log needs > 0)")
     ap.add_argument('--bank-steps', type=int, default=5,
                     help='timed steps of the bank-sharded LOKI leg reported beside the DREAM line '
                          '(bank_sharding; 0 = skip)')
@@ -423,6 +432,10 @@ def main():
     inst = (synthetic.dream_mantle() if args.workload == 'dream' else
             synthetic.loki_bank0() if args.workload == 'loki' else
             synthetic.bifrost_unified() if bifrost else None)
+    if inst is not None and (args.num_bins or args.toa_scale or args.toa_start is not None):
+        # EdgesModel's reachable TOA configurations (parameter_models.py:82-105)
+        inst = synthetic.with_toa_edges(inst, num_bins=args.num_bins, scale=args.toa_scale,
+                                        start=args.toa_start)
     from esslivedata_amd.edges import TOAEdges
 
     if monitor:
@@ -579,7 +592,7 @@ def main():
     # in wavelength mode the coordinate pass dominates the sieve)
     names = ('atomic', 'partition', 'tile_accumulate', 'plan', 'paged', 'page_plan',
              'page_accumulate', 'split', 'split_aux', 'coord', 'pixel', 'monitor', 'binning',
-             'finalize')
+             'finalize', 'wide', 'wide_accumulate')
     eng.timing_select(None)
     eng.timing_enable(True)
     n_prof = 3
@@ -730,6 +743,7 @@ def main():
             'replicas': n_rep,
             'toa_bins': eng.n_toa_bins,
             'toa_edges': 'linear' if monitor else inst.edges.scale,
+            **({} if monitor else {'toa_range_ms': [inst.edges.start, inst.edges.stop]}),
             'events_per_step': n_step,
             'pulses_per_step': args.pulses,
             'strategy': info['last_strategy'],

@@ -36,7 +36,7 @@ LDE_ENOTSUP = -6
 LDE_F64 = 0
 LDE_F32 = 1
 
-STRATEGIES = {'auto': 0, 'atomic': 1, 'partition': 2, 'paged': 3, 'split': 4, 'pixel': 5}
+STRATEGIES = {'auto': 0, 'atomic': 1, 'partition': 2, 'paged': 3, 'split': 4, 'pixel': 5, 'wide': 6}
 
 LDE_CURRENT = 0
 LDE_CUMULATIVE = 1
@@ -48,6 +48,12 @@ COUNTERS = {
     'waits': 3,
     'waits_blocked': 4,
     'wait_pred_us': 5,
+    # 6, 7: reserved (removed sieve counters, read as 0)
+    'wide_levels': 8,
+    'wide_parts': 9,
+    'wide_tree_words': 10,
+    'wide_tree_lds': 11,
+    'wide_items': 12,
 }
 
 KERNELS = {
@@ -65,6 +71,8 @@ KERNELS = {
     'split_aux': 11,
     'coord': 12,
     'pixel': 13,
+    'wide': 14,
+    'wide_accumulate': 15,
 }
 
 # every symbol include/lde.h declares (checked by tests/test_abi.py)

@@ -192,6 +192,26 @@ struct lde_handle {
     bool pix_last_pred = false;  // the last PIXEL batch used predicted slots
     int pix_prev_grid = 0;
     std::vector<double> edges;  // the create-time edges (event unit)
+    // WIDE strategy (lde_wide.hip): any TOA edges, any S * T < 2^32 bins
+    bool wide_ok = false;
+    lde::WideToa wtoa{};
+    uint32_t *d_wtree = nullptr;
+    int wide_levels = 0, wide_pbits = 0, wide_parts = 0, wide_tpb_bits = 0, wide_tiles = 0, wide_cbits = 0;
+    std::vector<int> wide_uses;  // per replica: batches since its pixel table was built (-1: none)
+    uint32_t *d_wtab = nullptr, *d_wpixcnt = nullptr, *d_wcounters = nullptr;
+    lde::PixChunk *d_wctab = nullptr;
+    size_t wctab_cap = 0;
+    unsigned char *d_wpages1 = nullptr;
+    size_t wpages1_cap = 0;  // bytes
+    uint16_t *d_wpages2 = nullptr;
+    size_t wpages2_cap = 0;  // entries
+    uint32_t *d_wpage_cnt = nullptr, *d_wpage_part = nullptr, *d_wlist = nullptr;
+    size_t wmeta_cap = 0;  // pages (each of the three arrays)
+    uint32_t *d_wrows1 = nullptr, *d_wrows2 = nullptr;
+    size_t wrows1_cap = 0, wrows2_cap = 0;  // words
+    uint4 *d_witems1 = nullptr, *d_witems2 = nullptr;
+    size_t witems1_cap = 0, witems2_cap = 0;
+    uint2 *d_wband = nullptr;
 
     // finalize scratch
     unsigned long long *d_tot4 = nullptr;
@@ -545,6 +565,118 @@ bool build_sieve_toa(const lde::ToaParams &tp, const std::vector<unsigned char> 
     return true;
 }
 
+// WIDE TOA tree (lde_internal.h WideToa) over the integer thresholds thr[0..T]
+// of the edges.  A bucket [x, x + 2^sh) is a leaf when at most one threshold
+// lies strictly inside it; its word holds the bin at x (the largest b < T with
+// thr[b] - lo <= x) and that threshold's offset from the start of its ROOT
+// bucket, so the kernel needs no per-level width.  A bucket with two or more
+// (equal thresholds count separately) becomes 2^fb children of width
+// 2^max(0, sh - fb); a width-1 bucket never holds one inside, so the descent
+// ends.  (sh0, fb) are chosen for the fewest words (LDS first), then the
+// shallowest tree.
+struct WideTreeBuilder {
+    const std::vector<long long> &r;  // thresholds relative to lo, r[0] = 0
+    int T, sh0, fb;
+    std::vector<uint32_t> words;
+    int depth = 0;
+    bool ok = true;
+    WideTreeBuilder(const std::vector<long long> &r_, int T_, int sh0_, int fb_) : r(r_), T(T_), sh0(sh0_), fb(fb_) {}
+    // bin at x: largest b in [0, T - 1] with r[b] <= x
+    int bin_at(long long x) const {
+        const int b = (int)(std::upper_bound(r.begin(), r.begin() + T, x) - r.begin()) - 1;
+        return std::max(0, std::min(b, T - 1));
+    }
+    // thresholds r[1..T-1] strictly inside [x, x + w): indices [a, e)
+    void inside(long long x, long long w, int &a, int &e) const {
+        a = (int)(std::upper_bound(r.begin() + 1, r.begin() + T, x) - r.begin());
+        e = (int)(std::upper_bound(r.begin() + 1, r.begin() + T, x + w - 1) - r.begin());
+    }
+    // word of bucket [x, x + 2^sh) at level lv; root_x: its root bucket's start
+    uint32_t node(long long x, int sh, int lv, long long root_x) {
+        int a, e;
+        inside(x, 1LL << sh, a, e);
+        const uint32_t b0 = (uint32_t)bin_at(x);
+        if (e - a == 0) {
+            depth = std::max(depth, lv);
+            return b0 | (0xFFFFu << 16);
+        }
+        if (e - a == 1) {
+            depth = std::max(depth, lv);
+            return b0 | ((uint32_t)(r[(size_t)a] - root_x) << 16);
+        }
+        const int F = 1 << fb;
+        const size_t base = words.size();
+        if (base + (size_t)F > 0xFFFFu || lv >= 32) {
+            ok = false;
+            return 0;
+        }
+        words.resize(base + (size_t)F);
+        const int csh = std::max(0, sh - fb);
+        for (int k = 0; k < F && ok; ++k) {
+            // nodes narrower than the fan-out: child k is position (x & ~(F - 1)) + k
+            // (the kernel indexes width-1 children by the low fb bits of d)
+            const long long cx = sh >= fb ? x + ((long long)k << csh) : (x & ~(long long)(F - 1)) + k;
+            words[base + (size_t)k] = node(cx, csh, lv + 1, root_x);
+        }
+        return 0xFFFFu | ((uint32_t)base << 16);
+    }
+    bool build(long long span) {
+        const long long nroot = (span + (1LL << sh0) - 1) >> sh0;
+        if (nroot > 0xFFFF) return false;
+        words.assign((size_t)nroot, 0u);
+        for (long long g = 0; g < nroot && ok; ++g) {
+            const uint32_t w = node(g << sh0, sh0, 0, g << sh0);
+            words[(size_t)g] = w;
+        }
+        return ok;
+    }
+};
+
+bool build_wide_tree(const std::vector<double> &edges, int T, std::vector<uint32_t> &tree, lde::WideToa &wt) {
+    std::vector<long long> thr((size_t)T + 1);
+    for (int i = 0; i <= T; ++i) thr[(size_t)i] = ceil_clamped(edges[(size_t)i]);
+    const long long lo = thr[0], span = thr[(size_t)T] - thr[0];
+    std::memset(&wt, 0, sizeof wt);
+    wt.lo = (uint32_t)lo;
+    wt.fb = 2;
+    if (span <= 0) {  // no event can be in range
+        wt.empty = 1;
+        tree.assign(4, 0u);
+        wt.words = 1;
+        return true;
+    }
+    if (span > (1LL << 31)) return false;  // root buckets <= 2^15 wide, at most 65535 of them
+    wt.last = (uint32_t)(span - 1);
+    std::vector<long long> r((size_t)T + 1);
+    for (int i = 0; i <= T; ++i) r[(size_t)i] = thr[(size_t)i] - lo;
+    size_t best = ~(size_t)0;
+    int bsh = -1, bfb = 0, bdepth = 0;
+    for (int sh0 = 15; sh0 >= 0; --sh0) {
+        if (((span + (1LL << sh0) - 1) >> sh0) > 0xFFFF) break;
+        for (int fb = 2; fb <= 4; ++fb) {
+            WideTreeBuilder b(r, T, sh0, fb);
+            if (!b.build(span)) continue;
+            const size_t n = b.words.size();
+            // fewest words, LDS-sized trees first; then the shallower
+            const bool fits = n <= (size_t)lde::kWideTreeLds, bfits = best <= (size_t)lde::kWideTreeLds;
+            if (bsh < 0 || (fits && !bfits) || (fits == bfits && (n < best || (n == best && b.depth < bdepth)))) {
+                best = n;
+                bsh = sh0;
+                bfb = fb;
+                bdepth = b.depth;
+                tree = std::move(b.words);
+            }
+        }
+    }
+    if (bsh < 0) return false;
+    wt.sh0 = bsh;
+    wt.fb = bfb;
+    wt.depth = bdepth;
+    wt.words = (int)tree.size();
+    tree.resize((size_t)lde::align4(wt.words), 0u);
+    return true;
+}
+
 // ---- timing ----------------------------------------------------------------
 hipEvent_t pool_event(lde_handle *h) {
     if (!h->event_pool.empty()) {
@@ -847,8 +979,14 @@ int coord_prepass(lde_handle *h, std::vector<lde::SegDesc> &sd) {
     return LDE_OK;
 }
 
+// AUTO: the partitioned family (SPLIT, PIXEL, WIDE, PAGED; LDE_STRATEGY_PAGED
+// stands for it here) from 2^20 events on -- WIDE's cost does not grow with the
+// histogram, so a batch smaller than the histogram is no reason for ATOMIC's
+// memory-side atomics (DREAM at 10,000 bins: 1.4e8 events, 2.6e8 bins) --
+// else ATOMIC.  Without WIDE, PAGED needs half as many events as bins.
 int auto_strategy(const lde_handle *h, long long total) {
     if (h->strategy != LDE_STRATEGY_AUTO) return h->strategy;
+    if (h->wide_ok) return total >= (1 << 20) ? LDE_STRATEGY_PAGED : LDE_STRATEGY_ATOMIC;
     const long long thr = std::max<long long>(1 << 20, h->nbins / 2);
     return (h->n_tiles > 0 && total >= thr) ? LDE_STRATEGY_PAGED : LDE_STRATEGY_ATOMIC;
 }
@@ -1250,6 +1388,201 @@ int bin_pixel(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chun
     return LDE_OK;
 }
 
+// WIDE setup (lde_create; lde_set_coord_lut rebuilds the tree for integer
+// bins): the TOA tree, the partition form and the pixel table size.  Leaves
+// wide_ok false (nothing allocated) where the strategy does not apply.
+int wide_tree(lde_handle *h, const std::vector<double> &edges) {
+    std::vector<uint32_t> tree;
+    lde::WideToa wt;
+    if (!build_wide_tree(edges, h->T, tree, wt)) {
+        h->wide_ok = false;
+        return LDE_OK;
+    }
+    uint32_t *d = nullptr;
+    if (int rc = dev_alloc(h, &d, tree.size())) return rc;
+    const hipError_t e = hipMemcpy(d, tree.data(), tree.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        dev_free(d);
+        return fail(h, LDE_EHIP, "tree upload failed: %s", hipGetErrorString(e));
+    }
+    dev_free(h->d_wtree);
+    h->d_wtree = d;
+    wt.tree = d;
+    wt.lds = wt.words <= lde::kWideTreeLds ? 1 : 0;
+    h->wtoa = wt;
+    return LDE_OK;
+}
+
+int setup_wide(lde_handle *h) {
+    h->wide_ok = false;
+    if (h->monitor || env_ll("LDE_WIDE", 1) == 0) return LDE_OK;  // (diagnostics: off)
+    const unsigned long long nb = (unsigned long long)h->S * (unsigned long long)h->T;
+    if (nb == 0 || nb >= 0xFFFFFFFFULL || h->S >= (long long)0x3FFFFF || h->L < 1 || h->L >= 0x7FFFFFFFLL)
+        return LDE_OK;
+    if (int rc = wide_tree(h, h->edges)) return rc;
+    if (!h->d_wtree) return LDE_OK;
+    const long long tiles = (long long)((nb + (1ULL << lde::kWideTileBits) - 1) >> lde::kWideTileBits);
+    if (tiles <= lde::kWideMaxParts && env_ll("LDE_WIDE_LEVELS", 1) < 2) {
+        h->wide_levels = 1;
+        h->wide_pbits = lde::kWideTileBits;
+        h->wide_parts = (int)tiles;
+        h->wide_tpb_bits = 0;
+    } else {  // bands of tpb tiles (at most kWideMaxBands of them), then tiles
+        int tb = 1;  // (LDE_WIDE_LEVELS=2, diagnostics: the two-level form at any size)
+        while (((tiles + (1LL << tb) - 1) >> tb) > lde::kWideMaxBands) ++tb;
+        h->wide_levels = 2;
+        h->wide_tpb_bits = tb;
+        h->wide_pbits = lde::kWideTileBits + tb;
+        h->wide_parts = (int)((nb + (1ULL << h->wide_pbits) - 1) >> h->wide_pbits);
+    }
+    h->wide_tiles = (int)tiles;
+    // pixel table: 2^13 slots (the whole LUT when it fits in half of that),
+    // tags of 9 bits; smaller when the first pass's LDS needs the room
+    auto bits = [](long long n) { int b = 0; while ((1LL << b) < n) ++b; return b; };
+    int cb = (int)std::max<long long>(0, std::min<long long>(14, env_ll("LDE_WIDE_CACHE_BITS", 13)));
+    if (cb > 0 && (1LL << cb) >= 2 * h->L) cb = bits(h->L);
+    while (cb > 0 && ((h->L - 1) >> cb) > 511) ++cb;
+    if (cb > 16) cb = 0;
+    lde::WideArgs a{};
+    a.n_parts = h->wide_parts;
+    a.toa = h->wtoa;
+    auto fits = [&](int c) {
+        a.cbits = c;
+        return lde::wide_scatter_smem(a) <= 160 * 1024;
+    };
+    while (cb > 8 && !fits(cb)) --cb;
+    if (!fits(cb)) {  // the tree from global memory instead
+        h->wtoa.lds = 0;
+        a.toa = h->wtoa;
+    }
+    if (!fits(cb)) cb = 0;
+    if (!fits(cb)) return LDE_OK;
+    h->wide_cbits = cb;
+    if (cb > 0) {
+        if (int rc = dev_alloc(h, &h->d_wtab, (size_t)h->R << cb)) return rc;
+        if (int rc = dev_alloc(h, &h->d_wpixcnt, (size_t)h->L)) return rc;
+    }
+    if (int rc = dev_alloc(h, &h->d_wcounters, 4)) return rc;
+    if (!h->d_overflow) {
+        if (int rc = dev_alloc(h, &h->d_overflow, 1)) return rc;
+        HIPCALL(h, hipMemset(h->d_overflow, 0, 4));
+    }
+    if (int rc = dev_alloc(h, &h->d_wband, (size_t)lde::kWideMaxParts)) return rc;
+    h->wide_uses.assign((size_t)h->R, -1);
+    h->wide_ok = true;
+    if (env_ll("LDE_VERBOSE", 0))
+        fprintf(stderr, "lde wide: %lld tiles, %d level(s), %d partitions of 2^%d bins, TOA tree %d words "
+                        "(root 2^%d, fan-out %d, depth %d, %s), pixel table 2^%d, %zu B LDS\n",
+                tiles, h->wide_levels, h->wide_parts, h->wide_pbits, h->wtoa.words, h->wtoa.sh0, 1 << h->wtoa.fb,
+                h->wtoa.depth, h->wtoa.lds ? "LDS" : "global", cb, lde::wide_scatter_smem(a));
+    return LDE_OK;
+}
+
+// WIDE: key, partition into pages, (second level), tile pass B
+int bin_wide(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks, long long total, int replica) {
+    if (int rc = upload_segments(h, sd)) return rc;
+    const int P = h->wide_parts;
+    const long long units = (chunks + 1) / 2;
+    const int grid1 = (int)std::min<long long>(units, std::min<long long>(h->cus, lde::kWideMaxRows));
+    const long long upb = (units + grid1 - 1) / grid1;
+    const uint32_t cap1 = (uint32_t)((upb * lde::kWideUnit + lde::kWidePage - 1) / lde::kWidePage + P + 1);
+    const size_t pages1 = (size_t)grid1 * cap1;
+    const size_t esz1 = h->wide_levels == 1 ? 2 : 4;
+    // work items: pass B about one per tile (a tile past item_max entries,
+    // a hot one, is split over several, added with atomics); the second pass
+    // ~2 per CU
+    const long long item_max1 = h->wide_levels == 1
+                                    ? std::max<long long>(65536, (total + h->cus - 1) / h->cus)
+                                    : std::max<long long>(65536, (total + 2LL * h->cus - 1) / (2LL * h->cus));
+    const long long item_max2 = std::max<long long>(65536, (total + h->cus - 1) / h->cus);
+    const long long max_items1 = P + total / item_max1 + 2;
+    const long long max_items2 = h->wide_levels == 2 ? h->wide_tiles + total / item_max2 + 2 : 0;
+    const int tpb = 1 << h->wide_tpb_bits;
+    const size_t pool2 = h->wide_levels == 2 ? (size_t)(total / lde::kWidePage) + (size_t)max_items1 * (tpb + 2) + 1 : 0;
+    if (pages1 + pool2 >= 0xFFFFFFF0ULL || total >= 0xFFFFFFFFLL)
+        return fail(h, LDE_EINVAL, "batch too large for the WIDE page pools");
+    if (int rc = grow(h, &h->d_wctab, h->wctab_cap, (size_t)chunks)) return rc;
+    if (int rc = grow(h, &h->d_wpages1, h->wpages1_cap, pages1 * lde::kWidePage * esz1)) return rc;
+    if (pool2)
+        if (int rc = grow(h, &h->d_wpages2, h->wpages2_cap, pool2 * lde::kWidePage)) return rc;
+    size_t mc = h->wmeta_cap;
+    if (pages1 + pool2 > mc || !h->d_wpage_cnt) {
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        const size_t n = std::max(pages1 + pool2, mc * 2);
+        dev_free(h->d_wpage_cnt);
+        dev_free(h->d_wpage_part);
+        dev_free(h->d_wlist);
+        h->wmeta_cap = 0;
+        if (int rc = dev_alloc(h, &h->d_wpage_cnt, n)) return rc;
+        if (int rc = dev_alloc(h, &h->d_wpage_part, n)) return rc;
+        if (int rc = dev_alloc(h, &h->d_wlist, n)) return rc;
+        h->wmeta_cap = n;
+    }
+    if (int rc = grow(h, &h->d_wrows1, h->wrows1_cap, (size_t)grid1 * ((size_t)3 * P + 1))) return rc;
+    if (int rc = grow(h, &h->d_witems1, h->witems1_cap, (size_t)max_items1)) return rc;
+    if (h->wide_levels == 2) {
+        if (int rc = grow(h, &h->d_wrows2, h->wrows2_cap, (size_t)max_items1 * ((size_t)3 * tpb + 1))) return rc;
+        if (int rc = grow(h, &h->d_witems2, h->witems2_cap, (size_t)max_items2)) return rc;
+    }
+    lde::WideArgs a{};
+    a.ctab = h->d_wctab;
+    a.segs = h->d_segs;
+    a.n_segs = (int)sd.size();
+    a.n_chunks = chunks;
+    a.pid_off = h->pid_off;
+    a.L = (unsigned)h->L;
+    a.lut = (const unsigned char *)h->d_lut + (size_t)replica * h->L * (h->lut16 ? 2 : 4);
+    a.lut16 = h->lut16 ? 1 : 0;
+    a.T = h->T;
+    a.cbits = h->wide_cbits;
+    a.pix_tab = h->wide_cbits ? h->d_wtab + ((size_t)replica << h->wide_cbits) : nullptr;
+    a.toa = h->wtoa;
+    a.levels = h->wide_levels;
+    a.pbits = h->wide_pbits;
+    a.n_parts = P;
+    a.tpb_bits = h->wide_tpb_bits;
+    a.n_tiles = h->wide_tiles;
+    a.pages1 = h->d_wpages1;
+    a.pages2 = h->d_wpages2;
+    a.page_cnt = h->d_wpage_cnt;
+    a.page_part = h->d_wpage_part;
+    a.list = h->d_wlist;
+    a.cap1 = cap1;
+    a.rows1 = {h->d_wrows1, h->d_wrows1 + (size_t)grid1 * P, h->d_wrows1 + (size_t)2 * grid1 * P,
+               h->d_wrows1 + (size_t)3 * grid1 * P, P};
+    if (h->wide_levels == 2)
+        a.rows2 = {h->d_wrows2, h->d_wrows2 + (size_t)max_items1 * tpb, h->d_wrows2 + (size_t)2 * max_items1 * tpb,
+                   h->d_wrows2 + (size_t)3 * max_items1 * tpb, tpb};
+    a.pool2_next = h->d_wcounters + 2;
+    a.pool2_cap = (uint32_t)pool2;
+    a.page0_2 = (uint32_t)pages1;
+    a.items1 = h->d_witems1;
+    a.items2 = h->d_witems2;
+    a.counters = h->d_wcounters;
+    a.overflow = h->d_overflow;
+    a.max_items1 = (uint32_t)max_items1;
+    a.max_items2 = (uint32_t)max_items2;
+    a.band_items = h->d_wband;
+    a.item_max1 = (uint32_t)std::min<long long>(item_max1, 0x7FFFFFFF);
+    a.item_max2 = (uint32_t)std::min<long long>(item_max2, 0x7FFFFFFF);
+    a.hist = h->d_win32;
+    a.n_bins = h->nbins;
+    a.grid1 = grid1;
+    HIPCALL(h, lde::launch_wide_chunks(a, h->stream));
+    int &uses = h->wide_uses[(size_t)replica];
+    if (h->wide_cbits && (uses < 0 || uses >= h->hot_refresh)) {
+        Timed tm(h, LDE_K_SPLIT_AUX);
+        HIPCALL(h, lde::launch_wide_table(a, a.lut, h->d_wpixcnt, const_cast<uint32_t *>(a.pix_tab), h->stream));
+        uses = 0;
+    }
+    ++uses;
+    Stamp sa(h, LDE_K_WIDE);
+    Stamp sb(h, LDE_K_WIDE_ACC);
+    HIPCALL(h, lde::launch_wide(a, h->stream, sa.a, sa.b, sb.a, sb.b));
+    sa.done = sb.done = true;
+    return LDE_OK;
+}
+
 int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int replica,
                  bool coord_deferred) {
     const size_t lut_es = h->lut16 ? 2 : 4;
@@ -1295,17 +1628,22 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
     }
     int strat = auto_strategy(h, total);
     const bool auto_split = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && h->split_ok;
-    if (strat == LDE_STRATEGY_SPLIT && !h->split_ok) strat = LDE_STRATEGY_PAGED;
+    // AUTO without SPLIT or PIXEL: WIDE (any edges, any histogram size)
+    // before PAGED; a forced strategy that cannot run takes WIDE too
+    const bool auto_wide = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && h->wide_ok;
+    if (strat == LDE_STRATEGY_WIDE && !h->wide_ok) strat = LDE_STRATEGY_PAGED;
+    if (strat == LDE_STRATEGY_SPLIT && !h->split_ok) strat = h->wide_ok ? LDE_STRATEGY_WIDE : LDE_STRATEGY_PAGED;
     // PIXEL's payload offsets are u32: batches whose payload (events + pads)
     // could reach 2^31 take PAGED
     const long long max_chunks = total / lde::kChunk + (long long)segs.size() + 1;
     const bool pixel_ok = h->pixel_ok && total + 3LL * (max_chunks / h->pix_unit + 1) * h->pix.nr < 0x7FFFFFF0LL;
-    if (strat == LDE_STRATEGY_PIXEL && !pixel_ok) strat = LDE_STRATEGY_PAGED;
+    if (strat == LDE_STRATEGY_PIXEL && !pixel_ok) strat = h->wide_ok ? LDE_STRATEGY_WIDE : LDE_STRATEGY_PAGED;
     // AUTO without skew: PIXEL (no LUT gather) where the footprints fit
     const bool auto_pixel = h->strategy == LDE_STRATEGY_AUTO && strat == LDE_STRATEGY_PAGED && pixel_ok;
     if (auto_pixel && !auto_split) strat = LDE_STRATEGY_PIXEL;
+    else if (auto_wide && !auto_split) strat = LDE_STRATEGY_WIDE;
     if ((strat == LDE_STRATEGY_PARTITION || strat == LDE_STRATEGY_PAGED) && h->n_tiles == 0)
-        strat = LDE_STRATEGY_ATOMIC;
+        strat = h->wide_ok ? LDE_STRATEGY_WIDE : LDE_STRATEGY_ATOMIC;
     if (coord_deferred && !coord_keyed_candidate(h, total)) {
         // this piece does not take the keyed path: the plain coordinate pass
         if (int rc = coord_prepass(h, segs)) return rc;
@@ -1410,11 +1748,16 @@ int bin_segments(lde_handle *h, std::vector<Segment> segs, long long total, int 
             h->last_strategy = LDE_STRATEGY_PIXEL;
             return bin_pixel(h, sd, chunks, total, replica);
         }
+        if (h->wide_ok) {
+            h->last_strategy = LDE_STRATEGY_WIDE;
+            return bin_wide(h, sd, chunks, total, replica);
+        }
         // (bin_split uploads the descriptors lazily: this batch's may not be)
         h->last_strategy = LDE_STRATEGY_PAGED;
         return bin_paged(h, sd, chunks, total, lut);
     }
     if (strat == LDE_STRATEGY_PIXEL) return bin_pixel(h, sd, chunks, total, replica);
+    if (strat == LDE_STRATEGY_WIDE) return bin_wide(h, sd, chunks, total, replica);
     if (strat == LDE_STRATEGY_PAGED) return bin_paged(h, sd, chunks, total, lut);
     long long item_events = h->item_events_override > 0
                                 ? h->item_events_override
@@ -1717,7 +2060,11 @@ void release(lde_handle *h) {
                     (void *)h->d_cold_items, (void *)h->d_cold_ttot, (void *)h->d_row_screen,
                     (void *)h->d_sel_stats, (void *)h->d_sample_part, (void *)h->d_screen_cnt,
                     (void *)h->d_screen_row, (void *)h->d_hot_part, (void *)h->d_cold, (void *)h->d_cold_cnt,
-                    (void *)h->d_hot_fmt, (void *)h->d_tot4, (void *)h->d_snap})
+                    (void *)h->d_hot_fmt, (void *)h->d_tot4, (void *)h->d_snap, (void *)h->d_wtree,
+                    (void *)h->d_wtab, (void *)h->d_wpixcnt, (void *)h->d_wcounters, (void *)h->d_wctab,
+                    (void *)h->d_wpages1, (void *)h->d_wpages2, (void *)h->d_wpage_cnt, (void *)h->d_wpage_part,
+                    (void *)h->d_wlist, (void *)h->d_wrows1, (void *)h->d_wrows2, (void *)h->d_witems1,
+                    (void *)h->d_witems2, (void *)h->d_wband})
         if (p) (void)hipFree(p);
     for (void *p : {(void *)h->h_ppid, (void *)h->h_ptoa, (void *)h->h_segs, (void *)h->h_sel_stats,
                     (void *)h->h_pack})
@@ -1905,7 +2252,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     if (!monitor) {
         h->lut16 = h->S < 0xFFFF && env_ll("LDE_LUT32", 0) == 0;
         CREATE_CHECK(upload_lut(h, cfg->out_lut));
-        if (cfg->strategy < LDE_STRATEGY_AUTO || cfg->strategy > LDE_STRATEGY_PIXEL)
+        if (cfg->strategy < LDE_STRATEGY_AUTO || cfg->strategy > LDE_STRATEGY_WIDE)
             CREATE_CHECK(fail(h, LDE_EINVAL, "unknown strategy %d", cfg->strategy));
     }
     CREATE_CHECK(dev_alloc(h, &h->d_tab, tab.size()));
@@ -2043,6 +2390,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         h->item_events_override = env_ll("LDE_ITEM_EVENTS", 0);
     }
     if (!monitor) CREATE_CHECK(build_pixel(h, cfg->out_lut));
+    if (!monitor) CREATE_CHECK(setup_wide(h));
     CREATE_HIP(hipEventCreateWithFlags(&h->pin_done, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&h->segs_done, hipEventDisableTiming));
     CREATE_HIP(hipStreamSynchronize(h->stream));
@@ -2685,11 +3033,13 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     struct Staged {
         unsigned char *tab = nullptr;
         uint32_t *ttab = nullptr;
+        uint32_t *wtree = nullptr;
         double *cpd = nullptr, *ctable = nullptr, *cedges = nullptr;
         uint16_t *cbuck = nullptr;
         ~Staged() {  // whatever was not committed
             dev_free(tab);
             dev_free(ttab);
+            dev_free(wtree);
             dev_free(cpd);
             dev_free(ctable);
             dev_free(cedges);
@@ -2701,12 +3051,25 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     int tsh = 0;
     uint32_t tcap = 0;
     bool sieve_fits = h->split_ok;
+    lde::WideToa wt = h->wtoa;
+    bool wide_fits = h->wide_ok;
     if (!rebind) {
         // the binning stage now sees integer bins: edges 0..T
         std::vector<double> idx((size_t)T + 1);
         for (int i = 0; i <= T; ++i) idx[(size_t)i] = (double)i;
         std::vector<unsigned char> tab;
         if (int rc = build_toa_tables(h, idx.data(), T, tab, tp)) return rc;
+        if (h->wide_ok) {  // WIDE's TOA tree over the integer edges
+            std::vector<uint32_t> tree;
+            wide_fits = build_wide_tree(idx, T, tree, wt);
+            if (wide_fits) {
+                if (int rc = dev_alloc(h, &st.wtree, tree.size())) return rc;
+                HIPCALL(h, hipMemcpy(st.wtree, tree.data(), tree.size() * 4, hipMemcpyHostToDevice));
+                wt.tree = st.wtree;
+                // (integer edges: a flat tree, never larger than the create-time one)
+                wt.lds = h->wtoa.lds && wt.words <= h->wtoa.words ? 1 : 0;
+            }
+        }
         if (int rc = dev_alloc(h, &st.tab, tab.size())) return rc;
         HIPCALL(h, hipMemcpy(st.tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
         if (h->split_ok) {
@@ -2765,6 +3128,12 @@ int lde_set_coord_lut(lde_handle *h, const lde_coord_lut *lut) {
     if (!rebind) {
         std::swap(h->d_tab, st.tab);
         h->tp = tp;
+        if (h->wide_ok && wide_fits) {
+            std::swap(h->d_wtree, st.wtree);
+            h->wtoa = wt;
+        } else {
+            h->wide_ok = false;
+        }
         if (h->split_ok && sieve_fits) {
             std::swap(h->d_ttab, st.ttab);
             h->ttab = std::move(tt);
@@ -2829,6 +3198,7 @@ int lde_set_lut(lde_handle *h, const int32_t *out_lut) {
     }
     // every replica's hot set / SIEVE tables derive from the LUT: rebuild lazily
     for (auto &u : h->hot_uses) u = -1;
+    for (auto &u : h->wide_uses) u = -1;  // and the WIDE pixel tables
     commit_pixel(h, st);
     return LDE_OK;
 }
@@ -2906,6 +3276,31 @@ int lde_counter(lde_handle *h, int32_t id, int64_t *value) {
     case LDE_C_WAIT_PRED_US:
         *value = (int64_t)h->wait_pred_us;
         return LDE_OK;
+    case 6:  // reserved (removed sieve pair counters)
+    case 7:
+        *value = 0;
+        return LDE_OK;
+    case LDE_C_WIDE_LEVELS:
+        *value = h->wide_ok ? h->wide_levels : 0;
+        return LDE_OK;
+    case LDE_C_WIDE_PARTS:
+        *value = h->wide_ok ? h->wide_parts : 0;
+        return LDE_OK;
+    case LDE_C_WIDE_TREE_WORDS:
+        *value = h->wide_ok ? h->wtoa.words : 0;
+        return LDE_OK;
+    case LDE_C_WIDE_TREE_LDS:
+        *value = h->wide_ok ? h->wtoa.lds : 0;
+        return LDE_OK;
+    case LDE_C_WIDE_ITEMS: {
+        *value = 0;
+        if (!h->d_wcounters) return LDE_OK;
+        uint32_t c[2] = {0, 0};
+        HIPCALL(h, hipStreamSynchronize(h->stream));
+        HIPCALL(h, hipMemcpy(c, h->d_wcounters, 8, hipMemcpyDeviceToHost));
+        *value = h->wide_levels == 2 ? c[1] : c[0];
+        return LDE_OK;
+    }
     default:
         return fail(h, LDE_EINVAL, "unknown counter id %d", id);
     }

@@ -434,6 +434,105 @@ hipError_t launch_pixel(const PixArgs &a, const PixSetup &s, int replica, uint32
                         int max_items, uint4 *items, uint32_t *item_count, uint32_t *hist,
                         hipStream_t st, int phase, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
+// WIDE strategy (lde_wide.hip): any TOA edges, any S * T up to 2^32 bins.
+// Events are keyed (screen * T + bin) by a front end with an LDS table of
+// the most frequent pixels (misses gather the LUT) and an LDS bucket tree
+// over the TOA range, then partitioned into page chains by tile of 2^15 bins
+// (one level, <= kWideMaxParts tiles) or by band of tiles first (two levels),
+// and every tile is histogrammed in LDS.  Each partitioning pass writes, per
+// row (its block or work item) and partition, the pages / events / offset of
+// the partition's pages in the row's sorted page list; a plan pass turns those
+// into work items (partition, row range) for the next pass.
+constexpr int kWideThreads = 1024;        // partition passes: one block per CU
+constexpr int kWideEPT = 16;              // entries per thread per unit
+constexpr int kWideUnit = kWideThreads * kWideEPT;  // 16,384 entries (two chunks)
+constexpr int kWidePageBits = 10;
+constexpr int kWidePage = 1 << kWidePageBits;       // entries per page
+constexpr int kWideTileBits = 15;         // pass-B tile: 2^15 u32 counters (128 KB LDS)
+constexpr int kWideMaxParts = 1024;       // partitions of one pass (one owner thread each)
+constexpr int kWideMaxBands = 512;        // first-level bands of the two-level form
+constexpr int kWideMaxRows = 1024;        // rows per work item
+constexpr int kWideTreeLds = 6144;        // TOA tree words kept in LDS (larger trees: global)
+constexpr int kWideLdsChunks = 128;
+constexpr int kWideSample = 64;           // chunks sampled per pixel-table selection
+
+// TOA lookup tree over d = t - lo in [0, last]: root buckets of 2^sh0, each
+// word either a leaf (bits 0..15 bin at the bucket start, bits 16..31 offset
+// of the only threshold inside it, 0xFFFF none; leaf width <= 2^15) or an
+// internal node (bits 0..15 = 0xFFFF, bits 16..31 first word of its 2^fb
+// children of width / 2^fb).  Exact for any sorted edges: a bucket holding two
+// or more thresholds (or equal thresholds) is split until it holds at most one.
+struct WideToa {
+    uint32_t lo;     // ceil(edge[0]) as u32 (d = (u32)t - lo)
+    uint32_t last;   // span - 1; valid d <= last
+    int empty;       // span == 0: no event is in range
+    int sh0, fb;     // root bucket width 2^sh0, fan-out 2^fb
+    int words;       // tree words
+    int lds;         // 1: the tree fits kWideTreeLds words (copied into LDS)
+    int depth;       // deepest leaf below the root
+    const uint32_t *tree;  // device copy
+};
+
+struct WideRows {  // per-row output of a partitioning pass
+    uint32_t *cnt;   // [row][ncols] pages of each partition
+    uint32_t *ev;    // [row][ncols] entries
+    uint32_t *off;   // [row][ncols] first index of the partition in the row's page list
+    uint32_t *pool;  // [row] first page of the row's pool
+    int ncols;
+};
+
+struct WideArgs {
+    // batch
+    const PixChunk *ctab;        // [n_chunks] (k_wide_chunks)
+    const SegDesc *segs;
+    int n_segs;
+    long long n_chunks;
+    int pid_off;
+    unsigned L;
+    const void *lut;             // this replica's LUT (u16 screen or i32 screen * T)
+    int lut16;
+    int T;
+    const uint32_t *pix_tab;     // this replica's pixel table image (1 << cbits words)
+    int cbits;
+    WideToa toa;
+    // first pass
+    int levels;                  // 1: parts are tiles; 2: parts are bands of tpb tiles
+    int pbits;                   // part = key >> pbits (15, or the band bits)
+    int n_parts;
+    int tpb_bits;                // two levels: tiles per band = 1 << tpb_bits
+    int n_tiles;
+    void *pages1;                // first-pass pages (u16 tile-local, or u32 band-local entries)
+    void *pages2;                // second-pass pages (u16 tile-local)
+    uint32_t *page_cnt, *page_part;  // per page (both passes share the numbering)
+    uint32_t *list;              // sorted page lists, at each row's pool
+    uint32_t cap1;               // pages per first-pass block pool
+    WideRows rows1, rows2;
+    uint32_t *pool2_next;        // second-pass page allocator
+    uint32_t pool2_cap;
+    uint32_t page0_2;            // first second-pass page (= grid1 * cap1; pages2 holds pages from here)
+    uint4 *items1, *items2;      // plans: {part, row begin, row end, flags}
+    uint32_t *counters;          // [0] items1, [1] items2 (zeroed by k_wide_chunks)
+    uint32_t *overflow;          // pool / plan overflow flag (internal error, reported by finalize)
+    uint32_t max_items1, max_items2;
+    uint2 *band_items;           // [band] the second pass's rows of the band
+    uint32_t item_max1, item_max2;
+    uint32_t *hist;              // the window
+    long long n_bins;
+    int grid1;                   // first-pass blocks
+};
+
+// the batch's chunk table; call before launch_wide_table / launch_wide
+hipError_t launch_wide_chunks(const WideArgs &a, hipStream_t st);
+// pixel-table selection for one replica: sample the batch, pick the most
+// frequent pixel of every slot (pix_cnt zeroed here)
+hipError_t launch_wide_table(const WideArgs &a, const void *lut_rep, uint32_t *pix_cnt, uint32_t *tab,
+                             hipStream_t st);
+// first pass + plan (+ second pass + plan) + pass B; start/stop stamp the
+// first pass, bstop the end of pass B (optional)
+hipError_t launch_wide(const WideArgs &a, hipStream_t st, hipEvent_t start = nullptr,
+                       hipEvent_t stop = nullptr, hipEvent_t bstart = nullptr, hipEvent_t bstop = nullptr);
+size_t wide_scatter_smem(const WideArgs &a);
+
 hipError_t launch_rebin_f64(const double *se, const double *sv, long long ns, const double *de,
                             long long nd, double *out_a, double *out_b, hipStream_t st);
 

@@ -1,0 +1,803 @@
+// lde_wide.hip -- WIDE strategy: large and arbitrary TOA binnings.
+//
+// The reference's EdgesModel allows 1..10,000 TOA bins, linear or log, from
+// any start (SRC/parameter_models.py:82-105, 290-295; the detector view's
+// edges, SRC/workflows/detector_view_specs.py:73-124), so a DREAM-sized view
+// (25,600 screens) reaches 2.56e8 (screen, bin) counters.  SIEVE and PIXEL
+// keep rows or footprints of the histogram in LDS and stop scaling at a few
+// hundred bins; WIDE instead keys every event and sorts the keys into tiles
+// of 2^15 bins through page chains, so its cost per event does not depend on
+// T or on the edges:
+//
+//   k_wide_chunks     the batch's chunk table; zeroes the pass counters
+//   k_wide_scatter    first pass, one 1024-thread block per CU.  Per unit of
+//                     16,384 events: pixel word from an LDS table of the
+//                     sampled most frequent pixels (misses gather the LUT
+//                     with a raw buffer load; hits load out of range, which
+//                     issues no request), TOA bin from an LDS bucket tree
+//                     (WideToa), key = screen * T + bin; rank by partition
+//                     (LDS atomics), block scan, page allocation from the
+//                     block's pool (owner thread per partition), key-sorted
+//                     LDS staging, and every run appended to its partition's
+//                     open page with per-lane stores (a run's lanes write
+//                     consecutive entries of one page).  At its end the
+//                     block sorts its pages by partition into its page list
+//                     and writes, per partition, pages / entries / list
+//                     offset (WideRows).
+//   k_wide_plan       per partition: work items (partition, range of rows)
+//                     of at most ~item_max entries
+//   k_wide_split      two-level form only (more than kWideMaxParts tiles):
+//                     per item of a band, its u32 band-local keys partitioned
+//                     by tile exactly as the first pass does
+//   k_wide_accumulate per item of a tile: its pages histogrammed in a 128 KB
+//                     LDS tile, then added to the window (a plain 16-byte
+//                     read-modify-write when the tile has one item, global
+//                     atomics when hot tiles are split over several)
+//
+// Counts are integers and every event is added exactly once whatever the
+// table holds or how the work is split, so the histogram is bit-identical to
+// the other strategies and to the oracle.
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "lde_device.h"
+#include "lde_internal.h"
+
+namespace lde {
+
+namespace {
+
+constexpr int NT = kWideThreads;
+constexpr int EPT = kWideEPT;
+constexpr int UNIT = kWideUnit;
+constexpr int PAGE = kWidePage;
+constexpr int PB = kWidePageBits;
+constexpr int CT = kChunk / EPT;  // threads per chunk of a unit (512)
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kOOB = 0x80000000u;         // buffer offset past every num_records
+constexpr uint32_t kRsrcWord3 = 0x00020000u;   // gfx9 raw buffer, 32-bit data format
+constexpr uint32_t kTabValid = 0x80000000u;    // pixel table word: valid | tag << 22 | screen
+constexpr int kTagShift = 22;
+constexpr uint32_t kTabValue = (1u << kTagShift) - 1u;  // (the value kTabValue: a dropped pixel)
+constexpr uint32_t kTagMask = 0x1FFu;
+constexpr uint32_t kLeafNone = 0xFFFFu;        // leaf: no threshold inside / internal-node marker
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, (int)kRsrcWord3);
+}
+
+template <bool TL>
+__device__ __forceinline__ uint32_t tree_word(const uint32_t *tree, uint32_t i) {
+    if (TL) return tree[i];  // LDS
+    return ld_global_u32(tree + i);
+}
+
+// TOA bins of N events t[o..o+N) (kNone: outside the edges).  All root
+// words are read first; the descent is one wave-uniform round per tree level
+// that still holds an internal node in some lane (none for most edge sets).
+template <bool TL, int N, int O>
+__device__ __forceinline__ void toa_bins(const WideToa &tp, const uint32_t *tree, const int (&t)[EPT],
+                                         uint32_t (&bin)[N]) {
+    uint32_t dc[N], w[N];
+    const uint32_t rmask = (1u << tp.sh0) - 1u;
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+        const uint32_t d = (uint32_t)t[O + e] - tp.lo;
+        const bool ok = d <= tp.last && !tp.empty;
+        dc[e] = ok ? d : 0u;
+        bin[e] = ok ? 0u : kNone;
+        w[e] = tree_word<TL>(tree, dc[e] >> tp.sh0);
+    }
+    const uint32_t fmask = (1u << tp.fb) - 1u;
+    for (int lv = 1; lv <= tp.depth; ++lv) {
+        bool any = false;
+#pragma unroll
+        for (int e = 0; e < N; ++e) any |= (w[e] & 0xFFFFu) == kLeafNone;
+        if (!__builtin_amdgcn_ballot_w64(any)) break;
+        const int sh = max(0, tp.sh0 - lv * tp.fb);  // (nodes narrower than the fan-out: width-1 children)
+#pragma unroll
+        for (int e = 0; e < N; ++e)
+            if ((w[e] & 0xFFFFu) == kLeafNone) w[e] = tree_word<TL>(tree, (w[e] >> 16) + ((dc[e] >> sh) & fmask));
+    }
+    // leaf: bin at its start + (the offset inside the ROOT bucket reached the
+    // one threshold inside the leaf)
+#pragma unroll
+    for (int e = 0; e < N; ++e)
+        bin[e] = bin[e] == kNone ? kNone : (w[e] & 0xFFFFu) + ((dc[e] & rmask) >= (w[e] >> 16) ? 1u : 0u);
+}
+
+// events of unit u: chunks 2u, 2u + 1; thread tid takes chunk 2u + tid / CT
+// (wave-uniform) as thread tid % CT of it.  Chunk pointers from the block's
+// LDS copy of the chunk table (s_ct, chunks from c0 on) or the global table.
+__device__ __forceinline__ void unit_load(const WideArgs &a, const PixChunk *s_ct, long long c0, long long u,
+                                          int (&p)[EPT], int (&t)[EPT]) {
+    const int tid = threadIdx.x;
+    const long long c = u * 2 + __builtin_amdgcn_readfirstlane(tid / CT);
+    const int tl = tid % CT;
+    if (c >= a.n_chunks) {
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+            p[e] = a.pid_off - 1;  // outside the LUT: dropped
+            t[e] = 0;
+        }
+        return;
+    }
+    const PixChunk ch = s_ct ? s_ct[c - c0] : a.ctab[c];
+    if (ch.n == kChunk) {  // full and 16-byte aligned
+#pragma unroll
+        for (int j = 0; j < EPT / 4; ++j) {
+            const int off = (j * CT + tl) * 4;
+            const v4i pv = ld_stream4(ch.pid + off);
+            const v4i tv = ld_stream4(ch.toa + off);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                p[j * 4 + q] = pv[q];
+                t[j * 4 + q] = tv[q];
+            }
+        }
+        return;
+    }
+    const int rem = ch.n < 0 ? -ch.n : ch.n;  // < 0: full but misaligned
+#pragma unroll
+    for (int j = 0; j < EPT / 4; ++j) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int off = (j * CT + tl) * 4 + q;
+            const bool ok = off < rem;
+            p[j * 4 + q] = ok ? ld_global(ch.pid + off) : a.pid_off - 1;
+            t[j * 4 + q] = ok ? ld_global(ch.toa + off) : 0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The partitioning step shared by both passes.  LDS (words): staging
+// [UNIT] | counts x 2 (unit parity) [P4 + 64 lane dummies] | staging offset
+// and write fill per partition [P4] (offset | fill << 16) | page of the run's
+// first entries [P4] | first new page [P4] | scan scratch [32] | pool [4].
+// Thread p < P owns partition p: its open page and fill, and the row's page
+// and entry counts, live in that thread's registers.
+// ---------------------------------------------------------------------------
+struct PartLds {
+    uint32_t *stg, *cnt0, *cnt1, *offw, *wcur, *newp, *w, *pool;
+};
+
+__device__ __forceinline__ size_t part_words(int P) {
+    const size_t P4 = (size_t)align4(P);
+    return (size_t)UNIT + 2 * (P4 + 64) + 3 * P4 + 32 + 4;
+}
+
+__device__ __forceinline__ PartLds part_lds(uint32_t *sm, int P) {
+    const uint32_t P4 = (uint32_t)align4(P);
+    PartLds s;
+    s.stg = sm;
+    s.cnt0 = s.stg + UNIT;
+    s.cnt1 = s.cnt0 + P4 + 64;
+    s.offw = s.cnt1 + P4 + 64;
+    s.wcur = s.offw + P4;
+    s.newp = s.wcur + P4;
+    s.w = s.newp + P4;
+    s.pool = s.w + 32;
+    return s;
+}
+
+struct Owner {  // registers of the owner thread of one partition
+    uint32_t cur = kNone, fill = (uint32_t)PAGE, np = 0, ev = 0;
+};
+
+// One unit: keys (kNone = no entry) are ranked per partition (part = key >>
+// pbits) with returning LDS atomics, staged sorted by partition and appended
+// to the partitions' pages (entries: key & emask, as u16 or u32).
+// `next()` runs right after the rank atomics (the next unit's loads).
+template <bool E16, typename NEXT>
+__device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, uint32_t emask, int parity,
+                                          const uint32_t (&key)[EPT], Owner &own, uint32_t pool_base,
+                                          uint32_t cap, void *pages, uint32_t page0, uint32_t *__restrict__ page_cnt,
+                                          uint32_t *__restrict__ page_part, uint32_t *overflow, NEXT next) {
+    const int tid = threadIdx.x;
+    const uint32_t P4 = (uint32_t)align4(P);
+    uint32_t *cnt = parity ? s.cnt1 : s.cnt0;
+    uint32_t *cnt_next = parity ? s.cnt0 : s.cnt1;
+    const uint32_t dummy = P4 + (uint32_t)(tid & 63);
+    uint32_t rank[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+        rank[e] = __hip_atomic_fetch_add(cnt + (key[e] != kNone ? key[e] >> pbits : dummy), 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    next();
+    __syncthreads();
+    uint32_t n = 0;
+    if (tid < P) {
+        n = cnt[tid];
+        cnt_next[tid] = 0;
+    }
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan(n, s.w, &total);
+    if (tid < P && n > 0) {
+        // the run occupies positions [fill, fill + n) of the partition's
+        // chain: < PAGE in the open page, the rest in n_new new pages
+        const uint32_t room = (uint32_t)PAGE - own.fill;
+        uint32_t first = kNone;
+        if (n > room) {
+            const uint32_t n_new = (n - room + PAGE - 1) >> PB;
+            const uint32_t o = __hip_atomic_fetch_add(s.pool, n_new, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (o + n_new <= cap) {
+                first = pool_base + o;
+                if (own.cur != kNone) page_cnt[own.cur] = PAGE;
+                for (uint32_t k = 0; k < n_new; ++k) {
+                    page_part[first + k] = (uint32_t)tid;
+                    page_cnt[first + k] = PAGE;
+                }
+                own.np += n_new;
+            } else {
+                *overflow = 1u;  // cannot happen with the host's pool size
+            }
+        }
+        s.offw[tid] = off | (own.fill << 16);
+        s.wcur[tid] = own.cur;
+        s.newp[tid] = first;
+        const uint32_t end = own.fill + n;
+        if (end > (uint32_t)PAGE) {
+            const uint32_t k_last = (end - 1) >> PB;  // the last entry's page, counted from the open one
+            own.cur = first == kNone ? kNone : first + k_last - 1;
+            own.fill = end - (k_last << PB);
+        } else {
+            own.fill = end;
+        }
+        own.ev += n;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+        if (key[e] != kNone) s.stg[(s.offw[key[e] >> pbits] & 0xFFFFu) + rank[e]] = key[e];
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t j = (uint32_t)tid; j < total; j += NT) {
+        const uint32_t k = s.stg[j];
+        const uint32_t part = k >> pbits;
+        const uint32_t ow = s.offw[part];
+        const uint32_t x = (ow >> 16) + j - (ow & 0xFFFFu);
+        const uint32_t page = x < (uint32_t)PAGE ? s.wcur[part] : s.newp[part] + (x >> PB) - 1u;
+        if (x >= (uint32_t)PAGE && s.newp[part] == kNone) continue;  // pool overflow (flagged)
+        const size_t at = (size_t)(page - page0) * PAGE + (x & (PAGE - 1));
+        if (E16)
+            reinterpret_cast<uint16_t *>(pages)[at] = (uint16_t)(k & emask);
+        else
+            reinterpret_cast<uint32_t *>(pages)[at] = k & emask;
+    }
+}
+
+// End of a partitioning block: the open pages' counts, the row's counts and
+// its page list sorted by partition (rows.*[row][p], list[pool_base ..]).
+__device__ __forceinline__ void part_finish(const PartLds &s, int P, const Owner &own, uint32_t pool_base,
+                                            uint32_t cap, uint32_t *__restrict__ page_cnt,
+                                            const uint32_t *__restrict__ page_part, uint32_t *__restrict__ list,
+                                            const WideRows &rows, uint32_t row) {
+    const int tid = threadIdx.x;
+    __syncthreads();  // the last unit's write-out read offw / cnt0
+    if (tid < P) {
+        if (own.cur != kNone) page_cnt[own.cur] = own.fill;
+        rows.cnt[(size_t)row * rows.ncols + tid] = own.np;
+        rows.ev[(size_t)row * rows.ncols + tid] = own.ev;
+    }
+    uint32_t tot;
+    const uint32_t lo = block_exclusive_scan(tid < P ? own.np : 0u, s.w, &tot);
+    if (tid < P) {
+        rows.off[(size_t)row * rows.ncols + tid] = lo;
+        s.cnt0[tid] = lo;  // list cursors
+    }
+    if (tid == 0) rows.pool[row] = pool_base;
+    __syncthreads();
+    const uint32_t used = min(s.pool[0], cap);
+    for (uint32_t i = (uint32_t)tid; i < used; i += NT) {
+        const uint32_t part = page_part[pool_base + i];
+        if (part >= (uint32_t)P) continue;  // (a page of a failed allocation: overflow, flagged)
+        const uint32_t slot = __hip_atomic_fetch_add(s.cnt0 + part, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        list[pool_base + slot] = pool_base + i;
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// chunk table (+ the counters of this batch's passes)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_wide_chunks(WideArgs a, PixChunk *__restrict__ ctab) {
+    const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (c == 0) {
+        a.counters[0] = a.counters[1] = 0u;
+        *a.pool2_next = 0u;
+    }
+    if (c >= a.n_chunks) return;
+    int lo = 0, hi = a.n_segs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+    }
+    const SegDesc sd = a.segs[lo];
+    const long long base = (c - sd.chunk0) * kChunk;
+    const long long left = sd.n - base;
+    PixChunk ch;
+    ch.pid = sd.pid + base;
+    ch.toa = sd.toa + base;
+    ch.n = (int)(left < kChunk ? left : kChunk);
+    if (ch.n == kChunk && (((uintptr_t)ch.pid | (uintptr_t)ch.toa) & 15u) != 0) ch.n = -kChunk;
+    ch.pad = 0;
+    ctab[c] = ch;
+}
+
+// ---------------------------------------------------------------------------
+// pixel table: sampled pixel counts, then per slot the most frequent pixel
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_wide_sample(WideArgs a, uint32_t *__restrict__ cnt) {
+    const long long n = a.n_chunks;
+    const long long c = (long long)blockIdx.x * n / gridDim.x;
+    if (c >= n) return;
+    const PixChunk ch = a.ctab[c];
+    const int m = ch.n < 0 ? -ch.n : ch.n;
+    for (int i = threadIdx.x; i < m; i += 256) {
+        const uint32_t q = (uint32_t)ld_global(ch.pid + i) - (uint32_t)a.pid_off;
+        if (q < a.L) atomicAdd(cnt + q, 1u);
+    }
+}
+
+template <bool L16>
+__global__ __launch_bounds__(256) void k_wide_table(WideArgs a, const void *__restrict__ lut_rep,
+                                                    const uint32_t *__restrict__ cnt, uint32_t *__restrict__ tab) {
+    const uint32_t C = 1u << a.cbits;
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    if (j >= C) return;
+    uint32_t best = 0, bq = kNone;
+    for (uint32_t q = j; q < a.L; q += C) {
+        const uint32_t v = cnt[q];
+        if (v > best || bq == kNone) {
+            best = v;
+            bq = q;
+        }
+    }
+    uint32_t w = 0;  // empty slot: never a hit
+    if (bq != kNone) {
+        uint32_t val;
+        if (L16) {
+            const uint32_t v = reinterpret_cast<const uint16_t *>(lut_rep)[bq];
+            val = v == 0xFFFFu ? kTabValue : v;
+        } else {
+            const int v = reinterpret_cast<const int *>(lut_rep)[bq];
+            val = v < 0 ? kTabValue : (uint32_t)v / (uint32_t)a.T;
+        }
+        w = kTabValid | ((bq >> a.cbits) << kTagShift) | val;
+    }
+    tab[j] = w;
+}
+
+// ---------------------------------------------------------------------------
+// first pass
+// ---------------------------------------------------------------------------
+template <bool L16, bool TL, bool E16>
+__global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    const int P = a.n_parts;
+    const PartLds s = part_lds(sm, P);
+    const uint32_t C = a.cbits ? 1u << a.cbits : 0u;
+    uint32_t *s_tab = sm + part_words(P);
+    uint32_t *s_tree = s_tab + C;
+    const uint32_t tw = TL ? (uint32_t)align4(a.toa.words) : 0u;
+    PixChunk *s_ctab = reinterpret_cast<PixChunk *>(s_tree + tw);
+    const int tid = threadIdx.x;
+    {  // pixel table and TOA tree: every load of a thread issued before its stores
+        const uint4 *pt = reinterpret_cast<const uint4 *>(a.pix_tab);
+        const uint4 *tt = reinterpret_cast<const uint4 *>(a.toa.tree);
+        const int c4 = (int)(C / 4u);
+        lds_fill<4>(reinterpret_cast<uint4 *>(s_tab), c4 + (int)(tw / 4u),
+                    [&](int i) { return g_ld(i < c4 ? pt + i : tt + (i - c4)); });
+    }
+    for (int i = tid; i < 2 * (align4(P) + 64); i += NT) s.cnt0[i] = 0;
+    if (tid == 0) s.pool[0] = 0;
+    const long long n_units = (a.n_chunks + 1) / 2;
+    const long long cb = (long long)blockIdx.x * n_units / gridDim.x;
+    const long long ce = ((long long)blockIdx.x + 1) * n_units / gridDim.x;
+    const long long c0 = cb * 2, c1 = ce * 2 < a.n_chunks ? ce * 2 : a.n_chunks;
+    const bool fit = c1 - c0 <= kWideLdsChunks;
+    if (fit)
+        for (long long i = tid; i < c1 - c0; i += NT) s_ctab[i] = a.ctab[c0 + i];
+    __syncthreads();
+    const PixChunk *s_ct = fit ? s_ctab : nullptr;
+    const uint32_t pool_base = blockIdx.x * a.cap1;
+    const uint32_t cmask = C ? C - 1u : 0u;
+    const uint32_t lut_bytes = a.L * (L16 ? 2u : 4u);
+    const __amdgpu_buffer_rsrc_t lut = make_rsrc(a.lut, lut_bytes);
+    const uint32_t T = (uint32_t)a.T;
+    const uint32_t emask = (1u << a.pbits) - 1u;
+    Owner own;
+    int p[EPT], t[EPT];
+    // the unit's keys: TOA bins first (t dies), then pixel words (table
+    // probe, a gather for the misses only) in two halves of eight events
+    auto pixel_half = [&](auto o, const uint32_t (&bin)[EPT], uint32_t (&key)[EPT]) __attribute__((always_inline)) {
+        constexpr int O = decltype(o)::value;
+        constexpr int H = EPT / 2;
+        uint32_t q[H], w[H], g[H];
+#pragma unroll
+        for (int e = 0; e < H; ++e) {
+            q[e] = (uint32_t)p[O + e] - (uint32_t)a.pid_off;
+            w[e] = C ? s_tab[q[e] & cmask] : 0u;
+        }
+#pragma unroll
+        for (int e = 0; e < H; ++e) {
+            const bool hit = (w[e] & kTabValid) && ((w[e] >> kTagShift) & kTagMask) == (q[e] >> a.cbits);
+            const bool miss = q[e] < a.L && !hit;
+            const uint32_t off = miss ? q[e] * (L16 ? 2u : 4u) : kOOB;
+            g[e] = L16 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(lut, (int)off, 0, 0)
+                       : __builtin_amdgcn_raw_buffer_load_b32(lut, (int)off, 0, 0);
+            w[e] = hit ? w[e] : kNone;
+        }
+#pragma unroll
+        for (int e = 0; e < H; ++e) {
+            uint32_t base;
+            bool ok;
+            if (w[e] != kNone) {
+                const uint32_t v = w[e] & kTabValue;
+                ok = v != kTabValue;
+                base = v * T;
+            } else if (L16) {
+                ok = q[e] < a.L && g[e] != 0xFFFFu;
+                base = g[e] * T;
+            } else {
+                ok = q[e] < a.L && (int)g[e] >= 0;
+                base = g[e];
+            }
+            key[O + e] = ok && bin[O + e] != kNone ? base + bin[O + e] : kNone;
+        }
+    };
+    if (cb < ce) unit_load(a, s_ct, c0, cb, p, t);
+    for (long long u = cb; u < ce; ++u) {
+        // keys in two halves of eight events (half the front end's registers)
+        uint32_t bin[EPT], key[EPT];
+        toa_bins<TL, EPT, 0>(a.toa, TL ? s_tree : a.toa.tree, t, bin);
+        pixel_half(std::integral_constant<int, 0>{}, bin, key);
+        pixel_half(std::integral_constant<int, EPT / 2>{}, bin, key);
+        part_unit<E16>(s, P, a.pbits, emask, (int)(u & 1), key, own, pool_base, a.cap1, a.pages1, 0u, a.page_cnt,
+                       a.page_part, a.overflow, [&]() __attribute__((always_inline)) {
+                           if (u + 1 < ce) unit_load(a, s_ct, c0, u + 1, p, t);
+                       });
+    }
+    part_finish(s, P, own, pool_base, a.cap1, a.page_cnt, a.page_part, a.list, a.rows1, blockIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// plan: per partition p, items of consecutive rows (rows [0, nrows) of the
+// first pass, or the second pass's rows of p's band); band_out: the items of
+// each partition (the second pass's rows of that band)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_wide_plan(WideRows rows, int nrows, const uint2 *__restrict__ band_rows,
+                                                   int tpb_bits, uint32_t item_max, uint4 *__restrict__ items,
+                                                   uint32_t *__restrict__ count, uint32_t max_items,
+                                                   uint2 *__restrict__ band_out, uint32_t *__restrict__ overflow) {
+    __shared__ unsigned long long s_sum[4];
+    __shared__ uint32_t s_base;
+    const int p = blockIdx.x;
+    uint32_t r0 = 0, nr = (uint32_t)nrows, col = (uint32_t)p;
+    if (band_rows) {
+        const uint2 br = band_rows[p >> tpb_bits];
+        r0 = br.x;
+        nr = br.y;
+        col = (uint32_t)p & ((1u << tpb_bits) - 1u);
+    }
+    unsigned long long sum = 0;
+    for (uint32_t r = threadIdx.x; r < nr; r += 256) sum += rows.ev[(size_t)(r0 + r) * rows.ncols + col];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    const unsigned long long total = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+    uint32_t n = 0;
+    if (total > 0) {
+        const unsigned long long k = (total + item_max - 1) / item_max;
+        n = (uint32_t)(k < nr ? k : nr);
+        if (n > (uint32_t)kWideMaxRows) n = kWideMaxRows;
+        n = n < 1 ? 1 : n;
+    }
+    if (threadIdx.x == 0) {
+        uint32_t base = n ? atomicAdd(count, n) : 0u;
+        if (base + n > max_items) {
+            *overflow = 1u;  // cannot happen with the host's bound
+            n = base < max_items ? max_items - base : 0u;
+        }
+        s_base = base;
+        if (band_out) band_out[p] = make_uint2(base, n);
+    }
+    __syncthreads();
+    const uint32_t base = s_base;
+    if (base + n > max_items) n = base < max_items ? max_items - base : 0u;
+    for (uint32_t j = threadIdx.x; j < n; j += 256)
+        items[base + j] = make_uint4((uint32_t)p, r0 + (uint32_t)((unsigned long long)j * nr / n),
+                                     r0 + (uint32_t)((unsigned long long)(j + 1) * nr / n), n == 1 ? 1u : 0u);
+}
+
+namespace {
+
+// The pages of one item (partition col of rows [r0, r0 + nr)): prefix of the
+// rows' page counts in LDS (s_pref[nr] = the item's pages).  Ends with a barrier.
+__device__ __forceinline__ uint32_t item_prefix(const WideRows &rows, uint32_t r0, uint32_t nr, uint32_t col,
+                                                uint32_t *s_pref, uint32_t *s_w) {
+    const int tid = threadIdx.x;
+    const uint32_t v = (uint32_t)tid < nr ? rows.cnt[(size_t)(r0 + tid) * rows.ncols + col] : 0u;
+    uint32_t tot;
+    const uint32_t x = block_exclusive_scan(v, s_w, &tot);
+    if ((uint32_t)tid <= nr) s_pref[tid] = (uint32_t)tid < nr ? x : tot;
+    __syncthreads();
+    return tot;
+}
+
+// page k of the item: its row (last r with s_pref[r] <= k), then the list entry
+__device__ __forceinline__ uint32_t item_page(const WideRows &rows, const uint32_t *__restrict__ list,
+                                              uint32_t r0, uint32_t nr, uint32_t col, const uint32_t *s_pref,
+                                              uint32_t k) {
+    uint32_t lo = 0, hi = nr - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_pref[mid] <= k) lo = mid; else hi = mid - 1;
+    }
+    const size_t r = r0 + lo;
+    return list[rows.pool[r] + rows.off[r * rows.ncols + col] + (k - s_pref[lo])];
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// second pass (two-level form): one item of a band -> tile pages
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    if (blockIdx.x >= a.counters[0]) return;
+    const uint4 it = a.items1[blockIdx.x];
+    const int P = 1 << a.tpb_bits;
+    const PartLds s = part_lds(sm, P);
+    uint32_t *s_pref = sm + part_words(P);
+    __shared__ unsigned long long s_ev[16];
+    const int tid = threadIdx.x;
+    const uint32_t band = it.x, r0 = it.y, nr = it.z - it.y;
+    for (int i = tid; i < 2 * (align4(P) + 64); i += NT) s.cnt0[i] = 0;
+    // the item's entries size its pool (one allocation per item)
+    unsigned long long ev = (uint32_t)tid < nr ? a.rows1.ev[(size_t)(r0 + tid) * a.rows1.ncols + band] : 0u;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) ev += __shfl_xor(ev, d, 64);
+    if ((tid & 63) == 0) s_ev[tid >> 6] = ev;
+    const uint32_t n_pages = item_prefix(a.rows1, r0, nr, band, s_pref, s.w);
+    if (tid == 0) {
+        unsigned long long e = 0;
+        for (int i = 0; i < NT / 64; ++i) e += s_ev[i];
+        const unsigned long long need = (e + PAGE - 1) / PAGE + (unsigned long long)P + 1;
+        const uint32_t base = atomicAdd(a.pool2_next, (uint32_t)(need < 0x7FFFFFFFull ? need : 0x7FFFFFFFull));
+        uint32_t cap = (uint32_t)need;
+        if ((unsigned long long)base + need > a.pool2_cap) {
+            *a.overflow = 1u;  // cannot happen with the host's bound
+            cap = 0;
+        }
+        s.pool[0] = 0;
+        s.pool[1] = a.page0_2 + base;  // second-pass pages follow the first pass's
+        s.pool[2] = cap;
+    }
+    __syncthreads();
+    const uint32_t pool_base = s.pool[1], cap = s.pool[2];
+    const int lane = tid & 63;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t *pages1 = reinterpret_cast<const uint32_t *>(a.pages1);
+    // unit u: pages 16u .. 16u + 15, wave wv takes page 16u + wv, lane 16
+    // consecutive entries
+    auto load = [&](uint32_t u, uint32_t (&key)[EPT]) __attribute__((always_inline)) {
+        const uint32_t k = u * (NT / 64) + wv;
+        uint32_t cnt = 0, page = 0;
+        if (k < n_pages) {
+            page = item_page(a.rows1, a.list, r0, nr, band, s_pref, k);
+            cnt = a.page_cnt[page];
+        }
+        const uint32_t e0 = (uint32_t)lane * EPT;
+        const uint4 *src = reinterpret_cast<const uint4 *>(pages1 + (size_t)page * PAGE + e0);
+#pragma unroll
+        for (int j = 0; j < EPT / 4; ++j) {
+            const uint4 v = e0 + 4u * j < cnt ? src[j] : make_uint4(kNone, kNone, kNone, kNone);
+            key[4 * j] = v.x;
+            key[4 * j + 1] = v.y;
+            key[4 * j + 2] = v.z;
+            key[4 * j + 3] = v.w;
+        }
+#pragma unroll
+        for (int e = 0; e < EPT; ++e)
+            if (e0 + (uint32_t)e >= cnt) key[e] = kNone;
+    };
+    Owner own;
+    const uint32_t n_units = (n_pages + NT / 64 - 1) / (NT / 64);
+    uint32_t key[EPT], nxt[EPT];
+    if (n_units) load(0, nxt);
+    for (uint32_t u = 0; u < n_units; ++u) {
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) key[e] = nxt[e];
+        part_unit<true>(s, P, kWideTileBits, (1u << kWideTileBits) - 1u, (int)(u & 1), key, own, pool_base, cap,
+                        a.pages2, a.page0_2, a.page_cnt, a.page_part, a.overflow, [&]() __attribute__((always_inline)) {
+                            if (u + 1 < n_units) load(u + 1, nxt);
+                        });
+    }
+    part_finish(s, P, own, pool_base, cap, a.page_cnt, a.page_part, a.list, a.rows2, blockIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// pass B: one item of a tile histogrammed in LDS
+// ---------------------------------------------------------------------------
+constexpr int kWideAccThreads = 1024;
+__global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4 *__restrict__ items,
+                                                                     const uint32_t *__restrict__ item_count,
+                                                                     WideRows rows, const uint32_t *__restrict__ list,
+                                                                     const uint32_t *__restrict__ page_cnt,
+                                                                     const uint16_t *__restrict__ pages,
+                                                                     uint32_t page0, uint32_t colmask, uint32_t *__restrict__ hist,
+                                                                     long long n_bins) {
+    constexpr int NB = 1 << kWideTileBits;
+    constexpr int NW = kWideAccThreads / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[NB + 64];
+    __shared__ uint32_t s_pref[kWideMaxRows + 1];
+    __shared__ uint32_t s_w[32];
+    const uint32_t n_items = *item_count;
+    const uint4 it = items[blockIdx.x];
+    if (blockIdx.x >= n_items) return;
+    const int tid = threadIdx.x;
+    for (int i = tid * 4; i < NB + 64; i += kWideAccThreads * 4)
+        *reinterpret_cast<uint4 *>(s_tile + i) = make_uint4(0, 0, 0, 0);
+    const uint32_t tile = it.x, r0 = it.y, nr = it.z - it.y, col = tile & colmask;
+    const uint32_t n_pages = item_prefix(rows, r0, nr, col, s_pref, s_w);  // (+ the barrier for s_tile)
+    const int lane = tid & 63;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t e0 = (uint32_t)lane * 16u;
+    const uint32_t dummy = NB + (uint32_t)lane;
+    auto fetch = [&](uint32_t k, uint4 &x, uint4 &y, uint32_t &cnt) __attribute__((always_inline)) {
+        cnt = 0;
+        x = y = make_uint4(0, 0, 0, 0);
+        if (k < n_pages) {
+            const uint32_t page = item_page(rows, list, r0, nr, col, s_pref, k);
+            cnt = page_cnt[page];
+            const uint4 *src = reinterpret_cast<const uint4 *>(pages + (size_t)(page - page0) * PAGE + e0);
+            x = src[0];
+            y = src[1];
+        }
+    };
+    uint4 a, b, na, nb;
+    uint32_t cnt, ncnt;
+    fetch(wv, a, b, cnt);
+    for (uint32_t k = wv; k < n_pages; k += NW) {
+        fetch(k + NW, na, nb, ncnt);  // the wave's next page in flight
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint32_t v = (w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu;
+            __hip_atomic_fetch_add(s_tile + (e0 + (uint32_t)q < cnt ? v : dummy), 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        a = na;
+        b = nb;
+        cnt = ncnt;
+    }
+    __syncthreads();
+    const long long base = (long long)tile << kWideTileBits;
+    if ((it.w & 1u) && base + NB <= n_bins) {
+        // the tile's only item owns its bins: 16-byte read-modify-write
+        constexpr int V = NB / 4 / kWideAccThreads;
+        uint4 *h4 = reinterpret_cast<uint4 *>(hist + base);
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(s_tile);
+        uint4 hv[V];
+#pragma unroll
+        for (int u = 0; u < V; ++u) hv[u] = h4[u * kWideAccThreads + tid];
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            const uint4 v = s4[u * kWideAccThreads + tid];
+            if (v.x | v.y | v.z | v.w)
+                h4[u * kWideAccThreads + tid] = make_uint4(hv[u].x + v.x, hv[u].y + v.y, hv[u].z + v.z, hv[u].w + v.w);
+        }
+    } else {
+        for (int i = tid; i < NB; i += kWideAccThreads) {
+            const uint32_t v = s_tile[i];
+            if (v != 0u && base + i < n_bins) atomicAdd(hist + base + i, v);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launch wrappers
+// ---------------------------------------------------------------------------
+size_t wide_scatter_smem(const WideArgs &a) {
+    const size_t P4 = (size_t)align4(a.n_parts);
+    const size_t words = (size_t)UNIT + 2 * (P4 + 64) + 3 * P4 + 32 + 4 + (a.cbits ? (size_t)1 << a.cbits : 0) +
+                         (a.toa.lds ? (size_t)align4(a.toa.words) : 0);
+    return 4 * words + sizeof(PixChunk) * kWideLdsChunks;
+}
+
+static size_t wide_split_smem(const WideArgs &a) {
+    const size_t P4 = (size_t)align4(1 << a.tpb_bits);
+    return 4 * ((size_t)UNIT + 2 * (P4 + 64) + 3 * P4 + 32 + 4 + kWideMaxRows + 1);
+}
+
+hipError_t launch_wide_chunks(const WideArgs &a, hipStream_t st) {
+    const unsigned g = (unsigned)((a.n_chunks + 255) / 256);
+    hipLaunchKernelGGL(k_wide_chunks, dim3(g > 0 ? g : 1), dim3(256), 0, st, a, const_cast<PixChunk *>(a.ctab));
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_table(const WideArgs &a, const void *lut_rep, uint32_t *pix_cnt, uint32_t *tab,
+                             hipStream_t st) {
+    if (a.cbits == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(pix_cnt, 0, (size_t)a.L * 4, st);
+    if (e != hipSuccess) return e;
+    const int g = (int)(a.n_chunks < kWideSample ? a.n_chunks : kWideSample);
+    if (g > 0) hipLaunchKernelGGL(k_wide_sample, dim3(g), dim3(256), 0, st, a, pix_cnt);
+    const unsigned gt = (unsigned)(((1u << a.cbits) + 255) / 256);
+    if (a.lut16)
+        hipLaunchKernelGGL(k_wide_table<true>, dim3(gt), dim3(256), 0, st, a, lut_rep, pix_cnt, tab);
+    else
+        hipLaunchKernelGGL(k_wide_table<false>, dim3(gt), dim3(256), 0, st, a, lut_rep, pix_cnt, tab);
+    return hipGetLastError();
+}
+
+template <bool L16, bool TL, bool E16>
+static hipError_t launch_scatter_t(const WideArgs &a, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
+    const size_t sm = wide_scatter_smem(a);
+    if (sm > 160 * 1024) return hipErrorInvalidValue;
+    (void)hipFuncSetAttribute((const void *)k_wide_scatter<L16, TL, E16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
+    hipExtLaunchKernelGGL((k_wide_scatter<L16, TL, E16>), dim3(a.grid1), dim3(NT), sm, st, start, stop, 0, a);
+    return hipGetLastError();
+}
+
+template <bool L16, bool TL>
+static hipError_t launch_scatter_tl(const WideArgs &a, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
+    return a.levels == 1 ? launch_scatter_t<L16, TL, true>(a, st, start, stop)
+                         : launch_scatter_t<L16, TL, false>(a, st, start, stop);
+}
+
+hipError_t launch_wide(const WideArgs &a, hipStream_t st, hipEvent_t start, hipEvent_t stop, hipEvent_t bstart,
+                       hipEvent_t bstop) {
+    if (a.n_parts < 1 || a.n_parts > kWideMaxParts || a.grid1 < 1 || a.grid1 > kWideMaxRows)
+        return hipErrorInvalidValue;
+    hipError_t e = a.lut16 ? (a.toa.lds ? launch_scatter_tl<true, true>(a, st, start, stop)
+                             : launch_scatter_tl<true, false>(a, st, start, stop))
+                : (a.toa.lds ? launch_scatter_tl<false, true>(a, st, start, stop)
+                             : launch_scatter_tl<false, false>(a, st, start, stop));
+    if (e != hipSuccess) return e;
+    const uint32_t *cnt2 = a.counters + 1;
+    WideRows rows = a.rows1;
+    const uint4 *items = a.items1;
+    const uint32_t *count = a.counters;
+    const uint16_t *pages = reinterpret_cast<const uint16_t *>(a.pages1);
+    uint32_t colmask = 0xFFFFFFFFu;
+    uint32_t max_items = a.max_items1;
+    uint32_t page0 = 0;
+    if (a.levels == 1) {
+        hipLaunchKernelGGL(k_wide_plan, dim3(a.n_parts), dim3(256), 0, st, a.rows1, a.grid1,
+                           (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.max_items1,
+                           (uint2 *)nullptr, a.overflow);
+    } else {
+        hipLaunchKernelGGL(k_wide_plan, dim3(a.n_parts), dim3(256), 0, st, a.rows1, a.grid1,
+                           (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.max_items1,
+                           a.band_items, a.overflow);
+        const size_t sm2 = wide_split_smem(a);
+        (void)hipFuncSetAttribute((const void *)k_wide_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm2);
+        hipLaunchKernelGGL(k_wide_split, dim3(a.max_items1), dim3(NT), sm2, st, a);
+        hipLaunchKernelGGL(k_wide_plan, dim3(a.n_tiles), dim3(256), 0, st, a.rows2, 0,
+                           (const uint2 *)a.band_items, a.tpb_bits, a.item_max2, a.items2,
+                           const_cast<uint32_t *>(cnt2), a.max_items2, (uint2 *)nullptr, a.overflow);
+        rows = a.rows2;
+        items = a.items2;
+        count = cnt2;
+        pages = reinterpret_cast<const uint16_t *>(a.pages2);
+        colmask = (1u << a.tpb_bits) - 1u;
+        max_items = a.max_items2;
+        page0 = a.page0_2;
+    }
+    hipExtLaunchKernelGGL(k_wide_accumulate, dim3(max_items), dim3(kWideAccThreads), 0, st, bstart, bstop, 0, items,
+                          count, rows, a.list, a.page_cnt, pages, page0, colmask, a.hist, a.n_bins);
+    return hipGetLastError();
+}
+
+}  // namespace lde

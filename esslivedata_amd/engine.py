@@ -567,7 +567,7 @@ class BinningEngine:
             'tile_bits': tb.value,
             'n_tiles': nt.value,
             'events_binned': eb.value,
-            'last_strategy': {0: 'monitor', 1: 'atomic', 2: 'partition', 3: 'paged', 4: 'split', 5: 'pixel'}.get(ls.value, '?'),
+            'last_strategy': {0: 'monitor', 1: 'atomic', 2: 'partition', 3: 'paged', 4: 'split', 5: 'pixel', 6: 'wide'}.get(ls.value, '?'),
             'device': self._device,
         }
 

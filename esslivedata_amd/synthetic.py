@@ -319,7 +319,23 @@ def zipf_pixel_weights(p: int, s: float = 1.2, seed: int = 7) -> np.ndarray:
 
 
 def dream_hot_bins(edges_ns: np.ndarray) -> list[tuple[float, float]]:
-    return [(edges_ns[b], edges_ns[b + 1]) for b in (40, 62, 85)]
+    # bins 40, 62 and 85 of 100: the same fractions of the edge list for any
+    # bin count, so the peaks stay at the same times when the edges share
+    # start, stop and scale
+    nb = len(edges_ns) - 1
+    return [(edges_ns[b], edges_ns[b + 1]) for b in (40 * nb // 100, 62 * nb // 100, 85 * nb // 100)]
+
+
+def with_toa_edges(inst: Instrument, num_bins: int | None = None, scale: str | None = None,
+                   start: float | None = None) -> Instrument:
+    """The instrument with other TOA edges (any ``EdgesModel`` configuration:
+    1..10000 bins, linear or log, parameter_models.py:82-105)."""
+    import dataclasses
+
+    e = inst.edges
+    edges = dataclasses.replace(e, num_bins=num_bins or e.num_bins, scale=scale or e.scale,
+                                start=e.start if start is None else start)
+    return dataclasses.replace(inst, edges=edges)
 
 
 def dream_events(n: int, inst: Instrument, seed: int = 7, cdf: np.ndarray | None = None):

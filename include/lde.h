@@ -56,6 +56,8 @@ extern "C" {
 #define LDE_STRATEGY_SPLIT 4       /* hot screen rows in LDS + cold remainder through PAGED (skewed streams) */
 #define LDE_STRATEGY_PIXEL 5       /* partition by pixel range (no LUT gather) + the range's LUT slice and
                                       screen footprint in LDS; needs footprints that fit (else PAGED) */
+#define LDE_STRATEGY_WIDE 6        /* any TOA edges and histogram size: pixel-table front end, keys into page
+                                      chains by tile (one level, or bands then tiles), LDS tiles (lde_wide.hip) */
 
 /* histogram selectors for lde_read_histogram */
 #define LDE_CURRENT 0    /* window since the last finalize  (accumulators.py:138-163) */
@@ -335,7 +337,9 @@ int lde_synchronize(lde_handle *h);
 #define LDE_K_SPLIT_AUX 11 /* hot-set selection, hot-row reduce, cold segment table */
 #define LDE_K_COORD 12    /* k_event_coord / k_event_key: wavelength-mode coordinate pass */
 #define LDE_K_PIXEL 13    /* k_pix_scatter: PIXEL pass A (stamped by its own dispatch) */
-#define LDE_K_COUNT 14
+#define LDE_K_WIDE 14     /* k_wide_scatter: WIDE first pass (stamped by its own dispatch) */
+#define LDE_K_WIDE_ACC 15 /* k_wide_accumulate: WIDE pass B (stamped by its own dispatch) */
+#define LDE_K_COUNT 16
 int lde_timing_enable(lde_handle *h, int32_t enable);
 /* Record only the kernels whose bit (1 << LDE_K_*) is set in mask (default:
  * all).  Fewer recorded events = less host work per batch. */
@@ -357,6 +361,12 @@ int lde_kernel_stats(lde_handle *h, int32_t kernel_id, double *ms, int64_t *laun
 #define LDE_C_WAITS 3
 #define LDE_C_WAITS_BLOCKED 4
 #define LDE_C_WAIT_PRED_US 5
+/* 6, 7: reserved (sieve pair counters of round 4, removed; read as 0) */
+#define LDE_C_WIDE_LEVELS 8      /* WIDE partition levels (1 or 2; 0: WIDE unavailable for this view) */
+#define LDE_C_WIDE_PARTS 9       /* WIDE first-level partitions (tiles or bands) */
+#define LDE_C_WIDE_TREE_WORDS 10 /* words of the WIDE TOA lookup tree */
+#define LDE_C_WIDE_TREE_LDS 11   /* 1 if the tree is kept in LDS (else read from global memory) */
+#define LDE_C_WIDE_ITEMS 12      /* pass-B work items of the last WIDE batch (synchronizes) */
 int lde_counter(lde_handle *h, int32_t id, int64_t *value);
 
 /* Introspection for tests and reports. */
