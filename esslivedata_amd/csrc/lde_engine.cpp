@@ -1485,7 +1485,10 @@ int bin_wide(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunk
     const long long units = (chunks + 1) / 2;
     const int grid1 = (int)std::min<long long>(units, std::min<long long>(h->cus, lde::kWideMaxRows));
     const long long upb = (units + grid1 - 1) / grid1;
-    const uint32_t cap1 = (uint32_t)((upb * lde::kWideUnit + lde::kWidePage - 1) / lde::kWidePage + P + 1);
+    // a block's pool: its events plus the runs' pads (< 4 per partition and
+    // unit) in whole pages, plus one partly filled page per partition
+    const uint32_t cap1 =
+        (uint32_t)((upb * ((long long)lde::kWideUnit + 3LL * P) + lde::kWidePage - 1) / lde::kWidePage + P + 1);
     const size_t pages1 = (size_t)grid1 * cap1;
     const size_t esz1 = h->wide_levels == 1 ? 2 : 4;
     // work items: pass B about one per tile (a tile past item_max entries,
@@ -1498,7 +1501,15 @@ int bin_wide(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunk
     const long long max_items1 = P + total / item_max1 + 2;
     const long long max_items2 = h->wide_levels == 2 ? h->wide_tiles + total / item_max2 + 2 : 0;
     const int tpb = 1 << h->wide_tpb_bits;
-    const size_t pool2 = h->wide_levels == 2 ? (size_t)(total / lde::kWidePage) + (size_t)max_items1 * (tpb + 2) + 1 : 0;
+    // second-pass pool: every item's allocation (k_wide_split) summed: the
+    // first pass's entries with their pads, this pass's pads (<= 3 per tile
+    // and 16-page unit, + 2 units per item), one partly filled page per tile
+    const long long in1 = (long long)grid1 * upb * ((long long)lde::kWideUnit + 3LL * P);
+    const long long pages_in = in1 / lde::kWidePage + (long long)grid1 * P;  // (+ partly filled pages)
+    const long long units2 = pages_in / 16 + pages_in / 1024 + 2 * max_items1 + 1;
+    const size_t pool2 = h->wide_levels == 2
+                             ? (size_t)((in1 + 3LL * tpb * units2) / lde::kWidePage) + (size_t)max_items1 * (tpb + 3) + 1
+                             : 0;
     if (pages1 + pool2 >= 0xFFFFFFF0ULL || total >= 0xFFFFFFFFLL)
         return fail(h, LDE_EINVAL, "batch too large for the WIDE page pools");
     if (int rc = grow(h, &h->d_wctab, h->wctab_cap, (size_t)chunks)) return rc;

@@ -114,12 +114,15 @@ __device__ __forceinline__ void toa_bins(const WideToa &tp, const uint32_t *tree
 // events of unit u: chunks 2u, 2u + 1; thread tid takes chunk 2u + tid / CT
 // (wave-uniform) as thread tid % CT of it.  Chunk pointers from the block's
 // LDS copy of the chunk table (s_ct, chunks from c0 on) or the global table.
+// (u >= ue, past the block's units: dropped events, no loads -- p and t are
+// always assigned, so the caller needs no branch and the registers no
+// liveness across the unit)
 __device__ __forceinline__ void unit_load(const WideArgs &a, const PixChunk *s_ct, long long c0, long long u,
-                                          int (&p)[EPT], int (&t)[EPT]) {
+                                          long long ue, int (&p)[EPT], int (&t)[EPT]) {
     const int tid = threadIdx.x;
     const long long c = u * 2 + __builtin_amdgcn_readfirstlane(tid / CT);
     const int tl = tid % CT;
-    if (c >= a.n_chunks) {
+    if (c >= a.n_chunks || u >= ue) {
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
             p[e] = a.pid_off - 1;  // outside the LUT: dropped
@@ -157,26 +160,32 @@ __device__ __forceinline__ void unit_load(const WideArgs &a, const PixChunk *s_c
 
 // ---------------------------------------------------------------------------
 // The partitioning step shared by both passes.  LDS (words): staging
-// [UNIT] | counts x 2 (unit parity) [P4 + 64 lane dummies] | staging offset
-// and write fill per partition [P4] (offset | fill << 16) | page of the run's
-// first entries [P4] | first new page [P4] | scan scratch [32] | pool [4].
-// Thread p < P owns partition p: its open page and fill, and the row's page
-// and entry counts, live in that thread's registers.
+// [UNIT + 3 P4] (runs padded to 4) | counts x 2 (unit parity) [P4 + 64 lane
+// dummies] | staging offset and write fill per partition [P4] (offset | fill
+// << 16) | page of the run's first entries [P4] | first new page [P4] | scan
+// scratch [32] | pool [4].  Thread p < P owns partition p: its open page and
+// fill, and the row's page and entry counts, live in that thread's registers.
+// Every run is padded to a multiple of 4 entries (pads: kNone in staging,
+// kPad16 / kNone in the pages, skipped by the readers), so fills stay 4-aligned
+// and the write-out moves groups of four entries (one 16-byte LDS read, one 8-
+// or 16-byte store) that never straddle a run or a page.
 // ---------------------------------------------------------------------------
+constexpr uint32_t kPad16 = 0xFFFFu;
+
 struct PartLds {
     uint32_t *stg, *cnt0, *cnt1, *offw, *wcur, *newp, *w, *pool;
 };
 
-__device__ __forceinline__ size_t part_words(int P) {
+__host__ __device__ inline size_t part_words(int P) {
     const size_t P4 = (size_t)align4(P);
-    return (size_t)UNIT + 2 * (P4 + 64) + 3 * P4 + 32 + 4;
+    return (size_t)UNIT + 3 * P4 + 2 * (P4 + 64) + 3 * P4 + 32 + 4;
 }
 
 __device__ __forceinline__ PartLds part_lds(uint32_t *sm, int P) {
     const uint32_t P4 = (uint32_t)align4(P);
     PartLds s;
     s.stg = sm;
-    s.cnt0 = s.stg + UNIT;
+    s.cnt0 = s.stg + UNIT + 3 * P4;
     s.cnt1 = s.cnt0 + P4 + 64;
     s.offw = s.cnt1 + P4 + 64;
     s.wcur = s.offw + P4;
@@ -192,13 +201,15 @@ struct Owner {  // registers of the owner thread of one partition
 
 // One unit: keys (kNone = no entry) are ranked per partition (part = key >>
 // pbits) with returning LDS atomics, staged sorted by partition and appended
-// to the partitions' pages (entries: key & emask, as u16 or u32).
-// `next()` runs right after the rank atomics (the next unit's loads).
-template <bool E16, typename NEXT>
+// to the partitions' pages (entries: key & emask, as u16 or u32).  next()
+// runs right after the rank atomics (the next unit's loads), mid() between
+// the staging and the write-out (the next unit's front end, whose gathers
+// then fly behind the write-out).
+template <bool E16, typename NEXT, typename MID>
 __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, uint32_t emask, int parity,
                                           const uint32_t (&key)[EPT], Owner &own, uint32_t pool_base,
                                           uint32_t cap, void *pages, uint32_t page0, uint32_t *__restrict__ page_cnt,
-                                          uint32_t *__restrict__ page_part, uint32_t *overflow, NEXT next) {
+                                          uint32_t *__restrict__ page_part, uint32_t *overflow, NEXT next, MID mid) {
     const int tid = threadIdx.x;
     const uint32_t P4 = (uint32_t)align4(P);
     uint32_t *cnt = parity ? s.cnt1 : s.cnt0;
@@ -211,20 +222,23 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
                                          __HIP_MEMORY_SCOPE_WORKGROUP);
     next();
     __syncthreads();
-    uint32_t n = 0;
+    uint32_t n = 0, v = 0;
     if (tid < P) {
         n = cnt[tid];
+        v = (n + 3u) & ~3u;
         cnt_next[tid] = 0;
     }
     uint32_t total;
-    const uint32_t off = block_exclusive_scan(n, s.w, &total);
+    const uint32_t off = block_exclusive_scan(v, s.w, &total);
     if (tid < P && n > 0) {
-        // the run occupies positions [fill, fill + n) of the partition's
+        for (uint32_t j = n; j < v; ++j) s.stg[off + j] = kNone;  // the run's pads
+        // the run occupies positions [fill, fill + v) of the partition's
         // chain: < PAGE in the open page, the rest in n_new new pages
         const uint32_t room = (uint32_t)PAGE - own.fill;
         uint32_t first = kNone;
-        if (n > room) {
-            const uint32_t n_new = (n - room + PAGE - 1) >> PB;
+        bool lost = false;
+        if (v > room) {
+            const uint32_t n_new = (v - room + PAGE - 1) >> PB;
             const uint32_t o = __hip_atomic_fetch_add(s.pool, n_new, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (o + n_new <= cap) {
                 first = pool_base + o;
@@ -235,40 +249,57 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
                 }
                 own.np += n_new;
             } else {
-                *overflow = 1u;  // cannot happen with the host's pool size
+                // pool exhausted (cannot happen with the host's pool size):
+                // the reserved pages inside the pool are marked unused, the
+                // run's entries past its open page are dropped, and the flag
+                // makes finalize fail
+                *overflow = 1u;
+                for (uint32_t k = o; k < cap && k < o + n_new; ++k) page_part[pool_base + k] = kNone;
+                lost = true;
             }
         }
         s.offw[tid] = off | (own.fill << 16);
         s.wcur[tid] = own.cur;
         s.newp[tid] = first;
-        const uint32_t end = own.fill + n;
-        if (end > (uint32_t)PAGE) {
+        const uint32_t end = own.fill + v;
+        if (lost) {  // the open page is full now: the next run allocates again
+            if (own.cur != kNone) page_cnt[own.cur] = PAGE;
+            own.cur = kNone;
+            own.fill = PAGE;
+        } else if (end > (uint32_t)PAGE) {
             const uint32_t k_last = (end - 1) >> PB;  // the last entry's page, counted from the open one
-            own.cur = first == kNone ? kNone : first + k_last - 1;
+            own.cur = first + k_last - 1;
             own.fill = end - (k_last << PB);
         } else {
             own.fill = end;
         }
-        own.ev += n;
+        own.ev += v;
     }
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < EPT; ++e)
         if (key[e] != kNone) s.stg[(s.offw[key[e] >> pbits] & 0xFFFFu) + rank[e]] = key[e];
     __syncthreads();
+    mid();
 #pragma unroll 1
-    for (uint32_t j = (uint32_t)tid; j < total; j += NT) {
-        const uint32_t k = s.stg[j];
-        const uint32_t part = k >> pbits;
+    for (uint32_t g = (uint32_t)tid * 4u; g < total; g += NT * 4u) {
+        const uint4 k4 = *reinterpret_cast<const uint4 *>(s.stg + g);
+        const uint32_t part = k4.x >> pbits;  // a group's first entry is never a pad
         const uint32_t ow = s.offw[part];
-        const uint32_t x = (ow >> 16) + j - (ow & 0xFFFFu);
-        const uint32_t page = x < (uint32_t)PAGE ? s.wcur[part] : s.newp[part] + (x >> PB) - 1u;
-        if (x >= (uint32_t)PAGE && s.newp[part] == kNone) continue;  // pool overflow (flagged)
+        const uint32_t x = (ow >> 16) + g - (ow & 0xFFFFu);
+        const uint32_t np = s.newp[part], wc = s.wcur[part];
+        const uint32_t page = x < (uint32_t)PAGE ? wc : np + (x >> PB) - 1u;
+        if (x < (uint32_t)PAGE ? wc == kNone : np == kNone) continue;  // pool overflow (flagged)
         const size_t at = (size_t)(page - page0) * PAGE + (x & (PAGE - 1));
-        if (E16)
-            reinterpret_cast<uint16_t *>(pages)[at] = (uint16_t)(k & emask);
-        else
-            reinterpret_cast<uint32_t *>(pages)[at] = k & emask;
+        if (E16) {
+            auto e16 = [&](uint32_t k) { return k == kNone ? kPad16 : (k & emask); };
+            *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(pages) + at) =
+                make_uint2(e16(k4.x) | (e16(k4.y) << 16), e16(k4.z) | (e16(k4.w) << 16));
+        } else {
+            auto e32 = [&](uint32_t k) { return k == kNone ? kNone : (k & emask); };
+            *reinterpret_cast<uint4 *>(reinterpret_cast<uint32_t *>(pages) + at) =
+                make_uint4(e32(k4.x), e32(k4.y), e32(k4.z), e32(k4.w));
+        }
     }
 }
 
@@ -334,16 +365,35 @@ __global__ __launch_bounds__(256) void k_wide_chunks(WideArgs a, PixChunk *__res
 // ---------------------------------------------------------------------------
 // pixel table: sampled pixel counts, then per slot the most frequent pixel
 // ---------------------------------------------------------------------------
+// sampled chunks: per block, counts aggregated in an LDS table of 2048
+// tagged slots first (a Zipf-hot pixel holds a large share of a DREAM sample:
+// one global address would serialize at the memory side), then one global
+// atomic per slot; pixels whose slot is taken count with global atomics
 __global__ __launch_bounds__(256) void k_wide_sample(WideArgs a, uint32_t *__restrict__ cnt) {
+    constexpr int NS = 2048;
+    __shared__ uint32_t s_key[NS], s_cnt[NS];
+    for (int i = threadIdx.x; i < NS; i += 256) {
+        s_key[i] = kNone;
+        s_cnt[i] = 0;
+    }
+    __syncthreads();
     const long long n = a.n_chunks;
     const long long c = (long long)blockIdx.x * n / gridDim.x;
-    if (c >= n) return;
-    const PixChunk ch = a.ctab[c];
-    const int m = ch.n < 0 ? -ch.n : ch.n;
-    for (int i = threadIdx.x; i < m; i += 256) {
-        const uint32_t q = (uint32_t)ld_global(ch.pid + i) - (uint32_t)a.pid_off;
-        if (q < a.L) atomicAdd(cnt + q, 1u);
+    if (c < n) {
+        const PixChunk ch = a.ctab[c];
+        const int m = ch.n < 0 ? -ch.n : ch.n;
+        for (int i = threadIdx.x; i < m; i += 256) {
+            const uint32_t q = (uint32_t)ld_global(ch.pid + i) - (uint32_t)a.pid_off;
+            if (q >= a.L) continue;
+            const uint32_t slot = (q * 2654435761u) >> 21;
+            const uint32_t old = atomicCAS(s_key + slot, kNone, q);
+            if (old == kNone || old == q) atomicAdd(s_cnt + slot, 1u);
+            else atomicAdd(cnt + q, 1u);
+        }
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NS; i += 256)
+        if (s_key[i] != kNone) atomicAdd(cnt + s_key[i], s_cnt[i]);
 }
 
 template <bool L16>
@@ -415,19 +465,20 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
     const uint32_t emask = (1u << a.pbits) - 1u;
     Owner own;
     int p[EPT], t[EPT];
-    // the unit's keys: TOA bins first (t dies), then pixel words (table
-    // probe, a gather for the misses only) in two halves of eight events
-    auto pixel_half = [&](auto o, const uint32_t (&bin)[EPT], uint32_t (&key)[EPT]) __attribute__((always_inline)) {
-        constexpr int O = decltype(o)::value;
-        constexpr int H = EPT / 2;
-        uint32_t q[H], w[H], g[H];
+    // Front end of a unit, in two steps so its latency hides behind the
+    // previous unit's write-out: issue() bins the TOA (t dies), probes the
+    // pixel table and issues the gathers of the misses (hits and unknown ids
+    // load out of range: no request); finish() turns the words into keys.
+    uint32_t q[EPT], w[EPT], g[EPT], bin[EPT];
+    auto issue = [&]() __attribute__((always_inline)) {
+        toa_bins<TL, EPT, 0>(a.toa, TL ? s_tree : a.toa.tree, t, bin);
 #pragma unroll
-        for (int e = 0; e < H; ++e) {
-            q[e] = (uint32_t)p[O + e] - (uint32_t)a.pid_off;
+        for (int e = 0; e < EPT; ++e) {
+            q[e] = (uint32_t)p[e] - (uint32_t)a.pid_off;
             w[e] = C ? s_tab[q[e] & cmask] : 0u;
         }
 #pragma unroll
-        for (int e = 0; e < H; ++e) {
+        for (int e = 0; e < EPT; ++e) {
             const bool hit = (w[e] & kTabValid) && ((w[e] >> kTagShift) & kTagMask) == (q[e] >> a.cbits);
             const bool miss = q[e] < a.L && !hit;
             const uint32_t off = miss ? q[e] * (L16 ? 2u : 4u) : kOOB;
@@ -435,8 +486,10 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
                        : __builtin_amdgcn_raw_buffer_load_b32(lut, (int)off, 0, 0);
             w[e] = hit ? w[e] : kNone;
         }
+    };
+    auto finish = [&](uint32_t (&key)[EPT]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int e = 0; e < H; ++e) {
+        for (int e = 0; e < EPT; ++e) {
             uint32_t base;
             bool ok;
             if (w[e] != kNone) {
@@ -450,20 +503,19 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
                 ok = q[e] < a.L && (int)g[e] >= 0;
                 base = g[e];
             }
-            key[O + e] = ok && bin[O + e] != kNone ? base + bin[O + e] : kNone;
+            key[e] = ok && bin[e] != kNone ? base + bin[e] : kNone;
         }
     };
-    if (cb < ce) unit_load(a, s_ct, c0, cb, p, t);
+    unit_load(a, s_ct, c0, cb, ce, p, t);
+    issue();
     for (long long u = cb; u < ce; ++u) {
-        // keys in two halves of eight events (half the front end's registers)
-        uint32_t bin[EPT], key[EPT];
-        toa_bins<TL, EPT, 0>(a.toa, TL ? s_tree : a.toa.tree, t, bin);
-        pixel_half(std::integral_constant<int, 0>{}, bin, key);
-        pixel_half(std::integral_constant<int, EPT / 2>{}, bin, key);
+        uint32_t key[EPT];
+        finish(key);
         part_unit<E16>(s, P, a.pbits, emask, (int)(u & 1), key, own, pool_base, a.cap1, a.pages1, 0u, a.page_cnt,
-                       a.page_part, a.overflow, [&]() __attribute__((always_inline)) {
-                           if (u + 1 < ce) unit_load(a, s_ct, c0, u + 1, p, t);
-                       });
+                       a.page_part, a.overflow,
+                       // (unconditional: past the last unit, dropped events)
+                       [&]() __attribute__((always_inline)) { unit_load(a, s_ct, c0, u + 1, ce, p, t); },
+                       [&]() __attribute__((always_inline)) { issue(); });
     }
     part_finish(s, P, own, pool_base, a.cap1, a.page_cnt, a.page_part, a.list, a.rows1, blockIdx.x);
 }
@@ -548,6 +600,20 @@ __device__ __forceinline__ uint32_t item_page(const WideRows &rows, const uint32
 
 }  // namespace
 
+// The pages of an item, staged in LDS in chunks of kWidePagesLds: page id and
+// entry count of pages [base, base + m) (independent loads, one round trip).
+constexpr int kWidePagesLds = 1024;
+__device__ __forceinline__ void stage_pages(const WideRows &rows, const uint32_t *__restrict__ list,
+                                            const uint32_t *__restrict__ page_cnt, uint32_t r0, uint32_t nr,
+                                            uint32_t col, const uint32_t *s_pref, uint32_t base, uint32_t m,
+                                            uint32_t *s_pg, uint32_t *s_pc) {
+    for (uint32_t k = threadIdx.x; k < m; k += blockDim.x) {
+        const uint32_t page = item_page(rows, list, r0, nr, col, s_pref, base + k);
+        s_pg[k] = page;
+        s_pc[k] = page_cnt[page];
+    }
+}
+
 // ---------------------------------------------------------------------------
 // second pass (two-level form): one item of a band -> tile pages
 // ---------------------------------------------------------------------------
@@ -558,6 +624,8 @@ __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
     const int P = 1 << a.tpb_bits;
     const PartLds s = part_lds(sm, P);
     uint32_t *s_pref = sm + part_words(P);
+    uint32_t *s_pg = s_pref + kWideMaxRows + 1;
+    uint32_t *s_pc = s_pg + kWidePagesLds;
     __shared__ unsigned long long s_ev[16];
     const int tid = threadIdx.x;
     const uint32_t band = it.x, r0 = it.y, nr = it.z - it.y;
@@ -571,7 +639,10 @@ __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
     if (tid == 0) {
         unsigned long long e = 0;
         for (int i = 0; i < NT / 64; ++i) e += s_ev[i];
-        const unsigned long long need = (e + PAGE - 1) / PAGE + (unsigned long long)P + 1;
+        // entries in (first-pass pads included) + this pass's pads (<= 3 per
+        // partition and unit; a unit per 16 pages, one more per LDS chunk)
+        const unsigned long long units = (n_pages + NT / 64 - 1) / (NT / 64) + (n_pages + kWidePagesLds - 1) / kWidePagesLds;
+        const unsigned long long need = (e + 3ull * P * units + PAGE - 1) / PAGE + (unsigned long long)P + 1;
         const uint32_t base = atomicAdd(a.pool2_next, (uint32_t)(need < 0x7FFFFFFFull ? need : 0x7FFFFFFFull));
         uint32_t cap = (uint32_t)need;
         if ((unsigned long long)base + need > a.pool2_cap) {
@@ -587,40 +658,43 @@ __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
     const int lane = tid & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t *pages1 = reinterpret_cast<const uint32_t *>(a.pages1);
-    // unit u: pages 16u .. 16u + 15, wave wv takes page 16u + wv, lane 16
-    // consecutive entries
-    auto load = [&](uint32_t u, uint32_t (&key)[EPT]) __attribute__((always_inline)) {
-        const uint32_t k = u * (NT / 64) + wv;
-        uint32_t cnt = 0, page = 0;
-        if (k < n_pages) {
-            page = item_page(a.rows1, a.list, r0, nr, band, s_pref, k);
-            cnt = a.page_cnt[page];
-        }
-        const uint32_t e0 = (uint32_t)lane * EPT;
-        const uint4 *src = reinterpret_cast<const uint4 *>(pages1 + (size_t)page * PAGE + e0);
-#pragma unroll
-        for (int j = 0; j < EPT / 4; ++j) {
-            const uint4 v = e0 + 4u * j < cnt ? src[j] : make_uint4(kNone, kNone, kNone, kNone);
-            key[4 * j] = v.x;
-            key[4 * j + 1] = v.y;
-            key[4 * j + 2] = v.z;
-            key[4 * j + 3] = v.w;
-        }
-#pragma unroll
-        for (int e = 0; e < EPT; ++e)
-            if (e0 + (uint32_t)e >= cnt) key[e] = kNone;
-    };
     Owner own;
-    const uint32_t n_units = (n_pages + NT / 64 - 1) / (NT / 64);
     uint32_t key[EPT], nxt[EPT];
-    if (n_units) load(0, nxt);
-    for (uint32_t u = 0; u < n_units; ++u) {
+    uint32_t u = 0;  // units so far (parity)
+    for (uint32_t pb = 0; pb < n_pages; pb += kWidePagesLds) {
+        const uint32_t m = min((uint32_t)kWidePagesLds, n_pages - pb);
+        __syncthreads();  // the previous chunk's readers are done with s_pg / s_pc
+        stage_pages(a.rows1, a.list, a.page_cnt, r0, nr, band, s_pref, pb, m, s_pg, s_pc);
+        __syncthreads();
+        // unit: pages 16v .. 16v + 15 of the chunk, wave wv takes one, each
+        // lane 16 consecutive entries (4 x 16 bytes)
+        auto load = [&](uint32_t v, uint32_t (&k)[EPT]) __attribute__((always_inline)) {
+            const uint32_t j = v * (NT / 64) + wv;
+            const uint32_t cnt = j < m ? s_pc[j] : 0u;
+            const uint32_t e0 = (uint32_t)lane * EPT;
+            const uint4 *src = reinterpret_cast<const uint4 *>(pages1 + (size_t)(j < m ? s_pg[j] : 0u) * PAGE + e0);
 #pragma unroll
-        for (int e = 0; e < EPT; ++e) key[e] = nxt[e];
-        part_unit<true>(s, P, kWideTileBits, (1u << kWideTileBits) - 1u, (int)(u & 1), key, own, pool_base, cap,
-                        a.pages2, a.page0_2, a.page_cnt, a.page_part, a.overflow, [&]() __attribute__((always_inline)) {
-                            if (u + 1 < n_units) load(u + 1, nxt);
-                        });
+            for (int q = 0; q < EPT / 4; ++q) {
+                const uint4 x = e0 + 4u * q < cnt ? src[q] : make_uint4(kNone, kNone, kNone, kNone);
+                k[4 * q] = x.x;
+                k[4 * q + 1] = x.y;
+                k[4 * q + 2] = x.z;
+                k[4 * q + 3] = x.w;
+            }
+#pragma unroll
+            for (int e = 0; e < EPT; ++e)
+                if (e0 + (uint32_t)e >= cnt) k[e] = kNone;  // (pads are kNone already)
+        };
+        const uint32_t n_units = (m + NT / 64 - 1) / (NT / 64);
+        load(0, nxt);
+        for (uint32_t v = 0; v < n_units; ++v, ++u) {
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) key[e] = nxt[e];
+            part_unit<true>(s, P, kWideTileBits, (1u << kWideTileBits) - 1u, (int)(u & 1), key, own, pool_base, cap,
+                            a.pages2, a.page0_2, a.page_cnt, a.page_part, a.overflow,
+                            [&]() __attribute__((always_inline)) { load(v + 1, nxt); },
+                            []() {});
+        }
     }
     part_finish(s, P, own, pool_base, cap, a.page_cnt, a.page_part, a.list, a.rows2, blockIdx.x);
 }
@@ -629,17 +703,20 @@ __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
 // pass B: one item of a tile histogrammed in LDS
 // ---------------------------------------------------------------------------
 constexpr int kWideAccThreads = 1024;
+constexpr int kWideAccDepth = 4;  // pages in flight per wave
 __global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4 *__restrict__ items,
                                                                      const uint32_t *__restrict__ item_count,
                                                                      WideRows rows, const uint32_t *__restrict__ list,
                                                                      const uint32_t *__restrict__ page_cnt,
                                                                      const uint16_t *__restrict__ pages,
-                                                                     uint32_t page0, uint32_t colmask, uint32_t *__restrict__ hist,
-                                                                     long long n_bins) {
+                                                                     uint32_t page0, uint32_t colmask,
+                                                                     uint32_t *__restrict__ hist, long long n_bins) {
     constexpr int NB = 1 << kWideTileBits;
     constexpr int NW = kWideAccThreads / 64;
+    constexpr int D = kWideAccDepth;
     __shared__ __attribute__((aligned(16))) uint32_t s_tile[NB + 64];
     __shared__ uint32_t s_pref[kWideMaxRows + 1];
+    __shared__ uint32_t s_pg[kWidePagesLds], s_pc[kWidePagesLds];
     __shared__ uint32_t s_w[32];
     const uint32_t n_items = *item_count;
     const uint4 it = items[blockIdx.x];
@@ -653,32 +730,35 @@ __global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t e0 = (uint32_t)lane * 16u;
     const uint32_t dummy = NB + (uint32_t)lane;
-    auto fetch = [&](uint32_t k, uint4 &x, uint4 &y, uint32_t &cnt) __attribute__((always_inline)) {
-        cnt = 0;
-        x = y = make_uint4(0, 0, 0, 0);
-        if (k < n_pages) {
-            const uint32_t page = item_page(rows, list, r0, nr, col, s_pref, k);
-            cnt = page_cnt[page];
-            const uint4 *src = reinterpret_cast<const uint4 *>(pages + (size_t)(page - page0) * PAGE + e0);
-            x = src[0];
-            y = src[1];
-        }
-    };
-    uint4 a, b, na, nb;
-    uint32_t cnt, ncnt;
-    fetch(wv, a, b, cnt);
-    for (uint32_t k = wv; k < n_pages; k += NW) {
-        fetch(k + NW, na, nb, ncnt);  // the wave's next page in flight
-        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    for (uint32_t pb = 0; pb < n_pages; pb += kWidePagesLds) {
+        const uint32_t m = min((uint32_t)kWidePagesLds, n_pages - pb);
+        if (pb) __syncthreads();
+        stage_pages(rows, list, page_cnt, r0, nr, col, s_pref, pb, m, s_pg, s_pc);
+        __syncthreads();
+        // each wave D pages at a time: 2 x 16 bytes per lane and page
+        for (uint32_t k0 = wv; k0 < m; k0 += NW * D) {
+            uint4 x[D], y[D];
+            uint32_t c[D];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const uint32_t v = (w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu;
-            __hip_atomic_fetch_add(s_tile + (e0 + (uint32_t)q < cnt ? v : dummy), 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            for (int d = 0; d < D; ++d) {
+                const uint32_t k = k0 + (uint32_t)d * NW;
+                c[d] = k < m ? s_pc[k] : 0u;
+                const uint4 *src =
+                    reinterpret_cast<const uint4 *>(pages + (size_t)((k < m ? s_pg[k] : page0) - page0) * PAGE + e0);
+                x[d] = c[d] > e0 ? src[0] : make_uint4(0, 0, 0, 0);
+                y[d] = c[d] > e0 + 8u ? src[1] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const uint32_t wd[8] = {x[d].x, x[d].y, x[d].z, x[d].w, y[d].x, y[d].y, y[d].z, y[d].w};
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const uint32_t v = (wd[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu;
+                    __hip_atomic_fetch_add(s_tile + (e0 + (uint32_t)q < c[d] && v != kPad16 ? v : dummy), 1u,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
         }
-        a = na;
-        b = nb;
-        cnt = ncnt;
     }
     __syncthreads();
     const long long base = (long long)tile << kWideTileBits;
@@ -708,15 +788,13 @@ __global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4
 // launch wrappers
 // ---------------------------------------------------------------------------
 size_t wide_scatter_smem(const WideArgs &a) {
-    const size_t P4 = (size_t)align4(a.n_parts);
-    const size_t words = (size_t)UNIT + 2 * (P4 + 64) + 3 * P4 + 32 + 4 + (a.cbits ? (size_t)1 << a.cbits : 0) +
+    const size_t words = part_words(a.n_parts) + (a.cbits ? (size_t)1 << a.cbits : 0) +
                          (a.toa.lds ? (size_t)align4(a.toa.words) : 0);
     return 4 * words + sizeof(PixChunk) * kWideLdsChunks;
 }
 
 static size_t wide_split_smem(const WideArgs &a) {
-    const size_t P4 = (size_t)align4(1 << a.tpb_bits);
-    return 4 * ((size_t)UNIT + 2 * (P4 + 64) + 3 * P4 + 32 + 4 + kWideMaxRows + 1);
+    return 4 * (part_words(1 << a.tpb_bits) + kWideMaxRows + 1 + 2 * (size_t)kWidePagesLds);
 }
 
 hipError_t launch_wide_chunks(const WideArgs &a, hipStream_t st) {
