@@ -41,6 +41,24 @@ __device__ __forceinline__ uint4 g_ld(const uint4 *p) {  // (HIP's uint4 is a cl
     const v4u_t v = *(const __attribute__((address_space(1))) v4u_t *)p;
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
+// (the form with `at`: element i goes to *at(i), for two tables in one round)
+template <int R, typename T, typename F, typename A>
+__device__ __forceinline__ void lds_fill(T *, int n, F val, A at) {
+    const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
+    for (int b = 0; b < n; b += R * nt) {
+        T v[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int i = b + k * nt + tid;
+            v[k] = val(i < n ? i : n - 1);
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int i = b + k * nt + tid;
+            if (i < n) *at(i) = v[k];
+        }
+    }
+}
 template <int R, typename T, typename F>
 __device__ __forceinline__ void lds_fill(T *dst, int n, F val) {
     const int nt = (int)blockDim.x, tid = (int)threadIdx.x;

@@ -1439,10 +1439,11 @@ int setup_wide(lde_handle *h) {
     // pixel table: 2^13 slots (the whole LUT when it fits in half of that),
     // tags of 9 bits; smaller when the first pass's LDS needs the room
     auto bits = [](long long n) { int b = 0; while ((1LL << b) < n) ++b; return b; };
-    int cb = (int)std::max<long long>(0, std::min<long long>(14, env_ll("LDE_WIDE_CACHE_BITS", 13)));
-    if (cb > 0 && (1LL << cb) >= 2 * h->L) cb = bits(h->L);
-    while (cb > 0 && ((h->L - 1) >> cb) > 511) ++cb;
-    if (cb > 16) cb = 0;
+    int cb = (int)std::max<long long>(0, std::min<long long>(lde::kWideMaxCacheBits,
+                                                             env_ll("LDE_WIDE_CACHE_BITS", lde::kWideMaxCacheBits)));
+    // (at least 4 slots: the table is copied into LDS in 16-byte units)
+    if (cb > 0 && (1LL << cb) >= 2 * h->L) cb = std::max(2, bits(h->L));
+    if (cb > 0 && ((h->L - 1) >> cb) > 511) cb = 0;  // tags of 9 bits: beyond 2^22 pixels, no table
     lde::WideArgs a{};
     a.n_parts = h->wide_parts;
     a.toa = h->wtoa;
@@ -1480,7 +1481,14 @@ int setup_wide(lde_handle *h) {
 
 // WIDE: key, partition into pages, (second level), tile pass B
 int bin_wide(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunks, long long total, int replica) {
-    if (int rc = upload_segments(h, sd)) return rc;
+    // up to kKargSegs messages reach the chunk-table kernel as kernel
+    // arguments (no descriptor upload in front of it)
+    const bool karg = (long long)sd.size() <= lde::kKargSegs;
+    if (karg) {
+        if (int rc = ensure_segs_cap(h, (long long)sd.size())) return rc;
+    } else if (int rc = upload_segments(h, sd)) {
+        return rc;
+    }
     const int P = h->wide_parts;
     const long long units = (chunks + 1) / 2;
     const int grid1 = (int)std::min<long long>(units, std::min<long long>(h->cus, lde::kWideMaxRows));
@@ -1579,7 +1587,7 @@ int bin_wide(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunk
     a.hist = h->d_win32;
     a.n_bins = h->nbins;
     a.grid1 = grid1;
-    HIPCALL(h, lde::launch_wide_chunks(a, h->stream));
+    HIPCALL(h, lde::launch_wide_chunks(a, karg ? sd.data() : nullptr, h->stream));
     int &uses = h->wide_uses[(size_t)replica];
     if (h->wide_cbits && (uses < 0 || uses >= h->hot_refresh)) {
         Timed tm(h, LDE_K_SPLIT_AUX);
@@ -2320,7 +2328,11 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
         // bounds the hot rows
         auto bits = [](long long n) { int b = 0; while ((1LL << b) < n) ++b; return b; };
         int cbits = (int)std::max<long long>(0, std::min<long long>(16, env_ll("LDE_PIXEL_CACHE_BITS", 13)));
-        if ((1LL << cbits) >= 2 * h->L) cbits = std::max(0, bits(h->L));  // whole LUT fits
+        // whole LUT fits; at least 4 slots, as the sieve copies the table and
+        // the TOA words in 16-byte units from offset C (a 2-pixel
+        // view had C = 2, so no table word was copied and the TOA words
+        // landed at the table's offset)
+        if ((1LL << cbits) >= 2 * h->L) cbits = std::max(2, bits(h->L));
         std::vector<uint32_t> tt;
         int tsh = 0;
         uint32_t tcap = 0;

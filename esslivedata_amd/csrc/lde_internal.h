@@ -453,6 +453,7 @@ constexpr int kWideMaxParts = 1024;       // partitions of one pass (one owner t
 constexpr int kWideMaxBands = 512;        // first-level bands of the two-level form
 constexpr int kWideMaxRows = 1024;        // rows per work item
 constexpr int kWideTreeLds = 6144;        // TOA tree words kept in LDS (larger trees: global)
+constexpr int kWideMaxCacheBits = 13;     // pixel table slots (2^13 words of LDS)
 constexpr int kWideLdsChunks = 128;
 constexpr int kWideSample = 64;           // chunks sampled per pixel-table selection
 
@@ -521,8 +522,10 @@ struct WideArgs {
     int grid1;                   // first-pass blocks
 };
 
-// the batch's chunk table; call before launch_wide_table / launch_wide
-hipError_t launch_wide_chunks(const WideArgs &a, hipStream_t st);
+// the batch's chunk table; call before launch_wide_table / launch_wide.
+// host_segs (the batch's descriptors on the host): passed as kernel
+// arguments when they fit kKargSegs, else a.segs (device) is read
+hipError_t launch_wide_chunks(const WideArgs &a, const SegDesc *host_segs, hipStream_t st);
 // pixel-table selection for one replica: sample the batch, pick the most
 // frequent pixel of every slot (pix_cnt zeroed here)
 hipError_t launch_wide_table(const WideArgs &a, const void *lut_rep, uint32_t *pix_cnt, uint32_t *tab,

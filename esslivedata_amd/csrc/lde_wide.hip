@@ -100,9 +100,13 @@ __device__ __forceinline__ void toa_bins(const WideToa &tp, const uint32_t *tree
         for (int e = 0; e < N; ++e) any |= (w[e] & 0xFFFFu) == kLeafNone;
         if (!__builtin_amdgcn_ballot_w64(any)) break;
         const int sh = max(0, tp.sh0 - lv * tp.fb);  // (nodes narrower than the fan-out: width-1 children)
+        // (branch-free: leaves read word 0 and keep their word)
 #pragma unroll
-        for (int e = 0; e < N; ++e)
-            if ((w[e] & 0xFFFFu) == kLeafNone) w[e] = tree_word<TL>(tree, (w[e] >> 16) + ((dc[e] >> sh) & fmask));
+        for (int e = 0; e < N; ++e) {
+            const bool in = (w[e] & 0xFFFFu) == kLeafNone;
+            const uint32_t nw = tree_word<TL>(tree, in ? (w[e] >> 16) + ((dc[e] >> sh) & fmask) : 0u);
+            w[e] = in ? nw : w[e];
+        }
     }
     // leaf: bin at its start + (the offset inside the ROOT bucket reached the
     // one threshold inside the leaf)
@@ -176,10 +180,16 @@ struct PartLds {
     uint32_t *stg, *cnt0, *cnt1, *offw, *wcur, *newp, *w, *pool;
 };
 
-__host__ __device__ inline size_t part_words(int P) {
-    const size_t P4 = (size_t)align4(P);
-    return (size_t)UNIT + 3 * P4 + 2 * (P4 + 64) + 3 * P4 + 32 + 4;
+__host__ __device__ constexpr size_t part_words(int P) {
+    return (size_t)UNIT + 3 * (size_t)align4(P) + 2 * ((size_t)align4(P) + 64) + 3 * (size_t)align4(P) + 32 + 4;
 }
+constexpr int kWideMaxTpb = 256;  // tiles per band (second pass partitions)
+// first pass: partition layout | pixel table | TOA tree | chunk table
+constexpr size_t kWideScatterWords = part_words(kWideMaxParts) + ((size_t)1 << kWideMaxCacheBits) + kWideTreeLds +
+                                     sizeof(PixChunk) / 4 * kWideLdsChunks;
+static_assert(kWideScatterWords * 4 <= 160 * 1024, "first pass LDS");
+// second pass: partition layout | item row prefix | staged page ids, counts
+constexpr size_t kWideSplitWords = part_words(kWideMaxTpb) + kWideMaxRows + 1 + 2 * 1024;
 
 __device__ __forceinline__ PartLds part_lds(uint32_t *sm, int P) {
     const uint32_t P4 = (uint32_t)align4(P);
@@ -208,7 +218,7 @@ struct Owner {  // registers of the owner thread of one partition
 template <bool E16, typename NEXT, typename MID>
 __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, uint32_t emask, int parity,
                                           const uint32_t (&key)[EPT], Owner &own, uint32_t pool_base,
-                                          uint32_t cap, void *pages, uint32_t page0, uint32_t *__restrict__ page_cnt,
+                                          uint32_t cap, __amdgpu_buffer_rsrc_t pool, uint32_t *__restrict__ page_cnt,
                                           uint32_t *__restrict__ page_part, uint32_t *overflow, NEXT next, MID mid) {
     const int tid = threadIdx.x;
     const uint32_t P4 = (uint32_t)align4(P);
@@ -228,8 +238,24 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
         v = (n + 3u) & ~3u;
         cnt_next[tid] = 0;
     }
-    uint32_t total;
-    const uint32_t off = block_exclusive_scan(v, s.w, &total);
+    // exclusive scan of the padded runs with one barrier: every wave adds
+    // the totals of the waves before it itself (16 broadcast LDS reads)
+    const uint32_t inc = wave_inclusive_scan(v);
+    const int wid = tid >> 6;
+    if ((tid & 63) == 63) s.w[wid] = inc;
+    __syncthreads();
+    // lanes 0..15 hold the wave totals; their inclusive scan gives this
+    // wave's base (lane wid - 1) and the unit total (lane 15)
+    const int lane = tid & 63;
+    uint32_t x = lane < NT / 64 ? s.w[lane] : 0u;
+#pragma unroll
+    for (int d = 1; d < NT / 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)x, NT / 64 - 1);
+    const uint32_t wbase = wid ? (uint32_t)__builtin_amdgcn_readlane((int)x, wid - 1) : 0u;
+    const uint32_t off = wbase + inc - v;
     if (tid < P && n > 0) {
         for (uint32_t j = n; j < v; ++j) s.stg[off + j] = kNone;  // the run's pads
         // the run occupies positions [fill, fill + v) of the partition's
@@ -276,9 +302,15 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
         own.ev += v;
     }
     __syncthreads();
+    // (branch-free: entries without a key store into the lane's dummy word
+    // of the other count array, which is never read)
 #pragma unroll
-    for (int e = 0; e < EPT; ++e)
-        if (key[e] != kNone) s.stg[(s.offw[key[e] >> pbits] & 0xFFFFu) + rank[e]] = key[e];
+    for (int e = 0; e < EPT; ++e) {
+        const bool ok = key[e] != kNone;
+        const uint32_t o = s.offw[ok ? key[e] >> pbits : 0u] & 0xFFFFu;
+        uint32_t *dst = ok ? s.stg + o + rank[e] : cnt_next + dummy;
+        *dst = key[e];
+    }
     __syncthreads();
     mid();
 #pragma unroll 1
@@ -289,16 +321,19 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
         const uint32_t x = (ow >> 16) + g - (ow & 0xFFFFu);
         const uint32_t np = s.newp[part], wc = s.wcur[part];
         const uint32_t page = x < (uint32_t)PAGE ? wc : np + (x >> PB) - 1u;
-        if (x < (uint32_t)PAGE ? wc == kNone : np == kNone) continue;  // pool overflow (flagged)
-        const size_t at = (size_t)(page - page0) * PAGE + (x & (PAGE - 1));
+        const bool lost = x < (uint32_t)PAGE ? wc == kNone : np == kNone;  // pool overflow (flagged)
+        // byte offset inside the row's pool (a store out of range is dropped)
+        const uint32_t at = ((page - pool_base) << PB) + (x & (PAGE - 1));
+        const int boff = lost ? (int)kOOB : (int)(at << (E16 ? 1 : 2));
         if (E16) {
             auto e16 = [&](uint32_t k) { return k == kNone ? kPad16 : (k & emask); };
-            *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(pages) + at) =
-                make_uint2(e16(k4.x) | (e16(k4.y) << 16), e16(k4.z) | (e16(k4.w) << 16));
+            typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(v2u{e16(k4.x) | (e16(k4.y) << 16), e16(k4.z) | (e16(k4.w) << 16)},
+                                                  pool, boff, 0, 0);
         } else {
             auto e32 = [&](uint32_t k) { return k == kNone ? kNone : (k & emask); };
-            *reinterpret_cast<uint4 *>(reinterpret_cast<uint32_t *>(pages) + at) =
-                make_uint4(e32(k4.x), e32(k4.y), e32(k4.z), e32(k4.w));
+            __builtin_amdgcn_raw_buffer_store_b128(v4u{e32(k4.x), e32(k4.y), e32(k4.z), e32(k4.w)}, pool, boff,
+                                                   0, 0);
         }
     }
 }
@@ -338,19 +373,30 @@ __device__ __forceinline__ void part_finish(const PartLds &s, int P, const Owner
 // ---------------------------------------------------------------------------
 // chunk table (+ the counters of this batch's passes)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_wide_chunks(WideArgs a, PixChunk *__restrict__ ctab) {
+// KARG: the messages come as kernel arguments (at most kKargSegs: a batch of
+// 14 pulses), so no descriptor upload precedes the launch
+template <bool KARG>
+__global__ __launch_bounds__(256) void k_wide_chunks(WideArgs a, SegKarg sk, PixChunk *__restrict__ ctab) {
     const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
     if (c == 0) {
         a.counters[0] = a.counters[1] = 0u;
         *a.pool2_next = 0u;
     }
     if (c >= a.n_chunks) return;
-    int lo = 0, hi = a.n_segs - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (a.segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+    SegDesc sd;
+    if (KARG) {  // last message with chunk0 <= c (static indices: scalar kernarg loads)
+        sd = sk.s[0];
+#pragma unroll
+        for (int i = 1; i < kKargSegs; ++i)
+            if (i < a.n_segs && sk.s[i].chunk0 <= c) sd = sk.s[i];
+    } else {
+        int lo = 0, hi = a.n_segs - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (a.segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+        }
+        sd = a.segs[lo];
     }
-    const SegDesc sd = a.segs[lo];
     const long long base = (c - sd.chunk0) * kChunk;
     const long long left = sd.n - base;
     PixChunk ch;
@@ -430,23 +476,27 @@ __global__ __launch_bounds__(256) void k_wide_table(WideArgs a, const void *__re
 // ---------------------------------------------------------------------------
 template <bool L16, bool TL, bool E16>
 __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    // static layout for the largest partition count and table, so every LDS
+    // address is a constant (fewer live scalar registers in the loop)
+    __shared__ __attribute__((aligned(16))) uint32_t sm[kWideScatterWords];
     const int P = a.n_parts;
-    const PartLds s = part_lds(sm, P);
+    const PartLds s = part_lds(sm, kWideMaxParts);
     const uint32_t C = a.cbits ? 1u << a.cbits : 0u;
-    uint32_t *s_tab = sm + part_words(P);
-    uint32_t *s_tree = s_tab + C;
+    uint32_t *s_tab = sm + part_words(kWideMaxParts);
+    uint32_t *s_tree = s_tab + (1u << kWideMaxCacheBits);
     const uint32_t tw = TL ? (uint32_t)align4(a.toa.words) : 0u;
-    PixChunk *s_ctab = reinterpret_cast<PixChunk *>(s_tree + tw);
+    PixChunk *s_ctab = reinterpret_cast<PixChunk *>(s_tree + kWideTreeLds);
     const int tid = threadIdx.x;
-    {  // pixel table and TOA tree: every load of a thread issued before its stores
+    {  // pixel table and TOA tree, each into its own slot: every load of a
+       // thread issued before its stores
         const uint4 *pt = reinterpret_cast<const uint4 *>(a.pix_tab);
         const uint4 *tt = reinterpret_cast<const uint4 *>(a.toa.tree);
-        const int c4 = (int)(C / 4u);
-        lds_fill<4>(reinterpret_cast<uint4 *>(s_tab), c4 + (int)(tw / 4u),
-                    [&](int i) { return g_ld(i < c4 ? pt + i : tt + (i - c4)); });
+        const int c4 = (int)(C / 4u), t4 = (int)(tw / 4u);
+        lds_fill<4>(reinterpret_cast<uint4 *>(s_tab), c4 + t4, [&](int i) {
+            return g_ld(i < c4 ? pt + i : tt + (i - c4));
+        }, [&](int i) { return reinterpret_cast<uint4 *>(i < c4 ? s_tab + 4 * i : s_tree + 4 * (i - c4)); });
     }
-    for (int i = tid; i < 2 * (align4(P) + 64); i += NT) s.cnt0[i] = 0;
+    for (int i = tid; i < 2 * (kWideMaxParts + 64); i += NT) s.cnt0[i] = 0;
     if (tid == 0) s.pool[0] = 0;
     const long long n_units = (a.n_chunks + 1) / 2;
     const long long cb = (long long)blockIdx.x * n_units / gridDim.x;
@@ -458,6 +508,10 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
     __syncthreads();
     const PixChunk *s_ct = fit ? s_ctab : nullptr;
     const uint32_t pool_base = blockIdx.x * a.cap1;
+    // the block's pool (its pages only), as a buffer: 32-bit store offsets
+    const __amdgpu_buffer_rsrc_t pool = make_rsrc(
+        reinterpret_cast<unsigned char *>(a.pages1) + (size_t)pool_base * PAGE * (E16 ? 2 : 4),
+        a.cap1 * (uint32_t)PAGE * (E16 ? 2u : 4u));
     const uint32_t cmask = C ? C - 1u : 0u;
     const uint32_t lut_bytes = a.L * (L16 ? 2u : 4u);
     const __amdgpu_buffer_rsrc_t lut = make_rsrc(a.lut, lut_bytes);
@@ -511,7 +565,7 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
     for (long long u = cb; u < ce; ++u) {
         uint32_t key[EPT];
         finish(key);
-        part_unit<E16>(s, P, a.pbits, emask, (int)(u & 1), key, own, pool_base, a.cap1, a.pages1, 0u, a.page_cnt,
+        part_unit<E16>(s, P, a.pbits, emask, (int)(u & 1), key, own, pool_base, a.cap1, pool, a.page_cnt,
                        a.page_part, a.overflow,
                        // (unconditional: past the last unit, dropped events)
                        [&]() __attribute__((always_inline)) { unit_load(a, s_ct, c0, u + 1, ce, p, t); },
@@ -618,18 +672,18 @@ __device__ __forceinline__ void stage_pages(const WideRows &rows, const uint32_t
 // second pass (two-level form): one item of a band -> tile pages
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    __shared__ __attribute__((aligned(16))) uint32_t sm[kWideSplitWords];
     if (blockIdx.x >= a.counters[0]) return;
     const uint4 it = a.items1[blockIdx.x];
     const int P = 1 << a.tpb_bits;
-    const PartLds s = part_lds(sm, P);
-    uint32_t *s_pref = sm + part_words(P);
+    const PartLds s = part_lds(sm, kWideMaxTpb);
+    uint32_t *s_pref = sm + part_words(kWideMaxTpb);
     uint32_t *s_pg = s_pref + kWideMaxRows + 1;
     uint32_t *s_pc = s_pg + kWidePagesLds;
     __shared__ unsigned long long s_ev[16];
     const int tid = threadIdx.x;
     const uint32_t band = it.x, r0 = it.y, nr = it.z - it.y;
-    for (int i = tid; i < 2 * (align4(P) + 64); i += NT) s.cnt0[i] = 0;
+    for (int i = tid; i < 2 * (kWideMaxTpb + 64); i += NT) s.cnt0[i] = 0;
     // the item's entries size its pool (one allocation per item)
     unsigned long long ev = (uint32_t)tid < nr ? a.rows1.ev[(size_t)(r0 + tid) * a.rows1.ncols + band] : 0u;
 #pragma unroll
@@ -655,6 +709,8 @@ __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
     }
     __syncthreads();
     const uint32_t pool_base = s.pool[1], cap = s.pool[2];
+    const __amdgpu_buffer_rsrc_t pool = make_rsrc(
+        reinterpret_cast<unsigned char *>(a.pages2) + (size_t)(pool_base - a.page0_2) * PAGE * 2, cap * (uint32_t)PAGE * 2u);
     const int lane = tid & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t *pages1 = reinterpret_cast<const uint32_t *>(a.pages1);
@@ -691,7 +747,7 @@ __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
 #pragma unroll
             for (int e = 0; e < EPT; ++e) key[e] = nxt[e];
             part_unit<true>(s, P, kWideTileBits, (1u << kWideTileBits) - 1u, (int)(u & 1), key, own, pool_base, cap,
-                            a.pages2, a.page0_2, a.page_cnt, a.page_part, a.overflow,
+                            pool, a.page_cnt, a.page_part, a.overflow,
                             [&]() __attribute__((always_inline)) { load(v + 1, nxt); },
                             []() {});
         }
@@ -788,18 +844,23 @@ __global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4
 // launch wrappers
 // ---------------------------------------------------------------------------
 size_t wide_scatter_smem(const WideArgs &a) {
-    const size_t words = part_words(a.n_parts) + (a.cbits ? (size_t)1 << a.cbits : 0) +
-                         (a.toa.lds ? (size_t)align4(a.toa.words) : 0);
-    return 4 * words + sizeof(PixChunk) * kWideLdsChunks;
+    // (static layout: fits when the table and the tree fit their slots)
+    if (a.cbits > kWideMaxCacheBits || a.n_parts > kWideMaxParts || (a.toa.lds && a.toa.words > kWideTreeLds))
+        return 1u << 30;
+    return kWideScatterWords * 4;
 }
 
-static size_t wide_split_smem(const WideArgs &a) {
-    return 4 * (part_words(1 << a.tpb_bits) + kWideMaxRows + 1 + 2 * (size_t)kWidePagesLds);
-}
-
-hipError_t launch_wide_chunks(const WideArgs &a, hipStream_t st) {
+hipError_t launch_wide_chunks(const WideArgs &a, const SegDesc *host_segs, hipStream_t st) {
     const unsigned g = (unsigned)((a.n_chunks + 255) / 256);
-    hipLaunchKernelGGL(k_wide_chunks, dim3(g > 0 ? g : 1), dim3(256), 0, st, a, const_cast<PixChunk *>(a.ctab));
+    SegKarg sk{};
+    if (host_segs && a.n_segs <= kKargSegs) {
+        for (int i = 0; i < a.n_segs; ++i) sk.s[i] = host_segs[i];
+        hipLaunchKernelGGL(k_wide_chunks<true>, dim3(g > 0 ? g : 1), dim3(256), 0, st, a, sk,
+                           const_cast<PixChunk *>(a.ctab));
+    } else {
+        hipLaunchKernelGGL(k_wide_chunks<false>, dim3(g > 0 ? g : 1), dim3(256), 0, st, a, sk,
+                           const_cast<PixChunk *>(a.ctab));
+    }
     return hipGetLastError();
 }
 
@@ -820,11 +881,8 @@ hipError_t launch_wide_table(const WideArgs &a, const void *lut_rep, uint32_t *p
 
 template <bool L16, bool TL, bool E16>
 static hipError_t launch_scatter_t(const WideArgs &a, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
-    const size_t sm = wide_scatter_smem(a);
-    if (sm > 160 * 1024) return hipErrorInvalidValue;
-    (void)hipFuncSetAttribute((const void *)k_wide_scatter<L16, TL, E16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sm);
-    hipExtLaunchKernelGGL((k_wide_scatter<L16, TL, E16>), dim3(a.grid1), dim3(NT), sm, st, start, stop, 0, a);
+    if (wide_scatter_smem(a) > 160 * 1024) return hipErrorInvalidValue;
+    hipExtLaunchKernelGGL((k_wide_scatter<L16, TL, E16>), dim3(a.grid1), dim3(NT), 0, st, start, stop, 0, a);
     return hipGetLastError();
 }
 
@@ -859,9 +917,8 @@ hipError_t launch_wide(const WideArgs &a, hipStream_t st, hipEvent_t start, hipE
         hipLaunchKernelGGL(k_wide_plan, dim3(a.n_parts), dim3(256), 0, st, a.rows1, a.grid1,
                            (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.max_items1,
                            a.band_items, a.overflow);
-        const size_t sm2 = wide_split_smem(a);
-        (void)hipFuncSetAttribute((const void *)k_wide_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm2);
-        hipLaunchKernelGGL(k_wide_split, dim3(a.max_items1), dim3(NT), sm2, st, a);
+        if (a.tpb_bits > 8) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_wide_split, dim3(a.max_items1), dim3(NT), 0, st, a);
         hipLaunchKernelGGL(k_wide_plan, dim3(a.n_tiles), dim3(256), 0, st, a.rows2, 0,
                            (const uint2 *)a.band_items, a.tpb_bits, a.item_max2, a.items2,
                            const_cast<uint32_t *>(cnt2), a.max_items2, (uint2 *)nullptr, a.overflow);

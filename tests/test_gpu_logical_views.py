@@ -140,10 +140,10 @@ def test_dream_logical_view_headline_bit_exact(dream_steps, view_name, strategy)
         assert out['current'].dims == wf.view.screen_dims
     info = wf.engine.info()
     if strategy != 'auto':
-        # forced strategies may fall back (SPLIT -> PAGED without a sieve
-        # encoding, tiled strategies -> ATOMIC without tiles), never silently
-        # to something else
-        assert info['last_strategy'] in (strategy, 'paged', 'atomic')
+        # forced strategies may fall back (SPLIT -> WIDE / PAGED without a
+        # sieve encoding, tiled strategies -> ATOMIC without tiles), never
+        # silently to something else
+        assert info['last_strategy'] in (strategy, 'wide', 'paged', 'atomic')
     print(f'\n[{view_name} {strategy}] last_strategy={info["last_strategy"]} '
           f'accumulate+read {1e3 * min(times):.2f} ms')
     if view_name == 'mantle_front_layer':

@@ -11,7 +11,7 @@ from oracle import scipp_semantics as ora
 
 pytestmark = pytest.mark.gpu
 
-STRATEGIES = ['atomic', 'partition', 'paged', 'split', 'pixel']
+STRATEGIES = ['atomic', 'partition', 'paged', 'split', 'pixel', 'wide']
 
 # internal kernel variants that must all be bit-identical
 VARIANTS = [
@@ -172,10 +172,10 @@ def test_dream_mantle_geometric_skewed(strategy, variant, knobs):
     res = eng.finalize(hists=True)
     exp = o.finalize()
     # PIXEL needs footprints that fit LDS: the mantle's 2048-pixel ranges span
-    # two arc columns of 320 screens, so it falls back to PAGED here; so does
+    # two arc columns of 320 screens, so it falls back to WIDE here; so does
     # SPLIT on the general TOA layout (the sieve bins through the fast one)
     fallback = strategy == 'pixel' or (strategy == 'split' and 'LDE_TOA_GENERAL' in VARIANTS[variant])
-    assert eng.info()['last_strategy'] == ('paged' if fallback else strategy)
+    assert eng.info()['last_strategy'] == ('wide' if fallback else strategy)
     np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
     np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
     np.testing.assert_array_equal(res.current_image.reshape(80, 320), exp['current'])
@@ -812,7 +812,7 @@ def test_finalize_images_written_in_place_are_never_reused_while_held():
     eng.close()
 
 
-@pytest.mark.parametrize('strategy', ['pixel', 'paged'])
+@pytest.mark.parametrize('strategy', ['pixel', 'paged', 'wide'])
 def test_loki_pixel_ranges_multi_replica_and_move(strategy):
     """PIXEL (pixel-range partition, LUT slice in LDS) on LOKI bank 0 with
     five replicas, unknown ids, TOAs outside the edges, misaligned and empty

@@ -15,7 +15,7 @@ from oracle import scipp_semantics as ora
 
 pytestmark = pytest.mark.gpu
 
-STRATEGIES = ['atomic', 'partition', 'paged', 'split', 'pixel']
+STRATEGIES = ['atomic', 'partition', 'paged', 'split', 'pixel', 'wide']
 
 
 @pytest.fixture(scope='module', autouse=True)
@@ -81,8 +81,8 @@ def test_dream_wavelength_matches_oracle(strategy, scale, table_min):
         o.accumulate(pid, toa)
     res = eng.finalize(hists=True)
     exp = o.finalize()
-    # PIXEL needs footprints that fit LDS; the mantle's do not (PAGED runs)
-    assert eng.info()['last_strategy'] == (strategy if strategy != 'pixel' else 'paged')
+    # PIXEL needs footprints that fit LDS; the mantle's do not (WIDE runs)
+    assert eng.info()['last_strategy'] == (strategy if strategy != 'pixel' else 'wide')
     assert exp['histogram_cumulative'].sum() > 1_000_000  # most events binned
     np.testing.assert_array_equal(res.current_hist, exp['histogram_current'])
     np.testing.assert_array_equal(res.cumulative_hist, exp['histogram_cumulative'])
@@ -252,7 +252,7 @@ def test_monitor_wavelength_mode(unit):
     assert float(out['counts_total'].values) == exp.sum()
 
 
-@pytest.mark.parametrize('strategy', ['atomic', 'split'])
+@pytest.mark.parametrize('strategy', ['atomic', 'split', 'wide'])
 @pytest.mark.parametrize('kind', ['duplicates', 'many_bins'])
 def test_coordinate_bins_for_unusual_edges(kind, strategy):
     """Edges with empty (repeated) bins, and 20000 bins (edges too large for
