@@ -170,6 +170,24 @@ def cpu_baseline(inst, ps, view, pid_h, toa_h, replica, gpu_hist, seconds: float
             ref_total = int(ref.sum())
         done += n
         k += 1
+    capped = {'value': done / t_total, 'cores': c.threads_used, 'passes': k, 'seconds': t_total}
+    # the same restatement on every CPU this process may run on (the
+    # reference's scipp/TBB kernels and job pool use all host cores,
+    # core/job_manager.py:304-306); the harness's OMP_NUM_THREADS share above
+    every = None
+    if visible > c.threads_used:
+        ca = c_oracle.CDetectorView(inst.detector_number, ps, view.n_screen, inst.edges.edges_ns(),
+                                    threads=visible)
+        done_a, t_a, k_a = 0, 0.0, 0
+        while (t_a < seconds / 2 and k_a < 50) or k_a == 0:
+            t0 = time.perf_counter()
+            ca.accumulate(pid_h, toa_h, replica)
+            t_a += time.perf_counter() - t0
+            done_a += n
+            k_a += 1
+        every = {'value': done_a / t_a, 'cores': ca.threads_used, 'passes': k_a, 'seconds': t_a}
+        del ca
+    main = every if every is not None and every['value'] > capped['value'] else capped
     m = min(n, 4_000_000)
     o = ora.OracleDetectorView(
         detector_number=inst.detector_number, pixel_screen=ps,
@@ -178,14 +196,19 @@ def cpu_baseline(inst, ps, view, pid_h, toa_h, replica, gpu_hist, seconds: float
     o.batch_histogram(pid_h[:m], toa_h[:m], replica)
     t_np = time.perf_counter() - t0
     return {
-        'value': done / t_total,
+        'value': main['value'],
         'unit': 'events/s',
-        'cores': c.threads_used,
+        'cores': main['cores'],
         'cpus_visible': visible,
         'kind': 'port',
-        'sample': f'{k} passes over the bench step batch ({n} events, replica {replica}) through '
-        f'oracle/binning_ref.c with {c.threads_used} OpenMP threads, {t_total:.1f} s; NumPy oracle '
-        f'(1 core) on {m} events of it: {m / t_np:.3e} events/s',
+        'sample': f'passes over the bench step batch ({n} events, replica {replica}) through '
+        f'oracle/binning_ref.c: {capped["passes"]} with {capped["cores"]} OpenMP threads (the harness '
+        f'share, OMP_NUM_THREADS) in {capped["seconds"]:.1f} s'
+        + (f', {every["passes"]} with {every["cores"]} threads (every visible CPU) in {every["seconds"]:.1f} s'
+           if every else '')
+        + f'; value = the faster; NumPy oracle (1 core) on {m} events of it: {m / t_np:.3e} events/s',
+        'share_threads': capped,
+        'all_visible_threads': every,
         'numpy_1core': m / t_np,
         'parity': {'events': n, 'replica': replica, 'bit_exact': bit_exact,
                    'oracle_total': ref_total, 'gpu_total': int(gpu_hist.sum())},

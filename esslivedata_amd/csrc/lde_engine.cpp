@@ -333,7 +333,7 @@ long long env_ll(const char *name, long long dflt) {
 int check_knobs() {
 #ifndef LDE_DIAGNOSTICS
     static const char *const diag[] = {"LDE_ABLATE", "LDE_SIEVE_ABLATE", "LDE_COLD_SORT_ABLATE",
-                                       "LDE_PIX_ABLATE", "LDE_KEY_ABLATE"};
+                                       "LDE_PIX_ABLATE", "LDE_KEY_ABLATE", "LDE_WIDE_ABLATE"};
     for (const char *n : diag)
         if (const char *v = std::getenv(n); v && std::atoll(v) != 0)
             return fail(nullptr, LDE_EINVAL,
@@ -651,15 +651,22 @@ bool build_wide_tree(const std::vector<double> &edges, int T, std::vector<uint32
     for (int i = 0; i <= T; ++i) r[(size_t)i] = thr[(size_t)i] - lo;
     size_t best = ~(size_t)0;
     int bsh = -1, bfb = 0, bdepth = 0;
+    const bool shallow = env_ll("LDE_WIDE_TREE_SHALLOW", 1) != 0;  // (diagnostics: 0 = fewest words)
     for (int sh0 = 15; sh0 >= 0; --sh0) {
         if (((span + (1LL << sh0) - 1) >> sh0) > 0xFFFF) break;
         for (int fb = 2; fb <= 4; ++fb) {
             WideTreeBuilder b(r, T, sh0, fb);
             if (!b.build(span)) continue;
             const size_t n = b.words.size();
-            // fewest words, LDS-sized trees first; then the shallower
+            // LDS-sized trees first; among those the shallowest (every level
+            // below the root is one more dependent LDS read for the waves
+            // whose events reach it: DREAM's 1000 log bins, 20 % of the
+            // events in three narrow hot bins, took a second level in every
+            // wave), then the fewest words; trees too large for LDS: the
+            // fewest words
             const bool fits = n <= (size_t)lde::kWideTreeLds, bfits = best <= (size_t)lde::kWideTreeLds;
-            if (bsh < 0 || (fits && !bfits) || (fits == bfits && (n < best || (n == best && b.depth < bdepth)))) {
+            const bool better = fits && shallow ? (b.depth < bdepth || (b.depth == bdepth && n < best)) : n < best;
+            if (bsh < 0 || (fits && !bfits) || (fits == bfits && better)) {
                 best = n;
                 bsh = sh0;
                 bfb = fb;
@@ -1587,6 +1594,16 @@ int bin_wide(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunk
     a.hist = h->d_win32;
     a.n_bins = h->nbins;
     a.grid1 = grid1;
+#ifdef LDE_DIAGNOSTICS
+    a.ablate = (int)env_ll("LDE_WIDE_ABLATE", 0);
+#endif
+    // an integer view's u32 window is all zero until its first batch after
+    // a finalize / clear (both zero it; win_events counts what this window's
+    // earlier pieces added): pass B then stores its tiles without reading them
+    a.wzero = (h->out_dtype != LDE_F32 && !h->window_has_data && h->win_events == 0 && !h->f32_pending &&
+               env_ll("LDE_WIDE_WZERO", 1) != 0)
+                  ? 1
+                  : 0;
     HIPCALL(h, lde::launch_wide_chunks(a, karg ? sd.data() : nullptr, h->stream));
     int &uses = h->wide_uses[(size_t)replica];
     if (h->wide_cbits && (uses < 0 || uses >= h->hot_refresh)) {

@@ -520,6 +520,8 @@ struct WideArgs {
     uint32_t *hist;              // the window
     long long n_bins;
     int grid1;                   // first-pass blocks
+    int ablate = 0;              // LDE_WIDE_ABLATE (diagnostics build): first-pass timing ablations
+    int wzero = 0;               // 1: the window is all zero before this batch (pass B stores, reads nothing)
 };
 
 // the batch's chunk table; call before launch_wide_table / launch_wide.

@@ -177,7 +177,9 @@ __device__ __forceinline__ void unit_load(const WideArgs &a, const PixChunk *s_c
 constexpr uint32_t kPad16 = 0xFFFFu;
 
 struct PartLds {
-    uint32_t *stg, *cnt0, *cnt1, *offw, *wcur, *newp, *w, *pool;
+    uint32_t *stg, *cnt0, *cnt1, *w, *pool;
+    uint32_t *offw;  // per partition: staging offset | write fill << 16 (read per event: one word, banks spread)
+    uint2 *pg;       // per partition: {page of the run's first entries, first new page}
 };
 
 __host__ __device__ constexpr size_t part_words(int P) {
@@ -198,9 +200,8 @@ __device__ __forceinline__ PartLds part_lds(uint32_t *sm, int P) {
     s.cnt0 = s.stg + UNIT + 3 * P4;
     s.cnt1 = s.cnt0 + P4 + 64;
     s.offw = s.cnt1 + P4 + 64;
-    s.wcur = s.offw + P4;
-    s.newp = s.wcur + P4;
-    s.w = s.newp + P4;
+    s.pg = reinterpret_cast<uint2 *>(s.offw + P4);  // (8-byte aligned: P4 a multiple of 4)
+    s.w = s.offw + 3 * P4;
     s.pool = s.w + 32;
     return s;
 }
@@ -215,7 +216,7 @@ struct Owner {  // registers of the owner thread of one partition
 // runs right after the rank atomics (the next unit's loads), mid() between
 // the staging and the write-out (the next unit's front end, whose gathers
 // then fly behind the write-out).
-template <bool E16, typename NEXT, typename MID>
+template <bool E16, int ABL = 0, typename NEXT, typename MID>
 __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, uint32_t emask, int parity,
                                           const uint32_t (&key)[EPT], Owner &own, uint32_t pool_base,
                                           uint32_t cap, __amdgpu_buffer_rsrc_t pool, uint32_t *__restrict__ page_cnt,
@@ -285,8 +286,7 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
             }
         }
         s.offw[tid] = off | (own.fill << 16);
-        s.wcur[tid] = own.cur;
-        s.newp[tid] = first;
+        s.pg[tid] = make_uint2(own.cur, first);
         const uint32_t end = own.fill + v;
         if (lost) {  // the open page is full now: the next run allocates again
             if (own.cur != kNone) page_cnt[own.cur] = PAGE;
@@ -302,6 +302,10 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
         own.ev += v;
     }
     __syncthreads();
+    if (ABL & 4) {  // (ablation: counts and pages only)
+        mid();
+        return;
+    }
     // (branch-free: entries without a key store into the lane's dummy word
     // of the other count array, which is never read)
 #pragma unroll
@@ -318,13 +322,14 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
         const uint4 k4 = *reinterpret_cast<const uint4 *>(s.stg + g);
         const uint32_t part = k4.x >> pbits;  // a group's first entry is never a pad
         const uint32_t ow = s.offw[part];
+        const uint2 pp = s.pg[part];  // (one 8-byte read for both pages)
         const uint32_t x = (ow >> 16) + g - (ow & 0xFFFFu);
-        const uint32_t np = s.newp[part], wc = s.wcur[part];
+        const uint32_t np = pp.y, wc = pp.x;
         const uint32_t page = x < (uint32_t)PAGE ? wc : np + (x >> PB) - 1u;
         const bool lost = x < (uint32_t)PAGE ? wc == kNone : np == kNone;  // pool overflow (flagged)
         // byte offset inside the row's pool (a store out of range is dropped)
         const uint32_t at = ((page - pool_base) << PB) + (x & (PAGE - 1));
-        const int boff = lost ? (int)kOOB : (int)(at << (E16 ? 1 : 2));
+        const int boff = (lost || (ABL & 2)) ? (int)kOOB : (int)(at << (E16 ? 1 : 2));
         if (E16) {
             auto e16 = [&](uint32_t k) { return k == kNone ? kPad16 : (k & emask); };
             typedef unsigned int v2u __attribute__((ext_vector_type(2)));
@@ -474,7 +479,10 @@ __global__ __launch_bounds__(256) void k_wide_table(WideArgs a, const void *__re
 // ---------------------------------------------------------------------------
 // first pass
 // ---------------------------------------------------------------------------
-template <bool L16, bool TL, bool E16>
+// ABL (diagnostics build only, wrong results by design): timing ablations of
+// the first pass -- 1 no gathers, 2 no page stores, 4 no staging or
+// write-out, 16 no front end (keys from a hash of the raw words)
+template <bool L16, bool TL, bool E16, int ABL = 0>
 __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
     // static layout for the largest partition count and table, so every LDS
     // address is a constant (fewer live scalar registers in the loop)
@@ -525,6 +533,7 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
     // load out of range: no request); finish() turns the words into keys.
     uint32_t q[EPT], w[EPT], g[EPT], bin[EPT];
     auto issue = [&]() __attribute__((always_inline)) {
+        if (ABL & 16) return;
         toa_bins<TL, EPT, 0>(a.toa, TL ? s_tree : a.toa.tree, t, bin);
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
@@ -536,12 +545,21 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
             const bool hit = (w[e] & kTabValid) && ((w[e] >> kTagShift) & kTagMask) == (q[e] >> a.cbits);
             const bool miss = q[e] < a.L && !hit;
             const uint32_t off = miss ? q[e] * (L16 ? 2u : 4u) : kOOB;
-            g[e] = L16 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(lut, (int)off, 0, 0)
-                       : __builtin_amdgcn_raw_buffer_load_b32(lut, (int)off, 0, 0);
+            if (ABL & 1)
+                g[e] = q[e] & 0xFFu;
+            else
+                g[e] = L16 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(lut, (int)off, 0, 0)
+                           : __builtin_amdgcn_raw_buffer_load_b32(lut, (int)off, 0, 0);
             w[e] = hit ? w[e] : kNone;
         }
     };
     auto finish = [&](uint32_t (&key)[EPT]) __attribute__((always_inline)) {
+        if (ABL & 16) {  // (ablation: no front end; issue() did nothing)
+#pragma unroll
+            for (int e = 0; e < EPT; ++e)
+                key[e] = ((uint32_t)p[e] * 2654435761u ^ (uint32_t)t[e]) & ((1u << (a.pbits + 9)) - 1u);
+            return;
+        }
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
             uint32_t base;
@@ -565,7 +583,7 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
     for (long long u = cb; u < ce; ++u) {
         uint32_t key[EPT];
         finish(key);
-        part_unit<E16>(s, P, a.pbits, emask, (int)(u & 1), key, own, pool_base, a.cap1, pool, a.page_cnt,
+        part_unit<E16, ABL>(s, P, a.pbits, emask, (int)(u & 1), key, own, pool_base, a.cap1, pool, a.page_cnt,
                        a.page_part, a.overflow,
                        // (unconditional: past the last unit, dropped events)
                        [&]() __attribute__((always_inline)) { unit_load(a, s_ct, c0, u + 1, ce, p, t); },
@@ -766,7 +784,8 @@ __global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4
                                                                      const uint32_t *__restrict__ page_cnt,
                                                                      const uint16_t *__restrict__ pages,
                                                                      uint32_t page0, uint32_t colmask,
-                                                                     uint32_t *__restrict__ hist, long long n_bins) {
+                                                                     uint32_t *__restrict__ hist, long long n_bins,
+                                                                     int wzero) {
     constexpr int NB = 1 << kWideTileBits;
     constexpr int NW = kWideAccThreads / 64;
     constexpr int D = kWideAccDepth;
@@ -818,7 +837,18 @@ __global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4
     }
     __syncthreads();
     const long long base = (long long)tile << kWideTileBits;
-    if ((it.w & 1u) && base + NB <= n_bins) {
+    if ((it.w & 1u) && base + NB <= n_bins && wzero) {
+        // the tile's only item owns its bins, and the window held nothing
+        // before this batch: its non-zero groups are stored, nothing is read
+        constexpr int V = NB / 4 / kWideAccThreads;
+        uint4 *h4 = reinterpret_cast<uint4 *>(hist + base);
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(s_tile);
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            const uint4 v = s4[u * kWideAccThreads + tid];
+            if (v.x | v.y | v.z | v.w) h4[u * kWideAccThreads + tid] = v;
+        }
+    } else if ((it.w & 1u) && base + NB <= n_bins) {
         // the tile's only item owns its bins: 16-byte read-modify-write
         constexpr int V = NB / 4 / kWideAccThreads;
         uint4 *h4 = reinterpret_cast<uint4 *>(hist + base);
@@ -882,6 +912,20 @@ hipError_t launch_wide_table(const WideArgs &a, const void *lut_rep, uint32_t *p
 template <bool L16, bool TL, bool E16>
 static hipError_t launch_scatter_t(const WideArgs &a, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
     if (wide_scatter_smem(a) > 160 * 1024) return hipErrorInvalidValue;
+#ifdef LDE_DIAGNOSTICS
+    if (a.ablate && L16 && TL && E16) {
+        switch (a.ablate) {
+#define LDE_WABL(m)                                                                                         \
+    case m:                                                                                                 \
+        hipExtLaunchKernelGGL((k_wide_scatter<true, true, true, m>), dim3(a.grid1), dim3(NT), 0, st, start, stop, \
+                              0, a);                                                                        \
+        return hipGetLastError();
+            LDE_WABL(1) LDE_WABL(2) LDE_WABL(3) LDE_WABL(4) LDE_WABL(5) LDE_WABL(16) LDE_WABL(18) LDE_WABL(20)
+#undef LDE_WABL
+        default: return hipErrorInvalidValue;
+        }
+    }
+#endif
     hipExtLaunchKernelGGL((k_wide_scatter<L16, TL, E16>), dim3(a.grid1), dim3(NT), 0, st, start, stop, 0, a);
     return hipGetLastError();
 }
@@ -931,7 +975,7 @@ hipError_t launch_wide(const WideArgs &a, hipStream_t st, hipEvent_t start, hipE
         page0 = a.page0_2;
     }
     hipExtLaunchKernelGGL(k_wide_accumulate, dim3(max_items), dim3(kWideAccThreads), 0, st, bstart, bstop, 0, items,
-                          count, rows, a.list, a.page_cnt, pages, page0, colmask, a.hist, a.n_bins);
+                          count, rows, a.list, a.page_cnt, pages, page0, colmask, a.hist, a.n_bins, a.wzero);
     return hipGetLastError();
 }
 

@@ -101,11 +101,21 @@ def reset_scipp_module() -> None:
     _SCIPP.clear()
 
 
+# numpy dtypes the stand-ins carry, as scipp dtype names (counts as float64 /
+# float32, exact partial sums as uint64 -> int64 is not needed: scipp has no
+# unsigned 64-bit dtype, so they are refused, as are object / string arrays)
+_SC_DTYPES = {'float64': 'float64', 'float32': 'float32', 'int64': 'int64', 'int32': 'int32',
+              'bool': 'bool'}
+
+
 def _sc_variable(sc, dims, values, unit):
     a = np.asarray(values)
+    dt = _SC_DTYPES.get(str(a.dtype))
+    if dt is None:
+        raise TypeError(f'no scipp dtype for a {a.dtype} output (float64, float32, int64, int32, bool)')
     if not dims:
-        return sc.scalar(a.item(), unit=unit, dtype=str(a.dtype))
-    return sc.array(dims=list(dims), values=a, unit=unit, dtype=str(a.dtype))
+        return sc.scalar(a.item(), unit=unit, dtype=dt)
+    return sc.array(dims=list(dims), values=a, unit=unit, dtype=dt)
 
 
 def scalar(value, *, unit: str | None = None):
@@ -127,9 +137,12 @@ def publish(outputs: dict) -> dict:
 
 
 def add_time_coords(data: dict, start_time, end_time) -> dict:
-    """``Job._add_time_coords`` (SRC/core/job.py:212-262) for stand-in
-    outputs: 0-D ``start_time`` / ``time`` (int64, 'ns') on every DataArray
-    that carries neither yet; no time bounds -> ValueError."""
+    """``Job._add_time_coords`` (SRC/core/job.py:212-262): 0-D
+    ``start_time`` / ``time`` (int64, 'ns') on every data array that carries
+    neither yet -- stand-ins and ``scipp.DataArray`` alike (anything with
+    ``coords`` and ``assign_coords``, as the reference stamps every
+    DataArray, so outputs already published as scipp objects are stamped
+    too); no time bounds -> ValueError."""
     if start_time is None or end_time is None:
         raise ValueError('Job has no time bounds to stamp on its outputs: finalized before '
                          'accumulating any primary data.')
@@ -140,4 +153,7 @@ def add_time_coords(data: dict, start_time, end_time) -> dict:
             return v
         return v.assign_coords(start_time=st, time=tt)
 
-    return {k: stamp(v) if isinstance(v, DataArray) else v for k, v in data.items()}
+    def stampable(v):
+        return hasattr(v, 'coords') and hasattr(v, 'assign_coords')
+
+    return {k: stamp(v) if stampable(v) else v for k, v in data.items()}

@@ -136,6 +136,8 @@ WIDE_VARIANTS = [
     {'LDE_WIDE_CACHE_BITS': '4'},
     {'LDE_WIDE_CACHE_BITS': '0'},
     {'LDE_WIDE_LEVELS': '2', 'LDE_WIDE_CACHE_BITS': '0'},
+    # pass B's read-modify-write on a fresh window too (it stores otherwise)
+    {'LDE_WIDE_WZERO': '0'},
 ]
 
 

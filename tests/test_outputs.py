@@ -30,6 +30,9 @@ class _FakeDataArray:
     def __init__(self, data, coords=None):
         self.data, self.coords = data, dict(coords or {})
 
+    def assign_coords(self, **coords):
+        return _FakeDataArray(self.data, {**self.coords, **coords})
+
 
 @pytest.fixture
 def fake_scipp(monkeypatch):
@@ -113,3 +116,23 @@ def test_int64_ns_coords_through_da00():
     back = da00.da00_to_dataarray(da00.deserialise_da00(da00.serialise_da00('s', 0, variables))[2])
     assert back.coords['time'].value == 2000 and back.coords['time'].unit == 'ns'
     assert np.asarray(back.coords['time'].values).dtype == np.int64
+
+
+def test_add_time_coords_stamps_published_scipp_arrays(fake_scipp):
+    """with scipp present, finalize hands over scipp.DataArray
+    values; the Job's stamp must reach them too (job.py:251-259 stamps every
+    DataArray), with int64 'ns' scalars."""
+    out = dam.publish({'cumulative': DataArray(np.zeros(2), ('x',)), 'n': 3})
+    assert isinstance(out['cumulative'], _FakeDataArray)
+    st = dam.add_time_coords(out, Timestamp.from_ns(10), Timestamp.from_ns(20))
+    c = st['cumulative'].coords
+    assert c['start_time'].value == 10 and c['time'].value == 20
+    assert c['time'].unit == 'ns' and c['time'].dtype == 'int64'
+    assert st['n'] == 3
+
+
+@pytest.mark.parametrize('bad', [np.array(['a', 'b']), np.array([object(), 1], dtype=object),
+                                 np.array([1, 2], dtype=np.uint64)])
+def test_scipp_conversion_refuses_dtypes_without_a_scipp_match(fake_scipp, bad):
+    with pytest.raises(TypeError, match='no scipp dtype'):
+        DataArray(bad, ('x',)).to_scipp()
