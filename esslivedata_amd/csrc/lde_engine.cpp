@@ -1470,7 +1470,7 @@ int setup_wide(lde_handle *h) {
         if (int rc = dev_alloc(h, &h->d_wtab, (size_t)h->R << cb)) return rc;
         if (int rc = dev_alloc(h, &h->d_wpixcnt, (size_t)h->L)) return rc;
     }
-    if (int rc = dev_alloc(h, &h->d_wcounters, 4)) return rc;
+    if (int rc = dev_alloc(h, &h->d_wcounters, 8)) return rc;
     if (!h->d_overflow) {
         if (int rc = dev_alloc(h, &h->d_overflow, 1)) return rc;
         HIPCALL(h, hipMemset(h->d_overflow, 0, 4));
@@ -3335,10 +3335,10 @@ int lde_counter(lde_handle *h, int32_t id, int64_t *value) {
     case LDE_C_WIDE_ITEMS: {
         *value = 0;
         if (!h->d_wcounters) return LDE_OK;
-        uint32_t c[2] = {0, 0};
+        uint32_t c[5] = {0, 0, 0, 0, 0};  // items of several / single items per pass
         HIPCALL(h, hipStreamSynchronize(h->stream));
-        HIPCALL(h, hipMemcpy(c, h->d_wcounters, 8, hipMemcpyDeviceToHost));
-        *value = h->wide_levels == 2 ? c[1] : c[0];
+        HIPCALL(h, hipMemcpy(c, h->d_wcounters, sizeof c, hipMemcpyDeviceToHost));
+        *value = h->wide_levels == 2 ? c[1] + c[4] : c[0] + c[3];
         return LDE_OK;
     }
     default:

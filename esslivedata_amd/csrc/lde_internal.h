@@ -512,7 +512,8 @@ struct WideArgs {
     uint32_t pool2_cap;
     uint32_t page0_2;            // first second-pass page (= grid1 * cap1; pages2 holds pages from here)
     uint4 *items1, *items2;      // plans: {part, row begin, row end, flags}
-    uint32_t *counters;          // [0] items1, [1] items2 (zeroed by k_wide_chunks)
+    uint32_t *counters;          // items of several [0] items1, [1] items2; single [3], [4]
+                                 // (zeroed by k_wide_chunks; [2] is pool2_next)
     uint32_t *overflow;          // pool / plan overflow flag (internal error, reported by finalize)
     uint32_t max_items1, max_items2;
     uint2 *band_items;           // [band] the second pass's rows of the band

@@ -384,7 +384,7 @@ template <bool KARG>
 __global__ __launch_bounds__(256) void k_wide_chunks(WideArgs a, SegKarg sk, PixChunk *__restrict__ ctab) {
     const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
     if (c == 0) {
-        a.counters[0] = a.counters[1] = 0u;
+        a.counters[0] = a.counters[1] = a.counters[3] = a.counters[4] = 0u;
         *a.pool2_next = 0u;
     }
     if (c >= a.n_chunks) return;
@@ -595,14 +595,19 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
 // ---------------------------------------------------------------------------
 // plan: per partition p, items of consecutive rows (rows [0, nrows) of the
 // first pass, or the second pass's rows of p's band); band_out: the items of
-// each partition (the second pass's rows of that band)
+// each partition (the second pass's rows of that band).  Items of partitions
+// that need several (the hot ones: Zipf pixels, peaked TOA) are numbered from
+// the front (count[0]), single items from the back (count[1] of them, at
+// max_items - 1 down), so the consuming pass -- which takes item_at(block) --
+// runs the long items first and the short ones fill the tail.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_wide_plan(WideRows rows, int nrows, const uint2 *__restrict__ band_rows,
                                                    int tpb_bits, uint32_t item_max, uint4 *__restrict__ items,
-                                                   uint32_t *__restrict__ count, uint32_t max_items,
-                                                   uint2 *__restrict__ band_out, uint32_t *__restrict__ overflow) {
+                                                   uint32_t *__restrict__ count, uint32_t *__restrict__ count1,
+                                                   uint32_t max_items, uint2 *__restrict__ band_out,
+                                                   uint32_t *__restrict__ overflow) {
     __shared__ unsigned long long s_sum[4];
-    __shared__ uint32_t s_base;
+    __shared__ uint32_t s_base, s_n;
     const int p = blockIdx.x;
     uint32_t r0 = 0, nr = (uint32_t)nrows, col = (uint32_t)p;
     if (band_rows) {
@@ -626,20 +631,37 @@ __global__ __launch_bounds__(256) void k_wide_plan(WideRows rows, int nrows, con
         n = n < 1 ? 1 : n;
     }
     if (threadIdx.x == 0) {
-        uint32_t base = n ? atomicAdd(count, n) : 0u;
-        if (base + n > max_items) {
+        uint32_t base = 0;
+        if (n > 1) {
+            base = atomicAdd(count, n);
+        } else if (n == 1) {
+            const uint32_t k = atomicAdd(count1, 1u);
+            base = k < max_items ? max_items - 1u - k : max_items;
+        }
+        // (the two ends cannot meet with the host's bound: max_items counts
+        // every partition once more than the item sizes need)
+        if (base + n > max_items || (n > 1 && base + n + *count1 > max_items)) {
             *overflow = 1u;  // cannot happen with the host's bound
-            n = base < max_items ? max_items - base : 0u;
+            n = 0;
         }
         s_base = base;
+        s_n = n;
         if (band_out) band_out[p] = make_uint2(base, n);
     }
     __syncthreads();
     const uint32_t base = s_base;
-    if (base + n > max_items) n = base < max_items ? max_items - base : 0u;
+    n = s_n;
     for (uint32_t j = threadIdx.x; j < n; j += 256)
         items[base + j] = make_uint4((uint32_t)p, r0 + (uint32_t)((unsigned long long)j * nr / n),
                                      r0 + (uint32_t)((unsigned long long)(j + 1) * nr / n), n == 1 ? 1u : 0u);
+}
+
+// item of block b: the multi-item partitions' items first, then the singles
+__device__ __forceinline__ uint32_t item_at(uint32_t b, const uint32_t *count, const uint32_t *count1,
+                                            uint32_t max_items) {
+    const uint32_t nm = *count, ns = *count1;
+    if (b < nm) return b;
+    return b - nm < ns ? max_items - 1u - (b - nm) : kNone;
 }
 
 namespace {
@@ -691,8 +713,9 @@ __device__ __forceinline__ void stage_pages(const WideRows &rows, const uint32_t
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t sm[kWideSplitWords];
-    if (blockIdx.x >= a.counters[0]) return;
-    const uint4 it = a.items1[blockIdx.x];
+    const uint32_t item = item_at(blockIdx.x, a.counters, a.counters + 3, a.max_items1);
+    if (item == kNone) return;
+    const uint4 it = a.items1[item];
     const int P = 1 << a.tpb_bits;
     const PartLds s = part_lds(sm, kWideMaxTpb);
     uint32_t *s_pref = sm + part_words(kWideMaxTpb);
@@ -770,7 +793,7 @@ __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
                             []() {});
         }
     }
-    part_finish(s, P, own, pool_base, cap, a.page_cnt, a.page_part, a.list, a.rows2, blockIdx.x);
+    part_finish(s, P, own, pool_base, cap, a.page_cnt, a.page_part, a.list, a.rows2, item);
 }
 
 // ---------------------------------------------------------------------------
@@ -780,6 +803,8 @@ constexpr int kWideAccThreads = 1024;
 constexpr int kWideAccDepth = 4;  // pages in flight per wave
 __global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4 *__restrict__ items,
                                                                      const uint32_t *__restrict__ item_count,
+                                                                     const uint32_t *__restrict__ item_count1,
+                                                                     uint32_t max_items,
                                                                      WideRows rows, const uint32_t *__restrict__ list,
                                                                      const uint32_t *__restrict__ page_cnt,
                                                                      const uint16_t *__restrict__ pages,
@@ -793,9 +818,9 @@ __global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4
     __shared__ uint32_t s_pref[kWideMaxRows + 1];
     __shared__ uint32_t s_pg[kWidePagesLds], s_pc[kWidePagesLds];
     __shared__ uint32_t s_w[32];
-    const uint32_t n_items = *item_count;
-    const uint4 it = items[blockIdx.x];
-    if (blockIdx.x >= n_items) return;
+    const uint32_t item = item_at(blockIdx.x, item_count, item_count1, max_items);
+    if (item == kNone) return;
+    const uint4 it = items[item];
     const int tid = threadIdx.x;
     for (int i = tid * 4; i < NB + 64; i += kWideAccThreads * 4)
         *reinterpret_cast<uint4 *>(s_tile + i) = make_uint4(0, 0, 0, 0);
@@ -945,37 +970,37 @@ hipError_t launch_wide(const WideArgs &a, hipStream_t st, hipEvent_t start, hipE
                 : (a.toa.lds ? launch_scatter_tl<false, true>(a, st, start, stop)
                              : launch_scatter_tl<false, false>(a, st, start, stop));
     if (e != hipSuccess) return e;
-    const uint32_t *cnt2 = a.counters + 1;
     WideRows rows = a.rows1;
     const uint4 *items = a.items1;
-    const uint32_t *count = a.counters;
+    const uint32_t *count = a.counters, *count1 = a.counters + 3;
     const uint16_t *pages = reinterpret_cast<const uint16_t *>(a.pages1);
     uint32_t colmask = 0xFFFFFFFFu;
     uint32_t max_items = a.max_items1;
     uint32_t page0 = 0;
     if (a.levels == 1) {
         hipLaunchKernelGGL(k_wide_plan, dim3(a.n_parts), dim3(256), 0, st, a.rows1, a.grid1,
-                           (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.max_items1,
-                           (uint2 *)nullptr, a.overflow);
+                           (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.counters + 3,
+                           a.max_items1, (uint2 *)nullptr, a.overflow);
     } else {
         hipLaunchKernelGGL(k_wide_plan, dim3(a.n_parts), dim3(256), 0, st, a.rows1, a.grid1,
-                           (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.max_items1,
-                           a.band_items, a.overflow);
+                           (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.counters + 3,
+                           a.max_items1, a.band_items, a.overflow);
         if (a.tpb_bits > 8) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_wide_split, dim3(a.max_items1), dim3(NT), 0, st, a);
         hipLaunchKernelGGL(k_wide_plan, dim3(a.n_tiles), dim3(256), 0, st, a.rows2, 0,
-                           (const uint2 *)a.band_items, a.tpb_bits, a.item_max2, a.items2,
-                           const_cast<uint32_t *>(cnt2), a.max_items2, (uint2 *)nullptr, a.overflow);
+                           (const uint2 *)a.band_items, a.tpb_bits, a.item_max2, a.items2, a.counters + 1,
+                           a.counters + 4, a.max_items2, (uint2 *)nullptr, a.overflow);
         rows = a.rows2;
         items = a.items2;
-        count = cnt2;
+        count = a.counters + 1;
+        count1 = a.counters + 4;
         pages = reinterpret_cast<const uint16_t *>(a.pages2);
         colmask = (1u << a.tpb_bits) - 1u;
         max_items = a.max_items2;
         page0 = a.page0_2;
     }
     hipExtLaunchKernelGGL(k_wide_accumulate, dim3(max_items), dim3(kWideAccThreads), 0, st, bstart, bstop, 0, items,
-                          count, rows, a.list, a.page_cnt, pages, page0, colmask, a.hist, a.n_bins, a.wzero);
+                          count, count1, max_items, rows, a.list, a.page_cnt, pages, page0, colmask, a.hist, a.n_bins, a.wzero);
     return hipGetLastError();
 }
 
