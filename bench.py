@@ -733,6 +733,10 @@ def main():
     achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
     prof_name = ('wavelength' if args.coordinate == 'wavelength' else
                  args.workload if args.view == 'geometric' else args.view)
+    if args.num_bins or args.toa_scale or args.toa_start is not None:
+        # a non-default TOA binning has its own profile (tools/prof_round.sh NAME=)
+        prof_name += f'_t{args.num_bins or "def"}{args.toa_scale or ""}' + (
+            f'_s{args.toa_start:g}' if args.toa_start is not None else '')
     traffic = profiled_traffic(prof_name, dom)
     if traffic is not None:
         # per-dispatch tracing slows a kernel: the traced run's own line agrees

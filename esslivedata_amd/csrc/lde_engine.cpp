@@ -74,6 +74,10 @@ struct lde_handle {
     uint32_t *d_win32 = nullptr;
     unsigned long long *d_win64 = nullptr;
     unsigned long long *d_cum = nullptr;
+    // per screen: cumulative sum in the TOA range | over all bins (2 x S),
+    // current when cumrow_ok (kept by the wide-row finalize, launch_finalize)
+    unsigned long long *d_cumrow = nullptr;
+    int cumrow_ok = 0;
     float *d_winf = nullptr;
     float *d_cumf = nullptr;
 
@@ -2038,6 +2042,8 @@ int zero_state(lde_handle *h) {
     const size_t nb = (size_t)h->nbins;
     HIPCALL(h, hipMemsetAsync(h->d_win32, 0, nb * 4, h->stream));
     HIPCALL(h, hipMemsetAsync(h->d_cum, 0, nb * 8, h->stream));
+    if (h->d_cumrow) HIPCALL(h, hipMemsetAsync(h->d_cumrow, 0, (size_t)h->S * 16, h->stream));
+    h->cumrow_ok = h->d_cumrow ? 1 : 0;
     if (h->d_win64) HIPCALL(h, hipMemsetAsync(h->d_win64, 0, nb * 8, h->stream));
     if (h->d_winf) HIPCALL(h, hipMemsetAsync(h->d_winf, 0, nb * 4, h->stream));
     if (h->d_cumf) HIPCALL(h, hipMemsetAsync(h->d_cumf, 0, nb * 4, h->stream));
@@ -2084,7 +2090,7 @@ void release(lde_handle *h) {
                     (void *)h->d_pfp_scr, (void *)h->d_pcounts, (void *)h->d_prstart, (void *)h->d_ppayload,
                     (void *)h->d_pctab, (void *)h->d_pitems, (void *)h->d_pitem_count, (void *)h->d_pprev,
                     (void *)h->d_povf, (void *)h->d_povf_grp, (void *)h->d_win32, (void *)h->d_win64,
-                    (void *)h->d_cum, (void *)h->d_winf, (void *)h->d_cumf, (void *)h->d_spid,
+                    (void *)h->d_cum, (void *)h->d_cumrow, (void *)h->d_winf, (void *)h->d_cumf, (void *)h->d_spid,
                     (void *)h->d_stoa, (void *)h->d_payload, (void *)h->d_starts, (void *)h->d_part,
                     (void *)h->d_ttot, (void *)h->d_tile_items, (void *)h->d_item_count, (void *)h->d_items,
                     (void *)h->d_segs, (void *)h->d_pages, (void *)h->d_page_tile, (void *)h->d_page_cnt,
@@ -2297,6 +2303,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     // histograms
     CREATE_CHECK(dev_alloc(h, &h->d_win32, (size_t)nbins));
     CREATE_CHECK(dev_alloc(h, &h->d_cum, (size_t)nbins));
+    CREATE_CHECK(dev_alloc(h, &h->d_cumrow, (size_t)h->S * 2));
     if (h->out_dtype == LDE_F32) {
         CREATE_CHECK(dev_alloc(h, &h->d_winf, (size_t)nbins));
         CREATE_CHECK(dev_alloc(h, &h->d_cumf, (size_t)nbins));
@@ -2768,6 +2775,7 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
                            h->d_overflow, (uint32_t *)(d_tail + 32), &n_parts, h->stream, sp.a, sp.b));
             sp.done = true;
         }
+        h->cumrow_ok = 0;  // (the f32 finalize does not keep the per-screen sums)
         h->f32_pending = false;
         if (want_cur_hist)
             HIPCALL(h, hipMemcpyAsync(out->current_hist, snap, nb * 4, hipMemcpyDeviceToHost, h->stream));
@@ -2782,7 +2790,7 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
                        h->range_hi, out->current_image ? img_cur : nullptr,
                        out->cumulative_image ? img_cum : nullptr, h->d_tot4,
                        (unsigned long long *)d_tail, h->d_overflow, (uint32_t *)(d_tail + 32),
-                       h->stream, (unsigned long long *)(d_tail + 48), &n_parts));
+                       h->stream, (unsigned long long *)(d_tail + 48), &n_parts, h->d_cumrow, &h->cumrow_ok));
     }
     const size_t isz = f32 ? 4 : 8;
     // a system-scope release after the kernel: its host writes are visible
@@ -2843,7 +2851,7 @@ int lde_finalize_partials(lde_handle *h, void *d_out) {
         HIPCALL(h, lde::launch_finalize(2, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr,
                                         h->d_cum, nullptr, h->S, h->T, h->range_lo, h->range_hi,
                                         o, o + h->S, h->d_tot4, o + 2 * h->S, nullptr, nullptr,
-                                        h->stream));
+                                        h->stream, nullptr, nullptr, h->d_cumrow, &h->cumrow_ok));
     }
     if (h->out_dtype == LDE_F32)  // the window's f32 accumulator restarts too
         HIPCALL(h, hipMemsetAsync(h->d_winf, 0, (size_t)h->nbins * 4, h->stream));

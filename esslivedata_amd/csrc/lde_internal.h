@@ -294,7 +294,11 @@ hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *wi
                            int lo, int hi, void *cur_img, void *cum_img,
                            unsigned long long *totals, unsigned long long *tot_copy,
                            const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st,
-                           unsigned long long *host_parts = nullptr, int *n_parts = nullptr);
+                           unsigned long long *host_parts = nullptr, int *n_parts = nullptr,
+                           unsigned long long *cumrow = nullptr, int *cumrow_ok = nullptr);
+// cumrow: 2 x S u64, each screen's cumulative sum in the TOA range and over
+// all bins.  *cumrow_ok in: they are current (the wide-row finalize then skips
+// the cumulative of groups the window left empty); out: current afterwards.
 // float32 finalize in one pass with the window's pending push (batch, may be
 // null): f32 adds, images, exact totals and cumulative, window reset
 hipError_t launch_finalize_f32(uint32_t *batch, unsigned long long *win64, unsigned long long *cum,

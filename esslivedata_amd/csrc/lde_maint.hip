@@ -254,7 +254,8 @@ __global__ __launch_bounds__(256) void k_finalize_w4(uint32_t *__restrict__ win3
                                                      OUT *__restrict__ cum_img,
                                                      unsigned long long *__restrict__ totals,
                                                      const uint32_t *__restrict__ ovf_src,
-                                                     uint32_t *__restrict__ ovf_dst) {
+                                                     uint32_t *__restrict__ ovf_dst,
+                                                     unsigned long long *__restrict__ cumrow, int inc) {
     typedef unsigned long long u64;
     __shared__ u64 s_tot[4][4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -273,11 +274,22 @@ __global__ __launch_bounds__(256) void k_finalize_w4(uint32_t *__restrict__ win3
                 *reinterpret_cast<ulonglong2 *>(win64 + k) = make_ulonglong2(0, 0);
                 *reinterpret_cast<ulonglong2 *>(win64 + k + 2) = make_ulonglong2(0, 0);
             }
-            const ulonglong2 c01 = *reinterpret_cast<const ulonglong2 *>(cum + k);
-            const ulonglong2 c23 = *reinterpret_cast<const ulonglong2 *>(cum + k + 2);
-            const u64 c[4] = {c01.x + w[0], c01.y + w[1], c23.x + w[2], c23.y + w[3]};
-            *reinterpret_cast<ulonglong2 *>(cum + k) = make_ulonglong2(c[0], c[1]);
-            *reinterpret_cast<ulonglong2 *>(cum + k + 2) = make_ulonglong2(c[2], c[3]);
+            // with the per-screen cumulative sums kept (inc), a group the
+            // window left empty neither reads nor writes the cumulative
+            const bool nz = (w[0] | w[1] | w[2] | w[3]) != 0;
+            u64 c[4] = {0, 0, 0, 0};
+            if (!inc || nz) {
+                const ulonglong2 c01 = *reinterpret_cast<const ulonglong2 *>(cum + k);
+                const ulonglong2 c23 = *reinterpret_cast<const ulonglong2 *>(cum + k + 2);
+                c[0] = c01.x + w[0];
+                c[1] = c01.y + w[1];
+                c[2] = c23.x + w[2];
+                c[3] = c23.y + w[3];
+                if (nz) {
+                    *reinterpret_cast<ulonglong2 *>(cum + k) = make_ulonglong2(c[0], c[1]);
+                    *reinterpret_cast<ulonglong2 *>(cum + k + 2) = make_ulonglong2(c[2], c[3]);
+                }
+            }
             if (snap) {
                 *reinterpret_cast<ulonglong2 *>(snap + k) = make_ulonglong2(w[0], w[1]);
                 *reinterpret_cast<ulonglong2 *>(snap + k + 2) = make_ulonglong2(w[2], w[3]);
@@ -301,6 +313,16 @@ __global__ __launch_bounds__(256) void k_finalize_w4(uint32_t *__restrict__ win3
             tc += __shfl_xor(tc, d, 64);
         }
         if (lane == 0) {
+            if (cumrow) {
+                // the screen's cumulative sums (in range, all bins): kept
+                // across finalizes, recomputed from the bins when !inc
+                if (inc) {
+                    rc = cumrow[s] + rw;
+                    tc = cumrow[S + s] + tw;
+                }
+                cumrow[s] = rc;
+                cumrow[S + s] = tc;
+            }
             if (cur_img) cur_img[s] = (OUT)rw;
             if (cum_img) cum_img[s] = (OUT)rc;
             acc[0] += tw;
@@ -515,7 +537,7 @@ static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsign
                               void *cur_img, void *cum_img, unsigned long long *totals,
                               unsigned long long *tot_copy, const uint32_t *ovf_src,
                               uint32_t *ovf_dst, unsigned long long *host_parts, int *n_parts,
-                              hipStream_t st) {
+                              hipStream_t st, unsigned long long *cumrow, int *cumrow_ok) {
     const bool v4 = T % 4 == 0 && T <= 128;
     const long long rows_per_block = v4 ? 8 : 4;
     long long blocks = (S + rows_per_block - 1) / rows_per_block;
@@ -530,10 +552,13 @@ static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsign
                            cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, dst, ks, kd);
     else if (T % 4 == 0)
         hipLaunchKernelGGL(k_finalize_w4<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
-                           cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, dst, ks, kd);
+                           cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, dst, ks, kd, cumrow,
+                           cumrow && cumrow_ok && *cumrow_ok ? 1 : 0);
     else
         hipLaunchKernelGGL(k_finalize<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
                            cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, dst, ks, kd);
+    // the per-screen cumulative sums are current after a wide-row finalize only
+    if (cumrow_ok) *cumrow_ok = cumrow && !v4 && T % 4 == 0 ? 1 : 0;
     if (n_parts) *n_parts = (int)blocks;
     if (!host_parts)
         hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(1024), 0, st, totals, (int)blocks, tot_copy,
@@ -547,15 +572,16 @@ hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *wi
                            int lo, int hi, void *cur_img, void *cum_img,
                            unsigned long long *totals, unsigned long long *tot_copy,
                            const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st,
-                           unsigned long long *host_parts, int *n_parts) {
+                           unsigned long long *host_parts, int *n_parts, unsigned long long *cumrow,
+                           int *cumrow_ok) {
     if (img_kind == 1) return hipErrorInvalidValue;
     if (img_kind == 2)
         launch_finalize_t<unsigned long long>(win32, win64, cum, snap, S, T, lo, hi, cur_img,
                                               cum_img, totals, tot_copy, ovf_src, ovf_dst,
-                                              host_parts, n_parts, st);
+                                              host_parts, n_parts, st, cumrow, cumrow_ok);
     else
         launch_finalize_t<double>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals,
-                                  tot_copy, ovf_src, ovf_dst, host_parts, n_parts, st);
+                                  tot_copy, ovf_src, ovf_dst, host_parts, n_parts, st, cumrow, cumrow_ok);
     return hipGetLastError();
 }
 

@@ -19,6 +19,9 @@ prof_args() {  # name -> workload and bench args of the profile
     wavelength) echo "dream|--coordinate wavelength" ;;
     monitor) echo "monitor|" ;;
     bifrost) echo "bifrost|" ;;
+    dream_t1000log) echo "dream|--num-bins 1000 --toa-scale log" ;;
+    dream_t10000log) echo "dream|--num-bins 10000 --toa-scale log" ;;
+    loki_t1000linear) echo "loki|--num-bins 1000 --toa-scale linear" ;;
     *) echo "dream|--view $1" ;;
   esac
 }
@@ -29,6 +32,9 @@ line_args() {  # name -> args of the untraced bench line
     wavelength) echo "--coordinate wavelength --e2e-steps 0" ;;
     monitor) echo "--workload monitor --cpu-baseline-seconds 3" ;;
     bifrost) echo "--workload bifrost" ;;
+    dream_t1000log) echo "--num-bins 1000 --toa-scale log --e2e-steps 0 --cpu-baseline-seconds 3" ;;
+    dream_t10000log) echo "--num-bins 10000 --toa-scale log --e2e-steps 0 --cpu-baseline-seconds 3" ;;
+    loki_t1000linear) echo "--workload loki --num-bins 1000 --toa-scale linear --e2e-steps 0 --cpu-baseline-seconds 3" ;;
     *) echo "--view $1 --e2e-steps 0 --cpu-baseline-seconds 3" ;;
   esac
 }
