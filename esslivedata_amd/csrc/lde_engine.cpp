@@ -1439,8 +1439,22 @@ int setup_wide(lde_handle *h) {
         h->wide_parts = (int)tiles;
         h->wide_tpb_bits = 0;
     } else {  // bands of tpb tiles (at most kWideMaxBands of them), then tiles
-        int tb = 1;  // (LDE_WIDE_LEVELS=2, diagnostics: the two-level form at any size)
+        // (LDE_WIDE_LEVELS=2, diagnostics: the two-level form at any size).
+        // Partitions per pass balanced (the larger of the bands and the tiles
+        // per band as small as it goes): a pass into few partitions ranks with
+        // LDS atomics that many lanes of a wave aim at one counter.
+        int tb = 1;
         while (((tiles + (1LL << tb) - 1) >> tb) > lde::kWideMaxBands) ++tb;
+        long long best = -1;
+        for (int b = tb; b <= 8; ++b) {
+            const long long m = std::max<long long>((tiles + (1LL << b) - 1) >> b, 1LL << b);
+            if (best < 0 || m < best) {
+                best = m;
+                tb = b;
+            }
+        }
+        const long long force = env_ll("LDE_WIDE_TPB_BITS", 0);  // (diagnostics)
+        if (force > 0 && force <= 8 && ((tiles + (1LL << force) - 1) >> force) <= lde::kWideMaxBands) tb = (int)force;
         h->wide_levels = 2;
         h->wide_tpb_bits = tb;
         h->wide_pbits = lde::kWideTileBits + tb;

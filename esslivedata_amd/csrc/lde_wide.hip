@@ -601,57 +601,74 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
 // max_items - 1 down), so the consuming pass -- which takes item_at(block) --
 // runs the long items first and the short ones fill the tail.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_wide_plan(WideRows rows, int nrows, const uint2 *__restrict__ band_rows,
-                                                   int tpb_bits, uint32_t item_max, uint4 *__restrict__ items,
-                                                   uint32_t *__restrict__ count, uint32_t *__restrict__ count1,
-                                                   uint32_t max_items, uint2 *__restrict__ band_out,
-                                                   uint32_t *__restrict__ overflow) {
-    __shared__ unsigned long long s_sum[4];
-    __shared__ uint32_t s_base, s_n;
-    const int p = blockIdx.x;
-    uint32_t r0 = 0, nr = (uint32_t)nrows, col = (uint32_t)p;
-    if (band_rows) {
-        const uint2 br = band_rows[p >> tpb_bits];
-        r0 = br.x;
-        nr = br.y;
-        col = (uint32_t)p & ((1u << tpb_bits) - 1u);
-    }
-    unsigned long long sum = 0;
-    for (uint32_t r = threadIdx.x; r < nr; r += 256) sum += rows.ev[(size_t)(r0 + r) * rows.ncols + col];
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
-    if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = sum;
-    __syncthreads();
-    const unsigned long long total = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-    uint32_t n = 0;
-    if (total > 0) {
-        const unsigned long long k = (total + item_max - 1) / item_max;
-        n = (uint32_t)(k < nr ? k : nr);
-        if (n > (uint32_t)kWideMaxRows) n = kWideMaxRows;
-        n = n < 1 ? 1 : n;
-    }
-    if (threadIdx.x == 0) {
-        uint32_t base = 0;
-        if (n > 1) {
-            base = atomicAdd(count, n);
-        } else if (n == 1) {
-            const uint32_t k = atomicAdd(count1, 1u);
-            base = k < max_items ? max_items - 1u - k : max_items;
+constexpr int kPlanWaves = 16;  // partitions per plan block (a wave each)
+__global__ __launch_bounds__(64 * kPlanWaves) void k_wide_plan(WideRows rows, int nrows,
+                                                              const uint2 *__restrict__ band_rows, int tpb_bits,
+                                                              uint32_t item_max, uint4 *__restrict__ items,
+                                                              uint32_t *__restrict__ count,
+                                                              uint32_t *__restrict__ count1, uint32_t max_items,
+                                                              uint2 *__restrict__ band_out,
+                                                              uint32_t *__restrict__ overflow, int n_parts) {
+    __shared__ uint32_t s_n[kPlanWaves], s_base[kPlanWaves];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int p = blockIdx.x * kPlanWaves + wv;
+    uint32_t r0 = 0, nr = (uint32_t)nrows, col = (uint32_t)p, n = 0;
+    if (p < n_parts) {
+        if (band_rows) {
+            const uint2 br = band_rows[p >> tpb_bits];
+            r0 = br.x;
+            nr = br.y;
+            col = (uint32_t)p & ((1u << tpb_bits) - 1u);
         }
+        unsigned long long sum = 0;
+        for (uint32_t r = lane; r < nr; r += 64) sum += rows.ev[(size_t)(r0 + r) * rows.ncols + col];
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+        if (sum > 0) {
+            const unsigned long long k = (sum + item_max - 1) / item_max;
+            n = (uint32_t)(k < nr ? k : nr);
+            if (n > (uint32_t)kWideMaxRows) n = kWideMaxRows;
+            n = n < 1 ? 1 : n;
+        }
+    }
+    if (lane == 0) s_n[wv] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // one reservation per block and end (a single counter that every
+        // partition hit serialised the plan of 8k tiles)
+        uint32_t multi = 0, singles = 0;
+        for (int i = 0; i < kPlanWaves; ++i) {
+            multi += s_n[i] > 1 ? s_n[i] : 0u;
+            singles += s_n[i] == 1 ? 1u : 0u;
+        }
+        uint32_t bm = multi ? atomicAdd(count, multi) : 0u;
+        uint32_t bs = singles ? atomicAdd(count1, singles) : 0u;
         // (the two ends cannot meet with the host's bound: max_items counts
         // every partition once more than the item sizes need)
-        if (base + n > max_items || (n > 1 && base + n + *count1 > max_items)) {
-            *overflow = 1u;  // cannot happen with the host's bound
-            n = 0;
+        const bool meet = multi && bm + multi + *count1 > max_items;
+        for (int i = 0; i < kPlanWaves; ++i) {
+            uint32_t ni = s_n[i], base = 0;
+            if (ni > 1) {
+                base = bm;
+                bm += ni;
+            } else if (ni == 1) {
+                const uint32_t k = bs++;
+                base = k < max_items ? max_items - 1u - k : max_items;
+            }
+            if (ni && (base + ni > max_items || meet)) {
+                *overflow = 1u;  // cannot happen with the host's bound
+                ni = 0;
+            }
+            s_n[i] = ni;
+            s_base[i] = base;
+            const int pi = blockIdx.x * kPlanWaves + i;
+            if (band_out && pi < n_parts) band_out[pi] = make_uint2(base, ni);
         }
-        s_base = base;
-        s_n = n;
-        if (band_out) band_out[p] = make_uint2(base, n);
     }
     __syncthreads();
-    const uint32_t base = s_base;
-    n = s_n;
-    for (uint32_t j = threadIdx.x; j < n; j += 256)
+    n = s_n[wv];
+    const uint32_t base = s_base[wv];
+    for (uint32_t j = lane; j < n; j += 64)
         items[base + j] = make_uint4((uint32_t)p, r0 + (uint32_t)((unsigned long long)j * nr / n),
                                      r0 + (uint32_t)((unsigned long long)(j + 1) * nr / n), n == 1 ? 1u : 0u);
 }
@@ -961,6 +978,8 @@ static hipError_t launch_scatter_tl(const WideArgs &a, hipStream_t st, hipEvent_
                          : launch_scatter_t<L16, TL, false>(a, st, start, stop);
 }
 
+static unsigned plan_grid(int parts) { return (unsigned)((parts + kPlanWaves - 1) / kPlanWaves); }
+
 hipError_t launch_wide(const WideArgs &a, hipStream_t st, hipEvent_t start, hipEvent_t stop, hipEvent_t bstart,
                        hipEvent_t bstop) {
     if (a.n_parts < 1 || a.n_parts > kWideMaxParts || a.grid1 < 1 || a.grid1 > kWideMaxRows)
@@ -978,18 +997,18 @@ hipError_t launch_wide(const WideArgs &a, hipStream_t st, hipEvent_t start, hipE
     uint32_t max_items = a.max_items1;
     uint32_t page0 = 0;
     if (a.levels == 1) {
-        hipLaunchKernelGGL(k_wide_plan, dim3(a.n_parts), dim3(256), 0, st, a.rows1, a.grid1,
-                           (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.counters + 3,
-                           a.max_items1, (uint2 *)nullptr, a.overflow);
+        hipLaunchKernelGGL(k_wide_plan, dim3(plan_grid(a.n_parts)), dim3(64 * kPlanWaves), 0, st, a.rows1,
+                           a.grid1, (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.counters + 3,
+                           a.max_items1, (uint2 *)nullptr, a.overflow, a.n_parts);
     } else {
-        hipLaunchKernelGGL(k_wide_plan, dim3(a.n_parts), dim3(256), 0, st, a.rows1, a.grid1,
-                           (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.counters + 3,
-                           a.max_items1, a.band_items, a.overflow);
+        hipLaunchKernelGGL(k_wide_plan, dim3(plan_grid(a.n_parts)), dim3(64 * kPlanWaves), 0, st, a.rows1,
+                           a.grid1, (const uint2 *)nullptr, 0, a.item_max1, a.items1, a.counters, a.counters + 3,
+                           a.max_items1, a.band_items, a.overflow, a.n_parts);
         if (a.tpb_bits > 8) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_wide_split, dim3(a.max_items1), dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_wide_plan, dim3(a.n_tiles), dim3(256), 0, st, a.rows2, 0,
+        hipLaunchKernelGGL(k_wide_plan, dim3(plan_grid(a.n_tiles)), dim3(64 * kPlanWaves), 0, st, a.rows2, 0,
                            (const uint2 *)a.band_items, a.tpb_bits, a.item_max2, a.items2, a.counters + 1,
-                           a.counters + 4, a.max_items2, (uint2 *)nullptr, a.overflow);
+                           a.counters + 4, a.max_items2, (uint2 *)nullptr, a.overflow, a.n_tiles);
         rows = a.rows2;
         items = a.items2;
         count = a.counters + 1;
