@@ -78,6 +78,9 @@ def parse():
                          'cylinder_mantle_z projection (diagnostic lines, not the headline)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-finalize-overlap', dest='finalize_overlap', action='store_false',
+                    help='wait for each finalize before the next batch is enqueued (default: '
+                         'the next batch is binned while the host reads the outputs)')
     ap.add_argument('--timing-stride', type=int, default=5,
                     help='stamp the dominant kernel with HIP events on every Nth timed step '
                          '(a stamped dispatch costs ~16 us of step time on the sieve path)')
@@ -601,13 +604,26 @@ def main():
             eng.stage_tensors_batch(batch_msgs[(i + 1) % n_batches])
         if reducer is not None:
             reducer.finalize()
+        elif args.finalize_overlap:
+            # the previous window's outputs are read once this batch's binning
+            # is enqueued behind them; this window's finalize is enqueued next
+            drain()
+            pending[0] = eng.finalize(images=True, wait=False)
         else:
             eng.finalize(images=True)
+
+    pending = [None]
+
+    def drain():  # the outputs of the finalize still pending (every step's are read)
+        if pending[0] is not None:
+            pending[0].result()
+            pending[0] = None
 
     if not bifrost:
         eng.stage_tensors_batch(batch_msgs[0])
     for i in range(args.warmup):
         step(i)
+    drain()
     torch.cuda.synchronize(dev)
     # per-kernel breakdown (every kernel bracketed with HIP events) from 3
     # extra steps before the timed region; the dominant kernel is the one
@@ -621,6 +637,7 @@ def main():
     n_prof = 3
     for i in range(n_prof):
         step(args.warmup + i)
+    drain()
     torch.cuda.synchronize(dev)
     stats = {k: eng.kernel_stats(k) for k in names}
     info = eng.info()
@@ -654,6 +671,7 @@ def main():
             eng.timing_select([])
         else:
             step(first + i)
+    drain()  # the last step's outputs, inside the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -666,6 +684,7 @@ def main():
     timed = {dom: eng.kernel_stats(dom)}
     eng.timing_enable(False)
     step(first + args.steps, stage_next=False)  # bins the batch the last timed step staged
+    drain()
     # the parity legs bin the batch after the last one binned (never a repeat)
     b_chk = (first + args.steps + 1) % n_batches
     pid, toa = batches[b_chk]
@@ -778,6 +797,10 @@ def main():
                 'pushes_per_step': len(batch_pushes[0]),
                 'messages_per_push': len(batch_pushes[0][0])} if bifrost else {}),
             'tile_bits': info['tile_bits'],
+            # each step's finalize outputs are read after the next batch's
+            # binning is enqueued (lde_finalize_begin/_end); every one inside
+            # the timed region
+            'finalize_overlap': bool(args.finalize_overlap and not bifrost and reducer is None),
             'parallelism': (f'event-batch sharding x{world} + '
                             f'{"RCCL" if dist.get_backend() == "nccl" else dist.get_backend()} '
                             'reduce of partial outputs') if world > 1 else 'single GPU',

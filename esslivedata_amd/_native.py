@@ -89,6 +89,8 @@ EXPORTED_SYMBOLS = (
     'lde_rebin_f64',
     'lde_accumulate',
     'lde_finalize',
+    'lde_finalize_begin',
+    'lde_finalize_end',
     'lde_read_histogram',
     'lde_clear',
     'lde_reset_cumulative',
@@ -184,6 +186,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         'lde_stage_ev44': (ctypes.c_int, [H, P, i64, i64, i32, ctypes.POINTER(i64)]),
         'lde_accumulate': (ctypes.c_int, [H, i32]),
         'lde_finalize': (ctypes.c_int, [H, ctypes.POINTER(LdeOutputs)]),
+        'lde_finalize_begin': (ctypes.c_int, [H, ctypes.POINTER(LdeOutputs)]),
+        'lde_finalize_end': (ctypes.c_int, [H, ctypes.POINTER(LdeOutputs)]),
         'lde_read_histogram': (ctypes.c_int, [H, i32, P]),
         'lde_clear': (ctypes.c_int, [H]),
         'lde_reset_cumulative': (ctypes.c_int, [H]),

@@ -78,6 +78,13 @@ struct lde_handle {
     // current when cumrow_ok (kept by the wide-row finalize, launch_finalize)
     unsigned long long *d_cumrow = nullptr;
     int cumrow_ok = 0;
+    // a finalize enqueued by lde_finalize_begin, read by lde_finalize_end:
+    // images to copy out of the pack (not mapped), their element size, and
+    // the number of per-block total partials
+    bool fin_pending = false;
+    void *fin_images[2] = {nullptr, nullptr};
+    size_t fin_isz = 8;
+    int fin_parts = 0;
     float *d_winf = nullptr;
     float *d_cumf = nullptr;
 
@@ -2744,8 +2751,9 @@ int accumulate_impl(lde_handle *h, int32_t replica, unsigned long long *d_push) 
 }
 }  // namespace
 
-int lde_finalize(lde_handle *h, lde_outputs *out) {
+int lde_finalize_begin(lde_handle *h, lde_outputs *out) {
     if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (h->fin_pending) return fail(h, LDE_ESTATE, "a finalize is pending (lde_finalize_end)");
     if (!h->window_has_data) return fail(h, LDE_ENODATA, "No data has been added");
     DeviceGuard guard(h->device);
     const bool f32 = h->out_dtype == LDE_F32;
@@ -2822,7 +2830,25 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
         HIPCALL(h, hipStreamSynchronize(h->stream));
         convert_u64(tmp.data(), out->cumulative_hist, (long long)nb, LDE_F64);
     }
-    HIPCALL(h, wait_stream(h));
+    // the outputs are complete once fin_event has passed (lde_finalize_end);
+    // the window restarts now, so the next accumulate may be enqueued first
+    h->fin_pending = true;
+    h->fin_images[0] = out->current_image && !map_cur ? out->current_image : nullptr;
+    h->fin_images[1] = out->cumulative_image && !map_cum ? out->cumulative_image : nullptr;
+    h->fin_isz = isz;
+    h->fin_parts = n_parts;
+    h->window_has_data = false;
+    h->win64_dirty = false;
+    h->win_events = 0;
+    return LDE_OK;
+}
+
+int lde_finalize_end(lde_handle *h, lde_outputs *out) {
+    if (!h) return fail(nullptr, LDE_EINVAL, "handle is NULL");
+    if (!h->fin_pending) return fail(h, LDE_ESTATE, "no finalize is pending (lde_finalize_begin)");
+    DeviceGuard guard(h->device);
+    h->fin_pending = false;
+    HIPCALL(h, wait_stream(h, h->fin_event));
     const auto t_waited = h->probe ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
     struct PostProbe {
         lde_handle *h;
@@ -2838,18 +2864,20 @@ int lde_finalize(lde_handle *h, lde_outputs *out) {
     uint32_t ovf = 0;
     std::memcpy(&ovf, h_tail + 32, 4);
     if (ovf) return fail(h, LDE_ESTATE, "page pool overflow (internal error)");
-    if (out->current_image && !map_cur) std::memcpy(out->current_image, h->h_pack, (size_t)h->S * isz);
-    if (out->cumulative_image && !map_cum)
-        std::memcpy(out->cumulative_image, h->h_pack + (size_t)h->S * 8, (size_t)h->S * isz);
+    if (h->fin_images[0]) std::memcpy(h->fin_images[0], h->h_pack, (size_t)h->S * h->fin_isz);
+    if (h->fin_images[1]) std::memcpy(h->fin_images[1], h->h_pack + (size_t)h->S * 8, (size_t)h->S * h->fin_isz);
     unsigned long long tot[4] = {0, 0, 0, 0};
     const unsigned long long *parts = reinterpret_cast<const unsigned long long *>(h_tail + 48);
-    for (int b = 0; b < n_parts; ++b)
+    for (int b = 0; b < h->fin_parts; ++b)
         for (int q = 0; q < 4; ++q) tot[q] += parts[4 * b + q];
-    for (int q = 0; q < 4; ++q) out->totals[q] = tot[q];
-    h->window_has_data = false;
-    h->win64_dirty = false;
-    h->win_events = 0;
+    if (out)
+        for (int q = 0; q < 4; ++q) out->totals[q] = tot[q];
     return LDE_OK;
+}
+
+int lde_finalize(lde_handle *h, lde_outputs *out) {
+    if (int rc = lde_finalize_begin(h, out)) return rc;
+    return lde_finalize_end(h, out);
 }
 
 int lde_finalize_partials(lde_handle *h, void *d_out) {

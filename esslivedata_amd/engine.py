@@ -98,6 +98,24 @@ class _OutputPool:
         return a
 
 
+class PendingFinalize:
+    """A finalize enqueued by ``BinningEngine.finalize(wait=False)``
+    (``lde_finalize_begin``); ``result()`` waits for it alone
+    (``lde_finalize_end``) and returns its :class:`FinalizeResult`."""
+
+    def __init__(self, engine, ref, make) -> None:
+        self._engine, self._ref, self._make, self._res = engine, ref, make, None
+
+    def result(self) -> 'FinalizeResult':
+        if self._res is None:
+            e = self._engine
+            rc = e._lib.lde_finalize_end(e._h, self._ref)
+            if rc:
+                check(rc, e._h, e._lib)
+            self._res = self._make()
+        return self._res
+
+
 _I32_MIN, _I32_MAX = -(2**31), 2**31 - 1
 
 
@@ -391,8 +409,15 @@ class BinningEngine:
             check(rc, self._h, self._lib)
         self._keepalive.clear()
 
-    def finalize(self, *, images: bool = True, hists: bool = False) -> FinalizeResult:
-        out = self._out
+    def finalize(self, *, images: bool = True, hists: bool = False, wait: bool = True):
+        """Cumulative += window, the outputs, window cleared (``lde_finalize``).
+
+        ``wait=False`` returns a :class:`PendingFinalize` at once: the finalize
+        is enqueued and the window restarted, so the next ``accumulate`` can be
+        enqueued before ``.result()`` waits for this window's outputs (the
+        device bins the next batch while the host handles these).  One
+        finalize may be pending per engine."""
+        out = _native.LdeOutputs() if not wait else self._out
         ci = mi = ch = mh = None
         if images:
             # written in place by the finalize kernel (page-locked pool)
@@ -405,21 +430,31 @@ class BinningEngine:
         out.cumulative_image = mi.ctypes.data if mi is not None else None
         out.current_hist = ch.ctypes.data if ch is not None else None
         out.cumulative_hist = mh.ctypes.data if mh is not None else None
-        rc = self._lib.lde_finalize(self._h, self._out_ref)
+        ref = self._out_ref if wait else ctypes.byref(out)
+        shape = (self._S, self._T)
+
+        def result() -> FinalizeResult:
+            t0, t1, t2, t3 = out.totals
+            return FinalizeResult(
+                current_image=ci,
+                cumulative_image=mi,
+                current_hist=ch.reshape(shape) if hists else None,
+                cumulative_hist=mh.reshape(shape) if hists else None,
+                current_total=t0,
+                current_in_range=t1,
+                cumulative_total=t2,
+                cumulative_in_range=t3,
+            )
+
+        if wait:
+            rc = self._lib.lde_finalize(self._h, ref)
+            if rc:
+                check(rc, self._h, self._lib)
+            return result()
+        rc = self._lib.lde_finalize_begin(self._h, ref)
         if rc:
             check(rc, self._h, self._lib)
-        t0, t1, t2, t3 = out.totals
-        shape = (self._S, self._T)
-        return FinalizeResult(
-            current_image=ci,
-            cumulative_image=mi,
-            current_hist=ch.reshape(shape) if hists else None,
-            cumulative_hist=mh.reshape(shape) if hists else None,
-            current_total=t0,
-            current_in_range=t1,
-            cumulative_total=t2,
-            cumulative_in_range=t3,
-        )
+        return PendingFinalize(self, ref, result)
 
     def read_histogram(self, which: str = 'current') -> np.ndarray:
         w = {'current': _native.LDE_CURRENT, 'cumulative': _native.LDE_CUMULATIVE}[which]

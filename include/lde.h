@@ -195,6 +195,19 @@ int lde_accumulate(lde_handle *h, int32_t replica);
  * accumulator raises ValueError). */
 int lde_finalize(lde_handle *h, lde_outputs *out);
 
+/* lde_finalize in two halves, so that a service can enqueue its next
+ * lde_accumulate before it waits for this window's outputs: the device bins
+ * the next batch while the host serializes and publishes the outputs of this
+ * one (the reference runs Job.get, job.py:435-467, and the next batch's
+ * Job.add one after the other on the host; the outputs are the same).  _begin enqueues the
+ * finalize and restarts the window (histogram outputs, when requested, are
+ * complete on return); _end waits for the finalize alone -- not for work
+ * enqueued after it -- and fills out->totals and the images (same `out`).
+ * One finalize may be pending per handle: _begin returns LDE_ESTATE until
+ * _end has run.  lde_finalize == _begin + _end. */
+int lde_finalize_begin(lde_handle *h, lde_outputs *out);
+int lde_finalize_end(lde_handle *h, lde_outputs *out);
+
 /* Page-locked, device-mapped host memory for finalize outputs.  An image
  * pointer of lde_outputs that lies inside such a block is written by the
  * finalize kernel directly (no staging buffer, no host copy after the wait):

@@ -442,3 +442,48 @@ def test_output_buffers_fresh_without_reuse():
         if not reuse:
             assert len({id(i) for i, _ in held}) == 4
         eng.close()
+
+
+@pytest.mark.parametrize('num_bins', [100, 1000])
+def test_finalize_overlapped_with_next_batch(num_bins):
+    """``finalize(wait=False)`` (lde_finalize_begin/_end): the next batch is
+    enqueued before the outputs are read; every window's images, totals and
+    cumulative match the synchronous engine's, a second pending finalize is
+    refused, and a window with no data is refused as with lde_finalize."""
+    import torch
+
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.engine import BinningEngine
+
+    inst = synthetic.with_toa_edges(synthetic.dream_mantle(), num_bins=num_bins, scale='log')
+    view = projection.geometric_lut(inst.detector_number, inst.coords, inst.resolution)
+    edges = inst.edges.edges_ns()
+    kw = dict(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset, n_screen=view.n_screen,
+              reuse_output_buffers=False)
+    a, b = BinningEngine(**kw), BinningEngine(**kw)
+    batches = [synthetic.dream_events(2_000_000, inst, seed=90 + k) for k in range(4)]
+    dev = [(torch.as_tensor(p, device='cuda'), torch.as_tensor(t, device='cuda')) for p, t in batches]
+    pending, got, exp = None, [], []
+    for k, (p, t) in enumerate(dev):
+        a.stage_tensors_batch([(p, t)])
+        a.accumulate(k % view.n_replicas)
+        if pending is not None:
+            got.append(pending.result())
+        pending = a.finalize(images=True, wait=False)
+        if k == 0:
+            with pytest.raises(RuntimeError, match='pending'):
+                a.finalize(images=True, wait=False)  # one pending finalize per engine
+        b.stage_tensors_batch([(p, t)])
+        b.accumulate(k % view.n_replicas)
+        exp.append(b.finalize(images=True))
+    got.append(pending.result())
+    for g, e in zip(got, exp):
+        np.testing.assert_array_equal(g.current_image, e.current_image)
+        np.testing.assert_array_equal(g.cumulative_image, e.cumulative_image)
+        assert (g.current_total, g.current_in_range, g.cumulative_total, g.cumulative_in_range) == (
+            e.current_total, e.current_in_range, e.cumulative_total, e.cumulative_in_range)
+    np.testing.assert_array_equal(a.read_histogram('cumulative'), b.read_histogram('cumulative'))
+    with pytest.raises(ValueError):
+        a.finalize(images=True, wait=False)  # nothing accumulated since
+    a.close()
+    b.close()
