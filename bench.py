@@ -29,7 +29,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-PROFILE_ROUND = 'r5'  # profiles/<round>_<workload>_bench.json (tools/prof_round.sh)
+PROFILE_ROUND = 'r6'  # profiles/<round>_<workload>_bench.json (tools/prof_round.sh)
 # bench kernel name -> device symbol in the rocprofv3 summary
 KERNEL_SYMBOL = {
     'atomic': 'k_bin_atomic',

@@ -6,7 +6,7 @@
 # strip_view wire_view mantle_front_layer"); SET=main|views kept as shorthands.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/profiles
-TAG=${TAG:-r5}
+TAG=${TAG:-r6}
 case "${SET:-}" in
   main) NAMES=${NAMES:-"dream loki wavelength monitor bifrost"} ;;
   views) NAMES=${NAMES:-"strip_view wire_view mantle_front_layer"} ;;
