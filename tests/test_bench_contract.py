@@ -56,9 +56,11 @@ def _check_line(d: dict, n_gpus: int = 1):
 
 R = bench.PROFILE_ROUND
 MAIN = ['dream', 'loki', 'wavelength']
+# round 6: the reference's larger TOA binnings on the WIDE strategy
+TOA = ['dream_t1000log', 'dream_t10000log', 'loki_t1000linear']
 
 
-@pytest.mark.parametrize('wl', MAIN)
+@pytest.mark.parametrize('wl', MAIN + TOA)
 def test_committed_bench_line_contract(wl):
     d = json.loads((ROOT / 'profiles' / f'{R}_{wl}_bench_line.json').read_text())
     _check_line(d)
@@ -78,8 +80,8 @@ def test_committed_bench_line_contract(wl):
     assert t['read'] >= 0.95 * bench.BYTES_PER_EVENT * events_per_launch
 
 
-@pytest.mark.parametrize('wl', MAIN + ['monitor', 'bifrost', 'strip_view', 'wire_view',
-                                       'mantle_front_layer'])
+@pytest.mark.parametrize('wl', MAIN + TOA + ['monitor', 'bifrost', 'strip_view', 'wire_view',
+                                             'mantle_front_layer'])
 def test_traced_line_agrees_with_its_profile(wl):
     """The bench line printed by the traced run itself (tools/prof_round.sh,
     every step stamped) and the rocprofv3 kernel average of the same run agree
