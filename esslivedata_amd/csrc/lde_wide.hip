@@ -818,6 +818,7 @@ __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int kWideAccThreads = 1024;
 constexpr int kWideAccDepth = 4;  // pages in flight per wave
+template <int D>
 __global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4 *__restrict__ items,
                                                                      const uint32_t *__restrict__ item_count,
                                                                      const uint32_t *__restrict__ item_count1,
@@ -830,7 +831,6 @@ __global__ __launch_bounds__(kWideAccThreads) void k_wide_accumulate(const uint4
                                                                      int wzero) {
     constexpr int NB = 1 << kWideTileBits;
     constexpr int NW = kWideAccThreads / 64;
-    constexpr int D = kWideAccDepth;
     __shared__ __attribute__((aligned(16))) uint32_t s_tile[NB + 64];
     __shared__ uint32_t s_pref[kWideMaxRows + 1];
     __shared__ uint32_t s_pg[kWidePagesLds], s_pc[kWidePagesLds];
@@ -1018,8 +1018,17 @@ hipError_t launch_wide(const WideArgs &a, hipStream_t st, hipEvent_t start, hipE
         max_items = a.max_items2;
         page0 = a.page0_2;
     }
-    hipExtLaunchKernelGGL(k_wide_accumulate, dim3(max_items), dim3(kWideAccThreads), 0, st, bstart, bstop, 0, items,
-                          count, count1, max_items, rows, a.list, a.page_cnt, pages, page0, colmask, a.hist, a.n_bins, a.wzero);
+#ifdef LDE_DIAGNOSTICS
+    if (a.acc_depth == 8) {  // (diagnostics: eight pages in flight per wave)
+        hipExtLaunchKernelGGL(k_wide_accumulate<8>, dim3(max_items), dim3(kWideAccThreads), 0, st, bstart, bstop, 0,
+                              items, count, count1, max_items, rows, a.list, a.page_cnt, pages, page0, colmask, a.hist,
+                              a.n_bins, a.wzero);
+        return hipGetLastError();
+    }
+#endif
+    hipExtLaunchKernelGGL(k_wide_accumulate<kWideAccDepth>, dim3(max_items), dim3(kWideAccThreads), 0, st, bstart,
+                          bstop, 0, items, count, count1, max_items, rows, a.list, a.page_cnt, pages, page0, colmask,
+                          a.hist, a.n_bins, a.wzero);
     return hipGetLastError();
 }
 

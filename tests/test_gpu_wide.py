@@ -184,3 +184,55 @@ def test_wide_counters_and_levels():
         assert eng.counter('wide_parts') <= 1024
         assert eng.counter('wide_tree_words') > 0
         eng.close()
+
+
+def _random_edges(rng, kind):
+    """Sorted float64 edges of the shapes the bucket tree must split: bin
+    widths spread over nine decades, runs of equal edges, non-integer edges
+    around integers, negative starts and spans past the int32 range."""
+    n = int(rng.integers(2, 4000))
+    if kind == 0:  # widths log-uniform from 1 ns to 1 s
+        w = 10.0 ** rng.uniform(0, 9, n - 1)
+        e = np.concatenate([[rng.uniform(-1e6, 1e6)], rng.uniform(-1e6, 1e6) + np.cumsum(w)])
+    elif kind == 1:  # clustered: most edges within a few ns of a handful of points
+        c = rng.uniform(-1e8, 1e8, 5)
+        e = np.sort(rng.choice(c, n) + rng.normal(0, 3, n))
+    elif kind == 2:  # duplicates and half-integers
+        e = np.sort(np.round(rng.uniform(-5e4, 5e4, n) * 2) / 2)
+        e[rng.integers(0, n, n // 4)] = e[0]
+        e = np.sort(e)
+    else:  # past the int32 range on both sides
+        e = np.sort(rng.uniform(-6e9, 6e9, n))
+    return np.sort(e.astype(np.float64))
+
+
+@pytest.mark.parametrize('seed', range(12))
+def test_wide_random_edges_match_oracle(seed):
+    """Randomized TOA edges through WIDE's bucket tree (forced and AUTO on a
+    2e6-event batch), TOAs drawn on, beside and between the edges; every bin
+    against the NumPy oracle.  Parity unpinned beyond the oracle's restated
+    scipp rule (`t` in bin i iff e[i] <= t < e[i+1])."""
+    from esslivedata_amd import projection
+    from esslivedata_amd.engine import BinningEngine
+
+    rng = np.random.default_rng(1000 + seed)
+    edges = _random_edges(rng, seed % 4)
+    dn = np.arange(1, 257, dtype=np.int32)
+    view = projection.logical_lut(dn)
+    n = 2_000_000
+    c = np.ceil(edges).astype(np.int64)
+    toa = np.concatenate([
+        rng.choice(np.concatenate([c - 1, c, c + 1]), n // 2),
+        rng.uniform(edges[0] - 10, edges[-1] + 10, n - n // 2).astype(np.int64)])
+    toa = np.clip(toa, -(2**31), 2**31 - 1).astype(np.int32)
+    pid = rng.integers(0, 258, n).astype(np.int32)  # ids 0 and 257 unknown
+    pix = ora.pixel_index(pid, dn)
+    exp = ora.detector_histogram(np.arange(256), 256, pix, toa, edges)
+    for strategy in ('wide', 'auto'):
+        eng = BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                            n_screen=view.n_screen, strategy=strategy)
+        eng.stage(pid, toa)
+        eng.accumulate(0)
+        got = eng.finalize(hists=True).current_hist
+        np.testing.assert_array_equal(got, exp)
+        eng.close()
