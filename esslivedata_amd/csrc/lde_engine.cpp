@@ -78,6 +78,10 @@ struct lde_handle {
     // current when cumrow_ok (kept by the wide-row finalize, launch_finalize)
     unsigned long long *d_cumrow = nullptr;
     int cumrow_ok = 0;
+    // > 0: d_cum holds the cumulative in split form (u32 low words, then u32
+    // high words, cum32 bins each): integer views with wide rows, whose
+    // finalize (k_finalize_w4) then moves 4 bytes of cumulative per bin
+    long long cum32 = 0;
     // a finalize enqueued by lde_finalize_begin, read by lde_finalize_end:
     // images to copy out of the pack (not mapped), their element size, and
     // the number of per-block total partials
@@ -2330,6 +2334,7 @@ int lde_create(const lde_config *cfg, lde_handle **out) {
     CREATE_CHECK(dev_alloc(h, &h->d_win32, (size_t)nbins));
     CREATE_CHECK(dev_alloc(h, &h->d_cum, (size_t)nbins));
     CREATE_CHECK(dev_alloc(h, &h->d_cumrow, (size_t)h->S * 2));
+    h->cum32 = (h->out_dtype != LDE_F32 && h->T % 4 == 0 && h->T > 128 && env_ll("LDE_CUM32", 1) != 0) ? nbins : 0;
     if (h->out_dtype == LDE_F32) {
         CREATE_CHECK(dev_alloc(h, &h->d_winf, (size_t)nbins));
         CREATE_CHECK(dev_alloc(h, &h->d_cumf, (size_t)nbins));
@@ -2817,7 +2822,8 @@ int lde_finalize_begin(lde_handle *h, lde_outputs *out) {
                        h->range_hi, out->current_image ? img_cur : nullptr,
                        out->cumulative_image ? img_cum : nullptr, h->d_tot4,
                        (unsigned long long *)d_tail, h->d_overflow, (uint32_t *)(d_tail + 32),
-                       h->stream, (unsigned long long *)(d_tail + 48), &n_parts, h->d_cumrow, &h->cumrow_ok));
+                       h->stream, (unsigned long long *)(d_tail + 48), &n_parts, h->d_cumrow, &h->cumrow_ok,
+                       h->cum32));
     }
     const size_t isz = f32 ? 4 : 8;
     // a system-scope release after the kernel: its host writes are visible
@@ -2831,7 +2837,14 @@ int lde_finalize_begin(lde_handle *h, lde_outputs *out) {
         convert_u64(tmp.data(), out->current_hist, (long long)nb, LDE_F64);
     }
     if (!f32 && want_cum_hist) {
-        HIPCALL(h, hipMemcpyAsync(tmp.data(), h->d_cum, nb * 8, hipMemcpyDeviceToHost, h->stream));
+        const unsigned long long *src = h->d_cum;
+        if (h->cum32) {  // the split words joined (d_snap is free again: copied above)
+            if (!h->d_snap)
+                if (int rc = dev_alloc(h, &h->d_snap, nb)) return rc;
+            HIPCALL(h, lde::launch_sum3(h->d_cum, nullptr, nullptr, h->d_snap, (long long)nb, h->stream, h->cum32));
+            src = h->d_snap;
+        }
+        HIPCALL(h, hipMemcpyAsync(tmp.data(), src, nb * 8, hipMemcpyDeviceToHost, h->stream));
         HIPCALL(h, hipStreamSynchronize(h->stream));
         convert_u64(tmp.data(), out->cumulative_hist, (long long)nb, LDE_F64);
     }
@@ -2898,7 +2911,7 @@ int lde_finalize_partials(lde_handle *h, void *d_out) {
         HIPCALL(h, lde::launch_finalize(2, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr,
                                         h->d_cum, nullptr, h->S, h->T, h->range_lo, h->range_hi,
                                         o, o + h->S, h->d_tot4, o + 2 * h->S, nullptr, nullptr,
-                                        h->stream, nullptr, nullptr, h->d_cumrow, &h->cumrow_ok));
+                                        h->stream, nullptr, nullptr, h->d_cumrow, &h->cumrow_ok, h->cum32));
     }
     if (h->out_dtype == LDE_F32)  // the window's f32 accumulator restarts too
         HIPCALL(h, hipMemsetAsync(h->d_winf, 0, (size_t)h->nbins * 4, h->stream));
@@ -2932,7 +2945,7 @@ int lde_read_histogram(lde_handle *h, int32_t which, void *host_out) {
     if (which == LDE_CURRENT)
         HIPCALL(h, lde::launch_sum3(w64, nullptr, h->d_win32, h->d_snap, h->nbins, h->stream));
     else
-        HIPCALL(h, lde::launch_sum3(h->d_cum, w64, h->d_win32, h->d_snap, h->nbins, h->stream));
+        HIPCALL(h, lde::launch_sum3(h->d_cum, w64, h->d_win32, h->d_snap, h->nbins, h->stream, h->cum32));
     std::vector<unsigned long long> tmp(nb);
     HIPCALL(h, hipMemcpyAsync(tmp.data(), h->d_snap, nb * 8, hipMemcpyDeviceToHost, h->stream));
     HIPCALL(h, hipStreamSynchronize(h->stream));
@@ -3020,7 +3033,7 @@ int lde_group_spectra(lde_handle *h, int32_t slot, int32_t which, void *host_out
                        f32 ? 2 : (which == LDE_CUMULATIVE ? 1 : 0), gs.d_items, gs.n_items,
                        gs.d_screens, h->T, h->d_win32, h->win64_dirty ? h->d_win64 : nullptr,
                        h->d_cum, f32 ? (which == LDE_CUMULATIVE ? h->d_cumf : h->d_winf) : nullptr,
-                       gs.d_out, h->stream));
+                       gs.d_out, h->stream, h->cum32));
     }
     std::vector<unsigned long long> tmp(n);
     HIPCALL(h, hipMemcpyAsync(tmp.data(), gs.d_out, n * 8, hipMemcpyDeviceToHost, h->stream));

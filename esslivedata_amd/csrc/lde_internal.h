@@ -287,15 +287,16 @@ hipError_t launch_merge_f32_u64(const unsigned long long *src, unsigned long lon
                                 float *cumf, long long n, int first_win, int first_cum,
                                 hipStream_t st);
 hipError_t launch_push_export(uint32_t *batch, unsigned long long *out, long long n, hipStream_t st);
+// a32: a is a split cumulative of a32 bins (u32 low words, then high words)
 hipError_t launch_sum3(const unsigned long long *a, const unsigned long long *b, const uint32_t *c,
-                       unsigned long long *out, long long n, hipStream_t st);
+                       unsigned long long *out, long long n, hipStream_t st, long long a32 = 0);
 hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *win64,
                            unsigned long long *cum, unsigned long long *snap, long long S, int T,
                            int lo, int hi, void *cur_img, void *cum_img,
                            unsigned long long *totals, unsigned long long *tot_copy,
                            const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st,
                            unsigned long long *host_parts = nullptr, int *n_parts = nullptr,
-                           unsigned long long *cumrow = nullptr, int *cumrow_ok = nullptr);
+                           unsigned long long *cumrow = nullptr, int *cumrow_ok = nullptr, long long cum32 = 0);
 // cumrow: 2 x S u64, each screen's cumulative sum in the TOA range and over
 // all bins.  *cumrow_ok in: they are current (the wide-row finalize then skips
 // the cumulative of groups the window left empty); out: current afterwards.
@@ -313,7 +314,7 @@ constexpr int GROUP_ITEM = 64;  // screens per work item of k_group_spectra
 hipError_t launch_group_spectra(int mode, const int4 *items, int n_items, const int *screens,
                                 int T, const uint32_t *win32, const unsigned long long *win64,
                                 const unsigned long long *cum, const float *fsrc,
-                                unsigned long long *out, hipStream_t st);
+                                unsigned long long *out, hipStream_t st, long long cum32 = 0);
 
 // wavelength mode (lde_coord.hip): per-event coordinate bin via a (distance,
 // time) lookup table, written as the int32 "time" of a second binning pass

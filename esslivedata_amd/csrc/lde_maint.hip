@@ -71,13 +71,22 @@ __global__ void k_push_export(uint32_t *__restrict__ batch, unsigned long long *
 }
 
 // snapshot: out = a (+ b) (+ c) as u64, for reads that must not finalize
+// A cumulative in split form (cum32 = its bin count, wide-row views): u32 low
+// words [cum32] then u32 high words [cum32], so the finalize moves 4 bytes per
+// bin instead of 8 and carries into the high word only on a wrap.
+__device__ __forceinline__ unsigned long long cum_at(const unsigned long long *cum, long long cum32, size_t i) {
+    if (!cum32) return cum[i];
+    const uint32_t *lo = reinterpret_cast<const uint32_t *>(cum);
+    return (unsigned long long)lo[i] | ((unsigned long long)lo[cum32 + i] << 32);
+}
+
 __global__ void k_sum3(const unsigned long long *__restrict__ a, const unsigned long long *__restrict__ b,
                        const uint32_t *__restrict__ c, unsigned long long *__restrict__ out,
-                       long long n) {
+                       long long n, long long a32) {
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x) {
-        unsigned long long v = c[i];
-        if (a) v += a[i];
+        unsigned long long v = c ? c[i] : 0ull;
+        if (a) v += cum_at(a, a32, (size_t)i);
         if (b) v += b[i];
         out[i] = v;
     }
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(256) void k_finalize_v4(uint32_t *__restrict__ win3
 // loads and 2 x 16-byte cumulative loads and stores, two row slices in flight
 // per lane (k_finalize's scalar loop held one 4-byte load per lane in flight:
 // 3.7 TB/s on DREAM at 1,000 bins).
-template <typename OUT>
+template <typename OUT, bool CUM32, bool INC>
 __global__ __launch_bounds__(256) void k_finalize_w4(uint32_t *__restrict__ win32,
                                                      unsigned long long *__restrict__ win64,
                                                      unsigned long long *__restrict__ cum,
@@ -255,8 +264,9 @@ __global__ __launch_bounds__(256) void k_finalize_w4(uint32_t *__restrict__ win3
                                                      unsigned long long *__restrict__ totals,
                                                      const uint32_t *__restrict__ ovf_src,
                                                      uint32_t *__restrict__ ovf_dst,
-                                                     unsigned long long *__restrict__ cumrow, int inc) {
+                                                     unsigned long long *__restrict__ cumrow, long long cum32) {
     typedef unsigned long long u64;
+    constexpr bool inc = INC;
     __shared__ u64 s_tot[4][4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     u64 acc[4] = {0, 0, 0, 0};
@@ -278,7 +288,32 @@ __global__ __launch_bounds__(256) void k_finalize_w4(uint32_t *__restrict__ win3
             // window left empty neither reads nor writes the cumulative
             const bool nz = (w[0] | w[1] | w[2] | w[3]) != 0;
             u64 c[4] = {0, 0, 0, 0};
-            if (!inc || nz) {
+            if (CUM32 && (!inc || nz)) {
+                // split form: low words read and written, a wrap carries into
+                // the high word (read only to recompute the sums)
+                uint32_t *lo32 = reinterpret_cast<uint32_t *>(cum);
+                uint32_t *hi32 = lo32 + cum32;
+                const uint4 l4 = *reinterpret_cast<const uint4 *>(lo32 + k);
+                const uint32_t l[4] = {l4.x, l4.y, l4.z, l4.w};
+                uint32_t nl[4], cy[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    nl[q] = l[q] + (uint32_t)w[q];
+                    cy[q] = (uint32_t)(w[q] >> 32) + (nl[q] < l[q] ? 1u : 0u);
+                }
+                if (!inc) {
+                    const uint4 h4 = *reinterpret_cast<const uint4 *>(hi32 + k);
+                    const uint32_t h[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) c[q] = (((u64)h[q] << 32) | l[q]) + w[q];
+                }
+                if (nz) {
+                    *reinterpret_cast<uint4 *>(lo32 + k) = make_uint4(nl[0], nl[1], nl[2], nl[3]);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (cy[q]) hi32[k + q] += cy[q];  // (this thread owns the bin)
+                }
+            } else if (!CUM32 && (!inc || nz)) {
                 const ulonglong2 c01 = *reinterpret_cast<const ulonglong2 *>(cum + k);
                 const ulonglong2 c23 = *reinterpret_cast<const ulonglong2 *>(cum + k + 2);
                 c[0] = c01.x + w[0];
@@ -458,7 +493,7 @@ __global__ __launch_bounds__(128) void k_group_spectra(
     int mode, const int4 *__restrict__ items, const int *__restrict__ screens, int T,
     const uint32_t *__restrict__ win32, const unsigned long long *__restrict__ win64,
     const unsigned long long *__restrict__ cum, const float *__restrict__ fsrc,
-    unsigned long long *__restrict__ out) {
+    unsigned long long *__restrict__ out, long long cum32) {
     const int4 it = items[blockIdx.x];  // {group, begin, end, single}
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         unsigned long long acc = 0;
@@ -472,7 +507,9 @@ __global__ __launch_bounds__(128) void k_group_spectra(
             } else {
                 acc += (unsigned long long)win32[i0] + win32[i1] + win32[i2] + win32[i3];
                 if (win64) acc += win64[i0] + win64[i1] + win64[i2] + win64[i3];
-                if (mode == 1) acc += cum[i0] + cum[i1] + cum[i2] + cum[i3];
+                if (mode == 1)
+                    acc += cum_at(cum, cum32, i0) + cum_at(cum, cum32, i1) + cum_at(cum, cum32, i2) +
+                           cum_at(cum, cum32, i3);
             }
         }
         for (; k < it.z; ++k) {
@@ -482,7 +519,7 @@ __global__ __launch_bounds__(128) void k_group_spectra(
             } else {
                 acc += win32[i];
                 if (win64) acc += win64[i];
-                if (mode == 1) acc += cum[i];
+                if (mode == 1) acc += cum_at(cum, cum32, i);
             }
         }
         unsigned long long *o = out + (size_t)it.x * T + t;
@@ -523,8 +560,8 @@ hipError_t launch_push_export(uint32_t *batch, unsigned long long *out, long lon
 }
 
 hipError_t launch_sum3(const unsigned long long *a, const unsigned long long *b, const uint32_t *c,
-                       unsigned long long *out, long long n, hipStream_t st) {
-    hipLaunchKernelGGL(k_sum3, dim3(grid_for(n)), dim3(256), 0, st, a, b, c, out, n);
+                       unsigned long long *out, long long n, hipStream_t st, long long a32) {
+    hipLaunchKernelGGL(k_sum3, dim3(grid_for(n)), dim3(256), 0, st, a, b, c, out, n, a32);
     return hipGetLastError();
 }
 
@@ -537,7 +574,7 @@ static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsign
                               void *cur_img, void *cum_img, unsigned long long *totals,
                               unsigned long long *tot_copy, const uint32_t *ovf_src,
                               uint32_t *ovf_dst, unsigned long long *host_parts, int *n_parts,
-                              hipStream_t st, unsigned long long *cumrow, int *cumrow_ok) {
+                              hipStream_t st, unsigned long long *cumrow, int *cumrow_ok, long long cum32) {
     const bool v4 = T % 4 == 0 && T <= 128;
     const long long rows_per_block = v4 ? 8 : 4;
     long long blocks = (S + rows_per_block - 1) / rows_per_block;
@@ -550,10 +587,18 @@ static void launch_finalize_t(uint32_t *win32, unsigned long long *win64, unsign
     if (v4)
         hipLaunchKernelGGL(k_finalize_v4<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
                            cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, dst, ks, kd);
-    else if (T % 4 == 0)
-        hipLaunchKernelGGL(k_finalize_w4<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
-                           cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, dst, ks, kd, cumrow,
-                           cumrow && cumrow_ok && *cumrow_ok ? 1 : 0);
+    else if (T % 4 == 0) {
+        // (the per-screen sums current: empty groups skip the cumulative)
+        const bool inc = cumrow && cumrow_ok && *cumrow_ok;
+#define LDE_FW4(C, I)                                                                                        \
+    hipLaunchKernelGGL((k_finalize_w4<OUT, C, I>), dim3((unsigned)blocks), dim3(256), 0, st, win32, win64, cum, \
+                       snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, dst, ks, kd, cumrow, C ? cum32 : 0LL)
+        if (cum32 && inc) LDE_FW4(true, true);
+        else if (cum32) LDE_FW4(true, false);
+        else if (inc) LDE_FW4(false, true);
+        else LDE_FW4(false, false);
+#undef LDE_FW4
+    }
     else
         hipLaunchKernelGGL(k_finalize<OUT>, dim3((unsigned)blocks), dim3(256), 0, st, win32, win64,
                            cum, snap, S, T, lo, hi, (OUT *)cur_img, (OUT *)cum_img, dst, ks, kd);
@@ -573,15 +618,17 @@ hipError_t launch_finalize(int img_kind, uint32_t *win32, unsigned long long *wi
                            unsigned long long *totals, unsigned long long *tot_copy,
                            const uint32_t *ovf_src, uint32_t *ovf_dst, hipStream_t st,
                            unsigned long long *host_parts, int *n_parts, unsigned long long *cumrow,
-                           int *cumrow_ok) {
+                           int *cumrow_ok, long long cum32) {
     if (img_kind == 1) return hipErrorInvalidValue;
+    // the split cumulative exists for wide rows only (k_finalize_w4)
+    if (cum32 && !(T % 4 == 0 && T > 128)) return hipErrorInvalidValue;
     if (img_kind == 2)
         launch_finalize_t<unsigned long long>(win32, win64, cum, snap, S, T, lo, hi, cur_img,
                                               cum_img, totals, tot_copy, ovf_src, ovf_dst,
-                                              host_parts, n_parts, st, cumrow, cumrow_ok);
+                                              host_parts, n_parts, st, cumrow, cumrow_ok, cum32);
     else
         launch_finalize_t<double>(win32, win64, cum, snap, S, T, lo, hi, cur_img, cum_img, totals,
-                                  tot_copy, ovf_src, ovf_dst, host_parts, n_parts, st, cumrow, cumrow_ok);
+                                  tot_copy, ovf_src, ovf_dst, host_parts, n_parts, st, cumrow, cumrow_ok, cum32);
     return hipGetLastError();
 }
 
@@ -603,10 +650,10 @@ hipError_t launch_finalize_f32(uint32_t *batch, unsigned long long *win64, unsig
 hipError_t launch_group_spectra(int mode, const int4 *items, int n_items, const int *screens,
                                 int T, const uint32_t *win32, const unsigned long long *win64,
                                 const unsigned long long *cum, const float *fsrc,
-                                unsigned long long *out, hipStream_t st) {
+                                unsigned long long *out, hipStream_t st, long long cum32) {
     if (n_items <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_group_spectra, dim3((unsigned)n_items), dim3(128), 0, st, mode, items,
-                       screens, T, win32, win64, cum, fsrc, out);
+                       screens, T, win32, win64, cum, fsrc, out, cum32);
     return hipGetLastError();
 }
 

@@ -236,3 +236,46 @@ def test_wide_random_edges_match_oracle(seed):
         got = eng.finalize(hists=True).current_hist
         np.testing.assert_array_equal(got, exp)
         eng.close()
+
+
+def test_split_cumulative_carries_past_2_32():
+    """Views with wide rows keep the cumulative as u32 low words + high words
+    (k_finalize_w4 moves 4 bytes per bin): windows imported as uint64 counts
+    past 2^32 (lde_import_window_u64) force both carries, a low word that
+    wraps and a window count with high bits; the cumulative histogram, its
+    readback, group spectra and totals equal the exact uint64 sums."""
+    import torch
+
+    from esslivedata_amd import projection
+    from esslivedata_amd.engine import BinningEngine
+
+    dn = np.arange(1, 65, dtype=np.int32)
+    view = projection.logical_lut(dn)
+    T = 200
+    edges = np.linspace(0, 71.43, T + 1) * 1e6
+    eng = BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                        n_screen=view.n_screen)
+    rng = np.random.default_rng(5)
+    n = 64 * T
+    cum = np.zeros(n, dtype=np.uint64)
+    eng.set_groups(0, [np.arange(0, 64, 2), np.arange(10, 20), np.array([63])])
+    for step in range(4):
+        w = rng.integers(0, 2**32, n, dtype=np.uint64)
+        w[rng.integers(0, n, n // 3)] = 0  # empty groups too
+        w[:8] = 2**32 - 1  # low words wrap from the second window on
+        w[8:16] = np.uint64(2**33 + 7)  # counts with high bits
+        d = torch.as_tensor(w.view(np.int64), device='cuda')
+        eng.import_window_u64(d.data_ptr())
+        torch.cuda.synchronize()
+        cum += w
+        res = eng.finalize(images=True, hists=True)
+        np.testing.assert_array_equal(res.cumulative_hist.ravel(), cum.astype(np.float64))
+        assert res.cumulative_total == int(cum.sum(dtype=np.uint64))
+        np.testing.assert_array_equal(
+            res.cumulative_image, cum.reshape(64, T).sum(axis=1, dtype=np.uint64).astype(np.float64))
+    np.testing.assert_array_equal(eng.read_histogram('cumulative').ravel(), cum.astype(np.float64))
+    spec = eng.group_spectra(0, 'cumulative')
+    c2 = cum.reshape(64, T)
+    exp = np.stack([c2[0:64:2].sum(0, dtype=np.uint64), c2[10:20].sum(0, dtype=np.uint64), c2[63]])
+    np.testing.assert_array_equal(spec, exp.astype(np.float64))
+    eng.close()
