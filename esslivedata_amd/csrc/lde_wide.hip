@@ -182,8 +182,11 @@ struct PartLds {
     uint2 *pg;       // per partition: {page of the run's first entries, first new page}
 };
 
-__host__ __device__ constexpr size_t part_words(int P) {
-    return (size_t)UNIT + 3 * (size_t)align4(P) + 2 * ((size_t)align4(P) + 64) + 3 * (size_t)align4(P) + 32 + 4;
+// sub: rank counters per partition (lane groups of 64 / sub lanes each own
+// one), so lanes of one wave that hit the same partition spread over sub
+// counters; the counts become per-group staging offsets after the scan
+__host__ __device__ constexpr size_t part_words(int P, int sub = 1) {
+    return (size_t)UNIT + 3 * (size_t)align4(P) + 2 * ((size_t)align4(P) * sub + 64) + 3 * (size_t)align4(P) + 32 + 4;
 }
 constexpr int kWideMaxTpb = 256;  // tiles per band (second pass partitions)
 // first pass: partition layout | pixel table | TOA tree | chunk table
@@ -191,15 +194,16 @@ constexpr size_t kWideScatterWords = part_words(kWideMaxParts) + ((size_t)1 << k
                                      sizeof(PixChunk) / 4 * kWideLdsChunks;
 static_assert(kWideScatterWords * 4 <= 160 * 1024, "first pass LDS");
 // second pass: partition layout | item row prefix | staged page ids, counts
-constexpr size_t kWideSplitWords = part_words(kWideMaxTpb) + kWideMaxRows + 1 + 2 * 1024;
+constexpr int kWideSplitSub = 4;  // the second pass: few partitions (<= 256 tiles of a band)
+constexpr size_t kWideSplitWords = part_words(kWideMaxTpb, kWideSplitSub) + kWideMaxRows + 1 + 2 * 1024;
 
-__device__ __forceinline__ PartLds part_lds(uint32_t *sm, int P) {
+__device__ __forceinline__ PartLds part_lds(uint32_t *sm, int P, int sub = 1) {
     const uint32_t P4 = (uint32_t)align4(P);
     PartLds s;
     s.stg = sm;
     s.cnt0 = s.stg + UNIT + 3 * P4;
-    s.cnt1 = s.cnt0 + P4 + 64;
-    s.offw = s.cnt1 + P4 + 64;
+    s.cnt1 = s.cnt0 + P4 * (uint32_t)sub + 64;
+    s.offw = s.cnt1 + P4 * (uint32_t)sub + 64;
     s.pg = reinterpret_cast<uint2 *>(s.offw + P4);  // (8-byte aligned: P4 a multiple of 4)
     s.w = s.offw + 3 * P4;
     s.pool = s.w + 32;
@@ -216,7 +220,7 @@ struct Owner {  // registers of the owner thread of one partition
 // runs right after the rank atomics (the next unit's loads), mid() between
 // the staging and the write-out (the next unit's front end, whose gathers
 // then fly behind the write-out).
-template <bool E16, int ABL = 0, typename NEXT, typename MID>
+template <bool E16, int ABL = 0, int SUB = 1, typename NEXT, typename MID>
 __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, uint32_t emask, int parity,
                                           const uint32_t (&key)[EPT], Owner &own, uint32_t pool_base,
                                           uint32_t cap, __amdgpu_buffer_rsrc_t pool, uint32_t *__restrict__ page_cnt,
@@ -225,19 +229,26 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
     const uint32_t P4 = (uint32_t)align4(P);
     uint32_t *cnt = parity ? s.cnt1 : s.cnt0;
     uint32_t *cnt_next = parity ? s.cnt0 : s.cnt1;
-    const uint32_t dummy = P4 + (uint32_t)(tid & 63);
+    const uint32_t dummy = P4 * SUB + (uint32_t)(tid & 63);
+    // this lane's counter of a partition (SUB > 1: its lane group's)
+    const uint32_t grp = SUB > 1 ? (uint32_t)(tid & 63) / (64u / SUB) : 0u;
     uint32_t rank[EPT];
 #pragma unroll
     for (int e = 0; e < EPT; ++e)
-        rank[e] = __hip_atomic_fetch_add(cnt + (key[e] != kNone ? key[e] >> pbits : dummy), 1u, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+        rank[e] = __hip_atomic_fetch_add(cnt + (key[e] != kNone ? (key[e] >> pbits) * SUB + grp : dummy), 1u,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     next();
     __syncthreads();
     uint32_t n = 0, v = 0;
+    uint32_t sc[SUB];
     if (tid < P) {
-        n = cnt[tid];
+#pragma unroll
+        for (int c = 0; c < SUB; ++c) {
+            sc[c] = cnt[tid * SUB + c];
+            n += sc[c];
+            cnt_next[tid * SUB + c] = 0;
+        }
         v = (n + 3u) & ~3u;
-        cnt_next[tid] = 0;
     }
     // exclusive scan of the padded runs with one barrier: every wave adds
     // the totals of the waves before it itself (16 broadcast LDS reads)
@@ -257,6 +268,15 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)x, NT / 64 - 1);
     const uint32_t wbase = wid ? (uint32_t)__builtin_amdgcn_readlane((int)x, wid - 1) : 0u;
     const uint32_t off = wbase + inc - v;
+    if (SUB > 1 && tid < P) {
+        // the lane groups' staging offsets, over their counts
+        uint32_t o = off;
+#pragma unroll
+        for (int c = 0; c < SUB; ++c) {
+            cnt[tid * SUB + c] = o;
+            o += sc[c];
+        }
+    }
     if (tid < P && n > 0) {
         for (uint32_t j = n; j < v; ++j) s.stg[off + j] = kNone;  // the run's pads
         // the run occupies positions [fill, fill + v) of the partition's
@@ -311,7 +331,8 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
         const bool ok = key[e] != kNone;
-        const uint32_t o = s.offw[ok ? key[e] >> pbits : 0u] & 0xFFFFu;
+        const uint32_t o = SUB > 1 ? cnt[ok ? (key[e] >> pbits) * SUB + grp : 0u]
+                                   : s.offw[ok ? key[e] >> pbits : 0u] & 0xFFFFu;
         uint32_t *dst = ok ? s.stg + o + rank[e] : cnt_next + dummy;
         *dst = key[e];
     }
@@ -734,14 +755,14 @@ __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
     if (item == kNone) return;
     const uint4 it = a.items1[item];
     const int P = 1 << a.tpb_bits;
-    const PartLds s = part_lds(sm, kWideMaxTpb);
-    uint32_t *s_pref = sm + part_words(kWideMaxTpb);
+    const PartLds s = part_lds(sm, kWideMaxTpb, kWideSplitSub);
+    uint32_t *s_pref = sm + part_words(kWideMaxTpb, kWideSplitSub);
     uint32_t *s_pg = s_pref + kWideMaxRows + 1;
     uint32_t *s_pc = s_pg + kWidePagesLds;
     __shared__ unsigned long long s_ev[16];
     const int tid = threadIdx.x;
     const uint32_t band = it.x, r0 = it.y, nr = it.z - it.y;
-    for (int i = tid; i < 2 * (kWideMaxTpb + 64); i += NT) s.cnt0[i] = 0;
+    for (int i = tid; i < 2 * (kWideMaxTpb * kWideSplitSub + 64); i += NT) s.cnt0[i] = 0;
     // the item's entries size its pool (one allocation per item)
     unsigned long long ev = (uint32_t)tid < nr ? a.rows1.ev[(size_t)(r0 + tid) * a.rows1.ncols + band] : 0u;
 #pragma unroll
@@ -804,7 +825,8 @@ __global__ __launch_bounds__(NT) void k_wide_split(WideArgs a) {
         for (uint32_t v = 0; v < n_units; ++v, ++u) {
 #pragma unroll
             for (int e = 0; e < EPT; ++e) key[e] = nxt[e];
-            part_unit<true>(s, P, kWideTileBits, (1u << kWideTileBits) - 1u, (int)(u & 1), key, own, pool_base, cap,
+            part_unit<true, 0, kWideSplitSub>(s, P, kWideTileBits, (1u << kWideTileBits) - 1u, (int)(u & 1), key, own,
+                                              pool_base, cap,
                             pool, a.page_cnt, a.page_part, a.overflow,
                             [&]() __attribute__((always_inline)) { load(v + 1, nxt); },
                             []() {});
@@ -982,7 +1004,8 @@ static unsigned plan_grid(int parts) { return (unsigned)((parts + kPlanWaves - 1
 
 hipError_t launch_wide(const WideArgs &a, hipStream_t st, hipEvent_t start, hipEvent_t stop, hipEvent_t bstart,
                        hipEvent_t bstop) {
-    if (a.n_parts < 1 || a.n_parts > kWideMaxParts || a.grid1 < 1 || a.grid1 > kWideMaxRows)
+    if (a.n_parts < 1 || a.n_parts > kWideMaxParts || a.grid1 < 1 || a.grid1 > kWideMaxRows ||
+        (a.levels == 2 && a.n_parts > kWideMaxBands))
         return hipErrorInvalidValue;
     hipError_t e = a.lut16 ? (a.toa.lds ? launch_scatter_tl<true, true>(a, st, start, stop)
                              : launch_scatter_tl<true, false>(a, st, start, stop))
