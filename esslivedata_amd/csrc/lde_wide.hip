@@ -571,7 +571,9 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
             else
                 g[e] = L16 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(lut, (int)off, 0, 0)
                            : __builtin_amdgcn_raw_buffer_load_b32(lut, (int)off, 0, 0);
-            w[e] = hit ? w[e] : kNone;
+            // a hit keeps its word with the valid bit cleared, so no word --
+            // not a dropped pixel's under tag 511 either -- reads as kNone
+            w[e] = hit ? (w[e] & ~kTabValid) : kNone;
         }
     };
     auto finish = [&](uint32_t (&key)[EPT]) __attribute__((always_inline)) {

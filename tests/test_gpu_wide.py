@@ -279,3 +279,31 @@ def test_split_cumulative_carries_past_2_32():
     exp = np.stack([c2[0:64:2].sum(0, dtype=np.uint64), c2[10:20].sum(0, dtype=np.uint64), c2[63]])
     np.testing.assert_array_equal(spec, exp.astype(np.float64))
     eng.close()
+
+
+def test_wide_hot_dropped_pixels_under_the_last_tag():
+    """A view of 2^22 pixels keeps WIDE's 2^13-slot pixel table with tags up
+    to 511; hot pixels with no screen (LUT -1) whose table words carry tag 511
+    must stay dropped (their word once equalled the front end's 'no word'
+    marker, which would have sent them to screen 0)."""
+    from esslivedata_amd.engine import BinningEngine
+
+    L, S = 1 << 22, 1000
+    lut = (np.arange(L, dtype=np.int64) % S).astype(np.int32)
+    hot = np.arange(4_190_000, 4_190_064)
+    lut[hot] = -1
+    lut[5:9] = -1  # dropped pixels under tag 0 as well
+    edges = np.geomspace(0.5, 71.43, 1001) * 1e6
+    rng = np.random.default_rng(11)
+    n = 3_000_000
+    pid = np.where(rng.random(n) < 0.5, rng.choice(hot, n), rng.integers(0, L, n)).astype(np.int32)
+    toa = rng.uniform(0.4e6, 72e6, n).astype(np.int32)
+    exp = ora.detector_histogram(lut, S, pid.astype(np.int64), toa, edges)
+    for strategy in ('wide', 'auto'):
+        eng = BinningEngine(toa_edges_ns=edges, out_lut=lut, pid_offset=0, n_screen=S, strategy=strategy)
+        eng.stage(pid, toa)
+        eng.accumulate(0)
+        assert eng.info()['last_strategy'] == 'wide'
+        got = eng.finalize(hists=True).current_hist
+        np.testing.assert_array_equal(got, exp)
+        eng.close()
