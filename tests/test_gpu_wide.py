@@ -307,3 +307,48 @@ def test_wide_hot_dropped_pixels_under_the_last_tag():
         got = eng.finalize(hists=True).current_hist
         np.testing.assert_array_equal(got, exp)
         eng.close()
+
+
+def test_wide_windows_with_mixed_strategies():
+    """Windows whose batches take different strategies (WIDE, then a small
+    batch on ATOMIC in the same window): the fresh-window store-only flush,
+    the read-modify-write flush and the per-screen cumulative sums across
+    them.  Three windows at 1,000 bins: WIDE only, WIDE + ATOMIC, WIDE only;
+    current and cumulative histograms against the C oracle."""
+    import torch
+
+    from esslivedata_amd.engine import BinningEngine
+    from oracle import c_oracle
+
+    inst, view, ps = _setup('dream', 1000, 'log')
+    edges = inst.edges.edges_ns()
+    eng = BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                        n_screen=view.n_screen)
+    cur = c_oracle.CDetectorView(inst.detector_number, ps, view.n_screen, edges)
+    cum = np.zeros(view.n_screen * 1000, dtype=np.int64)
+    plan = [[2_000_000], [2_000_000, 50_000], [1_500_000]]
+    seed = 300
+    for w, sizes in enumerate(plan):
+        cur.hist[:] = 0
+        strategies = []
+        for n in sizes:
+            pid, toa = synthetic_events(inst, n, seed)
+            seed += 1
+            eng.stage_tensors_batch([(torch.as_tensor(pid, device='cuda'), torch.as_tensor(toa, device='cuda'))])
+            eng.accumulate(0)
+            strategies.append(eng.info()['last_strategy'])
+            cur.accumulate(pid, toa, 0)
+        assert strategies[0] == 'wide' and (len(sizes) == 1 or strategies[1] == 'atomic')
+        res = eng.finalize(hists=True)
+        ref = cur.hist.astype(np.int64)
+        cum += ref
+        np.testing.assert_array_equal(res.current_hist.ravel(), ref.astype(np.float64))
+        np.testing.assert_array_equal(res.cumulative_hist.ravel(), cum.astype(np.float64))
+        assert res.current_total == int(ref.sum())
+    eng.close()
+
+
+def synthetic_events(inst, n, seed):
+    from esslivedata_amd import synthetic
+
+    return synthetic.dream_events(n, inst, seed=seed)
