@@ -82,7 +82,7 @@ MONITOR_VARIANTS = [{}]
 
 @pytest.mark.parametrize('layout', ['large', 'small'])
 @pytest.mark.parametrize('variant', range(len(MONITOR_VARIANTS)))
-@pytest.mark.parametrize('n_bins', [100, 7, 1000, 3000])
+@pytest.mark.parametrize('n_bins', [100, 7, 1000, 3000, 10000])
 def test_monitor_matches_oracle(n_bins, variant, layout, request):
     """Several messages per launch, message sizes not multiples of 4 or of
     the grid; each message gets its own range of blocks."""
