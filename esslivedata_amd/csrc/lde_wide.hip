@@ -18,21 +18,23 @@
 //                     (WideToa), key = screen * T + bin; rank by partition
 //                     (LDS atomics), block scan, page allocation from the
 //                     block's pool (owner thread per partition), key-sorted
-//                     LDS staging, and every run appended to its partition's
-//                     open page with per-lane stores (a run's lanes write
-//                     consecutive entries of one page).  At its end the
-//                     block sorts its pages by partition into its page list
-//                     and writes, per partition, pages / entries / list
-//                     offset (WideRows).
-//   k_wide_plan       per partition: work items (partition, range of rows)
-//                     of at most ~item_max entries
+//                     LDS staging (runs padded to 4), and each run appended
+//                     to its partition's open page in groups of four entries
+//                     (8- or 16-byte buffer stores).  At its end the block
+//                     sorts its pages by partition into its page list and
+//                     writes, per partition, pages / entries / list offset
+//                     (WideRows).
+//   k_wide_plan       a wave per partition: work items (partition, range of
+//                     rows) of at most ~item_max entries, one reservation per
+//                     block; items of multi-item (hot) partitions first
 //   k_wide_split      two-level form only (more than kWideMaxParts tiles):
 //                     per item of a band, its u32 band-local keys partitioned
-//                     by tile exactly as the first pass does
+//                     by tile as the first pass does, with a rank counter per
+//                     16-lane group (few partitions per band)
 //   k_wide_accumulate per item of a tile: its pages histogrammed in a 128 KB
-//                     LDS tile, then added to the window (a plain 16-byte
-//                     read-modify-write when the tile has one item, global
-//                     atomics when hot tiles are split over several)
+//                     LDS tile, then added to the window (store-only on a
+//                     fresh window, a 16-byte read-modify-write when the tile
+//                     has one item, global atomics when hot tiles are split)
 //
 // Counts are integers and every event is added exactly once whatever the
 // table holds or how the work is split, so the histogram is bit-identical to
