@@ -1630,6 +1630,7 @@ int bin_wide(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunk
 #ifdef LDE_DIAGNOSTICS
     a.ablate = (int)env_ll("LDE_WIDE_ABLATE", 0);
     a.acc_depth = (int)env_ll("LDE_WIDE_ACC_DEPTH", 4);
+    a.tree_hybrid = (int)env_ll("LDE_WIDE_TREE_HYBRID", 1);
 #endif
     // an integer view's u32 window is all zero until its first batch after
     // a finalize / clear (both zero it; win_events counts what this window's

@@ -529,6 +529,7 @@ struct WideArgs {
     int ablate = 0;              // LDE_WIDE_ABLATE (diagnostics build): first-pass timing ablations
     int wzero = 0;               // 1: the window is all zero before this batch (pass B stores, reads nothing)
     int acc_depth = 4;           // pass-B pages in flight per wave (diagnostics: 8)
+    int tree_hybrid = 1;         // a tree past the LDS slot: its first words from LDS (diagnostics: 0)
 };
 
 // the batch's chunk table; call before launch_wide_table / launch_wide.

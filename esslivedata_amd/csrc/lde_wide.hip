@@ -73,18 +73,26 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint3
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, (int)kRsrcWord3);
 }
 
-template <bool TL>
-__device__ __forceinline__ uint32_t tree_word(const uint32_t *tree, uint32_t i) {
-    if (TL) return tree[i];  // LDS
-    return ld_global_u32(tree + i);
+// TM: where the TOA tree is read -- 1: all of it from LDS; 2: its first
+// kWideTreeLds words (the root level first: the builder lays the tree out
+// level by level) from LDS and the rest through a buffer load that has no
+// request for an LDS-resident index; 0: all through L2 (diagnostics)
+template <int TM>
+__device__ __forceinline__ uint32_t tree_word(const uint32_t *tree, __amdgpu_buffer_rsrc_t gt, uint32_t i) {
+    if (TM == 1) return tree[i];  // LDS
+    if (TM == 0) return __builtin_amdgcn_raw_buffer_load_b32(gt, (int)(i << 2), 0, 0);
+    const bool in_lds = i < (uint32_t)kWideTreeLds;
+    const uint32_t l = tree[in_lds ? i : 0u];
+    const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(gt, (int)(in_lds ? kOOB : i << 2), 0, 0);
+    return in_lds ? l : g;
 }
 
 // TOA bins of N events t[o..o+N) (kNone: outside the edges).  All root
 // words are read first; the descent is one wave-uniform round per tree level
 // that still holds an internal node in some lane (none for most edge sets).
-template <bool TL, int N, int O>
-__device__ __forceinline__ void toa_bins(const WideToa &tp, const uint32_t *tree, const int (&t)[EPT],
-                                         uint32_t (&bin)[N]) {
+template <int TM, int N, int O>
+__device__ __forceinline__ void toa_bins(const WideToa &tp, const uint32_t *tree, __amdgpu_buffer_rsrc_t gt,
+                                         const int (&t)[EPT], uint32_t (&bin)[N]) {
     uint32_t dc[N], w[N];
     const uint32_t rmask = (1u << tp.sh0) - 1u;
 #pragma unroll
@@ -93,7 +101,7 @@ __device__ __forceinline__ void toa_bins(const WideToa &tp, const uint32_t *tree
         const bool ok = d <= tp.last && !tp.empty;
         dc[e] = ok ? d : 0u;
         bin[e] = ok ? 0u : kNone;
-        w[e] = tree_word<TL>(tree, dc[e] >> tp.sh0);
+        w[e] = tree_word<TM>(tree, gt, dc[e] >> tp.sh0);
     }
     const uint32_t fmask = (1u << tp.fb) - 1u;
     for (int lv = 1; lv <= tp.depth; ++lv) {
@@ -106,7 +114,7 @@ __device__ __forceinline__ void toa_bins(const WideToa &tp, const uint32_t *tree
 #pragma unroll
         for (int e = 0; e < N; ++e) {
             const bool in = (w[e] & 0xFFFFu) == kLeafNone;
-            const uint32_t nw = tree_word<TL>(tree, in ? (w[e] >> 16) + ((dc[e] >> sh) & fmask) : 0u);
+            const uint32_t nw = tree_word<TM>(tree, gt, in ? (w[e] >> 16) + ((dc[e] >> sh) & fmask) : 0u);
             w[e] = in ? nw : w[e];
         }
     }
@@ -505,7 +513,7 @@ __global__ __launch_bounds__(256) void k_wide_table(WideArgs a, const void *__re
 // ABL (diagnostics build only, wrong results by design): timing ablations of
 // the first pass -- 1 no gathers, 2 no page stores, 4 no staging or
 // write-out, 16 no front end (keys from a hash of the raw words)
-template <bool L16, bool TL, bool E16, int ABL = 0>
+template <bool L16, int TM, bool E16, int ABL = 0>
 __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
     // static layout for the largest partition count and table, so every LDS
     // address is a constant (fewer live scalar registers in the loop)
@@ -515,7 +523,8 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
     const uint32_t C = a.cbits ? 1u << a.cbits : 0u;
     uint32_t *s_tab = sm + part_words(kWideMaxParts);
     uint32_t *s_tree = s_tab + (1u << kWideMaxCacheBits);
-    const uint32_t tw = TL ? (uint32_t)align4(a.toa.words) : 0u;
+    const uint32_t tw = TM == 1 ? (uint32_t)align4(a.toa.words) : TM == 2 ? (uint32_t)kWideTreeLds : 0u;
+    const __amdgpu_buffer_rsrc_t gtree = make_rsrc(a.toa.tree, (uint32_t)a.toa.words * 4u);
     PixChunk *s_ctab = reinterpret_cast<PixChunk *>(s_tree + kWideTreeLds);
     const int tid = threadIdx.x;
     {  // pixel table and TOA tree, each into its own slot: every load of a
@@ -557,7 +566,7 @@ __global__ __launch_bounds__(NT) void k_wide_scatter(WideArgs a) {
     uint32_t q[EPT], w[EPT], g[EPT], bin[EPT];
     auto issue = [&]() __attribute__((always_inline)) {
         if (ABL & 16) return;
-        toa_bins<TL, EPT, 0>(a.toa, TL ? s_tree : a.toa.tree, t, bin);
+        toa_bins<TM, EPT, 0>(a.toa, s_tree, gtree, t, bin);
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
             q[e] = (uint32_t)p[e] - (uint32_t)a.pid_off;
@@ -977,15 +986,15 @@ hipError_t launch_wide_table(const WideArgs &a, const void *lut_rep, uint32_t *p
     return hipGetLastError();
 }
 
-template <bool L16, bool TL, bool E16>
+template <bool L16, int TM, bool E16>
 static hipError_t launch_scatter_t(const WideArgs &a, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
     if (wide_scatter_smem(a) > 160 * 1024) return hipErrorInvalidValue;
 #ifdef LDE_DIAGNOSTICS
-    if (a.ablate && L16 && TL && E16) {
+    if (a.ablate && L16 && TM == 1 && E16) {
         switch (a.ablate) {
 #define LDE_WABL(m)                                                                                         \
     case m:                                                                                                 \
-        hipExtLaunchKernelGGL((k_wide_scatter<true, true, true, m>), dim3(a.grid1), dim3(NT), 0, st, start, stop, \
+        hipExtLaunchKernelGGL((k_wide_scatter<true, 1, true, m>), dim3(a.grid1), dim3(NT), 0, st, start, stop, \
                               0, a);                                                                        \
         return hipGetLastError();
             LDE_WABL(1) LDE_WABL(2) LDE_WABL(3) LDE_WABL(4) LDE_WABL(5) LDE_WABL(16) LDE_WABL(18) LDE_WABL(20)
@@ -994,14 +1003,23 @@ static hipError_t launch_scatter_t(const WideArgs &a, hipStream_t st, hipEvent_t
         }
     }
 #endif
-    hipExtLaunchKernelGGL((k_wide_scatter<L16, TL, E16>), dim3(a.grid1), dim3(NT), 0, st, start, stop, 0, a);
+    hipExtLaunchKernelGGL((k_wide_scatter<L16, TM, E16>), dim3(a.grid1), dim3(NT), 0, st, start, stop, 0, a);
     return hipGetLastError();
 }
 
-template <bool L16, bool TL>
+template <bool L16, int TM>
 static hipError_t launch_scatter_tl(const WideArgs &a, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
-    return a.levels == 1 ? launch_scatter_t<L16, TL, true>(a, st, start, stop)
-                         : launch_scatter_t<L16, TL, false>(a, st, start, stop);
+    return a.levels == 1 ? launch_scatter_t<L16, TM, true>(a, st, start, stop)
+                         : launch_scatter_t<L16, TM, false>(a, st, start, stop);
+}
+
+// the tree in LDS when it fits, else its first kWideTreeLds words in LDS and
+// the rest through L2 (diagnostics: tree_hybrid = 0, all through L2)
+template <bool L16>
+static hipError_t launch_scatter_l(const WideArgs &a, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
+    if (a.toa.lds) return launch_scatter_tl<L16, 1>(a, st, start, stop);
+    if (a.tree_hybrid) return launch_scatter_tl<L16, 2>(a, st, start, stop);
+    return launch_scatter_tl<L16, 0>(a, st, start, stop);
 }
 
 static unsigned plan_grid(int parts) { return (unsigned)((parts + kPlanWaves - 1) / kPlanWaves); }
@@ -1011,10 +1029,7 @@ hipError_t launch_wide(const WideArgs &a, hipStream_t st, hipEvent_t start, hipE
     if (a.n_parts < 1 || a.n_parts > kWideMaxParts || a.grid1 < 1 || a.grid1 > kWideMaxRows ||
         (a.levels == 2 && a.n_parts > kWideMaxBands))
         return hipErrorInvalidValue;
-    hipError_t e = a.lut16 ? (a.toa.lds ? launch_scatter_tl<true, true>(a, st, start, stop)
-                             : launch_scatter_tl<true, false>(a, st, start, stop))
-                : (a.toa.lds ? launch_scatter_tl<false, true>(a, st, start, stop)
-                             : launch_scatter_tl<false, false>(a, st, start, stop));
+    hipError_t e = a.lut16 ? launch_scatter_l<true>(a, st, start, stop) : launch_scatter_l<false>(a, st, start, stop);
     if (e != hipSuccess) return e;
     WideRows rows = a.rows1;
     const uint4 *items = a.items1;
