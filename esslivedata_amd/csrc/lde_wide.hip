@@ -74,9 +74,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint3
 }
 
 // TM: where the TOA tree is read -- 1: all of it from LDS; 2: its first
-// kWideTreeLds words (the root level first: the builder lays the tree out
-// level by level) from LDS and the rest through a buffer load that has no
-// request for an LDS-resident index; 0: all through L2 (diagnostics)
+// kWideTreeLds words (the builder puts the root level first, then each root
+// bucket's subtree in TOA order) from LDS and the rest through a buffer load
+// that has no request for an LDS-resident index; 0: all through L2
+// (diagnostics)
 template <int TM>
 __device__ __forceinline__ uint32_t tree_word(const uint32_t *tree, __amdgpu_buffer_rsrc_t gt, uint32_t i) {
     if (TM == 1) return tree[i];  // LDS
