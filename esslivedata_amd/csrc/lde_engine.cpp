@@ -635,6 +635,32 @@ struct WideTreeBuilder {
         }
         return 0xFFFFu | ((uint32_t)base << 16);
     }
+    // reads past the kernel's LDS copy (the first kWideTreeLds words) per
+    // event, for TOAs spread evenly over the span (a tree too large for LDS)
+    double l2_reads(long long span) const {
+        const long long nroot = (span + (1LL << sh0) - 1) >> sh0;
+        const int F = 1 << fb;
+        double c = 0;
+        struct Walk {
+            const std::vector<uint32_t> &w;
+            int F;
+            double cost(uint32_t word, double wt) const {
+                if ((word & 0xFFFFu) != 0xFFFFu) return 0;  // a leaf
+                const uint32_t base = word >> 16;
+                double c = 0;
+                for (int k = 0; k < F; ++k) {
+                    const size_t i = (size_t)base + (size_t)k;
+                    c += (i >= (size_t)lde::kWideTreeLds ? wt / F : 0) + cost(w[i], wt / F);
+                }
+                return c;
+            }
+        } walk{words, F};
+        for (long long g = 0; g < nroot; ++g) {
+            const double wt = (double)std::min<long long>(1LL << sh0, span - (g << sh0)) / (double)span;
+            c += (g >= lde::kWideTreeLds ? wt : 0) + walk.cost(words[(size_t)g], wt);
+        }
+        return c;
+    }
     bool build(long long span) {
         const long long nroot = (span + (1LL << sh0) - 1) >> sh0;
         if (nroot > 0xFFFF) return false;
@@ -666,7 +692,10 @@ bool build_wide_tree(const std::vector<double> &edges, int T, std::vector<uint32
     for (int i = 0; i <= T; ++i) r[(size_t)i] = thr[(size_t)i] - lo;
     size_t best = ~(size_t)0;
     int bsh = -1, bfb = 0, bdepth = 0;
+    double bl2 = 0;
     const bool shallow = env_ll("LDE_WIDE_TREE_SHALLOW", 1) != 0;  // (diagnostics: 0 = fewest words)
+    // (diagnostics: 0 = a tree past LDS takes the fewest words)
+    const bool hybrid = env_ll("LDE_WIDE_TREE_L2PICK", 1) != 0;
     for (int sh0 = 15; sh0 >= 0; --sh0) {
         if (((span + (1LL << sh0) - 1) >> sh0) > 0xFFFF) break;
         for (int fb = 2; fb <= 4; ++fb) {
@@ -678,14 +707,19 @@ bool build_wide_tree(const std::vector<double> &edges, int T, std::vector<uint32
             // whose events reach it: DREAM's 1000 log bins, 20 % of the
             // events in three narrow hot bins, took a second level in every
             // wave), then the fewest words; trees too large for LDS: the
-            // fewest words
+            // fewest reads past the LDS copy of their first kWideTreeLds words
+            // (for TOAs spread evenly), then the fewest words
             const bool fits = n <= (size_t)lde::kWideTreeLds, bfits = best <= (size_t)lde::kWideTreeLds;
-            const bool better = fits && shallow ? (b.depth < bdepth || (b.depth == bdepth && n < best)) : n < best;
+            const double l2 = fits ? 0.0 : (hybrid ? b.l2_reads(span) : 0.0);
+            const bool better = fits && shallow ? (b.depth < bdepth || (b.depth == bdepth && n < best))
+                                : !fits && hybrid ? (l2 < bl2 - 1e-6 || (l2 <= bl2 + 1e-6 && n < best))
+                                                  : n < best;
             if (bsh < 0 || (fits && !bfits) || (fits == bfits && better)) {
                 best = n;
                 bsh = sh0;
                 bfb = fb;
                 bdepth = b.depth;
+                bl2 = l2;
                 tree = std::move(b.words);
             }
         }
