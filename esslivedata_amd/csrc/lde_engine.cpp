@@ -635,29 +635,31 @@ struct WideTreeBuilder {
         }
         return 0xFFFFu | ((uint32_t)base << 16);
     }
-    // reads past the kernel's LDS copy (the first kWideTreeLds words) per
-    // event, for TOAs spread evenly over the span (a tree too large for LDS)
-    double l2_reads(long long span) const {
+    // reads of words at index >= from per event, for TOAs spread evenly over
+    // the span (from = kWideTreeLds: the reads past the kernel's LDS copy of a
+    // tree too large for LDS; 0: all reads)
+    double reads(long long span, size_t from) const {
         const long long nroot = (span + (1LL << sh0) - 1) >> sh0;
         const int F = 1 << fb;
         double c = 0;
         struct Walk {
             const std::vector<uint32_t> &w;
             int F;
+            size_t from;
             double cost(uint32_t word, double wt) const {
                 if ((word & 0xFFFFu) != 0xFFFFu) return 0;  // a leaf
                 const uint32_t base = word >> 16;
                 double c = 0;
                 for (int k = 0; k < F; ++k) {
                     const size_t i = (size_t)base + (size_t)k;
-                    c += (i >= (size_t)lde::kWideTreeLds ? wt / F : 0) + cost(w[i], wt / F);
+                    c += (i >= from ? wt / F : 0) + cost(w[i], wt / F);
                 }
                 return c;
             }
-        } walk{words, F};
+        } walk{words, F, from};
         for (long long g = 0; g < nroot; ++g) {
             const double wt = (double)std::min<long long>(1LL << sh0, span - (g << sh0)) / (double)span;
-            c += (g >= lde::kWideTreeLds ? wt : 0) + walk.cost(words[(size_t)g], wt);
+            c += ((size_t)g >= from ? wt : 0) + walk.cost(words[(size_t)g], wt);
         }
         return c;
     }
@@ -710,7 +712,7 @@ bool build_wide_tree(const std::vector<double> &edges, int T, std::vector<uint32
             // fewest reads past the LDS copy of their first kWideTreeLds words
             // (for TOAs spread evenly), then the fewest words
             const bool fits = n <= (size_t)lde::kWideTreeLds, bfits = best <= (size_t)lde::kWideTreeLds;
-            const double l2 = fits ? 0.0 : (hybrid ? b.l2_reads(span) : 0.0);
+            const double l2 = fits ? 0.0 : (hybrid ? b.reads(span, (size_t)lde::kWideTreeLds) : 0.0);
             const bool better = fits && shallow ? (b.depth < bdepth || (b.depth == bdepth && n < best))
                                 : !fits && hybrid ? (l2 < bl2 - 1e-6 || (l2 <= bl2 + 1e-6 && n < best))
                                                   : n < best;
