@@ -233,3 +233,23 @@ def test_bench_shard_banks_gpus2():
     assert d['n_gpus'] == 2 and 'bank sharding x2' in d['config']['parallelism']
     _check_bank_leg(d['bank_sharding'], 2)
     assert d['value'] == d['bank_sharding']['value']
+
+
+@pytest.mark.parametrize('wl,bins', [('dream_t1000log', 1000), ('dream_t10000log', 10000),
+                                     ('loki_t1000linear', 1000)])
+def test_committed_toa_binning_lines(wl, bins):
+    """Round 6 (review item 1): the larger TOA binnings run on WIDE, exact,
+    with the finalize overlapped and a CPU baseline beside them."""
+    d = json.loads((ROOT / 'profiles' / f'{R}_{wl}_bench_line.json').read_text())
+    assert d['config']['strategy'] == 'wide' and d['config']['toa_bins'] == bins
+    assert d['config']['finalize_overlap'] is True
+    assert d['check']['bit_exact_vs_oracle'] is True
+    assert d['cpu_baseline']['value'] > 0
+
+
+def test_committed_headline_cpu_baseline_both_core_counts():
+    """Review item 4: the box's share of cores and every visible core."""
+    cb = json.loads((ROOT / 'profiles' / f'{R}_dream_bench_line.json').read_text())['cpu_baseline']
+    share, allv = cb['share_threads'], cb['all_visible_threads']
+    assert share['cores'] >= 1 and allv['cores'] >= share['cores']
+    assert cb['value'] == max(share['value'], allv['value'])
