@@ -8,6 +8,7 @@ single-thread-affine like the reference's jobs (SRC/core/job_manager.py:698-701)
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -106,9 +107,23 @@ class PendingFinalize:
     def __init__(self, engine, ref, make) -> None:
         self._engine, self._ref, self._make, self._res = engine, ref, make, None
 
+    def __del__(self) -> None:
+        # dropped unread: complete it while its output arrays are still alive,
+        # so the engine is not left with a pending finalize
+        try:
+            if self._res is None and getattr(self._engine, '_h', None) is not None:
+                self.result()
+        except Exception:
+            pass
+
     def result(self) -> 'FinalizeResult':
         if self._res is None:
             e = self._engine
+            if getattr(e, '_h', None) is None:
+                raise RuntimeError('the engine was closed before this finalize was read')
+            cur = getattr(e, '_pending', None)
+            if cur is not None and cur() is self:
+                e._pending = None
             rc = e._lib.lde_finalize_end(e._h, self._ref)
             if rc:
                 check(rc, e._h, e._lib)
@@ -454,7 +469,9 @@ class BinningEngine:
         rc = self._lib.lde_finalize_begin(self._h, ref)
         if rc:
             check(rc, self._h, self._lib)
-        return PendingFinalize(self, ref, result)
+        pending = PendingFinalize(self, ref, result)
+        self._pending = weakref.ref(pending)  # (no cycle: the pending result holds the engine)
+        return pending
 
     def read_histogram(self, which: str = 'current') -> np.ndarray:
         w = {'current': _native.LDE_CURRENT, 'cumulative': _native.LDE_CUMULATIVE}[which]
@@ -609,6 +626,13 @@ class BinningEngine:
     def close(self) -> None:
         h = getattr(self, '_h', None)
         if h:
+            ref = getattr(self, '_pending', None)
+            p = ref() if ref is not None else None
+            if p is not None:  # its outputs first (the pack dies with the handle)
+                try:
+                    p.result()
+                except Exception:
+                    pass
             self._lib.lde_destroy(h)
             self._h = None
 

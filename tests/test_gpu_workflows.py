@@ -487,3 +487,32 @@ def test_finalize_overlapped_with_next_batch(num_bins):
         a.finalize(images=True, wait=False)  # nothing accumulated since
     a.close()
     b.close()
+
+
+def test_pending_finalize_dropped_or_engine_closed():
+    """A pending finalize dropped unread completes itself (the next one is
+    accepted); closing the engine completes one that is still held, whose
+    outputs stay readable after the close."""
+    from esslivedata_amd import projection, synthetic
+    from esslivedata_amd.engine import BinningEngine
+
+    inst = synthetic.dummy_panel()
+    view = projection.logical_lut(inst.detector_number)
+    edges = inst.edges.edges_ns()
+    eng = BinningEngine(toa_edges_ns=edges, out_lut=view.lut, pid_offset=view.pid_offset,
+                        n_screen=view.n_screen, reuse_output_buffers=False)
+    pid, toa = synthetic.fake_detector_events(100_000, 1, 16384, seed=3)
+    exp = ora.detector_histogram(view.lut[0], view.n_screen, ora.pixel_index(pid, inst.detector_number),
+                                 toa, edges).sum(-1)
+    eng.stage(pid, toa)
+    eng.accumulate(0)
+    eng.finalize(images=True, wait=False)  # dropped at once
+    eng.stage(pid, toa)
+    eng.accumulate(0)
+    p = eng.finalize(images=True, wait=False)
+    np.testing.assert_array_equal(p.result().current_image, exp)
+    eng.stage(pid, toa)
+    eng.accumulate(0)
+    held = eng.finalize(images=True, wait=False)
+    eng.close()
+    np.testing.assert_array_equal(held.result().current_image, exp)
