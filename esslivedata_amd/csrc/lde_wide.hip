@@ -362,15 +362,17 @@ __device__ __forceinline__ void part_unit(const PartLds &s, int P, int pbits, ui
         // byte offset inside the row's pool (a store out of range is dropped)
         const uint32_t at = ((page - pool_base) << PB) + (x & (PAGE - 1));
         const int boff = (lost || (ABL & 2)) ? (int)kOOB : (int)(at << (E16 ? 1 : 2));
+        // (diagnostics, ABL & 64: the page stores with the non-temporal hint)
+        constexpr int kAux = (ABL & 64) ? 2 : 0;
         if (E16) {
             auto e16 = [&](uint32_t k) { return k == kNone ? kPad16 : (k & emask); };
             typedef unsigned int v2u __attribute__((ext_vector_type(2)));
             __builtin_amdgcn_raw_buffer_store_b64(v2u{e16(k4.x) | (e16(k4.y) << 16), e16(k4.z) | (e16(k4.w) << 16)},
-                                                  pool, boff, 0, 0);
+                                                  pool, boff, 0, kAux);
         } else {
             auto e32 = [&](uint32_t k) { return k == kNone ? kNone : (k & emask); };
             __builtin_amdgcn_raw_buffer_store_b128(v4u{e32(k4.x), e32(k4.y), e32(k4.z), e32(k4.w)}, pool, boff,
-                                                   0, 0);
+                                                   0, kAux);
         }
     }
 }
@@ -999,6 +1001,7 @@ static hipError_t launch_scatter_t(const WideArgs &a, hipStream_t st, hipEvent_t
                               0, a);                                                                        \
         return hipGetLastError();
             LDE_WABL(1) LDE_WABL(2) LDE_WABL(3) LDE_WABL(4) LDE_WABL(5) LDE_WABL(16) LDE_WABL(18) LDE_WABL(20)
+            LDE_WABL(64)
 #undef LDE_WABL
         default: return hipErrorInvalidValue;
         }
