@@ -1577,11 +1577,14 @@ int bin_wide(lde_handle *h, const std::vector<lde::SegDesc> &sd, long long chunk
     // pass B: items of at most 1/(2 x CUs) of the batch (half as large as
     // one per CU: the hot tiles' items finish with the rest; DREAM 1,000 bins
     // −20 µs, 10,000 bins −0.12 ms).  (diagnostics: LDE_WIDE_ITEM_DIV)
+    // The second level's tile items at 1/(3 x CUs) (10,000 bins: pass B
+    // 0.39 -> 0.33 ms; one level at 1/3: +7 us).  (diagnostics: _DIV2)
     const long long idiv = std::max<long long>(1, std::min<long long>(16, env_ll("LDE_WIDE_ITEM_DIV", 2)));
+    const long long idiv2 = std::max<long long>(1, std::min<long long>(16, env_ll("LDE_WIDE_ITEM_DIV2", 3)));
     const long long item_max1 = h->wide_levels == 1
                                     ? std::max<long long>(65536, (total + idiv * h->cus - 1) / (idiv * h->cus))
                                     : std::max<long long>(65536, (total + 2LL * h->cus - 1) / (2LL * h->cus));
-    const long long item_max2 = std::max<long long>(65536, (total + idiv * h->cus - 1) / (idiv * h->cus));
+    const long long item_max2 = std::max<long long>(65536, (total + idiv2 * h->cus - 1) / (idiv2 * h->cus));
     const long long max_items1 = P + total / item_max1 + 2;
     const long long max_items2 = h->wide_levels == 2 ? h->wide_tiles + total / item_max2 + 2 : 0;
     const int tpb = 1 << h->wide_tpb_bits;
