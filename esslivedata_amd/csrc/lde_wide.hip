@@ -30,7 +30,7 @@
 //   k_wide_split      two-level form only (more than kWideMaxParts tiles):
 //                     per item of a band, its u32 band-local keys partitioned
 //                     by tile as the first pass does, with a rank counter per
-//                     16-lane group (few partitions per band)
+//                     8-lane group (few partitions per band)
 //   k_wide_accumulate per item of a tile: its pages histogrammed in a 128 KB
 //                     LDS tile, then added to the window (store-only on a
 //                     fresh window, a 16-byte read-modify-write when the tile
@@ -205,7 +205,7 @@ constexpr size_t kWideScatterWords = part_words(kWideMaxParts) + ((size_t)1 << k
                                      sizeof(PixChunk) / 4 * kWideLdsChunks;
 static_assert(kWideScatterWords * 4 <= 160 * 1024, "first pass LDS");
 // second pass: partition layout | item row prefix | staged page ids, counts
-constexpr int kWideSplitSub = 4;  // the second pass: few partitions (<= 256 tiles of a band)
+constexpr int kWideSplitSub = 8;  // the second pass: few partitions (<= 256 tiles of a band)
 constexpr size_t kWideSplitWords = part_words(kWideMaxTpb, kWideSplitSub) + kWideMaxRows + 1 + 2 * 1024;
 
 __device__ __forceinline__ PartLds part_lds(uint32_t *sm, int P, int sub = 1) {
