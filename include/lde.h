@@ -53,9 +53,9 @@ extern "C" {
 #define LDE_STRATEGY_ATOMIC 1      /* one pass, global atomics             */
 #define LDE_STRATEGY_PARTITION 2   /* tile partition (chunk-major runs) + LDS sub-histograms */
 #define LDE_STRATEGY_PAGED 3       /* tile partition into per-block page chains + LDS sub-histograms */
-#define LDE_STRATEGY_SPLIT 4       /* hot screen rows in LDS + cold remainder through PAGED (skewed streams) */
+#define LDE_STRATEGY_SPLIT 4       /* hot screen rows in LDS + cold keys sorted into tiles (skewed streams) */
 #define LDE_STRATEGY_PIXEL 5       /* partition by pixel range (no LUT gather) + the range's LUT slice and
-                                      screen footprint in LDS; needs footprints that fit (else PAGED) */
+                                      screen footprint in LDS; needs footprints that fit (else WIDE) */
 #define LDE_STRATEGY_WIDE 6        /* any TOA edges and histogram size: pixel-table front end, keys into page
                                       chains by tile (one level, or bands then tiles), LDS tiles (lde_wide.hip) */
 
@@ -378,7 +378,7 @@ int lde_kernel_stats(lde_handle *h, int32_t kernel_id, double *ms, int64_t *laun
 #define LDE_C_WIDE_LEVELS 8      /* WIDE partition levels (1 or 2; 0: WIDE unavailable for this view) */
 #define LDE_C_WIDE_PARTS 9       /* WIDE first-level partitions (tiles or bands) */
 #define LDE_C_WIDE_TREE_WORDS 10 /* words of the WIDE TOA lookup tree */
-#define LDE_C_WIDE_TREE_LDS 11   /* 1 if the tree is kept in LDS (else read from global memory) */
+#define LDE_C_WIDE_TREE_LDS 11   /* 1 if the whole tree is kept in LDS (else its first 6,144 words, the rest read through L2) */
 #define LDE_C_WIDE_ITEMS 12      /* pass-B work items of the last WIDE batch (synchronizes) */
 int lde_counter(lde_handle *h, int32_t id, int64_t *value);
 
